@@ -1,0 +1,551 @@
+// bitset.hip — dictionary-rank bitsets and the tiled AND+popcount N×N kernel.
+//
+// Replaces the SequenceKmers.distance(other) loop over many pairs
+// (FastaDistanceProcessor.java:177-186, GenomeProcessor.java:336,
+// WidthProcessor.java:159-165): |A∩B| = Σ_w popcount(a_w & b_w) over
+// per-set bitsets indexed by the rank of each kmer in a global dictionary.
+//
+// Dictionary: all codes of all sets, radix-sorted with their set id; a run of
+// equal codes is one dictionary entry. Kmers present in only one set can
+// never contribute to any intersection, so by default they are left out of
+// the dictionary (|A| still counts them: it comes from the CSR sizes). The
+// result is exact either way (tests check both).
+//
+// Kernel (bitset_tile_kernel): a 256-thread workgroup owns a 128×128 tile of
+// (row set, column set) pairs and a K-slice of the bitset words; each thread
+// keeps an 8×8 register tile of popcount accumulators. Per 16-word chunk the
+// row and column tiles are staged into LDS (XOR-swizzled 128-B rows, read as
+// ds_read_b128 without bank conflicts); the inner step is 2×v_and_b32 +
+// 2×v_bcnt_u32_b32 (accumulating) per 64-bit word pair — pure VALU integer
+// work, no MFMA. K-slices are summed with exact int32 atomics.
+#include <cstring>
+#include <rocprim/rocprim.hpp>
+
+#include <algorithm>
+
+#include "gdist_internal.hpp"
+
+namespace gdist {
+namespace {
+
+inline int grid_for(int64_t n, int block = 256, int64_t cap = 256 * 32) {
+    int64_t g = ceil_div(n, block);
+    return (int)std::max<int64_t>(1, std::min<int64_t>(g, cap));
+}
+
+__global__ void set_ids_kernel(const int64_t* __restrict__ off, int64_t s0, int64_t s1, int32_t* __restrict__ ids) {
+    const int64_t base = off[s0];
+    const int64_t n = off[s1] - base;
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
+        const int64_t i = base + e;
+        int64_t lo = s0, hi = s1;   // upper_bound(off, i) - 1
+        while (hi - lo > 1) {
+            int64_t mid = (lo + hi) >> 1;
+            if (off[mid] <= i) lo = mid; else hi = mid;
+        }
+        ids[e] = (int32_t)lo;
+    }
+}
+
+__global__ void head_flags_u64(const uint64_t* __restrict__ keys, int64_t n, int32_t* __restrict__ flag) {
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        flag[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1 : 0;
+}
+
+// run heads -> unique code and run start
+__global__ void run_heads_kernel(const uint64_t* __restrict__ keys, const int32_t* __restrict__ flag,
+                                 const int64_t* __restrict__ pos, int64_t n, uint64_t* __restrict__ uniq,
+                                 int64_t* __restrict__ start) {
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        if (flag[i]) { uniq[pos[i]] = keys[i]; start[pos[i]] = i; }
+}
+
+// total weight per run: weights given (prefix sums cw over elements) or 1 per element
+__global__ void run_totals_kernel(const int64_t* __restrict__ start, int64_t nruns, int64_t n,
+                                  const int64_t* __restrict__ cw, uint32_t* __restrict__ total) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nruns) return;
+    const int64_t b = start[r], e = (r + 1 < nruns) ? start[r + 1] : n;
+    const int64_t t = cw ? (cw[e] - cw[b]) : (e - b);
+    total[r] = (uint32_t)(t > 0xFFFFFFFFll ? 0xFFFFFFFFll : t);
+}
+
+__global__ void dict_flag_kernel(const uint32_t* __restrict__ cnt, int64_t n, int keep, int32_t* __restrict__ flag) {
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        flag[i] = (keep || cnt[i] >= 2) ? 1 : 0;
+}
+
+__global__ void compact_u64_kernel(const uint64_t* __restrict__ v, const int32_t* __restrict__ flag,
+                                   const int64_t* __restrict__ pos, int64_t n, uint64_t* __restrict__ out) {
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        if (flag[i]) out[pos[i]] = v[i];
+}
+
+__global__ void widen_u32_kernel(const uint32_t* __restrict__ in, int64_t n, int64_t* __restrict__ out) {
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) out[i] = in[i];
+}
+
+// rank of each run's code in the dictionary (or -1)
+__global__ void run_rank_kernel(const uint64_t* __restrict__ keys, const int64_t* __restrict__ start, int64_t nruns,
+                                const uint64_t* __restrict__ dict, int64_t U, int64_t* __restrict__ rank) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nruns) return;
+    const uint64_t k = keys[start[r]];
+    int64_t lo = 0, hi = U;
+    while (lo < hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if (dict[mid] < k) lo = mid + 1; else hi = mid;
+    }
+    rank[r] = (lo < U && dict[lo] == k) ? lo : -1;
+}
+
+__global__ void scatter_bits_kernel(const int32_t* __restrict__ ids, const int32_t* __restrict__ flag,
+                                    const int64_t* __restrict__ pos, const int64_t* __restrict__ rank, int64_t n,
+                                    int64_t W, unsigned long long* __restrict__ bits) {
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const int64_t run = pos[i] + flag[i] - 1;       // inclusive run index
+        const int64_t r = rank[run];
+        if (r < 0) continue;
+        atomicOr(bits + (int64_t)ids[i] * W + (r >> 6), 1ull << (r & 63));
+    }
+}
+
+constexpr int BT = 128;                 // tile edge (sets)
+constexpr int KC = 16;                  // 64-bit words per staged chunk
+constexpr int ROWB = KC * 8;            // 128 B per set row in LDS
+constexpr int TILE_BYTES = BT * ROWB;   // 16 KiB per operand per chunk
+constexpr int NT = 256;
+
+// LDS image: row g, logical 16-B slot q stored at slot q ^ ((g >> 1) & 7):
+// the 16 lanes of a ds_read_b128 group read 16 consecutive rows at one
+// logical slot and land on 16 distinct 4-bank groups.
+__device__ __forceinline__ int lds_off(int g, int q) { return g * ROWB + ((q ^ ((g >> 1) & 7)) << 4); }
+
+// v_bcnt_u32_b32 d, x, acc = popcount(x) + acc. Written as asm because hipcc
+// otherwise reassociates the sums into extra v_add3_u32 (10 VALU ops per
+// 4 dwords instead of 8).
+__device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc) {
+    uint32_t r;
+    asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(acc));
+    return r;
+}
+
+__device__ __forceinline__ uint32_t and_popc(uint4 a, uint4 b, uint32_t acc) {
+    acc = bcnt_acc(a.x & b.x, acc);
+    acc = bcnt_acc(a.y & b.y, acc);
+    acc = bcnt_acc(a.z & b.z, acc);
+    acc = bcnt_acc(a.w & b.w, acc);
+    return acc;
+}
+
+__global__ __launch_bounds__(NT, 2) void bitset_tile_kernel(
+    const unsigned long long* __restrict__ bits, int64_t W, const int2* __restrict__ tiles, int splits,
+    int64_t nchunks, int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I,
+    int64_t ldI) {
+    __shared__ __attribute__((aligned(16))) unsigned char lds[2 * TILE_BYTES];
+    unsigned char* ldsA = lds;
+    unsigned char* ldsB = lds + TILE_BYTES;
+
+    const int tile = blockIdx.x / splits;
+    const int split = blockIdx.x % splits;
+    const int2 t = tiles[tile];
+    if (t.x < 0 || t.y < 0) return;   // defensive: never address outside the region
+    const int64_t row0 = r0 + (int64_t)t.x * BT;
+    const int64_t col0 = c0 + (int64_t)t.y * BT;
+    const int64_t kc_per = ceil_div(nchunks, splits);
+    const int64_t kc0 = (int64_t)split * kc_per;
+    const int64_t kc1 = kc0 + kc_per < nchunks ? kc0 + kc_per : nchunks;
+
+    const int tid = threadIdx.x;
+    const int tx = tid & 15, ty = tid >> 4;
+
+    uint32_t acc[8][8];
+#pragma unroll
+    for (int r = 0; r < 8; r++)
+#pragma unroll
+        for (int c = 0; c < 8; c++) acc[r][c] = 0;
+
+    for (int64_t kc = kc0; kc < kc1; kc++) {
+        // stage: 128 rows × 8 slots of 16 B per operand = 1024 pieces, 4 per thread
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int piece = tid + NT * q;
+            const int g = piece >> 3, slot = piece & 7;
+            const int64_t wofs = kc * KC + slot * 2;
+            const int64_t ra = row0 + g, cb = col0 + g;
+            uint4 va = make_uint4(0, 0, 0, 0), vb = make_uint4(0, 0, 0, 0);
+            if (ra < r1) va = *reinterpret_cast<const uint4*>(bits + ra * W + wofs);
+            if (cb < c1) vb = *reinterpret_cast<const uint4*>(bits + cb * W + wofs);
+            *reinterpret_cast<uint4*>(ldsA + lds_off(g, slot)) = va;
+            *reinterpret_cast<uint4*>(ldsB + lds_off(g, slot)) = vb;
+        }
+        __syncthreads();
+#pragma unroll 2
+        for (int q = 0; q < 8; q++) {
+            uint4 a[8];
+#pragma unroll
+            for (int r = 0; r < 8; r++) a[r] = *reinterpret_cast<const uint4*>(ldsA + lds_off(ty + 16 * r, q));
+#pragma unroll
+            for (int c = 0; c < 8; c++) {
+                const uint4 b = *reinterpret_cast<const uint4*>(ldsB + lds_off(tx + 16 * c, q));
+#pragma unroll
+                for (int r = 0; r < 8; r++) acc[r][c] = and_popc(a[r], b, acc[r][c]);
+            }
+        }
+        __syncthreads();
+    }
+
+    // exact integer reduction of the K-slices
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+        const int64_t i = row0 + ty + 16 * r;
+        if (i >= r1) continue;
+#pragma unroll
+        for (int c = 0; c < 8; c++) {
+            const int64_t j = col0 + tx + 16 * c;
+            if (j >= c1 || (upper && j <= i)) continue;
+            if (acc[r][c]) atomicAdd(I + (i - r0) * ldI + (j - c0), (int32_t)acc[r][c]);
+        }
+    }
+}
+
+// Self pairs: |A ∩ A| = |A|. The pruned dictionary drops kmers held by one
+// set only, so the bitset count of a self pair misses them; take |A|.
+__global__ void self_pairs_kernel(const int64_t* __restrict__ off, int64_t lo, int64_t hi, int64_t r0, int64_t c0,
+                                  int32_t* __restrict__ I, int64_t ldI) {
+    const int64_t i = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= hi) return;
+    I[(i - r0) * ldI + (i - c0)] = (int32_t)(off[i + 1] - off[i]);
+}
+
+// Java expression of SequenceKmers.distance, fp64 with contraction off:
+// d = I > 0 ? 1.0 - (double)I / (double)(nA + nB - I) : 1.0
+__global__ void epilogue_kernel(const int64_t* __restrict__ off, int64_t r0, int64_t r1, int64_t c0,
+                                int64_t c1, int upper, int empty_nan, const int32_t* __restrict__ I,
+                                int64_t ldI, double* __restrict__ D, int64_t ldD) {
+#pragma clang fp contract(off)
+    const int64_t ncol = c1 - c0;
+    const int64_t n = (r1 - r0) * ncol;
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
+        const int64_t ri = e / ncol, cj = e - ri * ncol;
+        const int64_t i = r0 + ri, j = c0 + cj;
+        if (upper && j <= i) continue;
+        const int64_t inter = I[ri * ldI + cj];
+        const int64_t na = off[i + 1] - off[i], nb = off[j + 1] - off[j];
+        double d;
+        if (inter > 0) {
+            const double uni = (double)(na + nb - inter);
+            d = 1.0 - (double)inter / uni;
+        } else {
+            d = (empty_nan && na + nb == 0) ? __builtin_nan("") : 1.0;
+        }
+        D[ri * ldD + cj] = d;
+    }
+}
+
+// one query row against a column list: one wave per column, streaming
+__global__ __launch_bounds__(256) void bitset_row_kernel(const unsigned long long* __restrict__ bits, int64_t W,
+                                                         int64_t q, const int64_t* __restrict__ cols,
+                                                         int64_t ncols, int32_t* __restrict__ I) {
+    const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (c >= ncols) return;
+    const unsigned long long* a = bits + q * W;
+    const unsigned long long* b = bits + cols[c] * W;
+    uint32_t acc = 0;
+    for (int64_t w = lane; w < W; w += 64) acc += __popcll(a[w] & b[w]);
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if (lane == 0) I[c] = (cols[c] == q) ? -1 : (int32_t)acc;   // -1: self pair, fixed by the epilogue
+}
+
+__global__ void row_epilogue_kernel(const int64_t* __restrict__ off, int64_t q, const int64_t* __restrict__ cols,
+                                    int64_t ncols, int empty_nan, const int32_t* __restrict__ I,
+                                    double* __restrict__ D) {
+#pragma clang fp contract(off)
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= ncols) return;
+    const int64_t j = cols[c];
+    const int64_t na = off[q + 1] - off[q], nb = off[j + 1] - off[j];
+    const int64_t inter = (j == q) ? na : I[c];
+    double d;
+    if (inter > 0) {
+        const double uni = (double)(na + nb - inter);
+        d = 1.0 - (double)inter / uni;
+    } else {
+        d = (empty_nan && na + nb == 0) ? __builtin_nan("") : 1.0;
+    }
+    D[c] = d;
+}
+
+}  // namespace
+
+void bitset_row(gdist_ctx* ctx, const gdist_sets* s, int64_t q, const int64_t* d_cols, int64_t ncols,
+                int32_t* d_I) {
+    if (ncols <= 0) return;
+    bitset_row_kernel<<<(unsigned)ceil_div(ncols, 4), 256, 0, ctx->stream>>>(s->bits.as<unsigned long long>(), s->W,
+                                                                             q, d_cols, ncols, d_I);
+    GD_HIP(hipGetLastError());
+}
+
+void row_epilogue(gdist_ctx* ctx, const gdist_sets* s, int64_t q, const int64_t* d_cols, int64_t ncols,
+                  unsigned flags, const int32_t* d_I, double* d_D) {
+    if (ncols <= 0) return;
+    row_epilogue_kernel<<<(unsigned)ceil_div(ncols, 256), 256, 0, ctx->stream>>>(
+        s->off.as<int64_t>(), q, d_cols, ncols, (flags & GDIST_EMPTY_NAN) ? 1 : 0, d_I, d_D);
+    GD_HIP(hipGetLastError());
+}
+
+// ---- dictionary construction ------------------------------------------
+// A Summary is a sorted array of distinct codes with the number of sets
+// holding each. Summaries of disjoint set ranges merge by summing counts; the
+// dictionary is the codes with count >= 2 (or all codes, keep_singletons).
+
+namespace {
+
+constexpr int64_t kBitsChunk = int64_t(1) << 30;   // codes per working chunk
+
+// (keys sorted) -> runs: unique codes, run starts, run count
+void runs_of(gdist_ctx* ctx, const uint64_t* keys, int64_t n, DevBuf& flag, DevBuf& pos, DevBuf& uniq,
+             DevBuf& start, int64_t& nruns) {
+    hipStream_t st = ctx->stream;
+    flag.alloc(n * 4 + 4, st);
+    pos.alloc(n * 8 + 8, st);
+    nruns = 0;
+    if (n == 0) { uniq.alloc(8, st); start.alloc(8, st); return; }
+    head_flags_u64<<<grid_for(n), 256, 0, st>>>(keys, n, flag.as<int32_t>());
+    GD_HIP(hipGetLastError());
+    exclusive_scan_i32_to_i64(ctx, flag.as<int32_t>(), pos.as<int64_t>(), (size_t)n);
+    int64_t last = 0;
+    int32_t lf = 0;
+    GD_HIP(hipMemcpyAsync(&last, pos.as<int64_t>() + n - 1, 8, hipMemcpyDeviceToHost, st));
+    GD_HIP(hipMemcpyAsync(&lf, flag.as<int32_t>() + n - 1, 4, hipMemcpyDeviceToHost, st));
+    GD_HIP(hipStreamSynchronize(st));
+    nruns = last + lf;
+    uniq.alloc(nruns * 8 + 8, st);
+    start.alloc(nruns * 8 + 8, st);
+    run_heads_kernel<<<grid_for(n), 256, 0, st>>>(keys, flag.as<int32_t>(), pos.as<int64_t>(), n,
+                                                   uniq.as<uint64_t>(), start.as<int64_t>());
+    GD_HIP(hipGetLastError());
+}
+
+// merge (codes, counts) parts into one summary
+void merge_parts(gdist_ctx* ctx, const std::vector<SummaryView>& parts, Summary& out) {
+    hipStream_t st = ctx->stream;
+    int64_t m = 0;
+    for (auto& p : parts) m += p.n;
+    DevBuf kA(m * 8 + 8, st), kB(m * 8 + 8, st), vA(m * 4 + 4, st), vB(m * 4 + 4, st);
+    int64_t at = 0;
+    for (auto& p : parts) {
+        if (p.n) {
+            GD_HIP(hipMemcpyAsync(kA.as<uint64_t>() + at, p.codes, p.n * 8, hipMemcpyDeviceToDevice, st));
+            GD_HIP(hipMemcpyAsync(vA.as<uint32_t>() + at, p.counts, p.n * 4, hipMemcpyDeviceToDevice, st));
+        }
+        at += p.n;
+    }
+    uint64_t* keys = kA.as<uint64_t>(); uint64_t* kalt = kB.as<uint64_t>();
+    int32_t* vals = vA.as<int32_t>(); int32_t* valt = vB.as<int32_t>();
+    if (parts.size() > 1) sort_pairs_u64_i32(ctx, keys, kalt, vals, valt, (size_t)m, 0, 64);
+    DevBuf flag, pos, start;
+    runs_of(ctx, keys, m, flag, pos, out.codes, start, out.n);
+    // per-run sum of counts via prefix sums of the counts
+    DevBuf wide((m + 1) * 8, st), cw((m + 1) * 8, st);
+    if (m) {
+        widen_u32_kernel<<<grid_for(m), 256, 0, st>>>(reinterpret_cast<const uint32_t*>(vals), m, wide.as<int64_t>());
+        GD_HIP(hipGetLastError());
+    }
+    GD_HIP(hipMemsetAsync(wide.as<int64_t>() + m, 0, 8, st));
+    exclusive_scan_i64(ctx, wide.as<int64_t>(), cw.as<int64_t>(), (size_t)(m + 1));
+    out.counts.alloc(out.n * 4 + 4, st);
+    if (out.n) {
+        run_totals_kernel<<<(int)ceil_div(out.n, 256), 256, 0, st>>>(start.as<int64_t>(), out.n, m, cw.as<int64_t>(),
+                                                                      out.counts.as<uint32_t>());
+        GD_HIP(hipGetLastError());
+    }
+    GD_HIP(hipStreamSynchronize(st));
+}
+
+}  // namespace
+
+// Summary of sets [0, nsets): chunked sort + run-length, then merge.
+void local_summary(gdist_ctx* ctx, const gdist_sets* s, Summary& out) {
+    hipStream_t st = ctx->stream;
+    const int cbits = std::min(64, code_bits(s->kind, s->k, s->flags));
+    std::vector<Summary> chunks;
+    int64_t s0 = 0;
+    while (s0 < s->nsets) {
+        int64_t s1 = s0 + 1;
+        while (s1 < s->nsets && s->h_off[s1 + 1] - s->h_off[s0] <= kBitsChunk) s1++;
+        const int64_t b = s->h_off[s0], n = s->h_off[s1] - b;
+        DevBuf kA(n * 8 + 8, st), kB(n * 8 + 8, st);
+        if (n) GD_HIP(hipMemcpyAsync(kA.p, s->codes.as<uint64_t>() + b, n * 8, hipMemcpyDeviceToDevice, st));
+        uint64_t* keys = kA.as<uint64_t>(); uint64_t* alt = kB.as<uint64_t>();
+        sort_keys_u64(ctx, keys, alt, (size_t)n, 0, cbits);
+        Summary c;
+        DevBuf flag, pos, start;
+        runs_of(ctx, keys, n, flag, pos, c.codes, start, c.n);
+        c.counts.alloc(c.n * 4 + 4, st);
+        if (c.n) {   // codes are unique per set: run length = number of sets
+            run_totals_kernel<<<(int)ceil_div(c.n, 256), 256, 0, st>>>(start.as<int64_t>(), c.n, n, nullptr,
+                                                                        c.counts.as<uint32_t>());
+            GD_HIP(hipGetLastError());
+        }
+        GD_HIP(hipStreamSynchronize(st));
+        chunks.push_back(std::move(c));
+        s0 = s1;
+    }
+    if (chunks.size() == 1) {
+        out.codes = std::move(chunks[0].codes);
+        out.counts = std::move(chunks[0].counts);
+        out.n = chunks[0].n;
+        return;
+    }
+    std::vector<SummaryView> parts;
+    for (auto& c : chunks) parts.push_back({c.codes.as<uint64_t>(), c.counts.as<uint32_t>(), c.n});
+    merge_parts(ctx, parts, out);
+}
+
+// dictionary = codes of the merged summary with count >= 2 (or all)
+void dictionary_from(gdist_ctx* ctx, const std::vector<SummaryView>& parts, bool keep, DevBuf& dict, int64_t& U) {
+    hipStream_t st = ctx->stream;
+    Summary all;
+    SummaryView m = parts.size() == 1 ? parts[0] : SummaryView{nullptr, nullptr, 0};
+    if (parts.size() != 1) {
+        merge_parts(ctx, parts, all);
+        m = {all.codes.as<uint64_t>(), all.counts.as<uint32_t>(), all.n};
+    }
+    const int64_t n = m.n;
+    DevBuf flag(n * 4 + 4, st), pos(n * 8 + 8, st);
+    U = 0;
+    if (n) {
+        dict_flag_kernel<<<grid_for(n), 256, 0, st>>>(m.counts, n, keep ? 1 : 0, flag.as<int32_t>());
+        GD_HIP(hipGetLastError());
+        exclusive_scan_i32_to_i64(ctx, flag.as<int32_t>(), pos.as<int64_t>(), (size_t)n);
+        int64_t last = 0;
+        int32_t lf = 0;
+        GD_HIP(hipMemcpyAsync(&last, pos.as<int64_t>() + n - 1, 8, hipMemcpyDeviceToHost, st));
+        GD_HIP(hipMemcpyAsync(&lf, flag.as<int32_t>() + n - 1, 4, hipMemcpyDeviceToHost, st));
+        GD_HIP(hipStreamSynchronize(st));
+        U = last + lf;
+    }
+    dict.alloc(U * 8 + 8, st);
+    if (n) {
+        compact_u64_kernel<<<grid_for(n), 256, 0, st>>>(m.codes, flag.as<int32_t>(), pos.as<int64_t>(), n,
+                                                        dict.as<uint64_t>());
+        GD_HIP(hipGetLastError());
+    }
+    GD_HIP(hipStreamSynchronize(st));
+}
+
+int64_t bitset_words(int64_t dict_size) {
+    return std::max<int64_t>(KC, ceil_div(ceil_div(dict_size, 64), KC) * KC);
+}
+
+// bits of sets [0, nsets) against a dictionary (chunked pairs sort, run ranks, scatter)
+void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_t U, int64_t W,
+               unsigned long long* bits) {
+    hipStream_t st = ctx->stream;
+    const int cbits = std::min(64, code_bits(s->kind, s->k, s->flags));
+    GD_HIP(hipMemsetAsync(bits, 0, (size_t)s->nsets * W * 8, st));
+    if (U == 0) return;
+    int64_t s0 = 0;
+    while (s0 < s->nsets) {
+        int64_t s1 = s0 + 1;
+        while (s1 < s->nsets && s->h_off[s1 + 1] - s->h_off[s0] <= kBitsChunk) s1++;
+        const int64_t b = s->h_off[s0], n = s->h_off[s1] - b;
+        if (n) {
+            DevBuf kA(n * 8, st), kB(n * 8, st), vA(n * 4, st), vB(n * 4, st);
+            GD_HIP(hipMemcpyAsync(kA.p, s->codes.as<uint64_t>() + b, n * 8, hipMemcpyDeviceToDevice, st));
+            set_ids_kernel<<<grid_for(n), 256, 0, st>>>(s->off.as<int64_t>(), s0, s1, vA.as<int32_t>());
+            GD_HIP(hipGetLastError());
+            uint64_t* keys = kA.as<uint64_t>(); uint64_t* kalt = kB.as<uint64_t>();
+            int32_t* ids = vA.as<int32_t>(); int32_t* ialt = vB.as<int32_t>();
+            sort_pairs_u64_i32(ctx, keys, kalt, ids, ialt, (size_t)n, 0, cbits);
+            DevBuf flag, pos, uniq, start;
+            int64_t nruns = 0;
+            runs_of(ctx, keys, n, flag, pos, uniq, start, nruns);
+            DevBuf rank(nruns * 8 + 8, st);
+            run_rank_kernel<<<(int)ceil_div(nruns, 256), 256, 0, st>>>(keys, start.as<int64_t>(), nruns, dict, U,
+                                                                       rank.as<int64_t>());
+            GD_HIP(hipGetLastError());
+            scatter_bits_kernel<<<grid_for(n), 256, 0, st>>>(ids, flag.as<int32_t>(), pos.as<int64_t>(),
+                                                             rank.as<int64_t>(), n, W, bits);
+            GD_HIP(hipGetLastError());
+            GD_HIP(hipStreamSynchronize(st));
+        }
+        s0 = s1;
+    }
+}
+
+void build_bitsets(gdist_ctx* ctx, gdist_sets* s, unsigned flags) {
+    const bool keep = (flags & GDIST_BITSET_KEEP_SINGLETONS) != 0;
+    Summary sum;
+    local_summary(ctx, s, sum);
+    DevBuf dict;
+    int64_t U = 0;
+    dictionary_from(ctx, {SummaryView{sum.codes.as<uint64_t>(), sum.counts.as<uint32_t>(), sum.n}}, keep, dict, U);
+    const int64_t W = bitset_words(U);
+    s->bits.alloc((size_t)s->nsets * W * 8 + 8, ctx->stream);
+    fill_bits(ctx, s, dict.as<uint64_t>(), U, W, s->bits.as<unsigned long long>());
+    GD_HIP(hipStreamSynchronize(ctx->stream));
+    s->W = W;
+    s->dict_size = U;
+    s->bits_keep_singletons = keep;
+}
+
+void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1,
+                   bool upper, int32_t* d_I, int64_t ldI) {
+    hipStream_t st = ctx->stream;
+    const int64_t nr = r1 - r0, nc = c1 - c0;
+    if (nr <= 0 || nc <= 0) return;
+    const int tr = (int)ceil_div(nr, BT), tc = (int)ceil_div(nc, BT);
+    std::vector<int2> tiles;
+    for (int a = 0; a < tr; a++)
+        for (int b = 0; b < tc; b++) {
+            // skip tiles holding no pair with j > i
+            const int64_t rmin = r0 + (int64_t)a * BT;
+            const int64_t cmax = std::min<int64_t>(c1, c0 + (int64_t)(b + 1) * BT) - 1;
+            if (upper && cmax <= rmin) continue;
+            tiles.push_back(make_int2(a, b));
+        }
+    if (tiles.empty()) return;
+    const int64_t nchunks = s->W / KC;
+    // split the word dimension so the launch holds ≳ 8 workgroups per CU
+    const int64_t target = (int64_t)ctx->cus * 8;
+    int splits = (int)std::max<int64_t>(1, std::min<int64_t>(nchunks, ceil_div(target, (int64_t)tiles.size())));
+    DevBuf dt(tiles.size() * sizeof(int2), st);
+    h2d_sync(dt.p, tiles.data(), tiles.size() * sizeof(int2), st);
+    const int64_t grid = (int64_t)tiles.size() * splits;
+    GD_REQUIRE(grid < (int64_t(1) << 31), "bitset matrix grid too large");
+    GD_HIP(hipEventRecord(ctx->ev_k0, st));
+    bitset_tile_kernel<<<(unsigned)grid, NT, 0, st>>>(s->bits.as<unsigned long long>(), s->W, dt.as<int2>(),
+                                                       splits, nchunks, r0, r1, c0, c1, upper ? 1 : 0, d_I, ldI);
+    GD_HIP(hipGetLastError());
+    GD_HIP(hipEventRecord(ctx->ev_k1, st));
+    ctx->last.launches = 1;
+    const int64_t lo = std::max(r0, c0), hi = std::min(r1, c1);
+    if (!upper && hi > lo) {
+        self_pairs_kernel<<<(unsigned)ceil_div(hi - lo, 256), 256, 0, st>>>(s->off.as<int64_t>(), lo, hi, r0, c0, d_I,
+                                                                             ldI);
+        GD_HIP(hipGetLastError());
+    }
+}
+
+void distance_epilogue(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1,
+                       bool upper, unsigned flags, const int32_t* d_I, int64_t ldI, double* d_D, int64_t ldD) {
+    const int64_t n = (r1 - r0) * (c1 - c0);
+    if (n <= 0) return;
+    epilogue_kernel<<<grid_for(n), 256, 0, ctx->stream>>>(s->off.as<int64_t>(), r0, r1, c0, c1, upper ? 1 : 0,
+                                                           (flags & GDIST_EMPTY_NAN) ? 1 : 0, d_I, ldI, d_D,
+                                                           ldD);
+    GD_HIP(hipGetLastError());
+}
+
+}  // namespace gdist

@@ -1,0 +1,782 @@
+// gdist_api.hip — the C-ABI of libgdist.so (declared in include/gdist.h).
+//
+// Thin host layer: argument checking with the reference's error behaviour
+// (bad parameters -> GDIST_EINVAL, which the JNI shim maps to
+// IllegalArgumentException, like ParseFailureException at
+// FastaDistanceProcessor.java:98-102), context/stream management, H2D/D2H,
+// dispatch to the device paths in pack/bitset/sorted/sketch.hip, and the
+// RCCL communicator for row-sharded multi-GPU runs.
+#include <cstring>
+#include <rocprim/rocprim.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <new>
+
+#include "gdist_internal.hpp"
+
+namespace gdist {
+
+static thread_local std::string g_last_error;
+
+void set_last_error(const std::string& msg) { g_last_error = msg; }
+
+template <class F>
+static int guard(F&& f) {
+    try {
+        f();
+        return GDIST_OK;
+    } catch (const Error& e) {
+        set_last_error(e.what());
+        return e.code;
+    } catch (const std::bad_alloc&) {
+        set_last_error("host allocation failed");
+        return GDIST_ENOMEM;
+    } catch (const std::exception& e) {
+        set_last_error(e.what());
+        return GDIST_EDEVICE;
+    } catch (...) {
+        set_last_error("unknown failure");
+        return GDIST_EDEVICE;
+    }
+}
+
+#define GD_NCCL(x)                                                                                    \
+    do {                                                                                              \
+        ncclResult_t r_ = (x);                                                                        \
+        if (r_ != ncclSuccess) throw ::gdist::Error(GDIST_ECOMM, std::string(#x) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+static void use_device(gdist_ctx* ctx) {
+    GD_REQUIRE(ctx != nullptr, "null context");
+    GD_HIP(hipSetDevice(ctx->device));
+}
+
+static void check_sets(const gdist_sets* s) { GD_REQUIRE(s != nullptr && s->ctx != nullptr, "null sets handle"); }
+
+static void finish_timing(gdist_ctx* ctx, bool kernel_recorded) {
+    GD_HIP(hipEventRecord(ctx->ev_call1, ctx->stream));
+    GD_HIP(hipEventSynchronize(ctx->ev_call1));
+    float ms = 0.f;
+    GD_HIP(hipEventElapsedTime(&ms, ctx->ev_call0, ctx->ev_call1));
+    ctx->last.call_ms = ms;
+    if (kernel_recorded) {
+        float km = 0.f;
+        GD_HIP(hipEventElapsedTime(&km, ctx->ev_k0, ctx->ev_k1));
+        ctx->last.kernel_ms = km;
+    } else {
+        ctx->last.kernel_ms = 0.0;
+    }
+}
+
+}  // namespace gdist
+
+using namespace gdist;
+
+extern "C" {
+
+const char* gdist_version(void) { return "gdist 0.1.0 (gfx950)"; }
+int gdist_abi_version(void) { return GDIST_ABI_VERSION; }
+const char* gdist_last_error(void) { return g_last_error.c_str(); }
+
+int gdist_device_count(int* n) {
+    return guard([&] {
+        GD_REQUIRE(n, "null output");
+        GD_HIP(hipGetDeviceCount(n));
+    });
+}
+
+int gdist_ctx_create(int device, gdist_ctx** out) {
+    return guard([&] {
+        GD_REQUIRE(out, "null output");
+        int n = 0;
+        GD_HIP(hipGetDeviceCount(&n));
+        GD_REQUIRE(device >= 0 && device < n, "device index out of range");
+        GD_HIP(hipSetDevice(device));
+        auto* c = new gdist_ctx();
+        c->device = device;
+        GD_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        GD_HIP(hipEventCreate(&c->ev_call0));
+        GD_HIP(hipEventCreate(&c->ev_call1));
+        GD_HIP(hipEventCreate(&c->ev_k0));
+        GD_HIP(hipEventCreate(&c->ev_k1));
+        GD_HIP(hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device));
+        // keep stream-ordered allocations cached across calls
+        hipMemPool_t pool;
+        if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+            uint64_t thr = UINT64_MAX;
+            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+        }
+        *out = c;
+    });
+}
+
+int gdist_ctx_destroy(gdist_ctx* ctx) {
+    return guard([&] {
+        if (!ctx) return;
+        (void)hipSetDevice(ctx->device);
+        (void)hipStreamSynchronize(ctx->stream);
+        if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
+        (void)hipEventDestroy(ctx->ev_call0);
+        (void)hipEventDestroy(ctx->ev_call1);
+        (void)hipEventDestroy(ctx->ev_k0);
+        (void)hipEventDestroy(ctx->ev_k1);
+        (void)hipStreamDestroy(ctx->stream);
+        delete ctx;
+    });
+}
+
+int gdist_ctx_synchronize(gdist_ctx* ctx) {
+    return guard([&] {
+        use_device(ctx);
+        GD_HIP(hipStreamSynchronize(ctx->stream));
+    });
+}
+
+int gdist_ctx_last_timing(gdist_ctx* ctx, double* kernel_ms, double* call_ms, int64_t* launches) {
+    return guard([&] {
+        GD_REQUIRE(ctx, "null context");
+        if (kernel_ms) *kernel_ms = ctx->last.kernel_ms;
+        if (call_ms) *call_ms = ctx->last.call_ms;
+        if (launches) *launches = ctx->last.launches;
+    });
+}
+
+int gdist_dev_alloc(gdist_ctx* ctx, int64_t bytes, void** dptr) {
+    return guard([&] {
+        use_device(ctx);
+        GD_REQUIRE(dptr && bytes >= 0, "bad allocation request");
+        *dptr = nullptr;
+        if (bytes) GD_HIP(hipMalloc(dptr, (size_t)bytes));
+    });
+}
+
+int gdist_dev_free(gdist_ctx* ctx, void* dptr) {
+    return guard([&] {
+        use_device(ctx);
+        GD_HIP(hipStreamSynchronize(ctx->stream));
+        if (dptr) GD_HIP(hipFree(dptr));
+    });
+}
+
+int gdist_memcpy_d2h(gdist_ctx* ctx, void* dst, const void* src, int64_t bytes) {
+    return guard([&] {
+        use_device(ctx);
+        if (bytes <= 0) return;
+        GD_HIP(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToHost, ctx->stream));
+        GD_HIP(hipStreamSynchronize(ctx->stream));
+    });
+}
+
+int gdist_memcpy_h2d(gdist_ctx* ctx, void* dst, const void* src, int64_t bytes) {
+    return guard([&] {
+        use_device(ctx);
+        if (bytes <= 0) return;
+        GD_HIP(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyHostToDevice, ctx->stream));
+        GD_HIP(hipStreamSynchronize(ctx->stream));
+    });
+}
+
+// ---------------------------------------------------------------------------
+int gdist_sets_pack(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* seqs, const int64_t* seq_off,
+                    int64_t nseqs, gdist_sets** out) {
+    return guard([&] {
+        use_device(ctx);
+        std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+        GD_REQUIRE(out && nseqs >= 0 && (nseqs == 0 || (seqs && seq_off)), "bad pack arguments");
+        *out = nullptr;
+        std::vector<int64_t> h(nseqs + 1, 0);
+        const int64_t base = nseqs ? seq_off[0] : 0;
+        for (int64_t s = 0; s <= nseqs; s++) h[s] = (nseqs ? seq_off[s] : 0) - base;
+        for (int64_t s = 0; s < nseqs; s++) GD_REQUIRE(h[s + 1] >= h[s], "sequence offsets must be non-decreasing");
+        const int64_t bytes = h[nseqs];
+        DevBuf dseq(bytes + 1, ctx->stream), doff((nseqs + 1) * 8, ctx->stream);
+        if (bytes) GD_HIP(hipMemcpyAsync(dseq.p, seqs + base, bytes, hipMemcpyHostToDevice, ctx->stream));
+        GD_HIP(hipMemcpyAsync(doff.p, h.data(), (nseqs + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+        auto* s = new gdist_sets();
+        s->ctx = ctx;
+        try {
+            pack_sets(ctx, kind, k, flags, dseq.as<char>(), doff.as<int64_t>(), h, s);
+        } catch (...) {
+            delete s;
+            throw;
+        }
+        *out = s;
+    });
+}
+
+int gdist_sets_pack_device(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_seqs,
+                           const int64_t* d_seq_off, int64_t nseqs, int64_t total_bytes, gdist_sets** out) {
+    return guard([&] {
+        use_device(ctx);
+        std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+        GD_REQUIRE(out && nseqs >= 0 && d_seq_off, "bad pack arguments");
+        *out = nullptr;
+        std::vector<int64_t> h(nseqs + 1, 0);
+        GD_HIP(hipMemcpyAsync(h.data(), d_seq_off, (nseqs + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+        GD_HIP(hipStreamSynchronize(ctx->stream));
+        for (int64_t s = 0; s < nseqs; s++) GD_REQUIRE(h[s + 1] >= h[s], "sequence offsets must be non-decreasing");
+        GD_REQUIRE(h[0] >= 0 && h[nseqs] <= total_bytes, "sequence offsets exceed the byte buffer");
+        auto* s = new gdist_sets();
+        s->ctx = ctx;
+        try {
+            pack_sets(ctx, kind, k, flags, d_seqs, d_seq_off, h, s);
+        } catch (...) {
+            delete s;
+            throw;
+        }
+        *out = s;
+    });
+}
+
+int gdist_sets_upload(gdist_ctx* ctx, int kind, int k, int64_t nsets, const int64_t* offsets, const uint64_t* codes,
+                      gdist_sets** out) {
+    return guard([&] {
+        use_device(ctx);
+        std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+        GD_REQUIRE(out && nsets >= 0 && offsets, "bad upload arguments");
+        GD_REQUIRE(kind == GDIST_DNA || kind == GDIST_PROT, "kind must be GDIST_DNA or GDIST_PROT");
+        *out = nullptr;
+        GD_REQUIRE(offsets[0] == 0, "offsets[0] must be 0");
+        for (int64_t s = 0; s < nsets; s++) {
+            GD_REQUIRE(offsets[s + 1] >= offsets[s], "offsets must be non-decreasing");
+            for (int64_t e = offsets[s] + 1; e < offsets[s + 1]; e++)
+                GD_REQUIRE(codes[e - 1] < codes[e], "codes of each set must be sorted and unique");
+        }
+        const int64_t total = offsets[nsets];
+        auto* s = new gdist_sets();
+        s->ctx = ctx; s->kind = kind; s->k = k; s->nsets = nsets; s->total = total;
+        s->h_off.assign(offsets, offsets + nsets + 1);
+        s->off.alloc((nsets + 1) * 8, ctx->stream);
+        s->codes.alloc(total * 8 + 8, ctx->stream);
+        GD_HIP(hipMemcpyAsync(s->off.p, offsets, (nsets + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+        if (total) GD_HIP(hipMemcpyAsync(s->codes.p, codes, total * 8, hipMemcpyHostToDevice, ctx->stream));
+        GD_HIP(hipStreamSynchronize(ctx->stream));
+        *out = s;
+    });
+}
+
+int gdist_sets_free(gdist_sets* s) {
+    return guard([&] {
+        if (!s) return;
+        gdist_ctx* ctx = s->ctx;
+        (void)hipSetDevice(ctx->device);
+        (void)hipStreamSynchronize(ctx->stream);
+        delete s;   // stream-ordered frees
+        (void)hipStreamSynchronize(ctx->stream);
+    });
+}
+
+int gdist_sets_info(const gdist_sets* s, int* kind, int* k, int64_t* nsets, int64_t* total) {
+    return guard([&] {
+        check_sets(s);
+        if (kind) *kind = s->kind;
+        if (k) *k = s->kind == GDIST_SKETCH ? s->width : s->k;
+        if (nsets) *nsets = s->nsets;
+        if (total) *total = s->total;
+    });
+}
+
+int gdist_sets_sizes(const gdist_sets* s, int64_t* sizes) {
+    return guard([&] {
+        check_sets(s);
+        GD_REQUIRE(sizes, "null output");
+        for (int64_t i = 0; i < s->nsets; i++) sizes[i] = s->h_off[i + 1] - s->h_off[i];
+    });
+}
+
+int gdist_sets_download(const gdist_sets* s, int64_t* offsets, uint64_t* codes) {
+    return guard([&] {
+        check_sets(s);
+        GD_REQUIRE(s->kind != GDIST_SKETCH, "use gdist_sketch_download for sketches");
+        use_device(s->ctx);
+        if (offsets) std::memcpy(offsets, s->h_off.data(), (s->nsets + 1) * 8);
+        if (codes && s->total)
+            GD_HIP(hipMemcpyAsync(codes, s->codes.p, s->total * 8, hipMemcpyDeviceToHost, s->ctx->stream));
+        GD_HIP(hipStreamSynchronize(s->ctx->stream));
+    });
+}
+
+int gdist_sets_build_bitsets(gdist_sets* s, unsigned flags) {
+    return guard([&] {
+        check_sets(s);
+        GD_REQUIRE(s->kind != GDIST_SKETCH, "bitsets are built from kmer sets");
+        use_device(s->ctx);
+        std::lock_guard<std::recursive_mutex> lk(s->ctx->mu);
+        build_bitsets(s->ctx, s, flags);
+    });
+}
+
+int gdist_sets_bitset_info(const gdist_sets* s, int64_t* dict_size, int64_t* words_per_set) {
+    return guard([&] {
+        check_sets(s);
+        if (dict_size) *dict_size = s->bits.p ? s->dict_size : -1;
+        if (words_per_set) *words_per_set = s->bits.p ? s->W : 0;
+    });
+}
+
+int gdist_sets_concat(const gdist_sets* a, const gdist_sets* b, gdist_sets** out) {
+    return guard([&] {
+        check_sets(a);
+        check_sets(b);
+        GD_REQUIRE(out, "null output");
+        GD_REQUIRE(a->ctx == b->ctx, "sets belong to different contexts");
+        GD_REQUIRE(a->kind == b->kind && a->k == b->k && a->width == b->width &&
+                       (a->flags & ~GDIST_NO_CASE_FOLD) == (b->flags & ~GDIST_NO_CASE_FOLD),
+                   "sets were packed with different kmer specs");
+        gdist_ctx* ctx = a->ctx;
+        use_device(ctx);
+        std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+        const size_t es = a->kind == GDIST_SKETCH ? 4 : 8;
+        auto* s = new gdist_sets();
+        s->ctx = ctx; s->kind = a->kind; s->k = a->k; s->flags = a->flags; s->width = a->width;
+        s->nsets = a->nsets + b->nsets;
+        s->total = a->total + b->total;
+        s->h_off = a->h_off;
+        for (int64_t i = 1; i <= b->nsets; i++) s->h_off.push_back(b->h_off[i] + a->total);
+        s->off.alloc((s->nsets + 1) * 8, ctx->stream);
+        GD_HIP(hipMemcpyAsync(s->off.p, s->h_off.data(), (s->nsets + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+        s->codes.alloc(s->total * es + 8, ctx->stream);
+        if (a->total)
+            GD_HIP(hipMemcpyAsync(s->codes.p, a->codes.p, a->total * es, hipMemcpyDeviceToDevice, ctx->stream));
+        if (b->total)
+            GD_HIP(hipMemcpyAsync((char*)s->codes.p + a->total * es, b->codes.p, b->total * es,
+                                  hipMemcpyDeviceToDevice, ctx->stream));
+        GD_HIP(hipStreamSynchronize(ctx->stream));
+        *out = s;
+    });
+}
+
+// ---------------------------------------------------------------------------
+int gdist_intersect_matrix(gdist_ctx* ctx, const gdist_sets* sets, int64_t r0, int64_t r1, int64_t c0, int64_t c1,
+                           int method, unsigned flags, int32_t* I_out, double* D_out, int64_t ld) {
+    return guard([&] {
+        use_device(ctx);
+        check_sets(sets);
+        GD_REQUIRE(sets->ctx == ctx, "sets belong to another context");
+        GD_REQUIRE(sets->kind != GDIST_SKETCH, "use gdist_sketch_matrix for sketches");
+        GD_REQUIRE(0 <= r0 && r0 <= r1 && r1 <= sets->nsets && 0 <= c0 && c0 <= c1 && c1 <= sets->nsets,
+                   "row/column range outside the set collection");
+        const int64_t nr = r1 - r0, nc = c1 - c0;
+        GD_REQUIRE(ld >= nc, "leading dimension smaller than the column range");
+        GD_REQUIRE(method >= GDIST_METHOD_AUTO && method <= GDIST_METHOD_BITSET, "unknown method");
+        std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+        auto* s = const_cast<gdist_sets*>(sets);
+        int m = method;
+        if (m == GDIST_METHOD_AUTO) m = s->bits.p ? GDIST_METHOD_BITSET : GDIST_METHOD_SORTED;
+        GD_REQUIRE(m == GDIST_METHOD_BITSET || s->has_codes, "this collection holds bitsets only");
+        if (m == GDIST_METHOD_BITSET && !s->bits.p) build_bitsets(ctx, s, 0);
+        if (m == GDIST_METHOD_SORTED && !s->segoff.p) build_segments(ctx, s);
+        const bool upper = (flags & GDIST_UPPER_TRIANGLE) != 0;
+        const bool dev = (flags & GDIST_OUT_DEVICE) != 0;
+        hipStream_t st = ctx->stream;
+        ctx->last = Timing{};
+        GD_HIP(hipEventRecord(ctx->ev_call0, st));
+        if (nr == 0 || nc == 0) {
+            gdist::finish_timing(ctx, false);
+            return;
+        }
+        // intersection counts: caller's device buffer or a temporary
+        DevBuf tI;
+        int32_t* dI;
+        int64_t ldI;
+        if (dev && I_out) {
+            dI = I_out; ldI = ld;
+        } else {
+            tI.alloc((size_t)nr * nc * 4, st);
+            dI = tI.as<int32_t>(); ldI = nc;
+        }
+        if (m == GDIST_METHOD_BITSET)   // accumulated with atomics
+            GD_HIP(hipMemset2DAsync(dI, ldI * 4, 0, nc * 4, nr, st));
+        if (m == GDIST_METHOD_BITSET) bitset_matrix(ctx, s, r0, r1, c0, c1, upper, dI, ldI);
+        else sorted_matrix(ctx, s, r0, r1, c0, c1, upper, dI, ldI);
+        DevBuf tD;
+        std::vector<double> hD;
+        std::vector<int32_t> hI;
+        if (D_out) {
+            double* dD;
+            int64_t ldD;
+            if (dev) { dD = D_out; ldD = ld; }
+            else { tD.alloc((size_t)nr * nc * 8, st); dD = tD.as<double>(); ldD = nc; }
+            distance_epilogue(ctx, s, r0, r1, c0, c1, upper, flags, dI, ldI, dD, ldD);
+            if (!dev) {
+                hD.resize((size_t)nr * nc);
+                GD_HIP(hipMemcpyAsync(hD.data(), dD, (size_t)nr * nc * 8, hipMemcpyDeviceToHost, st));
+            }
+        }
+        if (I_out && !dev) {
+            hI.resize((size_t)nr * nc);
+            GD_HIP(hipMemcpyAsync(hI.data(), dI, (size_t)nr * nc * 4, hipMemcpyDeviceToHost, st));
+        }
+        gdist::finish_timing(ctx, true);
+        // host outputs: entries excluded by the upper triangle stay untouched
+        for (int64_t a = 0; a < nr && !dev; a++)
+            for (int64_t b = 0; b < nc; b++) {
+                if (upper && c0 + b <= r0 + a) continue;
+                if (D_out) D_out[a * ld + b] = hD[a * nc + b];
+                if (I_out) I_out[a * ld + b] = hI[a * nc + b];
+            }
+    });
+}
+
+int gdist_row_query(gdist_ctx* ctx, const gdist_sets* sets, int64_t q, const int64_t* cols, int64_t ncols, int mode,
+                    double t, double* D_out, int32_t* hit, int64_t* best_idx, double* best_d) {
+    return guard([&] {
+        use_device(ctx);
+        check_sets(sets);
+        GD_REQUIRE(sets->ctx == ctx, "sets belong to another context");
+        GD_REQUIRE(sets->kind != GDIST_SKETCH, "row queries run on kmer sets");
+        GD_REQUIRE(q >= 0 && q < sets->nsets, "query index out of range");
+        GD_REQUIRE(ncols >= 0 && (ncols == 0 || cols), "bad column list");
+        GD_REQUIRE(mode >= GDIST_QUERY_ALL && mode <= GDIST_QUERY_ARGMIN, "unknown query mode");
+        for (int64_t c = 0; c < ncols; c++) GD_REQUIRE(cols[c] >= 0 && cols[c] < sets->nsets, "column index out of range");
+        std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+        auto* s = const_cast<gdist_sets*>(sets);
+        GD_REQUIRE(s->bits.p || s->has_codes, "this collection holds bitsets only");
+        hipStream_t st = ctx->stream;
+        std::vector<double> d(ncols);
+        if (ncols) {
+            DevBuf dc(ncols * 8, st), dI(ncols * 4, st), dD(ncols * 8, st);
+            GD_HIP(hipMemcpyAsync(dc.p, cols, ncols * 8, hipMemcpyHostToDevice, st));
+            if (s->bits.p) {
+                bitset_row(ctx, s, q, dc.as<int64_t>(), ncols, dI.as<int32_t>());
+            } else {
+                if (!s->segoff.p) build_segments(ctx, s);
+                sorted_row(ctx, s, q, dc.as<int64_t>(), ncols, dI.as<int32_t>());
+            }
+            row_epilogue(ctx, s, q, dc.as<int64_t>(), ncols, 0, dI.as<int32_t>(), dD.as<double>());
+            GD_HIP(hipMemcpyAsync(d.data(), dD.p, ncols * 8, hipMemcpyDeviceToHost, st));
+            GD_HIP(hipStreamSynchronize(st));
+        }
+        if (D_out) std::memcpy(D_out, d.data(), ncols * 8);
+        if (mode == GDIST_QUERY_ANY_LE && hit) {
+            // anyMatch(x -> x.distance(kmers) <= maxDist), DistanceRepsProcessor.java:400
+            int32_t h = 0;
+            for (int64_t c = 0; c < ncols; c++) if (d[c] <= t) { h = 1; break; }
+            *hit = h;
+        }
+        if (mode == GDIST_QUERY_ARGMIN) {
+            // reduce(NULL_RESULT, (x,y) -> x.distance <= y.distance ? x : y),
+            // DistanceRepsProcessor.java:330-332,448-449: the 1.0 identity wins ties at 1.0
+            int64_t bi = -1;
+            double bd = 1.0;
+            for (int64_t c = 0; c < ncols; c++) if (d[c] < bd) { bd = d[c]; bi = c; }
+            if (best_idx) *best_idx = bi;
+            if (best_d) *best_d = bd;
+        }
+    });
+}
+
+// ---------------------------------------------------------------------------
+int gdist_sketch_build(gdist_ctx* ctx, const gdist_sets* sets, int width, gdist_sets** out) {
+    return guard([&] {
+        use_device(ctx);
+        check_sets(sets);
+        GD_REQUIRE(out, "null output");
+        *out = nullptr;
+        std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+        auto* s = new gdist_sets();
+        s->ctx = ctx;
+        try {
+            sketch_build(ctx, sets, width, s);
+        } catch (...) {
+            delete s;
+            throw;
+        }
+        *out = s;
+    });
+}
+
+int gdist_sketch_upload(gdist_ctx* ctx, int width, int64_t nsets, const int64_t* offsets, const int32_t* sigs,
+                        gdist_sets** out) {
+    return guard([&] {
+        use_device(ctx);
+        GD_REQUIRE(out && nsets >= 0 && offsets && width > 0, "bad sketch upload arguments");
+        *out = nullptr;
+        GD_REQUIRE(offsets[0] == 0, "offsets[0] must be 0");
+        for (int64_t s = 0; s < nsets; s++) {
+            GD_REQUIRE(offsets[s + 1] >= offsets[s] && offsets[s + 1] - offsets[s] <= width,
+                       "each signature holds at most `width` hashes");
+            for (int64_t e = offsets[s] + 1; e < offsets[s + 1]; e++)
+                GD_REQUIRE(sigs[e - 1] < sigs[e], "signatures must be sorted ascending and unique");
+        }
+        std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+        const int64_t total = offsets[nsets];
+        auto* s = new gdist_sets();
+        s->ctx = ctx; s->kind = GDIST_SKETCH; s->width = width; s->nsets = nsets; s->total = total;
+        s->h_off.assign(offsets, offsets + nsets + 1);
+        s->off.alloc((nsets + 1) * 8, ctx->stream);
+        s->codes.alloc(total * 4 + 4, ctx->stream);
+        GD_HIP(hipMemcpyAsync(s->off.p, offsets, (nsets + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+        if (total) GD_HIP(hipMemcpyAsync(s->codes.p, sigs, total * 4, hipMemcpyHostToDevice, ctx->stream));
+        GD_HIP(hipStreamSynchronize(ctx->stream));
+        *out = s;
+    });
+}
+
+int gdist_sketch_download(const gdist_sets* sk, int64_t* offsets, int32_t* sigs) {
+    return guard([&] {
+        check_sets(sk);
+        GD_REQUIRE(sk->kind == GDIST_SKETCH, "not a sketch collection");
+        use_device(sk->ctx);
+        if (offsets) std::memcpy(offsets, sk->h_off.data(), (sk->nsets + 1) * 8);
+        if (sigs && sk->total)
+            GD_HIP(hipMemcpyAsync(sigs, sk->codes.p, sk->total * 4, hipMemcpyDeviceToHost, sk->ctx->stream));
+        GD_HIP(hipStreamSynchronize(sk->ctx->stream));
+    });
+}
+
+int gdist_sketch_matrix(gdist_ctx* ctx, const gdist_sets* sk, int64_t r0, int64_t r1, int64_t c0, int64_t c1,
+                        unsigned flags, int32_t* common_out, double* D_out, int64_t ld) {
+    return guard([&] {
+        use_device(ctx);
+        check_sets(sk);
+        GD_REQUIRE(sk->ctx == ctx, "sketches belong to another context");
+        GD_REQUIRE(sk->kind == GDIST_SKETCH, "not a sketch collection");
+        GD_REQUIRE(0 <= r0 && r0 <= r1 && r1 <= sk->nsets && 0 <= c0 && c0 <= c1 && c1 <= sk->nsets,
+                   "row/column range outside the sketch collection");
+        const int64_t nr = r1 - r0, nc = c1 - c0;
+        GD_REQUIRE(ld >= nc, "leading dimension smaller than the column range");
+        std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+        hipStream_t st = ctx->stream;
+        ctx->last = Timing{};
+        GD_HIP(hipEventRecord(ctx->ev_call0, st));
+        if (nr == 0 || nc == 0) {
+            gdist::finish_timing(ctx, false);
+            return;
+        }
+        const bool dev = (flags & GDIST_OUT_DEVICE) != 0;
+        DevBuf tC, tD;
+        int32_t* dC = nullptr;
+        double* dD = nullptr;
+        int64_t ldo = ld;
+        if (dev) {
+            dC = common_out; dD = D_out;
+        } else {
+            ldo = nc;
+            if (common_out) { tC.alloc((size_t)nr * nc * 4, st); dC = tC.as<int32_t>(); }
+            if (D_out) { tD.alloc((size_t)nr * nc * 8, st); dD = tD.as<double>(); }
+            // untouched (upper-triangle-excluded) entries keep the caller's values
+            if (dC) GD_HIP(hipMemcpy2DAsync(dC, nc * 4, common_out, ld * 4, nc * 4, nr, hipMemcpyHostToDevice, st));
+            if (dD) GD_HIP(hipMemcpy2DAsync(dD, nc * 8, D_out, ld * 8, nc * 8, nr, hipMemcpyHostToDevice, st));
+        }
+        sketch_matrix(ctx, sk, r0, r1, c0, c1, flags, dC, dD, ldo);
+        if (!dev) {
+            if (dC) GD_HIP(hipMemcpy2DAsync(common_out, ld * 4, dC, nc * 4, nc * 4, nr, hipMemcpyDeviceToHost, st));
+            if (dD) GD_HIP(hipMemcpy2DAsync(D_out, ld * 8, dD, nc * 8, nc * 8, nr, hipMemcpyDeviceToHost, st));
+        }
+        gdist::finish_timing(ctx, true);
+    });
+}
+
+// ---------------------------------------------------------------------------
+int gdist_comm_unique_id(char id[GDIST_UNIQUE_ID_BYTES]) {
+    return guard([&] {
+        static_assert(sizeof(ncclUniqueId) <= GDIST_UNIQUE_ID_BYTES, "unique id size");
+        ncclUniqueId u;
+        GD_NCCL(ncclGetUniqueId(&u));
+        std::memset(id, 0, GDIST_UNIQUE_ID_BYTES);
+        std::memcpy(id, &u, sizeof(u));
+    });
+}
+
+int gdist_comm_init(gdist_ctx* ctx, const char id[GDIST_UNIQUE_ID_BYTES], int nranks, int rank) {
+    return guard([&] {
+        use_device(ctx);
+        GD_REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank / world size");
+        ncclUniqueId u;
+        std::memcpy(&u, id, sizeof(u));
+        if (ctx->comm) { (void)ncclCommDestroy(ctx->comm); ctx->comm = nullptr; }
+        GD_NCCL(ncclCommInitRank(&ctx->comm, nranks, u, rank));
+        ctx->nranks = nranks;
+        ctx->rank = rank;
+    });
+}
+
+int gdist_comm_destroy(gdist_ctx* ctx) {
+    return guard([&] {
+        use_device(ctx);
+        if (ctx->comm) GD_NCCL(ncclCommDestroy(ctx->comm));
+        ctx->comm = nullptr;
+        ctx->nranks = 1;
+        ctx->rank = 0;
+    });
+}
+
+int gdist_sets_allgather(gdist_ctx* ctx, const gdist_sets* local, gdist_sets** out) {
+    return guard([&] {
+        use_device(ctx);
+        check_sets(local);
+        GD_REQUIRE(out, "null output");
+        GD_REQUIRE(ctx->comm, "communicator not initialised (gdist_comm_init)");
+        std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+        hipStream_t st = ctx->stream;
+        const int R = ctx->nranks;
+        const size_t es = local->kind == GDIST_SKETCH ? 4 : 8;
+        // 1. (nsets, total) of every rank
+        DevBuf mine(16, st), all(16 * R, st);
+        int64_t h2[2] = {local->nsets, local->total};
+        GD_HIP(hipMemcpyAsync(mine.p, h2, 16, hipMemcpyHostToDevice, st));
+        GD_NCCL(ncclAllGather(mine.p, all.p, 2, ncclInt64, ctx->comm, st));
+        std::vector<int64_t> hall(2 * R);
+        GD_HIP(hipMemcpyAsync(hall.data(), all.p, 16 * R, hipMemcpyDeviceToHost, st));
+        GD_HIP(hipStreamSynchronize(st));
+        int64_t mxs = 0, mxt = 0, ns = 0, nt = 0;
+        for (int r = 0; r < R; r++) {
+            mxs = std::max(mxs, hall[2 * r]); mxt = std::max(mxt, hall[2 * r + 1]);
+            ns += hall[2 * r]; nt += hall[2 * r + 1];
+        }
+        // 2. offsets and codes, padded to the largest shard (one all-gather each)
+        DevBuf so((mxs + 1) * 8, st), ao((mxs + 1) * 8 * R, st), sc(mxt * es + 8, st), ac((mxt * es + 8) * R, st);
+        GD_HIP(hipMemcpyAsync(so.p, local->off.p, (local->nsets + 1) * 8, hipMemcpyDeviceToDevice, st));
+        if (local->total) GD_HIP(hipMemcpyAsync(sc.p, local->codes.p, local->total * es, hipMemcpyDeviceToDevice, st));
+        GD_NCCL(ncclAllGather(so.p, ao.p, (mxs + 1), ncclInt64, ctx->comm, st));
+        GD_NCCL(ncclAllGather(sc.p, ac.p, mxt * es + 8, ncclUint8, ctx->comm, st));
+        std::vector<int64_t> hoff((mxs + 1) * R);
+        GD_HIP(hipMemcpyAsync(hoff.data(), ao.p, (mxs + 1) * 8 * R, hipMemcpyDeviceToHost, st));
+        GD_HIP(hipStreamSynchronize(st));
+        auto* s = new gdist_sets();
+        s->ctx = ctx; s->kind = local->kind; s->k = local->k; s->flags = local->flags; s->width = local->width;
+        s->nsets = ns; s->total = nt;
+        s->h_off.assign(1, 0);
+        s->codes.alloc(nt * es + 8, st);
+        int64_t at = 0;
+        for (int r = 0; r < R; r++) {
+            const int64_t rn = hall[2 * r], rt = hall[2 * r + 1];
+            for (int64_t i = 1; i <= rn; i++) s->h_off.push_back(at + hoff[(mxs + 1) * r + i]);
+            if (rt)
+                GD_HIP(hipMemcpyAsync((char*)s->codes.p + at * es, (char*)ac.p + (mxt * es + 8) * r, rt * es,
+                                      hipMemcpyDeviceToDevice, st));
+            at += rt;
+        }
+        s->off.alloc((ns + 1) * 8, st);
+        GD_HIP(hipMemcpyAsync(s->off.p, s->h_off.data(), (ns + 1) * 8, hipMemcpyHostToDevice, st));
+        GD_HIP(hipStreamSynchronize(st));
+        *out = s;
+    });
+}
+
+int gdist_sets_allgather_bitsets(gdist_ctx* ctx, const gdist_sets* local, unsigned flags, gdist_sets** out) {
+    return guard([&] {
+        use_device(ctx);
+        check_sets(local);
+        GD_REQUIRE(out, "null output");
+        GD_REQUIRE(local->kind != GDIST_SKETCH && local->has_codes, "local kmer sets with codes required");
+        std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+        hipStream_t st = ctx->stream;
+        const int R = ctx->comm ? ctx->nranks : 1;
+        const bool keep = (flags & GDIST_BITSET_KEEP_SINGLETONS) != 0;
+        // 1. local dictionary summary
+        Summary sum;
+        local_summary(ctx, local, sum);
+        // 2. every rank's (nsets, summary length)
+        std::vector<int64_t> hall(2 * R);
+        hall[0] = local->nsets; hall[1] = sum.n;
+        if (R > 1) {
+            DevBuf mine(16, st), all(16 * R, st);
+            GD_HIP(hipMemcpyAsync(mine.p, hall.data(), 16, hipMemcpyHostToDevice, st));
+            GD_NCCL(ncclAllGather(mine.p, all.p, 2, ncclInt64, ctx->comm, st));
+            GD_HIP(hipMemcpyAsync(hall.data(), all.p, 16 * R, hipMemcpyDeviceToHost, st));
+            GD_HIP(hipStreamSynchronize(st));
+        }
+        int64_t mxs = 0, mxn = 0, N = 0;
+        for (int r = 0; r < R; r++) { mxs = std::max(mxs, hall[2 * r]); mxn = std::max(mxn, hall[2 * r + 1]); N += hall[2 * r]; }
+        // 3. all-gather the summaries (padded), merge into the global dictionary
+        DevBuf gc, gn;
+        std::vector<SummaryView> parts;
+        if (R > 1) {
+            DevBuf sc(mxn * 8 + 8, st), sn(mxn * 4 + 4, st);
+            if (sum.n) {
+                GD_HIP(hipMemcpyAsync(sc.p, sum.codes.p, sum.n * 8, hipMemcpyDeviceToDevice, st));
+                GD_HIP(hipMemcpyAsync(sn.p, sum.counts.p, sum.n * 4, hipMemcpyDeviceToDevice, st));
+            }
+            gc.alloc((mxn * 8 + 8) * R, st);
+            gn.alloc((mxn * 4 + 4) * R, st);
+            GD_NCCL(ncclAllGather(sc.p, gc.p, mxn * 8 + 8, ncclUint8, ctx->comm, st));
+            GD_NCCL(ncclAllGather(sn.p, gn.p, mxn * 4 + 4, ncclUint8, ctx->comm, st));
+            for (int r = 0; r < R; r++)
+                parts.push_back({reinterpret_cast<const uint64_t*>((char*)gc.p + (mxn * 8 + 8) * r),
+                                 reinterpret_cast<const uint32_t*>((char*)gn.p + (mxn * 4 + 4) * r), hall[2 * r + 1]});
+        } else {
+            parts.push_back({sum.codes.as<uint64_t>(), sum.counts.as<uint32_t>(), sum.n});
+        }
+        DevBuf dict;
+        int64_t U = 0;
+        dictionary_from(ctx, parts, keep, dict, U);
+        gc.release(); gn.release();
+        const int64_t W = bitset_words(U);
+        // 4. local bitsets, padded to the largest shard, then one all-gather
+        DevBuf lb((size_t)mxs * W * 8 + 8, st);
+        if (local->nsets) fill_bits(ctx, local, dict.as<uint64_t>(), U, W, lb.as<unsigned long long>());
+        auto* s = new gdist_sets();
+        s->ctx = ctx; s->kind = local->kind; s->k = local->k; s->flags = local->flags;
+        s->nsets = N; s->has_codes = false;
+        s->bits.alloc((size_t)N * W * 8 + 8, st);
+        if (R > 1) {
+            DevBuf gb((size_t)mxs * W * 8 * R + 8, st);
+            GD_NCCL(ncclAllGather(lb.p, gb.p, (size_t)mxs * W, ncclUint64, ctx->comm, st));
+            int64_t at = 0;
+            for (int r = 0; r < R; r++) {
+                if (hall[2 * r])
+                    GD_HIP(hipMemcpyAsync(s->bits.as<uint64_t>() + at * W, gb.as<uint64_t>() + (size_t)mxs * W * r,
+                                          (size_t)hall[2 * r] * W * 8, hipMemcpyDeviceToDevice, st));
+                at += hall[2 * r];
+            }
+            GD_HIP(hipStreamSynchronize(st));
+        } else if (N) {
+            GD_HIP(hipMemcpyAsync(s->bits.p, lb.p, (size_t)N * W * 8, hipMemcpyDeviceToDevice, st));
+        }
+        // 5. set sizes of all ranks (one all-gather of the padded size arrays)
+        std::vector<int64_t> sizes(mxs + 1, 0), allsz((mxs + 1) * R, 0);
+        for (int64_t i = 0; i < local->nsets; i++) sizes[i] = local->h_off[i + 1] - local->h_off[i];
+        if (R > 1) {
+            DevBuf ds((mxs + 1) * 8, st), da((mxs + 1) * 8 * R, st);
+            GD_HIP(hipMemcpyAsync(ds.p, sizes.data(), (mxs + 1) * 8, hipMemcpyHostToDevice, st));
+            GD_NCCL(ncclAllGather(ds.p, da.p, mxs + 1, ncclInt64, ctx->comm, st));
+            GD_HIP(hipMemcpyAsync(allsz.data(), da.p, (mxs + 1) * 8 * R, hipMemcpyDeviceToHost, st));
+            GD_HIP(hipStreamSynchronize(st));
+        } else {
+            allsz = sizes;
+        }
+        s->h_off.assign(1, 0);
+        for (int r = 0; r < R; r++)
+            for (int64_t i = 0; i < hall[2 * r]; i++) s->h_off.push_back(s->h_off.back() + allsz[(mxs + 1) * r + i]);
+        s->total = s->h_off.back();
+        s->off.alloc((N + 1) * 8, st);
+        GD_HIP(hipMemcpyAsync(s->off.p, s->h_off.data(), (N + 1) * 8, hipMemcpyHostToDevice, st));
+        s->codes.alloc(8, st);
+        s->W = W; s->dict_size = U; s->bits_keep_singletons = keep;
+        GD_HIP(hipStreamSynchronize(st));
+        *out = s;
+    });
+}
+
+int gdist_comm_allreduce_max(gdist_ctx* ctx, double* value) {
+    return guard([&] {
+        use_device(ctx);
+        GD_REQUIRE(value, "null value");
+        if (!ctx->comm) return;
+        DevBuf d(8, ctx->stream);
+        GD_HIP(hipMemcpyAsync(d.p, value, 8, hipMemcpyHostToDevice, ctx->stream));
+        GD_NCCL(ncclAllReduce(d.p, d.p, 1, ncclFloat64, ncclMax, ctx->comm, ctx->stream));
+        GD_HIP(hipMemcpyAsync(value, d.p, 8, hipMemcpyDeviceToHost, ctx->stream));
+        GD_HIP(hipStreamSynchronize(ctx->stream));
+    });
+}
+
+int gdist_triangle_partition(int64_t n, int nparts, int64_t align, int64_t* bounds) {
+    return guard([&] {
+        GD_REQUIRE(n >= 0 && nparts >= 1 && align >= 1 && bounds, "bad partition arguments");
+        bounds[0] = 0;
+        for (int g = 1; g < nparts; g++) {
+            const double r = (double)n * (1.0 - std::sqrt(1.0 - (double)g / (double)nparts));
+            int64_t b = (int64_t)std::llround(r / (double)align) * align;
+            b = std::min<int64_t>(n, std::max<int64_t>(bounds[g - 1], b));
+            bounds[g] = b;
+        }
+        bounds[nparts] = n;
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,189 @@
+// gdist_internal.hpp — shared host/device definitions of libgdist.so.
+//
+// Everything here is gfx950 (MI355X) only: 64-lane waves, 160 KiB LDS per CU,
+// 8 XCDs of 32 CUs. No CUDA compatibility layer, no dual paths.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdint>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/gdist.h"
+
+namespace gdist {
+
+// ---------------------------------------------------------------------------
+// errors: every C-ABI entry point converts an Error into its status code and
+// stores the message in a thread-local string (gdist_last_error()).
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+void set_last_error(const std::string& msg);
+
+#define GD_HIP(x)                                                                        \
+    do {                                                                                 \
+        hipError_t e_ = (x);                                                             \
+        if (e_ != hipSuccess)                                                            \
+            throw ::gdist::Error(e_ == hipErrorOutOfMemory ? GDIST_ENOMEM : GDIST_EDEVICE, \
+                                 std::string(#x) + ": " + hipGetErrorString(e_));       \
+    } while (0)
+
+#define GD_REQUIRE(cond, msg)                                                            \
+    do {                                                                                 \
+        if (!(cond)) throw ::gdist::Error(GDIST_EINVAL, msg);                            \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// device buffers: stream-ordered allocations on the context stream.
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipStream_t stream = nullptr;
+    DevBuf() = default;
+    DevBuf(size_t n, hipStream_t s) { alloc(n, s); }
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    DevBuf(DevBuf&& o) noexcept { *this = std::move(o); }
+    DevBuf& operator=(DevBuf&& o) noexcept {
+        release();
+        p = o.p; bytes = o.bytes; stream = o.stream;
+        o.p = nullptr; o.bytes = 0;
+        return *this;
+    }
+    ~DevBuf() { release(); }
+    void alloc(size_t n, hipStream_t s) {
+        release();
+        stream = s;
+        bytes = n;
+        if (n) GD_HIP(hipMallocAsync(&p, n, s));
+    }
+    void release() noexcept {
+        if (p) (void)hipFreeAsync(p, stream);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+// H2D copy of a host temporary: a pageable-source hipMemcpyAsync may be
+// executed by the stream after the call returns (behind earlier work), so a
+// host buffer that dies at scope exit must be copied synchronously.
+inline void h2d_sync(void* dst, const void* src, size_t bytes, hipStream_t s) {
+    if (!bytes) return;
+    GD_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
+    GD_HIP(hipStreamSynchronize(s));
+}
+
+// ---------------------------------------------------------------------------
+struct Timing {
+    double kernel_ms = 0.0, call_ms = 0.0;
+    int64_t launches = 0;
+};
+
+}  // namespace gdist
+
+struct gdist_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::recursive_mutex mu;
+    hipEvent_t ev_call0 = nullptr, ev_call1 = nullptr, ev_k0 = nullptr, ev_k1 = nullptr;
+    gdist::Timing last;
+    int cus = 256;
+    // RCCL communicator (multi-GPU row sharding)
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+};
+
+// A collection of kmer sets resident in HBM.
+//   codes:  CSR of sorted unique uint64 codes (kind DNA / PROT)
+//   sigs:   CSR of sorted int32 signatures (kind SKETCH)
+//   bits:   optional dictionary-rank bitsets, [nsets][W] uint64 row-major
+//   segoff: optional value-range segment index for the sorted path,
+//           [nsets][nseg+1] absolute positions into codes
+struct gdist_sets {
+    gdist_ctx* ctx = nullptr;
+    int kind = GDIST_DNA;
+    int k = 0;
+    unsigned flags = 0;
+    int width = 0;                        // sketches
+    int64_t nsets = 0, total = 0;
+    std::vector<int64_t> h_off;           // nsets+1, host mirror (sizes)
+    gdist::DevBuf off;                    // int64 [nsets+1]
+    gdist::DevBuf codes;                  // uint64 [total] or int32 [total] for sketches
+    // bitset representation
+    gdist::DevBuf bits;                   // uint64 [nsets][W]
+    int64_t W = 0, dict_size = 0;
+    bool bits_keep_singletons = false;
+    // segment index of the sorted path
+    gdist::DevBuf segoff;                 // int64 [nsets][nseg+1]
+    int nseg = 0;
+    int64_t max_seg = 0;
+    bool has_codes = true;                // false for all-gathered bitset-only collections
+};
+
+namespace gdist {
+
+// pack.hip
+void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_seqs,
+               const int64_t* d_seq_off, const std::vector<int64_t>& h_seq_off, gdist_sets* out);
+void sort_pairs_u64_i32(gdist_ctx* ctx, uint64_t*& keys, uint64_t*& keys_alt, int32_t*& vals,
+                        int32_t*& vals_alt, size_t n, int begin_bit, int end_bit);
+void sort_keys_u64(gdist_ctx* ctx, uint64_t*& keys, uint64_t*& keys_alt, size_t n, int begin_bit,
+                   int end_bit);
+void exclusive_scan_i64(gdist_ctx* ctx, const int64_t* in, int64_t* out, size_t n);
+void exclusive_scan_i32_to_i64(gdist_ctx* ctx, const int32_t* in, int64_t* out, size_t n);
+int code_bits(int kind, int k, unsigned flags);
+
+// bitset.hip — dictionary summaries: sorted distinct codes + number of sets holding each
+struct Summary {
+    DevBuf codes;    // uint64 [n]
+    DevBuf counts;   // uint32 [n]
+    int64_t n = 0;
+};
+struct SummaryView {
+    const uint64_t* codes;
+    const uint32_t* counts;
+    int64_t n;
+};
+void local_summary(gdist_ctx* ctx, const gdist_sets* s, Summary& out);
+void dictionary_from(gdist_ctx* ctx, const std::vector<SummaryView>& parts, bool keep, DevBuf& dict,
+                     int64_t& U);
+int64_t bitset_words(int64_t dict_size);
+void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_t U, int64_t W,
+               unsigned long long* bits);
+void build_bitsets(gdist_ctx* ctx, gdist_sets* s, unsigned flags);
+void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0,
+                   int64_t c1, bool upper, int32_t* d_I, int64_t ldI);
+
+// sorted.hip
+void build_segments(gdist_ctx* ctx, gdist_sets* s);
+void sorted_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0,
+                   int64_t c1, bool upper, int32_t* d_I, int64_t ldI);
+void sorted_row(gdist_ctx* ctx, const gdist_sets* s, int64_t q, const int64_t* d_cols, int64_t ncols,
+                int32_t* d_I);
+
+void bitset_row(gdist_ctx* ctx, const gdist_sets* s, int64_t q, const int64_t* d_cols, int64_t ncols,
+                int32_t* d_I);
+void row_epilogue(gdist_ctx* ctx, const gdist_sets* s, int64_t q, const int64_t* d_cols, int64_t ncols,
+                  unsigned flags, const int32_t* d_I, double* d_D);
+
+// epilogue (bitset.hip): D from I and set sizes, Java expression, fp64
+void distance_epilogue(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0,
+                       int64_t c1, bool upper, unsigned flags, const int32_t* d_I, int64_t ldI,
+                       double* d_D, int64_t ldD);
+
+// sketch.hip
+void sketch_build(gdist_ctx* ctx, const gdist_sets* s, int width, gdist_sets* out);
+void sketch_matrix(gdist_ctx* ctx, const gdist_sets* sk, int64_t r0, int64_t r1, int64_t c0,
+                   int64_t c1, unsigned flags, int32_t* d_common, double* d_D, int64_t ld);
+
+__host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+}  // namespace gdist

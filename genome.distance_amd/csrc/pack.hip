@@ -1,0 +1,415 @@
+// pack.hip — device-side kmer extraction and packing into sorted unique
+// uint64 code sets (CSR).  Replaces KmerType.createKmers(seq, K)
+// (FastaDistanceProcessor.java:153,184), new GenomeKmers(genome)
+// (GenomeProcessor.java:305,335) and new ProteinKmers(seq)
+// (ProteinKmerReader.java:101), which build a HashSet<String> per sequence.
+//
+// Pipeline per chunk of sequences (bounded so keys+values fit comfortably):
+//   1. validate   — unencodable chars in keep / 5-bit modes -> EINVAL
+//   2. extract    — one thread per window: code (fwd, rc or canonical),
+//                   value = set id, or the "invalid" id for skipped windows
+//   3. radix sort by code (code bits only), then stable radix sort by set id
+//   4. unique flags + exclusive scan -> compacted CSR codes, offsets by
+//      lower_bound of each set id in the sorted id array
+// The alphabet maps are order preserving, so code order == Java String order.
+#include <cstring>
+#include <rocprim/rocprim.hpp>
+
+#include <algorithm>
+
+#include "gdist_internal.hpp"
+
+namespace gdist {
+
+int code_bits(int kind, int k, unsigned flags) {
+    unsigned am = flags & GDIST_AMBIG_MASK;
+    if (kind == GDIST_DNA) {
+        bool skip = (am != GDIST_AMBIG_KEEP);
+        return skip ? 2 * k : 3 * k;
+    }
+    return k <= 8 ? 8 * k : 5 * k;
+}
+
+namespace {
+
+// Symbol table per (kind, flags): sym[c] = code symbol, -1 = unencodable,
+// -2 = skip the window (ambiguity skip mode). comp[sym] for DNA.
+struct Alphabet {
+    int8_t sym[256];
+    int8_t comp[8];
+    int bits;
+    bool fold;
+};
+
+Alphabet make_alphabet(int kind, int k, unsigned flags) {
+    Alphabet a{};
+    unsigned am = flags & GDIST_AMBIG_MASK;
+    bool skip = (am == GDIST_AMBIG_SKIP) || (am == GDIST_AMBIG_DEFAULT && kind == GDIST_DNA);
+    a.fold = (kind == GDIST_DNA) || !(flags & GDIST_NO_CASE_FOLD);
+    for (int c = 0; c < 256; c++) a.sym[c] = -1;
+    for (int i = 0; i < 8; i++) a.comp[i] = 0;
+    if (kind == GDIST_DNA) {
+        if (skip) {
+            a.bits = 2;
+            const char* al = "ACGT";
+            for (int i = 0; i < 4; i++) a.sym[(unsigned char)al[i]] = (int8_t)i;
+            for (int c = 0; c < 256; c++) if (a.sym[c] < 0) a.sym[c] = -2;
+            a.comp[0] = 3; a.comp[1] = 2; a.comp[2] = 1; a.comp[3] = 0;
+        } else {
+            a.bits = 3;
+            const char* al = "ACGNRTY";
+            for (int i = 0; i < 7; i++) a.sym[(unsigned char)al[i]] = (int8_t)i;
+            const int8_t cp[7] = {5, 2, 1, 3, 6, 0, 4};
+            for (int i = 0; i < 7; i++) a.comp[i] = cp[i];
+        }
+    } else {
+        a.bits = (k <= 8) ? 8 : 5;
+        for (int c = 0; c < 256; c++) {
+            if (a.bits == 8) a.sym[c] = 0;            // raw byte (value taken from c)
+            else if (c == '*') a.sym[c] = 0;
+            else if (c >= 'A' && c <= 'Z') a.sym[c] = (int8_t)(1 + c - 'A');
+        }
+        if (skip) {
+            for (int c = 0; c < 256; c++) {
+                bool std_aa = c != 0 && std::char_traits<char>::find("ACDEFGHIKLMNPQRSTVWY", 20, (char)c);
+                if (!std_aa) a.sym[c] = -2;
+            }
+        }
+    }
+    // fold lower case onto upper case entries
+    if (a.fold)
+        for (int c = 'a'; c <= 'z'; c++) a.sym[c] = a.sym[c - 32];
+    a.sym[0] = -2;   // sequence separator: no kmer spans it, in every mode
+    return a;
+}
+
+struct AlphabetDev {
+    int8_t sym[256];
+    int8_t comp[8];
+};
+
+__global__ void validate_kernel(const unsigned char* __restrict__ seqs, int64_t begin, int64_t end,
+                                AlphabetDev al, int* __restrict__ bad) {
+    int64_t i = begin + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    int local = 0;
+    for (; i < end; i += stride) local |= (al.sym[seqs[i]] == -1);
+    if (__any(local) && (threadIdx.x & 63) == 0) atomicOr(bad, 1);
+}
+
+// Window w of the chunk -> sequence s (binary search in win_off), position,
+// then the k symbols. Emits 1 or 2 (BOTH) entries per window.
+template <bool RAW8>
+__global__ __launch_bounds__(256) void extract_kernel(
+    const unsigned char* __restrict__ seqs, const int64_t* __restrict__ seq_off,
+    const int64_t* __restrict__ win_off, int nseq, int64_t nwin, int k, int bits, int strand,
+    AlphabetDev al, uint64_t* __restrict__ keys, int32_t* __restrict__ vals) {
+    __shared__ int8_t sym[256];
+    __shared__ int8_t comp[8];
+    for (int t = threadIdx.x; t < 256; t += blockDim.x) sym[t] = al.sym[t];
+    if (threadIdx.x < 8) comp[threadIdx.x] = al.comp[threadIdx.x];
+    __syncthreads();
+    const uint64_t mask = (k * bits >= 64) ? ~0ULL : ((1ULL << (k * bits)) - 1);
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nwin; w += stride) {
+        // upper_bound(win_off[0..nseq], w) - 1
+        int lo = 0, hi = nseq;
+        while (hi - lo > 1) {
+            int mid = (lo + hi) >> 1;
+            if (win_off[mid] <= w) lo = mid; else hi = mid;
+        }
+        const int s = lo;
+        const unsigned char* p = seqs + seq_off[s] + (w - win_off[s]);
+        uint64_t fwd = 0, rc = 0;
+        bool valid = true;
+        for (int t = 0; t < k; t++) {
+            unsigned char c = p[t];
+            int sy = sym[c];
+            valid &= (sy >= 0);
+            // raw 8-bit protein codes take the (pre-folded) byte itself
+            uint64_t v = RAW8 ? (uint64_t)c : (uint64_t)(sy < 0 ? 0 : sy);
+            fwd = (fwd << bits) | v;
+            if (strand != GDIST_STRAND_FWD)
+                rc |= (uint64_t)comp[sy < 0 ? 0 : sy] << (bits * t);
+        }
+        fwd &= mask;
+        const int32_t id = valid ? s : nseq;
+        if (strand == GDIST_STRAND_BOTH) {
+            keys[2 * w] = fwd; vals[2 * w] = id;
+            keys[2 * w + 1] = rc; vals[2 * w + 1] = id;
+        } else if (strand == GDIST_STRAND_CANON) {
+            keys[w] = fwd < rc ? fwd : rc; vals[w] = id;
+        } else {
+            keys[w] = fwd; vals[w] = id;
+        }
+    }
+}
+
+// Raw 8-bit protein codes with case folding need the folded byte value.
+__global__ __launch_bounds__(256) void fold_bytes_kernel(unsigned char* __restrict__ dst,
+                                                         const unsigned char* __restrict__ src,
+                                                         int64_t n) {
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        unsigned char c = src[i];
+        dst[i] = (c >= 'a' && c <= 'z') ? (unsigned char)(c - 32) : c;
+    }
+}
+
+// After the two sorts: unique & valid flags.
+__global__ void unique_flags_kernel(const uint64_t* __restrict__ codes, const int32_t* __restrict__ ids,
+                                    int64_t n, int32_t invalid, int32_t* __restrict__ flag) {
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        int32_t id = ids[i];
+        bool f = id != invalid && (i == 0 || codes[i] != codes[i - 1] || id != ids[i - 1]);
+        flag[i] = f ? 1 : 0;
+    }
+}
+
+__global__ void compact_kernel(const uint64_t* __restrict__ codes, const int32_t* __restrict__ flag,
+                               const int64_t* __restrict__ pos, int64_t n, uint64_t* __restrict__ out) {
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        if (flag[i]) out[pos[i]] = codes[i];
+}
+
+// off[s] = pos[lower_bound(ids, s)] (or the unique total past the end).
+__global__ void set_offsets_kernel(const int32_t* __restrict__ ids, const int64_t* __restrict__ pos,
+                                   const int32_t* __restrict__ flag, int64_t n, int nsets,
+                                   int64_t base, int64_t* __restrict__ off) {
+    int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s > nsets) return;
+    int64_t lo = 0, hi = n;   // first index with ids[idx] >= s
+    while (lo < hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if (ids[mid] < s) lo = mid + 1; else hi = mid;
+    }
+    int64_t total = n ? pos[n - 1] + flag[n - 1] : 0;
+    off[s] = base + (lo < n ? pos[lo] : total);
+}
+
+inline int grid_for(int64_t n, int block = 256, int64_t cap = 256 * 32) {
+    int64_t g = ceil_div(n, block);
+    return (int)std::max<int64_t>(1, std::min<int64_t>(g, cap));
+}
+
+}  // namespace
+
+void sort_pairs_u64_i32(gdist_ctx* ctx, uint64_t*& keys, uint64_t*& keys_alt, int32_t*& vals,
+                        int32_t*& vals_alt, size_t n, int begin_bit, int end_bit) {
+    if (n == 0) return;
+    rocprim::double_buffer<uint64_t> kb(keys, keys_alt);
+    rocprim::double_buffer<int32_t> vb(vals, vals_alt);
+    size_t tmp = 0;
+    GD_HIP(rocprim::radix_sort_pairs(nullptr, tmp, kb, vb, n, begin_bit, end_bit, ctx->stream));
+    DevBuf t(tmp, ctx->stream);
+    GD_HIP(rocprim::radix_sort_pairs(t.p, tmp, kb, vb, n, begin_bit, end_bit, ctx->stream));
+    keys = kb.current(); keys_alt = kb.alternate();
+    vals = vb.current(); vals_alt = vb.alternate();
+}
+
+static void sort_pairs_i32_u64(gdist_ctx* ctx, int32_t*& keys, int32_t*& keys_alt, uint64_t*& vals,
+                               uint64_t*& vals_alt, size_t n, int end_bit) {
+    if (n == 0) return;
+    // ids are non-negative: sort them as unsigned
+    rocprim::double_buffer<uint32_t> kb(reinterpret_cast<uint32_t*>(keys),
+                                        reinterpret_cast<uint32_t*>(keys_alt));
+    rocprim::double_buffer<uint64_t> vb(vals, vals_alt);
+    size_t tmp = 0;
+    GD_HIP(rocprim::radix_sort_pairs(nullptr, tmp, kb, vb, n, 0, end_bit, ctx->stream));
+    DevBuf t(tmp, ctx->stream);
+    GD_HIP(rocprim::radix_sort_pairs(t.p, tmp, kb, vb, n, 0, end_bit, ctx->stream));
+    keys = reinterpret_cast<int32_t*>(kb.current());
+    keys_alt = reinterpret_cast<int32_t*>(kb.alternate());
+    vals = vb.current(); vals_alt = vb.alternate();
+}
+
+void sort_keys_u64(gdist_ctx* ctx, uint64_t*& keys, uint64_t*& keys_alt, size_t n, int begin_bit,
+                   int end_bit) {
+    if (n == 0) return;
+    rocprim::double_buffer<uint64_t> kb(keys, keys_alt);
+    size_t tmp = 0;
+    GD_HIP(rocprim::radix_sort_keys(nullptr, tmp, kb, n, begin_bit, end_bit, ctx->stream));
+    DevBuf t(tmp, ctx->stream);
+    GD_HIP(rocprim::radix_sort_keys(t.p, tmp, kb, n, begin_bit, end_bit, ctx->stream));
+    keys = kb.current(); keys_alt = kb.alternate();
+}
+
+void exclusive_scan_i64(gdist_ctx* ctx, const int64_t* in, int64_t* out, size_t n) {
+    if (n == 0) return;
+    size_t tmp = 0;
+    GD_HIP(rocprim::exclusive_scan(nullptr, tmp, in, out, (int64_t)0, n, rocprim::plus<int64_t>(),
+                                   ctx->stream));
+    DevBuf t(tmp, ctx->stream);
+    GD_HIP(rocprim::exclusive_scan(t.p, tmp, in, out, (int64_t)0, n, rocprim::plus<int64_t>(),
+                                   ctx->stream));
+}
+
+void exclusive_scan_i32_to_i64(gdist_ctx* ctx, const int32_t* in, int64_t* out, size_t n) {
+    if (n == 0) return;
+    size_t tmp = 0;
+    auto it = rocprim::make_transform_iterator(in, [] __device__(int32_t v) { return (int64_t)v; });
+    GD_HIP(rocprim::exclusive_scan(nullptr, tmp, it, out, (int64_t)0, n, rocprim::plus<int64_t>(),
+                                   ctx->stream));
+    DevBuf t(tmp, ctx->stream);
+    GD_HIP(rocprim::exclusive_scan(t.p, tmp, it, out, (int64_t)0, n, rocprim::plus<int64_t>(),
+                                   ctx->stream));
+}
+
+// Pack sequences [0, nseq) (device bytes + device/host offsets) into `out`.
+void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_seqs,
+               const int64_t* d_seq_off, const std::vector<int64_t>& h_seq_off, gdist_sets* out) {
+    const int64_t nseq = (int64_t)h_seq_off.size() - 1;
+    GD_REQUIRE(kind == GDIST_DNA || kind == GDIST_PROT, "kind must be GDIST_DNA or GDIST_PROT");
+    unsigned am = flags & GDIST_AMBIG_MASK;
+    GD_REQUIRE(am != (GDIST_AMBIG_SKIP | GDIST_AMBIG_KEEP), "AMBIG_SKIP and AMBIG_KEEP are exclusive");
+    bool dna_keep = kind == GDIST_DNA && am == GDIST_AMBIG_KEEP;
+    if (kind == GDIST_DNA)
+        GD_REQUIRE(k >= 1 && k <= (dna_keep ? 21 : 32), "DNA kmer size out of range (1..32 skip, 1..21 keep)");
+    else
+        GD_REQUIRE(k >= 1 && k <= 12, "protein kmer size out of range (1..12)");
+    int strand = (kind == GDIST_DNA) ? (int)(flags & GDIST_STRAND_MASK) : (int)GDIST_STRAND_FWD;
+    GD_REQUIRE(strand != 3, "invalid strand mode");
+    const int mult = (strand == GDIST_STRAND_BOTH) ? 2 : 1;
+
+    Alphabet alh = make_alphabet(kind, k, flags);
+    AlphabetDev al{};
+    for (int c = 0; c < 256; c++) al.sym[c] = alh.sym[c];
+    for (int c = 0; c < 8; c++) al.comp[c] = alh.comp[c];
+    const int bits = alh.bits;
+    const bool raw8 = (kind == GDIST_PROT && bits == 8);
+    const int cbits = code_bits(kind, k, flags);
+    hipStream_t st = ctx->stream;
+
+    out->kind = kind; out->k = k; out->flags = flags; out->nsets = nseq;
+
+    // 1. validation of the whole byte range (keep modes; 5-bit protein)
+    const int64_t total_bytes = h_seq_off.back() - h_seq_off.front();
+    bool need_validate = dna_keep || (kind == GDIST_PROT && bits == 5);
+    if (need_validate && total_bytes > 0) {
+        DevBuf bad(sizeof(int), st);
+        GD_HIP(hipMemsetAsync(bad.p, 0, sizeof(int), st));
+        validate_kernel<<<grid_for(total_bytes), 256, 0, st>>>(
+            reinterpret_cast<const unsigned char*>(d_seqs), h_seq_off.front(), h_seq_off.back(), al,
+            bad.as<int>());
+        GD_HIP(hipGetLastError());
+        int hbad = 0;
+        GD_HIP(hipMemcpyAsync(&hbad, bad.p, sizeof(int), hipMemcpyDeviceToHost, st));
+        GD_HIP(hipStreamSynchronize(st));
+        GD_REQUIRE(!hbad, "sequence holds a character the kmer code cannot represent "
+                          "(DNA keep mode: ACGNRTY; protein k>8: A-Z and '*')");
+    }
+
+    // raw 8-bit protein codes take the folded byte value
+    DevBuf folded;
+    const unsigned char* src = reinterpret_cast<const unsigned char*>(d_seqs);
+    if (raw8 && alh.fold && total_bytes > 0) {
+        folded.alloc((size_t)h_seq_off.back(), st);
+        fold_bytes_kernel<<<grid_for(h_seq_off.back()), 256, 0, st>>>(folded.as<unsigned char>(), src,
+                                                                        h_seq_off.back());
+        GD_HIP(hipGetLastError());
+        src = folded.as<unsigned char>();
+    }
+
+    // windows per sequence
+    std::vector<int64_t> nwin(nseq);
+    for (int64_t s = 0; s < nseq; s++) {
+        int64_t len = h_seq_off[s + 1] - h_seq_off[s];
+        GD_REQUIRE(len >= 0, "sequence offsets must be non-decreasing");
+        nwin[s] = std::max<int64_t>(0, len - k + 1);
+    }
+
+    // 2-4. chunks of sequences, at most kChunk entries each
+    const int64_t kChunk = int64_t(1) << 30;
+    std::vector<DevBuf> chunk_codes;
+    std::vector<int64_t> chunk_total;
+    std::vector<int64_t> h_off(nseq + 1, 0);
+    DevBuf d_off((nseq + 1) * sizeof(int64_t), st);
+    int64_t base = 0;
+    int64_t s0 = 0;
+    while (s0 < nseq || (nseq == 0 && s0 == 0)) {
+        if (nseq == 0) break;
+        int64_t s1 = s0, entries = 0;
+        while (s1 < nseq && (s1 == s0 || entries + nwin[s1] * mult <= kChunk)) {
+            entries += nwin[s1] * mult;
+            s1++;
+        }
+        const int nc = (int)(s1 - s0);
+        std::vector<int64_t> hwo(nc + 1, 0);
+        for (int i = 0; i < nc; i++) hwo[i + 1] = hwo[i] + nwin[s0 + i];
+        const int64_t nw = hwo[nc];
+        const int64_t n = nw * mult;
+        DevBuf cw((nc + 1) * sizeof(int64_t), st);
+        h2d_sync(cw.p, hwo.data(), (nc + 1) * sizeof(int64_t), st);
+
+        DevBuf kA(n * 8 + 8, st), kB(n * 8 + 8, st), vA(n * 4 + 4, st), vB(n * 4 + 4, st);
+        if (nw > 0) {
+            if (raw8)
+                extract_kernel<true><<<grid_for(nw, 256, 256 * 64), 256, 0, st>>>(
+                    src, d_seq_off + s0, cw.as<int64_t>(), nc, nw, k, bits, strand, al, kA.as<uint64_t>(),
+                    vA.as<int32_t>());
+            else
+                extract_kernel<false><<<grid_for(nw, 256, 256 * 64), 256, 0, st>>>(
+                    src, d_seq_off + s0, cw.as<int64_t>(), nc, nw, k, bits, strand, al, kA.as<uint64_t>(),
+                    vA.as<int32_t>());
+            GD_HIP(hipGetLastError());
+        }
+        uint64_t* keys = kA.as<uint64_t>(); uint64_t* keys_alt = kB.as<uint64_t>();
+        int32_t* ids = vA.as<int32_t>(); int32_t* ids_alt = vB.as<int32_t>();
+        sort_pairs_u64_i32(ctx, keys, keys_alt, ids, ids_alt, (size_t)n, 0, std::min(64, cbits));
+        int idbits = 1;
+        while ((int64_t(1) << idbits) <= nc) idbits++;
+        sort_pairs_i32_u64(ctx, ids, ids_alt, keys, keys_alt, (size_t)n, idbits);
+
+        DevBuf flag(n * 4 + 4, st), pos(n * 8 + 8, st);
+        if (n > 0) {
+            unique_flags_kernel<<<grid_for(n), 256, 0, st>>>(keys, ids, n, nc, flag.as<int32_t>());
+            GD_HIP(hipGetLastError());
+            exclusive_scan_i32_to_i64(ctx, flag.as<int32_t>(), pos.as<int64_t>(), (size_t)n);
+        }
+        // chunk offsets straight into the final offsets array
+        set_offsets_kernel<<<(int)ceil_div(nc + 1, 256), 256, 0, st>>>(
+            ids, pos.as<int64_t>(), flag.as<int32_t>(), n, nc, base, d_off.as<int64_t>() + s0);
+        GD_HIP(hipGetLastError());
+        std::vector<int64_t> co(nc + 1);
+        GD_HIP(hipMemcpyAsync(co.data(), d_off.as<int64_t>() + s0, (nc + 1) * sizeof(int64_t),
+                              hipMemcpyDeviceToHost, st));
+        GD_HIP(hipStreamSynchronize(st));
+        const int64_t uniq = co[nc] - base;
+        DevBuf cc(uniq * 8 + 8, st);
+        if (n > 0) {
+            compact_kernel<<<grid_for(n), 256, 0, st>>>(keys, flag.as<int32_t>(), pos.as<int64_t>(), n,
+                                                         cc.as<uint64_t>());
+            GD_HIP(hipGetLastError());
+        }
+        for (int i = 0; i <= nc; i++) h_off[s0 + i] = co[i];
+        chunk_codes.push_back(std::move(cc));
+        chunk_total.push_back(uniq);
+        base += uniq;
+        s0 = s1;
+    }
+    out->h_off = h_off;
+    out->total = base;
+    out->off = std::move(d_off);
+    if (nseq == 0) {
+        out->off.alloc(sizeof(int64_t), st);
+        GD_HIP(hipMemsetAsync(out->off.p, 0, sizeof(int64_t), st));
+        out->h_off.assign(1, 0);
+    }
+    if (chunk_codes.size() == 1) {
+        out->codes = std::move(chunk_codes[0]);
+    } else {
+        out->codes.alloc(base * 8 + 8, st);
+        int64_t at = 0;
+        for (size_t c = 0; c < chunk_codes.size(); c++) {
+            if (chunk_total[c])
+                GD_HIP(hipMemcpyAsync(out->codes.as<uint64_t>() + at, chunk_codes[c].p, chunk_total[c] * 8,
+                                      hipMemcpyDeviceToDevice, st));
+            at += chunk_total[c];
+        }
+    }
+    GD_HIP(hipStreamSynchronize(st));
+}
+
+}  // namespace gdist

@@ -1,0 +1,306 @@
+// sketch.hip — MinHash bottom-s sketches and the all-pairs sketch distance.
+//
+// sketch_build replaces SequenceKmers.hashSet(width) (SketchProcessor.java:88,
+// WidthProcessor.java:178): the `width` smallest distinct murmur3_x86_32
+// (seed 0) hashes, in Java signed-int order, of the set's kmer strings.
+// sketch_matrix replaces Sketch.distance over all pairs
+// (WidthProcessor.java:183-185, TuningProcessor.java:131-133). The
+// reference's hash function and sketch formula live in the un-vendored
+// org.theseed:sequence module: this contract is the restatement of
+// SURVEY App. B Q6 (parity unpinned), mirrored by oracle/.
+//
+// Build: hash every code of a chunk of sets, radix-sort 64-bit keys
+// (set id << 32 | biased hash), keep the first `width` distinct hashes of
+// each set. Matrix: a workgroup owns a 16×16 tile of sketch pairs; the 32
+// sketches are staged in LDS and each thread merges one pair.
+#include <cstring>
+#include <rocprim/rocprim.hpp>
+
+#include <algorithm>
+
+#include "gdist_internal.hpp"
+
+namespace gdist {
+namespace {
+
+inline int grid_for(int64_t n, int block = 256, int64_t cap = 256 * 32) {
+    int64_t g = ceil_div(n, block);
+    return (int)std::max<int64_t>(1, std::min<int64_t>(g, cap));
+}
+
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+
+// kmer string byte t of code (first char most significant), decoded per spec
+__device__ __forceinline__ uint32_t kmer_byte(uint64_t code, int t, int k, int bits, int dna_mode) {
+    const uint32_t s = (uint32_t)((code >> (bits * (k - 1 - t))) & ((1u << bits) - 1));
+    if (dna_mode == 2) return "ACGT"[s & 3];
+    if (dna_mode == 3) return "ACGNRTY"[s < 7 ? s : 3];
+    if (bits == 8) return s;
+    return s == 0 ? (uint32_t)'*' : (uint32_t)('A' + s - 1);
+}
+
+__device__ uint32_t murmur3_kmer(uint64_t code, int k, int bits, int dna_mode) {
+    const uint32_t c1 = 0xcc9e2d51u, c2 = 0x1b873593u;
+    uint32_t h = 0;
+    int t = 0;
+    for (; t + 4 <= k; t += 4) {
+        uint32_t kk = kmer_byte(code, t, k, bits, dna_mode) | (kmer_byte(code, t + 1, k, bits, dna_mode) << 8) |
+                      (kmer_byte(code, t + 2, k, bits, dna_mode) << 16) |
+                      (kmer_byte(code, t + 3, k, bits, dna_mode) << 24);
+        kk *= c1; kk = rotl32(kk, 15); kk *= c2;
+        h ^= kk; h = rotl32(h, 13); h = h * 5 + 0xe6546b64u;
+    }
+    uint32_t k1 = 0;
+    const int tail = k - t;
+    if (tail >= 3) k1 ^= kmer_byte(code, t + 2, k, bits, dna_mode) << 16;
+    if (tail >= 2) k1 ^= kmer_byte(code, t + 1, k, bits, dna_mode) << 8;
+    if (tail >= 1) {
+        k1 ^= kmer_byte(code, t, k, bits, dna_mode);
+        k1 *= c1; k1 = rotl32(k1, 15); k1 *= c2; h ^= k1;
+    }
+    h ^= (uint32_t)k;
+    h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
+    return h;
+}
+
+// key = (local set id << 32) | (hash ^ 0x80000000): unsigned order == (set, signed hash)
+__global__ void hash_keys_kernel(const uint64_t* __restrict__ codes, const int64_t* __restrict__ off,
+                                 int64_t s0, int64_t ns, int k, int bits, int dna_mode,
+                                 uint64_t* __restrict__ keys) {
+    const int64_t base = off[s0];
+    const int64_t n = off[s0 + ns] - base;
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
+        const int64_t g = base + e;
+        int64_t lo = s0, hi = s0 + ns;
+        while (hi - lo > 1) {
+            int64_t mid = (lo + hi) >> 1;
+            if (off[mid] <= g) lo = mid; else hi = mid;
+        }
+        const uint32_t h = murmur3_kmer(codes[g], k, bits, dna_mode);
+        keys[e] = ((uint64_t)(lo - s0) << 32) | (uint64_t)(h ^ 0x80000000u);
+    }
+}
+
+__global__ void head_flags_kernel(const uint64_t* __restrict__ keys, int64_t n, int32_t* __restrict__ flag) {
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        flag[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1 : 0;
+}
+
+// per local set: first index (lower_bound of set<<32) and distinct count
+__global__ void set_starts_kernel(const uint64_t* __restrict__ keys, const int64_t* __restrict__ pos,
+                                  const int32_t* __restrict__ flag, int64_t n, int64_t ns,
+                                  int64_t* __restrict__ ustart) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s > ns) return;
+    const uint64_t v = (uint64_t)s << 32;
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if (keys[mid] < v) lo = mid + 1; else hi = mid;
+    }
+    const int64_t total = n ? pos[n - 1] + flag[n - 1] : 0;
+    ustart[s] = lo < n ? pos[lo] : total;
+}
+
+__global__ void emit_sig_kernel(const uint64_t* __restrict__ keys, const int32_t* __restrict__ flag,
+                                const int64_t* __restrict__ pos, const int64_t* __restrict__ ustart,
+                                const int64_t* __restrict__ out_off, int64_t n, int width,
+                                int32_t* __restrict__ sig) {
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        if (!flag[i]) continue;
+        const int64_t s = (int64_t)(keys[i] >> 32);
+        const int64_t r = pos[i] - ustart[s];
+        if (r < width) sig[out_off[s] + r] = (int32_t)((uint32_t)keys[i] ^ 0x80000000u);
+    }
+}
+
+constexpr int ST = 16;                      // tile edge (sketches)
+constexpr int LDS_SK_BYTES = 128 * 1024;
+
+template <bool LDS>
+__global__ __launch_bounds__(256) void sketch_tile_kernel(const int32_t* __restrict__ sig,
+                                                          const int64_t* __restrict__ off, int width,
+                                                          int64_t r0, int64_t r1, int64_t c0, int64_t c1,
+                                                          int tiles_c, int upper, int jaccard, int empty_nan,
+                                                          int32_t* __restrict__ common_out,
+                                                          double* __restrict__ D, int64_t ld) {
+#pragma clang fp contract(off)
+    extern __shared__ int32_t sm[];   // [2*ST][width]
+    const int tr = blockIdx.x / tiles_c, tcb = blockIdx.x % tiles_c;
+    const int64_t row0 = r0 + (int64_t)tr * ST, col0 = c0 + (int64_t)tcb * ST;
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    if (upper && col0 + ST - 1 <= row0) return;
+    if (LDS) {
+        for (int s = 0; s < 2 * ST; s++) {
+            const int64_t g = s < ST ? row0 + s : col0 + (s - ST);
+            const bool ok = s < ST ? g < r1 : g < c1;
+            const int64_t b = ok ? off[g] : 0, n = ok ? off[g + 1] - off[g] : 0;
+            for (int t = threadIdx.x; t < n; t += 256) sm[s * width + t] = sig[b + t];
+        }
+        __syncthreads();
+    }
+    const int64_t i = row0 + ty, j = col0 + tx;
+    if (i >= r1 || j >= c1 || (upper && j <= i)) return;
+    const int64_t na = off[i + 1] - off[i], nb = off[j + 1] - off[j];
+    const int32_t* A = LDS ? sm + ty * width : sig + off[i];
+    const int32_t* B = LDS ? sm + (ST + tx) * width : sig + off[j];
+    int64_t ia = 0, ib = 0, taken = 0, common = 0;
+    int64_t va = na ? (int64_t)A[0] : INT64_MAX, vb = nb ? (int64_t)B[0] : INT64_MAX;
+    if (jaccard) {
+        while (ia < na && ib < nb) {
+            if (va < vb) { ia++; va = ia < na ? (int64_t)A[ia] : INT64_MAX; }
+            else if (vb < va) { ib++; vb = ib < nb ? (int64_t)B[ib] : INT64_MAX; }
+            else {
+                common++;
+                ia++; va = ia < na ? (int64_t)A[ia] : INT64_MAX;
+                ib++; vb = ib < nb ? (int64_t)B[ib] : INT64_MAX;
+            }
+        }
+    } else {
+        while (taken < width && (ia < na || ib < nb)) {
+            if (va < vb) { ia++; va = ia < na ? (int64_t)A[ia] : INT64_MAX; }
+            else if (vb < va) { ib++; vb = ib < nb ? (int64_t)B[ib] : INT64_MAX; }
+            else {
+                common++;
+                ia++; va = ia < na ? (int64_t)A[ia] : INT64_MAX;
+                ib++; vb = ib < nb ? (int64_t)B[ib] : INT64_MAX;
+            }
+            taken++;
+        }
+    }
+    double d;
+    if (jaccard) {
+        if (common > 0) d = 1.0 - (double)common / (double)(na + nb - common);
+        else d = (empty_nan && na + nb == 0) ? __builtin_nan("") : 1.0;
+    } else {
+        if (common > 0) d = 1.0 - (double)common / (double)taken;
+        else d = (empty_nan && taken == 0) ? __builtin_nan("") : 1.0;
+    }
+    const int64_t o = (i - r0) * ld + (j - c0);
+    if (common_out) common_out[o] = (int32_t)common;
+    if (D) D[o] = d;
+}
+
+}  // namespace
+
+void sketch_build(gdist_ctx* ctx, const gdist_sets* s, int width, gdist_sets* out) {
+    hipStream_t st = ctx->stream;
+    GD_REQUIRE(width > 0, "sketch width must be positive");
+    GD_REQUIRE(s->kind == GDIST_DNA || s->kind == GDIST_PROT, "sketches are built from kmer sets");
+    const int k = s->k;
+    const unsigned am = s->flags & GDIST_AMBIG_MASK;
+    int bits, dna_mode = 0;
+    if (s->kind == GDIST_DNA) {
+        const bool keep = am == GDIST_AMBIG_KEEP;
+        bits = keep ? 3 : 2;
+        dna_mode = keep ? 3 : 2;
+    } else {
+        bits = k <= 8 ? 8 : 5;
+    }
+    const int64_t nsets = s->nsets;
+    std::vector<int64_t> h_out(nsets + 1, 0);
+    std::vector<DevBuf> parts;
+    std::vector<int64_t> part_n;
+    DevBuf d_out_off((nsets + 1) * 8, st);
+    const int64_t kChunk = int64_t(1) << 29;
+    int64_t s0 = 0;
+    while (s0 < nsets) {
+        int64_t s1 = s0 + 1;
+        while (s1 < nsets && s->h_off[s1 + 1] - s->h_off[s0] <= kChunk) s1++;
+        const int64_t ns = s1 - s0;
+        const int64_t n = s->h_off[s1] - s->h_off[s0];
+        DevBuf kA(n * 8 + 8, st), kB(n * 8 + 8, st), flag(n * 4 + 4, st), pos(n * 8 + 8, st), us((ns + 1) * 8, st);
+        if (n) {
+            hash_keys_kernel<<<grid_for(n), 256, 0, st>>>(s->codes.as<uint64_t>(), s->off.as<int64_t>(), s0, ns, k,
+                                                         bits, dna_mode, kA.as<uint64_t>());
+            GD_HIP(hipGetLastError());
+        }
+        uint64_t* keys = kA.as<uint64_t>(); uint64_t* alt = kB.as<uint64_t>();
+        int idbits = 1;
+        while ((int64_t(1) << idbits) <= ns) idbits++;
+        sort_keys_u64(ctx, keys, alt, (size_t)n, 0, 32 + idbits);
+        if (n) {
+            head_flags_kernel<<<grid_for(n), 256, 0, st>>>(keys, n, flag.as<int32_t>());
+            GD_HIP(hipGetLastError());
+            exclusive_scan_i32_to_i64(ctx, flag.as<int32_t>(), pos.as<int64_t>(), (size_t)n);
+        }
+        set_starts_kernel<<<(int)ceil_div(ns + 1, 256), 256, 0, st>>>(keys, pos.as<int64_t>(), flag.as<int32_t>(), n,
+                                                                       ns, us.as<int64_t>());
+        GD_HIP(hipGetLastError());
+        std::vector<int64_t> hus(ns + 1);
+        GD_HIP(hipMemcpyAsync(hus.data(), us.p, (ns + 1) * 8, hipMemcpyDeviceToHost, st));
+        GD_HIP(hipStreamSynchronize(st));
+        std::vector<int64_t> loc(ns + 1, 0);
+        for (int64_t t = 0; t < ns; t++) {
+            const int64_t cnt = std::min<int64_t>(width, hus[t + 1] - hus[t]);
+            loc[t + 1] = loc[t] + cnt;
+            h_out[s0 + t + 1] = h_out[s0 + t] + cnt;
+        }
+        DevBuf dloc((ns + 1) * 8, st), sig(loc[ns] * 4 + 4, st);
+        h2d_sync(dloc.p, loc.data(), (ns + 1) * 8, st);
+        if (n) {
+            emit_sig_kernel<<<grid_for(n), 256, 0, st>>>(keys, flag.as<int32_t>(), pos.as<int64_t>(), us.as<int64_t>(),
+                                                         dloc.as<int64_t>(), n, width, sig.as<int32_t>());
+            GD_HIP(hipGetLastError());
+        }
+        parts.push_back(std::move(sig));
+        part_n.push_back(loc[ns]);
+        s0 = s1;
+    }
+    out->kind = GDIST_SKETCH;
+    out->k = s->k;
+    out->flags = s->flags;
+    out->width = width;
+    out->nsets = nsets;
+    out->total = h_out[nsets];
+    out->h_off = h_out;
+    h2d_sync(d_out_off.p, h_out.data(), (nsets + 1) * 8, st);
+    out->off = std::move(d_out_off);
+    out->codes.alloc(out->total * 4 + 4, st);
+    int64_t at = 0;
+    for (size_t p = 0; p < parts.size(); p++) {
+        if (part_n[p])
+            GD_HIP(hipMemcpyAsync(out->codes.as<int32_t>() + at, parts[p].p, part_n[p] * 4, hipMemcpyDeviceToDevice,
+                                  st));
+        at += part_n[p];
+    }
+    GD_HIP(hipStreamSynchronize(st));
+}
+
+void sketch_matrix(gdist_ctx* ctx, const gdist_sets* sk, int64_t r0, int64_t r1, int64_t c0, int64_t c1,
+                   unsigned flags, int32_t* d_common, double* d_D, int64_t ld) {
+    hipStream_t st = ctx->stream;
+    const int64_t nr = r1 - r0, nc = c1 - c0;
+    if (nr <= 0 || nc <= 0) return;
+    const int tr = (int)ceil_div(nr, ST), tc = (int)ceil_div(nc, ST);
+    const int64_t grid = (int64_t)tr * tc;
+    GD_REQUIRE(grid < (int64_t(1) << 31), "sketch grid too large");
+    const bool upper = (flags & GDIST_UPPER_TRIANGLE) != 0;
+    const int jac = (flags & GDIST_SKETCH_JACCARD) ? 1 : 0, en = (flags & GDIST_EMPTY_NAN) ? 1 : 0;
+    int width = std::max(1, sk->width);
+    const size_t lds = (size_t)2 * ST * width * 4;
+    static bool attr_set = false;
+    if (!attr_set) {
+        GD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&sketch_tile_kernel<true>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, LDS_SK_BYTES));
+        attr_set = true;
+    }
+    GD_HIP(hipEventRecord(ctx->ev_k0, st));
+    if (lds <= (size_t)LDS_SK_BYTES) {
+        sketch_tile_kernel<true><<<(unsigned)grid, 256, lds, st>>>(sk->codes.as<int32_t>(), sk->off.as<int64_t>(),
+                                                                    width, r0, r1, c0, c1, tc, upper, jac, en,
+                                                                    d_common, d_D, ld);
+    } else {
+        sketch_tile_kernel<false><<<(unsigned)grid, 256, 0, st>>>(sk->codes.as<int32_t>(), sk->off.as<int64_t>(),
+                                                                   width, r0, r1, c0, c1, tc, upper, jac, en,
+                                                                   d_common, d_D, ld);
+    }
+    GD_HIP(hipGetLastError());
+    GD_HIP(hipEventRecord(ctx->ev_k1, st));
+    ctx->last.launches = 1;
+}
+
+}  // namespace gdist

@@ -1,0 +1,116 @@
+"""ctypes binding of libgdist.so (the C-ABI declared in include/gdist.h).
+
+The product path: every call goes to the HIP library. If libgdist.so is
+missing this module raises at import time — there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgdist.so")
+
+OK, EINVAL, ENOMEM, EDEVICE, ECOMM = 0, -1, -2, -3, -4
+DNA, PROT, SKETCH = 0, 1, 2
+STRAND_BOTH, STRAND_FWD, STRAND_CANON = 0x0, 0x1, 0x2
+AMBIG_DEFAULT, AMBIG_SKIP, AMBIG_KEEP = 0x0, 0x4, 0x8
+NO_CASE_FOLD = 0x10
+UPPER_TRIANGLE, OUT_DEVICE, EMPTY_NAN, SKETCH_JACCARD = 0x100, 0x200, 0x400, 0x800
+METHOD_AUTO, METHOD_SORTED, METHOD_BITSET = 0, 1, 2
+BITSET_KEEP_SINGLETONS = 0x1
+QUERY_ALL, QUERY_ANY_LE, QUERY_ARGMIN = 0, 1, 2
+UNIQUE_ID_BYTES = 128
+
+
+class GdistError(RuntimeError):
+    """Device / communicator failure (IllegalStateException in the JNI shim)."""
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"libgdist.so not found at {LIB_PATH}: build it with "
+            "`make -C genome.distance_amd` (or __graft_entry__.build()); "
+            "there is no CPU fallback")
+    return C.CDLL(LIB_PATH)
+
+
+lib = _load()
+
+_i64, _i32, _u32, _dbl = C.c_int64, C.c_int32, C.c_uint, C.c_double
+_vp, _i64p, _i32p, _u64p, _dblp = (C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int32),
+                                   C.POINTER(C.c_uint64), C.POINTER(C.c_double))
+_ctxp, _setp = C.c_void_p, C.c_void_p
+
+_SIGS = {
+    "gdist_version": (C.c_char_p, []),
+    "gdist_abi_version": (C.c_int, []),
+    "gdist_last_error": (C.c_char_p, []),
+    "gdist_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "gdist_ctx_create": (C.c_int, [C.c_int, C.POINTER(_ctxp)]),
+    "gdist_ctx_destroy": (C.c_int, [_ctxp]),
+    "gdist_ctx_synchronize": (C.c_int, [_ctxp]),
+    "gdist_ctx_last_timing": (C.c_int, [_ctxp, _dblp, _dblp, _i64p]),
+    "gdist_dev_alloc": (C.c_int, [_ctxp, _i64, C.POINTER(_vp)]),
+    "gdist_dev_free": (C.c_int, [_ctxp, _vp]),
+    "gdist_memcpy_d2h": (C.c_int, [_ctxp, _vp, _vp, _i64]),
+    "gdist_memcpy_h2d": (C.c_int, [_ctxp, _vp, _vp, _i64]),
+    "gdist_sets_pack": (C.c_int, [_ctxp, C.c_int, C.c_int, _u32, C.c_char_p, _i64p, _i64, C.POINTER(_setp)]),
+    "gdist_sets_pack_device": (C.c_int, [_ctxp, C.c_int, C.c_int, _u32, _vp, _vp, _i64, _i64,
+                                         C.POINTER(_setp)]),
+    "gdist_sets_upload": (C.c_int, [_ctxp, C.c_int, C.c_int, _i64, _i64p, _u64p, C.POINTER(_setp)]),
+    "gdist_sets_free": (C.c_int, [_setp]),
+    "gdist_sets_info": (C.c_int, [_setp, C.POINTER(C.c_int), C.POINTER(C.c_int), _i64p, _i64p]),
+    "gdist_sets_sizes": (C.c_int, [_setp, _i64p]),
+    "gdist_sets_download": (C.c_int, [_setp, _i64p, _u64p]),
+    "gdist_sets_build_bitsets": (C.c_int, [_setp, _u32]),
+    "gdist_sets_bitset_info": (C.c_int, [_setp, _i64p, _i64p]),
+    "gdist_sets_concat": (C.c_int, [_setp, _setp, C.POINTER(_setp)]),
+    "gdist_intersect_matrix": (C.c_int, [_ctxp, _setp, _i64, _i64, _i64, _i64, C.c_int, _u32, _vp, _vp, _i64]),
+    "gdist_row_query": (C.c_int, [_ctxp, _setp, _i64, _i64p, _i64, C.c_int, _dbl, _dblp, _i32p, _i64p, _dblp]),
+    "gdist_sketch_build": (C.c_int, [_ctxp, _setp, C.c_int, C.POINTER(_setp)]),
+    "gdist_sketch_upload": (C.c_int, [_ctxp, C.c_int, _i64, _i64p, _i32p, C.POINTER(_setp)]),
+    "gdist_sketch_download": (C.c_int, [_setp, _i64p, _i32p]),
+    "gdist_sketch_matrix": (C.c_int, [_ctxp, _setp, _i64, _i64, _i64, _i64, _u32, _vp, _vp, _i64]),
+    "gdist_comm_unique_id": (C.c_int, [C.c_char_p]),
+    "gdist_comm_init": (C.c_int, [_ctxp, C.c_char_p, C.c_int, C.c_int]),
+    "gdist_comm_destroy": (C.c_int, [_ctxp]),
+    "gdist_sets_allgather": (C.c_int, [_ctxp, _setp, C.POINTER(_setp)]),
+    "gdist_sets_allgather_bitsets": (C.c_int, [_ctxp, _setp, _u32, C.POINTER(_setp)]),
+    "gdist_comm_allreduce_max": (C.c_int, [_ctxp, _dblp]),
+    "gdist_triangle_partition": (C.c_int, [_i64, C.c_int, _i64, _i64p]),
+}
+
+for _name, (_res, _args) in _SIGS.items():
+    _f = getattr(lib, _name)
+    _f.restype = _res
+    _f.argtypes = _args
+
+EXPORTED = tuple(_SIGS)
+
+
+def check(rc: int) -> None:
+    """Map a status code to the exception the reference throws for it."""
+    if rc == OK:
+        return
+    msg = lib.gdist_last_error().decode(errors="replace")
+    if rc == EINVAL:
+        raise ValueError(msg)          # IllegalArgumentException / ParseFailureException
+    if rc == ENOMEM:
+        raise MemoryError(msg)         # OutOfMemoryError
+    raise GdistError(f"[{rc}] {msg}")  # IllegalStateException
+
+
+def ptr(a: np.ndarray, t):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+def vptr(a) -> int | None:
+    if a is None:
+        return None
+    if isinstance(a, int):
+        return a
+    return a.ctypes.data

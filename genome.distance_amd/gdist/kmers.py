@@ -1,0 +1,365 @@
+"""Host-side mirror of the reference's kmer-set API over libgdist.so.
+
+Reference surface (org.theseed:sequence, un-vendored; call sites in-repo):
+  KmerType.DNA / KmerType.PROT, getKmerSize(), createKmers(seq, K)
+      FastaDistanceProcessor.java:81-96,153,184
+  SequenceKmers.distance(other), size(), hashSet(width)
+      FastaDistanceProcessor.java:186, SketchProcessor.java:88, WidthProcessor.java:178
+  Sketch(int[] signature, name).distance(other), getSignature()
+      WidthProcessor.java:178-185
+The GPU-native form of these is a *collection*: `KmerSets` holds many kmer
+sets packed on the device and answers whole matrices / row queries in one
+call; `SequenceKmers` is a per-set view whose `distance()` is kept for API
+parity (one pair per call is a correctness path, not a fast path).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import enum
+from typing import Iterable, Sequence
+
+import numpy as np
+
+from . import _lib as L
+
+
+class Context:
+    """One HIP device + stream (gdist_ctx)."""
+
+    _defaults: dict[int, "Context"] = {}
+
+    def __init__(self, device: int = 0):
+        h = C.c_void_p()
+        L.check(L.lib.gdist_ctx_create(device, C.byref(h)))
+        self.h = h
+        self.device = device
+
+    @classmethod
+    def default(cls, device: int = 0) -> "Context":
+        if device not in cls._defaults:
+            cls._defaults[device] = cls(device)
+        return cls._defaults[device]
+
+    def close(self):
+        if self.h:
+            L.lib.gdist_ctx_destroy(self.h)
+            self.h = None
+
+    def synchronize(self):
+        L.check(L.lib.gdist_ctx_synchronize(self.h))
+
+    def last_timing(self) -> tuple[float, float, int]:
+        k, c, n = C.c_double(), C.c_double(), C.c_int64()
+        L.check(L.lib.gdist_ctx_last_timing(self.h, C.byref(k), C.byref(c), C.byref(n)))
+        return k.value, c.value, n.value
+
+    def alloc(self, nbytes: int) -> "DeviceBuffer":
+        return DeviceBuffer(self, nbytes)
+
+    # ---- RCCL communicator (row-sharded multi-GPU)
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = C.create_string_buffer(L.UNIQUE_ID_BYTES)
+        L.check(L.lib.gdist_comm_unique_id(buf))
+        return buf.raw
+
+    def comm_init(self, uid: bytes, nranks: int, rank: int) -> None:
+        L.check(L.lib.gdist_comm_init(self.h, uid, nranks, rank))
+
+    def comm_destroy(self) -> None:
+        L.check(L.lib.gdist_comm_destroy(self.h))
+
+    def allreduce_max(self, v: float) -> float:
+        x = C.c_double(v)
+        L.check(L.lib.gdist_comm_allreduce_max(self.h, C.byref(x)))
+        return x.value
+
+
+class DeviceBuffer:
+    def __init__(self, ctx: Context, nbytes: int):
+        p = C.c_void_p()
+        L.check(L.lib.gdist_dev_alloc(ctx.h, int(nbytes), C.byref(p)))
+        self.ctx, self.ptr, self.nbytes = ctx, p.value or 0, int(nbytes)
+
+    def to_host(self, dtype, count: int | None = None) -> np.ndarray:
+        dt = np.dtype(dtype)
+        n = self.nbytes // dt.itemsize if count is None else count
+        out = np.empty(n, dtype=dt)
+        L.check(L.lib.gdist_memcpy_d2h(self.ctx.h, out.ctypes.data, self.ptr, n * dt.itemsize))
+        return out
+
+    def from_host(self, a: np.ndarray):
+        a = np.ascontiguousarray(a)
+        assert a.nbytes <= self.nbytes
+        L.check(L.lib.gdist_memcpy_h2d(self.ctx.h, self.ptr, a.ctypes.data, a.nbytes))
+
+    def free(self):
+        if self.ptr:
+            L.check(L.lib.gdist_dev_free(self.ctx.h, self.ptr))
+            self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class KmerType(enum.Enum):
+    """KmerType.DNA / KmerType.PROT (FastaDistanceProcessor.java:81-96)."""
+    DNA = (L.DNA, 21)
+    PROT = (L.PROT, 8)
+
+    @property
+    def kind(self) -> int:
+        return self.value[0]
+
+    def getKmerSize(self) -> int:
+        return self.value[1]
+
+    def createKmers(self, seq: str | bytes, k: int, flags: int = 0, ctx: Context | None = None) -> "SequenceKmers":
+        return KmerSets.from_sequences([seq], k, self, flags, ctx)[0]
+
+    @classmethod
+    def parse(cls, name: str) -> "KmerType":
+        return cls[name.upper()]
+
+
+def _as_bytes(s) -> bytes:
+    return s if isinstance(s, (bytes, bytearray)) else str(s).encode("latin-1")
+
+
+class _Handle:
+    def __init__(self, ctx: Context, h: C.c_void_p):
+        self.ctx, self.h = ctx, h
+
+    def free(self):
+        if getattr(self, "h", None):
+            L.lib.gdist_sets_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+    def info(self):
+        kind, k, n, t = C.c_int(), C.c_int(), C.c_int64(), C.c_int64()
+        L.check(L.lib.gdist_sets_info(self.h, C.byref(kind), C.byref(k), C.byref(n), C.byref(t)))
+        return kind.value, k.value, n.value, t.value
+
+    def __len__(self) -> int:
+        return self.info()[2]
+
+    def allgather(self):
+        """Concatenation of every rank's local collection, in rank order
+        (one RCCL all-gather of offsets, one of codes / signatures)."""
+        h = C.c_void_p()
+        L.check(L.lib.gdist_sets_allgather(self.ctx.h, self.h, C.byref(h)))
+        return type(self)(self.ctx, h)
+
+
+class KmerSets(_Handle):
+    """A collection of kmer sets (sorted unique uint64 codes) resident in HBM."""
+
+    @classmethod
+    def from_sequences(cls, seqs: Sequence, k: int, kmer_type: KmerType = KmerType.DNA, flags: int = 0,
+                       ctx: Context | None = None) -> "KmerSets":
+        ctx = ctx or Context.default()
+        bs = [_as_bytes(s) for s in seqs]
+        off = np.zeros(len(bs) + 1, dtype=np.int64)
+        if bs:
+            off[1:] = np.cumsum([len(b) for b in bs])
+        blob = b"".join(bs) or b"\0"
+        h = C.c_void_p()
+        L.check(L.lib.gdist_sets_pack(ctx.h, kmer_type.kind, int(k), flags, blob, L.ptr(off, C.c_int64),
+                                      len(bs), C.byref(h)))
+        return cls(ctx, h)
+
+    @classmethod
+    def from_device(cls, ctx: Context, d_seqs: int, d_off: int, nseqs: int, total_bytes: int, k: int,
+                    kmer_type: KmerType = KmerType.DNA, flags: int = 0) -> "KmerSets":
+        h = C.c_void_p()
+        L.check(L.lib.gdist_sets_pack_device(ctx.h, kmer_type.kind, int(k), flags, d_seqs, d_off, nseqs,
+                                             total_bytes, C.byref(h)))
+        return cls(ctx, h)
+
+    @classmethod
+    def from_codes(cls, offsets: np.ndarray, codes: np.ndarray, k: int, kmer_type: KmerType = KmerType.DNA,
+                   ctx: Context | None = None) -> "KmerSets":
+        ctx = ctx or Context.default()
+        off = np.ascontiguousarray(offsets, dtype=np.int64)
+        cd = np.ascontiguousarray(codes, dtype=np.uint64)
+        if cd.size == 0:
+            cd = np.zeros(1, dtype=np.uint64)
+        h = C.c_void_p()
+        L.check(L.lib.gdist_sets_upload(ctx.h, kmer_type.kind, int(k), len(off) - 1, L.ptr(off, C.c_int64),
+                                        L.ptr(cd, C.c_uint64), C.byref(h)))
+        return cls(ctx, h)
+
+    def sizes(self) -> np.ndarray:
+        n = len(self)
+        out = np.zeros(n, dtype=np.int64)
+        L.check(L.lib.gdist_sets_sizes(self.h, L.ptr(out, C.c_int64)))
+        return out
+
+    def download(self) -> tuple[np.ndarray, np.ndarray]:
+        _, _, n, t = self.info()
+        off = np.zeros(n + 1, dtype=np.int64)
+        codes = np.zeros(max(t, 1), dtype=np.uint64)
+        L.check(L.lib.gdist_sets_download(self.h, L.ptr(off, C.c_int64), L.ptr(codes, C.c_uint64)))
+        return off, codes[:t]
+
+    def build_bitsets(self, keep_singletons: bool = False) -> tuple[int, int]:
+        L.check(L.lib.gdist_sets_build_bitsets(self.h, L.BITSET_KEEP_SINGLETONS if keep_singletons else 0))
+        return self.bitset_info()
+
+    def bitset_info(self) -> tuple[int, int]:
+        d, w = C.c_int64(), C.c_int64()
+        L.check(L.lib.gdist_sets_bitset_info(self.h, C.byref(d), C.byref(w)))
+        return d.value, w.value
+
+    def allgather_bitsets(self, keep_singletons: bool = False) -> "KmerSets":
+        """Bitsets of every rank's sets over one global dictionary (bitset-only collection)."""
+        h = C.c_void_p()
+        L.check(L.lib.gdist_sets_allgather_bitsets(self.ctx.h, self.h,
+                                                   L.BITSET_KEEP_SINGLETONS if keep_singletons else 0,
+                                                   C.byref(h)))
+        return KmerSets(self.ctx, h)
+
+    def concat(self, other: "KmerSets") -> "KmerSets":
+        h = C.c_void_p()
+        L.check(L.lib.gdist_sets_concat(self.h, other.h, C.byref(h)))
+        return KmerSets(self.ctx, h)
+
+    def matrix(self, rows: tuple[int, int] | None = None, cols: tuple[int, int] | None = None,
+               upper: bool = False, method: int = L.METHOD_AUTO, flags: int = 0,
+               want_I: bool = True, want_D: bool = True):
+        """|A_i ∩ A_j| and distances for rows × cols (host numpy outputs)."""
+        n = len(self)
+        r0, r1 = rows or (0, n)
+        c0, c1 = cols or (0, n)
+        nr, nc = r1 - r0, c1 - c0
+        I = np.full((nr, nc), -1, dtype=np.int32) if want_I else None
+        D = np.full((nr, nc), np.nan, dtype=np.float64) if want_D else None
+        fl = flags | (L.UPPER_TRIANGLE if upper else 0)
+        L.check(L.lib.gdist_intersect_matrix(self.ctx.h, self.h, r0, r1, c0, c1, method, fl, L.vptr(I),
+                                             L.vptr(D), max(nc, 1)))
+        return I, D
+
+    def matrix_device(self, d_I: int | None, d_D: int | None, ld: int, rows: tuple[int, int],
+                      cols: tuple[int, int], upper: bool = False, method: int = L.METHOD_AUTO,
+                      flags: int = 0) -> None:
+        fl = flags | L.OUT_DEVICE | (L.UPPER_TRIANGLE if upper else 0)
+        L.check(L.lib.gdist_intersect_matrix(self.ctx.h, self.h, rows[0], rows[1], cols[0], cols[1], method,
+                                             fl, d_I, d_D, ld))
+
+    def row_query(self, q: int, cols: Iterable[int], mode: int = L.QUERY_ALL, t: float = 1.0):
+        cl = np.ascontiguousarray(np.fromiter(cols, dtype=np.int64))
+        D = np.zeros(max(len(cl), 1), dtype=np.float64)
+        hit, bi, bd = C.c_int32(0), C.c_int64(-1), C.c_double(1.0)
+        L.check(L.lib.gdist_row_query(self.ctx.h, self.h, q, L.ptr(cl, C.c_int64) if len(cl) else None,
+                                      len(cl), mode, t, L.ptr(D, C.c_double), C.byref(hit), C.byref(bi),
+                                      C.byref(bd)))
+        if mode == L.QUERY_ANY_LE:
+            return bool(hit.value)
+        if mode == L.QUERY_ARGMIN:
+            return int(bi.value), float(bd.value)
+        return D[:len(cl)]
+
+    def sketches(self, width: int) -> "SketchSets":
+        h = C.c_void_p()
+        L.check(L.lib.gdist_sketch_build(self.ctx.h, self.h, int(width), C.byref(h)))
+        return SketchSets(self.ctx, h)
+
+    def __getitem__(self, i: int) -> "SequenceKmers":
+        n = len(self)
+        if i < 0:
+            i += n
+        if not 0 <= i < n:
+            raise IndexError(i)
+        return SequenceKmers(self, i)
+
+
+class SequenceKmers:
+    """SequenceKmers view of one set of a KmerSets collection."""
+
+    def __init__(self, sets: KmerSets, index: int):
+        self.sets, self.index = sets, index
+
+    def size(self) -> int:
+        return int(self.sets.sizes()[self.index])
+
+    def distance(self, other: "SequenceKmers") -> float:
+        """SequenceKmers.distance(other) — FastaDistanceProcessor.java:186."""
+        if other.sets is self.sets:
+            return float(self.sets.row_query(self.index, [other.index])[0])
+        both = self.sets.concat(other.sets)
+        return float(both.row_query(self.index, [len(self.sets) + other.index])[0])
+
+    def similarity(self, other: "SequenceKmers") -> int:
+        if other.sets is self.sets:
+            I, _ = self.sets.matrix((self.index, self.index + 1), (other.index, other.index + 1), want_D=False)
+            return int(I[0, 0])
+        both = self.sets.concat(other.sets)
+        j = len(self.sets) + other.index
+        I, _ = both.matrix((self.index, self.index + 1), (j, j + 1), want_D=False)
+        return int(I[0, 0])
+
+    def hashSet(self, width: int) -> np.ndarray:
+        """SequenceKmers.hashSet(width) — SketchProcessor.java:88."""
+        return self.sets.sketches(width).signature(self.index)
+
+
+class SketchSets(_Handle):
+    """Bottom-s MinHash signatures (int32) resident in HBM."""
+
+    @classmethod
+    def from_signatures(cls, sigs: Sequence[np.ndarray], width: int, ctx: Context | None = None) -> "SketchSets":
+        ctx = ctx or Context.default()
+        off = np.zeros(len(sigs) + 1, dtype=np.int64)
+        if sigs:
+            off[1:] = np.cumsum([len(s) for s in sigs])
+        flat = np.concatenate([np.asarray(s, dtype=np.int32) for s in sigs]) if sigs else np.zeros(0, np.int32)
+        if flat.size == 0:
+            flat = np.zeros(1, dtype=np.int32)
+        h = C.c_void_p()
+        L.check(L.lib.gdist_sketch_upload(ctx.h, int(width), len(sigs), L.ptr(off, C.c_int64),
+                                          L.ptr(np.ascontiguousarray(flat), C.c_int32), C.byref(h)))
+        return cls(ctx, h)
+
+    def download(self) -> tuple[np.ndarray, np.ndarray]:
+        _, _, n, t = self.info()
+        off = np.zeros(n + 1, dtype=np.int64)
+        sig = np.zeros(max(t, 1), dtype=np.int32)
+        L.check(L.lib.gdist_sketch_download(self.h, L.ptr(off, C.c_int64), L.ptr(sig, C.c_int32)))
+        return off, sig[:t]
+
+    def signature(self, i: int) -> np.ndarray:
+        off, sig = self.download()
+        return sig[off[i]:off[i + 1]].copy()
+
+    def matrix(self, rows=None, cols=None, upper: bool = False, flags: int = 0):
+        n = len(self)
+        r0, r1 = rows or (0, n)
+        c0, c1 = cols or (0, n)
+        nr, nc = r1 - r0, c1 - c0
+        common = np.full((nr, nc), -1, dtype=np.int32)
+        D = np.full((nr, nc), np.nan, dtype=np.float64)
+        fl = flags | (L.UPPER_TRIANGLE if upper else 0)
+        L.check(L.lib.gdist_sketch_matrix(self.ctx.h, self.h, r0, r1, c0, c1, fl, common.ctypes.data,
+                                          D.ctypes.data, max(nc, 1)))
+        return common, D
+
+    def matrix_device(self, d_common: int | None, d_D: int | None, ld: int, rows, cols, upper=False, flags=0):
+        fl = flags | L.OUT_DEVICE | (L.UPPER_TRIANGLE if upper else 0)
+        L.check(L.lib.gdist_sketch_matrix(self.ctx.h, self.h, rows[0], rows[1], cols[0], cols[1], fl, d_common,
+                                          d_D, ld))
+
+
+def triangle_partition(n: int, nparts: int, align: int = 1) -> list[int]:
+    """Row bounds with equal upper-triangle area per part."""
+    b = np.zeros(nparts + 1, dtype=np.int64)
+    L.check(L.lib.gdist_triangle_partition(n, nparts, align, L.ptr(b, C.c_int64)))
+    return [int(x) for x in b]

@@ -1,0 +1,200 @@
+/*
+ * gdist.h — C-ABI of the MI355X-native pairwise kmer-distance hot path of
+ * SEEDtk genome.distance (libgdist.so).
+ *
+ * Plain C types only: pointers, sizes and status codes. No torch, no C++.
+ * Every entry point returns GDIST_OK (0) or a negative GDIST_E* code; the
+ * message of the last failure on the calling thread is gdist_last_error().
+ *
+ * What each entry point replaces in the reference (paths relative to the
+ * reference root /root/reference; the kmer classes live in the un-vendored
+ * org.theseed:sequence:1.0.0 module, pom.xml:46-49, so their behaviour is
+ * taken from the in-repo call sites):
+ *
+ *   gdist_sets_pack        KmerType.createKmers(seq, K)          FastaDistanceProcessor.java:153,184
+ *                          new GenomeKmers(genome)               GenomeProcessor.java:305,335
+ *                          new ProteinKmers(seq)                 ProteinKmerReader.java:101
+ *   gdist_sets_sizes       SequenceKmers.size()                  (used by distance())
+ *   gdist_intersect_matrix SequenceKmers.distance(other) over the
+ *                          N×N upper triangle                    FastaDistanceProcessor.java:177-186
+ *                          M×N rectangle                         GenomeProcessor.java:336
+ *                          group all-pairs                       WidthProcessor.java:159-165
+ *   gdist_row_query        anyMatch(d <= maxDist)                DistanceRepsProcessor.java:400
+ *                          reduce(NULL_RESULT, merge) argmin     DistanceRepsProcessor.java:448-449
+ *                          sequential early exit                 FastaDistanceRepsProcessor.java:117-128
+ *   gdist_sketch_build     SequenceKmers.hashSet(width)          SketchProcessor.java:88, WidthProcessor.java:178
+ *   gdist_sketch_matrix    Sketch.distance(other) all-pairs      WidthProcessor.java:183-185, TuningProcessor.java:131-133
+ *   gdist_sets_allgather   (new) RCCL all-gather of packed sets for row-sharded N×N
+ *
+ * Kmer code spec (shared by the device packer, the CPU oracle in oracle/ and
+ * the Python restatement; see DESIGN.md "Packing spec"). A kmer is k
+ * consecutive characters of the sequence after case folding; its code is an
+ * order-preserving (code order == Java String order) injective uint64:
+ *   DNA, AMBIG_SKIP (default): 2-bit A0 C1 G2 T3, first char most significant,
+ *        k <= 32; kmers holding any other char are skipped.
+ *   DNA, AMBIG_KEEP: 3-bit A0 C1 G2 N3 R4 T5 Y6, k <= 21; any other char -> EINVAL.
+ *   PROT, k <= 8: the k ASCII bytes big-endian (any byte value).
+ *   PROT, 8 < k <= 12: 5-bit '*'0 'A'..'Z' 1..26; any other char -> EINVAL.
+ *   PROT, AMBIG_SKIP: kmers holding a char outside ACDEFGHIKLMNPQRSTVWY skipped.
+ * Byte 0x00 is a sequence separator in every mode: no kmer spans it (used to
+ * pack the contigs of one genome, or the proteins of one group, as one set).
+ * DNA strand modes: FWD (forward only), BOTH (forward kmers ∪ reverse-
+ * complement kmers, the default), CANON (per-position min(fwd, rc)).
+ * Distance: d = (I > 0) ? 1.0 - (double)I / (double)(|A|+|B|-I) : 1.0
+ * (GDIST_EMPTY_NAN turns the I == 0 && |A|+|B| == 0 case into NaN), fp64,
+ * no contraction: bit-identical to the Java expression.
+ */
+#ifndef GDIST_H
+#define GDIST_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GDIST_ABI_VERSION 1
+
+/* status codes */
+#define GDIST_OK        0
+#define GDIST_EINVAL   -1   /* bad argument / unencodable input        -> IllegalArgumentException */
+#define GDIST_ENOMEM   -2   /* host or device allocation failed         -> OutOfMemoryError */
+#define GDIST_EDEVICE  -3   /* HIP runtime / kernel failure             -> IllegalStateException */
+#define GDIST_ECOMM    -4   /* RCCL failure                             -> IllegalStateException */
+
+/* set kinds (KmerType) */
+#define GDIST_DNA     0
+#define GDIST_PROT    1
+#define GDIST_SKETCH  2
+
+/* pack flags */
+#define GDIST_STRAND_BOTH   0x0u   /* default for DNA */
+#define GDIST_STRAND_FWD    0x1u
+#define GDIST_STRAND_CANON  0x2u
+#define GDIST_STRAND_MASK   0x3u
+#define GDIST_AMBIG_DEFAULT 0x0u   /* DNA: skip, PROT: keep */
+#define GDIST_AMBIG_SKIP    0x4u
+#define GDIST_AMBIG_KEEP    0x8u
+#define GDIST_AMBIG_MASK    0xCu
+#define GDIST_NO_CASE_FOLD  0x10u  /* PROT only; DNA always folds to upper case */
+
+/* distance / matrix flags */
+#define GDIST_UPPER_TRIANGLE 0x100u /* only pairs with global col > global row */
+#define GDIST_OUT_DEVICE     0x200u /* I_out / D_out are device pointers (gdist_dev_alloc) */
+#define GDIST_EMPTY_NAN      0x400u /* |A|+|B| == 0 -> NaN instead of 1.0 */
+#define GDIST_SKETCH_JACCARD 0x800u /* sketch distance: plain Jaccard of the two signatures
+                                       (default: Mash bottom-s of the union) */
+
+/* intersection methods */
+#define GDIST_METHOD_AUTO    0
+#define GDIST_METHOD_SORTED  1   /* sorted uint64 sets: LDS hash-join tiles */
+#define GDIST_METHOD_BITSET  2   /* dictionary-rank bitsets: AND + popcount tiles */
+
+/* bitset build flags */
+#define GDIST_BITSET_KEEP_SINGLETONS 0x1u /* keep kmers present in only one set
+                                             (default prunes them: they never intersect) */
+
+/* row-query modes */
+#define GDIST_QUERY_ALL     0
+#define GDIST_QUERY_ANY_LE  1
+#define GDIST_QUERY_ARGMIN  2
+
+typedef struct gdist_ctx  gdist_ctx;
+typedef struct gdist_sets gdist_sets;
+
+/* ---- library / context ---------------------------------------------- */
+const char* gdist_version(void);
+int  gdist_abi_version(void);
+const char* gdist_last_error(void);                 /* thread-local */
+int  gdist_device_count(int* n);
+int  gdist_ctx_create(int device, gdist_ctx** out);
+int  gdist_ctx_destroy(gdist_ctx* ctx);
+int  gdist_ctx_synchronize(gdist_ctx* ctx);
+/* HIP-event time of the last intersect/sketch matrix call's main kernel(s)
+ * and of the whole call, in ms (recorded on the stream they run on). */
+int  gdist_ctx_last_timing(gdist_ctx* ctx, double* kernel_ms, double* call_ms, int64_t* launches);
+int  gdist_dev_alloc(gdist_ctx* ctx, int64_t bytes, void** dptr);
+int  gdist_dev_free(gdist_ctx* ctx, void* dptr);
+int  gdist_memcpy_d2h(gdist_ctx* ctx, void* dst, const void* src, int64_t bytes);
+int  gdist_memcpy_h2d(gdist_ctx* ctx, void* dst, const void* src, int64_t bytes);
+
+/* ---- kmer sets ------------------------------------------------------- */
+/* Build kmer sets of nseqs sequences on the device. seqs is the byte
+ * concatenation, sequence s = seqs[seq_off[s] .. seq_off[s+1]). */
+int  gdist_sets_pack(gdist_ctx* ctx, int kind, int k, unsigned flags,
+                     const char* seqs, const int64_t* seq_off, int64_t nseqs,
+                     gdist_sets** out);
+/* Same, but the sequences are already in device memory (no H2D). */
+int  gdist_sets_pack_device(gdist_ctx* ctx, int kind, int k, unsigned flags,
+                            const char* d_seqs, const int64_t* d_seq_off, int64_t nseqs,
+                            int64_t total_bytes, gdist_sets** out);
+/* Adopt caller-packed sets: CSR of sorted, unique codes (host arrays, copied). */
+int  gdist_sets_upload(gdist_ctx* ctx, int kind, int k, int64_t nsets,
+                       const int64_t* offsets, const uint64_t* codes, gdist_sets** out);
+int  gdist_sets_free(gdist_sets* sets);
+int  gdist_sets_info(const gdist_sets* sets, int* kind, int* k, int64_t* nsets, int64_t* total_codes);
+int  gdist_sets_sizes(const gdist_sets* sets, int64_t* sizes);           /* nsets values */
+int  gdist_sets_download(const gdist_sets* sets, int64_t* offsets, uint64_t* codes);
+/* Build the dictionary-rank bitset representation (kept with the sets). */
+int  gdist_sets_build_bitsets(gdist_sets* sets, unsigned flags);
+int  gdist_sets_bitset_info(const gdist_sets* sets, int64_t* dict_size, int64_t* words_per_set);
+/* Concatenate two collections (e.g. base genomes + comparison genomes). */
+int  gdist_sets_concat(const gdist_sets* a, const gdist_sets* b, gdist_sets** out);
+
+/* ---- distances ------------------------------------------------------- */
+/* Pairs (i, j), r0 <= i < r1, c0 <= j < c1 (global set indices of `sets`).
+ * I_out[(i-r0)*ld + (j-c0)] = |A_i ∩ A_j|, D_out[...] = distance; either
+ * output may be NULL. With GDIST_UPPER_TRIANGLE, entries with j <= i are
+ * left untouched. */
+int  gdist_intersect_matrix(gdist_ctx* ctx, const gdist_sets* sets,
+                            int64_t r0, int64_t r1, int64_t c0, int64_t c1,
+                            int method, unsigned flags,
+                            int32_t* I_out, double* D_out, int64_t ld);
+/* One query set q against ncols sets (indices cols[]):
+ *  ALL:    D_out[c] for every c
+ *  ANY_LE: *hit = 1 if any distance <= t (D_out may be NULL)
+ *  ARGMIN: *best_idx = position in cols[] of the smallest distance (ties ->
+ *          lowest position), *best_d = that distance; -1 / 1.0 when no
+ *          distance is below 1.0 (the reference's NULL_RESULT identity wins
+ *          ties at 1.0, DistanceRepsProcessor.java:318-332). */
+int  gdist_row_query(gdist_ctx* ctx, const gdist_sets* sets, int64_t q,
+                     const int64_t* cols, int64_t ncols, int mode, double t,
+                     double* D_out, int32_t* hit, int64_t* best_idx, double* best_d);
+
+/* ---- MinHash sketches ------------------------------------------------ */
+/* Bottom-`width` signature per set: the width smallest distinct
+ * murmur3_x86_32(seed 0) hashes (signed int order) of the kmer strings. */
+int  gdist_sketch_build(gdist_ctx* ctx, const gdist_sets* sets, int width, gdist_sets** out);
+int  gdist_sketch_upload(gdist_ctx* ctx, int width, int64_t nsets, const int64_t* offsets,
+                         const int32_t* sigs, gdist_sets** out);
+int  gdist_sketch_download(const gdist_sets* sk, int64_t* offsets, int32_t* sigs);
+int  gdist_sketch_matrix(gdist_ctx* ctx, const gdist_sets* sk,
+                         int64_t r0, int64_t r1, int64_t c0, int64_t c1, unsigned flags,
+                         int32_t* common_out, double* D_out, int64_t ld);
+
+/* ---- multi-GPU (RCCL over xGMI) -------------------------------------- */
+#define GDIST_UNIQUE_ID_BYTES 128
+int  gdist_comm_unique_id(char id[GDIST_UNIQUE_ID_BYTES]);
+int  gdist_comm_init(gdist_ctx* ctx, const char id[GDIST_UNIQUE_ID_BYTES], int nranks, int rank);
+int  gdist_comm_destroy(gdist_ctx* ctx);
+/* Every rank passes its local shard; every rank receives the concatenation
+ * in rank order (one RCCL all-gather of offsets and one of codes). */
+int  gdist_sets_allgather(gdist_ctx* ctx, const gdist_sets* local, gdist_sets** out);
+/* Dictionary-rank bitsets of the concatenation (in rank order) of every
+ * rank's local sets: one all-gather of the local dictionary summaries
+ * (distinct codes + counts), one of the local bitsets. The result holds the
+ * bitsets and sizes of all sets but no codes: use it with
+ * GDIST_METHOD_BITSET (or AUTO). Memory per rank ~ N * W words instead of
+ * every rank's codes. */
+int  gdist_sets_allgather_bitsets(gdist_ctx* ctx, const gdist_sets* local, unsigned flags, gdist_sets** out);
+/* Scalar max-reduction and barrier over the communicator (timing only). */
+int  gdist_comm_allreduce_max(gdist_ctx* ctx, double* value);
+
+/* Row partition with equal upper-triangle area:
+ * r_g = N (1 - sqrt(1 - g/G)), rounded to multiples of `align`. */
+int  gdist_triangle_partition(int64_t n, int nparts, int64_t align, int64_t* bounds /* nparts+1 */);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GDIST_H */

@@ -1,0 +1,131 @@
+"""ctypes binding of the CPU oracle (oracle/build/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg — never by the product package. Parity unpinned
+(see gdist_oracle.h).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = C.CDLL(_LIB_PATH)
+        i64, u64p, i64p = C.c_int64, C.POINTER(C.c_uint64), C.POINTER(C.c_int64)
+        L.or_kmer_codes.restype = i64
+        L.or_kmer_codes.argtypes = [C.c_int, C.c_int, C.c_uint, C.c_char_p, i64, u64p]
+        L.or_intersect.restype = i64
+        L.or_intersect.argtypes = [u64p, i64, u64p, i64]
+        L.or_distance.restype = C.c_double
+        L.or_distance.argtypes = [i64, i64, i64, C.c_uint]
+        L.or_java_dtoa.restype = C.c_int
+        L.or_java_dtoa.argtypes = [C.c_double, C.c_char_p]
+        L.or_murmur3_32.restype = C.c_uint32
+        L.or_murmur3_32.argtypes = [C.c_char_p, C.c_int, C.c_uint32]
+        L.or_sketch.restype = i64
+        L.or_sketch.argtypes = [C.c_int, C.c_int, C.c_uint, u64p, i64, C.c_int, C.POINTER(C.c_int32)]
+        L.or_sketch_distance.restype = C.c_double
+        L.or_sketch_distance.argtypes = [C.POINTER(C.c_int32), i64, C.POINTER(C.c_int32), i64,
+                                         C.c_int, C.c_uint, i64p]
+        L.or_matrix.restype = None
+        L.or_matrix.argtypes = [i64p, u64p, i64, i64, i64, i64, C.c_uint,
+                                C.POINTER(C.c_int32), C.POINTER(C.c_double), i64, C.c_int]
+        L.or_faithful_fasta_dist.restype = i64
+        L.or_faithful_fasta_dist.argtypes = [C.c_int, C.c_int, C.c_uint, C.c_char_p, i64p, i64,
+                                             C.c_int, i64, C.POINTER(C.c_double), C.c_int]
+        _lib = L
+    return _lib
+
+
+def _p(a, t):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+def kmer_codes(seq: bytes, k: int, kind: int = 0, flags: int = 0) -> np.ndarray:
+    out = np.empty(max(2 * len(seq), 1), dtype=np.uint64)
+    n = lib().or_kmer_codes(kind, k, flags, seq, len(seq), _p(out, C.c_uint64))
+    if n < 0:
+        raise ValueError("unencodable sequence for this kmer spec")
+    return out[:n].copy()
+
+
+def pack(seqs: list[bytes], k: int, kind: int = 0, flags: int = 0):
+    sets = [kmer_codes(s, k, kind, flags) for s in seqs]
+    off = np.zeros(len(sets) + 1, dtype=np.int64)
+    off[1:] = np.cumsum([len(s) for s in sets])
+    codes = np.concatenate(sets) if sets else np.zeros(0, np.uint64)
+    return off, codes.astype(np.uint64)
+
+
+def intersect(a: np.ndarray, b: np.ndarray) -> int:
+    a = np.ascontiguousarray(a, np.uint64); b = np.ascontiguousarray(b, np.uint64)
+    return int(lib().or_intersect(_p(a, C.c_uint64), len(a), _p(b, C.c_uint64), len(b)))
+
+
+def distance(inter: int, na: int, nb: int, flags: int = 0) -> float:
+    return float(lib().or_distance(inter, na, nb, flags))
+
+
+def java_dtoa(d: float) -> str:
+    buf = C.create_string_buffer(64)
+    n = lib().or_java_dtoa(d, buf)
+    return buf.raw[:n].decode()
+
+
+def murmur3(data: bytes, seed: int = 0) -> int:
+    h = lib().or_murmur3_32(data, len(data), seed)
+    return h - (1 << 32) if h & 0x80000000 else h
+
+
+def sketch(codes: np.ndarray, k: int, kind: int, width: int, flags: int = 0) -> np.ndarray:
+    codes = np.ascontiguousarray(codes, np.uint64)
+    out = np.empty(max(width, 1), dtype=np.int32)
+    n = lib().or_sketch(kind, k, flags, _p(codes, C.c_uint64), len(codes), width, _p(out, C.c_int32))
+    return out[:n].copy()
+
+
+def sketch_distance(a: np.ndarray, b: np.ndarray, width: int, flags: int = 0):
+    a = np.ascontiguousarray(a, np.int32); b = np.ascontiguousarray(b, np.int32)
+    common = C.c_int64(0)
+    d = lib().or_sketch_distance(_p(a, C.c_int32), len(a), _p(b, C.c_int32), len(b), width, flags,
+                                 C.byref(common))
+    return float(d), int(common.value)
+
+
+def matrix(off: np.ndarray, codes: np.ndarray, r0: int, r1: int, c0: int, c1: int,
+           flags: int = 0, nthreads: int = 0):
+    off = np.ascontiguousarray(off, np.int64); codes = np.ascontiguousarray(codes, np.uint64)
+    I = np.zeros((r1 - r0, c1 - c0), dtype=np.int32)
+    D = np.zeros((r1 - r0, c1 - c0), dtype=np.float64)
+    lib().or_matrix(_p(off, C.c_int64), _p(codes, C.c_uint64), r0, r1, c0, c1, flags,
+                    _p(I, C.c_int32), _p(D, C.c_double), c1 - c0, nthreads)
+    return I, D
+
+
+def faithful_fasta_dist(seqs: list[bytes], k: int, kind: int = 0, flags: int = 0, batch: int = 20,
+                        max_rows: int = 0, nthreads: int = 0):
+    blob = b"".join(seqs)
+    off = np.zeros(len(seqs) + 1, dtype=np.int64)
+    off[1:] = np.cumsum([len(s) for s in seqs])
+    n = len(seqs)
+    D = np.full((n, n), np.nan, dtype=np.float64)
+    pairs = lib().or_faithful_fasta_dist(kind, k, flags, blob, _p(off, C.c_int64), n, batch, max_rows,
+                                         _p(D, C.c_double), nthreads)
+    return int(pairs), D

@@ -1,0 +1,329 @@
+"""GPU parity: the HIP path (through libgdist.so's C-ABI) against the CPU
+oracle and the committed golden vectors. Bit-exact for codes, counts and
+distances (fp64, no tolerance). Parity is unpinned against the reference
+itself — these pin the device to the two restatements."""
+import io
+import json
+import math
+import os
+import random
+
+import numpy as np
+import pytest
+
+import oracle
+import pyref
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "kmer_golden.json")
+
+
+def golden_cases():
+    with open(GOLDEN) as f:
+        return json.load(f)["cases"]
+
+
+def bits_equal(a, b):
+    a = np.ascontiguousarray(a, np.float64)
+    b = np.ascontiguousarray(b, np.float64)
+    return np.array_equal(a.view(np.uint64), b.view(np.uint64))
+
+
+def oracle_pack(seqs, k, kind, flags):
+    return oracle.pack([s if isinstance(s, bytes) else s.encode("latin-1") for s in seqs], k, kind, flags)
+
+
+# ---------------------------------------------------------------- golden
+@pytest.mark.parametrize("case", golden_cases(), ids=lambda c: c["name"])
+def test_golden_through_device(ctx, case):
+    import gdist
+    kt = gdist.KmerType.DNA if case["kind"] == 0 else gdist.KmerType.PROT
+    sets = gdist.KmerSets.from_sequences(case["seqs"], case["k"], kt, case["flags"], ctx)
+    off, codes = sets.download()
+    got = [[str(int(x)) for x in codes[off[i]:off[i + 1]]] for i in range(len(off) - 1)]
+    assert got == case["codes"]
+    assert sets.sizes().tolist() == case["sizes"]
+    for method in (gdist.METHOD_SORTED, gdist.METHOD_BITSET):
+        I, D = sets.matrix(method=method)
+        assert I.tolist() == case["I"], method
+        assert [[gdist.java_double(x) for x in r] for r in D] == case["D"], method
+    w = case["width"]
+    sk = sets.sketches(w)
+    so, sv = sk.download()
+    assert [sv[so[i]:so[i + 1]].tolist() for i in range(len(so) - 1)] == case["sketch"]
+    _, SD = sk.matrix()
+    assert [[gdist.java_double(x) for x in r] for r in SD] == case["sketch_D"]
+    _, SJ = sk.matrix(flags=gdist.SKETCH_JACCARD)
+    assert [[gdist.java_double(x) for x in r] for r in SJ] == case["sketch_D_jaccard"]
+
+
+# ---------------------------------------------------------------- packing
+@pytest.mark.parametrize("seed", range(6))
+def test_pack_random_modes(ctx, seed):
+    import gdist
+    rng = random.Random(seed)
+    for _ in range(12):
+        kind = rng.choice([0, 1])
+        if kind == 0:
+            alpha = rng.choice(["ACGT", "acgtACGT", "ACGTN", "ACGTNRYacgt", "ACGT\0"])
+            flags = rng.choice([0, 1, 2]) | rng.choice([0, 4, 8])
+            k = rng.randint(1, 21 if flags & 8 else 32)
+        else:
+            alpha = rng.choice(["ACDEFGHIKLMNPQRSTVWY", "ACDEFGHIKLMNPQRSTVWYX*", "acdefgACD", "ACD\0"])
+            flags = rng.choice([0, 4, 8]) | rng.choice([0, 0x10])
+            k = rng.randint(1, 12)
+        seqs = ["".join(rng.choice(alpha) for _ in range(rng.randint(0, 300))) for _ in range(rng.randint(1, 40))]
+        kt = gdist.KmerType.DNA if kind == 0 else gdist.KmerType.PROT
+        try:
+            eo, ec = oracle_pack(seqs, k, kind, flags)
+        except ValueError:
+            with pytest.raises(ValueError):
+                gdist.KmerSets.from_sequences(seqs, k, kt, flags, ctx)
+            continue
+        sets = gdist.KmerSets.from_sequences(seqs, k, kt, flags, ctx)
+        off, codes = sets.download()
+        assert np.array_equal(off, eo) and np.array_equal(codes, ec), (kind, k, flags)
+
+
+def test_pack_rejects_unencodable_and_bad_k(ctx):
+    import gdist
+    with pytest.raises(ValueError):
+        gdist.KmerSets.from_sequences(["ACGTX"], 5, gdist.KmerType.DNA, gdist.AMBIG_KEEP, ctx)
+    with pytest.raises(ValueError):
+        gdist.KmerSets.from_sequences(["ACGT"], 33, gdist.KmerType.DNA, 0, ctx)
+    with pytest.raises(ValueError):
+        gdist.KmerSets.from_sequences(["ACDE"], 13, gdist.KmerType.PROT, 0, ctx)
+    with pytest.raises(ValueError):
+        gdist.KmerSets.from_sequences(["AC1DE"], 10, gdist.KmerType.PROT, 0, ctx)
+
+
+def test_empty_and_short_inputs(ctx):
+    import gdist
+    sets = gdist.KmerSets.from_sequences(["", "AC", "ACGTACGT", ""], 5, gdist.KmerType.DNA, 0, ctx)
+    assert sets.sizes().tolist()[:2] == [0, 0]
+    I, D = sets.matrix()
+    assert I[0, 1] == 0 and D[0, 1] == 1.0 and D[0, 0] == 1.0
+    _, Dn = sets.matrix(flags=gdist.EMPTY_NAN)
+    assert math.isnan(Dn[0, 1]) and Dn[2, 2] == 0.0
+    none = gdist.KmerSets.from_sequences([], 5, gdist.KmerType.DNA, 0, ctx)
+    assert len(none) == 0
+    I0, D0 = none.matrix()
+    assert I0.shape == (0, 0)
+
+
+# ---------------------------------------------------------------- matrices
+def synth_sets(n, length, pmax, cfg, protein=False):
+    from gdist import synth
+    g = synth.genomes(n, length, pmax, cfg, protein=protein)
+    return [bytes(r) for r in g]
+
+
+@pytest.mark.parametrize("method", ["sorted", "bitset", "bitset_keep"])
+def test_matrix_vs_oracle_rectangles(ctx, method):
+    import gdist
+    seqs = synth_sets(300, 3000, 0.05, 91)
+    sets = gdist.KmerSets.from_sequences(seqs, 15, gdist.KmerType.DNA, 0, ctx)
+    m = gdist.METHOD_SORTED
+    if method != "sorted":
+        sets.build_bitsets(keep_singletons=(method == "bitset_keep"))
+        m = gdist.METHOD_BITSET
+    off, codes = oracle_pack(seqs, 15, 0, 0)
+    for (r0, r1, c0, c1, upper) in [(0, 300, 0, 300, True), (0, 300, 0, 300, False), (37, 201, 5, 290, False),
+                                    (100, 101, 0, 300, False), (129, 260, 0, 300, True), (0, 1, 0, 1, False)]:
+        I, D = sets.matrix((r0, r1), (c0, c1), upper=upper, method=m)
+        eI, eD = oracle.matrix(off, codes, r0, r1, c0, c1, flags=0x100 if upper else 0)
+        if upper:
+            mask = np.fromfunction(lambda a, b: (c0 + b) > (r0 + a), (r1 - r0, c1 - c0))
+            assert (I[~mask] == -1).all() and np.isnan(D[~mask]).all()   # untouched
+            I, D, eI, eD = I[mask], D[mask], eI[mask], eD[mask]
+        assert np.array_equal(I, eI)
+        assert bits_equal(D, eD)
+
+
+def test_bitset_prune_equals_keep_and_dictionary(ctx):
+    import gdist
+    seqs = synth_sets(150, 5000, 0.01, 92)
+    a = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
+    b = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
+    da, wa = a.build_bitsets(keep_singletons=False)
+    db, wb = b.build_bitsets(keep_singletons=True)
+    assert da < db
+    Ia, Da = a.matrix(method=gdist.METHOD_BITSET)
+    Ib, Db = b.matrix(method=gdist.METHOD_BITSET)
+    Is, Ds = a.matrix(method=gdist.METHOD_SORTED)
+    assert np.array_equal(Ia, Ib) and np.array_equal(Ia, Is)
+    assert bits_equal(Da, Db) and bits_equal(Da, Ds)
+    # dictionary with singletons == number of distinct kmers overall
+    off, codes = oracle_pack(seqs, 21, 0, 0)
+    assert db == len(np.unique(codes))
+
+
+def test_protein_sorted_vs_oracle(ctx):
+    import gdist
+    seqs = synth_sets(200, 2000, 0.10, 93, protein=True)
+    sets = gdist.KmerSets.from_sequences(seqs, 8, gdist.KmerType.PROT, 0, ctx)
+    off, codes = oracle_pack(seqs, 8, 1, 0)
+    I, D = sets.matrix(upper=True, method=gdist.METHOD_SORTED)
+    eI, eD = oracle.matrix(off, codes, 0, 200, 0, 200, flags=0x100)
+    iu = np.triu_indices(200, 1)
+    assert np.array_equal(I[iu], eI[iu]) and bits_equal(D[iu], eD[iu])
+
+
+def test_large_segments_and_sentinel_code(ctx):
+    """Segments larger than one LDS table fill, and the all-ones code."""
+    import gdist
+    rng = np.random.default_rng(4)
+    sets_codes = []
+    base = np.unique(rng.integers(0, 2 ** 63, 30000, dtype=np.uint64))
+    for t in range(5):
+        keep = base[rng.random(len(base)) < 0.8]
+        extra = np.array([~np.uint64(0)], dtype=np.uint64) if t % 2 == 0 else np.zeros(0, np.uint64)
+        sets_codes.append(np.unique(np.concatenate([keep, extra])))
+    off = np.zeros(6, np.int64)
+    off[1:] = np.cumsum([len(c) for c in sets_codes])
+    flat = np.concatenate(sets_codes)
+    sets = gdist.KmerSets.from_codes(off, flat, 8, gdist.KmerType.PROT, ctx)
+    I, D = sets.matrix(method=gdist.METHOD_SORTED)
+    eI, eD = oracle.matrix(off, flat, 0, 5, 0, 5)
+    assert np.array_equal(I, eI) and bits_equal(D, eD)
+    sets.build_bitsets()
+    I2, D2 = sets.matrix(method=gdist.METHOD_BITSET)
+    assert np.array_equal(I2, eI) and bits_equal(D2, eD)
+
+
+# ---------------------------------------------------------------- properties at size
+def test_full_size_properties_bitset(ctx):
+    """Size-independent properties on a larger collection: symmetry,
+    diagonal I = |A|, D = 0 on the diagonal, and agreement with the oracle
+    on a sampled row block."""
+    import gdist
+    n = 600
+    seqs = synth_sets(n, 20000, 0.002, 94)
+    sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
+    sets.build_bitsets()
+    I, D = sets.matrix(method=gdist.METHOD_BITSET)
+    assert np.array_equal(I, I.T) and bits_equal(D, D.T)
+    assert np.array_equal(np.diag(I), sets.sizes())
+    assert (np.diag(D) == 0.0).all()
+    off, codes = oracle_pack(seqs[:40], 21, 0, 0)
+    eI, eD = oracle.matrix(off, codes, 0, 40, 0, 40)
+    assert np.array_equal(I[:40, :40], eI) and bits_equal(D[:40, :40], eD)
+    Is, Ds = sets.matrix((0, 64), (0, n), method=gdist.METHOD_SORTED)
+    assert np.array_equal(Is, I[:64]) and bits_equal(Ds, D[:64])
+
+
+def test_device_outputs_and_leading_dimension(ctx):
+    import gdist
+    seqs = synth_sets(130, 4000, 0.05, 95)
+    sets = gdist.KmerSets.from_sequences(seqs, 12, gdist.KmerType.DNA, 0, ctx)
+    sets.build_bitsets()
+    ld = 200
+    dI = ctx.alloc(130 * ld * 4)
+    dD = ctx.alloc(130 * ld * 8)
+    sets.matrix_device(dI.ptr, dD.ptr, ld, (0, 130), (0, 130), method=gdist.METHOD_BITSET)
+    I = dI.to_host(np.int32).reshape(130, ld)[:, :130]
+    D = dD.to_host(np.float64).reshape(130, ld)[:, :130]
+    eI, eD = sets.matrix(method=gdist.METHOD_SORTED)
+    assert np.array_equal(I, eI) and bits_equal(D, eD)
+    k_ms, call_ms, launches = ctx.last_timing()
+    assert launches == 1 and 0 < k_ms <= call_ms
+
+
+# ---------------------------------------------------------------- row queries
+def test_row_queries(ctx):
+    import gdist
+    seqs = synth_sets(80, 3000, 0.2, 96)
+    sets = gdist.KmerSets.from_sequences(seqs, 11, gdist.KmerType.DNA, 0, ctx)
+    _, D = sets.matrix(method=gdist.METHOD_SORTED)
+    cols = [5, 17, 3, 60, 22, 79]
+    for use_bits in (False, True):
+        if use_bits:
+            sets.build_bitsets()
+        d = sets.row_query(9, cols)
+        assert bits_equal(d, D[9, cols])
+        t = float(np.median(D[9, cols]))
+        assert sets.row_query(9, cols, gdist.QUERY_ANY_LE, t) == bool((D[9, cols] <= t).any())
+        assert sets.row_query(9, cols, gdist.QUERY_ANY_LE, -1.0) is False
+        pos, bd = sets.row_query(9, cols, gdist.QUERY_ARGMIN)
+        assert pos == int(np.argmin(D[9, cols])) and bd == D[9, cols].min()
+    far = gdist.KmerSets.from_sequences(["AAAAAAAAAAAAAAAA", "CCCCCCCCCCCCCCCC"], 11, gdist.KmerType.DNA, 0, ctx)
+    assert far.row_query(0, [1], gdist.QUERY_ARGMIN) == (-1, 1.0)      # NULL_RESULT semantics
+
+
+def test_sequence_kmers_view_api(ctx):
+    import gdist
+    a = gdist.KmerType.DNA.createKmers("ACGTTGCAACGTAGCTAGCT", 5)
+    b = gdist.KmerType.DNA.createKmers("ACGTTGCAACGTAGCTTTTT", 5)
+    sa = pyref.kmer_set("ACGTTGCAACGTAGCTAGCT", 5)
+    sb = pyref.kmer_set("ACGTTGCAACGTAGCTTTTT", 5)
+    assert a.size() == len(sa) and b.size() == len(sb)
+    assert a.distance(b) == pyref.set_distance(sa, sb)
+    assert a.similarity(b) == len(sa & sb)
+    assert a.hashSet(8).tolist() == pyref.sketch(sa, 8)
+
+
+# ---------------------------------------------------------------- sketches
+def test_sketch_matrix_vs_oracle(ctx):
+    import gdist
+    seqs = synth_sets(70, 2000, 0.1, 97)
+    sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
+    off, codes = oracle_pack(seqs, 21, 0, 0)
+    for w in (50, 1000, 1500):
+        sk = sets.sketches(w)
+        so, sv = sk.download()
+        ref = [oracle.sketch(codes[off[i]:off[i + 1]], 21, 0, w) for i in range(70)]
+        for i in range(70):
+            assert np.array_equal(sv[so[i]:so[i + 1]], ref[i])
+        for fl in (0, gdist.SKETCH_JACCARD):
+            C, D = sk.matrix(upper=True, flags=fl)
+            for i in range(0, 70, 7):
+                for j in range(i + 1, 70):
+                    d, c = oracle.sketch_distance(ref[i], ref[j], w, fl)
+                    assert C[i, j] == c and D[i, j] == d
+    up = gdist.SketchSets.from_signatures([np.array([1, 5, 9], np.int32), np.array([5, 9, 11], np.int32)], 4, ctx)
+    C, D = up.matrix()
+    assert C[0, 1] == 2 and D[0, 1] == pyref.sketch_distance([1, 5, 9], [5, 9, 11], 4)[0]
+
+
+# ---------------------------------------------------------------- processors
+def test_fasta_distance_processor_output(ctx):
+    import gdist
+    from gdist import processors
+    seqs = synth_sets(40, 800, 0.05, 98)
+    recs = [gdist.Sequence(f"s{i}", f"genome {i}", s.decode()) for i, s in enumerate(seqs)]
+    buf = io.StringIO()
+    pairs = processors.fasta_distance(recs, buf, kmer_size=13, ctx=ctx)
+    assert pairs == 40 * 39 // 2
+    lines = buf.getvalue().splitlines()
+    assert lines[0] == "seq1\tname1\tseq2\tname2\tdistance"
+    sets = [pyref.kmer_set(s.decode(), 13) for s in seqs]
+    exp = {f"s{i}\tgenome {i}\ts{j}\tgenome {j}\t{pyref.java_double_str(pyref.set_distance(sets[i], sets[j]))}"
+           for i in range(40) for j in range(i + 1, 40)}
+    assert set(lines[1:]) == exp
+    with pytest.raises(processors.ParseFailureException):
+        processors.fasta_distance(recs, io.StringIO(), kmer_size=1, ctx=ctx)
+
+
+def test_genome_and_reps_processors(ctx):
+    from gdist import processors
+    seqs = synth_sets(30, 1500, 0.3, 99)
+    gens = [processors.Genome(f"g{i}", f"name {i}", [s[:700].decode(), s[700:].decode()]) for i, s in enumerate(seqs)]
+    buf = io.StringIO()
+    n = processors.genome_distance(gens[:10], [gens[10:20], gens[20:]], buf, kmer_size=12, ctx=ctx)
+    assert n == 20 * 10
+    lines = buf.getvalue().splitlines()
+    ks = [pyref.kmer_set("\0".join(g.contigs), 12) for g in gens]
+    assert lines[1] == f"g10\tg0\t{pyref.java_double_str(pyref.set_distance(ks[10], ks[0]))}"
+    prefix, lst, stats = processors.distance_reps(gens, kmer_size=12, max_dist=0.5, ctx=ctx)
+    assert prefix == "rep0.5000_K12"
+    reps = []
+    for i in range(30):                        # greedy pass-1 restated on string sets
+        if not any(pyref.set_distance(ks[r], ks[i]) <= 0.5 for r in reps):
+            reps.append(i)
+    rows = [l.split("\t") for l in lst.splitlines()[1:]]
+    assert len(rows) == 30
+    rep_ids = {f"g{r}" for r in reps}
+    for i, row in enumerate(rows):
+        d = min(pyref.set_distance(ks[i], ks[r]) for r in reps)
+        assert row[2] in rep_ids and row[4] == pyref.java_double_str(0.0 if i in reps else d)

@@ -1,0 +1,138 @@
+"""CPU: the C oracle against the golden vectors, the independent Python
+restatement and hand-derived known answers (parity unpinned: SURVEY §8c)."""
+import json
+import math
+import os
+import random
+
+import numpy as np
+import pytest
+
+import oracle
+import pyref
+from gdist.javafmt import java_double
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "kmer_golden.json")
+
+
+def load_cases():
+    with open(GOLDEN) as f:
+        return json.load(f)["cases"]
+
+
+@pytest.mark.parametrize("case", load_cases(), ids=lambda c: c["name"])
+def test_oracle_matches_golden(case):
+    kind, k, flags = case["kind"], case["k"], case["flags"]
+    codes = [oracle.kmer_codes(s.encode("latin-1"), k, kind, flags) for s in case["seqs"]]
+    assert [len(c) for c in codes] == case["sizes"]
+    for c, exp in zip(codes, case["codes"]):
+        assert [str(int(x)) for x in c] == exp
+    off = np.zeros(len(codes) + 1, np.int64)
+    off[1:] = np.cumsum([len(c) for c in codes])
+    flat = np.concatenate(codes) if codes else np.zeros(0, np.uint64)
+    n = len(codes)
+    I, D = oracle.matrix(off, flat, 0, n, 0, n)
+    assert I.tolist() == case["I"]
+    assert [[oracle.java_dtoa(x) for x in row] for row in D] == case["D"]
+    w = case["width"]
+    sk = [oracle.sketch(c, k, kind, w, flags) for c in codes]
+    assert [s.tolist() for s in sk] == case["sketch"]
+    for i in range(n):
+        for j in range(n):
+            d, _ = oracle.sketch_distance(sk[i], sk[j], w)
+            assert oracle.java_dtoa(d) == case["sketch_D"][i][j]
+            dj, _ = oracle.sketch_distance(sk[i], sk[j], w, pyref.SKETCH_JACCARD)
+            assert oracle.java_dtoa(dj) == case["sketch_D_jaccard"][i][j]
+
+
+def test_known_answers():
+    # identical sets -> 0.0, disjoint -> 1.0 (GroupTypeSpec.java:84 treats 1.0 as "nothing shared")
+    a = oracle.kmer_codes(b"ACGTT", 3, 0, pyref.STRAND_FWD)
+    b = oracle.kmer_codes(b"CGTTA", 3, 0, pyref.STRAND_FWD)
+    assert len(a) == 3 and len(b) == 3
+    assert oracle.intersect(a, a) == 3 and oracle.java_dtoa(oracle.distance(3, 3, 3)) == "0.0"
+    # worked example: {ACG,CGT,GTT} vs {CGT,GTT,TTA}: I=2, union 4 -> 0.5
+    assert oracle.intersect(a, b) == 2
+    assert oracle.java_dtoa(oracle.distance(2, 3, 3)) == "0.5"
+    g = oracle.kmer_codes(b"GGGGG", 3, 0, pyref.STRAND_FWD)
+    assert oracle.intersect(a, g) == 0 and oracle.java_dtoa(oracle.distance(0, 3, 1)) == "1.0"
+    # repeated kmers collapse; shorter than k -> empty; empty vs empty -> 1.0 (NaN mode available)
+    assert len(oracle.kmer_codes(b"AAAAAA", 3, 0, pyref.STRAND_FWD)) == 1
+    assert len(oracle.kmer_codes(b"AC", 3, 0, 0)) == 0
+    assert oracle.distance(0, 0, 0) == 1.0
+    assert math.isnan(oracle.distance(0, 0, 0, pyref.EMPTY_NAN))
+    # both strands: ACGT is its own reverse complement -> {AC, CG, GT}
+    assert len(oracle.kmer_codes(b"ACGT", 2, 0, pyref.STRAND_BOTH)) == 3
+    # case folding and ambiguity skip (DNA default): acgNt -> only 'ACG' (k=3)
+    assert [int(x) for x in oracle.kmer_codes(b"acgNt", 3, 0, pyref.STRAND_FWD)] == [pyref.encode("ACG")]
+    # 1 - 1/3
+    assert oracle.java_dtoa(oracle.distance(1, 2, 2)) == "0.6666666666666667"
+
+
+@pytest.mark.parametrize("v,s", [(0.5, "0.5"), (1.0, "1.0"), (0.0, "0.0"), (9.5e-4, "9.5E-4"), (1e-3, "0.001"),
+                                 (1e7, "1.0E7"), (1e-5, "1.0E-5"), (4.9e-324, "4.9E-324"), (1e23, "1.0E23"),
+                                 (123456.789, "123456.789"), (float("nan"), "NaN"), (-0.0, "-0.0"),
+                                 (float("inf"), "Infinity"), (2.0 / 3.0, "0.6666666666666666")])
+def test_java_double_to_string(v, s):
+    assert oracle.java_dtoa(v) == s
+    assert pyref.java_double_str(v) == s
+    assert java_double(v) == s
+
+
+def test_java_format_random_agreement():
+    rng = random.Random(7)
+    for _ in range(20000):
+        i = rng.randint(0, 10 ** 6)
+        na, nb = rng.randint(i, 10 ** 6), rng.randint(i, 10 ** 6)
+        d = pyref.distance(i, na, nb)
+        assert oracle.java_dtoa(d) == pyref.java_double_str(d) == java_double(d)
+        x = rng.random() * 10 ** rng.randint(-12, 12)
+        assert oracle.java_dtoa(x) == pyref.java_double_str(x) == java_double(x)
+
+
+def test_oracle_vs_pyref_random():
+    rng = random.Random(11)
+    for _ in range(1500):
+        kind = rng.choice([0, 1])
+        if kind == 0:
+            alpha = rng.choice(["ACGT", "acgtACGT", "ACGTN", "ACGTNRYacgt", "ACGT\0"])
+            flags = rng.choice([0, 1, 2]) | rng.choice([0, 4, 8])
+            k = rng.randint(1, 21)
+        else:
+            alpha = rng.choice(["ACDEFGHIKLMNPQRSTVWY", "ACDEFGHIKLMNPQRSTVWYX*", "acdefgACD", "AC1", "ACD\0"])
+            flags = rng.choice([0, 4, 8]) | rng.choice([0, 0x10])
+            k = rng.randint(1, 12)
+        s = "".join(rng.choice(alpha) for _ in range(rng.randint(0, 50)))
+        try:
+            c = [int(x) for x in oracle.kmer_codes(s.encode("latin-1"), k, kind, flags)]
+        except ValueError:
+            c = None
+        try:
+            e = sorted(pyref.encode(x, kind, flags) for x in pyref.kmer_set(s, k, kind, flags))
+        except ValueError:
+            e = None
+        assert c == e
+
+
+def test_murmur3_and_sketch_vs_pyref():
+    rng = random.Random(3)
+    for _ in range(300):
+        b = bytes(rng.randrange(256) for _ in range(rng.randint(0, 40)))
+        assert oracle.murmur3(b) == pyref.murmur3_32(b)
+    seq = "".join(rng.choice("ACGT") for _ in range(500))
+    codes = oracle.kmer_codes(seq.encode(), 11, 0, 0)
+    for w in (1, 10, 100, 5000):
+        assert oracle.sketch(codes, 11, 0, w).tolist() == pyref.sketch(pyref.kmer_set(seq, 11), w)
+
+
+def test_faithful_path_matches_oracle():
+    """The Java-faithful HashSet<String> baseline computes the same distances."""
+    rng = random.Random(5)
+    anc = "".join(rng.choice("ACGT") for _ in range(600))
+    seqs = ["".join(c if rng.random() > 0.02 else rng.choice("ACGT") for c in anc) for _ in range(25)]
+    pairs, D = oracle.faithful_fasta_dist([s.encode() for s in seqs], 11, 0, 0, batch=20)
+    assert pairs == 25 * 24 // 2
+    off, codes = oracle.pack([s.encode() for s in seqs], 11)
+    _, Dm = oracle.matrix(off, codes, 0, 25, 0, 25, flags=0x100)
+    iu = np.triu_indices(25, 1)
+    assert np.array_equal(D[iu], Dm[iu])
