@@ -325,8 +325,8 @@ void runs_of(gdist_ctx* ctx, const uint64_t* keys, int64_t n, DevBuf& flag, DevB
     exclusive_scan_i32_to_i64(ctx, flag.as<int32_t>(), pos.as<int64_t>(), (size_t)n);
     int64_t last = 0;
     int32_t lf = 0;
-    GD_HIP(hipMemcpyAsync(&last, pos.as<int64_t>() + n - 1, 8, hipMemcpyDeviceToHost, st));
-    GD_HIP(hipMemcpyAsync(&lf, flag.as<int32_t>() + n - 1, 4, hipMemcpyDeviceToHost, st));
+    d2h(&last, pos.as<int64_t>() + n - 1, 8, st);
+    d2h(&lf, flag.as<int32_t>() + n - 1, 4, st);
     GD_HIP(hipStreamSynchronize(st));
     nruns = last + lf;
     uniq.alloc(nruns * 8 + 8, st);
@@ -430,8 +430,8 @@ void dictionary_from(gdist_ctx* ctx, const std::vector<SummaryView>& parts, bool
         exclusive_scan_i32_to_i64(ctx, flag.as<int32_t>(), pos.as<int64_t>(), (size_t)n);
         int64_t last = 0;
         int32_t lf = 0;
-        GD_HIP(hipMemcpyAsync(&last, pos.as<int64_t>() + n - 1, 8, hipMemcpyDeviceToHost, st));
-        GD_HIP(hipMemcpyAsync(&lf, flag.as<int32_t>() + n - 1, 4, hipMemcpyDeviceToHost, st));
+        d2h(&last, pos.as<int64_t>() + n - 1, 8, st);
+        d2h(&lf, flag.as<int32_t>() + n - 1, 4, st);
         GD_HIP(hipStreamSynchronize(st));
         U = last + lf;
     }
@@ -521,7 +521,7 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     const int64_t target = (int64_t)ctx->cus * 8;
     int splits = (int)std::max<int64_t>(1, std::min<int64_t>(nchunks, ceil_div(target, (int64_t)tiles.size())));
     DevBuf dt(tiles.size() * sizeof(int2), st);
-    h2d_sync(dt.p, tiles.data(), tiles.size() * sizeof(int2), st);
+    h2d(dt.p, tiles.data(), tiles.size() * sizeof(int2), st);
     const int64_t grid = (int64_t)tiles.size() * splits;
     GD_REQUIRE(grid < (int64_t(1) << 31), "bitset matrix grid too large");
     GD_HIP(hipEventRecord(ctx->ev_k0, st));

@@ -164,7 +164,7 @@ int gdist_memcpy_d2h(gdist_ctx* ctx, void* dst, const void* src, int64_t bytes) 
     return guard([&] {
         use_device(ctx);
         if (bytes <= 0) return;
-        GD_HIP(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToHost, ctx->stream));
+        d2h(dst, src, (size_t)bytes, ctx->stream);
         GD_HIP(hipStreamSynchronize(ctx->stream));
     });
 }
@@ -173,7 +173,7 @@ int gdist_memcpy_h2d(gdist_ctx* ctx, void* dst, const void* src, int64_t bytes) 
     return guard([&] {
         use_device(ctx);
         if (bytes <= 0) return;
-        GD_HIP(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyHostToDevice, ctx->stream));
+        h2d(dst, src, (size_t)bytes, ctx->stream);
         GD_HIP(hipStreamSynchronize(ctx->stream));
     });
 }
@@ -192,8 +192,8 @@ int gdist_sets_pack(gdist_ctx* ctx, int kind, int k, unsigned flags, const char*
         for (int64_t s = 0; s < nseqs; s++) GD_REQUIRE(h[s + 1] >= h[s], "sequence offsets must be non-decreasing");
         const int64_t bytes = h[nseqs];
         DevBuf dseq(bytes + 1, ctx->stream), doff((nseqs + 1) * 8, ctx->stream);
-        if (bytes) GD_HIP(hipMemcpyAsync(dseq.p, seqs + base, bytes, hipMemcpyHostToDevice, ctx->stream));
-        GD_HIP(hipMemcpyAsync(doff.p, h.data(), (nseqs + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+        if (bytes) h2d(dseq.p, seqs + base, bytes, ctx->stream);
+        h2d(doff.p, h.data(), (nseqs + 1) * 8, ctx->stream);
         auto* s = new gdist_sets();
         s->ctx = ctx;
         try {
@@ -214,7 +214,7 @@ int gdist_sets_pack_device(gdist_ctx* ctx, int kind, int k, unsigned flags, cons
         GD_REQUIRE(out && nseqs >= 0 && d_seq_off, "bad pack arguments");
         *out = nullptr;
         std::vector<int64_t> h(nseqs + 1, 0);
-        GD_HIP(hipMemcpyAsync(h.data(), d_seq_off, (nseqs + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+        d2h(h.data(), d_seq_off, (nseqs + 1) * 8, ctx->stream);
         GD_HIP(hipStreamSynchronize(ctx->stream));
         for (int64_t s = 0; s < nseqs; s++) GD_REQUIRE(h[s + 1] >= h[s], "sequence offsets must be non-decreasing");
         GD_REQUIRE(h[0] >= 0 && h[nseqs] <= total_bytes, "sequence offsets exceed the byte buffer");
@@ -250,8 +250,8 @@ int gdist_sets_upload(gdist_ctx* ctx, int kind, int k, int64_t nsets, const int6
         s->h_off.assign(offsets, offsets + nsets + 1);
         s->off.alloc((nsets + 1) * 8, ctx->stream);
         s->codes.alloc(total * 8 + 8, ctx->stream);
-        GD_HIP(hipMemcpyAsync(s->off.p, offsets, (nsets + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
-        if (total) GD_HIP(hipMemcpyAsync(s->codes.p, codes, total * 8, hipMemcpyHostToDevice, ctx->stream));
+        h2d(s->off.p, offsets, (nsets + 1) * 8, ctx->stream);
+        if (total) h2d(s->codes.p, codes, total * 8, ctx->stream);
         GD_HIP(hipStreamSynchronize(ctx->stream));
         *out = s;
     });
@@ -293,7 +293,7 @@ int gdist_sets_download(const gdist_sets* s, int64_t* offsets, uint64_t* codes) 
         use_device(s->ctx);
         if (offsets) std::memcpy(offsets, s->h_off.data(), (s->nsets + 1) * 8);
         if (codes && s->total)
-            GD_HIP(hipMemcpyAsync(codes, s->codes.p, s->total * 8, hipMemcpyDeviceToHost, s->ctx->stream));
+            d2h(codes, s->codes.p, s->total * 8, s->ctx->stream);
         GD_HIP(hipStreamSynchronize(s->ctx->stream));
     });
 }
@@ -313,6 +313,17 @@ int gdist_sets_bitset_info(const gdist_sets* s, int64_t* dict_size, int64_t* wor
         check_sets(s);
         if (dict_size) *dict_size = s->bits.p ? s->dict_size : -1;
         if (words_per_set) *words_per_set = s->bits.p ? s->W : 0;
+    });
+}
+
+int gdist_sets_bitset_download(const gdist_sets* s, uint64_t* bits) {
+    return guard([&] {
+        check_sets(s);
+        GD_REQUIRE(s->bits.p, "no bitsets built");
+        GD_REQUIRE(bits, "null output");
+        use_device(s->ctx);
+        d2h(bits, s->bits.p, (size_t)s->nsets * s->W * 8, s->ctx->stream);
+        GD_HIP(hipStreamSynchronize(s->ctx->stream));
     });
 }
 
@@ -336,7 +347,7 @@ int gdist_sets_concat(const gdist_sets* a, const gdist_sets* b, gdist_sets** out
         s->h_off = a->h_off;
         for (int64_t i = 1; i <= b->nsets; i++) s->h_off.push_back(b->h_off[i] + a->total);
         s->off.alloc((s->nsets + 1) * 8, ctx->stream);
-        GD_HIP(hipMemcpyAsync(s->off.p, s->h_off.data(), (s->nsets + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+        h2d(s->off.p, s->h_off.data(), (s->nsets + 1) * 8, ctx->stream);
         s->codes.alloc(s->total * es + 8, ctx->stream);
         if (a->total)
             GD_HIP(hipMemcpyAsync(s->codes.p, a->codes.p, a->total * es, hipMemcpyDeviceToDevice, ctx->stream));
@@ -402,12 +413,12 @@ int gdist_intersect_matrix(gdist_ctx* ctx, const gdist_sets* sets, int64_t r0, i
             distance_epilogue(ctx, s, r0, r1, c0, c1, upper, flags, dI, ldI, dD, ldD);
             if (!dev) {
                 hD.resize((size_t)nr * nc);
-                GD_HIP(hipMemcpyAsync(hD.data(), dD, (size_t)nr * nc * 8, hipMemcpyDeviceToHost, st));
+                d2h(hD.data(), dD, (size_t)nr * nc * 8, st);
             }
         }
         if (I_out && !dev) {
             hI.resize((size_t)nr * nc);
-            GD_HIP(hipMemcpyAsync(hI.data(), dI, (size_t)nr * nc * 4, hipMemcpyDeviceToHost, st));
+            d2h(hI.data(), dI, (size_t)nr * nc * 4, st);
         }
         gdist::finish_timing(ctx, true);
         // host outputs: entries excluded by the upper triangle stay untouched
@@ -438,7 +449,7 @@ int gdist_row_query(gdist_ctx* ctx, const gdist_sets* sets, int64_t q, const int
         std::vector<double> d(ncols);
         if (ncols) {
             DevBuf dc(ncols * 8, st), dI(ncols * 4, st), dD(ncols * 8, st);
-            GD_HIP(hipMemcpyAsync(dc.p, cols, ncols * 8, hipMemcpyHostToDevice, st));
+            h2d(dc.p, cols, ncols * 8, st);
             if (s->bits.p) {
                 bitset_row(ctx, s, q, dc.as<int64_t>(), ncols, dI.as<int32_t>());
             } else {
@@ -446,7 +457,7 @@ int gdist_row_query(gdist_ctx* ctx, const gdist_sets* sets, int64_t q, const int
                 sorted_row(ctx, s, q, dc.as<int64_t>(), ncols, dI.as<int32_t>());
             }
             row_epilogue(ctx, s, q, dc.as<int64_t>(), ncols, 0, dI.as<int32_t>(), dD.as<double>());
-            GD_HIP(hipMemcpyAsync(d.data(), dD.p, ncols * 8, hipMemcpyDeviceToHost, st));
+            d2h(d.data(), dD.p, ncols * 8, st);
             GD_HIP(hipStreamSynchronize(st));
         }
         if (D_out) std::memcpy(D_out, d.data(), ncols * 8);
@@ -508,8 +519,8 @@ int gdist_sketch_upload(gdist_ctx* ctx, int width, int64_t nsets, const int64_t*
         s->h_off.assign(offsets, offsets + nsets + 1);
         s->off.alloc((nsets + 1) * 8, ctx->stream);
         s->codes.alloc(total * 4 + 4, ctx->stream);
-        GD_HIP(hipMemcpyAsync(s->off.p, offsets, (nsets + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
-        if (total) GD_HIP(hipMemcpyAsync(s->codes.p, sigs, total * 4, hipMemcpyHostToDevice, ctx->stream));
+        h2d(s->off.p, offsets, (nsets + 1) * 8, ctx->stream);
+        if (total) h2d(s->codes.p, sigs, total * 4, ctx->stream);
         GD_HIP(hipStreamSynchronize(ctx->stream));
         *out = s;
     });
@@ -522,7 +533,7 @@ int gdist_sketch_download(const gdist_sets* sk, int64_t* offsets, int32_t* sigs)
         use_device(sk->ctx);
         if (offsets) std::memcpy(offsets, sk->h_off.data(), (sk->nsets + 1) * 8);
         if (sigs && sk->total)
-            GD_HIP(hipMemcpyAsync(sigs, sk->codes.p, sk->total * 4, hipMemcpyDeviceToHost, sk->ctx->stream));
+            d2h(sigs, sk->codes.p, sk->total * 4, sk->ctx->stream);
         GD_HIP(hipStreamSynchronize(sk->ctx->stream));
     });
 }
@@ -547,6 +558,7 @@ int gdist_sketch_matrix(gdist_ctx* ctx, const gdist_sets* sk, int64_t r0, int64_
             return;
         }
         const bool dev = (flags & GDIST_OUT_DEVICE) != 0;
+        const bool upper = (flags & GDIST_UPPER_TRIANGLE) != 0;
         DevBuf tC, tD;
         int32_t* dC = nullptr;
         double* dD = nullptr;
@@ -557,14 +569,20 @@ int gdist_sketch_matrix(gdist_ctx* ctx, const gdist_sets* sk, int64_t r0, int64_
             ldo = nc;
             if (common_out) { tC.alloc((size_t)nr * nc * 4, st); dC = tC.as<int32_t>(); }
             if (D_out) { tD.alloc((size_t)nr * nc * 8, st); dD = tD.as<double>(); }
-            // untouched (upper-triangle-excluded) entries keep the caller's values
-            if (dC) GD_HIP(hipMemcpy2DAsync(dC, nc * 4, common_out, ld * 4, nc * 4, nr, hipMemcpyHostToDevice, st));
-            if (dD) GD_HIP(hipMemcpy2DAsync(dD, nc * 8, D_out, ld * 8, nc * 8, nr, hipMemcpyHostToDevice, st));
         }
         sketch_matrix(ctx, sk, r0, r1, c0, c1, flags, dC, dD, ldo);
+        std::vector<int32_t> hC;
+        std::vector<double> hD;
         if (!dev) {
-            if (dC) GD_HIP(hipMemcpy2DAsync(common_out, ld * 4, dC, nc * 4, nc * 4, nr, hipMemcpyDeviceToHost, st));
-            if (dD) GD_HIP(hipMemcpy2DAsync(D_out, ld * 8, dD, nc * 8, nc * 8, nr, hipMemcpyDeviceToHost, st));
+            if (dC) { hC.resize((size_t)nr * nc); d2h(hC.data(), dC, (size_t)nr * nc * 4, st); }
+            if (dD) { hD.resize((size_t)nr * nc); d2h(hD.data(), dD, (size_t)nr * nc * 8, st); }
+            // entries excluded by the upper triangle stay untouched
+            for (int64_t a = 0; a < nr; a++)
+                for (int64_t b = 0; b < nc; b++) {
+                    if (upper && c0 + b <= r0 + a) continue;
+                    if (dC) common_out[a * ld + b] = hC[a * nc + b];
+                    if (dD) D_out[a * ld + b] = hD[a * nc + b];
+                }
         }
         gdist::finish_timing(ctx, true);
     });
@@ -617,10 +635,10 @@ int gdist_sets_allgather(gdist_ctx* ctx, const gdist_sets* local, gdist_sets** o
         // 1. (nsets, total) of every rank
         DevBuf mine(16, st), all(16 * R, st);
         int64_t h2[2] = {local->nsets, local->total};
-        GD_HIP(hipMemcpyAsync(mine.p, h2, 16, hipMemcpyHostToDevice, st));
+        h2d(mine.p, h2, 16, st);
         GD_NCCL(ncclAllGather(mine.p, all.p, 2, ncclInt64, ctx->comm, st));
         std::vector<int64_t> hall(2 * R);
-        GD_HIP(hipMemcpyAsync(hall.data(), all.p, 16 * R, hipMemcpyDeviceToHost, st));
+        d2h(hall.data(), all.p, 16 * R, st);
         GD_HIP(hipStreamSynchronize(st));
         int64_t mxs = 0, mxt = 0, ns = 0, nt = 0;
         for (int r = 0; r < R; r++) {
@@ -634,7 +652,7 @@ int gdist_sets_allgather(gdist_ctx* ctx, const gdist_sets* local, gdist_sets** o
         GD_NCCL(ncclAllGather(so.p, ao.p, (mxs + 1), ncclInt64, ctx->comm, st));
         GD_NCCL(ncclAllGather(sc.p, ac.p, mxt * es + 8, ncclUint8, ctx->comm, st));
         std::vector<int64_t> hoff((mxs + 1) * R);
-        GD_HIP(hipMemcpyAsync(hoff.data(), ao.p, (mxs + 1) * 8 * R, hipMemcpyDeviceToHost, st));
+        d2h(hoff.data(), ao.p, (mxs + 1) * 8 * R, st);
         GD_HIP(hipStreamSynchronize(st));
         auto* s = new gdist_sets();
         s->ctx = ctx; s->kind = local->kind; s->k = local->k; s->flags = local->flags; s->width = local->width;
@@ -651,7 +669,7 @@ int gdist_sets_allgather(gdist_ctx* ctx, const gdist_sets* local, gdist_sets** o
             at += rt;
         }
         s->off.alloc((ns + 1) * 8, st);
-        GD_HIP(hipMemcpyAsync(s->off.p, s->h_off.data(), (ns + 1) * 8, hipMemcpyHostToDevice, st));
+        h2d(s->off.p, s->h_off.data(), (ns + 1) * 8, st);
         GD_HIP(hipStreamSynchronize(st));
         *out = s;
     });
@@ -675,9 +693,9 @@ int gdist_sets_allgather_bitsets(gdist_ctx* ctx, const gdist_sets* local, unsign
         hall[0] = local->nsets; hall[1] = sum.n;
         if (R > 1) {
             DevBuf mine(16, st), all(16 * R, st);
-            GD_HIP(hipMemcpyAsync(mine.p, hall.data(), 16, hipMemcpyHostToDevice, st));
+            h2d(mine.p, hall.data(), 16, st);
             GD_NCCL(ncclAllGather(mine.p, all.p, 2, ncclInt64, ctx->comm, st));
-            GD_HIP(hipMemcpyAsync(hall.data(), all.p, 16 * R, hipMemcpyDeviceToHost, st));
+            d2h(hall.data(), all.p, 16 * R, st);
             GD_HIP(hipStreamSynchronize(st));
         }
         int64_t mxs = 0, mxn = 0, N = 0;
@@ -732,9 +750,9 @@ int gdist_sets_allgather_bitsets(gdist_ctx* ctx, const gdist_sets* local, unsign
         for (int64_t i = 0; i < local->nsets; i++) sizes[i] = local->h_off[i + 1] - local->h_off[i];
         if (R > 1) {
             DevBuf ds((mxs + 1) * 8, st), da((mxs + 1) * 8 * R, st);
-            GD_HIP(hipMemcpyAsync(ds.p, sizes.data(), (mxs + 1) * 8, hipMemcpyHostToDevice, st));
+            h2d(ds.p, sizes.data(), (mxs + 1) * 8, st);
             GD_NCCL(ncclAllGather(ds.p, da.p, mxs + 1, ncclInt64, ctx->comm, st));
-            GD_HIP(hipMemcpyAsync(allsz.data(), da.p, (mxs + 1) * 8 * R, hipMemcpyDeviceToHost, st));
+            d2h(allsz.data(), da.p, (mxs + 1) * 8 * R, st);
             GD_HIP(hipStreamSynchronize(st));
         } else {
             allsz = sizes;
@@ -744,7 +762,7 @@ int gdist_sets_allgather_bitsets(gdist_ctx* ctx, const gdist_sets* local, unsign
             for (int64_t i = 0; i < hall[2 * r]; i++) s->h_off.push_back(s->h_off.back() + allsz[(mxs + 1) * r + i]);
         s->total = s->h_off.back();
         s->off.alloc((N + 1) * 8, st);
-        GD_HIP(hipMemcpyAsync(s->off.p, s->h_off.data(), (N + 1) * 8, hipMemcpyHostToDevice, st));
+        h2d(s->off.p, s->h_off.data(), (N + 1) * 8, st);
         s->codes.alloc(8, st);
         s->W = W; s->dict_size = U; s->bits_keep_singletons = keep;
         GD_HIP(hipStreamSynchronize(st));
@@ -758,9 +776,9 @@ int gdist_comm_allreduce_max(gdist_ctx* ctx, double* value) {
         GD_REQUIRE(value, "null value");
         if (!ctx->comm) return;
         DevBuf d(8, ctx->stream);
-        GD_HIP(hipMemcpyAsync(d.p, value, 8, hipMemcpyHostToDevice, ctx->stream));
+        h2d(d.p, value, 8, ctx->stream);
         GD_NCCL(ncclAllReduce(d.p, d.p, 1, ncclFloat64, ncclMax, ctx->comm, ctx->stream));
-        GD_HIP(hipMemcpyAsync(value, d.p, 8, hipMemcpyDeviceToHost, ctx->stream));
+        d2h(value, d.p, 8, ctx->stream);
         GD_HIP(hipStreamSynchronize(ctx->stream));
     });
 }

@@ -41,7 +41,10 @@ void set_last_error(const std::string& msg);
     } while (0)
 
 // ---------------------------------------------------------------------------
-// device buffers: stream-ordered allocations on the context stream.
+// device buffers. Plain hipMalloc/hipFree: with the stream-ordered pool
+// (hipMallocAsync/hipFreeAsync) reused blocks were intermittently read stale
+// by the next kernels on gfx950 / ROCm 7.2; hipFree
+// drains the device before the block can be handed out again.
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
@@ -62,22 +65,31 @@ struct DevBuf {
         release();
         stream = s;
         bytes = n;
-        if (n) GD_HIP(hipMallocAsync(&p, n, s));
+        if (n) GD_HIP(hipMalloc(&p, n));
     }
     void release() noexcept {
-        if (p) (void)hipFreeAsync(p, stream);
+        if (p) { (void)hipStreamSynchronize(stream); (void)hipFree(p); }
         p = nullptr;
         bytes = 0;
     }
     template <class T> T* as() const { return static_cast<T*>(p); }
 };
 
-// H2D copy of a host temporary: a pageable-source hipMemcpyAsync may be
-// executed by the stream after the call returns (behind earlier work), so a
-// host buffer that dies at scope exit must be copied synchronously.
-inline void h2d_sync(void* dst, const void* src, size_t bytes, hipStream_t s) {
+// Host <-> device copies are host-blocking and ordered on the stream: the
+// stream is drained, then a synchronous copy. Pageable-source
+// hipMemcpyAsync was observed (ROCm 7.2, gfx950) to let the next kernel on
+// the stream read partly stale bytes, and its host buffer may die before a
+// deferred copy runs; every host<->device transfer goes through these two.
+inline void h2d(void* dst, const void* src, size_t bytes, hipStream_t s) {
     if (!bytes) return;
-    GD_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
+    GD_HIP(hipStreamSynchronize(s));
+    GD_HIP(hipMemcpyWithStream(dst, src, bytes, hipMemcpyHostToDevice, s));
+    GD_HIP(hipStreamSynchronize(s));
+}
+inline void d2h(void* dst, const void* src, size_t bytes, hipStream_t s) {
+    if (!bytes) return;
+    GD_HIP(hipStreamSynchronize(s));
+    GD_HIP(hipMemcpyWithStream(dst, src, bytes, hipMemcpyDeviceToHost, s));
     GD_HIP(hipStreamSynchronize(s));
 }
 

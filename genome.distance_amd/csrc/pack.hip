@@ -257,6 +257,15 @@ void exclusive_scan_i32_to_i64(gdist_ctx* ctx, const int32_t* in, int64_t* out, 
                                    ctx->stream));
 }
 
+// Debug hook (diagnostics only): host copies of each stage of the first chunk.
+struct PackDebug {
+    uint64_t* k_extract; int32_t* v_extract;
+    uint64_t* k_sort1; int32_t* v_sort1;
+    uint64_t* k_sort2; int32_t* v_sort2;
+    int64_t n;
+};
+static PackDebug* g_pack_debug = nullptr;
+
 // Pack sequences [0, nseq) (device bytes + device/host offsets) into `out`.
 void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_seqs,
                const int64_t* d_seq_off, const std::vector<int64_t>& h_seq_off, gdist_sets* out) {
@@ -295,7 +304,7 @@ void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_se
             bad.as<int>());
         GD_HIP(hipGetLastError());
         int hbad = 0;
-        GD_HIP(hipMemcpyAsync(&hbad, bad.p, sizeof(int), hipMemcpyDeviceToHost, st));
+        d2h(&hbad, bad.p, sizeof(int), st);
         GD_HIP(hipStreamSynchronize(st));
         GD_REQUIRE(!hbad, "sequence holds a character the kmer code cannot represent "
                           "(DNA keep mode: ACGNRTY; protein k>8: A-Z and '*')");
@@ -341,7 +350,7 @@ void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_se
         const int64_t nw = hwo[nc];
         const int64_t n = nw * mult;
         DevBuf cw((nc + 1) * sizeof(int64_t), st);
-        h2d_sync(cw.p, hwo.data(), (nc + 1) * sizeof(int64_t), st);
+        h2d(cw.p, hwo.data(), (nc + 1) * sizeof(int64_t), st);
 
         DevBuf kA(n * 8 + 8, st), kB(n * 8 + 8, st), vA(n * 4 + 4, st), vB(n * 4 + 4, st);
         if (nw > 0) {
@@ -357,10 +366,14 @@ void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_se
         }
         uint64_t* keys = kA.as<uint64_t>(); uint64_t* keys_alt = kB.as<uint64_t>();
         int32_t* ids = vA.as<int32_t>(); int32_t* ids_alt = vB.as<int32_t>();
+        PackDebug* dbg = (s0 == 0) ? g_pack_debug : nullptr;
+        if (dbg) { dbg->n = n; d2h(dbg->k_extract, keys, n * 8, st); d2h(dbg->v_extract, ids, n * 4, st); }
         sort_pairs_u64_i32(ctx, keys, keys_alt, ids, ids_alt, (size_t)n, 0, std::min(64, cbits));
+        if (dbg) { d2h(dbg->k_sort1, keys, n * 8, st); d2h(dbg->v_sort1, ids, n * 4, st); }
         int idbits = 1;
         while ((int64_t(1) << idbits) <= nc) idbits++;
         sort_pairs_i32_u64(ctx, ids, ids_alt, keys, keys_alt, (size_t)n, idbits);
+        if (dbg) { d2h(dbg->k_sort2, keys, n * 8, st); d2h(dbg->v_sort2, ids, n * 4, st); }
 
         DevBuf flag(n * 4 + 4, st), pos(n * 8 + 8, st);
         if (n > 0) {
@@ -373,8 +386,7 @@ void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_se
             ids, pos.as<int64_t>(), flag.as<int32_t>(), n, nc, base, d_off.as<int64_t>() + s0);
         GD_HIP(hipGetLastError());
         std::vector<int64_t> co(nc + 1);
-        GD_HIP(hipMemcpyAsync(co.data(), d_off.as<int64_t>() + s0, (nc + 1) * sizeof(int64_t),
-                              hipMemcpyDeviceToHost, st));
+        d2h(co.data(), d_off.as<int64_t>() + s0, (nc + 1) * sizeof(int64_t), st);
         GD_HIP(hipStreamSynchronize(st));
         const int64_t uniq = co[nc] - base;
         DevBuf cc(uniq * 8 + 8, st);
@@ -413,3 +425,30 @@ void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_se
 }
 
 }  // namespace gdist
+
+// Not part of include/gdist.h: stage dump for diagnostics (tests/diag_*).
+extern "C" int gdist_debug_pack_stages(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* seqs,
+                                       const int64_t* seq_off, int64_t nseqs, uint64_t* k_extract,
+                                       int32_t* v_extract, uint64_t* k_sort1, int32_t* v_sort1, uint64_t* k_sort2,
+                                       int32_t* v_sort2, gdist_sets** out) {
+    using namespace gdist;
+    try {
+        GD_HIP(hipSetDevice(ctx->device));
+        PackDebug dbg{k_extract, v_extract, k_sort1, v_sort1, k_sort2, v_sort2, 0};
+        g_pack_debug = &dbg;
+        std::vector<int64_t> h(seq_off, seq_off + nseqs + 1);
+        DevBuf dseq(h[nseqs] + 1, ctx->stream), doff((nseqs + 1) * 8, ctx->stream);
+        h2d(dseq.p, seqs, h[nseqs], ctx->stream);
+        h2d(doff.p, h.data(), (nseqs + 1) * 8, ctx->stream);
+        auto* s = new gdist_sets();
+        s->ctx = ctx;
+        pack_sets(ctx, kind, k, flags, dseq.as<char>(), doff.as<int64_t>(), h, s);
+        g_pack_debug = nullptr;
+        *out = s;
+        return 0;
+    } catch (const Error& e) {
+        g_pack_debug = nullptr;
+        set_last_error(e.what());
+        return e.code;
+    }
+}

@@ -231,7 +231,7 @@ void sketch_build(gdist_ctx* ctx, const gdist_sets* s, int width, gdist_sets* ou
                                                                        ns, us.as<int64_t>());
         GD_HIP(hipGetLastError());
         std::vector<int64_t> hus(ns + 1);
-        GD_HIP(hipMemcpyAsync(hus.data(), us.p, (ns + 1) * 8, hipMemcpyDeviceToHost, st));
+        d2h(hus.data(), us.p, (ns + 1) * 8, st);
         GD_HIP(hipStreamSynchronize(st));
         std::vector<int64_t> loc(ns + 1, 0);
         for (int64_t t = 0; t < ns; t++) {
@@ -240,7 +240,7 @@ void sketch_build(gdist_ctx* ctx, const gdist_sets* s, int width, gdist_sets* ou
             h_out[s0 + t + 1] = h_out[s0 + t] + cnt;
         }
         DevBuf dloc((ns + 1) * 8, st), sig(loc[ns] * 4 + 4, st);
-        h2d_sync(dloc.p, loc.data(), (ns + 1) * 8, st);
+        h2d(dloc.p, loc.data(), (ns + 1) * 8, st);
         if (n) {
             emit_sig_kernel<<<grid_for(n), 256, 0, st>>>(keys, flag.as<int32_t>(), pos.as<int64_t>(), us.as<int64_t>(),
                                                          dloc.as<int64_t>(), n, width, sig.as<int32_t>());
@@ -257,7 +257,7 @@ void sketch_build(gdist_ctx* ctx, const gdist_sets* s, int width, gdist_sets* ou
     out->nsets = nsets;
     out->total = h_out[nsets];
     out->h_off = h_out;
-    h2d_sync(d_out_off.p, h_out.data(), (nsets + 1) * 8, st);
+    h2d(d_out_off.p, h_out.data(), (nsets + 1) * 8, st);
     out->off = std::move(d_out_off);
     out->codes.alloc(out->total * 4 + 4, st);
     int64_t at = 0;

@@ -176,12 +176,12 @@ void build_segments(gdist_ctx* ctx, gdist_sets* s) {
         std::vector<int64_t> idx(want);
         for (int64_t t = 0; t < want; t++) idx[t] = (int64_t)((double)(t + 0.5) * (double)s->total / (double)want);
         DevBuf di(want * 8, st), dv(want * 8, st);
-        h2d_sync(di.p, idx.data(), want * 8, st);
+        h2d(di.p, idx.data(), want * 8, st);
         gather_kernel<<<(int)ceil_div(want, 256), 256, 0, st>>>(s->codes.as<uint64_t>(), di.as<int64_t>(), want,
                                                                 dv.as<uint64_t>());
         GD_HIP(hipGetLastError());
         std::vector<uint64_t> v(want);
-        GD_HIP(hipMemcpyAsync(v.data(), dv.p, want * 8, hipMemcpyDeviceToHost, st));
+        d2h(v.data(), dv.p, want * 8, st);
         GD_HIP(hipStreamSynchronize(st));
         std::sort(v.begin(), v.end());
         for (int t = 1; t < nseg; t++) {
@@ -194,7 +194,7 @@ void build_segments(gdist_ctx* ctx, gdist_sets* s) {
     }
     DevBuf dsplit(split.size() * 8 + 8, st);
     if (!split.empty())
-        h2d_sync(dsplit.p, split.data(), split.size() * 8, st);
+        h2d(dsplit.p, split.data(), split.size() * 8, st);
     const int64_t n = s->nsets * (int64_t)(nseg + 1);
     s->segoff.alloc(n * 8 + 8, st);
     if (n)
@@ -202,7 +202,7 @@ void build_segments(gdist_ctx* ctx, gdist_sets* s) {
                                                             dsplit.as<uint64_t>(), nseg, s->segoff.as<int64_t>());
     GD_HIP(hipGetLastError());
     std::vector<int64_t> h(n);
-    if (n) GD_HIP(hipMemcpyAsync(h.data(), s->segoff.p, n * 8, hipMemcpyDeviceToHost, st));
+    if (n) d2h(h.data(), s->segoff.p, n * 8, st);
     GD_HIP(hipStreamSynchronize(st));
     int64_t mx = 0;
     for (int64_t e = 0; e < s->nsets; e++)
@@ -227,7 +227,7 @@ static void launch_join(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t
     if (nunits == 0) return;
     GD_REQUIRE(nunits < (int64_t(1) << 31), "sorted matrix grid too large");
     DevBuf dp((ncb + 1) * 8, st);
-    h2d_sync(dp.p, prefix.data(), (ncb + 1) * 8, st);
+    h2d(dp.p, prefix.data(), (ncb + 1) * 8, st);
     GD_HIP(hipEventRecord(ctx->ev_k0, st));
     sorted_join_kernel<<<(unsigned)nunits, NTJ, 0, st>>>(s->codes.as<uint64_t>(), s->segoff.as<int64_t>(), s->nseg,
                                                          dp.as<int64_t>(), ncb, nunits, r0, r1, c0, c1, d_colidx,

@@ -215,6 +215,14 @@ class KmerSets(_Handle):
         L.check(L.lib.gdist_sets_build_bitsets(self.h, L.BITSET_KEEP_SINGLETONS if keep_singletons else 0))
         return self.bitset_info()
 
+    def bitsets(self) -> np.ndarray:
+        """The dictionary-rank bitsets, (nsets, W) uint64."""
+        n = len(self)
+        _, w = self.bitset_info()
+        out = np.zeros((n, max(w, 1)), dtype=np.uint64)
+        L.check(L.lib.gdist_sets_bitset_download(self.h, L.ptr(out, C.c_uint64)))
+        return out[:, :w]
+
     def bitset_info(self) -> tuple[int, int]:
         d, w = C.c_int64(), C.c_int64()
         L.check(L.lib.gdist_sets_bitset_info(self.h, C.byref(d), C.byref(w)))

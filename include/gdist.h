@@ -138,6 +138,8 @@ int  gdist_sets_download(const gdist_sets* sets, int64_t* offsets, uint64_t* cod
 /* Build the dictionary-rank bitset representation (kept with the sets). */
 int  gdist_sets_build_bitsets(gdist_sets* sets, unsigned flags);
 int  gdist_sets_bitset_info(const gdist_sets* sets, int64_t* dict_size, int64_t* words_per_set);
+/* Copy the bitsets (nsets x words_per_set uint64, row-major) to the host. */
+int  gdist_sets_bitset_download(const gdist_sets* sets, uint64_t* bits);
 /* Concatenate two collections (e.g. base genomes + comparison genomes). */
 int  gdist_sets_concat(const gdist_sets* a, const gdist_sets* b, gdist_sets** out);
 
