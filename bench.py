@@ -36,7 +36,12 @@ sys.path.insert(0, os.path.join(ROOT, "genome.distance_amd"))
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0               # MI355X_MICROARCH.md chip table (spec)
-VALU_WORDPAIR_PEAK = 256 * 4 * 32 * 2.4e9 / 4.0   # 64-bit word pairs/s: 4 VALU ops each
+# VALU ceiling of the bitset inner step, MEASURED (scripts/microbench/valu_popc.hip,
+# profiles/r01/valu_microbench.txt): an interleaved v_and_b32 + v_bcnt_u32_b32 stream
+# issues at most 6.17e11 wave-instructions/s chip-wide (v_bcnt is half rate:
+# 5.7e11 alone vs 1.06e12 for v_and). One 64-bit word pair = 4 wave-lane
+# instructions (2 and + 2 bcnt) -> 6.17e11 * 64 / 4 word pairs/s.
+VALU_WORDPAIR_PEAK = 6.17e11 * 64 / 4.0
 
 CONFIGS = {
     # name: (n_genomes, length, p_max, kind, k, method, cfg index for the seed)
@@ -199,7 +204,8 @@ def main():
             wp = pairs_rank * width_words / (k_avg_ms * 1e-3) if k_avg_ms > 0 else 0.0
             roof["valu"] = {"achieved": round(wp / 1e12, 3), "peak": round(VALU_WORDPAIR_PEAK / 1e12, 3),
                             "unit": "T word-pairs/s", "frac": round(wp / VALU_WORDPAIR_PEAK, 4),
-                            "note": "2x v_and_b32 + 2x v_bcnt_u32_b32 per 64-bit word pair"}
+                            "note": "2x v_and_b32 + 2x v_bcnt_u32_b32 per 64-bit word pair; peak = measured "
+                                    "and+bcnt issue ceiling (profiles/r01/valu_microbench.txt)"}
         # ---------------------------------------------------------------- CPU baseline
         cpu = None
         cpu_opt = None

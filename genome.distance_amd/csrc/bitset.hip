@@ -216,6 +216,139 @@ __global__ __launch_bounds__(NT, 2) void bitset_tile_kernel(
     }
 }
 
+// ---- v2: LDS-DMA double buffering, split-major XCD-aware order -------------
+// 256 threads, 128×128 tile, 8×8 counts per thread as in v1, but
+//  * chunks of KC2 = 8 words are moved HBM/L2 -> LDS by global_load_lds_dwordx4
+//    (no register staging, so ≤ 128 VGPRs and 4 waves per SIMD), double
+//    buffered: chunk k+1 is in flight while chunk k is computed;
+//  * the LDS image swizzle (slot q of row g at q ^ ((g >> 2) & 3)) is applied on
+//    the DMA source address (the destination of one DMA instruction is linear);
+//  * blocks are ordered split-major and remapped so one XCD runs consecutive
+//    units: concurrently resident blocks work on the same K-range of every set,
+//    which stays in the L2 / Infinity Cache while all tiles consume it.
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_void_t;
+
+constexpr int KC2 = 8;                        // words per chunk
+constexpr int ROW2 = KC2 * 8;                 // 64 B per set row
+constexpr int OPB2 = BT * ROW2;               // 8 KiB per operand per stage
+constexpr int STAGE2 = 2 * OPB2;              // A + B
+
+__device__ __forceinline__ int lds_off2(int g, int q) { return g * ROW2 + ((q ^ ((g >> 2) & 3)) << 4); }
+
+// one operand's chunk: 8 DMA instructions of 1 KiB (16 rows), 2 per wave
+__device__ __forceinline__ void dma_chunk(const unsigned long long* __restrict__ bits, int64_t W, int64_t set0,
+                                          int64_t lim, int64_t kc, unsigned char* lds_op, int wave, int lane) {
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+        const int rbase = (wave * 2 + i) * 16;
+        const int g = rbase + (lane >> 2);
+        const int p = lane & 3;
+        const int q = p ^ ((g >> 2) & 3);
+        int64_t set = set0 + g;
+        set = set < lim ? set : lim - 1;              // clamp: rows past the range are masked at the end
+        const unsigned long long* src = bits + set * W + kc * KC2 + q * 2;
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(lds_op + rbase * ROW2), 16, 0, 0);
+    }
+}
+
+// ORDER 0: per column fragment, the 4 dwords of one pair back to back (a
+// dependent chain per accumulator). ORDER 1: two column fragments at once,
+// dword-outer, so consecutive v_and/v_bcnt pairs belong to 16 different
+// accumulators and no instruction waits on its predecessor.
+template <int ORDER>
+__global__ __launch_bounds__(NT, 4) void bitset_tile_kernel2(
+    const unsigned long long* __restrict__ bits, int64_t W, const int2* __restrict__ tiles, int ntiles, int splits,
+    int64_t nchunks, int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I,
+    int64_t ldI) {
+    __shared__ __attribute__((aligned(16))) unsigned char lds[2 * STAGE2];
+
+    // XCD-aware bijective remap, then split-major unit order
+    const int64_t G = gridDim.x, blk = blockIdx.x;
+    const int64_t xcd = blk & 7, kq = blk >> 3, qg = G >> 3, rem = G & 7;
+    const int64_t u = xcd * qg + (xcd < rem ? xcd : rem) + kq;
+    const int split = (int)(u / ntiles);
+    const int tile = (int)(u - (int64_t)split * ntiles);
+    const int2 t = tiles[tile];
+    if (split >= splits || t.x < 0 || t.y < 0) return;
+    const int64_t row0 = r0 + (int64_t)t.x * BT;
+    const int64_t col0 = c0 + (int64_t)t.y * BT;
+    const int64_t kc_per = ceil_div(nchunks, splits);
+    const int64_t kc0 = (int64_t)split * kc_per;
+    const int64_t kc1 = kc0 + kc_per < nchunks ? kc0 + kc_per : nchunks;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tx = tid & 15, ty = tid >> 4;
+
+    uint32_t acc[8][8];
+#pragma unroll
+    for (int r = 0; r < 8; r++)
+#pragma unroll
+        for (int c = 0; c < 8; c++) acc[r][c] = 0;
+
+    if (kc0 < kc1) {
+        dma_chunk(bits, W, row0, r1, kc0, lds, wave, lane);
+        dma_chunk(bits, W, col0, c1, kc0, lds + OPB2, wave, lane);
+    }
+    for (int64_t kc = kc0; kc < kc1; kc++) {
+        const int st = (int)((kc - kc0) & 1);
+        unsigned char* A = lds + st * STAGE2;
+        unsigned char* B = A + OPB2;
+        if (kc + 1 < kc1) {
+            unsigned char* An = lds + (st ^ 1) * STAGE2;
+            dma_chunk(bits, W, row0, r1, kc + 1, An, wave, lane);
+            dma_chunk(bits, W, col0, c1, kc + 1, An + OPB2, wave, lane);
+            asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");   // chunk kc landed everywhere
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+#pragma unroll 1
+        for (int q = 0; q < KC2 / 2; q++) {
+            uint4 a[8];
+#pragma unroll
+            for (int r = 0; r < 8; r++) a[r] = *reinterpret_cast<const uint4*>(A + lds_off2(ty + 16 * r, q));
+            if (ORDER == 0) {
+#pragma unroll
+                for (int c = 0; c < 8; c++) {
+                    const uint4 bv = *reinterpret_cast<const uint4*>(B + lds_off2(tx + 16 * c, q));
+#pragma unroll
+                    for (int r = 0; r < 8; r++) acc[r][c] = and_popc(a[r], bv, acc[r][c]);
+                }
+            } else {
+#pragma unroll
+                for (int c = 0; c < 8; c += 2) {
+                    const uint4 b0 = *reinterpret_cast<const uint4*>(B + lds_off2(tx + 16 * c, q));
+                    const uint4 b1 = *reinterpret_cast<const uint4*>(B + lds_off2(tx + 16 * (c + 1), q));
+                    const uint32_t bw0[4] = {b0.x, b0.y, b0.z, b0.w};
+                    const uint32_t bw1[4] = {b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+                    for (int d = 0; d < 4; d++) {
+#pragma unroll
+                        for (int r = 0; r < 8; r++) {
+                            const uint32_t ad = d == 0 ? a[r].x : d == 1 ? a[r].y : d == 2 ? a[r].z : a[r].w;
+                            acc[r][c] = bcnt_acc(ad & bw0[d], acc[r][c]);
+                            acc[r][c + 1] = bcnt_acc(ad & bw1[d], acc[r][c + 1]);
+                        }
+                    }
+                }
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // stage free for the next DMA
+    }
+
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+        const int64_t i = row0 + ty + 16 * r;
+        if (i >= r1) continue;
+#pragma unroll
+        for (int c = 0; c < 8; c++) {
+            const int64_t j = col0 + tx + 16 * c;
+            if (j >= c1 || (upper && j <= i)) continue;
+            if (acc[r][c]) atomicAdd(I + (i - r0) * ldI + (j - c0), (int32_t)acc[r][c]);
+        }
+    }
+}
+
 // Self pairs: |A ∩ A| = |A|. The pruned dictionary drops kmers held by one
 // set only, so the bitset count of a self pair misses them; take |A|.
 __global__ void self_pairs_kernel(const int64_t* __restrict__ off, int64_t lo, int64_t hi, int64_t r0, int64_t c0,
@@ -524,9 +657,22 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     h2d(dt.p, tiles.data(), tiles.size() * sizeof(int2), st);
     const int64_t grid = (int64_t)tiles.size() * splits;
     GD_REQUIRE(grid < (int64_t(1) << 31), "bitset matrix grid too large");
+    const char* ev = getenv("GDIST_BITSET_KERNEL");   // A/B selection (default: 3)
+    const int variant = ev ? atoi(ev) : 3;
     GD_HIP(hipEventRecord(ctx->ev_k0, st));
-    bitset_tile_kernel<<<(unsigned)grid, NT, 0, st>>>(s->bits.as<unsigned long long>(), s->W, dt.as<int2>(),
-                                                       splits, nchunks, r0, r1, c0, c1, upper ? 1 : 0, d_I, ldI);
+    if (variant == 1) {
+        bitset_tile_kernel<<<(unsigned)grid, NT, 0, st>>>(s->bits.as<unsigned long long>(), s->W, dt.as<int2>(),
+                                                           splits, nchunks, r0, r1, c0, c1, upper ? 1 : 0, d_I, ldI);
+    } else {
+        const int64_t nch2 = s->W / KC2;
+        const int64_t target2 = (int64_t)ctx->cus * 16;
+        const int sp2 = (int)std::max<int64_t>(1, std::min<int64_t>(nch2, ceil_div(target2, (int64_t)tiles.size())));
+        const int64_t grid2 = (int64_t)tiles.size() * sp2;
+        GD_REQUIRE(grid2 < (int64_t(1) << 31), "bitset matrix grid too large");
+        auto k2 = variant == 2 ? bitset_tile_kernel2<0> : bitset_tile_kernel2<1>;
+        k2<<<(unsigned)grid2, NT, 0, st>>>(s->bits.as<unsigned long long>(), s->W, dt.as<int2>(), (int)tiles.size(),
+                                           sp2, nch2, r0, r1, c0, c1, upper ? 1 : 0, d_I, ldI);
+    }
     GD_HIP(hipGetLastError());
     GD_HIP(hipEventRecord(ctx->ev_k1, st));
     ctx->last.launches = 1;
