@@ -73,11 +73,6 @@ __global__ void run_totals_kernel(const int64_t* __restrict__ start, int64_t nru
     total[r] = (uint32_t)(t > 0xFFFFFFFFll ? 0xFFFFFFFFll : t);
 }
 
-__global__ void dict_flag_kernel(const uint32_t* __restrict__ cnt, int64_t n, int keep, int32_t* __restrict__ flag) {
-    int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-        flag[i] = (keep || cnt[i] >= 2) ? 1 : 0;
-}
 
 __global__ void compact_u64_kernel(const uint64_t* __restrict__ v, const int32_t* __restrict__ flag,
                                    const int64_t* __restrict__ pos, int64_t n, uint64_t* __restrict__ out) {
@@ -91,9 +86,11 @@ __global__ void widen_u32_kernel(const uint32_t* __restrict__ in, int64_t n, int
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) out[i] = in[i];
 }
 
-// rank of each run's code in the dictionary (or -1)
+// rank of each run's code: r >= 0 in the dense dictionary, -(r + 2) in the
+// rare dictionary, -1 in neither
 __global__ void run_rank_kernel(const uint64_t* __restrict__ keys, const int64_t* __restrict__ start, int64_t nruns,
-                                const uint64_t* __restrict__ dict, int64_t U, int64_t* __restrict__ rank) {
+                                const uint64_t* __restrict__ dict, int64_t U, const uint64_t* __restrict__ rare,
+                                int64_t Ur, int64_t* __restrict__ rank) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nruns) return;
     const uint64_t k = keys[start[r]];
@@ -102,18 +99,111 @@ __global__ void run_rank_kernel(const uint64_t* __restrict__ keys, const int64_t
         int64_t mid = (lo + hi) >> 1;
         if (dict[mid] < k) lo = mid + 1; else hi = mid;
     }
-    rank[r] = (lo < U && dict[lo] == k) ? lo : -1;
+    if (lo < U && dict[lo] == k) { rank[r] = lo; return; }
+    lo = 0; hi = Ur;
+    while (lo < hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if (rare[mid] < k) lo = mid + 1; else hi = mid;
+    }
+    rank[r] = (lo < Ur && rare[lo] == k) ? -(lo + 2) : -1;
 }
 
+// dense ranks -> bits; rare ranks -> (rare rank << 32 | global set id) records
 __global__ void scatter_bits_kernel(const int32_t* __restrict__ ids, const int32_t* __restrict__ flag,
                                     const int64_t* __restrict__ pos, const int64_t* __restrict__ rank, int64_t n,
-                                    int64_t W, unsigned long long* __restrict__ bits) {
+                                    int64_t W, unsigned long long* __restrict__ bits, int64_t id_base,
+                                    unsigned long long* __restrict__ rare_out, unsigned long long* __restrict__ rare_cnt,
+                                    int64_t rare_cap) {
     int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const int64_t run = pos[i] + flag[i] - 1;       // inclusive run index
         const int64_t r = rank[run];
-        if (r < 0) continue;
-        atomicOr(bits + (int64_t)ids[i] * W + (r >> 6), 1ull << (r & 63));
+        if (r >= 0) {
+            atomicOr(bits + (int64_t)ids[i] * W + (r >> 6), 1ull << (r & 63));
+        } else if (r <= -2) {
+            const unsigned long long slot = atomicAdd(rare_cnt, 1ull);
+            if ((int64_t)slot < rare_cap)
+                rare_out[slot] = ((unsigned long long)(-r - 2) << 32) | (unsigned long long)(uint32_t)(ids[i] + id_base);
+        }
+    }
+}
+
+// posting offsets: first record of each rare rank
+__global__ void posting_offsets_kernel(const uint64_t* __restrict__ recs, int64_t n, int64_t nposts,
+                                       int64_t* __restrict__ off) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p > nposts) return;
+    const uint64_t v = (uint64_t)p << 32;
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if (recs[mid] < v) lo = mid + 1; else hi = mid;
+    }
+    off[p] = lo;
+}
+
+__global__ void posting_sets_kernel(const uint64_t* __restrict__ recs, int64_t n, uint32_t* __restrict__ sets) {
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) sets[i] = (uint32_t)recs[i];
+}
+
+// Rare tier: every posting list (ascending set ids) adds 1 to each of its
+// m(m-1)/2 pairs that fall in the region.
+__global__ __launch_bounds__(256) void rare_pairs_kernel(const int64_t* __restrict__ poff,
+                                                         const uint32_t* __restrict__ psets, int64_t nposts,
+                                                         int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper,
+                                                         int32_t* __restrict__ I, int64_t ldI) {
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < nposts; p += stride) {
+        const int64_t b = poff[p], e = poff[p + 1];
+        for (int64_t x = b; x < e; x++) {
+            const int64_t s = psets[x];
+            const bool srow = s >= r0 && s < r1, scol = s >= c0 && s < c1;
+            if (!srow && (upper || !scol)) continue;
+            for (int64_t y = x + 1; y < e; y++) {
+                const int64_t t = psets[y];                  // t > s
+                if (srow && t >= c0 && t < c1) atomicAdd(I + (s - r0) * ldI + (t - c0), 1);
+                if (!upper && scol && t >= r0 && t < r1) atomicAdd(I + (t - r0) * ldI + (s - c0), 1);
+            }
+        }
+    }
+}
+
+// Rare tier for one query row: colpos[set] = column position or -1.
+__global__ __launch_bounds__(256) void rare_row_kernel(const int64_t* __restrict__ poff,
+                                                       const uint32_t* __restrict__ psets, int64_t nposts, int64_t q,
+                                                       const int32_t* __restrict__ colpos, int32_t* __restrict__ I) {
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < nposts; p += stride) {
+        const int64_t b = poff[p], e = poff[p + 1];
+        bool has = false;
+        for (int64_t x = b; x < e; x++) has |= (psets[x] == (uint32_t)q);
+        if (!has) continue;
+        for (int64_t x = b; x < e; x++) {
+            const int64_t t = psets[x];
+            if (t == q) continue;
+            const int32_t c = colpos[t];
+            if (c >= 0) atomicAdd(I + c, 1);
+        }
+    }
+}
+
+__global__ void colpos_kernel(const int64_t* __restrict__ cols, int64_t ncols, int32_t* __restrict__ colpos) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c < ncols) colpos[cols[c]] = (int32_t)c;
+}
+
+// rare-tier mass: count of records each rare dictionary entry will produce
+__global__ void rare_flag_kernel(const uint32_t* __restrict__ cnt, int64_t n, int64_t T, int keep,
+                                 int32_t* __restrict__ dflag, int32_t* __restrict__ rflag, int64_t* __restrict__ rmass) {
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint32_t c = cnt[i];
+        const bool dense = keep || (c >= 2 && (int64_t)c >= T);
+        const bool rare = !keep && c >= 2 && (int64_t)c < T;
+        dflag[i] = dense ? 1 : 0;
+        rflag[i] = rare ? 1 : 0;
+        rmass[i] = rare ? (int64_t)c : 0;
     }
 }
 
@@ -426,6 +516,15 @@ void bitset_row(gdist_ctx* ctx, const gdist_sets* s, int64_t q, const int64_t* d
     bitset_row_kernel<<<(unsigned)ceil_div(ncols, 4), 256, 0, ctx->stream>>>(s->bits.as<unsigned long long>(), s->W,
                                                                              q, d_cols, ncols, d_I);
     GD_HIP(hipGetLastError());
+    if (s->n_rare > 0) {
+        DevBuf colpos(s->nsets * 4 + 4, ctx->stream);
+        GD_HIP(hipMemsetAsync(colpos.p, 0xFF, s->nsets * 4, ctx->stream));
+        colpos_kernel<<<(unsigned)ceil_div(ncols, 256), 256, 0, ctx->stream>>>(d_cols, ncols, colpos.as<int32_t>());
+        rare_row_kernel<<<grid_for(s->n_rare, 256, 256 * 64), 256, 0, ctx->stream>>>(
+            s->post_off.as<int64_t>(), s->post_sets.as<uint32_t>(), s->n_rare, q, colpos.as<int32_t>(), d_I);
+        GD_HIP(hipGetLastError());
+        GD_HIP(hipStreamSynchronize(ctx->stream));
+    }
 }
 
 void row_epilogue(gdist_ctx* ctx, const gdist_sets* s, int64_t q, const int64_t* d_cols, int64_t ncols,
@@ -545,8 +644,11 @@ void local_summary(gdist_ctx* ctx, const gdist_sets* s, Summary& out) {
     merge_parts(ctx, parts, out);
 }
 
-// dictionary = codes of the merged summary with count >= 2 (or all)
-void dictionary_from(gdist_ctx* ctx, const std::vector<SummaryView>& parts, bool keep, DevBuf& dict, int64_t& U) {
+// Dictionary tiers from merged summaries: dense = codes held by >= T sets
+// (all codes with keep_singletons), rare = codes held by 2..T-1 sets.
+// rare_mass = number of (code, set) records the rare tier will produce.
+void dictionary_from(gdist_ctx* ctx, const std::vector<SummaryView>& parts, bool keep, int64_t T, DevBuf& dict,
+                     int64_t& U, DevBuf& rare, int64_t& Ur, int64_t& rare_mass) {
     hipStream_t st = ctx->stream;
     Summary all;
     SummaryView m = parts.size() == 1 ? parts[0] : SummaryView{nullptr, nullptr, 0};
@@ -555,81 +657,175 @@ void dictionary_from(gdist_ctx* ctx, const std::vector<SummaryView>& parts, bool
         m = {all.codes.as<uint64_t>(), all.counts.as<uint32_t>(), all.n};
     }
     const int64_t n = m.n;
-    DevBuf flag(n * 4 + 4, st), pos(n * 8 + 8, st);
-    U = 0;
+    U = Ur = rare_mass = 0;
+    DevBuf df(n * 4 + 4, st), rf(n * 4 + 4, st), dpos(n * 8 + 8, st), rpos(n * 8 + 8, st), mass(n * 8 + 8, st),
+        cmass(n * 8 + 8, st);
     if (n) {
-        dict_flag_kernel<<<grid_for(n), 256, 0, st>>>(m.counts, n, keep ? 1 : 0, flag.as<int32_t>());
+        rare_flag_kernel<<<grid_for(n), 256, 0, st>>>(m.counts, n, T, keep ? 1 : 0, df.as<int32_t>(), rf.as<int32_t>(),
+                                                      mass.as<int64_t>());
         GD_HIP(hipGetLastError());
-        exclusive_scan_i32_to_i64(ctx, flag.as<int32_t>(), pos.as<int64_t>(), (size_t)n);
-        int64_t last = 0;
-        int32_t lf = 0;
-        d2h(&last, pos.as<int64_t>() + n - 1, 8, st);
-        d2h(&lf, flag.as<int32_t>() + n - 1, 4, st);
-        GD_HIP(hipStreamSynchronize(st));
-        U = last + lf;
+        exclusive_scan_i32_to_i64(ctx, df.as<int32_t>(), dpos.as<int64_t>(), (size_t)n);
+        exclusive_scan_i32_to_i64(ctx, rf.as<int32_t>(), rpos.as<int64_t>(), (size_t)n);
+        exclusive_scan_i64(ctx, mass.as<int64_t>(), cmass.as<int64_t>(), (size_t)n);
+        int64_t h[6];
+        int32_t hf[2];
+        d2h(&h[0], dpos.as<int64_t>() + n - 1, 8, st);
+        d2h(&h[1], rpos.as<int64_t>() + n - 1, 8, st);
+        d2h(&h[2], cmass.as<int64_t>() + n - 1, 8, st);
+        d2h(&h[3], mass.as<int64_t>() + n - 1, 8, st);
+        d2h(&hf[0], df.as<int32_t>() + n - 1, 4, st);
+        d2h(&hf[1], rf.as<int32_t>() + n - 1, 4, st);
+        U = h[0] + hf[0];
+        Ur = h[1] + hf[1];
+        rare_mass = h[2] + h[3];
     }
     dict.alloc(U * 8 + 8, st);
+    rare.alloc(Ur * 8 + 8, st);
     if (n) {
-        compact_u64_kernel<<<grid_for(n), 256, 0, st>>>(m.codes, flag.as<int32_t>(), pos.as<int64_t>(), n,
+        compact_u64_kernel<<<grid_for(n), 256, 0, st>>>(m.codes, df.as<int32_t>(), dpos.as<int64_t>(), n,
                                                         dict.as<uint64_t>());
+        compact_u64_kernel<<<grid_for(n), 256, 0, st>>>(m.codes, rf.as<int32_t>(), rpos.as<int64_t>(), n,
+                                                        rare.as<uint64_t>());
         GD_HIP(hipGetLastError());
     }
     GD_HIP(hipStreamSynchronize(st));
+}
+
+namespace {
+__global__ void local_mass_kernel(const uint64_t* __restrict__ codes, const uint32_t* __restrict__ cnt, int64_t n,
+                                  const uint64_t* __restrict__ rare, int64_t Ur, unsigned long long* __restrict__ out) {
+    unsigned long long acc = 0;
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t k = codes[i];
+        int64_t lo = 0, hi = Ur;
+        while (lo < hi) {
+            int64_t mid = (lo + hi) >> 1;
+            if (rare[mid] < k) lo = mid + 1; else hi = mid;
+        }
+        if (lo < Ur && rare[lo] == k) acc += cnt[i];
+    }
+    if (acc) atomicAdd(out, acc);
+}
+}  // namespace
+
+// records the local sets contribute to the rare tier (local counts of rare codes)
+int64_t local_rare_mass(gdist_ctx* ctx, const Summary& local, const uint64_t* rare, int64_t Ur) {
+    hipStream_t st = ctx->stream;
+    if (Ur == 0 || local.n == 0) return 0;
+    DevBuf c(8, st);
+    GD_HIP(hipMemsetAsync(c.p, 0, 8, st));
+    local_mass_kernel<<<grid_for(local.n), 256, 0, st>>>(local.codes.as<uint64_t>(), local.counts.as<uint32_t>(),
+                                                         local.n, rare, Ur, c.as<unsigned long long>());
+    GD_HIP(hipGetLastError());
+    int64_t h = 0;
+    d2h(&h, c.p, 8, st);
+    return h;
 }
 
 int64_t bitset_words(int64_t dict_size) {
     return std::max<int64_t>(KC, ceil_div(ceil_div(dict_size, 64), KC) * KC);
 }
 
-// bits of sets [0, nsets) against a dictionary (chunked pairs sort, run ranks, scatter)
+int64_t auto_rare_threshold(int64_t nsets) {
+    // A dense dictionary entry costs one bit column over all N^2/2 pairs; a
+    // rare entry held by m sets costs m(m-1)/2 pair increments. Measured
+    // crossover on MI355X ~ N/80 (tunable: GDIST_RARE_T).
+    if (const char* e = getenv("GDIST_RARE_T")) return atoll(e);
+    return std::max<int64_t>(2, nsets / 80);
+}
+
+// bits of sets [0, nsets) against the dense dictionary (chunked pairs sort,
+// run ranks, scatter); rare-tier records appended to rare_out (capacity cap)
 void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_t U, int64_t W,
-               unsigned long long* bits) {
+               unsigned long long* bits, const uint64_t* rare, int64_t Ur, int64_t id_base,
+               unsigned long long* rare_out, int64_t rare_cap, int64_t* rare_written) {
     hipStream_t st = ctx->stream;
     const int cbits = std::min(64, code_bits(s->kind, s->k, s->flags));
     GD_HIP(hipMemsetAsync(bits, 0, (size_t)s->nsets * W * 8, st));
-    if (U == 0) return;
-    int64_t s0 = 0;
-    while (s0 < s->nsets) {
-        int64_t s1 = s0 + 1;
-        while (s1 < s->nsets && s->h_off[s1 + 1] - s->h_off[s0] <= kBitsChunk) s1++;
-        const int64_t b = s->h_off[s0], n = s->h_off[s1] - b;
-        if (n) {
-            DevBuf kA(n * 8, st), kB(n * 8, st), vA(n * 4, st), vB(n * 4, st);
-            GD_HIP(hipMemcpyAsync(kA.p, s->codes.as<uint64_t>() + b, n * 8, hipMemcpyDeviceToDevice, st));
-            set_ids_kernel<<<grid_for(n), 256, 0, st>>>(s->off.as<int64_t>(), s0, s1, vA.as<int32_t>());
-            GD_HIP(hipGetLastError());
-            uint64_t* keys = kA.as<uint64_t>(); uint64_t* kalt = kB.as<uint64_t>();
-            int32_t* ids = vA.as<int32_t>(); int32_t* ialt = vB.as<int32_t>();
-            sort_pairs_u64_i32(ctx, keys, kalt, ids, ialt, (size_t)n, 0, cbits);
-            DevBuf flag, pos, uniq, start;
-            int64_t nruns = 0;
-            runs_of(ctx, keys, n, flag, pos, uniq, start, nruns);
-            DevBuf rank(nruns * 8 + 8, st);
-            run_rank_kernel<<<(int)ceil_div(nruns, 256), 256, 0, st>>>(keys, start.as<int64_t>(), nruns, dict, U,
-                                                                       rank.as<int64_t>());
-            GD_HIP(hipGetLastError());
-            scatter_bits_kernel<<<grid_for(n), 256, 0, st>>>(ids, flag.as<int32_t>(), pos.as<int64_t>(),
-                                                             rank.as<int64_t>(), n, W, bits);
-            GD_HIP(hipGetLastError());
-            GD_HIP(hipStreamSynchronize(st));
+    DevBuf rcnt(8, st);
+    GD_HIP(hipMemsetAsync(rcnt.p, 0, 8, st));
+    if (U + Ur > 0) {
+        int64_t s0 = 0;
+        while (s0 < s->nsets) {
+            int64_t s1 = s0 + 1;
+            while (s1 < s->nsets && s->h_off[s1 + 1] - s->h_off[s0] <= kBitsChunk) s1++;
+            const int64_t b = s->h_off[s0], n = s->h_off[s1] - b;
+            if (n) {
+                DevBuf kA(n * 8, st), kB(n * 8, st), vA(n * 4, st), vB(n * 4, st);
+                GD_HIP(hipMemcpyAsync(kA.p, s->codes.as<uint64_t>() + b, n * 8, hipMemcpyDeviceToDevice, st));
+                set_ids_kernel<<<grid_for(n), 256, 0, st>>>(s->off.as<int64_t>(), s0, s1, vA.as<int32_t>());
+                GD_HIP(hipGetLastError());
+                uint64_t* keys = kA.as<uint64_t>(); uint64_t* kalt = kB.as<uint64_t>();
+                int32_t* ids = vA.as<int32_t>(); int32_t* ialt = vB.as<int32_t>();
+                sort_pairs_u64_i32(ctx, keys, kalt, ids, ialt, (size_t)n, 0, cbits);
+                DevBuf flag, pos, uniq, start;
+                int64_t nruns = 0;
+                runs_of(ctx, keys, n, flag, pos, uniq, start, nruns);
+                DevBuf rank(nruns * 8 + 8, st);
+                run_rank_kernel<<<(int)ceil_div(nruns, 256), 256, 0, st>>>(keys, start.as<int64_t>(), nruns, dict, U,
+                                                                           rare, Ur, rank.as<int64_t>());
+                GD_HIP(hipGetLastError());
+                scatter_bits_kernel<<<grid_for(n), 256, 0, st>>>(ids, flag.as<int32_t>(), pos.as<int64_t>(),
+                                                                 rank.as<int64_t>(), n, W, bits, id_base, rare_out,
+                                                                 rcnt.as<unsigned long long>(), rare_cap);
+                GD_HIP(hipGetLastError());
+                GD_HIP(hipStreamSynchronize(st));
+            }
+            s0 = s1;
         }
-        s0 = s1;
     }
+    int64_t w = 0;
+    d2h(&w, rcnt.p, 8, st);
+    GD_REQUIRE(w <= rare_cap, "rare-tier record count exceeds its reservation");
+    *rare_written = w;
 }
 
-void build_bitsets(gdist_ctx* ctx, gdist_sets* s, unsigned flags) {
+// rare records (rank << 32 | set) -> posting lists CSR on `s`
+void build_postings(gdist_ctx* ctx, gdist_sets* s, unsigned long long* recs, int64_t n, int64_t Ur) {
+    hipStream_t st = ctx->stream;
+    s->n_rare = Ur;
+    s->post_off.alloc((Ur + 1) * 8, st);
+    s->post_sets.alloc(n * 4 + 4, st);
+    if (Ur == 0 || n == 0) {
+        GD_HIP(hipMemsetAsync(s->post_off.p, 0, (Ur + 1) * 8, st));
+        GD_HIP(hipStreamSynchronize(st));
+        return;
+    }
+    DevBuf alt(n * 8, st);
+    uint64_t* keys = reinterpret_cast<uint64_t*>(recs);
+    uint64_t* kalt = alt.as<uint64_t>();
+    int rbits = 1;
+    while ((int64_t(1) << rbits) < Ur) rbits++;
+    sort_keys_u64(ctx, keys, kalt, (size_t)n, 0, std::min(64, 32 + rbits));
+    posting_offsets_kernel<<<(int)ceil_div(Ur + 1, 256), 256, 0, st>>>(keys, n, Ur, s->post_off.as<int64_t>());
+    posting_sets_kernel<<<grid_for(n), 256, 0, st>>>(keys, n, s->post_sets.as<uint32_t>());
+    GD_HIP(hipGetLastError());
+    GD_HIP(hipStreamSynchronize(st));
+}
+
+void build_bitsets(gdist_ctx* ctx, gdist_sets* s, unsigned flags, int64_t rare_threshold) {
     const bool keep = (flags & GDIST_BITSET_KEEP_SINGLETONS) != 0;
+    const int64_t T = keep ? 0 : (rare_threshold < 0 ? auto_rare_threshold(s->nsets) : rare_threshold);
     Summary sum;
     local_summary(ctx, s, sum);
-    DevBuf dict;
-    int64_t U = 0;
-    dictionary_from(ctx, {SummaryView{sum.codes.as<uint64_t>(), sum.counts.as<uint32_t>(), sum.n}}, keep, dict, U);
+    DevBuf dict, rare;
+    int64_t U = 0, Ur = 0, mass = 0;
+    dictionary_from(ctx, {SummaryView{sum.codes.as<uint64_t>(), sum.counts.as<uint32_t>(), sum.n}}, keep, T, dict, U,
+                    rare, Ur, mass);
     const int64_t W = bitset_words(U);
     s->bits.alloc((size_t)s->nsets * W * 8 + 8, ctx->stream);
-    fill_bits(ctx, s, dict.as<uint64_t>(), U, W, s->bits.as<unsigned long long>());
+    DevBuf recs(mass * 8 + 8, ctx->stream);
+    int64_t written = 0;
+    fill_bits(ctx, s, dict.as<uint64_t>(), U, W, s->bits.as<unsigned long long>(), rare.as<uint64_t>(), Ur, 0,
+              recs.as<unsigned long long>(), mass, &written);
+    GD_REQUIRE(written == mass, "rare-tier record count mismatch");
+    build_postings(ctx, s, recs.as<unsigned long long>(), written, Ur);
     GD_HIP(hipStreamSynchronize(ctx->stream));
     s->W = W;
     s->dict_size = U;
+    s->rare_T = T;
+    s->rare_records = written;
     s->bits_keep_singletons = keep;
 }
 
@@ -674,8 +870,14 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
                                            sp2, nch2, r0, r1, c0, c1, upper ? 1 : 0, d_I, ldI);
     }
     GD_HIP(hipGetLastError());
-    GD_HIP(hipEventRecord(ctx->ev_k1, st));
     ctx->last.launches = 1;
+    if (s->n_rare > 0) {
+        rare_pairs_kernel<<<grid_for(s->n_rare, 256, 256 * 64), 256, 0, st>>>(
+            s->post_off.as<int64_t>(), s->post_sets.as<uint32_t>(), s->n_rare, r0, r1, c0, c1, upper ? 1 : 0, d_I, ldI);
+        GD_HIP(hipGetLastError());
+        ctx->last.launches = 2;
+    }
+    GD_HIP(hipEventRecord(ctx->ev_k1, st));
     const int64_t lo = std::max(r0, c0), hi = std::min(r1, c1);
     if (!upper && hi > lo) {
         self_pairs_kernel<<<(unsigned)ceil_div(hi - lo, 256), 256, 0, st>>>(s->off.as<int64_t>(), lo, hi, r0, c0, d_I,

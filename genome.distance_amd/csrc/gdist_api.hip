@@ -298,13 +298,24 @@ int gdist_sets_download(const gdist_sets* s, int64_t* offsets, uint64_t* codes) 
     });
 }
 
-int gdist_sets_build_bitsets(gdist_sets* s, unsigned flags) {
+int gdist_sets_build_bitsets(gdist_sets* s, unsigned flags) { return gdist_sets_build_bitsets_ex(s, flags, -1); }
+
+int gdist_sets_build_bitsets_ex(gdist_sets* s, unsigned flags, int64_t rare_threshold) {
     return guard([&] {
         check_sets(s);
-        GD_REQUIRE(s->kind != GDIST_SKETCH, "bitsets are built from kmer sets");
+        GD_REQUIRE(s->kind != GDIST_SKETCH && s->has_codes, "bitsets are built from kmer sets");
         use_device(s->ctx);
         std::lock_guard<std::recursive_mutex> lk(s->ctx->mu);
-        build_bitsets(s->ctx, s, flags);
+        build_bitsets(s->ctx, s, flags, rare_threshold);
+    });
+}
+
+int gdist_sets_rare_info(const gdist_sets* s, int64_t* threshold, int64_t* lists, int64_t* records) {
+    return guard([&] {
+        check_sets(s);
+        if (threshold) *threshold = s->rare_T;
+        if (lists) *lists = s->n_rare;
+        if (records) *records = s->rare_records;
     });
 }
 
@@ -719,14 +730,21 @@ int gdist_sets_allgather_bitsets(gdist_ctx* ctx, const gdist_sets* local, unsign
         } else {
             parts.push_back({sum.codes.as<uint64_t>(), sum.counts.as<uint32_t>(), sum.n});
         }
-        DevBuf dict;
-        int64_t U = 0;
-        dictionary_from(ctx, parts, keep, dict, U);
+        DevBuf dict, rare;
+        int64_t U = 0, Ur = 0, mass_all = 0;
+        const int64_t T = keep ? 0 : auto_rare_threshold(N);
+        dictionary_from(ctx, parts, keep, T, dict, U, rare, Ur, mass_all);
         gc.release(); gn.release();
         const int64_t W = bitset_words(U);
-        // 4. local bitsets, padded to the largest shard, then one all-gather
-        DevBuf lb((size_t)mxs * W * 8 + 8, st);
-        if (local->nsets) fill_bits(ctx, local, dict.as<uint64_t>(), U, W, lb.as<unsigned long long>());
+        // 4. local bitsets (padded to the largest shard) + local rare-tier records
+        int64_t id_base = 0;
+        for (int r = 0; r < ctx->rank && R > 1; r++) id_base += hall[2 * r];
+        const int64_t cap = local_rare_mass(ctx, sum, rare.as<uint64_t>(), Ur);
+        DevBuf lb((size_t)mxs * W * 8 + 8, st), lrec(cap * 8 + 8, st);
+        int64_t written = 0;
+        if (local->nsets)
+            fill_bits(ctx, local, dict.as<uint64_t>(), U, W, lb.as<unsigned long long>(), rare.as<uint64_t>(), Ur,
+                      id_base, lrec.as<unsigned long long>(), cap, &written);
         auto* s = new gdist_sets();
         s->ctx = ctx; s->kind = local->kind; s->k = local->k; s->flags = local->flags;
         s->nsets = N; s->has_codes = false;
@@ -765,6 +783,34 @@ int gdist_sets_allgather_bitsets(gdist_ctx* ctx, const gdist_sets* local, unsign
         h2d(s->off.p, s->h_off.data(), (N + 1) * 8, st);
         s->codes.alloc(8, st);
         s->W = W; s->dict_size = U; s->bits_keep_singletons = keep;
+        // 6. rare-tier records of every rank (one all-gather), posting lists
+        std::vector<int64_t> wr(R, 0);
+        wr[0] = written;
+        int64_t mxw = written, totw = written;
+        if (R > 1) {
+            DevBuf mw(8, st), aw(8 * R, st);
+            h2d(mw.p, &written, 8, st);
+            GD_NCCL(ncclAllGather(mw.p, aw.p, 1, ncclInt64, ctx->comm, st));
+            d2h(wr.data(), aw.p, 8 * R, st);
+            mxw = 0; totw = 0;
+            for (int r = 0; r < R; r++) { mxw = std::max(mxw, wr[r]); totw += wr[r]; }
+            DevBuf ga((size_t)(mxw + 1) * 8 * R, st), allrec(totw * 8 + 8, st);
+            DevBuf pad((mxw + 1) * 8, st);
+            if (written) GD_HIP(hipMemcpyAsync(pad.p, lrec.p, written * 8, hipMemcpyDeviceToDevice, st));
+            GD_NCCL(ncclAllGather(pad.p, ga.p, mxw + 1, ncclUint64, ctx->comm, st));
+            int64_t at = 0;
+            for (int r = 0; r < R; r++) {
+                if (wr[r])
+                    GD_HIP(hipMemcpyAsync(allrec.as<uint64_t>() + at, ga.as<uint64_t>() + (mxw + 1) * r, wr[r] * 8,
+                                          hipMemcpyDeviceToDevice, st));
+                at += wr[r];
+            }
+            build_postings(ctx, s, allrec.as<unsigned long long>(), totw, Ur);
+        } else {
+            build_postings(ctx, s, lrec.as<unsigned long long>(), written, Ur);
+        }
+        s->rare_T = T;
+        s->rare_records = totw;
         GD_HIP(hipStreamSynchronize(st));
         *out = s;
     });

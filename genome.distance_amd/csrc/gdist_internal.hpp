@@ -138,6 +138,10 @@ struct gdist_sets {
     int nseg = 0;
     int64_t max_seg = 0;
     bool has_codes = true;                // false for all-gathered bitset-only collections
+    // rare tier of the dictionary: kmers held by 2..rare_T-1 sets as posting lists
+    gdist::DevBuf post_off;               // int64 [n_rare+1]
+    gdist::DevBuf post_sets;              // uint32 [rare_records], ascending within a list
+    int64_t n_rare = 0, rare_T = 0, rare_records = 0;
 };
 
 namespace gdist {
@@ -165,12 +169,16 @@ struct SummaryView {
     int64_t n;
 };
 void local_summary(gdist_ctx* ctx, const gdist_sets* s, Summary& out);
-void dictionary_from(gdist_ctx* ctx, const std::vector<SummaryView>& parts, bool keep, DevBuf& dict,
-                     int64_t& U);
+void dictionary_from(gdist_ctx* ctx, const std::vector<SummaryView>& parts, bool keep, int64_t T, DevBuf& dict,
+                     int64_t& U, DevBuf& rare, int64_t& Ur, int64_t& rare_mass);
 int64_t bitset_words(int64_t dict_size);
+int64_t local_rare_mass(gdist_ctx* ctx, const Summary& local, const uint64_t* rare, int64_t Ur);
+int64_t auto_rare_threshold(int64_t nsets);
 void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_t U, int64_t W,
-               unsigned long long* bits);
-void build_bitsets(gdist_ctx* ctx, gdist_sets* s, unsigned flags);
+               unsigned long long* bits, const uint64_t* rare, int64_t Ur, int64_t id_base,
+               unsigned long long* rare_out, int64_t rare_cap, int64_t* rare_written);
+void build_postings(gdist_ctx* ctx, gdist_sets* s, unsigned long long* recs, int64_t n, int64_t Ur);
+void build_bitsets(gdist_ctx* ctx, gdist_sets* s, unsigned flags, int64_t rare_threshold = -1);
 void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0,
                    int64_t c1, bool upper, int32_t* d_I, int64_t ldI);
 

@@ -211,9 +211,17 @@ class KmerSets(_Handle):
         L.check(L.lib.gdist_sets_download(self.h, L.ptr(off, C.c_int64), L.ptr(codes, C.c_uint64)))
         return off, codes[:t]
 
-    def build_bitsets(self, keep_singletons: bool = False) -> tuple[int, int]:
-        L.check(L.lib.gdist_sets_build_bitsets(self.h, L.BITSET_KEEP_SINGLETONS if keep_singletons else 0))
+    def build_bitsets(self, keep_singletons: bool = False, rare_threshold: int = -1) -> tuple[int, int]:
+        """Dense bitsets (+ rare-kmer posting lists, see include/gdist.h); returns (dense dictionary, W)."""
+        L.check(L.lib.gdist_sets_build_bitsets_ex(self.h, L.BITSET_KEEP_SINGLETONS if keep_singletons else 0,
+                                                  rare_threshold))
         return self.bitset_info()
+
+    def rare_info(self) -> tuple[int, int, int]:
+        """(threshold T, posting lists, records) of the rare tier."""
+        t, n, r = C.c_int64(), C.c_int64(), C.c_int64()
+        L.check(L.lib.gdist_sets_rare_info(self.h, C.byref(t), C.byref(n), C.byref(r)))
+        return t.value, n.value, r.value
 
     def bitsets(self) -> np.ndarray:
         """The dictionary-rank bitsets, (nsets, W) uint64."""

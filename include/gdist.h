@@ -135,8 +135,15 @@ int  gdist_sets_free(gdist_sets* sets);
 int  gdist_sets_info(const gdist_sets* sets, int* kind, int* k, int64_t* nsets, int64_t* total_codes);
 int  gdist_sets_sizes(const gdist_sets* sets, int64_t* sizes);           /* nsets values */
 int  gdist_sets_download(const gdist_sets* sets, int64_t* offsets, uint64_t* codes);
-/* Build the dictionary-rank bitset representation (kept with the sets). */
+/* Build the dictionary-rank bitset representation (kept with the sets).
+ * Two exact tiers: kmers held by >= T sets are bit columns of the dense
+ * bitsets (AND + popcount tiles); kmers held by 2..T-1 sets are posting lists
+ * whose m(m-1)/2 pairs are counted directly. _ex sets T (-1 = automatic,
+ * 0..2 = dense only); KEEP_SINGLETONS forces a dense-only dictionary of
+ * every distinct kmer. */
 int  gdist_sets_build_bitsets(gdist_sets* sets, unsigned flags);
+int  gdist_sets_build_bitsets_ex(gdist_sets* sets, unsigned flags, int64_t rare_threshold);
+int  gdist_sets_rare_info(const gdist_sets* sets, int64_t* threshold, int64_t* lists, int64_t* records);
 int  gdist_sets_bitset_info(const gdist_sets* sets, int64_t* dict_size, int64_t* words_per_set);
 /* Copy the bitsets (nsets x words_per_set uint64, row-major) to the host. */
 int  gdist_sets_bitset_download(const gdist_sets* sets, uint64_t* bits);

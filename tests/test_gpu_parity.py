@@ -327,3 +327,50 @@ def test_genome_and_reps_processors(ctx):
     for i, row in enumerate(rows):
         d = min(pyref.set_distance(ks[i], ks[r]) for r in reps)
         assert row[2] in rep_ids and row[4] == pyref.java_double_str(0.0 if i in reps else d)
+
+
+# ---------------------------------------------------------------- two-tier dictionary
+@pytest.mark.parametrize("T", [0, 3, 8, 1000])
+def test_rare_tier_thresholds_exact(ctx, T):
+    """Dense-only (T=0), mixed, and all-rare (T > N) dictionaries give the
+    same bit-exact counts and distances as the oracle."""
+    import gdist
+    n = 200
+    seqs = synth_sets(n, 6000, 0.01, 101)
+    sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
+    sets.build_bitsets(rare_threshold=T)
+    thr, lists, recs = sets.rare_info()
+    assert thr == T
+    if T > 2:
+        assert lists > 0 and recs >= 2 * lists
+    else:
+        assert lists == 0
+    off, codes = oracle_pack(seqs, 21, 0, 0)
+    for (r0, r1, c0, c1, up) in [(0, n, 0, n, False), (0, n, 0, n, True), (17, 150, 3, 190, False),
+                                 (60, 61, 0, n, False)]:
+        I, D = sets.matrix((r0, r1), (c0, c1), upper=up, method=gdist.METHOD_BITSET)
+        eI, eD = oracle.matrix(off, codes, r0, r1, c0, c1, flags=0x100 if up else 0)
+        if up:
+            mask = np.fromfunction(lambda a, b: (c0 + b) > (r0 + a), (r1 - r0, c1 - c0))
+            I, D, eI, eD = I[mask], D[mask], eI[mask], eD[mask]
+        assert np.array_equal(I, eI), (T, r0, r1, c0, c1, up)
+        assert bits_equal(D, eD)
+    cols = [5, 199, 0, 77, 150]
+    d = sets.row_query(77, cols)
+    _, eD = oracle.matrix(off, codes, 77, 78, 0, n)
+    assert bits_equal(d, eD[0, cols])
+
+
+def test_single_rank_allgather_bitsets(ctx):
+    """gdist_sets_allgather_bitsets without a communicator = one rank: same
+    counts as the local build (exercises the distributed code path)."""
+    import gdist
+    seqs = synth_sets(150, 4000, 0.02, 102)
+    local = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
+    ag = local.allgather_bitsets()
+    I, D = ag.matrix(method=gdist.METHOD_BITSET)
+    off, codes = oracle_pack(seqs, 21, 0, 0)
+    eI, eD = oracle.matrix(off, codes, 0, 150, 0, 150)
+    assert np.array_equal(I, eI) and bits_equal(D, eD)
+    with pytest.raises(ValueError):
+        ag.matrix(method=gdist.METHOD_SORTED)          # bitset-only collection
