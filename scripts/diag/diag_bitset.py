@@ -1,6 +1,6 @@
 """Diagnostic (not collected by pytest): stage-by-stage check of the bitset path."""
 import os, sys
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [os.path.join(ROOT, "genome.distance_amd"), os.path.join(ROOT, "oracle")]
 import numpy as np
 import gdist, oracle

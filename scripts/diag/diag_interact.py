@@ -1,7 +1,7 @@
 """Diagnostic: reproduce rectangles -> prune interaction with state checks."""
 import os, sys
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [os.path.join(ROOT, "genome.distance_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")]
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [os.path.join(ROOT, "genome.distance_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "scripts", "diag")]
 import numpy as np
 import gdist, oracle
 from gdist import synth
