@@ -196,7 +196,7 @@ def main():
                 traffic = None
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": {"bitset": "bitset_tile_kernel", "sorted": "sorted_join_kernel",
+                "kernel": {"bitset": "bitset_tile_kernel2<1> (+ rare_pairs_kernel)", "sorted": "sorted_join_kernel",
                            "sketch": "sketch_tile_kernel"}[method],
                 "kernel_avg_ms": round(k_avg_ms, 4), "algo_bytes_per_launch": algo_bytes,
                 "bytes_per_pair": bytes_per_pair}
