@@ -42,6 +42,9 @@ HBM_PEAK_GBS = 8000.0               # MI355X_MICROARCH.md chip table (spec)
 # 5.7e11 alone vs 1.06e12 for v_and). One 64-bit word pair = 4 wave-lane
 # instructions (2 and + 2 bcnt) -> 6.17e11 * 64 / 4 word pairs/s.
 VALU_WORDPAIR_PEAK = 6.17e11 * 64 / 4.0
+# LDS read peak for ds_read_b32-class reads (ds_read2_b32 banks as two of them):
+# MI355X_MICROARCH.md §LDS, "≈75 TB/s for ds_read_b32" with every CU streaming.
+LDS_B32_PEAK_GBS = 75000.0
 
 CONFIGS = {
     # name: (n_genomes, length, p_max, kind, k, method, cfg index for the seed)
@@ -182,7 +185,11 @@ def main():
             sizes = local.sizes() if world == 1 else None
             bytes_per_pair = 16.0 * float(np.mean(sizes)) if sizes is not None else 0.0   # 8(n_i+n_j)
         else:
-            bytes_per_pair = 8.0 * cfg["width"]                  # 4(s_i+s_j)
+            # the sketch tile kernel keeps the tile's sketches in LDS; each merge
+            # step reads 2 dwords and a pair of full sketches takes exactly
+            # `width` steps (phase 1 ends at taken == width), so 8*width B of
+            # LDS reads per pair; HBM/L2 traffic is the tile fill, ~1/10 of that
+            bytes_per_pair = 8.0 * cfg["width"]
         algo_bytes = pairs_rank * bytes_per_pair
         achieved = algo_bytes / (k_avg_ms * 1e-3) / 1e9 if k_avg_ms > 0 else 0.0
         traffic = None
@@ -194,10 +201,11 @@ def main():
                     traffic = pmc.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
-        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+        peak = LDS_B32_PEAK_GBS if method == "sketch" else HBM_PEAK_GBS
+        roof = {"bound": "lds" if method == "sketch" else "hbm", "achieved": round(achieved, 1), "peak": peak,
+                "unit": "GB/s", "frac": round(achieved / peak, 4), "traffic": traffic,
                 "kernel": {"bitset": "bitset_tile_kernel2<1> (+ rare_pairs_kernel)", "sorted": "sorted_join_kernel",
-                           "sketch": "sketch_tile_kernel"}[method],
+                           "sketch": "sketch_tile_kernel<16,24,LDS,K=2>"}[method],
                 "kernel_avg_ms": round(k_avg_ms, 4), "algo_bytes_per_launch": algo_bytes,
                 "bytes_per_pair": bytes_per_pair}
         if method == "bitset":

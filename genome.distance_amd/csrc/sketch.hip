@@ -117,60 +117,114 @@ __global__ void emit_sig_kernel(const uint64_t* __restrict__ keys, const int32_t
     }
 }
 
-constexpr int ST = 16;                      // tile edge (sketches)
-constexpr int LDS_SK_BYTES = 128 * 1024;
+constexpr int LDS_SK_MAX = 160 * 1024;      // whole CU LDS: one workgroup per CU at width ~1000
+constexpr int LDS_SK_SLACK = 64;            // phase-1 reads stop at n-1, slack only guards rounding
 
-template <bool LDS>
-__global__ __launch_bounds__(256) void sketch_tile_kernel(const int32_t* __restrict__ sig,
-                                                          const int64_t* __restrict__ off, int width,
-                                                          int64_t r0, int64_t r1, int64_t c0, int64_t c1,
-                                                          int tiles_c, int upper, int jaccard, int empty_nan,
-                                                          int32_t* __restrict__ common_out,
-                                                          double* __restrict__ D, int64_t ld) {
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_void_t;
+
+// LDS row stride (dwords): odd, so the R+C rows of a tile start on distinct
+// banks (ds_read2_b32 banks by dword mod 32) - lanes advance at similar rates,
+// and with an even stride (1000 = 8 mod 32) the 24 column rows of a tile met
+// on 4 banks.
+inline int sketch_stride(int width) { return width | 1; }
+
+// One workgroup = an R x C tile of sketch pairs, one lane per pair
+// (R*C threads).  16x24 at width <= ~1000 puts 40 sketches (160,000 B) in LDS
+// and 6 waves on the CU; 16x16 covers wider sketches (and the global-memory
+// variant, LDS=false, anything wider still).
+//
+// Fill (LDS variant): the R+C sketches of the tile are DMA'd global->LDS with
+// global_load_lds, one 64-dword row segment per wave instruction, all issued
+// before a single vmcnt(0) wait.  Lanes past a sketch's length are masked off
+// (exec), so rows sit at the odd stride sketch_stride(width) with no padding.
+//
+// Merge (Sketch.distance, WidthProcessor.java:185; restated in
+// oracle/pyref.py:sketch_distance).  Sketches are strictly increasing
+// (built that way; uploads are validated), so:
+//   phase 1 - while both sides have elements (and, for Mash, fewer than
+//             `width` union elements were taken): load both heads, advance by
+//             the <=/>= masks.  Branch-free, one LDS latency per step.
+//             common = ia + ib - steps (a common element advances both).
+//   phase 2 - closed form: the rest of the non-exhausted side are distinct
+//             union elements with no common ones.
+template <int R, int C, bool LDS, int KW>
+__global__ __launch_bounds__(R * C) void sketch_tile_kernel(const int32_t* __restrict__ sig,
+                                                            const int64_t* __restrict__ off, int width, int sw,
+                                                            int64_t r0, int64_t r1, int64_t c0, int64_t c1,
+                                                            int tiles_c, int upper, int jaccard, int empty_nan,
+                                                            int32_t* __restrict__ common_out,
+                                                            double* __restrict__ D, int64_t ld) {
 #pragma clang fp contract(off)
-    extern __shared__ int32_t sm[];   // [2*ST][width]
+    constexpr int NT = R * C, NW = NT / 64, NS = R + C;
+    extern __shared__ int32_t sm[];   // [R+C][sketch_stride(width)] (+ slack)
+    __shared__ int64_t s_base[NS];
+    __shared__ int32_t s_n[NS];
     const int tr = blockIdx.x / tiles_c, tcb = blockIdx.x % tiles_c;
-    const int64_t row0 = r0 + (int64_t)tr * ST, col0 = c0 + (int64_t)tcb * ST;
-    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-    if (upper && col0 + ST - 1 <= row0) return;
+    const int64_t row0 = r0 + (int64_t)tr * R, col0 = c0 + (int64_t)tcb * C;
+    const int ty = threadIdx.x / C, tx = threadIdx.x - ty * C;
+    if (upper && col0 + C - 1 <= row0) return;
     if (LDS) {
-        for (int s = 0; s < 2 * ST; s++) {
-            const int64_t g = s < ST ? row0 + s : col0 + (s - ST);
-            const bool ok = s < ST ? g < r1 : g < c1;
-            const int64_t b = ok ? off[g] : 0, n = ok ? off[g + 1] - off[g] : 0;
-            for (int t = threadIdx.x; t < n; t += 256) sm[s * width + t] = sig[b + t];
+        if (threadIdx.x < NS) {
+            const int s = threadIdx.x;
+            const int64_t g = s < R ? row0 + s : col0 + (s - R);
+            const bool ok = s < R ? g < r1 : g < c1;
+            s_base[s] = ok ? off[g] : 0;
+            s_n[s] = ok ? (int32_t)(off[g + 1] - off[g]) : 0;
         }
         __syncthreads();
+        const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+        for (int s = wave; s < NS; s += NW) {
+            const int n = __builtin_amdgcn_readfirstlane(s_n[s]);
+            const int32_t* src = sig + s_base[s];
+            for (int t = 0; t < n; t += 64) {
+                if (t + lane < n)
+                    __builtin_amdgcn_global_load_lds((gbl_void_t*)(src + t + lane),
+                                                     (lds_void_t*)(sm + s * sw + t), 4, 0, 0);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
     }
     const int64_t i = row0 + ty, j = col0 + tx;
     if (i >= r1 || j >= c1 || (upper && j <= i)) return;
-    const int64_t na = off[i + 1] - off[i], nb = off[j + 1] - off[j];
-    const int32_t* A = LDS ? sm + ty * width : sig + off[i];
-    const int32_t* B = LDS ? sm + (ST + tx) * width : sig + off[j];
-    int64_t ia = 0, ib = 0, taken = 0, common = 0;
-    int64_t va = na ? (int64_t)A[0] : INT64_MAX, vb = nb ? (int64_t)B[0] : INT64_MAX;
-    if (jaccard) {
-        while (ia < na && ib < nb) {
-            if (va < vb) { ia++; va = ia < na ? (int64_t)A[ia] : INT64_MAX; }
-            else if (vb < va) { ib++; vb = ib < nb ? (int64_t)B[ib] : INT64_MAX; }
-            else {
-                common++;
-                ia++; va = ia < na ? (int64_t)A[ia] : INT64_MAX;
-                ib++; vb = ib < nb ? (int64_t)B[ib] : INT64_MAX;
+    const int ina = LDS ? s_n[ty] : (int)(off[i + 1] - off[i]);
+    const int inb = LDS ? s_n[R + tx] : (int)(off[j + 1] - off[j]);
+    const int32_t* A = LDS ? sm + ty * sw : sig + off[i];
+    const int32_t* B = LDS ? sm + (R + tx) * sw : sig + off[j];
+    const int lim = jaccard ? ina + inb : width;
+    int ia = 0, ib = 0, steps = 0;
+    if (KW > 1) {
+        // steady state: both sides have >= KW elements left and >= KW steps
+        // remain, so KW steps run unchecked on a KW-element window per side
+        // (one LDS round trip); a step shifts the window of the side(s) it
+        // advances.  Boundary rounds fall through to the one-step loop.
+        while (ina - ia >= KW && inb - ib >= KW && lim - steps >= KW) {
+            int32_t a[KW], b[KW];
+#pragma unroll
+            for (int u = 0; u < KW; u++) { a[u] = A[ia + u]; b[u] = B[ib + u]; }
+#pragma unroll
+            for (int s = 0; s < KW; s++) {
+                const bool le = a[0] <= b[0], ge = b[0] <= a[0];
+                ia += le;
+                ib += ge;
+#pragma unroll
+                for (int u = 0; u + 1 < KW - s; u++) {
+                    a[u] = le ? a[u + 1] : a[u];
+                    b[u] = ge ? b[u + 1] : b[u];
+                }
             }
-        }
-    } else {
-        while (taken < width && (ia < na || ib < nb)) {
-            if (va < vb) { ia++; va = ia < na ? (int64_t)A[ia] : INT64_MAX; }
-            else if (vb < va) { ib++; vb = ib < nb ? (int64_t)B[ib] : INT64_MAX; }
-            else {
-                common++;
-                ia++; va = ia < na ? (int64_t)A[ia] : INT64_MAX;
-                ib++; vb = ib < nb ? (int64_t)B[ib] : INT64_MAX;
-            }
-            taken++;
+            steps += KW;
         }
     }
+    while (ia < ina && ib < inb && steps < lim) {
+        const int32_t va = A[ia], vb = B[ib];
+        ia += va <= vb;
+        ib += vb <= va;
+        steps++;
+    }
+    const int common = ia + ib - steps;
+    const int taken = steps + min((ina - ia) + (inb - ib), width - steps);
+    const int64_t na = ina, nb = inb;
     double d;
     if (jaccard) {
         if (common > 0) d = 1.0 - (double)common / (double)(na + nb - common);
@@ -182,6 +236,48 @@ __global__ __launch_bounds__(256) void sketch_tile_kernel(const int32_t* __restr
     const int64_t o = (i - r0) * ld + (j - c0);
     if (common_out) common_out[o] = (int32_t)common;
     if (D) D[o] = d;
+}
+
+template <int R, int C>
+constexpr size_t sketch_meta_bytes() { return (size_t)(R + C) * (sizeof(int64_t) + sizeof(int32_t)); }
+
+template <int R, int C>
+bool launch_sketch_tiles(hipStream_t st, const gdist_sets* sk, int width, int64_t r0, int64_t r1, int64_t c0,
+                         int64_t c1, bool upper, int jac, int en, int32_t* d_common, double* d_D, int64_t ld,
+                         bool force_global) {
+    // GDIST_SKETCH_EVEN=1 keeps the unpadded stride (A/B of the bank spread)
+    const char* ev = getenv("GDIST_SKETCH_EVEN");
+    const int sw = (ev && atoi(ev) == 1) ? width : sketch_stride(width);
+    const size_t lds = (size_t)(R + C) * sw * 4 + LDS_SK_SLACK;
+    const bool use_lds = !force_global && lds + sketch_meta_bytes<R, C>() <= (size_t)LDS_SK_MAX;
+    if (!use_lds && !force_global) return false;
+    const int tr = (int)ceil_div(r1 - r0, R), tc = (int)ceil_div(c1 - c0, C);
+    const int64_t grid = (int64_t)tr * tc;
+    GD_REQUIRE(grid < (int64_t(1) << 31), "sketch grid too large");
+    // GDIST_SKETCH_K selects the merge window (1, 2, 4, 6; A/B measurements)
+    const char* env = getenv("GDIST_SKETCH_K");
+    const int kw = env ? atoi(env) : 2;
+    const int32_t* sig = sk->codes.as<int32_t>();
+    const int64_t* off = sk->off.as<int64_t>();
+    if (!use_lds) {
+        sketch_tile_kernel<R, C, false, 1><<<(unsigned)grid, R * C, 0, st>>>(
+            sig, off, width, sw, r0, r1, c0, c1, tc, upper, jac, en, d_common, d_D, ld);
+    } else {
+        auto go = [&](auto kern) {
+            GD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       LDS_SK_MAX - (int)sketch_meta_bytes<R, C>()));
+            kern<<<(unsigned)grid, R * C, lds, st>>>(sig, off, width, sw, r0, r1, c0, c1, tc, upper, jac, en, d_common,
+                                                      d_D, ld);
+        };
+        switch (kw) {
+            case 1: go(&sketch_tile_kernel<R, C, true, 1>); break;
+            case 4: go(&sketch_tile_kernel<R, C, true, 4>); break;
+            case 6: go(&sketch_tile_kernel<R, C, true, 6>); break;
+            default: go(&sketch_tile_kernel<R, C, true, 2>); break;
+        }
+    }
+    GD_HIP(hipGetLastError());
+    return true;
 }
 
 }  // namespace
@@ -273,32 +369,18 @@ void sketch_build(gdist_ctx* ctx, const gdist_sets* s, int width, gdist_sets* ou
 void sketch_matrix(gdist_ctx* ctx, const gdist_sets* sk, int64_t r0, int64_t r1, int64_t c0, int64_t c1,
                    unsigned flags, int32_t* d_common, double* d_D, int64_t ld) {
     hipStream_t st = ctx->stream;
-    const int64_t nr = r1 - r0, nc = c1 - c0;
-    if (nr <= 0 || nc <= 0) return;
-    const int tr = (int)ceil_div(nr, ST), tc = (int)ceil_div(nc, ST);
-    const int64_t grid = (int64_t)tr * tc;
-    GD_REQUIRE(grid < (int64_t(1) << 31), "sketch grid too large");
+    if (r1 - r0 <= 0 || c1 - c0 <= 0) return;
     const bool upper = (flags & GDIST_UPPER_TRIANGLE) != 0;
     const int jac = (flags & GDIST_SKETCH_JACCARD) ? 1 : 0, en = (flags & GDIST_EMPTY_NAN) ? 1 : 0;
-    int width = std::max(1, sk->width);
-    const size_t lds = (size_t)2 * ST * width * 4;
-    static bool attr_set = false;
-    if (!attr_set) {
-        GD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&sketch_tile_kernel<true>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, LDS_SK_BYTES));
-        attr_set = true;
-    }
+    const int width = std::max(1, sk->width);
+    // GDIST_SKETCH_TILE=16 forces the 16x16 tile (A/B measurements)
+    const char* env = getenv("GDIST_SKETCH_TILE");
+    const bool only16 = env && atoi(env) == 16;
     GD_HIP(hipEventRecord(ctx->ev_k0, st));
-    if (lds <= (size_t)LDS_SK_BYTES) {
-        sketch_tile_kernel<true><<<(unsigned)grid, 256, lds, st>>>(sk->codes.as<int32_t>(), sk->off.as<int64_t>(),
-                                                                    width, r0, r1, c0, c1, tc, upper, jac, en,
-                                                                    d_common, d_D, ld);
-    } else {
-        sketch_tile_kernel<false><<<(unsigned)grid, 256, 0, st>>>(sk->codes.as<int32_t>(), sk->off.as<int64_t>(),
-                                                                   width, r0, r1, c0, c1, tc, upper, jac, en,
-                                                                   d_common, d_D, ld);
-    }
-    GD_HIP(hipGetLastError());
+    if (only16 || !launch_sketch_tiles<16, 24>(st, sk, width, r0, r1, c0, c1, upper, jac, en, d_common, d_D, ld,
+                                               false))
+        if (!launch_sketch_tiles<16, 16>(st, sk, width, r0, r1, c0, c1, upper, jac, en, d_common, d_D, ld, false))
+            launch_sketch_tiles<16, 16>(st, sk, width, r0, r1, c0, c1, upper, jac, en, d_common, d_D, ld, true);
     GD_HIP(hipEventRecord(ctx->ev_k1, st));
     ctx->last.launches = 1;
 }

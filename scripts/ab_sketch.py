@@ -1,0 +1,64 @@
+"""A/B of sketch merge windows (GDIST_SKETCH_K: kN), tile shapes
+(GDIST_SKETCH_TILE: tN) and LDS row stride (GDIST_SKETCH_EVEN: even) in ONE process on the C5 workload: every variant's common
+counts on a row block are checked identical to the first variant's, then the
+full upper triangle is timed in interleaved rounds."""
+import os, sys, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "genome.distance_amd"))
+import numpy as np
+import gdist
+from gdist import synth
+
+n = int(os.environ.get("AB_N", "50000")); L = int(os.environ.get("AB_LEN", "100000"))
+width = int(os.environ.get("AB_WIDTH", "1000"))
+variants = os.environ.get("AB_VARIANTS", "k1,k2,k4,k6").split(",")
+rounds = int(os.environ.get("AB_ROUNDS", "3"))
+check_rows = min(n, 2048)
+
+
+def apply(v):
+    os.environ.pop("GDIST_SKETCH_TILE", None)
+    os.environ.pop("GDIST_SKETCH_K", None)
+    os.environ.pop("GDIST_SKETCH_EVEN", None)
+    for part in v.split("+"):
+        if part.startswith("k"):
+            os.environ["GDIST_SKETCH_K"] = part[1:]
+        elif part.startswith("t"):
+            os.environ["GDIST_SKETCH_TILE"] = part[1:]
+        elif part == "even":
+            os.environ["GDIST_SKETCH_EVEN"] = "1"
+
+
+ctx = gdist.Context(0)
+t = time.time()
+g = synth.genomes(n, L, 0.05, 5)
+blob, off = synth.to_blob(g); del g
+sets = gdist.KmerSets.from_sequences([blob[off[i]:off[i + 1]] for i in range(n)], 21, gdist.KmerType.DNA, 0, ctx)
+del blob
+sk = sets.sketches(width)
+del sets
+print(f"n={n} L={L} width={width} setup {time.time() - t:.1f}s", flush=True)
+dC = ctx.alloc(n * n * 4)
+ref = None
+for v in variants:
+    apply(v)
+    for fl in (0, gdist.SKETCH_JACCARD):
+        sk.matrix_device(dC.ptr, None, n, (0, check_rows), (0, n), upper=True, flags=fl)
+        C = dC.to_host(np.int32, check_rows * n).reshape(check_rows, n)
+        C = np.triu(C, 1)
+        if ref is None:
+            ref = {}
+        if fl not in ref:
+            ref[fl] = C.copy()
+        print(f"{v} flags={fl:#x}: identical to {variants[0]} = {np.array_equal(C, ref[fl])}", flush=True)
+times = {v: [] for v in variants}
+for rnd in range(rounds):
+    for v in variants:
+        apply(v)
+        sk.matrix_device(dC.ptr, None, n, (0, n), (0, n), upper=True)
+        times[v].append(ctx.last_timing()[0])
+pairs = n * (n - 1) // 2
+for v in variants:
+    tt = np.array(times[v])
+    print(f"{v}: kernel ms median {np.median(tt):.1f} min {tt.min():.1f} -> "
+          f"{pairs / (np.median(tt) * 1e-3) / 1e9:.3f} G pairs/s", flush=True)
