@@ -50,8 +50,9 @@ CONFIGS = {
     # name: (n_genomes, length, p_max, kind, k, method, cfg index for the seed)
     "c2": dict(n=1000, length=2_000_000, p_max=0.002, protein=False, k=21, method="bitset", cfg=2,
                desc="1000 synthetic 2 Mbp genomes, DNA k=21 both strands, dictionary-rank bitsets"),
-    "c3": dict(n=10000, length=33_333, p_max=0.10, protein=True, k=8, method="sorted", cfg=3,
-               desc="10000 synthetic 33,333-aa proteomes, protein k=8, sorted uint64 sets (LDS hash-join)"),
+    "c3": dict(n=10000, length=33_333, p_max=0.10, protein=True, k=8, method="auto", cfg=3,
+               desc="10000 synthetic 33,333-aa proteomes, protein k=8, sorted uint64 sets "
+                    "(METHOD_AUTO: two-tier bitsets built from them, or the LDS hash-join)"),
     "c5": dict(n=50000, length=100_000, p_max=0.05, protein=False, k=21, method="sketch", cfg=5, width=1000,
                desc="50000 MinHash bottom-1000 sketches of 100 kbp genomes (DNA k=21)"),
 }
@@ -69,6 +70,8 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--n", type=int, default=0, help="override genome count (testing)")
     ap.add_argument("--length", type=int, default=0, help="override genome length (testing)")
+    ap.add_argument("--method", default="", choices=["", "auto", "bitset", "sorted"],
+                    help="override the config's kernel family (experiments; the config's own is the bench line)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=8)
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_c2.json"),
@@ -122,18 +125,31 @@ def main():
     del blob
     pack_s = time.time() - t
     t = time.time()
-    method = cfg["method"]
+    method = args.method or cfg["method"]
     width_words = 0
+    rare = None
+    auto = None
     if world > 1:
         uid = gdist.Context.unique_id() if rank == 0 else None
         obj = [uid]
         dist.broadcast_object_list(obj, src=0)
         ctx.comm_init(obj[0], world, rank)
+    if method == "auto":
+        # METHOD_AUTO's own decision (gdist_sets_prepare); multi-GPU runs take the
+        # dictionary path (its cost needs the global dictionary, built by the all-gather)
+        if world == 1:
+            chosen, cb, cs = local.prepare(gdist.METHOD_AUTO)
+            auto = {"chosen": {gdist.METHOD_BITSET: "bitset", gdist.METHOD_SORTED: "sorted"}[chosen],
+                    "est_bitset_s": round(cb, 4), "est_sorted_s": round(cs, 4)}
+            method = auto["chosen"]
+        else:
+            method = "bitset"
     if method == "bitset":
         sets = local.allgather_bitsets() if world > 1 else local
-        if world == 1:
+        if world == 1 and auto is None:
             sets.build_bitsets()
         dict_size, width_words = sets.bitset_info()
+        rare = dict(zip(("threshold", "lists", "records"), sets.rare_info()))
         mflag = gdist.METHOD_BITSET
     elif method == "sorted":
         sets = local.allgather() if world > 1 else local
@@ -201,19 +217,29 @@ def main():
                     traffic = pmc.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
-        peak = LDS_B32_PEAK_GBS if method == "sketch" else HBM_PEAK_GBS
-        roof = {"bound": "lds" if method == "sketch" else "hbm", "achieved": round(achieved, 1), "peak": peak,
-                "unit": "GB/s", "frac": round(achieved / peak, 4), "traffic": traffic,
-                "kernel": {"bitset": "bitset_tile_kernel2<1> (+ rare_pairs_kernel)", "sorted": "sorted_join_kernel",
-                           "sketch": "sketch_tile_kernel<16,24,LDS,K=2>"}[method],
-                "kernel_avg_ms": round(k_avg_ms, 4), "algo_bytes_per_launch": algo_bytes,
-                "bytes_per_pair": bytes_per_pair}
+        kname = {"bitset": "bitset_tile_kernel2<1> (+ rare_pairs_kernel)", "sorted": "sorted_join_kernel",
+                 "sketch": "sketch_tile_kernel<16,24,LDS,K=2>"}[method]
         if method == "bitset":
+            # The tiles reuse each bitset from LDS across 128 partners, so the 16*W
+            # B/pair streaming figure runs far past the HBM peak: the binding
+            # resource is VALU issue. One 64-bit word pair = 4 lane-ops
+            # (2 v_and_b32 + 2 v_bcnt_u32_b32); peak = the measured and+bcnt ceiling.
             wp = pairs_rank * width_words / (k_avg_ms * 1e-3) if k_avg_ms > 0 else 0.0
-            roof["valu"] = {"achieved": round(wp / 1e12, 3), "peak": round(VALU_WORDPAIR_PEAK / 1e12, 3),
-                            "unit": "T word-pairs/s", "frac": round(wp / VALU_WORDPAIR_PEAK, 4),
-                            "note": "2x v_and_b32 + 2x v_bcnt_u32_b32 per 64-bit word pair; peak = measured "
-                                    "and+bcnt issue ceiling (profiles/r01/valu_microbench.txt)"}
+            tops, tops_peak = wp * 4 / 1e12, VALU_WORDPAIR_PEAK * 4 / 1e12
+            roof = {"bound": "valu", "achieved": round(tops, 3), "peak": round(tops_peak, 3), "unit": "TOP/s",
+                    "frac": round(tops / tops_peak, 4), "traffic": traffic, "kernel": kname,
+                    "kernel_avg_ms": round(k_avg_ms, 4), "ops_per_pair": 4 * width_words,
+                    "note": "lane-ops of the dense tier (pairs x W word pairs x 4); kernel time includes the "
+                            "rare tier; peak = measured and+bcnt issue ceiling (profiles/r01/valu_microbench.txt)",
+                    "hbm": {"achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": round(achieved / HBM_PEAK_GBS, 4), "bytes_per_pair": bytes_per_pair,
+                            "note": "16*W B/pair streaming model (SURVEY 8d); traffic = measured HBM bytes/launch"}}
+        else:
+            peak = LDS_B32_PEAK_GBS if method == "sketch" else HBM_PEAK_GBS
+            roof = {"bound": "lds" if method == "sketch" else "hbm", "achieved": round(achieved, 1), "peak": peak,
+                    "unit": "GB/s", "frac": round(achieved / peak, 4), "traffic": traffic, "kernel": kname,
+                    "kernel_avg_ms": round(k_avg_ms, 4), "algo_bytes_per_launch": algo_bytes,
+                    "bytes_per_pair": bytes_per_pair}
         # ---------------------------------------------------------------- CPU baseline
         cpu = None
         cpu_opt = None
@@ -235,7 +261,8 @@ def main():
             "config": {"workload": f"{args.config}: {cfg['desc']}", "genomes": N, "genome_length": cfg["length"],
                        "k": cfg["k"], "pairs_per_step": pairs_all, "parallelism": f"rows{world}",
                        "bitset_words_per_set": width_words or None,
-                       "dictionary_size": (dict_size if method == "bitset" else None)},
+                       "dictionary_size": (dict_size if method == "bitset" else None),
+                       "method": method, "auto": auto, "rare_tier": rare},
             "roofline": roof,
             "cpu_baseline": cpu,
             "cpu_optimized": cpu_opt,
@@ -249,32 +276,53 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baselines(cfg, threads):
+def cpu_baselines(cfg, threads, target_s=10.0, cap=6000):
     """The Java-faithful restatement (HashSet<String> + FastaDistanceProcessor
-    loop) on a bounded sample, plus the optimised sorted-merge CPU path."""
+    loop) on a bounded sample, plus the optimised sorted-merge CPU path.
+    Both samples are rows 0..T-1 against the later genomes of a prefix of the
+    workload; the prefix is calibrated so each leg runs ~target_s seconds."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     from gdist import synth
     T = max(1, threads)
-    n_s = T + max(1, T // 2)
-    g = synth.genomes(n_s, cfg["length"], cfg["p_max"], cfg["cfg"], protein=cfg["protein"])
-    seqs = [bytes(r) for r in g]
     kind = 1 if cfg["protein"] else 0
-    t = time.perf_counter()
-    pairs, _ = oracle.faithful_fasta_dist(seqs, cfg["k"], kind, 0, batch=T, max_rows=T, nthreads=T)
-    dt = time.perf_counter() - t
-    faithful = {"value": round(pairs / dt, 3), "unit": "pairs/s", "cores": T, "kind": "port",
-                "sample": f"rows 0..{T - 1} x all later columns of the first {n_s} genomes ({pairs} pairs, "
-                          f"batch {T}: cached rows + per-pair rebuilt sets as FastaDistanceProcessor.java:151-186), "
-                          f"{dt:.1f} s"}
-    off, codes = oracle.pack(seqs, cfg["k"], kind, 0)
-    t = time.perf_counter()
-    I, _ = oracle.matrix(off, codes, 0, n_s, 0, n_s, flags=0x100, nthreads=T)
-    dt2 = time.perf_counter() - t
-    p2 = n_s * (n_s - 1) // 2
+    cap = max(T + 2, min(cap, int(2e8 // cfg["length"])))    # bound the sample's residues too
+
+    def genomes(n):
+        return [bytes(r) for r in synth.genomes(n, cfg["length"], cfg["p_max"], cfg["cfg"], protein=cfg["protein"])]
+
+    def faithful(n):
+        seqs = genomes(n)
+        t = time.perf_counter()
+        pairs, _ = oracle.faithful_fasta_dist(seqs, cfg["k"], kind, 0, batch=T, max_rows=T, nthreads=T)
+        return pairs, time.perf_counter() - t
+
+    def optimised(n):
+        off, codes = oracle.pack(genomes(n), cfg["k"], kind, 0)
+        t = time.perf_counter()
+        oracle.matrix(off, codes, 0, T, 0, n, flags=0x100, nthreads=T)
+        return T * n - T * (T + 1) // 2, time.perf_counter() - t
+
+    def calibrated(run):
+        n = T + max(1, T // 2)
+        pairs, dt = run(n)
+        for _ in range(4):          # fixed costs make small runs look slow: grow in steps
+            if dt >= target_s / 2 or n >= cap:
+                break
+            n = min(cap, max(n + 1, int(n * min(50.0, target_s / max(dt, 1e-3)))))
+            pairs, dt = run(n)
+        return n, pairs, dt
+
+    n1, p1, dt1 = calibrated(faithful)
+    fa = {"value": round(p1 / dt1, 3), "unit": "pairs/s", "cores": T, "kind": "port",
+          "sample": f"rows 0..{T - 1} x all later columns of the first {n1} genomes ({p1} pairs, "
+                    f"batch {T}: cached rows + per-pair rebuilt sets as FastaDistanceProcessor.java:150-186), "
+                    f"{dt1:.1f} s"}
+    n2, p2, dt2 = calibrated(optimised)
     opt = {"value": round(p2 / dt2, 2), "unit": "pairs/s", "cores": T, "kind": "port-optimised",
-           "sample": f"all {p2} pairs of {n_s} genomes, sorted-uint64 merge, OpenMP"}
-    return faithful, opt
+           "sample": f"rows 0..{T - 1} x all later columns of the first {n2} genomes ({p2} pairs), "
+                     f"sorted-uint64 merge, OpenMP, {dt2:.1f} s"}
+    return fa, opt
 
 
 if __name__ == "__main__":

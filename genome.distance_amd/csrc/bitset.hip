@@ -707,6 +707,20 @@ __global__ void local_mass_kernel(const uint64_t* __restrict__ codes, const uint
     }
     if (acc) atomicAdd(out, acc);
 }
+
+// sum over posting lists of m(m-1)/2 (the rare tier's pair increments)
+__global__ void rare_incs_kernel(const int64_t* __restrict__ post_off, int64_t n, unsigned long long* __restrict__ out) {
+    unsigned long long acc = 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; l < n; l += stride) {
+        const unsigned long long m = (unsigned long long)(post_off[l + 1] - post_off[l]);
+        acc += m * (m - 1) / 2;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if ((threadIdx.x & 63) == 0 && acc) atomicAdd(out, acc);
+}
+
 }  // namespace
 
 // records the local sets contribute to the rare tier (local counts of rare codes)
@@ -729,8 +743,9 @@ int64_t bitset_words(int64_t dict_size) {
 
 int64_t auto_rare_threshold(int64_t nsets) {
     // A dense dictionary entry costs one bit column over all N^2/2 pairs; a
-    // rare entry held by m sets costs m(m-1)/2 pair increments. Measured
-    // crossover on MI355X ~ N/80 (tunable: GDIST_RARE_T).
+    // rare entry held by m sets costs m(m-1)/2 pair increments. Cost-model
+    // estimate of the crossover ~ N/80 (C2 sweep:
+    // profiles/r01/sweep_rare_threshold_c2.txt; tunable: GDIST_RARE_T).
     if (const char* e = getenv("GDIST_RARE_T")) return atoll(e);
     return std::max<int64_t>(2, nsets / 80);
 }
@@ -821,12 +836,44 @@ void build_bitsets(gdist_ctx* ctx, gdist_sets* s, unsigned flags, int64_t rare_t
               recs.as<unsigned long long>(), mass, &written);
     GD_REQUIRE(written == mass, "rare-tier record count mismatch");
     build_postings(ctx, s, recs.as<unsigned long long>(), written, Ur);
+    unsigned long long incs = 0;
+    if (s->n_rare > 0) {
+        DevBuf d_incs(8, ctx->stream);
+        GD_HIP(hipMemsetAsync(d_incs.p, 0, 8, ctx->stream));
+        rare_incs_kernel<<<grid_for(s->n_rare, 256, 256 * 64), 256, 0, ctx->stream>>>(
+            s->post_off.as<int64_t>(), s->n_rare, d_incs.as<unsigned long long>());
+        GD_HIP(hipGetLastError());
+        d2h(&incs, d_incs.p, 8, ctx->stream);
+    }
     GD_HIP(hipStreamSynchronize(ctx->stream));
+    s->rare_incs = (int64_t)incs;
     s->W = W;
     s->dict_size = U;
     s->rare_T = T;
     s->rare_records = written;
     s->bits_keep_singletons = keep;
+}
+
+double bitset_cost_s(const gdist_sets* s, double pairs) {
+    // dense tier: ~8.6e12 word pairs/s (0.87 of the measured and+bcnt issue
+    // ceiling, C2); rare tier: ~2.2e10 pair increments/s (C2, C3 rare kernels)
+    const double tot = 0.5 * (double)s->nsets * (double)(s->nsets - 1);
+    const double frac = tot > 0 ? std::min(1.0, pairs / tot) : 1.0;
+    return pairs * (double)s->W / 8.6e12 + frac * (double)s->rare_incs / 2.2e10;
+}
+
+double sorted_cost_s(const gdist_sets* s, double pairs) {
+    // streaming hash join: 8(n_i + n_j) bytes per pair at ~6 TB/s (C3)
+    const double mean_n = s->nsets ? (double)s->total / (double)s->nsets : 0.0;
+    return pairs * 16.0 * mean_n / 6.0e12;
+}
+
+void free_bitsets(gdist_sets* s) {
+    s->bits.release();
+    s->post_off.release();
+    s->post_sets.release();
+    s->W = s->dict_size = 0;
+    s->n_rare = s->rare_T = s->rare_records = s->rare_incs = 0;
 }
 
 void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1,

@@ -371,6 +371,46 @@ int gdist_sets_concat(const gdist_sets* a, const gdist_sets* b, gdist_sets** out
 }
 
 // ---------------------------------------------------------------------------
+// Method resolution (shared by gdist_intersect_matrix and gdist_sets_prepare).
+// AUTO: bitsets when built; otherwise, for a region of >= 2^20 pairs of a
+// collection not yet decided, build the two-tier dictionary and keep it only
+// when its cost estimate beats the sorted join's.
+static int resolve_method(gdist_ctx* ctx, gdist_sets* s, int method, double pairs) {
+    int m = method;
+    if (m == GDIST_METHOD_AUTO) {
+        if (!s->bits.p && !s->auto_sorted && !s->segoff.p && s->has_codes && pairs >= (double)(1 << 20)) {
+            build_bitsets(ctx, s, 0);
+            if (bitset_cost_s(s, pairs) > sorted_cost_s(s, pairs)) {
+                free_bitsets(s);
+                s->auto_sorted = true;
+            }
+        }
+        m = s->bits.p ? GDIST_METHOD_BITSET : GDIST_METHOD_SORTED;
+    }
+    GD_REQUIRE(m == GDIST_METHOD_BITSET || s->has_codes, "this collection holds bitsets only");
+    if (m == GDIST_METHOD_BITSET && !s->bits.p) build_bitsets(ctx, s, 0);
+    if (m == GDIST_METHOD_SORTED && !s->segoff.p) build_segments(ctx, s);
+    return m;
+}
+
+int gdist_sets_prepare(gdist_ctx* ctx, gdist_sets* sets, int method, double pairs, int* chosen,
+                       double* cost_bitset_s, double* cost_sorted_s) {
+    return guard([&] {
+        use_device(ctx);
+        check_sets(sets);
+        GD_REQUIRE(sets->ctx == ctx, "sets belong to another context");
+        GD_REQUIRE(sets->kind != GDIST_SKETCH, "sketch collections have one method");
+        GD_REQUIRE(method >= GDIST_METHOD_AUTO && method <= GDIST_METHOD_BITSET, "unknown method");
+        std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+        if (pairs < 0) pairs = 0.5 * (double)sets->nsets * (double)(sets->nsets - 1);
+        const int m = resolve_method(ctx, sets, method, pairs);
+        if (chosen) *chosen = m;
+        if (cost_bitset_s) *cost_bitset_s = sets->bits.p ? bitset_cost_s(sets, pairs) : -1.0;
+        if (cost_sorted_s) *cost_sorted_s = sorted_cost_s(sets, pairs);
+    });
+}
+
+// ---------------------------------------------------------------------------
 int gdist_intersect_matrix(gdist_ctx* ctx, const gdist_sets* sets, int64_t r0, int64_t r1, int64_t c0, int64_t c1,
                            int method, unsigned flags, int32_t* I_out, double* D_out, int64_t ld) {
     return guard([&] {
@@ -385,11 +425,8 @@ int gdist_intersect_matrix(gdist_ctx* ctx, const gdist_sets* sets, int64_t r0, i
         GD_REQUIRE(method >= GDIST_METHOD_AUTO && method <= GDIST_METHOD_BITSET, "unknown method");
         std::lock_guard<std::recursive_mutex> lk(ctx->mu);
         auto* s = const_cast<gdist_sets*>(sets);
-        int m = method;
-        if (m == GDIST_METHOD_AUTO) m = s->bits.p ? GDIST_METHOD_BITSET : GDIST_METHOD_SORTED;
-        GD_REQUIRE(m == GDIST_METHOD_BITSET || s->has_codes, "this collection holds bitsets only");
-        if (m == GDIST_METHOD_BITSET && !s->bits.p) build_bitsets(ctx, s, 0);
-        if (m == GDIST_METHOD_SORTED && !s->segoff.p) build_segments(ctx, s);
+        const int m = resolve_method(ctx, s, method,
+                                     (double)nr * (double)nc * (flags & GDIST_UPPER_TRIANGLE ? 0.5 : 1.0));
         const bool upper = (flags & GDIST_UPPER_TRIANGLE) != 0;
         const bool dev = (flags & GDIST_OUT_DEVICE) != 0;
         hipStream_t st = ctx->stream;

@@ -142,6 +142,8 @@ struct gdist_sets {
     gdist::DevBuf post_off;               // int64 [n_rare+1]
     gdist::DevBuf post_sets;              // uint32 [rare_records], ascending within a list
     int64_t n_rare = 0, rare_T = 0, rare_records = 0;
+    int64_t rare_incs = 0;                // sum over rare lists of m(m-1)/2 pair increments
+    bool auto_sorted = false;             // METHOD_AUTO measured the sorted join cheaper
 };
 
 namespace gdist {
@@ -178,6 +180,12 @@ void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_
                unsigned long long* bits, const uint64_t* rare, int64_t Ur, int64_t id_base,
                unsigned long long* rare_out, int64_t rare_cap, int64_t* rare_written);
 void build_postings(gdist_ctx* ctx, gdist_sets* s, unsigned long long* recs, int64_t n, int64_t Ur);
+// METHOD_AUTO cost model (seconds per region of `pairs` pairs), calibrated
+// on MI355X: bitset = dense AND+popcount + rare pair increments; sorted =
+// streaming hash join.
+double bitset_cost_s(const gdist_sets* s, double pairs);
+double sorted_cost_s(const gdist_sets* s, double pairs);
+void free_bitsets(gdist_sets* s);
 void build_bitsets(gdist_ctx* ctx, gdist_sets* s, unsigned flags, int64_t rare_threshold = -1);
 void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0,
                    int64_t c1, bool upper, int32_t* d_I, int64_t ldI);

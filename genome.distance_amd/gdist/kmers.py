@@ -217,6 +217,15 @@ class KmerSets(_Handle):
                                                   rare_threshold))
         return self.bitset_info()
 
+    def prepare(self, method: int = L.METHOD_AUTO, pairs: float = -1.0) -> tuple[int, float, float]:
+        """Build the representation `method` needs for `pairs` pairs (-1: the whole
+        triangle); returns (method a matrix call will run, bitset cost estimate s
+        (-1 without bitsets), sorted cost estimate s). See gdist_sets_prepare."""
+        m, cb, cs = C.c_int(), C.c_double(), C.c_double()
+        L.check(L.lib.gdist_sets_prepare(self.ctx.h, self.h, method, float(pairs), C.byref(m), C.byref(cb),
+                                         C.byref(cs)))
+        return m.value, cb.value, cs.value
+
     def rare_info(self) -> tuple[int, int, int]:
         """(threshold T, posting lists, records) of the rare tier."""
         t, n, r = C.c_int64(), C.c_int64(), C.c_int64()

@@ -86,7 +86,9 @@ extern "C" {
                                        (default: Mash bottom-s of the union) */
 
 /* intersection methods */
-#define GDIST_METHOD_AUTO    0
+#define GDIST_METHOD_AUTO    0   /* bitsets if built; for a region of >= 2^20 pairs of a
+                                    collection not yet decided, build the two-tier dictionary
+                                    and keep it when its cost estimate beats the sorted join */
 #define GDIST_METHOD_SORTED  1   /* sorted uint64 sets: LDS hash-join tiles */
 #define GDIST_METHOD_BITSET  2   /* dictionary-rank bitsets: AND + popcount tiles */
 
@@ -151,6 +153,15 @@ int  gdist_sets_bitset_download(const gdist_sets* sets, uint64_t* bits);
 int  gdist_sets_concat(const gdist_sets* a, const gdist_sets* b, gdist_sets** out);
 
 /* ---- distances ------------------------------------------------------- */
+/* Prepare the representation `method` needs for a region of `pairs` pairs
+ * (pairs < 0: the whole N(N-1)/2 triangle) and report the method a later
+ * gdist_intersect_matrix(method) call will run (*chosen: SORTED or BITSET).
+ * With METHOD_AUTO this is where the two-tier dictionary is built and costed;
+ * *cost_bitset_s / *cost_sorted_s (may be NULL) return the model's estimates
+ * (-1 when no bitsets are held). The setup step of FastaDistanceProcessor.java:150-155
+ * (a batch's kmer sets are built and cached before its pair loop). */
+int  gdist_sets_prepare(gdist_ctx* ctx, gdist_sets* sets, int method, double pairs, int* chosen,
+                        double* cost_bitset_s, double* cost_sorted_s);
 /* Pairs (i, j), r0 <= i < r1, c0 <= j < c1 (global set indices of `sets`).
  * I_out[(i-r0)*ld + (j-c0)] = |A_i ∩ A_j|, D_out[...] = distance; either
  * output may be NULL. With GDIST_UPPER_TRIANGLE, entries with j <= i are

@@ -361,6 +361,43 @@ def test_rare_tier_thresholds_exact(ctx, T):
     assert bits_equal(d, eD[0, cols])
 
 
+def test_auto_method_prepare(ctx):
+    """METHOD_AUTO: small regions stay on the sorted join without building a
+    dictionary; a large region of C3-like proteomes (two-tier structure) is
+    costed and runs on bitsets; a diverse collection is costed and falls back
+    to the sorted join (bitsets freed). Every route is bit-exact."""
+    import gdist
+    n = 240
+    seqs = synth_sets(n, 4000, 0.10, 103, protein=True)
+    off, codes = oracle_pack(seqs, 8, 1, 0)
+    eI, eD = oracle.matrix(off, codes, 0, n, 0, n)
+
+    small = gdist.KmerSets.from_sequences(seqs, 8, gdist.KmerType.PROT, 0, ctx)
+    m, cb, cs = small.prepare(gdist.METHOD_AUTO)        # 28,680 pairs < 2^20
+    assert m == gdist.METHOD_SORTED and cb == -1.0 and cs > 0
+    assert small.bitset_info()[1] == 0
+
+    sets = gdist.KmerSets.from_sequences(seqs, 8, gdist.KmerType.PROT, 0, ctx)
+    m, cb, cs = sets.prepare(gdist.METHOD_AUTO, pairs=float(1 << 22))
+    assert m == gdist.METHOD_BITSET and 0 < cb < cs
+    thr, lists, recs = sets.rare_info()
+    assert lists > 0
+    I, D = sets.matrix(method=gdist.METHOD_AUTO)
+    assert np.array_equal(I, eI) and bits_equal(D, eD)
+
+    # unrelated random proteomes: nothing is shared, the dictionary is empty,
+    # yet the model must not pick a path slower than the join; either way exact
+    rnd = [bytes(np.random.default_rng(7 + i).choice(np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", np.uint8), 4000))
+           for i in range(n)]
+    div = gdist.KmerSets.from_sequences(rnd, 8, gdist.KmerType.PROT, 0, ctx)
+    m, cb, cs = div.prepare(gdist.METHOD_AUTO, pairs=float(1 << 22))
+    assert (m == gdist.METHOD_BITSET) == (0 <= cb <= cs)
+    roff, rcodes = oracle_pack(rnd, 8, 1, 0)
+    rI, rD = oracle.matrix(roff, rcodes, 0, n, 0, n)
+    I, D = div.matrix(method=gdist.METHOD_AUTO)
+    assert np.array_equal(I, rI) and bits_equal(D, rD)
+
+
 def test_single_rank_allgather_bitsets(ctx):
     """gdist_sets_allgather_bitsets without a communicator = one rank: same
     counts as the local build (exercises the distributed code path)."""
