@@ -644,11 +644,33 @@ void local_summary(gdist_ctx* ctx, const gdist_sets* s, Summary& out) {
     merge_parts(ctx, parts, out);
 }
 
+namespace {
+// hist[c] += number of summary entries with count c (c <= nsets); small
+// counts (the singletons dominate) go through an LDS histogram first
+constexpr int kHistLds = 4096;
+__global__ void count_hist_kernel(const uint32_t* __restrict__ cnt, int64_t n, int64_t nsets,
+                                  unsigned long long* __restrict__ hist) {
+    __shared__ unsigned int h[kHistLds];
+    for (int t = threadIdx.x; t < kHistLds; t += blockDim.x) h[t] = 0;
+    __syncthreads();
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const int64_t c = cnt[i] < (uint32_t)nsets ? (int64_t)cnt[i] : nsets;
+        if (c < kHistLds) atomicAdd(&h[c], 1u);
+        else atomicAdd(&hist[c], 1ull);
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < kHistLds && t <= nsets; t += blockDim.x)
+        if (h[t]) atomicAdd(&hist[t], (unsigned long long)h[t]);
+}
+
+}  // namespace
+
 // Dictionary tiers from merged summaries: dense = codes held by >= T sets
 // (all codes with keep_singletons), rare = codes held by 2..T-1 sets.
 // rare_mass = number of (code, set) records the rare tier will produce.
-void dictionary_from(gdist_ctx* ctx, const std::vector<SummaryView>& parts, bool keep, int64_t T, DevBuf& dict,
-                     int64_t& U, DevBuf& rare, int64_t& Ur, int64_t& rare_mass) {
+void dictionary_from(gdist_ctx* ctx, const std::vector<SummaryView>& parts, bool keep, int64_t& T, int64_t nsets,
+                     DevBuf& dict, int64_t& U, DevBuf& rare, int64_t& Ur, int64_t& rare_mass) {
     hipStream_t st = ctx->stream;
     Summary all;
     SummaryView m = parts.size() == 1 ? parts[0] : SummaryView{nullptr, nullptr, 0};
@@ -657,6 +679,24 @@ void dictionary_from(gdist_ctx* ctx, const std::vector<SummaryView>& parts, bool
         m = {all.codes.as<uint64_t>(), all.counts.as<uint32_t>(), all.n};
     }
     const int64_t n = m.n;
+    if (keep) T = 0;
+    if (T < 0) {
+        if (const char* e = getenv("GDIST_RARE_T")) {
+            T = atoll(e);
+        } else {
+            DevBuf dh((nsets + 1) * 8, st);
+            GD_HIP(hipMemsetAsync(dh.p, 0, (nsets + 1) * 8, st));
+            if (n) {
+                count_hist_kernel<<<grid_for(n, 256, 256 * 16), 256, 0, st>>>(m.counts, n, nsets,
+                                                                             dh.as<unsigned long long>());
+                GD_HIP(hipGetLastError());
+            }
+            std::vector<uint64_t> hist(nsets + 1);
+            d2h(hist.data(), dh.p, (nsets + 1) * 8, st);
+            GD_HIP(hipStreamSynchronize(st));
+            T = choose_rare_threshold(hist, nsets);
+        }
+    }
     U = Ur = rare_mass = 0;
     DevBuf df(n * 4 + 4, st), rf(n * 4 + 4, st), dpos(n * 8 + 8, st), rpos(n * 8 + 8, st), mass(n * 8 + 8, st),
         cmass(n * 8 + 8, st);
@@ -742,12 +782,29 @@ int64_t bitset_words(int64_t dict_size) {
 }
 
 int64_t auto_rare_threshold(int64_t nsets) {
-    // A dense dictionary entry costs one bit column over all N^2/2 pairs; a
-    // rare entry held by m sets costs m(m-1)/2 pair increments. Cost-model
-    // estimate of the crossover ~ N/80 (C2 sweep:
-    // profiles/r01/sweep_rare_threshold_c2.txt; tunable: GDIST_RARE_T).
-    if (const char* e = getenv("GDIST_RARE_T")) return atoll(e);
+    // Fixed heuristic (before the histogram model): a dense entry costs one
+    // bit column over all N^2/2 pairs, a rare entry held by m sets m(m-1)/2
+    // pair increments; ~N/80 balances them for C2-like collections.
     return std::max<int64_t>(2, nsets / 80);
+}
+
+int64_t choose_rare_threshold(const std::vector<uint64_t>& hist, int64_t nsets) {
+    // cost(T) = pairs * W(dense kmers with count >= T) / dense rate
+    //         + sum_{2 <= c < T} hist[c] * c(c-1)/2 / rare rate
+    // evaluated for every T in [2, nsets+1]; T = 2 is dense-only.
+    const double pairs = 0.5 * (double)nsets * (double)(nsets - 1);
+    const int64_t top = (int64_t)hist.size() - 1;
+    std::vector<double> dense_ge(top + 2, 0.0);
+    for (int64_t c = top; c >= 2; c--) dense_ge[c] = dense_ge[c + 1] + (double)hist[c];
+    double incs = 0.0, best = -1.0;
+    int64_t bestT = 2;
+    for (int64_t T = 2; T <= top + 1; T++) {
+        if (T > 2) incs += (double)hist[T - 1] * (double)(T - 1) * (double)(T - 2) / 2.0;
+        const double U = T <= top ? dense_ge[T] : 0.0;
+        const double cost = pairs * (double)bitset_words((int64_t)U) / kDenseWordPairsPerS + incs / kRareIncsPerS;
+        if (best < 0 || cost < best) { best = cost; bestT = T; }
+    }
+    return bestT;
 }
 
 // bits of sets [0, nsets) against the dense dictionary (chunked pairs sort,
@@ -821,13 +878,13 @@ void build_postings(gdist_ctx* ctx, gdist_sets* s, unsigned long long* recs, int
 
 void build_bitsets(gdist_ctx* ctx, gdist_sets* s, unsigned flags, int64_t rare_threshold) {
     const bool keep = (flags & GDIST_BITSET_KEEP_SINGLETONS) != 0;
-    const int64_t T = keep ? 0 : (rare_threshold < 0 ? auto_rare_threshold(s->nsets) : rare_threshold);
+    int64_t T = keep ? 0 : rare_threshold;     // < 0: cost-optimal from the count histogram
     Summary sum;
     local_summary(ctx, s, sum);
     DevBuf dict, rare;
     int64_t U = 0, Ur = 0, mass = 0;
-    dictionary_from(ctx, {SummaryView{sum.codes.as<uint64_t>(), sum.counts.as<uint32_t>(), sum.n}}, keep, T, dict, U,
-                    rare, Ur, mass);
+    dictionary_from(ctx, {SummaryView{sum.codes.as<uint64_t>(), sum.counts.as<uint32_t>(), sum.n}}, keep, T, s->nsets,
+                    dict, U, rare, Ur, mass);
     const int64_t W = bitset_words(U);
     s->bits.alloc((size_t)s->nsets * W * 8 + 8, ctx->stream);
     DevBuf recs(mass * 8 + 8, ctx->stream);
@@ -859,13 +916,13 @@ double bitset_cost_s(const gdist_sets* s, double pairs) {
     // ceiling, C2); rare tier: ~2.2e10 pair increments/s (C2, C3 rare kernels)
     const double tot = 0.5 * (double)s->nsets * (double)(s->nsets - 1);
     const double frac = tot > 0 ? std::min(1.0, pairs / tot) : 1.0;
-    return pairs * (double)s->W / 8.6e12 + frac * (double)s->rare_incs / 2.2e10;
+    return pairs * (double)s->W / kDenseWordPairsPerS + frac * (double)s->rare_incs / kRareIncsPerS;
 }
 
 double sorted_cost_s(const gdist_sets* s, double pairs) {
     // streaming hash join: 8(n_i + n_j) bytes per pair at ~6 TB/s (C3)
     const double mean_n = s->nsets ? (double)s->total / (double)s->nsets : 0.0;
-    return pairs * 16.0 * mean_n / 6.0e12;
+    return pairs * 16.0 * mean_n / kSortedBytesPerS;
 }
 
 void free_bitsets(gdist_sets* s) {

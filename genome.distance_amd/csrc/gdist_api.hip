@@ -769,8 +769,8 @@ int gdist_sets_allgather_bitsets(gdist_ctx* ctx, const gdist_sets* local, unsign
         }
         DevBuf dict, rare;
         int64_t U = 0, Ur = 0, mass_all = 0;
-        const int64_t T = keep ? 0 : auto_rare_threshold(N);
-        dictionary_from(ctx, parts, keep, T, dict, U, rare, Ur, mass_all);
+        int64_t T = keep ? 0 : -1;                 // cost-optimal from the global count histogram
+        dictionary_from(ctx, parts, keep, T, N, dict, U, rare, Ur, mass_all);
         gc.release(); gn.release();
         const int64_t W = bitset_words(U);
         // 4. local bitsets (padded to the largest shard) + local rare-tier records

@@ -171,18 +171,26 @@ struct SummaryView {
     int64_t n;
 };
 void local_summary(gdist_ctx* ctx, const gdist_sets* s, Summary& out);
-void dictionary_from(gdist_ctx* ctx, const std::vector<SummaryView>& parts, bool keep, int64_t T, DevBuf& dict,
-                     int64_t& U, DevBuf& rare, int64_t& Ur, int64_t& rare_mass);
+// T (in/out): rare-tier threshold; T < 0 picks the cost-optimal one for a
+// collection of nsets sets from the histogram of kmer counts
+void dictionary_from(gdist_ctx* ctx, const std::vector<SummaryView>& parts, bool keep, int64_t& T, int64_t nsets,
+                     DevBuf& dict, int64_t& U, DevBuf& rare, int64_t& Ur, int64_t& rare_mass);
 int64_t bitset_words(int64_t dict_size);
 int64_t local_rare_mass(gdist_ctx* ctx, const Summary& local, const uint64_t* rare, int64_t Ur);
 int64_t auto_rare_threshold(int64_t nsets);
+// cost-optimal rare threshold from hist[c] = number of kmers held by c sets
+// (c = 0..nsets); the chosen T is reported by gdist_sets_rare_info
+int64_t choose_rare_threshold(const std::vector<uint64_t>& hist, int64_t nsets);
 void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_t U, int64_t W,
                unsigned long long* bits, const uint64_t* rare, int64_t Ur, int64_t id_base,
                unsigned long long* rare_out, int64_t rare_cap, int64_t* rare_written);
 void build_postings(gdist_ctx* ctx, gdist_sets* s, unsigned long long* recs, int64_t n, int64_t Ur);
-// METHOD_AUTO cost model (seconds per region of `pairs` pairs), calibrated
-// on MI355X: bitset = dense AND+popcount + rare pair increments; sorted =
-// streaming hash join.
+// Cost model (seconds per region of `pairs` pairs), calibrated on MI355X:
+// bitset = dense AND+popcount + rare pair increments; sorted = streaming hash
+// join. Used by METHOD_AUTO and by the rare-threshold choice.
+constexpr double kDenseWordPairsPerS = 8.6e12;   // 0.87 of the measured and+bcnt ceiling (C2)
+constexpr double kRareIncsPerS = 2.2e10;         // rare_pairs_kernel, C2 and C3
+constexpr double kSortedBytesPerS = 6.0e12;      // sorted_join_kernel streaming, C3
 double bitset_cost_s(const gdist_sets* s, double pairs);
 double sorted_cost_s(const gdist_sets* s, double pairs);
 void free_bitsets(gdist_sets* s);

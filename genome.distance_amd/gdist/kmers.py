@@ -81,11 +81,15 @@ class DeviceBuffer:
         L.check(L.lib.gdist_dev_alloc(ctx.h, int(nbytes), C.byref(p)))
         self.ctx, self.ptr, self.nbytes = ctx, p.value or 0, int(nbytes)
 
-    def to_host(self, dtype, count: int | None = None) -> np.ndarray:
+    def to_host(self, dtype, count: int | None = None, offset: int = 0) -> np.ndarray:
+        """`count` elements of `dtype` starting at element `offset`."""
         dt = np.dtype(dtype)
-        n = self.nbytes // dt.itemsize if count is None else count
+        n = (self.nbytes // dt.itemsize - offset) if count is None else count
+        if offset < 0 or n < 0 or (offset + n) * dt.itemsize > self.nbytes:
+            raise ValueError("read outside the device buffer")
         out = np.empty(n, dtype=dt)
-        L.check(L.lib.gdist_memcpy_d2h(self.ctx.h, out.ctypes.data, self.ptr, n * dt.itemsize))
+        L.check(L.lib.gdist_memcpy_d2h(self.ctx.h, out.ctypes.data, self.ptr + offset * dt.itemsize,
+                                       n * dt.itemsize))
         return out
 
     def from_host(self, a: np.ndarray):
