@@ -169,28 +169,89 @@ __global__ __launch_bounds__(256) void rare_pairs_kernel(const int64_t* __restri
     }
 }
 
-// Rare tier for one query row: colpos[set] = column position or -1.
-__global__ __launch_bounds__(256) void rare_row_kernel(const int64_t* __restrict__ poff,
-                                                       const uint32_t* __restrict__ psets, int64_t nposts, int64_t q,
-                                                       const int32_t* __restrict__ colpos, int32_t* __restrict__ I) {
-    int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < nposts; p += stride) {
-        const int64_t b = poff[p], e = poff[p + 1];
-        bool has = false;
-        for (int64_t x = b; x < e; x++) has |= (psets[x] == (uint32_t)q);
-        if (!has) continue;
-        for (int64_t x = b; x < e; x++) {
-            const int64_t t = psets[x];
-            if (t == q) continue;
-            const int32_t c = colpos[t];
-            if (c >= 0) atomicAdd(I + c, 1);
+// Rare tier, row-major: one workgroup per (row set i, chunk of RCH columns).
+// The row's rare kmers (set -> rare CSR) are walked by the threads; each
+// member j of their posting lists adds 1 to an LDS counter; the counters are
+// then added to I's row once, coalesced. No global atomics, and each (i, j)
+// is owned by exactly one workgroup (the dense kernel ran before, in stream
+// order).
+constexpr int RCH = 16384;   // max columns per LDS chunk (64 KiB of counters)
+
+// grid = nr rows x nch column chunks x nsplit slices of the row's rare kmers;
+// counters live in dynamic LDS sized to the chunk. With nsplit > 1 several
+// workgroups share a row chunk and flush with global atomics.
+__global__ __launch_bounds__(256) void rare_rows_kernel(const int64_t* __restrict__ soff,
+                                                        const uint32_t* __restrict__ sids,
+                                                        const int64_t* __restrict__ poff,
+                                                        const uint32_t* __restrict__ psets, int64_t r0, int64_t r1,
+                                                        int64_t c0, int64_t c1, int nch, int nsplit, int upper,
+                                                        int32_t* __restrict__ I, int64_t ldI) {
+    extern __shared__ int32_t cnt[];
+    const int64_t unit = blockIdx.x / nsplit;
+    const int split = blockIdx.x % nsplit;
+    const int64_t i = r0 + unit / nch;
+    const int ch = (int)(unit % nch);
+    const int64_t cb = c0 + (int64_t)ch * RCH;
+    const int64_t ce = cb + RCH < c1 ? cb + RCH : c1;
+    if (i >= r1 || cb >= ce || (upper && ce - 1 <= i)) return;
+    const int n = (int)(ce - cb);
+    for (int t = threadIdx.x; t < n; t += blockDim.x) cnt[t] = 0;
+    __syncthreads();
+    const int64_t lo = upper && i + 1 > cb ? i + 1 : cb;
+    const int64_t rb = soff[i], re = soff[i + 1];
+    const int64_t per = (re - rb + nsplit - 1) / nsplit;
+    const int64_t xb = rb + per * split;
+    const int64_t xe = xb + per < re ? xb + per : re;
+    for (int64_t x = xb + threadIdx.x; x < xe; x += blockDim.x) {
+        const uint32_t r = sids[x];
+        const int64_t b = poff[r], e = poff[r + 1];
+#pragma unroll 4
+        for (int64_t y = b; y < e; y++) {
+            const int64_t t = psets[y];
+            if (t >= lo && t < ce && t != i) atomicAdd(&cnt[t - cb], 1);
+        }
+    }
+    __syncthreads();
+    int32_t* row = I + (i - r0) * ldI + (cb - c0);
+    for (int t = threadIdx.x; t < n; t += blockDim.x) {
+        const int v = cnt[t];
+        if (v && cb + t >= lo) {
+            if (nsplit > 1) atomicAdd(row + t, v);
+            else row[t] += v;
         }
     }
 }
 
-__global__ void colpos_kernel(const int64_t* __restrict__ cols, int64_t ncols, int32_t* __restrict__ colpos) {
+// Rare tier of one query set q: cnt[t] += shared rare kmers of q and t
+// (global atomics, one row's worth); gather_add adds cnt[cols[c]] to I[c]
+// for every requested column position (duplicates included).
+__global__ __launch_bounds__(256) void rare_query_kernel(const int64_t* __restrict__ soff,
+                                                         const uint32_t* __restrict__ sids,
+                                                         const int64_t* __restrict__ poff,
+                                                         const uint32_t* __restrict__ psets, int64_t q,
+                                                         int32_t* __restrict__ cnt) {
+    const int64_t xb = soff[q], xe = soff[q + 1];
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t x = xb + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < xe; x += stride) {
+        const uint32_t r = sids[x];
+        for (int64_t y = poff[r]; y < poff[r + 1]; y++) {
+            const int64_t t = psets[y];
+            if (t != q) atomicAdd(cnt + t, 1);
+        }
+    }
+}
+
+__global__ void gather_add_kernel(const int64_t* __restrict__ cols, int64_t ncols, const int32_t* __restrict__ cnt,
+                                  int32_t* __restrict__ I) {
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (c < ncols) colpos[cols[c]] = (int32_t)c;
+    if (c < ncols) I[c] += cnt[cols[c]];
+}
+
+// set -> rare CSR: records (rare << 32 | set) become (set << 32 | rare)
+__global__ void swap_halves_kernel(const uint64_t* __restrict__ in, int64_t n, uint64_t* __restrict__ out) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        out[i] = (in[i] << 32) | (in[i] >> 32);
 }
 
 // rare-tier mass: count of records each rare dictionary entry will produce
@@ -517,11 +578,13 @@ void bitset_row(gdist_ctx* ctx, const gdist_sets* s, int64_t q, const int64_t* d
                                                                              q, d_cols, ncols, d_I);
     GD_HIP(hipGetLastError());
     if (s->n_rare > 0) {
-        DevBuf colpos(s->nsets * 4 + 4, ctx->stream);
-        GD_HIP(hipMemsetAsync(colpos.p, 0xFF, s->nsets * 4, ctx->stream));
-        colpos_kernel<<<(unsigned)ceil_div(ncols, 256), 256, 0, ctx->stream>>>(d_cols, ncols, colpos.as<int32_t>());
-        rare_row_kernel<<<grid_for(s->n_rare, 256, 256 * 64), 256, 0, ctx->stream>>>(
-            s->post_off.as<int64_t>(), s->post_sets.as<uint32_t>(), s->n_rare, q, colpos.as<int32_t>(), d_I);
+        DevBuf cnt(s->nsets * 4 + 4, ctx->stream);
+        GD_HIP(hipMemsetAsync(cnt.p, 0, s->nsets * 4, ctx->stream));
+        rare_query_kernel<<<256, 256, 0, ctx->stream>>>(s->srare_off.as<int64_t>(), s->srare_ids.as<uint32_t>(),
+                                                        s->post_off.as<int64_t>(), s->post_sets.as<uint32_t>(), q,
+                                                        cnt.as<int32_t>());
+        gather_add_kernel<<<(unsigned)ceil_div(ncols, 256), 256, 0, ctx->stream>>>(d_cols, ncols, cnt.as<int32_t>(),
+                                                                                   d_I);
         GD_HIP(hipGetLastError());
         GD_HIP(hipStreamSynchronize(ctx->stream));
     }
@@ -859,6 +922,7 @@ void build_postings(gdist_ctx* ctx, gdist_sets* s, unsigned long long* recs, int
     s->n_rare = Ur;
     s->post_off.alloc((Ur + 1) * 8, st);
     s->post_sets.alloc(n * 4 + 4, st);
+    s->rare_incs = 0;
     if (Ur == 0 || n == 0) {
         GD_HIP(hipMemsetAsync(s->post_off.p, 0, (Ur + 1) * 8, st));
         GD_HIP(hipStreamSynchronize(st));
@@ -873,7 +937,28 @@ void build_postings(gdist_ctx* ctx, gdist_sets* s, unsigned long long* recs, int
     posting_offsets_kernel<<<(int)ceil_div(Ur + 1, 256), 256, 0, st>>>(keys, n, Ur, s->post_off.as<int64_t>());
     posting_sets_kernel<<<grid_for(n), 256, 0, st>>>(keys, n, s->post_sets.as<uint32_t>());
     GD_HIP(hipGetLastError());
+    // the same records keyed by set: set -> rare CSR for the row-major kernels
+    swap_halves_kernel<<<grid_for(n), 256, 0, st>>>(keys, n, kalt);
+    GD_HIP(hipGetLastError());
+    int sbits = 1;
+    while ((int64_t(1) << sbits) < s->nsets) sbits++;
+    sort_keys_u64(ctx, kalt, keys, (size_t)n, 0, std::min(64, 32 + sbits));
+    s->srare_off.alloc((s->nsets + 1) * 8, st);
+    s->srare_ids.alloc(n * 4 + 4, st);
+    posting_offsets_kernel<<<(int)ceil_div(s->nsets + 1, 256), 256, 0, st>>>(kalt, n, s->nsets,
+                                                                             s->srare_off.as<int64_t>());
+    posting_sets_kernel<<<grid_for(n), 256, 0, st>>>(kalt, n, s->srare_ids.as<uint32_t>());
+    GD_HIP(hipGetLastError());
+    // pair increments of the tier (cost model, kernel choice)
+    DevBuf d_incs(8, st);
+    GD_HIP(hipMemsetAsync(d_incs.p, 0, 8, st));
+    rare_incs_kernel<<<grid_for(Ur, 256, 256 * 64), 256, 0, st>>>(s->post_off.as<int64_t>(), Ur,
+                                                                  d_incs.as<unsigned long long>());
+    GD_HIP(hipGetLastError());
+    unsigned long long incs = 0;
+    d2h(&incs, d_incs.p, 8, st);
     GD_HIP(hipStreamSynchronize(st));
+    s->rare_incs = (int64_t)incs;
 }
 
 void build_bitsets(gdist_ctx* ctx, gdist_sets* s, unsigned flags, int64_t rare_threshold) {
@@ -893,17 +978,6 @@ void build_bitsets(gdist_ctx* ctx, gdist_sets* s, unsigned flags, int64_t rare_t
               recs.as<unsigned long long>(), mass, &written);
     GD_REQUIRE(written == mass, "rare-tier record count mismatch");
     build_postings(ctx, s, recs.as<unsigned long long>(), written, Ur);
-    unsigned long long incs = 0;
-    if (s->n_rare > 0) {
-        DevBuf d_incs(8, ctx->stream);
-        GD_HIP(hipMemsetAsync(d_incs.p, 0, 8, ctx->stream));
-        rare_incs_kernel<<<grid_for(s->n_rare, 256, 256 * 64), 256, 0, ctx->stream>>>(
-            s->post_off.as<int64_t>(), s->n_rare, d_incs.as<unsigned long long>());
-        GD_HIP(hipGetLastError());
-        d2h(&incs, d_incs.p, 8, ctx->stream);
-    }
-    GD_HIP(hipStreamSynchronize(ctx->stream));
-    s->rare_incs = (int64_t)incs;
     s->W = W;
     s->dict_size = U;
     s->rare_T = T;
@@ -976,8 +1050,29 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     GD_HIP(hipGetLastError());
     ctx->last.launches = 1;
     if (s->n_rare > 0) {
-        rare_pairs_kernel<<<grid_for(s->n_rare, 256, 256 * 64), 256, 0, st>>>(
-            s->post_off.as<int64_t>(), s->post_sets.as<uint32_t>(), s->n_rare, r0, r1, c0, c1, upper ? 1 : 0, d_I, ldI);
+        // Posting-list-major for short lists (C2: ~2 members, one pair and one
+        // global atomic per list); row-major once a record feeds several pair
+        // increments (C3: ~7 per record), where scattered global atomics over
+        // the N x N counts cost more than re-reading lists per member row.
+        // GDIST_RARE_KERNEL=0|1 forces one (A/B).
+        const char* rv = getenv("GDIST_RARE_KERNEL");
+        const bool list_major = rv ? atoi(rv) == 0 : s->rare_incs < 2 * s->rare_records;
+        if (list_major) {
+            rare_pairs_kernel<<<grid_for(s->n_rare, 256, 256 * 64), 256, 0, st>>>(
+                s->post_off.as<int64_t>(), s->post_sets.as<uint32_t>(), s->n_rare, r0, r1, c0, c1, upper ? 1 : 0,
+                d_I, ldI);
+        } else {
+            const int nch = (int)ceil_div(nc, RCH);
+            const int64_t units = nr * nch;
+            // few rows (C2: 1000): slice each row's rare kmers over several workgroups
+            const int nsplit = (int)std::max<int64_t>(1, std::min<int64_t>(16, ceil_div((int64_t)ctx->cus * 8, units)));
+            const int64_t rgrid = units * nsplit;
+            GD_REQUIRE(rgrid < (int64_t(1) << 31), "rare-tier grid too large");
+            const size_t lds = (size_t)std::min<int64_t>(nc, RCH) * 4;
+            rare_rows_kernel<<<(unsigned)rgrid, 256, lds, st>>>(s->srare_off.as<int64_t>(), s->srare_ids.as<uint32_t>(),
+                                                                s->post_off.as<int64_t>(), s->post_sets.as<uint32_t>(),
+                                                                r0, r1, c0, c1, nch, nsplit, upper ? 1 : 0, d_I, ldI);
+        }
         GD_HIP(hipGetLastError());
         ctx->last.launches = 2;
     }

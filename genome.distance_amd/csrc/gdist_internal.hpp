@@ -143,6 +143,8 @@ struct gdist_sets {
     gdist::DevBuf post_sets;              // uint32 [rare_records], ascending within a list
     int64_t n_rare = 0, rare_T = 0, rare_records = 0;
     int64_t rare_incs = 0;                // sum over rare lists of m(m-1)/2 pair increments
+    gdist::DevBuf srare_off;              // int64 [nsets+1]: set -> its rare kmers (CSR)
+    gdist::DevBuf srare_ids;              // uint32 [rare_records], rare ranks ascending within a set
     bool auto_sorted = false;             // METHOD_AUTO measured the sorted join cheaper
 };
 

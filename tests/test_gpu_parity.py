@@ -251,6 +251,24 @@ def test_row_queries(ctx):
     assert far.row_query(0, [1], gdist.QUERY_ARGMIN) == (-1, 1.0)      # NULL_RESULT semantics
 
 
+@pytest.mark.parametrize("T", [0, 8, 1000])
+def test_row_query_repeated_columns(ctx, T):
+    """A column set listed twice gets the same distance at both positions, on
+    the dense and the rare tier (a set's rare counts are gathered per
+    position, not scattered per set)."""
+    import gdist
+    n = 120
+    seqs = synth_sets(n, 5000, 0.01, 104)
+    sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
+    off, codes = oracle_pack(seqs, 21, 0, 0)
+    _, eD = oracle.matrix(off, codes, 0, n, 0, n)
+    sets.build_bitsets(rare_threshold=T)
+    cols = [7, 30, 7, 119, 30, 30, 0, 55]
+    for q in (7, 55, 90):
+        d = sets.row_query(q, cols)
+        assert bits_equal(d, eD[q, cols]), (T, q)
+
+
 def test_sequence_kmers_view_api(ctx):
     import gdist
     a = gdist.KmerType.DNA.createKmers("ACGTTGCAACGTAGCTAGCT", 5)
