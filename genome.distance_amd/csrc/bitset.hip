@@ -1033,7 +1033,27 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     GD_REQUIRE(grid < (int64_t(1) << 31), "bitset matrix grid too large");
     const char* ev = getenv("GDIST_BITSET_KERNEL");   // A/B selection (default: 3)
     const int variant = ev ? atoi(ev) : 3;
+    // Posting-list-major rare kernel for short lists (C2: ~2 members, one pair
+    // and one global atomic per list); row-major once a record feeds several
+    // pair increments (C3: ~7 per record), where scattered global atomics over
+    // the N x N counts cost more than re-reading lists per member row.
+    // GDIST_RARE_KERNEL=0|1 forces one (A/B). The list-major kernel uses
+    // atomics only, like the dense kernel, so it runs beside the dense launch
+    // on the side stream (GDIST_RARE_OVERLAP=0 keeps it in line).
+    const char* rv = getenv("GDIST_RARE_KERNEL");
+    const bool list_major = rv ? atoi(rv) == 0 : s->rare_incs < 2 * s->rare_records;
+    const char* ov = getenv("GDIST_RARE_OVERLAP");
+    const bool overlap = s->n_rare > 0 && list_major && !(ov && atoi(ov) == 0);
     GD_HIP(hipEventRecord(ctx->ev_k0, st));
+    if (overlap) {
+        GD_HIP(hipEventRecord(ctx->ev_fork, st));
+        GD_HIP(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+        rare_pairs_kernel<<<grid_for(s->n_rare, 256, 256 * 64), 256, 0, ctx->side>>>(
+            s->post_off.as<int64_t>(), s->post_sets.as<uint32_t>(), s->n_rare, r0, r1, c0, c1, upper ? 1 : 0, d_I,
+            ldI);
+        GD_HIP(hipGetLastError());
+        GD_HIP(hipEventRecord(ctx->ev_join, ctx->side));
+    }
     if (variant == 1) {
         bitset_tile_kernel<<<(unsigned)grid, NT, 0, st>>>(s->bits.as<unsigned long long>(), s->W, dt.as<int2>(),
                                                            splits, nchunks, r0, r1, c0, c1, upper ? 1 : 0, d_I, ldI);
@@ -1050,14 +1070,9 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     GD_HIP(hipGetLastError());
     ctx->last.launches = 1;
     if (s->n_rare > 0) {
-        // Posting-list-major for short lists (C2: ~2 members, one pair and one
-        // global atomic per list); row-major once a record feeds several pair
-        // increments (C3: ~7 per record), where scattered global atomics over
-        // the N x N counts cost more than re-reading lists per member row.
-        // GDIST_RARE_KERNEL=0|1 forces one (A/B).
-        const char* rv = getenv("GDIST_RARE_KERNEL");
-        const bool list_major = rv ? atoi(rv) == 0 : s->rare_incs < 2 * s->rare_records;
-        if (list_major) {
+        if (overlap) {
+            GD_HIP(hipStreamWaitEvent(st, ctx->ev_join, 0));
+        } else if (list_major) {
             rare_pairs_kernel<<<grid_for(s->n_rare, 256, 256 * 64), 256, 0, st>>>(
                 s->post_off.as<int64_t>(), s->post_sets.as<uint32_t>(), s->n_rare, r0, r1, c0, c1, upper ? 1 : 0,
                 d_I, ldI);
@@ -1081,6 +1096,32 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     if (!upper && hi > lo) {
         self_pairs_kernel<<<(unsigned)ceil_div(hi - lo, 256), 256, 0, st>>>(s->off.as<int64_t>(), lo, hi, r0, c0, d_I,
                                                                              ldI);
+        GD_HIP(hipGetLastError());
+    }
+}
+
+namespace {
+__global__ void zero_upper_kernel(int32_t* __restrict__ I, int64_t ldI, int64_t r0, int64_t c0, int64_t nr, int64_t nc) {
+    const int64_t a = blockIdx.y;
+    const int64_t lo = r0 + a + 1 - c0;                 // first column position with j > i
+    for (int64_t b = (lo > 0 ? lo : 0) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nc;
+         b += (int64_t)gridDim.x * blockDim.x)
+        I[a * ldI + b] = 0;
+}
+}  // namespace
+
+void zero_counts(gdist_ctx* ctx, int64_t r0, int64_t r1, int64_t c0, int64_t c1, bool upper, int32_t* d_I,
+                 int64_t ldI) {
+    const int64_t nr = r1 - r0, nc = c1 - c0;
+    if (nr <= 0 || nc <= 0) return;
+    if (!upper) {
+        GD_HIP(hipMemset2DAsync(d_I, ldI * 4, 0, nc * 4, nr, ctx->stream));
+        return;
+    }
+    for (int64_t a0 = 0; a0 < nr; a0 += 65535) {       // grid.y limit
+        const int64_t rows = std::min<int64_t>(65535, nr - a0);
+        dim3 grid((unsigned)std::min<int64_t>(64, ceil_div(nc, 256)), (unsigned)rows);
+        zero_upper_kernel<<<grid, 256, 0, ctx->stream>>>(d_I + a0 * ldI, ldI, r0 + a0, c0, rows, nc);
         GD_HIP(hipGetLastError());
     }
 }

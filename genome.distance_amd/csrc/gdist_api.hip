@@ -101,13 +101,10 @@ int gdist_ctx_create(int device, gdist_ctx** out) {
         GD_HIP(hipEventCreate(&c->ev_call1));
         GD_HIP(hipEventCreate(&c->ev_k0));
         GD_HIP(hipEventCreate(&c->ev_k1));
+        GD_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+        GD_HIP(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+        GD_HIP(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
         GD_HIP(hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device));
-        // keep stream-ordered allocations cached across calls
-        hipMemPool_t pool;
-        if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
-            uint64_t thr = UINT64_MAX;
-            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
-        }
         *out = c;
     });
 }
@@ -122,6 +119,10 @@ int gdist_ctx_destroy(gdist_ctx* ctx) {
         (void)hipEventDestroy(ctx->ev_call1);
         (void)hipEventDestroy(ctx->ev_k0);
         (void)hipEventDestroy(ctx->ev_k1);
+        (void)hipStreamSynchronize(ctx->side);
+        (void)hipEventDestroy(ctx->ev_fork);
+        (void)hipEventDestroy(ctx->ev_join);
+        (void)hipStreamDestroy(ctx->side);
         (void)hipStreamDestroy(ctx->stream);
         delete ctx;
     });
@@ -447,7 +448,7 @@ int gdist_intersect_matrix(gdist_ctx* ctx, const gdist_sets* sets, int64_t r0, i
             dI = tI.as<int32_t>(); ldI = nc;
         }
         if (m == GDIST_METHOD_BITSET)   // accumulated with atomics
-            GD_HIP(hipMemset2DAsync(dI, ldI * 4, 0, nc * 4, nr, st));
+            zero_counts(ctx, r0, r1, c0, c1, upper && dev, dI, ldI);
         if (m == GDIST_METHOD_BITSET) bitset_matrix(ctx, s, r0, r1, c0, c1, upper, dI, ldI);
         else sorted_matrix(ctx, s, r0, r1, c0, c1, upper, dI, ldI);
         DevBuf tD;

@@ -106,6 +106,8 @@ struct gdist_ctx {
     hipStream_t stream = nullptr;
     std::recursive_mutex mu;
     hipEvent_t ev_call0 = nullptr, ev_call1 = nullptr, ev_k0 = nullptr, ev_k1 = nullptr;
+    hipStream_t side = nullptr;                          // concurrent rare-tier launches
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     gdist::Timing last;
     int cus = 256;
     // RCCL communicator (multi-GPU row sharding)
@@ -213,6 +215,10 @@ void row_epilogue(gdist_ctx* ctx, const gdist_sets* s, int64_t q, const int64_t*
                   unsigned flags, const int32_t* d_I, double* d_D);
 
 // epilogue (bitset.hip): D from I and set sizes, Java expression, fp64
+// zero I over the region, only entries with j > i when upper (the others
+// belong to the caller: gdist.h, GDIST_UPPER_TRIANGLE)
+void zero_counts(gdist_ctx* ctx, int64_t r0, int64_t r1, int64_t c0, int64_t c1, bool upper, int32_t* d_I,
+                 int64_t ldI);
 void distance_epilogue(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0,
                        int64_t c1, bool upper, unsigned flags, const int32_t* d_I, int64_t ldI,
                        double* d_D, int64_t ldD);

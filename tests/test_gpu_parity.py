@@ -230,6 +230,38 @@ def test_device_outputs_and_leading_dimension(ctx):
     assert launches == 1 and 0 < k_ms <= call_ms
 
 
+@pytest.mark.parametrize("method", ["sorted", "bitset", "sketch"])
+def test_device_upper_leaves_lower_untouched(ctx, method):
+    """GDIST_UPPER_TRIANGLE with device outputs: entries with j <= i keep the
+    caller's values (gdist.h), on a row block that straddles the diagonal."""
+    import gdist
+    n, ld = 150, 160
+    seqs = synth_sets(n, 4000, 0.02, 105)
+    sets = gdist.KmerSets.from_sequences(seqs, 15, gdist.KmerType.DNA, 0, ctx)
+    r0, r1, c0, c1 = 40, 110, 10, 150
+    nr = r1 - r0
+    dI, dD = ctx.alloc(nr * ld * 4), ctx.alloc(nr * ld * 8)
+    dI.from_host(np.full(nr * ld, -7, np.int32))
+    dD.from_host(np.full(nr * ld, 42.5))
+    if method == "sketch":
+        sk = sets.sketches(64)
+        sk.matrix_device(dI.ptr, dD.ptr, ld, (r0, r1), (c0, c1), upper=True)
+        eI, eD = sk.matrix((r0, r1), (c0, c1))
+    else:
+        m = gdist.METHOD_SORTED if method == "sorted" else gdist.METHOD_BITSET
+        if method == "bitset":
+            sets.build_bitsets()
+        sets.matrix_device(dI.ptr, dD.ptr, ld, (r0, r1), (c0, c1), upper=True, method=m)
+        eI, eD = sets.matrix((r0, r1), (c0, c1), method=gdist.METHOD_SORTED)
+    I = dI.to_host(np.int32).reshape(nr, ld)[:, :c1 - c0]
+    D = dD.to_host(np.float64).reshape(nr, ld)[:, :c1 - c0]
+    up = np.fromfunction(lambda a, b: (c0 + b) > (r0 + a), (nr, c1 - c0))
+    assert np.all(I[~up] == -7) and np.all(D[~up] == 42.5)
+    assert np.array_equal(I[up], eI[up]) and bits_equal(D[up], eD[up])
+    pad = dI.to_host(np.int32).reshape(nr, ld)[:, c1 - c0:]
+    assert np.all(pad == -7)
+
+
 # ---------------------------------------------------------------- row queries
 def test_row_queries(ctx):
     import gdist
