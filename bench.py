@@ -73,6 +73,10 @@ def main():
     ap.add_argument("--method", default="", choices=["", "auto", "bitset", "sorted"],
                     help="override the config's kernel family (experiments; the config's own is the bench line)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "host"],
+                    help="multi-rank exchange: RCCL (default) or host-staged over gloo (ranks sharing a GPU)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="testing: every rank uses device 0 (rehearse the multi-rank path on one GPU)")
     ap.add_argument("--cpu-threads", type=int, default=8)
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_c2.json"),
                     help="per-launch HBM traffic measured by rocprofv3 PMC passes (optional)")
@@ -95,7 +99,7 @@ def main():
     if args.length:
         cfg["length"] = args.length
     n_total = int(round(cfg["n"] * math.sqrt(world))) if world > 1 else cfg["n"]
-    ctx = gdist.Context(local_rank)
+    ctx = gdist.Context(0 if args.same_device else local_rank)
 
     def barrier():
         ctx.synchronize()
@@ -130,10 +134,20 @@ def main():
     rare = None
     auto = None
     if world > 1:
-        uid = gdist.Context.unique_id() if rank == 0 else None
-        obj = [uid]
-        dist.broadcast_object_list(obj, src=0)
-        ctx.comm_init(obj[0], world, rank)
+        if args.transport == "host":
+            import torch
+
+            def gloo_allgather(a):
+                t = torch.from_numpy(a)
+                outs = [torch.empty_like(t) for _ in range(world)]
+                dist.all_gather(outs, t)
+                return torch.cat(outs).numpy()
+            ctx.comm_init_host(world, rank, gloo_allgather)
+        else:
+            uid = gdist.Context.unique_id() if rank == 0 else None
+            obj = [uid]
+            dist.broadcast_object_list(obj, src=0)
+            ctx.comm_init(obj[0], world, rank)
     if method == "auto":
         # METHOD_AUTO's own decision (gdist_sets_prepare); multi-GPU runs take the
         # dictionary path (its cost needs the global dictionary, built by the all-gather)

@@ -53,6 +53,26 @@ static void use_device(gdist_ctx* ctx) {
     GD_HIP(hipSetDevice(ctx->device));
 }
 
+static bool has_comm(const gdist_ctx* ctx) { return ctx->comm != nullptr || ctx->host_ag != nullptr; }
+
+// The one collective the data path needs: every rank's `bytes` at d_send,
+// gathered in rank order into d_recv (nranks * bytes), stream-ordered on
+// ctx->stream. RCCL over xGMI, or staged through host memory and the
+// caller's all-gather (gdist_comm_init_host).
+static void allgather(gdist_ctx* ctx, const void* d_send, void* d_recv, size_t bytes) {
+    hipStream_t st = ctx->stream;
+    if (ctx->comm) {
+        GD_NCCL(ncclAllGather(d_send, d_recv, bytes, ncclUint8, ctx->comm, st));
+        return;
+    }
+    if (!ctx->host_ag) throw ::gdist::Error(GDIST_ECOMM, "communicator not initialised (gdist_comm_init)");
+    std::vector<char> hs(bytes + 1), hr((size_t)ctx->nranks * bytes + 1);
+    if (bytes) d2h(hs.data(), d_send, bytes, st);
+    if (ctx->host_ag(hs.data(), hr.data(), (int64_t)bytes, ctx->host_user) != 0)
+        throw ::gdist::Error(GDIST_ECOMM, "host all-gather callback failed");
+    if (bytes) h2d(d_recv, hr.data(), (size_t)ctx->nranks * bytes, st);
+}
+
 static void check_sets(const gdist_sets* s) { GD_REQUIRE(s != nullptr && s->ctx != nullptr, "null sets handle"); }
 
 static void finish_timing(gdist_ctx* ctx, bool kernel_recorded) {
@@ -655,7 +675,21 @@ int gdist_comm_init(gdist_ctx* ctx, const char id[GDIST_UNIQUE_ID_BYTES], int nr
         ncclUniqueId u;
         std::memcpy(&u, id, sizeof(u));
         if (ctx->comm) { (void)ncclCommDestroy(ctx->comm); ctx->comm = nullptr; }
+        ctx->host_ag = nullptr;
         GD_NCCL(ncclCommInitRank(&ctx->comm, nranks, u, rank));
+        ctx->nranks = nranks;
+        ctx->rank = rank;
+    });
+}
+
+int gdist_comm_init_host(gdist_ctx* ctx, int nranks, int rank, gdist_allgather_fn fn, void* user) {
+    return guard([&] {
+        use_device(ctx);
+        GD_REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank / world size");
+        GD_REQUIRE(fn != nullptr, "null all-gather callback");
+        if (ctx->comm) { (void)ncclCommDestroy(ctx->comm); ctx->comm = nullptr; }
+        ctx->host_ag = fn;
+        ctx->host_user = user;
         ctx->nranks = nranks;
         ctx->rank = rank;
     });
@@ -666,6 +700,8 @@ int gdist_comm_destroy(gdist_ctx* ctx) {
         use_device(ctx);
         if (ctx->comm) GD_NCCL(ncclCommDestroy(ctx->comm));
         ctx->comm = nullptr;
+        ctx->host_ag = nullptr;
+        ctx->host_user = nullptr;
         ctx->nranks = 1;
         ctx->rank = 0;
     });
@@ -676,7 +712,7 @@ int gdist_sets_allgather(gdist_ctx* ctx, const gdist_sets* local, gdist_sets** o
         use_device(ctx);
         check_sets(local);
         GD_REQUIRE(out, "null output");
-        GD_REQUIRE(ctx->comm, "communicator not initialised (gdist_comm_init)");
+        if (!has_comm(ctx)) throw ::gdist::Error(GDIST_ECOMM, "communicator not initialised (gdist_comm_init)");
         std::lock_guard<std::recursive_mutex> lk(ctx->mu);
         hipStream_t st = ctx->stream;
         const int R = ctx->nranks;
@@ -685,7 +721,7 @@ int gdist_sets_allgather(gdist_ctx* ctx, const gdist_sets* local, gdist_sets** o
         DevBuf mine(16, st), all(16 * R, st);
         int64_t h2[2] = {local->nsets, local->total};
         h2d(mine.p, h2, 16, st);
-        GD_NCCL(ncclAllGather(mine.p, all.p, 2, ncclInt64, ctx->comm, st));
+        allgather(ctx, mine.p, all.p, 16);
         std::vector<int64_t> hall(2 * R);
         d2h(hall.data(), all.p, 16 * R, st);
         GD_HIP(hipStreamSynchronize(st));
@@ -698,8 +734,8 @@ int gdist_sets_allgather(gdist_ctx* ctx, const gdist_sets* local, gdist_sets** o
         DevBuf so((mxs + 1) * 8, st), ao((mxs + 1) * 8 * R, st), sc(mxt * es + 8, st), ac((mxt * es + 8) * R, st);
         GD_HIP(hipMemcpyAsync(so.p, local->off.p, (local->nsets + 1) * 8, hipMemcpyDeviceToDevice, st));
         if (local->total) GD_HIP(hipMemcpyAsync(sc.p, local->codes.p, local->total * es, hipMemcpyDeviceToDevice, st));
-        GD_NCCL(ncclAllGather(so.p, ao.p, (mxs + 1), ncclInt64, ctx->comm, st));
-        GD_NCCL(ncclAllGather(sc.p, ac.p, mxt * es + 8, ncclUint8, ctx->comm, st));
+        allgather(ctx, so.p, ao.p, (mxs + 1) * 8);
+        allgather(ctx, sc.p, ac.p, mxt * es + 8);
         std::vector<int64_t> hoff((mxs + 1) * R);
         d2h(hoff.data(), ao.p, (mxs + 1) * 8 * R, st);
         GD_HIP(hipStreamSynchronize(st));
@@ -732,7 +768,7 @@ int gdist_sets_allgather_bitsets(gdist_ctx* ctx, const gdist_sets* local, unsign
         GD_REQUIRE(local->kind != GDIST_SKETCH && local->has_codes, "local kmer sets with codes required");
         std::lock_guard<std::recursive_mutex> lk(ctx->mu);
         hipStream_t st = ctx->stream;
-        const int R = ctx->comm ? ctx->nranks : 1;
+        const int R = has_comm(ctx) ? ctx->nranks : 1;
         const bool keep = (flags & GDIST_BITSET_KEEP_SINGLETONS) != 0;
         // 1. local dictionary summary
         Summary sum;
@@ -743,7 +779,7 @@ int gdist_sets_allgather_bitsets(gdist_ctx* ctx, const gdist_sets* local, unsign
         if (R > 1) {
             DevBuf mine(16, st), all(16 * R, st);
             h2d(mine.p, hall.data(), 16, st);
-            GD_NCCL(ncclAllGather(mine.p, all.p, 2, ncclInt64, ctx->comm, st));
+            allgather(ctx, mine.p, all.p, 16);
             d2h(hall.data(), all.p, 16 * R, st);
             GD_HIP(hipStreamSynchronize(st));
         }
@@ -760,8 +796,8 @@ int gdist_sets_allgather_bitsets(gdist_ctx* ctx, const gdist_sets* local, unsign
             }
             gc.alloc((mxn * 8 + 8) * R, st);
             gn.alloc((mxn * 4 + 4) * R, st);
-            GD_NCCL(ncclAllGather(sc.p, gc.p, mxn * 8 + 8, ncclUint8, ctx->comm, st));
-            GD_NCCL(ncclAllGather(sn.p, gn.p, mxn * 4 + 4, ncclUint8, ctx->comm, st));
+            allgather(ctx, sc.p, gc.p, mxn * 8 + 8);
+            allgather(ctx, sn.p, gn.p, mxn * 4 + 4);
             for (int r = 0; r < R; r++)
                 parts.push_back({reinterpret_cast<const uint64_t*>((char*)gc.p + (mxn * 8 + 8) * r),
                                  reinterpret_cast<const uint32_t*>((char*)gn.p + (mxn * 4 + 4) * r), hall[2 * r + 1]});
@@ -789,7 +825,7 @@ int gdist_sets_allgather_bitsets(gdist_ctx* ctx, const gdist_sets* local, unsign
         s->bits.alloc((size_t)N * W * 8 + 8, st);
         if (R > 1) {
             DevBuf gb((size_t)mxs * W * 8 * R + 8, st);
-            GD_NCCL(ncclAllGather(lb.p, gb.p, (size_t)mxs * W, ncclUint64, ctx->comm, st));
+            allgather(ctx, lb.p, gb.p, (size_t)mxs * W * 8);
             int64_t at = 0;
             for (int r = 0; r < R; r++) {
                 if (hall[2 * r])
@@ -807,7 +843,7 @@ int gdist_sets_allgather_bitsets(gdist_ctx* ctx, const gdist_sets* local, unsign
         if (R > 1) {
             DevBuf ds((mxs + 1) * 8, st), da((mxs + 1) * 8 * R, st);
             h2d(ds.p, sizes.data(), (mxs + 1) * 8, st);
-            GD_NCCL(ncclAllGather(ds.p, da.p, mxs + 1, ncclInt64, ctx->comm, st));
+            allgather(ctx, ds.p, da.p, (mxs + 1) * 8);
             d2h(allsz.data(), da.p, (mxs + 1) * 8 * R, st);
             GD_HIP(hipStreamSynchronize(st));
         } else {
@@ -828,14 +864,14 @@ int gdist_sets_allgather_bitsets(gdist_ctx* ctx, const gdist_sets* local, unsign
         if (R > 1) {
             DevBuf mw(8, st), aw(8 * R, st);
             h2d(mw.p, &written, 8, st);
-            GD_NCCL(ncclAllGather(mw.p, aw.p, 1, ncclInt64, ctx->comm, st));
+            allgather(ctx, mw.p, aw.p, 8);
             d2h(wr.data(), aw.p, 8 * R, st);
             mxw = 0; totw = 0;
             for (int r = 0; r < R; r++) { mxw = std::max(mxw, wr[r]); totw += wr[r]; }
             DevBuf ga((size_t)(mxw + 1) * 8 * R, st), allrec(totw * 8 + 8, st);
             DevBuf pad((mxw + 1) * 8, st);
             if (written) GD_HIP(hipMemcpyAsync(pad.p, lrec.p, written * 8, hipMemcpyDeviceToDevice, st));
-            GD_NCCL(ncclAllGather(pad.p, ga.p, mxw + 1, ncclUint64, ctx->comm, st));
+            allgather(ctx, pad.p, ga.p, (mxw + 1) * 8);
             int64_t at = 0;
             for (int r = 0; r < R; r++) {
                 if (wr[r])
@@ -858,12 +894,14 @@ int gdist_comm_allreduce_max(gdist_ctx* ctx, double* value) {
     return guard([&] {
         use_device(ctx);
         GD_REQUIRE(value, "null value");
-        if (!ctx->comm) return;
-        DevBuf d(8, ctx->stream);
+        if (!has_comm(ctx)) return;
+        DevBuf d(8, ctx->stream), all(8 * ctx->nranks, ctx->stream);
         h2d(d.p, value, 8, ctx->stream);
-        GD_NCCL(ncclAllReduce(d.p, d.p, 1, ncclFloat64, ncclMax, ctx->comm, ctx->stream));
-        d2h(value, d.p, 8, ctx->stream);
+        allgather(ctx, d.p, all.p, 8);
+        std::vector<double> h(ctx->nranks);
+        d2h(h.data(), all.p, 8 * ctx->nranks, ctx->stream);
         GD_HIP(hipStreamSynchronize(ctx->stream));
+        *value = *std::max_element(h.begin(), h.end());
     });
 }
 

@@ -112,6 +112,8 @@ struct gdist_ctx {
     int cus = 256;
     // RCCL communicator (multi-GPU row sharding)
     ncclComm_t comm = nullptr;
+    gdist_allgather_fn host_ag = nullptr;   // host-staged transport (gdist_comm_init_host)
+    void* host_user = nullptr;
     int nranks = 1, rank = 0;
 };
 

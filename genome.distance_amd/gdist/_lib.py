@@ -81,6 +81,7 @@ _SIGS = {
     "gdist_sketch_matrix": (C.c_int, [_ctxp, _setp, _i64, _i64, _i64, _i64, _u32, _vp, _vp, _i64]),
     "gdist_comm_unique_id": (C.c_int, [C.c_char_p]),
     "gdist_comm_init": (C.c_int, [_ctxp, C.c_char_p, C.c_int, C.c_int]),
+    "gdist_comm_init_host": (C.c_int, [_ctxp, C.c_int, C.c_int, C.c_void_p, _vp]),
     "gdist_comm_destroy": (C.c_int, [_ctxp]),
     "gdist_sets_allgather": (C.c_int, [_ctxp, _setp, C.POINTER(_setp)]),
     "gdist_sets_allgather_bitsets": (C.c_int, [_ctxp, _setp, _u32, C.POINTER(_setp)]),
@@ -94,6 +95,9 @@ for _name, (_res, _args) in _SIGS.items():
     _f.argtypes = _args
 
 EXPORTED = tuple(_SIGS)
+
+# int (*gdist_allgather_fn)(const void* send, void* recv, int64_t bytes, void* user)
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p)
 
 
 def check(rc: int) -> None:

@@ -66,8 +66,28 @@ class Context:
     def comm_init(self, uid: bytes, nranks: int, rank: int) -> None:
         L.check(L.lib.gdist_comm_init(self.h, uid, nranks, rank))
 
+    def comm_init_host(self, nranks: int, rank: int, allgather) -> None:
+        """Host-staged transport (gdist_comm_init_host): `allgather(np.uint8
+        array of n bytes) -> np.uint8 array of nranks * n bytes in rank order`,
+        e.g. torch.distributed.all_gather over gloo. For ranks sharing one GPU
+        (RCCL refuses that) and tests; RCCL is the multi-GPU transport."""
+        def cb(send, recv, nbytes, _user):
+            try:
+                src = np.ctypeslib.as_array((C.c_uint8 * max(int(nbytes), 1)).from_address(send))[:nbytes]
+                out = np.ascontiguousarray(allgather(src.copy()), dtype=np.uint8)
+                if out.nbytes != nbytes * nranks:
+                    return 1
+                if out.nbytes:
+                    C.memmove(recv, out.ctypes.data, out.nbytes)
+                return 0
+            except Exception:
+                return 1
+        self._host_ag = L.ALLGATHER_FN(cb)          # keep the thunk alive
+        L.check(L.lib.gdist_comm_init_host(self.h, nranks, rank, C.cast(self._host_ag, C.c_void_p), None))
+
     def comm_destroy(self) -> None:
         L.check(L.lib.gdist_comm_destroy(self.h))
+        self._host_ag = None
 
     def allreduce_max(self, v: float) -> float:
         x = C.c_double(v)

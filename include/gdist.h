@@ -196,9 +196,17 @@ int  gdist_sketch_matrix(gdist_ctx* ctx, const gdist_sets* sk,
 #define GDIST_UNIQUE_ID_BYTES 128
 int  gdist_comm_unique_id(char id[GDIST_UNIQUE_ID_BYTES]);
 int  gdist_comm_init(gdist_ctx* ctx, const char id[GDIST_UNIQUE_ID_BYTES], int nranks, int rank);
+/* Host-staged communicator: every collective of the library becomes one
+ * all-gather of host buffers through `fn`, which must place the `bytes` of
+ * every rank, in rank order, into recv (nranks * bytes) and return 0. For
+ * ranks that share one GPU (rehearsing the multi-rank path; RCCL refuses two
+ * ranks on one device) or hosts without RCCL peer access; RCCL
+ * (gdist_comm_init) is the transport of a multi-GPU node. */
+typedef int (*gdist_allgather_fn)(const void* send, void* recv, int64_t bytes, void* user);
+int  gdist_comm_init_host(gdist_ctx* ctx, int nranks, int rank, gdist_allgather_fn fn, void* user);
 int  gdist_comm_destroy(gdist_ctx* ctx);
 /* Every rank passes its local shard; every rank receives the concatenation
- * in rank order (one RCCL all-gather of offsets and one of codes). */
+ * in rank order (one all-gather of offsets and one of codes). */
 int  gdist_sets_allgather(gdist_ctx* ctx, const gdist_sets* local, gdist_sets** out);
 /* Dictionary-rank bitsets of the concatenation (in rank order) of every
  * rank's local sets: one all-gather of the local dictionary summaries
