@@ -877,6 +877,7 @@ void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_
                unsigned long long* rare_out, int64_t rare_cap, int64_t* rare_written) {
     hipStream_t st = ctx->stream;
     const int cbits = std::min(64, code_bits(s->kind, s->k, s->flags));
+    Trace tr(st);
     GD_HIP(hipMemsetAsync(bits, 0, (size_t)s->nsets * W * 8, st));
     DevBuf rcnt(8, st);
     GD_HIP(hipMemsetAsync(rcnt.p, 0, 8, st));
@@ -901,11 +902,13 @@ void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_
                 run_rank_kernel<<<(int)ceil_div(nruns, 256), 256, 0, st>>>(keys, start.as<int64_t>(), nruns, dict, U,
                                                                            rare, Ur, rank.as<int64_t>());
                 GD_HIP(hipGetLastError());
+                tr.mark("fill: copy+sort+runs+rank");
                 scatter_bits_kernel<<<grid_for(n), 256, 0, st>>>(ids, flag.as<int32_t>(), pos.as<int64_t>(),
                                                                  rank.as<int64_t>(), n, W, bits, id_base, rare_out,
                                                                  rcnt.as<unsigned long long>(), rare_cap);
                 GD_HIP(hipGetLastError());
                 GD_HIP(hipStreamSynchronize(st));
+                tr.mark("fill: scatter");
             }
             s0 = s1;
         }
@@ -964,20 +967,26 @@ void build_postings(gdist_ctx* ctx, gdist_sets* s, unsigned long long* recs, int
 void build_bitsets(gdist_ctx* ctx, gdist_sets* s, unsigned flags, int64_t rare_threshold) {
     const bool keep = (flags & GDIST_BITSET_KEEP_SINGLETONS) != 0;
     int64_t T = keep ? 0 : rare_threshold;     // < 0: cost-optimal from the count histogram
+    Trace tr(ctx->stream);
     Summary sum;
     local_summary(ctx, s, sum);
+    tr.mark("bitsets: summary");
     DevBuf dict, rare;
     int64_t U = 0, Ur = 0, mass = 0;
     dictionary_from(ctx, {SummaryView{sum.codes.as<uint64_t>(), sum.counts.as<uint32_t>(), sum.n}}, keep, T, s->nsets,
                     dict, U, rare, Ur, mass);
+    tr.mark("bitsets: dictionary");
     const int64_t W = bitset_words(U);
     s->bits.alloc((size_t)s->nsets * W * 8 + 8, ctx->stream);
     DevBuf recs(mass * 8 + 8, ctx->stream);
     int64_t written = 0;
+    tr.mark("bitsets: alloc");
     fill_bits(ctx, s, dict.as<uint64_t>(), U, W, s->bits.as<unsigned long long>(), rare.as<uint64_t>(), Ur, 0,
               recs.as<unsigned long long>(), mass, &written);
+    tr.mark("bitsets: fill");
     GD_REQUIRE(written == mass, "rare-tier record count mismatch");
     build_postings(ctx, s, recs.as<unsigned long long>(), written, Ur);
+    tr.mark("bitsets: postings");
     s->W = W;
     s->dict_size = U;
     s->rare_T = T;

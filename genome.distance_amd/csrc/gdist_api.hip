@@ -22,6 +22,73 @@ static thread_local std::string g_last_error;
 
 void set_last_error(const std::string& msg) { g_last_error = msg; }
 
+// ---------------------------------------------------------------------------
+// caching device allocator (see DevBuf)
+namespace {
+constexpr int kMaxDevices = 64;
+struct BlockCache {
+    std::mutex mu;
+    std::multimap<size_t, void*> free_blocks[kMaxDevices];
+};
+BlockCache& block_cache() {
+    static BlockCache* c = new BlockCache();   // never destroyed: blocks outlive static teardown
+    return *c;
+}
+// size classes: 256 B granules up to 1 MiB, then 8 classes per power of two
+// (<= 12.5 % rounding)
+size_t size_class(size_t n) {
+    if (n <= (size_t(1) << 20)) return (n + 255) & ~size_t(255);
+    size_t p = size_t(1) << (63 - __builtin_clzll((unsigned long long)n));
+    const size_t step = p >> 3;
+    return (n + step - 1) / step * step;
+}
+}  // namespace
+
+void* cache_alloc(int device, size_t bytes, size_t* cls_out) {
+    GD_REQUIRE(device >= 0 && device < kMaxDevices, "device index out of range");
+    const size_t cls = size_class(bytes);
+    *cls_out = cls;
+    auto& c = block_cache();
+    {
+        std::lock_guard<std::mutex> lk(c.mu);
+        auto it = c.free_blocks[device].find(cls);
+        if (it != c.free_blocks[device].end()) {
+            void* p = it->second;
+            c.free_blocks[device].erase(it);
+            return p;
+        }
+    }
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, cls);
+    if (e == hipErrorOutOfMemory) {
+        (void)hipGetLastError();
+        cache_trim(device);
+        e = hipMalloc(&p, cls);
+    }
+    GD_HIP(e);
+    return p;
+}
+
+void cache_free(int device, void* p, size_t cls) {
+    auto& c = block_cache();
+    std::lock_guard<std::mutex> lk(c.mu);
+    c.free_blocks[device].emplace(cls, p);
+}
+
+void cache_trim(int device) {
+    auto& c = block_cache();
+    std::multimap<size_t, void*> blocks;
+    {
+        std::lock_guard<std::mutex> lk(c.mu);
+        blocks.swap(c.free_blocks[device]);
+    }
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(device);
+    for (auto& b : blocks) (void)hipFree(b.second);
+    (void)hipSetDevice(cur);
+}
+
 template <class F>
 static int guard(F&& f) {
     try {
@@ -144,6 +211,7 @@ int gdist_ctx_destroy(gdist_ctx* ctx) {
         (void)hipEventDestroy(ctx->ev_join);
         (void)hipStreamDestroy(ctx->side);
         (void)hipStreamDestroy(ctx->stream);
+        gdist::cache_trim(ctx->device);
         delete ctx;
     });
 }

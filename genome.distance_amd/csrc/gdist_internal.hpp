@@ -8,9 +8,13 @@
 #include <rccl/rccl.h>
 
 #include <cstdint>
+#include <map>
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "../../include/gdist.h"
@@ -41,13 +45,26 @@ void set_last_error(const std::string& msg);
     } while (0)
 
 // ---------------------------------------------------------------------------
-// device buffers. Plain hipMalloc/hipFree: with the stream-ordered pool
-// (hipMallocAsync/hipFreeAsync) reused blocks were intermittently read stale
-// by the next kernels on gfx950 / ROCm 7.2; hipFree
-// drains the device before the block can be handed out again.
+// device buffers.
+//
+// Blocks come from a per-device caching allocator: a released block goes
+// back to a free list keyed by its size class once its stream has drained,
+// and later requests of that class reuse it without calling hipMalloc. On
+// gfx950 / ROCm 7.2 a large hipMalloc that misses the runtime's reuse can
+// stall for seconds (a fresh 16 GiB block: 3 s, scripts/diag/alloc_churn.py),
+// which made the chunked setup paths (pack, dictionary, bitsets) spend 90 % of
+// their time allocating. Reuse only after the owning stream has drained is
+// the same ordering guarantee hipFree gives (the stream-ordered pool,
+// hipMallocAsync/hipFreeAsync, was intermittently unsafe here: DESIGN.md §8).
+void* cache_alloc(int device, size_t bytes, size_t* cls_out);
+void cache_free(int device, void* p, size_t cls);
+void cache_trim(int device);     // hipFree every cached block of the device
+
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
+    size_t cls = 0;               // size class actually held
+    int device = 0;
     hipStream_t stream = nullptr;
     DevBuf() = default;
     DevBuf(size_t n, hipStream_t s) { alloc(n, s); }
@@ -56,8 +73,8 @@ struct DevBuf {
     DevBuf(DevBuf&& o) noexcept { *this = std::move(o); }
     DevBuf& operator=(DevBuf&& o) noexcept {
         release();
-        p = o.p; bytes = o.bytes; stream = o.stream;
-        o.p = nullptr; o.bytes = 0;
+        p = o.p; bytes = o.bytes; cls = o.cls; device = o.device; stream = o.stream;
+        o.p = nullptr; o.bytes = 0; o.cls = 0;
         return *this;
     }
     ~DevBuf() { release(); }
@@ -65,12 +82,19 @@ struct DevBuf {
         release();
         stream = s;
         bytes = n;
-        if (n) GD_HIP(hipMalloc(&p, n));
+        if (n) {
+            GD_HIP(hipGetDevice(&device));
+            p = cache_alloc(device, n, &cls);
+        }
     }
     void release() noexcept {
-        if (p) { (void)hipStreamSynchronize(stream); (void)hipFree(p); }
+        if (p) {
+            (void)hipStreamSynchronize(stream);
+            cache_free(device, p, cls);
+        }
         p = nullptr;
         bytes = 0;
+        cls = 0;
     }
     template <class T> T* as() const { return static_cast<T*>(p); }
 };
@@ -97,6 +121,22 @@ inline void d2h(void* dst, const void* src, size_t bytes, hipStream_t s) {
 struct Timing {
     double kernel_ms = 0.0, call_ms = 0.0;
     int64_t launches = 0;
+};
+
+// Stage timer for setup paths: GDIST_TRACE=1 prints "gdist: <stage> <ms>"
+// to stderr after synchronising the stream (off: no synchronisation, no cost).
+struct Trace {
+    bool on;
+    hipStream_t st;
+    std::chrono::steady_clock::time_point t;
+    explicit Trace(hipStream_t s) : on(getenv("GDIST_TRACE") != nullptr), st(s), t(std::chrono::steady_clock::now()) {}
+    void mark(const char* stage) {
+        if (!on) return;
+        (void)hipStreamSynchronize(st);
+        const auto n = std::chrono::steady_clock::now();
+        fprintf(stderr, "gdist: %-28s %9.1f ms\n", stage, std::chrono::duration<double, std::milli>(n - t).count());
+        t = n;
+    }
 };
 
 }  // namespace gdist

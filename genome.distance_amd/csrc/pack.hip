@@ -330,6 +330,8 @@ void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_se
     }
 
     // 2-4. chunks of sequences, at most kChunk entries each
+    Trace tr(st);
+    tr.mark("pack: validate/fold");
     const int64_t kChunk = int64_t(1) << 30;
     std::vector<DevBuf> chunk_codes;
     std::vector<int64_t> chunk_total;
@@ -364,6 +366,7 @@ void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_se
                     vA.as<int32_t>());
             GD_HIP(hipGetLastError());
         }
+        tr.mark("pack: alloc+extract");
         uint64_t* keys = kA.as<uint64_t>(); uint64_t* keys_alt = kB.as<uint64_t>();
         int32_t* ids = vA.as<int32_t>(); int32_t* ids_alt = vB.as<int32_t>();
         PackDebug* dbg = (s0 == 0) ? g_pack_debug : nullptr;
@@ -374,6 +377,7 @@ void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_se
         while ((int64_t(1) << idbits) <= nc) idbits++;
         sort_pairs_i32_u64(ctx, ids, ids_alt, keys, keys_alt, (size_t)n, idbits);
         if (dbg) { d2h(dbg->k_sort2, keys, n * 8, st); d2h(dbg->v_sort2, ids, n * 4, st); }
+        tr.mark("pack: sort by code, by set");
 
         DevBuf flag(n * 4 + 4, st), pos(n * 8 + 8, st);
         if (n > 0) {
@@ -396,6 +400,7 @@ void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_se
             GD_HIP(hipGetLastError());
         }
         for (int i = 0; i <= nc; i++) h_off[s0 + i] = co[i];
+        tr.mark("pack: unique+compact");
         chunk_codes.push_back(std::move(cc));
         chunk_total.push_back(uniq);
         base += uniq;
@@ -422,6 +427,7 @@ void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_se
         }
     }
     GD_HIP(hipStreamSynchronize(st));
+    tr.mark("pack: concat");
 }
 
 }  // namespace gdist
