@@ -58,3 +58,22 @@ def java_double(d: float) -> str:
 
 def java_doubles(a: np.ndarray) -> list[str]:
     return [java_double(x) for x in np.asarray(a, dtype=np.float64).ravel()]
+
+
+def java_format_f(x: float, width: int, prec: int) -> str:
+    """java.util.Formatter "%<width>.<prec>f" (WidthProcessor.java:193).
+    Java's Formatter (FormattedFloatingDecimal) rounds HALF_UP the decimal
+    digits FloatingDecimal produces for the double, i.e. the shortest
+    round-trip digits, not the exact binary value: "%.3f" of 1.0005 is
+    "1.001" and "%.4f" of 0.03125 is "0.0313" (Python's "%.4f" gives
+    "0.0312"). FloatingDecimal's digit generator is occasionally one digit
+    longer than shortest; that corner is unpinned (no JVM here)."""
+    from decimal import ROUND_HALF_UP, Decimal
+    if math.isnan(x):
+        s = "NaN"
+    elif math.isinf(x):
+        s = "Infinity" if x > 0 else "-Infinity"
+    else:
+        q = Decimal(repr(float(x))).quantize(Decimal(1).scaleb(-prec), rounding=ROUND_HALF_UP)
+        s = f"{q:.{prec}f}"
+    return s.rjust(width)

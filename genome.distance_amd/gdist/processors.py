@@ -8,6 +8,7 @@ row-block / row-query calls on the device:
   genome_distance  GenomeProcessor         (genomes)    GenomeProcessor.java:270-346
   fasta_reps       FastaDistanceRepsProcessor (fastaReps) FastaDistanceRepsProcessor.java:58-149
   distance_reps    DistanceRepsProcessor   (distReps)   DistanceRepsProcessor.java:350-485
+  width_processor  WidthProcessor          (width)      WidthProcessor.java:88-208
 
 Output rows are emitted in (row, column) order; the reference's fastaDist
 order is nondeterministic (rows run in parallel, FastaDistanceProcessor.java:157,188),
@@ -22,7 +23,7 @@ import numpy as np
 
 from . import _lib as L
 from .fasta import Sequence as FastaRecord
-from .javafmt import java_double
+from .javafmt import java_double, java_format_f
 from .kmers import Context, KmerSets, KmerType
 
 
@@ -151,3 +152,89 @@ def distance_reps(genomes: Sequence[Genome], kmer_size: int = 9, max_dist: float
     for r, c in sorted(counts.items(), key=lambda kv: (-kv[1], genomes[kv[0]].id)):   # sortedCounts (:478)
         stats.append(f"{genomes[r].id}\t{genomes[r].name}\t{c}")
     return prefix, "\n".join(lines) + "\n", "\n".join(stats) + "\n"
+
+
+# ----------------------------------------------------------------- width
+INVALID_TARGET_SIZE = 2**31 - 1          # Integer.MAX_VALUE, WidthProcessor.java:53
+
+
+def sketch_sizes(min_size: int, max_size: int, step: int) -> list[int]:
+    """SizeList.getSizes(min, max, step) (WidthProcessor.java:104; the class is
+    in the absent org.theseed jar): min, min+step, ... up to max (inferred)."""
+    return list(range(min_size, max_size + 1, step))
+
+
+def width_process_group(group_id: str, sets: KmerSets, sizes: Sequence[int], out: TextIO,
+                        target_error: float = 0.001) -> int | None:
+    """WidthProcessor.ProcessGroup (WidthProcessor.java:153-208): exact
+    all-pairs on the device, then per sketch size the sketch all-pairs and the
+    relative error |r - s| * 2 / (r + s) over every pair i < j whose distances
+    differ, summed in the reference's i-major order; one output line per size.
+    Returns the smallest size whose mean error meets the target
+    (INVALID_TARGET_SIZE if none), or None for a group with no pair < 1.0."""
+    n = len(sets)
+    _, D = sets.matrix(upper=True)
+    iu = np.triu_indices(n, 1)                      # (i, j) in i-major order
+    real = D[iu]
+    pairs = int(np.count_nonzero(real < 1.0))
+    if pairs == 0:
+        return None
+    min_good = INVALID_TARGET_SIZE
+    for size in sizes:
+        sk = sets.sketches(size)
+        soff, _ = sk.download()
+        dwarves = int(np.count_nonzero(np.diff(soff) < size))
+        _, SD = sk.matrix(upper=True)
+        s = SD[iu]
+        diff = real != s
+        err = np.abs(real[diff] - s[diff]) * 2.0 / (real[diff] + s[diff])
+        total = float(np.cumsum(err)[-1]) if err.size else 0.0     # sequential, as `total += error`
+        max_err = 0.0
+        if err.size:
+            m = float(np.max(err))
+            max_err = m if m > 0.0 else 0.0
+        mean = total / pairs
+        out.write(f"{group_id}\t{size:8d}\t{pairs:8d}\t{dwarves:8d}\t{java_format_f(mean, 8, 4)}\t"
+                  f"{java_format_f(max_err, 8, 4)}\n")
+        if size < min_good and mean <= target_error:
+            min_good = size
+    return min_good
+
+
+def width_processor(rows: Iterable[tuple[str, str]], min_size: int, max_size: int, out: TextIO,
+                    step: int = 10, max_group: int = 1000, target_error: float = 0.001, kmer_size: int = 8,
+                    ctx: Context | None = None) -> int:
+    """WidthProcessor (width): `rows` are (group id, protein sequence) in input
+    order; consecutive rows of one group form a group, split at max_group
+    (WidthProcessor.java:117-131). Validation as validateParms
+    (WidthProcessor.java:88-106). Returns the target sketch size (the largest
+    per-group minimum, INVALID_TARGET_SIZE when some group had none)."""
+    if min_size > max_size:
+        raise ParseFailureException("Minimum sketch size cannot be larger than maximum.")
+    if step <= 0:
+        raise ParseFailureException("Step size must be greater than 0.")
+    if max_group < 10:
+        raise ParseFailureException("Maximum group size must be 10 or greater.")
+    if target_error > 0.1 or target_error <= 0.0:
+        raise ParseFailureException("Target error must be > 0 and < 0.1.")
+    sizes = sketch_sizes(min_size, max_size, step)
+    target = min_size
+    out.write("Group\tSize\tPairs\tDwarves\tMean E\tMax E\n")
+
+    def flush(gid, prots):
+        nonlocal target
+        sets = KmerSets.from_sequences(prots, kmer_size, KmerType.PROT, 0, ctx)
+        good = width_process_group(gid, sets, sizes, out, target_error)
+        if good is not None and good > target:
+            target = good
+
+    group_id, prots = "", []
+    for gid, seq in rows:
+        if gid != group_id or len(prots) >= max_group:
+            if prots:
+                flush(group_id, prots)
+            group_id, prots = gid, []
+        prots.append(seq)
+    if prots:
+        flush(group_id, prots)
+    return target

@@ -461,3 +461,54 @@ def test_single_rank_allgather_bitsets(ctx):
     assert np.array_equal(I, eI) and bits_equal(D, eD)
     with pytest.raises(ValueError):
         ag.matrix(method=gdist.METHOD_SORTED)          # bitset-only collection
+
+
+def test_width_processor_vs_restatement(ctx):
+    """WidthProcessor output (WidthProcessor.java:115-208) against a pure-Python
+    restatement on pyref sets / sketches: same lines, bit for bit."""
+    import gdist
+    from gdist import processors as P
+    from gdist.javafmt import java_format_f
+    g1 = [bytes(r).decode() for r in __import__("gdist").synth.genomes(14, 300, 0.10, 107, protein=True)]
+    g2 = [bytes(r).decode() for r in __import__("gdist").synth.genomes(11, 250, 0.30, 108, protein=True)]
+    rows = [("fam1", s) for s in g1] + [("fam2", s) for s in g2]
+    out = io.StringIO()
+    target = P.width_processor(rows, 20, 60, out, step=20, max_group=12, target_error=0.05, kmer_size=8, ctx=ctx)
+    # restatement: groups of <= 12 consecutive rows of one id
+    exp, tgt = ["Group\tSize\tPairs\tDwarves\tMean E\tMax E"], 20
+    groups, cur, gid = [], [], ""
+    for g, s in rows:
+        if g != gid or len(cur) >= 12:
+            if cur:
+                groups.append((gid, cur))
+            gid, cur = g, []
+        cur.append(s)
+    groups.append((gid, cur))
+    for gid, prots in groups:
+        sets = [pyref.kmer_set(p, 8, pyref.PROT) for p in prots]
+        n = len(sets)
+        real = {(i, j): pyref.set_distance(sets[i], sets[j]) for i in range(n) for j in range(i + 1, n)}
+        pairs = sum(1 for v in real.values() if v < 1.0)
+        if not pairs:
+            continue
+        good = P.INVALID_TARGET_SIZE
+        for size in (20, 40, 60):
+            sk = [pyref.sketch(s, size) for s in sets]
+            dwarves = sum(1 for x in sk if len(x) < size)
+            total, mx = 0.0, 0.0
+            for i in range(n):
+                for j in range(i + 1, n):
+                    sd = pyref.sketch_distance(sk[i], sk[j], size)[0]
+                    r = real[(i, j)]
+                    if r != sd:
+                        e = abs(r - sd) * 2.0 / (r + sd)
+                        mx = e if e > mx else mx
+                        total += e
+            mean = total / pairs
+            exp.append(f"{gid}\t{size:8d}\t{pairs:8d}\t{dwarves:8d}\t{java_format_f(mean, 8, 4)}\t"
+                       f"{java_format_f(mx, 8, 4)}")
+            if size < good and mean <= 0.05:
+                good = size
+        tgt = max(tgt, good)
+    assert out.getvalue().splitlines() == exp
+    assert target == tgt

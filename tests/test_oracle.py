@@ -136,3 +136,25 @@ def test_faithful_path_matches_oracle():
     _, Dm = oracle.matrix(off, codes, 0, 25, 0, 25, flags=0x100)
     iu = np.triu_indices(25, 1)
     assert np.array_equal(D[iu], Dm[iu])
+
+
+def test_java_format_f_half_up_on_shortest_digits():
+    from gdist.javafmt import java_format_f
+    assert java_format_f(0.03125, 8, 4) == "  0.0313"      # Python "%8.4f" gives 0.0312
+    assert java_format_f(1.0005, 8, 3) == "   1.001"       # shortest digits, not the exact binary value
+    assert java_format_f(0.0, 8, 4) == "  0.0000"
+    assert java_format_f(-1e-05, 8, 4) == " -0.0000"
+    assert java_format_f(float("nan"), 8, 4) == "     NaN"
+
+
+def test_width_processor_validation_and_sizes():
+    import pytest
+    from gdist import processors as P
+    assert P.sketch_sizes(50, 100, 25) == [50, 75, 100]
+    assert P.sketch_sizes(50, 60, 20) == [50]
+    for kw, msg in ((dict(min_size=20, max_size=10), "Minimum"), (dict(step=0), "Step"),
+                    (dict(max_group=5), "group size"), (dict(target_error=0.2), "Target")):
+        args = dict(min_size=10, max_size=20)
+        args.update(kw)
+        with pytest.raises(P.ParseFailureException, match=msg):
+            P.width_processor([], out=None, **args)
