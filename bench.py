@@ -53,6 +53,9 @@ CONFIGS = {
     "c3": dict(n=10000, length=33_333, p_max=0.10, protein=True, k=8, method="auto", cfg=3,
                desc="10000 synthetic 33,333-aa proteomes, protein k=8, sorted uint64 sets "
                     "(METHOD_AUTO: two-tier bitsets built from them, or the LDS hash-join)"),
+    "c4": dict(n=100000, length=100_000, p_max=0.05, protein=False, k=21, method="auto", cfg=4,
+               desc="100000 synthetic 100 kbp genomes, DNA k=21 both strands, row-sharded over 8 GPUs "
+                    "(METHOD_AUTO; full size needs the 8-GPU node: use --n for a 1-GPU slice)"),
     "c5": dict(n=50000, length=100_000, p_max=0.05, protein=False, k=21, method="sketch", cfg=5, width=1000,
                desc="50000 MinHash bottom-1000 sketches of 100 kbp genomes (DNA k=21)"),
 }

@@ -859,12 +859,16 @@ int64_t choose_rare_threshold(const std::vector<uint64_t>& hist, int64_t nsets) 
     const int64_t top = (int64_t)hist.size() - 1;
     std::vector<double> dense_ge(top + 2, 0.0);
     for (int64_t c = top; c >= 2; c--) dense_ge[c] = dense_ge[c + 1] + (double)hist[c];
-    double incs = 0.0, best = -1.0;
+    double incs = 0.0, recs = 0.0, best = -1.0;
     int64_t bestT = 2;
     for (int64_t T = 2; T <= top + 1; T++) {
-        if (T > 2) incs += (double)hist[T - 1] * (double)(T - 1) * (double)(T - 2) / 2.0;
+        if (T > 2) {
+            incs += (double)hist[T - 1] * (double)(T - 1) * (double)(T - 2) / 2.0;
+            recs += (double)hist[T - 1] * (double)(T - 1);
+        }
         const double U = T <= top ? dense_ge[T] : 0.0;
-        const double cost = pairs * (double)bitset_words((int64_t)U) / kDenseWordPairsPerS + incs / kRareIncsPerS;
+        const double cost = pairs * (double)bitset_words((int64_t)U) / kDenseWordPairsPerS +
+                            (incs > 0 ? incs / rare_rate(incs, recs) : 0.0);
         if (best < 0 || cost < best) { best = cost; bestT = T; }
     }
     return bestT;
@@ -999,7 +1003,8 @@ double bitset_cost_s(const gdist_sets* s, double pairs) {
     // ceiling, C2); rare tier: ~2.2e10 pair increments/s (C2, C3 rare kernels)
     const double tot = 0.5 * (double)s->nsets * (double)(s->nsets - 1);
     const double frac = tot > 0 ? std::min(1.0, pairs / tot) : 1.0;
-    return pairs * (double)s->W / kDenseWordPairsPerS + frac * (double)s->rare_incs / kRareIncsPerS;
+    const double incs = (double)s->rare_incs, recs = (double)s->rare_records;
+    return pairs * (double)s->W / kDenseWordPairsPerS + (incs > 0 ? frac * incs / rare_rate(incs, recs) : 0.0);
 }
 
 double sorted_cost_s(const gdist_sets* s, double pairs) {
@@ -1050,7 +1055,7 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     // atomics only, like the dense kernel, so it runs beside the dense launch
     // on the side stream (GDIST_RARE_OVERLAP=0 keeps it in line).
     const char* rv = getenv("GDIST_RARE_KERNEL");
-    const bool list_major = rv ? atoi(rv) == 0 : s->rare_incs < 2 * s->rare_records;
+    const bool list_major = rv ? atoi(rv) == 0 : !rare_row_major((double)s->rare_incs, (double)s->rare_records);
     const char* ov = getenv("GDIST_RARE_OVERLAP");
     const bool overlap = s->n_rare > 0 && list_major && !(ov && atoi(ov) == 0);
     GD_HIP(hipEventRecord(ctx->ev_k0, st));

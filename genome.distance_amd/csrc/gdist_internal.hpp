@@ -235,7 +235,14 @@ void build_postings(gdist_ctx* ctx, gdist_sets* s, unsigned long long* recs, int
 // bitset = dense AND+popcount + rare pair increments; sorted = streaming hash
 // join. Used by METHOD_AUTO and by the rare-threshold choice.
 constexpr double kDenseWordPairsPerS = 8.6e12;   // 0.87 of the measured and+bcnt ceiling (C2)
-constexpr double kRareIncsPerS = 2.2e10;         // rare_pairs_kernel, C2 and C3
+constexpr double kRareIncsPerS = 2.2e10;         // list-major rare_pairs_kernel (C2)
+constexpr double kRareRowIncsPerS = 6.5e10;      // row-major rare_rows_kernel (C3, C4 slice)
+// the rare kernel a tier gets (bitset_matrix): row-major once a record feeds
+// several pair increments
+inline bool rare_row_major(double incs, double records) { return incs >= 2.0 * records; }
+inline double rare_rate(double incs, double records) {
+    return rare_row_major(incs, records) ? kRareRowIncsPerS : kRareIncsPerS;
+}
 constexpr double kSortedBytesPerS = 6.0e12;      // sorted_join_kernel streaming, C3
 double bitset_cost_s(const gdist_sets* s, double pairs);
 double sorted_cost_s(const gdist_sets* s, double pairs);
