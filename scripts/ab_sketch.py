@@ -1,5 +1,5 @@
 """A/B of sketch merge windows (GDIST_SKETCH_K: kN), tile shapes
-(GDIST_SKETCH_TILE: tN) and LDS row stride (GDIST_SKETCH_EVEN: even) in ONE process on the C5 workload: every variant's common
+(GDIST_SKETCH_TILE: tN) LDS row stride (GDIST_SKETCH_EVEN: even) in ONE process on the C5 workload: every variant's common
 counts on a row block are checked identical to the first variant's, then the
 full upper triangle is timed in interleaved rounds."""
 import os, sys, time
@@ -27,6 +27,7 @@ def apply(v):
             os.environ["GDIST_SKETCH_TILE"] = part[1:]
         elif part == "even":
             os.environ["GDIST_SKETCH_EVEN"] = "1"
+
 
 
 ctx = gdist.Context(0)
