@@ -407,7 +407,51 @@ __device__ __forceinline__ void dma_chunk(const unsigned long long* __restrict__
 // dependent chain per accumulator). ORDER 1: two column fragments at once,
 // dword-outer, so consecutive v_and/v_bcnt pairs belong to 16 different
 // accumulators and no instruction waits on its predecessor.
-template <int ORDER>
+// One staged chunk (KC2 words of 128 row sets and 128 column sets) into the
+// thread's 8x8 accumulators. DIAG: the tile sits on the diagonal of an
+// upper-triangle region, where accumulator (r, c) holds pairs with j > i only
+// when c >= r (rows ty + 16r, columns tx + 16c): the c < r ones (28 of 64) are
+// never computed.
+template <int ORDER, bool DIAG>
+__device__ __forceinline__ void chunk_pairs(const unsigned char* A, const unsigned char* B, int ty, int tx,
+                                            uint32_t (&acc)[8][8]) {
+#pragma unroll 1
+    for (int q = 0; q < KC2 / 2; q++) {
+        uint4 a[8];
+#pragma unroll
+        for (int r = 0; r < 8; r++) a[r] = *reinterpret_cast<const uint4*>(A + lds_off2(ty + 16 * r, q));
+        if (ORDER == 0) {
+#pragma unroll
+            for (int c = 0; c < 8; c++) {
+                const uint4 bv = *reinterpret_cast<const uint4*>(B + lds_off2(tx + 16 * c, q));
+#pragma unroll
+                for (int r = 0; r < 8; r++)
+                    if (!DIAG || c >= r) acc[r][c] = and_popc(a[r], bv, acc[r][c]);
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < 8; c += 2) {
+                const uint4 b0 = *reinterpret_cast<const uint4*>(B + lds_off2(tx + 16 * c, q));
+                const uint4 b1 = *reinterpret_cast<const uint4*>(B + lds_off2(tx + 16 * (c + 1), q));
+                const uint32_t bw0[4] = {b0.x, b0.y, b0.z, b0.w};
+                const uint32_t bw1[4] = {b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+                for (int d = 0; d < 4; d++) {
+#pragma unroll
+                    for (int r = 0; r < 8; r++) {
+                        const uint32_t ad = d == 0 ? a[r].x : d == 1 ? a[r].y : d == 2 ? a[r].z : a[r].w;
+                        if (!DIAG || c >= r) acc[r][c] = bcnt_acc(ad & bw0[d], acc[r][c]);
+                        if (!DIAG || c + 1 >= r) acc[r][c + 1] = bcnt_acc(ad & bw1[d], acc[r][c + 1]);
+                    }
+                }
+            }
+        }
+    }
+}
+
+// DIAG: every tile of the launch sits on the diagonal of an upper-triangle
+// region (bitset_matrix launches those tiles separately).
+template <int ORDER, bool DIAG>
 __global__ __launch_bounds__(NT, 4) void bitset_tile_kernel2(
     const unsigned long long* __restrict__ bits, int64_t W, const int2* __restrict__ tiles, int ntiles, int splits,
     int64_t nchunks, int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I,
@@ -453,37 +497,7 @@ __global__ __launch_bounds__(NT, 4) void bitset_tile_kernel2(
         } else {
             asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
         }
-#pragma unroll 1
-        for (int q = 0; q < KC2 / 2; q++) {
-            uint4 a[8];
-#pragma unroll
-            for (int r = 0; r < 8; r++) a[r] = *reinterpret_cast<const uint4*>(A + lds_off2(ty + 16 * r, q));
-            if (ORDER == 0) {
-#pragma unroll
-                for (int c = 0; c < 8; c++) {
-                    const uint4 bv = *reinterpret_cast<const uint4*>(B + lds_off2(tx + 16 * c, q));
-#pragma unroll
-                    for (int r = 0; r < 8; r++) acc[r][c] = and_popc(a[r], bv, acc[r][c]);
-                }
-            } else {
-#pragma unroll
-                for (int c = 0; c < 8; c += 2) {
-                    const uint4 b0 = *reinterpret_cast<const uint4*>(B + lds_off2(tx + 16 * c, q));
-                    const uint4 b1 = *reinterpret_cast<const uint4*>(B + lds_off2(tx + 16 * (c + 1), q));
-                    const uint32_t bw0[4] = {b0.x, b0.y, b0.z, b0.w};
-                    const uint32_t bw1[4] = {b1.x, b1.y, b1.z, b1.w};
-#pragma unroll
-                    for (int d = 0; d < 4; d++) {
-#pragma unroll
-                        for (int r = 0; r < 8; r++) {
-                            const uint32_t ad = d == 0 ? a[r].x : d == 1 ? a[r].y : d == 2 ? a[r].z : a[r].w;
-                            acc[r][c] = bcnt_acc(ad & bw0[d], acc[r][c]);
-                            acc[r][c + 1] = bcnt_acc(ad & bw1[d], acc[r][c + 1]);
-                        }
-                    }
-                }
-            }
-        }
+        chunk_pairs<ORDER, DIAG>(A, B, ty, tx, acc);
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // stage free for the next DMA
     }
 
@@ -1073,13 +1087,33 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
                                                            splits, nchunks, r0, r1, c0, c1, upper ? 1 : 0, d_I, ldI);
     } else {
         const int64_t nch2 = s->W / KC2;
-        const int64_t target2 = (int64_t)ctx->cus * 16;
-        const int sp2 = (int)std::max<int64_t>(1, std::min<int64_t>(nch2, ceil_div(target2, (int64_t)tiles.size())));
-        const int64_t grid2 = (int64_t)tiles.size() * sp2;
-        GD_REQUIRE(grid2 < (int64_t(1) << 31), "bitset matrix grid too large");
-        auto k2 = variant == 2 ? bitset_tile_kernel2<0> : bitset_tile_kernel2<1>;
-        k2<<<(unsigned)grid2, NT, 0, st>>>(s->bits.as<unsigned long long>(), s->W, dt.as<int2>(), (int)tiles.size(),
-                                           sp2, nch2, r0, r1, c0, c1, upper ? 1 : 0, d_I, ldI);
+        // Diagonal tiles of an upper-triangle region (row0 == col0) get their
+        // own launch of the DIAG variant, which skips the accumulators that
+        // only hold pairs with j <= i (GDIST_BITSET_DIAG=0 keeps one launch).
+        const char* dv = getenv("GDIST_BITSET_DIAG");
+        const bool split_diag = upper && r0 == c0 && !(dv && atoi(dv) == 0);
+        std::vector<int2> off_t, diag_t;
+        for (const int2& tt : tiles) ((split_diag && tt.x == tt.y) ? diag_t : off_t).push_back(tt);
+        DevBuf dt2((off_t.size() + diag_t.size()) * sizeof(int2) + 8, st);
+        if (!off_t.empty()) h2d(dt2.p, off_t.data(), off_t.size() * sizeof(int2), st);
+        if (!diag_t.empty())
+            h2d(dt2.as<int2>() + off_t.size(), diag_t.data(), diag_t.size() * sizeof(int2), st);
+        auto launch = [&](auto kern, const int2* dtiles, size_t nt) {
+            if (nt == 0) return;
+            const int64_t target2 = (int64_t)ctx->cus * 16;
+            const int sp2 = (int)std::max<int64_t>(1, std::min<int64_t>(nch2, ceil_div(target2, (int64_t)nt)));
+            const int64_t grid2 = (int64_t)nt * sp2;
+            GD_REQUIRE(grid2 < (int64_t(1) << 31), "bitset matrix grid too large");
+            kern<<<(unsigned)grid2, NT, 0, st>>>(s->bits.as<unsigned long long>(), s->W, dtiles, (int)nt, sp2, nch2,
+                                                 r0, r1, c0, c1, upper ? 1 : 0, d_I, ldI);
+        };
+        if (variant == 2) {
+            launch(bitset_tile_kernel2<0, false>, dt2.as<int2>(), off_t.size());
+            launch(bitset_tile_kernel2<0, true>, dt2.as<int2>() + off_t.size(), diag_t.size());
+        } else {
+            launch(bitset_tile_kernel2<1, false>, dt2.as<int2>(), off_t.size());
+            launch(bitset_tile_kernel2<1, true>, dt2.as<int2>() + off_t.size(), diag_t.size());
+        }
     }
     GD_HIP(hipGetLastError());
     ctx->last.launches = 1;
