@@ -1098,9 +1098,12 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
         if (!off_t.empty()) h2d(dt2.p, off_t.data(), off_t.size() * sizeof(int2), st);
         if (!diag_t.empty())
             h2d(dt2.as<int2>() + off_t.size(), diag_t.data(), diag_t.size() * sizeof(int2), st);
+        // workgroups per CU the K-split aims for (GDIST_BITSET_WG_PER_CU, A/B)
+        const char* wv = getenv("GDIST_BITSET_WG_PER_CU");
+        const int64_t wg_per_cu = wv ? std::max(1, atoi(wv)) : 16;
         auto launch = [&](auto kern, const int2* dtiles, size_t nt) {
             if (nt == 0) return;
-            const int64_t target2 = (int64_t)ctx->cus * 16;
+            const int64_t target2 = (int64_t)ctx->cus * wg_per_cu;
             const int sp2 = (int)std::max<int64_t>(1, std::min<int64_t>(nch2, ceil_div(target2, (int64_t)nt)));
             const int64_t grid2 = (int64_t)nt * sp2;
             GD_REQUIRE(grid2 < (int64_t(1) << 31), "bitset matrix grid too large");
