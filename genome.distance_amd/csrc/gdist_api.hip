@@ -568,6 +568,24 @@ int gdist_intersect_matrix(gdist_ctx* ctx, const gdist_sets* sets, int64_t r0, i
     });
 }
 
+int gdist_greedy_reps(gdist_ctx* ctx, const gdist_sets* sets, int method, double max_dist, const int64_t* tie_rank,
+                      int32_t* is_rep, int64_t* rep_of, double* rep_dist, int64_t* nreps) {
+    return guard([&] {
+        use_device(ctx);
+        check_sets(sets);
+        GD_REQUIRE(sets->ctx == ctx, "sets belong to another context");
+        GD_REQUIRE(sets->kind != GDIST_SKETCH, "representatives are chosen on kmer sets");
+        GD_REQUIRE(is_rep != nullptr, "is_rep is required");
+        GD_REQUIRE(method >= GDIST_METHOD_AUTO && method <= GDIST_METHOD_BITSET, "unknown method");
+        std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+        auto* s = const_cast<gdist_sets*>(sets);
+        const int64_t n = s->nsets;
+        const int m = resolve_method(ctx, s, method, (double)n * (double)n);
+        ctx->last = Timing{};
+        greedy_reps(ctx, s, m, max_dist, tie_rank, is_rep, rep_of, rep_dist, nreps);
+    });
+}
+
 int gdist_row_query(gdist_ctx* ctx, const gdist_sets* sets, int64_t q, const int64_t* cols, int64_t ncols, int mode,
                     double t, double* D_out, int32_t* hit, int64_t* best_idx, double* best_d) {
     return guard([&] {

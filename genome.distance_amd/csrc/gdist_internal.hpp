@@ -264,6 +264,8 @@ void row_epilogue(gdist_ctx* ctx, const gdist_sets* s, int64_t q, const int64_t*
                   unsigned flags, const int32_t* d_I, double* d_D);
 
 // epilogue (bitset.hip): D from I and set sizes, Java expression, fp64
+void greedy_reps(gdist_ctx* ctx, gdist_sets* s, int method, double t, const int64_t* tie_rank, int32_t* is_rep,
+                 int64_t* rep_of, double* rep_dist, int64_t* nreps);
 // zero I over the region, only entries with j > i when upper (the others
 // belong to the caller: gdist.h, GDIST_UPPER_TRIANGLE)
 void zero_counts(gdist_ctx* ctx, int64_t r0, int64_t r1, int64_t c0, int64_t c1, bool upper, int32_t* d_I,

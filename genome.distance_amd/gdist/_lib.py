@@ -74,6 +74,7 @@ _SIGS = {
     "gdist_sets_concat": (C.c_int, [_setp, _setp, C.POINTER(_setp)]),
     "gdist_sets_prepare": (C.c_int, [_ctxp, _setp, C.c_int, _dbl, C.POINTER(C.c_int), _dblp, _dblp]),
     "gdist_intersect_matrix": (C.c_int, [_ctxp, _setp, _i64, _i64, _i64, _i64, C.c_int, _u32, _vp, _vp, _i64]),
+    "gdist_greedy_reps": (C.c_int, [_ctxp, _setp, C.c_int, _dbl, _i64p, _i32p, _i64p, _dblp, _i64p]),
     "gdist_row_query": (C.c_int, [_ctxp, _setp, _i64, _i64p, _i64, C.c_int, _dbl, _dblp, _i32p, _i64p, _dblp]),
     "gdist_sketch_build": (C.c_int, [_ctxp, _setp, C.c_int, C.POINTER(_setp)]),
     "gdist_sketch_upload": (C.c_int, [_ctxp, C.c_int, _i64, _i64p, _i32p, C.POINTER(_setp)]),

@@ -250,6 +250,29 @@ class KmerSets(_Handle):
                                          C.byref(cs)))
         return m.value, cb.value, cs.value
 
+    def greedy_reps(self, max_dist: float, assign: bool = False, tie_rank: np.ndarray | None = None,
+                    method: int = L.METHOD_AUTO):
+        """Greedy representatives on the device (gdist_greedy_reps). Returns
+        is_rep (int32[N]); with assign=True also (rep_of int64[N], rep_dist
+        float64[N]): each set's closest representative, ties to the lowest
+        tie_rank (default: index)."""
+        n = len(self)
+        is_rep = np.zeros(max(n, 1), dtype=np.int32)
+        nreps = C.c_int64()
+        rep_of = np.zeros(max(n, 1), dtype=np.int64) if assign else None
+        rep_d = np.zeros(max(n, 1), dtype=np.float64) if assign else None
+        tr = None
+        if tie_rank is not None:
+            tr = np.ascontiguousarray(tie_rank, dtype=np.int64)
+            assert tr.shape == (n,)
+        L.check(L.lib.gdist_greedy_reps(self.ctx.h, self.h, method, float(max_dist),
+                                        L.ptr(tr, C.c_int64) if tr is not None else None, L.ptr(is_rep, C.c_int32),
+                                        L.ptr(rep_of, C.c_int64) if assign else None,
+                                        L.ptr(rep_d, C.c_double) if assign else None, C.byref(nreps)))
+        if assign:
+            return is_rep[:n], rep_of[:n], rep_d[:n]
+        return is_rep[:n]
+
     def rare_info(self) -> tuple[int, int, int]:
         """(threshold T, posting lists, records) of the rare tier."""
         t, n, r = C.c_int64(), C.c_int64(), C.c_int64()

@@ -102,49 +102,121 @@ def genome_distance(base: Sequence[Genome], others: Sequence[Sequence[Genome]], 
     return n
 
 
+def java_string_hash(s: str) -> int:
+    """java.lang.String.hashCode (UTF-16 code units, int32 wrap-around)."""
+    b = s.encode("utf-16-be")
+    h = 0
+    for i in range(0, len(b), 2):
+        h = (31 * h + ((b[i] << 8) | b[i + 1])) & 0xFFFFFFFF
+    return h - (1 << 32) if h & 0x80000000 else h
+
+
+def java_hashmap_order(keys: Sequence[str]) -> list[int]:
+    """Iteration order of a java.util.HashMap<String, V> into which `keys`
+    (distinct) were put in order: bucket (h ^ h >>> 16) & (cap - 1), cap the
+    table size after the 0.75-load resizes from 16; insertion order within a
+    bucket (resizes split bins keeping it). The reps processors iterate
+    repMap.values() in this order (DistanceRepsProcessor.java:190,236,
+    FastaDistanceRepsProcessor.java:124). Tree bins (>= 8 keys in one bucket
+    of a table >= 64) are not modelled."""
+    n = len(keys)
+    cap = 16
+    while n > cap * 3 // 4:
+        cap *= 2
+    def bucket(s):
+        h = java_string_hash(s) & 0xFFFFFFFF
+        return (h ^ (h >> 16)) & (cap - 1)
+    return sorted(range(n), key=lambda i: (bucket(keys[i]), i))
+
+
+def _greedy_host(sets: KmerSets, keys: Sequence[str], max_dist: float) -> list[int]:
+    """Pass 1 with the reference's repMap semantics, one row query per set:
+    a new representative whose key is already in repMap replaces the old one
+    (HashMap.put), keeping that key's slot. Returns the representatives in
+    insertion-key order (index of the set each key now maps to)."""
+    rep_of_key: dict[str, int] = {}
+    for i, key in enumerate(keys):
+        reps = list(rep_of_key.values())
+        if reps and sets.row_query(i, reps, L.QUERY_ANY_LE, max_dist):
+            continue
+        rep_of_key[key] = i
+    return list(rep_of_key.values())
+
+
+def _greedy(sets: KmerSets, keys: Sequence[str], max_dist: float) -> list[int]:
+    """Pass 1: on the device when keys are unique (gdist_greedy_reps),
+    otherwise the host loop with HashMap.put replacement."""
+    if len(set(keys)) == len(keys):
+        is_rep = sets.greedy_reps(max_dist)
+        return [int(i) for i in np.flatnonzero(is_rep)]
+    return _greedy_host(sets, keys, max_dist)
+
+
 def fasta_reps(records: Sequence[FastaRecord], out: TextIO, kmer_size: int = 0, max_dist: float = 0.97,
                kmer_type: KmerType = KmerType.DNA, flags: int = 0, ctx: Context | None = None) -> list[int]:
-    """fastaReps: greedy representatives in input order (sequential early exit)."""
+    """fastaReps (FastaDistanceRepsProcessor.java:111-149): greedy
+    representatives in input order; one output line per new representative
+    (a repeated label re-enters repMap under its key and is printed again)."""
     k = kmer_size or kmer_type.getKmerSize()
     if k < 2:
         raise ParseFailureException("Kmer size must be at least 2.")           # :96-97
-    out.write("seq\tname\n")                                                    # :121
+    out.write("seq\tname\n")                                                  # :121
     if not records:
         return []
     sets = KmerSets.from_sequences([r.sequence for r in records], k, kmer_type, flags, ctx)
-    reps: list[int] = []
-    for i, r in enumerate(records):
-        # any(rep distance <= maxDist) — order-independent boolean (:124-133)
-        if reps and sets.row_query(i, reps, L.QUERY_ANY_LE, max_dist):
-            continue
-        reps.append(i)
-        out.write(f"{r.label}\t{r.comment}\n")                                  # :139-141
+    labels = [r.label for r in records]
+    if len(set(labels)) == len(labels):
+        reps = _greedy(sets, labels, max_dist)
+        printed = reps
+    else:
+        # replayed on the host to print every put, including replacements
+        printed, rep_of_key = [], {}
+        for i, key in enumerate(labels):
+            cur = list(rep_of_key.values())
+            if cur and sets.row_query(i, cur, L.QUERY_ANY_LE, max_dist):
+                continue
+            rep_of_key[key] = i
+            printed.append(i)
+        reps = list(rep_of_key.values())
+    for i in printed:
+        out.write(f"{records[i].label}\t{records[i].comment}\n")            # :139-141
     return reps
 
 
 def distance_reps(genomes: Sequence[Genome], kmer_size: int = 9, max_dist: float = 0.97, flags: int = 0,
                   ctx: Context | None = None) -> tuple[str, str, str]:
-    """distReps: returns (file name prefix, list.tbl text, stats.tbl text)."""
+    """distReps (DistanceRepsProcessor.java:350-485): returns (file name
+    prefix, list.tbl text, stats.tbl text). Pass 1 picks representatives in
+    input order; pass 2 assigns every genome its closest representative,
+    ties to the earlier one in repMap's HashMap iteration order."""
     if kmer_size < 4:
         raise ParseFailureException("Kmer size must be at least 4.")           # :366-367
     if max_dist <= 0.0 or max_dist >= 1.0:
         raise ParseFailureException("Distance must be strictly between 0 and 1.")  # :370-371
     prefix = "rep%.4f_K%d" % (max_dist, kmer_size)                              # :422
     sets = KmerSets.from_sequences([g.kmer_text() for g in genomes], kmer_size, KmerType.DNA, flags, ctx)
-    reps: list[int] = []
-    for i in range(len(genomes)):                                               # pass 1 (:395-411)
-        if reps and sets.row_query(i, reps, L.QUERY_ANY_LE, max_dist):
-            continue
-        reps.append(i)
+    ids = [g.id for g in genomes]
+    reps = _greedy(sets, ids, max_dist)                                         # pass 1 (:185-200)
     rep_set = set(reps)
+    # repMap iteration order (keys = genome ids, put in pass-1 order)
+    order = java_hashmap_order([ids[r] for r in reps])
+    ordered_reps = [reps[o] for o in order]
     lines = ["genome_id\tgenome_name\trep_id\trep_name\tdistance"]
     counts: dict[int, int] = {}
-    for i, g in enumerate(genomes):                                             # pass 2 (:430-470)
+    unique = len(set(ids)) == len(ids)
+    if unique and reps:
+        rank = np.full(len(genomes), len(genomes), dtype=np.int64)
+        for pos, r in enumerate(ordered_reps):
+            rank[r] = pos
+        _, rep_of, rep_d = sets.greedy_reps(max_dist, assign=True, tie_rank=rank)
+    for i, g in enumerate(genomes):                                             # pass 2 (:227-262)
         if i in rep_set:
             r, d = i, 0.0
+        elif unique:
+            r, d = int(rep_of[i]), float(rep_d[i])
         else:
-            pos, d = sets.row_query(i, reps, L.QUERY_ARGMIN)
-            r = reps[pos]
+            pos, d = sets.row_query(i, ordered_reps, L.QUERY_ARGMIN)
+            r = ordered_reps[pos]
         rg = genomes[r]
         lines.append(f"{g.id}\t{g.name}\t{rg.id}\t{rg.name}\t{java_double(d)}")
         counts[r] = counts.get(r, 0) + 1

@@ -170,6 +170,19 @@ int  gdist_intersect_matrix(gdist_ctx* ctx, const gdist_sets* sets,
                             int64_t r0, int64_t r1, int64_t c0, int64_t c1,
                             int method, unsigned flags,
                             int32_t* I_out, double* D_out, int64_t ld);
+/* Greedy representatives over the whole collection, on the device.
+ * Pass 1 (DistanceRepsProcessor.java:185-200, FastaDistanceRepsProcessor.java:
+ * 117-144): sets in index order; set k becomes a representative unless an
+ * earlier representative lies within max_dist (d <= max_dist); is_rep[k] =
+ * 1 / 0, *nreps = their number. Keys are assumed unique (the reference's
+ * repMap.put would replace a representative with the same id).
+ * Pass 2, when rep_of or rep_dist is non-NULL (DistanceRepsProcessor.java:
+ * 227-237): every set's closest representative, ties to the lowest
+ * tie_rank (NULL: index), d < 1.0 only (NULL_RESULT identity); a
+ * representative maps to itself at 0.0; -1 / 1.0 when none. */
+int  gdist_greedy_reps(gdist_ctx* ctx, const gdist_sets* sets, int method, double max_dist,
+                       const int64_t* tie_rank, int32_t* is_rep, int64_t* rep_of, double* rep_dist,
+                       int64_t* nreps);
 /* One query set q against ncols sets (indices cols[]):
  *  ALL:    D_out[c] for every c
  *  ANY_LE: *hit = 1 if any distance <= t (D_out may be NULL)

@@ -379,6 +379,76 @@ def test_genome_and_reps_processors(ctx):
         assert row[2] in rep_ids and row[4] == pyref.java_double_str(0.0 if i in reps else d)
 
 
+@pytest.mark.parametrize("block", [None, "100", "37"])
+def test_greedy_reps_device(ctx, block, monkeypatch):
+    """gdist_greedy_reps: pass 1 equals the sequential loop of row queries
+    (DistanceRepsProcessor.java:185-200) for one block and several; pass 2
+    equals the argmin over representatives of the exact distances, ties to
+    the lowest tie rank, on a collection with duplicated genomes (exact ties)."""
+    import gdist
+    if block:
+        monkeypatch.setenv("GDIST_REPS_BLOCK", block)
+    base = synth_sets(150, 3000, 0.15, 109)
+    seqs = base + [base[i] for i in (3, 17, 40, 41, 99)]           # duplicates -> ties
+    n = len(seqs)
+    sets = gdist.KmerSets.from_sequences(seqs, 15, gdist.KmerType.DNA, 0, ctx)
+    _, D = sets.matrix(method=gdist.METHOD_SORTED)
+    for t in (0.3, 0.6):
+        reps = []
+        for k in range(n):
+            if not any(D[k, r] <= t for r in reps):
+                reps.append(k)
+        for method in (gdist.METHOD_SORTED, gdist.METHOD_BITSET):
+            is_rep = sets.greedy_reps(t, method=method)
+            assert [int(i) for i in np.flatnonzero(is_rep)] == reps, (t, method)
+        rank = np.random.default_rng(5).permutation(n).astype(np.int64)
+        is_rep, rep_of, rep_d = sets.greedy_reps(t, assign=True, tie_rank=rank)
+        for k in range(n):
+            if k in reps:
+                assert rep_of[k] == k and rep_d[k] == 0.0
+                continue
+            cand = [r for r in reps if D[k, r] < 1.0]
+            best = min(cand, key=lambda r: (D[k, r], rank[r]))
+            assert rep_of[k] == best and bits_equal(rep_d[k], D[k, best]), (t, k)
+
+
+def test_reps_processors_java_semantics(ctx):
+    """distReps breaks pass-2 ties in repMap's HashMap order; fastaReps with a
+    repeated label replaces the representative under that key (HashMap.put)."""
+    import gdist
+    from gdist import processors as P
+    base = synth_sets(12, 2000, 0.4, 110)
+    seqs = base + [base[2], base[2], base[5]]
+    ids = [f"fig|{1000 + 37 * i}.peg.{i}" for i in range(len(seqs))]
+    gens = [P.Genome(ids[i], f"n{i}", [s.decode()]) for i, s in enumerate(seqs)]
+    _, lst, _ = P.distance_reps(gens, kmer_size=12, max_dist=0.6, ctx=ctx)
+    ks = [pyref.kmer_set(s.decode(), 12) for s in seqs]
+    reps = []
+    for i in range(len(seqs)):
+        if not any(pyref.set_distance(ks[r], ks[i]) <= 0.6 for r in reps):
+            reps.append(i)
+    order = [reps[o] for o in P.java_hashmap_order([ids[r] for r in reps])]
+    rows = [l.split("\t") for l in lst.splitlines()[1:]]
+    for i, row in enumerate(rows):
+        if i in reps:
+            assert row[2] == ids[i] and row[4] == "0.0"
+            continue
+        best, bd = None, 1.0                    # reduce(NULL_RESULT, merge): left wins ties
+        for r in order:
+            d = pyref.set_distance(ks[i], ks[r])
+            if not (bd <= d):
+                best, bd = r, d
+        assert row[2] == ids[best] and row[4] == pyref.java_double_str(bd), i
+    # fastaReps, repeated label
+    recs = [gdist.Sequence("a", "x0", "ACGTACGTTTGACCAGT" * 8), gdist.Sequence("b", "x1", "TTTTGGGGCCCCAAAA" * 8),
+            gdist.Sequence("a", "x2", "GATTACAGATTACAGG" * 8), gdist.Sequence("c", "x3", "ACGTACGTTTGACCAGT" * 8)]
+    out = io.StringIO()
+    reps = P.fasta_reps(recs, out, kmer_size=8, max_dist=0.5, ctx=ctx)
+    # "a" (x0) is replaced by x2 under key "a", so x3 (equal to x0) finds no representative
+    assert out.getvalue().splitlines() == ["seq\tname", "a\tx0", "b\tx1", "a\tx2", "c\tx3"]
+    assert reps == [2, 1, 3]
+
+
 # ---------------------------------------------------------------- two-tier dictionary
 @pytest.mark.parametrize("T", [0, 3, 8, 1000])
 def test_rare_tier_thresholds_exact(ctx, T):

@@ -158,3 +158,16 @@ def test_width_processor_validation_and_sizes():
         args.update(kw)
         with pytest.raises(P.ParseFailureException, match=msg):
             P.width_processor([], out=None, **args)
+
+
+def test_java_string_hash_and_hashmap_order():
+    from gdist.processors import java_hashmap_order, java_string_hash
+    assert java_string_hash("hello") == 99162322
+    assert java_string_hash("") == 0
+    assert java_string_hash("Aa") == java_string_hash("BB") == 2112
+    assert java_string_hash("polygenelubricants") == -2147483648        # a known Integer.MIN_VALUE hash
+    # 3 keys: table of 16, buckets (h ^ h>>>16) & 15, insertion order within a bucket
+    keys = ["b", "a", "Aa", "BB"]
+    assert java_hashmap_order(keys) == sorted(range(4), key=lambda i: ((java_string_hash(keys[i]) & 0xFFFFFFFF ^
+                                                                         (java_string_hash(keys[i]) & 0xFFFFFFFF) >> 16) & 15, i))
+    assert java_hashmap_order(["Aa", "BB"]) == [0, 1] and java_hashmap_order(["BB", "Aa"]) == [0, 1]
