@@ -461,13 +461,14 @@ int gdist_sets_concat(const gdist_sets* a, const gdist_sets* b, gdist_sets** out
 
 // ---------------------------------------------------------------------------
 // Method resolution (shared by gdist_intersect_matrix and gdist_sets_prepare).
-// AUTO: bitsets when built; otherwise, for a region of >= 2^20 pairs of a
-// collection not yet decided, build the two-tier dictionary and keep it only
-// when its cost estimate beats the sorted join's.
+// AUTO: bitsets when built; otherwise, when the sorted join would take more
+// than ~20 ms on the region (small regions of small sets stay on the join
+// without building anything), build the two-tier dictionary and keep it
+// only when its cost estimate beats the sorted join's.
 static int resolve_method(gdist_ctx* ctx, gdist_sets* s, int method, double pairs) {
     int m = method;
     if (m == GDIST_METHOD_AUTO) {
-        if (!s->bits.p && !s->auto_sorted && !s->segoff.p && s->has_codes && pairs >= (double)(1 << 20)) {
+        if (!s->bits.p && !s->auto_sorted && !s->segoff.p && s->has_codes && sorted_cost_s(s, pairs) >= 0.02) {
             build_bitsets(ctx, s, 0);
             if (bitset_cost_s(s, pairs) > sorted_cost_s(s, pairs)) {
                 free_bitsets(s);

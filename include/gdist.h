@@ -86,9 +86,9 @@ extern "C" {
                                        (default: Mash bottom-s of the union) */
 
 /* intersection methods */
-#define GDIST_METHOD_AUTO    0   /* bitsets if built; for a region of >= 2^20 pairs of a
-                                    collection not yet decided, build the two-tier dictionary
-                                    and keep it when its cost estimate beats the sorted join */
+#define GDIST_METHOD_AUTO    0   /* bitsets if built; when the sorted join's estimate for the
+                                    region exceeds ~20 ms, build the two-tier dictionary and
+                                    keep it when its cost estimate beats the sorted join */
 #define GDIST_METHOD_SORTED  1   /* sorted uint64 sets: LDS hash-join tiles */
 #define GDIST_METHOD_BITSET  2   /* dictionary-rank bitsets: AND + popcount tiles */
 

@@ -493,7 +493,7 @@ def test_auto_method_prepare(ctx):
     eI, eD = oracle.matrix(off, codes, 0, n, 0, n)
 
     small = gdist.KmerSets.from_sequences(seqs, 8, gdist.KmerType.PROT, 0, ctx)
-    m, cb, cs = small.prepare(gdist.METHOD_AUTO)        # 28,680 pairs < 2^20
+    m, cb, cs = small.prepare(gdist.METHOD_AUTO)        # sorted estimate ~0.3 ms < 20 ms
     assert m == gdist.METHOD_SORTED and cb == -1.0 and cs > 0
     assert small.bitset_info()[1] == 0
 
