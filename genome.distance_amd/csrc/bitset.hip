@@ -181,8 +181,7 @@ constexpr int RCH = 16384;   // max columns per LDS chunk (64 KiB of counters)
 // counters live in dynamic LDS sized to the chunk. With nsplit > 1 several
 // workgroups share a row chunk and flush with global atomics.
 __global__ __launch_bounds__(256) void rare_rows_kernel(const int64_t* __restrict__ soff,
-                                                        const uint32_t* __restrict__ sids,
-                                                        const int64_t* __restrict__ poff,
+                                                        const uint64_t* __restrict__ sent,
                                                         const uint32_t* __restrict__ psets, int64_t r0, int64_t r1,
                                                         int64_t c0, int64_t c1, int nch, int nsplit, int upper,
                                                         int32_t* __restrict__ I, int64_t ldI) {
@@ -203,8 +202,8 @@ __global__ __launch_bounds__(256) void rare_rows_kernel(const int64_t* __restric
     const int64_t xb = rb + per * split;
     const int64_t xe = xb + per < re ? xb + per : re;
     for (int64_t x = xb + threadIdx.x; x < xe; x += blockDim.x) {
-        const uint32_t r = sids[x];
-        const int64_t b = poff[r], e = poff[r + 1];
+        const uint64_t ent = sent[x];                  // coalesced: no random bounds lookup
+        const int64_t b = (int64_t)(ent >> 24), e = b + (int64_t)(ent & 0xFFFFFFu);
 #pragma unroll 4
         for (int64_t y = b; y < e; y++) {
             const int64_t t = psets[y];
@@ -226,15 +225,15 @@ __global__ __launch_bounds__(256) void rare_rows_kernel(const int64_t* __restric
 // (global atomics, one row's worth); gather_add adds cnt[cols[c]] to I[c]
 // for every requested column position (duplicates included).
 __global__ __launch_bounds__(256) void rare_query_kernel(const int64_t* __restrict__ soff,
-                                                         const uint32_t* __restrict__ sids,
-                                                         const int64_t* __restrict__ poff,
+                                                         const uint64_t* __restrict__ sent,
                                                          const uint32_t* __restrict__ psets, int64_t q,
                                                          int32_t* __restrict__ cnt) {
     const int64_t xb = soff[q], xe = soff[q + 1];
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t x = xb + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < xe; x += stride) {
-        const uint32_t r = sids[x];
-        for (int64_t y = poff[r]; y < poff[r + 1]; y++) {
+        const uint64_t ent = sent[x];
+        const int64_t b = (int64_t)(ent >> 24), e = b + (int64_t)(ent & 0xFFFFFFu);
+        for (int64_t y = b; y < e; y++) {
             const int64_t t = psets[y];
             if (t != q) atomicAdd(cnt + t, 1);
         }
@@ -245,6 +244,17 @@ __global__ void gather_add_kernel(const int64_t* __restrict__ cols, int64_t ncol
                                   int32_t* __restrict__ I) {
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c < ncols) I[c] += cnt[cols[c]];
+}
+
+// set-side entries: rare rank -> (list start << 24 | list length)
+__global__ void rare_entries_kernel(const uint64_t* __restrict__ keys, int64_t n, const int64_t* __restrict__ poff,
+                                    uint64_t* __restrict__ ent) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint32_t r = (uint32_t)keys[i];
+        const int64_t b = poff[r];
+        ent[i] = ((uint64_t)b << 24) | (uint64_t)(poff[r + 1] - b);
+    }
 }
 
 // set -> rare CSR: records (rare << 32 | set) become (set << 32 | rare)
@@ -594,9 +604,8 @@ void bitset_row(gdist_ctx* ctx, const gdist_sets* s, int64_t q, const int64_t* d
     if (s->n_rare > 0) {
         DevBuf cnt(s->nsets * 4 + 4, ctx->stream);
         GD_HIP(hipMemsetAsync(cnt.p, 0, s->nsets * 4, ctx->stream));
-        rare_query_kernel<<<256, 256, 0, ctx->stream>>>(s->srare_off.as<int64_t>(), s->srare_ids.as<uint32_t>(),
-                                                        s->post_off.as<int64_t>(), s->post_sets.as<uint32_t>(), q,
-                                                        cnt.as<int32_t>());
+        rare_query_kernel<<<256, 256, 0, ctx->stream>>>(s->srare_off.as<int64_t>(), s->srare_ent.as<uint64_t>(),
+                                                        s->post_sets.as<uint32_t>(), q, cnt.as<int32_t>());
         gather_add_kernel<<<(unsigned)ceil_div(ncols, 256), 256, 0, ctx->stream>>>(d_cols, ncols, cnt.as<int32_t>(),
                                                                                    d_I);
         GD_HIP(hipGetLastError());
@@ -964,11 +973,14 @@ void build_postings(gdist_ctx* ctx, gdist_sets* s, unsigned long long* recs, int
     int sbits = 1;
     while ((int64_t(1) << sbits) < s->nsets) sbits++;
     sort_keys_u64(ctx, kalt, keys, (size_t)n, 0, std::min(64, 32 + sbits));
+    // packed entries: 40-bit list start, 24-bit length (a rare list has < T <= N + 1 sets)
+    GD_REQUIRE(n < (int64_t(1) << 40) && s->nsets < (int64_t(1) << 24), "rare tier too large for packed list entries");
     s->srare_off.alloc((s->nsets + 1) * 8, st);
-    s->srare_ids.alloc(n * 4 + 4, st);
+    s->srare_ent.alloc(n * 8 + 8, st);
     posting_offsets_kernel<<<(int)ceil_div(s->nsets + 1, 256), 256, 0, st>>>(kalt, n, s->nsets,
                                                                              s->srare_off.as<int64_t>());
-    posting_sets_kernel<<<grid_for(n), 256, 0, st>>>(kalt, n, s->srare_ids.as<uint32_t>());
+    rare_entries_kernel<<<grid_for(n), 256, 0, st>>>(kalt, n, s->post_off.as<int64_t>(),
+                                                     s->srare_ent.as<uint64_t>());
     GD_HIP(hipGetLastError());
     // pair increments of the tier (cost model, kernel choice)
     DevBuf d_incs(8, st);
@@ -1135,9 +1147,9 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
             const int64_t rgrid = units * nsplit;
             GD_REQUIRE(rgrid < (int64_t(1) << 31), "rare-tier grid too large");
             const size_t lds = (size_t)std::min<int64_t>(nc, RCH) * 4;
-            rare_rows_kernel<<<(unsigned)rgrid, 256, lds, st>>>(s->srare_off.as<int64_t>(), s->srare_ids.as<uint32_t>(),
-                                                                s->post_off.as<int64_t>(), s->post_sets.as<uint32_t>(),
-                                                                r0, r1, c0, c1, nch, nsplit, upper ? 1 : 0, d_I, ldI);
+            rare_rows_kernel<<<(unsigned)rgrid, 256, lds, st>>>(s->srare_off.as<int64_t>(), s->srare_ent.as<uint64_t>(),
+                                                                s->post_sets.as<uint32_t>(), r0, r1, c0, c1, nch,
+                                                                nsplit, upper ? 1 : 0, d_I, ldI);
         }
         GD_HIP(hipGetLastError());
         ctx->last.launches = 2;

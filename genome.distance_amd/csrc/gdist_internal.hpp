@@ -188,7 +188,8 @@ struct gdist_sets {
     int64_t n_rare = 0, rare_T = 0, rare_records = 0;
     int64_t rare_incs = 0;                // sum over rare lists of m(m-1)/2 pair increments
     gdist::DevBuf srare_off;              // int64 [nsets+1]: set -> its rare kmers (CSR)
-    gdist::DevBuf srare_ids;              // uint32 [rare_records], rare ranks ascending within a set
+    gdist::DevBuf srare_ent;              // uint64 [rare_records]: the set's rare lists as
+                                          // (list start << 24 | list length), by rare rank
     bool auto_sorted = false;             // METHOD_AUTO measured the sorted join cheaper
 };
 
