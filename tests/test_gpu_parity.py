@@ -449,6 +449,34 @@ def test_reps_processors_java_semantics(ctx):
     assert reps == [2, 1, 3]
 
 
+@pytest.mark.parametrize("strand", [0, 0x1, 0x2])
+def test_k32_all_ones_code(ctx, strand):
+    """DNA k=32 uses all 64 code bits: the poly-T kmer is ~0, the sorted
+    join's empty-slot sentinel (handled by its has-empty-key flag). Every
+    path must count it like any other kmer."""
+    import gdist
+    rng = np.random.default_rng(111)
+    polyT = "T" * 40
+    seqs = []
+    for i in range(24):
+        body = "".join(rng.choice(list("ACGT"), 300))
+        seqs.append((body[:150] + (polyT if i % 3 else "") + body[150:] + ("A" * 33 if i % 4 == 0 else "")).encode())
+    off, codes = oracle_pack(seqs, 32, 0, strand)
+    # canonical mode keeps min(poly-T, poly-A) = poly-A: ~0 cannot occur there
+    assert (np.asarray(codes) == np.uint64(2**64 - 1)).any() == (strand != 0x2)
+    eI, eD = oracle.matrix(off, codes, 0, 24, 0, 24)
+    sets = gdist.KmerSets.from_sequences(seqs, 32, gdist.KmerType.DNA, strand, ctx)
+    for m in (gdist.METHOD_SORTED, gdist.METHOD_BITSET):
+        I, D = sets.matrix(method=m)
+        assert np.array_equal(I, eI) and bits_equal(D, eD), m
+    for keep in (False, True):
+        sets.build_bitsets(keep_singletons=keep)
+        I, D = sets.matrix(method=gdist.METHOD_BITSET)
+        assert np.array_equal(I, eI) and bits_equal(D, eD), keep
+    d = sets.row_query(1, list(range(24)))
+    assert bits_equal(d, eD[1])
+
+
 # ---------------------------------------------------------------- two-tier dictionary
 @pytest.mark.parametrize("T", [0, 3, 8, 1000])
 def test_rare_tier_thresholds_exact(ctx, T):
