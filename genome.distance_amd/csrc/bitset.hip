@@ -1103,9 +1103,13 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
         // own launch of the DIAG variant, which skips the accumulators that
         // only hold pairs with j <= i (GDIST_BITSET_DIAG=0 keeps one launch).
         const char* dv = getenv("GDIST_BITSET_DIAG");
-        const bool split_diag = upper && r0 == c0 && !(dv && atoi(dv) == 0);
+        // row-sharded ranks compute [r_g, r_g+1) x [0, N) with r_g tile-aligned:
+        // their diagonal tiles are the ones with col0 == row0, b - a = (r0 - c0) / BT
+        const int64_t dlt = r0 - c0;
+        const bool split_diag = upper && dlt % BT == 0 && !(dv && atoi(dv) == 0);
         std::vector<int2> off_t, diag_t;
-        for (const int2& tt : tiles) ((split_diag && tt.x == tt.y) ? diag_t : off_t).push_back(tt);
+        for (const int2& tt : tiles)
+            ((split_diag && (int64_t)tt.y - tt.x == dlt / BT) ? diag_t : off_t).push_back(tt);
         DevBuf dt2((off_t.size() + diag_t.size()) * sizeof(int2) + 8, st);
         if (!off_t.empty()) h2d(dt2.p, off_t.data(), off_t.size() * sizeof(int2), st);
         if (!diag_t.empty())

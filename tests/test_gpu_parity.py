@@ -449,6 +449,23 @@ def test_reps_processors_java_semantics(ctx):
     assert reps == [2, 1, 3]
 
 
+def test_bitset_row_blocks_like_ranks(ctx):
+    """Row blocks as the multi-GPU partition hands them out (tile-aligned
+    r0 > 0, all columns, upper): the diagonal tiles of each block run the
+    trimmed variant and every pair is still exact; an unaligned block too."""
+    import gdist
+    n = 700
+    seqs = synth_sets(n, 3000, 0.01, 112)
+    sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
+    off, codes = oracle_pack(seqs, 21, 0, 0)
+    eI, eD = oracle.matrix(off, codes, 0, n, 0, n)
+    sets.build_bitsets()
+    for (r0, r1) in [(0, 256), (256, 512), (512, 700), (300, 450)]:
+        I, D = sets.matrix((r0, r1), (0, n), upper=True, method=gdist.METHOD_BITSET)
+        up = np.fromfunction(lambda a, b: b > (r0 + a), (r1 - r0, n))
+        assert np.array_equal(I[up], eI[r0:r1][up]) and bits_equal(D[up], eD[r0:r1][up]), (r0, r1)
+
+
 @pytest.mark.parametrize("strand", [0, 0x1, 0x2])
 def test_k32_all_ones_code(ctx, strand):
     """DNA k=32 uses all 64 code bits: the poly-T kmer is ~0, the sorted
