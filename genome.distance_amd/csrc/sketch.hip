@@ -245,9 +245,7 @@ template <int R, int C>
 bool launch_sketch_tiles(hipStream_t st, const gdist_sets* sk, int width, int64_t r0, int64_t r1, int64_t c0,
                          int64_t c1, bool upper, int jac, int en, int32_t* d_common, double* d_D, int64_t ld,
                          bool force_global) {
-    // GDIST_SKETCH_EVEN=1 keeps the unpadded stride (A/B of the bank spread)
-    const char* ev = getenv("GDIST_SKETCH_EVEN");
-    const int sw = (ev && atoi(ev) == 1) ? width : sketch_stride(width);
+    const int sw = sketch_stride(width);
     const size_t lds = (size_t)(R + C) * sw * 4 + LDS_SK_SLACK;
     const bool use_lds = !force_global && lds + sketch_meta_bytes<R, C>() <= (size_t)LDS_SK_MAX;
     if (!use_lds && !force_global) return false;

@@ -1,5 +1,5 @@
 """A/B of sketch merge windows (GDIST_SKETCH_K: kN), tile shapes
-(GDIST_SKETCH_TILE: tN) LDS row stride (GDIST_SKETCH_EVEN: even) in ONE process on the C5 workload: every variant's common
+(GDIST_SKETCH_TILE: tN) in ONE process on the C5 workload: every variant's common
 counts on a row block are checked identical to the first variant's, then the
 full upper triangle is timed in interleaved rounds."""
 import os, sys, time
@@ -19,14 +19,12 @@ check_rows = min(n, 2048)
 def apply(v):
     os.environ.pop("GDIST_SKETCH_TILE", None)
     os.environ.pop("GDIST_SKETCH_K", None)
-    os.environ.pop("GDIST_SKETCH_EVEN", None)
     for part in v.split("+"):
         if part.startswith("k"):
             os.environ["GDIST_SKETCH_K"] = part[1:]
         elif part.startswith("t"):
             os.environ["GDIST_SKETCH_TILE"] = part[1:]
-        elif part == "even":
-            os.environ["GDIST_SKETCH_EVEN"] = "1"
+
 
 
 
