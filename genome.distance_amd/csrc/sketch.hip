@@ -124,9 +124,9 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) const void gbl_void_t;
 
 // LDS row stride (dwords): odd, so the R+C rows of a tile start on distinct
-// banks (ds_read2_b32 banks by dword mod 32) - lanes advance at similar rates,
-// and with an even stride (1000 = 8 mod 32) the 24 column rows of a tile met
-// on 4 banks.
+// banks (ds_read2_b32 banks by dword mod 32). Measured against the even
+// stride it made no difference (lanes' merge positions spread the banks
+// anyway: DESIGN.md §4); kept as the conflict-neutral choice.
 inline int sketch_stride(int width) { return width | 1; }
 
 // One workgroup = an R x C tile of sketch pairs, one lane per pair
