@@ -469,8 +469,16 @@ static int resolve_method(gdist_ctx* ctx, gdist_sets* s, int method, double pair
     int m = method;
     if (m == GDIST_METHOD_AUTO) {
         if (!s->bits.p && !s->auto_sorted && !s->segoff.p && s->has_codes && sorted_cost_s(s, pairs) >= 0.02) {
-            build_bitsets(ctx, s, 0);
-            if (bitset_cost_s(s, pairs) > sorted_cost_s(s, pairs)) {
+            try {
+                build_bitsets(ctx, s, 0);
+            } catch (const Error& e) {
+                if (e.code != GDIST_ENOMEM) throw;
+                // the dictionary does not fit next to the codes: the join needs no more memory
+                (void)hipGetLastError();
+                free_bitsets(s);
+                gdist::cache_trim(ctx->device);
+            }
+            if (!s->bits.p || bitset_cost_s(s, pairs) > sorted_cost_s(s, pairs)) {
                 free_bitsets(s);
                 s->auto_sorted = true;
             }
