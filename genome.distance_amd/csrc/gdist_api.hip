@@ -10,6 +10,7 @@
 #include <rocprim/rocprim.hpp>
 
 #include <algorithm>
+#include <thread>
 #include <cmath>
 #include <cstring>
 #include <new>
@@ -191,6 +192,8 @@ int gdist_ctx_create(int device, gdist_ctx** out) {
         GD_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
         GD_HIP(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
         GD_HIP(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+        GD_HIP(hipEventCreateWithFlags(&c->ev_stage[0], hipEventDisableTiming));
+        GD_HIP(hipEventCreateWithFlags(&c->ev_stage[1], hipEventDisableTiming));
         GD_HIP(hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device));
         *out = c;
     });
@@ -210,6 +213,9 @@ int gdist_ctx_destroy(gdist_ctx* ctx) {
         (void)hipEventDestroy(ctx->ev_fork);
         (void)hipEventDestroy(ctx->ev_join);
         (void)hipStreamDestroy(ctx->side);
+        (void)hipEventDestroy(ctx->ev_stage[0]);
+        (void)hipEventDestroy(ctx->ev_stage[1]);
+        if (ctx->pinned) (void)hipHostFree(ctx->pinned);
         (void)hipStreamDestroy(ctx->stream);
         gdist::cache_trim(ctx->device);
         delete ctx;
@@ -508,6 +514,65 @@ int gdist_sets_prepare(gdist_ctx* ctx, gdist_sets* sets, int method, double pair
     });
 }
 
+// Device region (nr x nc, element `elem` bytes, device row stride nc) into a
+// host matrix with row stride ld, through double-buffered pinned staging in
+// row blocks; each row lands with one memcpy per contiguous span (rows of a
+// block split over a few host threads). With `upper` only the entries with
+// global column > global row are written: the others stay the caller's
+// (gdist.h, GDIST_UPPER_TRIANGLE).
+static void copy_out_rows(gdist_ctx* ctx, const void* dsrc, size_t elem, int64_t nr, int64_t nc, int64_t r0,
+                          int64_t c0, bool upper, void* hdst, int64_t ld) {
+    if (nr <= 0 || nc <= 0) return;
+    hipStream_t st = ctx->stream;
+    const size_t row_bytes = (size_t)nc * elem;
+    const size_t half = std::max(row_bytes, (size_t)64 << 20);
+    if (ctx->pinned_bytes < 2 * half) {
+        if (ctx->pinned) GD_HIP(hipHostFree(ctx->pinned));
+        ctx->pinned = nullptr;
+        ctx->pinned_bytes = 0;
+        GD_HIP(hipHostMalloc(&ctx->pinned, 2 * half, hipHostMallocDefault));
+        ctx->pinned_bytes = 2 * half;
+    }
+    const int64_t rows_per = (int64_t)(half / row_bytes);
+    char* stage[2] = {static_cast<char*>(ctx->pinned), static_cast<char*>(ctx->pinned) + half};
+    const char* src = static_cast<const char*>(dsrc);
+    char* dst = static_cast<char*>(hdst);
+    auto issue = [&](int64_t a0, int b) {
+        const int64_t a1 = std::min(nr, a0 + rows_per);
+        GD_HIP(hipMemcpyAsync(stage[b], src + (size_t)a0 * row_bytes, (size_t)(a1 - a0) * row_bytes,
+                              hipMemcpyDeviceToHost, st));
+        GD_HIP(hipEventRecord(ctx->ev_stage[b], st));
+    };
+    const int nthreads = (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    issue(0, 0);
+    int b = 0;
+    for (int64_t a0 = 0; a0 < nr; a0 += rows_per, b ^= 1) {
+        GD_HIP(hipEventSynchronize(ctx->ev_stage[b]));
+        if (a0 + rows_per < nr) issue(a0 + rows_per, b ^ 1);
+        const int64_t a1 = std::min(nr, a0 + rows_per);
+        auto rows = [&](int64_t lo, int64_t hi) {
+            for (int64_t a = lo; a < hi; a++) {
+                const int64_t first = upper ? std::max<int64_t>(0, r0 + a + 1 - c0) : 0;
+                if (first >= nc) continue;
+                std::memcpy(dst + ((size_t)a * ld + first) * elem, stage[b] + ((size_t)(a - a0) * nc + first) * elem,
+                            (size_t)(nc - first) * elem);
+            }
+        };
+        const int64_t nrows = a1 - a0;
+        if (nthreads == 1 || nrows * (int64_t)row_bytes < (int64_t(4) << 20)) {
+            rows(a0, a1);
+        } else {
+            std::vector<std::thread> pool;
+            const int64_t per = ceil_div(nrows, (int64_t)nthreads);
+            for (int t = 0; t < nthreads; t++) {
+                const int64_t lo = a0 + t * per, hi = std::min(a1, lo + per);
+                if (lo < hi) pool.emplace_back(rows, lo, hi);
+            }
+            for (auto& th : pool) th.join();
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 int gdist_intersect_matrix(gdist_ctx* ctx, const gdist_sets* sets, int64_t r0, int64_t r1, int64_t c0, int64_t c1,
                            int method, unsigned flags, int32_t* I_out, double* D_out, int64_t ld) {
@@ -549,31 +614,16 @@ int gdist_intersect_matrix(gdist_ctx* ctx, const gdist_sets* sets, int64_t r0, i
         if (m == GDIST_METHOD_BITSET) bitset_matrix(ctx, s, r0, r1, c0, c1, upper, dI, ldI);
         else sorted_matrix(ctx, s, r0, r1, c0, c1, upper, dI, ldI);
         DevBuf tD;
-        std::vector<double> hD;
-        std::vector<int32_t> hI;
         if (D_out) {
             double* dD;
             int64_t ldD;
             if (dev) { dD = D_out; ldD = ld; }
             else { tD.alloc((size_t)nr * nc * 8, st); dD = tD.as<double>(); ldD = nc; }
             distance_epilogue(ctx, s, r0, r1, c0, c1, upper, flags, dI, ldI, dD, ldD);
-            if (!dev) {
-                hD.resize((size_t)nr * nc);
-                d2h(hD.data(), dD, (size_t)nr * nc * 8, st);
-            }
+            if (!dev) copy_out_rows(ctx, dD, 8, nr, nc, r0, c0, upper, D_out, ld);
         }
-        if (I_out && !dev) {
-            hI.resize((size_t)nr * nc);
-            d2h(hI.data(), dI, (size_t)nr * nc * 4, st);
-        }
+        if (I_out && !dev) copy_out_rows(ctx, dI, 4, nr, nc, r0, c0, upper, I_out, ld);
         gdist::finish_timing(ctx, true);
-        // host outputs: entries excluded by the upper triangle stay untouched
-        for (int64_t a = 0; a < nr && !dev; a++)
-            for (int64_t b = 0; b < nc; b++) {
-                if (upper && c0 + b <= r0 + a) continue;
-                if (D_out) D_out[a * ld + b] = hD[a * nc + b];
-                if (I_out) I_out[a * ld + b] = hI[a * nc + b];
-            }
     });
 }
 
@@ -735,18 +785,9 @@ int gdist_sketch_matrix(gdist_ctx* ctx, const gdist_sets* sk, int64_t r0, int64_
             if (D_out) { tD.alloc((size_t)nr * nc * 8, st); dD = tD.as<double>(); }
         }
         sketch_matrix(ctx, sk, r0, r1, c0, c1, flags, dC, dD, ldo);
-        std::vector<int32_t> hC;
-        std::vector<double> hD;
         if (!dev) {
-            if (dC) { hC.resize((size_t)nr * nc); d2h(hC.data(), dC, (size_t)nr * nc * 4, st); }
-            if (dD) { hD.resize((size_t)nr * nc); d2h(hD.data(), dD, (size_t)nr * nc * 8, st); }
-            // entries excluded by the upper triangle stay untouched
-            for (int64_t a = 0; a < nr; a++)
-                for (int64_t b = 0; b < nc; b++) {
-                    if (upper && c0 + b <= r0 + a) continue;
-                    if (dC) common_out[a * ld + b] = hC[a * nc + b];
-                    if (dD) D_out[a * ld + b] = hD[a * nc + b];
-                }
+            if (dC) copy_out_rows(ctx, dC, 4, nr, nc, r0, c0, upper, common_out, ld);
+            if (dD) copy_out_rows(ctx, dD, 8, nr, nc, r0, c0, upper, D_out, ld);
         }
         gdist::finish_timing(ctx, true);
     });

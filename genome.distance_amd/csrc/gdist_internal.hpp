@@ -147,6 +147,9 @@ struct gdist_ctx {
     std::recursive_mutex mu;
     hipEvent_t ev_call0 = nullptr, ev_call1 = nullptr, ev_k0 = nullptr, ev_k1 = nullptr;
     hipStream_t side = nullptr;                          // concurrent rare-tier launches
+    void* pinned = nullptr;                              // host staging for host outputs (2 halves)
+    size_t pinned_bytes = 0;
+    hipEvent_t ev_stage[2] = {nullptr, nullptr};
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     gdist::Timing last;
     int cus = 256;
