@@ -180,7 +180,14 @@ def main():
     setup_s = time.time() - t_setup
 
     N = n_total
-    bounds = shard.triangle_bounds(N, world, 128)
+    # exact rows balancing the cost model's per-block time (dense tiles by
+    # area, the rare kernel each rank's block picks); equal area otherwise.
+    # Rank 0 cuts, every rank uses its cut.
+    bounds = shard.triangle_bounds(N, world, 1)
+    if method == "bitset" and world > 1:
+        obj = [shard.balanced_bounds(N, world, lambda a, b: sets.block_cost((a, b))[0]) if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        bounds = obj[0]
     r0, r1 = bounds[rank], bounds[rank + 1]
     rows = r1 - r0
     pairs_rank = shard.pairs_in_rows(N, r0, r1)

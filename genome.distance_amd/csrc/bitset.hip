@@ -147,25 +147,47 @@ __global__ void posting_sets_kernel(const uint64_t* __restrict__ recs, int64_t n
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) sets[i] = (uint32_t)recs[i];
 }
 
+// Lists of kLongList+ sets (gdist_internal.hpp) are walked by a whole wave
+// (lanes stride the members) instead of one lane: a lane-serial walk of an
+// m-member list is an O(m) (row-major) or O(m^2) (list-major) tail the rest
+// of the wave idles on.
+
+// pairs (s = psets[x], t = psets[y]) for y in [y0, e) step dy, s < t
+__device__ __forceinline__ void rare_pair_walk(const uint32_t* __restrict__ psets, int64_t x, int64_t y0, int64_t e,
+                                               int dy, int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper,
+                                               int32_t* __restrict__ I, int64_t ldI) {
+    const int64_t s = psets[x];
+    const bool srow = s >= r0 && s < r1, scol = s >= c0 && s < c1;
+    if (!srow && (upper || !scol)) return;
+    for (int64_t y = y0; y < e; y += dy) {
+        const int64_t t = psets[y];                  // t > s
+        if (srow && t >= c0 && t < c1) atomicAdd(I + (s - r0) * ldI + (t - c0), 1);
+        if (!upper && scol && t >= r0 && t < r1) atomicAdd(I + (t - r0) * ldI + (s - c0), 1);
+    }
+}
+
 // Rare tier: every posting list (ascending set ids) adds 1 to each of its
-// m(m-1)/2 pairs that fall in the region.
+// m(m-1)/2 pairs that fall in the region. One lane per list; lists of
+// kLongList+ members are taken by the wave (trip counts are wave-uniform).
 __global__ __launch_bounds__(256) void rare_pairs_kernel(const int64_t* __restrict__ poff,
                                                          const uint32_t* __restrict__ psets, int64_t nposts,
                                                          int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper,
                                                          int32_t* __restrict__ I, int64_t ldI) {
-    int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < nposts; p += stride) {
-        const int64_t b = poff[p], e = poff[p + 1];
-        for (int64_t x = b; x < e; x++) {
-            const int64_t s = psets[x];
-            const bool srow = s >= r0 && s < r1, scol = s >= c0 && s < c1;
-            if (!srow && (upper || !scol)) continue;
-            for (int64_t y = x + 1; y < e; y++) {
-                const int64_t t = psets[y];                  // t > s
-                if (srow && t >= c0 && t < c1) atomicAdd(I + (s - r0) * ldI + (t - c0), 1);
-                if (!upper && scol && t >= r0 && t < r1) atomicAdd(I + (t - r0) * ldI + (s - c0), 1);
-            }
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int lane = threadIdx.x & 63;
+    for (int64_t pb = (int64_t)blockIdx.x * blockDim.x; pb < nposts; pb += stride) {
+        const int64_t p = pb + threadIdx.x;
+        int64_t b = 0, e = 0;
+        if (p < nposts) { b = poff[p]; e = poff[p + 1]; }
+        const bool lng = e - b >= kLongList;
+        for (unsigned long long m = __ballot(lng); m; m &= m - 1) {
+            const int l = __ffsll((long long)m) - 1;
+            const int64_t lb = __shfl((long long)b, l, 64), le = __shfl((long long)e, l, 64);
+            for (int64_t x = lb; x < le - 1; x++)
+                rare_pair_walk(psets, x, x + 1 + lane, le, 64, r0, r1, c0, c1, upper, I, ldI);
         }
+        if (!lng)
+            for (int64_t x = b; x < e - 1; x++) rare_pair_walk(psets, x, x + 1, e, 1, r0, r1, c0, c1, upper, I, ldI);
     }
 }
 
@@ -201,9 +223,21 @@ __global__ __launch_bounds__(256) void rare_rows_kernel(const int64_t* __restric
     const int64_t per = (re - rb + nsplit - 1) / nsplit;
     const int64_t xb = rb + per * split;
     const int64_t xe = xb + per < re ? xb + per : re;
-    for (int64_t x = xb + threadIdx.x; x < xe; x += blockDim.x) {
-        const uint64_t ent = sent[x];                  // coalesced: no random bounds lookup
+    const int lane = threadIdx.x & 63;
+    for (int64_t xbase = xb; xbase < xe; xbase += blockDim.x) {   // wave-uniform trip count
+        const int64_t x = xbase + threadIdx.x;
+        const uint64_t ent = x < xe ? sent[x] : 0ull;  // coalesced: no random bounds lookup
         const int64_t b = (int64_t)(ent >> 24), e = b + (int64_t)(ent & 0xFFFFFFu);
+        const bool lng = e - b >= kLongList;
+        for (unsigned long long m = __ballot(lng); m; m &= m - 1) {   // long lists: the wave walks them
+            const int l = __ffsll((long long)m) - 1;
+            const int64_t lb = __shfl((long long)b, l, 64), le = __shfl((long long)e, l, 64);
+            for (int64_t y = lb + lane; y < le; y += 64) {
+                const int64_t t = psets[y];
+                if (t >= lo && t < ce && t != i) atomicAdd(&cnt[t - cb], 1);
+            }
+        }
+        if (lng) continue;
 #pragma unroll 4
         for (int64_t y = b; y < e; y++) {
             const int64_t t = psets[y];
@@ -230,9 +264,21 @@ __global__ __launch_bounds__(256) void rare_query_kernel(const int64_t* __restri
                                                          int32_t* __restrict__ cnt) {
     const int64_t xb = soff[q], xe = soff[q + 1];
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t x = xb + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < xe; x += stride) {
-        const uint64_t ent = sent[x];
+    const int lane = threadIdx.x & 63;
+    for (int64_t xbase = xb + (int64_t)blockIdx.x * blockDim.x; xbase < xe; xbase += stride) {
+        const int64_t x = xbase + threadIdx.x;
+        const uint64_t ent = x < xe ? sent[x] : 0ull;
         const int64_t b = (int64_t)(ent >> 24), e = b + (int64_t)(ent & 0xFFFFFFu);
+        const bool lng = e - b >= kLongList;
+        for (unsigned long long m = __ballot(lng); m; m &= m - 1) {
+            const int l = __ffsll((long long)m) - 1;
+            const int64_t lb = __shfl((long long)b, l, 64), le = __shfl((long long)e, l, 64);
+            for (int64_t y = lb + lane; y < le; y += 64) {
+                const int64_t t = psets[y];
+                if (t != q) atomicAdd(cnt + t, 1);
+            }
+        }
+        if (lng) continue;
         for (int64_t y = b; y < e; y++) {
             const int64_t t = psets[y];
             if (t != q) atomicAdd(cnt + t, 1);
@@ -279,6 +325,10 @@ __global__ void rare_flag_kernel(const uint32_t* __restrict__ cnt, int64_t n, in
 }
 
 constexpr int BT = 128;                 // tile edge (sets)
+// A block's last row tile holding RR <= kPartialMaxRR sixteen-row groups gets
+// its own launches with RR accumulator rows (RR = 7 saves less than the two
+// launches cost: C2, 104 rows, 4.51 vs 4.27 ms)
+constexpr int kPartialMaxRR = 6;
 constexpr int KC = 16;                  // 64-bit words per staged chunk
 constexpr int ROWB = KC * 8;            // 128 B per set row in LDS
 constexpr int TILE_BYTES = BT * ROWB;   // 16 KiB per operand per chunk
@@ -399,7 +449,8 @@ __device__ __forceinline__ int lds_off2(int g, int q) { return g * ROW2 + ((q ^ 
 
 // one operand's chunk: 8 DMA instructions of 1 KiB (16 rows), 2 per wave
 __device__ __forceinline__ void dma_chunk(const unsigned long long* __restrict__ bits, int64_t W, int64_t set0,
-                                          int64_t lim, int64_t kc, unsigned char* lds_op, int wave, int lane) {
+                                          int64_t lo, int64_t lim, int64_t kc, unsigned char* lds_op, int wave,
+                                          int lane) {
 #pragma unroll
     for (int i = 0; i < 2; i++) {
         const int rbase = (wave * 2 + i) * 16;
@@ -407,7 +458,8 @@ __device__ __forceinline__ void dma_chunk(const unsigned long long* __restrict__
         const int p = lane & 3;
         const int q = p ^ ((g >> 2) & 3);
         int64_t set = set0 + g;
-        set = set < lim ? set : lim - 1;              // clamp: rows past the range are masked at the end
+        set = set < lim ? set : lim - 1;              // clamp: rows outside [lo, lim) are masked at the end
+        set = set >= lo ? set : lo;
         const unsigned long long* src = bits + set * W + kc * KC2 + q * 2;
         __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(lds_op + rbase * ROW2), 16, 0, 0);
     }
@@ -421,21 +473,22 @@ __device__ __forceinline__ void dma_chunk(const unsigned long long* __restrict__
 // thread's 8x8 accumulators. DIAG: the tile sits on the diagonal of an
 // upper-triangle region, where accumulator (r, c) holds pairs with j > i only
 // when c >= r (rows ty + 16r, columns tx + 16c): the c < r ones (28 of 64) are
-// never computed.
-template <int ORDER, bool DIAG>
+// never computed. RR: only accumulator rows r < RR hold rows of the block (a
+// partial row tile at a block's end); the others are never computed.
+template <int ORDER, bool DIAG, int RR = 8>
 __device__ __forceinline__ void chunk_pairs(const unsigned char* A, const unsigned char* B, int ty, int tx,
                                             uint32_t (&acc)[8][8]) {
 #pragma unroll 1
     for (int q = 0; q < KC2 / 2; q++) {
         uint4 a[8];
 #pragma unroll
-        for (int r = 0; r < 8; r++) a[r] = *reinterpret_cast<const uint4*>(A + lds_off2(ty + 16 * r, q));
+        for (int r = 0; r < RR; r++) a[r] = *reinterpret_cast<const uint4*>(A + lds_off2(ty + 16 * r, q));
         if (ORDER == 0) {
 #pragma unroll
             for (int c = 0; c < 8; c++) {
                 const uint4 bv = *reinterpret_cast<const uint4*>(B + lds_off2(tx + 16 * c, q));
 #pragma unroll
-                for (int r = 0; r < 8; r++)
+                for (int r = 0; r < RR; r++)
                     if (!DIAG || c >= r) acc[r][c] = and_popc(a[r], bv, acc[r][c]);
             }
         } else {
@@ -448,7 +501,7 @@ __device__ __forceinline__ void chunk_pairs(const unsigned char* A, const unsign
 #pragma unroll
                 for (int d = 0; d < 4; d++) {
 #pragma unroll
-                    for (int r = 0; r < 8; r++) {
+                    for (int r = 0; r < RR; r++) {
                         const uint32_t ad = d == 0 ? a[r].x : d == 1 ? a[r].y : d == 2 ? a[r].z : a[r].w;
                         if (!DIAG || c >= r) acc[r][c] = bcnt_acc(ad & bw0[d], acc[r][c]);
                         if (!DIAG || c + 1 >= r) acc[r][c + 1] = bcnt_acc(ad & bw1[d], acc[r][c + 1]);
@@ -460,12 +513,14 @@ __device__ __forceinline__ void chunk_pairs(const unsigned char* A, const unsign
 }
 
 // DIAG: every tile of the launch sits on the diagonal of an upper-triangle
-// region (bitset_matrix launches those tiles separately).
-template <int ORDER, bool DIAG>
+// region (bitset_matrix launches those tiles separately). RR < 8: every tile
+// of the launch is the partial last row tile of the block, with at most 16 RR
+// rows (rows ty + 16r with r >= RR are past r1 for every thread).
+template <int ORDER, bool DIAG, int RR = 8>
 __global__ __launch_bounds__(NT, 4) void bitset_tile_kernel2(
     const unsigned long long* __restrict__ bits, int64_t W, const int2* __restrict__ tiles, int ntiles, int splits,
-    int64_t nchunks, int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I,
-    int64_t ldI) {
+    int64_t nchunks, int64_t r0, int64_t r1, int64_t c0, int64_t c1, int64_t corg, int upper,
+    int32_t* __restrict__ I, int64_t ldI) {
     __shared__ __attribute__((aligned(16))) unsigned char lds[2 * STAGE2];
 
     // XCD-aware bijective remap, then split-major unit order
@@ -477,7 +532,7 @@ __global__ __launch_bounds__(NT, 4) void bitset_tile_kernel2(
     const int2 t = tiles[tile];
     if (split >= splits || t.x < 0 || t.y < 0) return;
     const int64_t row0 = r0 + (int64_t)t.x * BT;
-    const int64_t col0 = c0 + (int64_t)t.y * BT;
+    const int64_t col0 = corg + (int64_t)t.y * BT;     // column tiles start at corg <= c0 (see bitset_matrix)
     const int64_t kc_per = ceil_div(nchunks, splits);
     const int64_t kc0 = (int64_t)split * kc_per;
     const int64_t kc1 = kc0 + kc_per < nchunks ? kc0 + kc_per : nchunks;
@@ -492,8 +547,8 @@ __global__ __launch_bounds__(NT, 4) void bitset_tile_kernel2(
         for (int c = 0; c < 8; c++) acc[r][c] = 0;
 
     if (kc0 < kc1) {
-        dma_chunk(bits, W, row0, r1, kc0, lds, wave, lane);
-        dma_chunk(bits, W, col0, c1, kc0, lds + OPB2, wave, lane);
+        dma_chunk(bits, W, row0, r0, r1, kc0, lds, wave, lane);
+        dma_chunk(bits, W, col0, c0, c1, kc0, lds + OPB2, wave, lane);
     }
     for (int64_t kc = kc0; kc < kc1; kc++) {
         const int st = (int)((kc - kc0) & 1);
@@ -501,13 +556,13 @@ __global__ __launch_bounds__(NT, 4) void bitset_tile_kernel2(
         unsigned char* B = A + OPB2;
         if (kc + 1 < kc1) {
             unsigned char* An = lds + (st ^ 1) * STAGE2;
-            dma_chunk(bits, W, row0, r1, kc + 1, An, wave, lane);
-            dma_chunk(bits, W, col0, c1, kc + 1, An + OPB2, wave, lane);
+            dma_chunk(bits, W, row0, r0, r1, kc + 1, An, wave, lane);
+            dma_chunk(bits, W, col0, c0, c1, kc + 1, An + OPB2, wave, lane);
             asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");   // chunk kc landed everywhere
         } else {
             asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
         }
-        chunk_pairs<ORDER, DIAG>(A, B, ty, tx, acc);
+        chunk_pairs<ORDER, DIAG, RR>(A, B, ty, tx, acc);
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // stage free for the next DMA
     }
 
@@ -518,7 +573,7 @@ __global__ __launch_bounds__(NT, 4) void bitset_tile_kernel2(
 #pragma unroll
         for (int c = 0; c < 8; c++) {
             const int64_t j = col0 + tx + 16 * c;
-            if (j >= c1 || (upper && j <= i)) continue;
+            if (j < c0 || j >= c1 || (upper && j <= i)) continue;
             if (acc[r][c]) atomicAdd(I + (i - r0) * ldI + (j - c0), (int32_t)acc[r][c]);
         }
     }
@@ -834,17 +889,40 @@ __global__ void local_mass_kernel(const uint64_t* __restrict__ codes, const uint
     if (acc) atomicAdd(out, acc);
 }
 
-// sum over posting lists of m(m-1)/2 (the rare tier's pair increments)
-__global__ void rare_incs_kernel(const int64_t* __restrict__ post_off, int64_t n, unsigned long long* __restrict__ out) {
-    unsigned long long acc = 0;
+// over the posting lists: sum of m(m-1)/2 (the rare tier's pair increments)
+// -> out[0], the longest list -> out[1], the increments of kLongList+ lists
+// -> out[2]. One atomic of each kind per workgroup.
+__global__ __launch_bounds__(256) void rare_incs_kernel(const int64_t* __restrict__ post_off, int64_t n,
+                                                        unsigned long long* __restrict__ out) {
+    __shared__ unsigned long long part[3][4];
+    unsigned long long acc = 0, mx = 0, lng = 0;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; l < n; l += stride) {
         const unsigned long long m = (unsigned long long)(post_off[l + 1] - post_off[l]);
-        acc += m * (m - 1) / 2;
+        const unsigned long long inc = m * (m - 1) / 2;
+        acc += inc;
+        if (m >= (unsigned long long)kLongList) lng += inc;
+        mx = m > mx ? m : mx;
     }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
-    if ((threadIdx.x & 63) == 0 && acc) atomicAdd(out, acc);
+    for (int o = 32; o > 0; o >>= 1) {
+        acc += __shfl_xor(acc, o, 64);
+        lng += __shfl_xor(lng, o, 64);
+        const unsigned long long om = __shfl_xor(mx, o, 64);
+        mx = om > mx ? om : mx;
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { part[0][w] = acc; part[1][w] = mx; part[2][w] = lng; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int v = 1; v < (int)(blockDim.x >> 6); v++) {
+            acc += part[0][v]; lng += part[2][v];
+            mx = part[1][v] > mx ? part[1][v] : mx;
+        }
+        if (acc) atomicAdd(out, acc);
+        if (mx) atomicMax(out + 1, mx);
+        if (lng) atomicAdd(out + 2, lng);
+    }
 }
 
 }  // namespace
@@ -876,22 +954,25 @@ int64_t auto_rare_threshold(int64_t nsets) {
 
 int64_t choose_rare_threshold(const std::vector<uint64_t>& hist, int64_t nsets) {
     // cost(T) = pairs * W(dense kmers with count >= T) / dense rate
-    //         + sum_{2 <= c < T} hist[c] * c(c-1)/2 / rare rate
-    // evaluated for every T in [2, nsets+1]; T = 2 is dense-only.
+    //         + the cheaper rare kernel on the lists of kmers with 2 <= count < T
+    // over the whole triangle, for every T in [2, nsets+1]; T = 2 is dense-only.
     const double pairs = 0.5 * (double)nsets * (double)(nsets - 1);
     const int64_t top = (int64_t)hist.size() - 1;
     std::vector<double> dense_ge(top + 2, 0.0);
     for (int64_t c = top; c >= 2; c--) dense_ge[c] = dense_ge[c + 1] + (double)hist[c];
-    double incs = 0.0, recs = 0.0, best = -1.0;
+    RareTier t;
+    double best = -1.0;
     int64_t bestT = 2;
     for (int64_t T = 2; T <= top + 1; T++) {
         if (T > 2) {
-            incs += (double)hist[T - 1] * (double)(T - 1) * (double)(T - 2) / 2.0;
-            recs += (double)hist[T - 1] * (double)(T - 1);
+            const double c = (double)(T - 1), h = (double)hist[T - 1], inc = h * c * (c - 1.0) / 2.0;
+            t.incs += inc;
+            if (T - 1 >= kLongList) t.incs_long += inc;
+            t.records += h * c;
+            t.lists += h;
         }
         const double U = T <= top ? dense_ge[T] : 0.0;
-        const double cost = pairs * (double)bitset_words((int64_t)U) / kDenseWordPairsPerS +
-                            (incs > 0 ? incs / rare_rate(incs, recs) : 0.0);
+        const double cost = pairs * (double)bitset_words((int64_t)U) / kDenseWordPairsPerS + rare_choice(t, 1.0, 1.0).cost();
         if (best < 0 || cost < best) { best = cost; bestT = T; }
     }
     return bestT;
@@ -952,7 +1033,7 @@ void build_postings(gdist_ctx* ctx, gdist_sets* s, unsigned long long* recs, int
     s->n_rare = Ur;
     s->post_off.alloc((Ur + 1) * 8, st);
     s->post_sets.alloc(n * 4 + 4, st);
-    s->rare_incs = 0;
+    s->rare_incs = s->rare_max_list = s->rare_incs_long = 0;
     if (Ur == 0 || n == 0) {
         GD_HIP(hipMemsetAsync(s->post_off.p, 0, (Ur + 1) * 8, st));
         GD_HIP(hipStreamSynchronize(st));
@@ -983,15 +1064,17 @@ void build_postings(gdist_ctx* ctx, gdist_sets* s, unsigned long long* recs, int
                                                      s->srare_ent.as<uint64_t>());
     GD_HIP(hipGetLastError());
     // pair increments of the tier (cost model, kernel choice)
-    DevBuf d_incs(8, st);
-    GD_HIP(hipMemsetAsync(d_incs.p, 0, 8, st));
-    rare_incs_kernel<<<grid_for(Ur, 256, 256 * 64), 256, 0, st>>>(s->post_off.as<int64_t>(), Ur,
-                                                                  d_incs.as<unsigned long long>());
+    DevBuf d_incs(24, st);
+    GD_HIP(hipMemsetAsync(d_incs.p, 0, 24, st));
+    rare_incs_kernel<<<grid_for(Ur, 256, 4096), 256, 0, st>>>(s->post_off.as<int64_t>(), Ur,
+                                                              d_incs.as<unsigned long long>());
     GD_HIP(hipGetLastError());
-    unsigned long long incs = 0;
-    d2h(&incs, d_incs.p, 8, st);
+    unsigned long long h[3] = {0, 0, 0};
+    d2h(h, d_incs.p, 24, st);
     GD_HIP(hipStreamSynchronize(st));
-    s->rare_incs = (int64_t)incs;
+    s->rare_incs = (int64_t)h[0];
+    s->rare_max_list = (int64_t)h[1];
+    s->rare_incs_long = (int64_t)h[2];
 }
 
 void build_bitsets(gdist_ctx* ctx, gdist_sets* s, unsigned flags, int64_t rare_threshold) {
@@ -1024,13 +1107,75 @@ void build_bitsets(gdist_ctx* ctx, gdist_sets* s, unsigned flags, int64_t rare_t
     s->bits_keep_singletons = keep;
 }
 
+RareTier rare_tier(const gdist_sets* s) {
+    RareTier t;
+    t.incs = (double)s->rare_incs;
+    t.incs_long = (double)s->rare_incs_long;
+    t.records = (double)s->rare_records;
+    t.lists = (double)s->n_rare;
+    return t;
+}
+
+double block_pairs(int64_t r0, int64_t r1, int64_t c0, int64_t c1, bool upper) {
+    if (r1 <= r0 || c1 <= c0) return 0.0;
+    if (!upper) return (double)(r1 - r0) * (double)(c1 - c0);
+    // row i holds columns max(c0, i + 1) .. c1 - 1: full rows while i + 1 <= c0,
+    // then c1 - 1 - i for i in [c0, c1 - 1)
+    const int64_t a = std::min(r1, std::max(r0, c0));            // rows [r0, a): all nc columns
+    double p = (double)(a - r0) * (double)(c1 - c0);
+    const int64_t b0 = a, b1 = std::min(r1, c1 - 1);              // rows [b0, b1): c1 - 1 - i columns
+    if (b1 > b0) p += 0.5 * (double)(b1 - b0) * (double)((c1 - 1 - b0) + (c1 - b1));
+    return p;
+}
+
+// The 128 x 128 tiles bitset_matrix launches on a block (same enumeration:
+// upper-triangle blocks tile their columns from corg = r0 mod BT, diagonal
+// tiles go to the DIAG launch), counted per row tile in closed form. A
+// partial last row tile with RR = ceil(rows / 16) <= kPartialMaxRR runs RR of
+// 8 accumulator rows and costs ~RR/8 of a tile (at least 2/8: the column
+// fragments are read from LDS whatever RR is); partial columns cost full
+// tiles. What the row partition must see.
+static void dense_tiles(int64_t r0, int64_t r1, int64_t c0, int64_t c1, bool upper, double* off, double* diag) {
+    *off = *diag = 0.0;
+    if (r1 <= r0 || c1 <= c0) return;
+    const int64_t tr = ceil_div(r1 - r0, BT);
+    const int64_t rr = ceil_div(r1 - r0 - (tr - 1) * BT, 16);
+    const double last_w = rr <= kPartialMaxRR ? (double)std::max<int64_t>(2, rr) / 8.0 : 1.0;
+    auto w = [&](int64_t a) { return a == tr - 1 ? std::min(1.0, last_w) : 1.0; };
+    if (!upper) {
+        *off = ((double)(tr - 1) + w(tr - 1)) * (double)ceil_div(c1 - c0, BT);
+        return;
+    }
+    const int64_t corg = c0 - (((c0 - r0) % BT) + BT) % BT;
+    const int64_t dlt_t = (r0 - corg) / BT, tc2 = ceil_div(c1 - corg, BT);
+    for (int64_t a = 0; a < tr; a++) {
+        const int64_t x = std::max(c0, r0 + a * BT + 1);   // tile b is launched iff its last column cmax >= x
+        if (c1 - 1 < x) break;                            // rows only grow: no later row tile has any
+        const int64_t b_lo = std::max<int64_t>(0, ceil_div(x + 1 - corg, BT) - 1);
+        if (b_lo >= tc2) continue;
+        const bool has_diag = a + dlt_t >= b_lo && a + dlt_t < tc2;
+        *diag += (has_diag ? 1.0 : 0.0) * w(a);
+        *off += ((double)(tc2 - b_lo) - (has_diag ? 1.0 : 0.0)) * w(a);
+    }
+}
+
+double bitset_block_cost_s(const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1, bool upper,
+                           bool* rare_row_major) {
+    const double n = (double)s->nsets, tot = 0.5 * n * (n - 1.0);
+    const double pairs = block_pairs(r0, r1, c0, c1, upper);
+    const RareChoice rc = rare_choice(rare_tier(s), tot > 0 ? std::min(1.0, pairs / tot) : 1.0,
+                                      n > 0 ? (double)(r1 - r0) / n : 1.0);
+    if (rare_row_major) *rare_row_major = rc.row_major;
+    double off, diag;
+    dense_tiles(r0, r1, c0, c1, upper, &off, &diag);
+    return (off + kDiagTileShare * diag) * (double)(BT * BT) * (double)s->W / kDenseWordPairsPerS + rc.cost();
+}
+
 double bitset_cost_s(const gdist_sets* s, double pairs) {
-    // dense tier: ~8.6e12 word pairs/s (0.87 of the measured and+bcnt issue
-    // ceiling, C2); rare tier: ~2.2e10 pair increments/s (C2, C3 rare kernels)
+    // a region given only by its pair count: its share of the rows taken as its share of the pairs
     const double tot = 0.5 * (double)s->nsets * (double)(s->nsets - 1);
     const double frac = tot > 0 ? std::min(1.0, pairs / tot) : 1.0;
-    const double incs = (double)s->rare_incs, recs = (double)s->rare_records;
-    return pairs * (double)s->W / kDenseWordPairsPerS + (incs > 0 ? frac * incs / rare_rate(incs, recs) : 0.0);
+    return pairs * (double)s->W / kDenseWordPairsPerS + rare_choice(rare_tier(s), frac, frac).cost();
 }
 
 double sorted_cost_s(const gdist_sets* s, double pairs) {
@@ -1044,7 +1189,7 @@ void free_bitsets(gdist_sets* s) {
     s->post_off.release();
     s->post_sets.release();
     s->W = s->dict_size = 0;
-    s->n_rare = s->rare_T = s->rare_records = s->rare_incs = 0;
+    s->n_rare = s->rare_T = s->rare_records = s->rare_incs = s->rare_max_list = s->rare_incs_long = 0;
 }
 
 void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1,
@@ -1073,15 +1218,19 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     GD_REQUIRE(grid < (int64_t(1) << 31), "bitset matrix grid too large");
     const char* ev = getenv("GDIST_BITSET_KERNEL");   // A/B selection (default: 3)
     const int variant = ev ? atoi(ev) : 3;
-    // Posting-list-major rare kernel for short lists (C2: ~2 members, one pair
-    // and one global atomic per list); row-major once a record feeds several
-    // pair increments (C3: ~7 per record), where scattered global atomics over
-    // the N x N counts cost more than re-reading lists per member row.
-    // GDIST_RARE_KERNEL=0|1 forces one (A/B). The list-major kernel uses
-    // atomics only, like the dense kernel, so it runs beside the dense launch
-    // on the side stream (GDIST_RARE_OVERLAP=0 keeps it in line).
+    // Rare kernel per call from the cost model (rare_choice): list-major opens
+    // every list and walks the pairs from this block's rows with global
+    // atomics (short lists, blocks with few pairs per row: C2, the last rank
+    // of a row-sharded triangle); row-major walks each row's lists into LDS
+    // counters (lists feeding several increments per record: C3, C4; ranks
+    // with many pairs per row). GDIST_RARE_KERNEL=0|1 forces one (A/B). The
+    // list-major kernel uses atomics only, like the dense kernel, so it runs
+    // beside the dense launch on the side stream (GDIST_RARE_OVERLAP=0 keeps
+    // it in line).
     const char* rv = getenv("GDIST_RARE_KERNEL");
-    const bool list_major = rv ? atoi(rv) == 0 : !rare_row_major((double)s->rare_incs, (double)s->rare_records);
+    bool row_major = false;
+    if (s->n_rare > 0) (void)bitset_block_cost_s(s, r0, r1, c0, c1, upper, &row_major);
+    const bool list_major = rv ? atoi(rv) == 0 : !row_major;
     const char* ov = getenv("GDIST_RARE_OVERLAP");
     const bool overlap = s->n_rare > 0 && list_major && !(ov && atoi(ov) == 0);
     GD_HIP(hipEventRecord(ctx->ev_k0, st));
@@ -1103,35 +1252,77 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
         // own launch of the DIAG variant, which skips the accumulators that
         // only hold pairs with j <= i (GDIST_BITSET_DIAG=0 keeps one launch).
         const char* dv = getenv("GDIST_BITSET_DIAG");
-        // row-sharded ranks compute [r_g, r_g+1) x [0, N) with r_g tile-aligned:
-        // their diagonal tiles are the ones with col0 == row0, b - a = (r0 - c0) / BT
-        const int64_t dlt = r0 - c0;
-        const bool split_diag = upper && dlt % BT == 0 && !(dv && atoi(dv) == 0);
-        std::vector<int2> off_t, diag_t;
-        for (const int2& tt : tiles)
-            ((split_diag && (int64_t)tt.y - tt.x == dlt / BT) ? diag_t : off_t).push_back(tt);
-        DevBuf dt2((off_t.size() + diag_t.size()) * sizeof(int2) + 8, st);
-        if (!off_t.empty()) h2d(dt2.p, off_t.data(), off_t.size() * sizeof(int2), st);
-        if (!diag_t.empty())
-            h2d(dt2.as<int2>() + off_t.size(), diag_t.data(), diag_t.size() * sizeof(int2), st);
+        // Upper-triangle regions tile their columns from an origin corg <= c0
+        // with corg = r0 (mod BT), so tiles lie exactly on the diagonal whatever
+        // r0 is (row-sharded ranks get exact equal-area row blocks); columns
+        // below c0 are loaded clamped and discarded. Diagonal tiles: col0 == row0.
+        const bool split_diag = upper && !(dv && atoi(dv) == 0);
+        const int64_t corg = split_diag ? c0 - (((c0 - r0) % BT) + BT) % BT : c0;
+        const int64_t dlt_t = (r0 - corg) / BT;
+        // The last row tile of a block whose rows are not a multiple of BT
+        // holds nlast rows: its tiles get launches instantiated for
+        // RR = ceil(nlast / 16) accumulator rows, skipping the others' work.
+        // (GDIST_BITSET_PARTIAL_RR: the largest RR given its own launches, A/B)
+        const int64_t nlast = nr - (int64_t)(tr - 1) * BT;
+        const int rr = (int)ceil_div(nlast, 16);
+        const char* pv = getenv("GDIST_BITSET_PARTIAL_RR");
+        const bool part = rr <= (pv ? atoi(pv) : kPartialMaxRR);
+        std::vector<int2> grp[4];   // off-diagonal, diagonal, partial off-diagonal, partial diagonal
+        const int tc2 = (int)ceil_div(c1 - corg, BT);
+        for (int a = 0; a < tr; a++)
+            for (int b = 0; b < tc2; b++) {
+                const int64_t rmin = r0 + (int64_t)a * BT;
+                const int64_t cmax = std::min<int64_t>(c1, corg + (int64_t)(b + 1) * BT) - 1;
+                if (cmax < c0 || (upper && cmax <= rmin)) continue;
+                const int g = ((split_diag && (int64_t)b - a == dlt_t) ? 1 : 0) + ((part && a == tr - 1) ? 2 : 0);
+                grp[g].push_back(make_int2(a, b));
+            }
+        size_t at[5] = {0, 0, 0, 0, 0};
+        for (int g = 0; g < 4; g++) at[g + 1] = at[g] + grp[g].size();
+        DevBuf dt2(at[4] * sizeof(int2) + 8, st);
+        for (int g = 0; g < 4; g++)
+            if (!grp[g].empty()) h2d(dt2.as<int2>() + at[g], grp[g].data(), grp[g].size() * sizeof(int2), st);
         // workgroups per CU the K-split aims for (GDIST_BITSET_WG_PER_CU, A/B)
         const char* wv = getenv("GDIST_BITSET_WG_PER_CU");
         const int64_t wg_per_cu = wv ? std::max(1, atoi(wv)) : 16;
+        // ... but each workgroup streams at least min_kc chunks: a split's
+        // prologue and its 16K accumulator atomics amortise over its chunks
+        // (launches of few tiles: diagonal, partial; GDIST_BITSET_MIN_CHUNKS, A/B)
+        const char* mv = getenv("GDIST_BITSET_MIN_CHUNKS");
+        const int64_t min_kc = mv ? std::max(1, atoi(mv)) : 16;
         auto launch = [&](auto kern, const int2* dtiles, size_t nt) {
             if (nt == 0) return;
             const int64_t target2 = (int64_t)ctx->cus * wg_per_cu;
-            const int sp2 = (int)std::max<int64_t>(1, std::min<int64_t>(nch2, ceil_div(target2, (int64_t)nt)));
+            const int sp2 = (int)std::max<int64_t>(
+                1, std::min<int64_t>(std::max<int64_t>(1, nch2 / min_kc), ceil_div(target2, (int64_t)nt)));
             const int64_t grid2 = (int64_t)nt * sp2;
             GD_REQUIRE(grid2 < (int64_t(1) << 31), "bitset matrix grid too large");
             kern<<<(unsigned)grid2, NT, 0, st>>>(s->bits.as<unsigned long long>(), s->W, dtiles, (int)nt, sp2, nch2,
-                                                 r0, r1, c0, c1, upper ? 1 : 0, d_I, ldI);
+                                                 r0, r1, c0, c1, corg, upper ? 1 : 0, d_I, ldI);
         };
-        if (variant == 2) {
-            launch(bitset_tile_kernel2<0, false>, dt2.as<int2>(), off_t.size());
-            launch(bitset_tile_kernel2<0, true>, dt2.as<int2>() + off_t.size(), diag_t.size());
+        const int2* dg = dt2.as<int2>();
+        if (variant == 2) {   // A/B: ORDER 0, full-height tiles throughout
+            launch(bitset_tile_kernel2<0, false>, dg, at[1]);
+            launch(bitset_tile_kernel2<0, true>, dg + at[1], at[2] - at[1]);
+            launch(bitset_tile_kernel2<0, false>, dg + at[2], at[3] - at[2]);
+            launch(bitset_tile_kernel2<0, true>, dg + at[3], at[4] - at[3]);
         } else {
-            launch(bitset_tile_kernel2<1, false>, dt2.as<int2>(), off_t.size());
-            launch(bitset_tile_kernel2<1, true>, dt2.as<int2>() + off_t.size(), diag_t.size());
+            launch(bitset_tile_kernel2<1, false>, dg, at[1]);
+            launch(bitset_tile_kernel2<1, true>, dg + at[1], at[2] - at[1]);
+            auto partial = [&](auto off_k, auto diag_k) {
+                launch(off_k, dg + at[2], at[3] - at[2]);
+                launch(diag_k, dg + at[3], at[4] - at[3]);
+            };
+            switch (part ? rr : 8) {
+                case 1: partial(bitset_tile_kernel2<1, false, 1>, bitset_tile_kernel2<1, true, 1>); break;
+                case 2: partial(bitset_tile_kernel2<1, false, 2>, bitset_tile_kernel2<1, true, 2>); break;
+                case 3: partial(bitset_tile_kernel2<1, false, 3>, bitset_tile_kernel2<1, true, 3>); break;
+                case 4: partial(bitset_tile_kernel2<1, false, 4>, bitset_tile_kernel2<1, true, 4>); break;
+                case 5: partial(bitset_tile_kernel2<1, false, 5>, bitset_tile_kernel2<1, true, 5>); break;
+                case 6: partial(bitset_tile_kernel2<1, false, 6>, bitset_tile_kernel2<1, true, 6>); break;
+                case 7: partial(bitset_tile_kernel2<1, false, 7>, bitset_tile_kernel2<1, true, 7>); break;
+                default: break;   // no partial row tile
+            }
         }
     }
     GD_HIP(hipGetLastError());

@@ -414,6 +414,14 @@ int gdist_sets_rare_info(const gdist_sets* s, int64_t* threshold, int64_t* lists
     });
 }
 
+int gdist_sets_rare_stats(const gdist_sets* s, int64_t* pair_incs, int64_t* max_list) {
+    return guard([&] {
+        check_sets(s);
+        if (pair_incs) *pair_incs = s->rare_incs;
+        if (max_list) *max_list = s->rare_max_list;
+    });
+}
+
 int gdist_sets_bitset_info(const gdist_sets* s, int64_t* dict_size, int64_t* words_per_set) {
     return guard([&] {
         check_sets(s);
@@ -1038,6 +1046,26 @@ int gdist_comm_allreduce_max(gdist_ctx* ctx, double* value) {
         d2h(h.data(), all.p, 8 * ctx->nranks, ctx->stream);
         GD_HIP(hipStreamSynchronize(ctx->stream));
         *value = *std::max_element(h.begin(), h.end());
+    });
+}
+
+int gdist_sets_block_cost(const gdist_sets* sets, int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper,
+                          double* seconds, int* rare_kernel) {
+    return guard([&] {
+        check_sets(sets);
+        GD_REQUIRE(0 <= r0 && r0 <= r1 && r1 <= sets->nsets && 0 <= c0 && c0 <= c1 && c1 <= sets->nsets,
+                   "block out of range");
+        int rk = -1;
+        double t;
+        if (sets->bits.p) {
+            bool row_major = false;
+            t = bitset_block_cost_s(sets, r0, r1, c0, c1, upper != 0, &row_major);
+            if (sets->n_rare > 0) rk = row_major ? 1 : 0;
+        } else {
+            t = sorted_cost_s(sets, block_pairs(r0, r1, c0, c1, upper != 0));
+        }
+        if (seconds) *seconds = t;
+        if (rare_kernel) *rare_kernel = rk;
     });
 }
 

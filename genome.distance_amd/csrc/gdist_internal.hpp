@@ -190,6 +190,8 @@ struct gdist_sets {
     gdist::DevBuf post_sets;              // uint32 [rare_records], ascending within a list
     int64_t n_rare = 0, rare_T = 0, rare_records = 0;
     int64_t rare_incs = 0;                // sum over rare lists of m(m-1)/2 pair increments
+    int64_t rare_max_list = 0;            // longest rare posting list
+    int64_t rare_incs_long = 0;           // pair increments of lists with kLongList+ sets
     gdist::DevBuf srare_off;              // int64 [nsets+1]: set -> its rare kmers (CSR)
     gdist::DevBuf srare_ent;              // uint64 [rare_records]: the set's rare lists as
                                           // (list start << 24 | list length), by rare rank
@@ -235,18 +237,48 @@ void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_
                unsigned long long* bits, const uint64_t* rare, int64_t Ur, int64_t id_base,
                unsigned long long* rare_out, int64_t rare_cap, int64_t* rare_written);
 void build_postings(gdist_ctx* ctx, gdist_sets* s, unsigned long long* recs, int64_t n, int64_t Ur);
-// Cost model (seconds per region of `pairs` pairs), calibrated on MI355X:
-// bitset = dense AND+popcount + rare pair increments; sorted = streaming hash
-// join. Used by METHOD_AUTO and by the rare-threshold choice.
-constexpr double kDenseWordPairsPerS = 8.6e12;   // 0.87 of the measured and+bcnt ceiling (C2)
-constexpr double kRareIncsPerS = 2.2e10;         // list-major rare_pairs_kernel (C2)
-constexpr double kRareRowIncsPerS = 6.5e10;      // row-major rare_rows_kernel (C3, C4 slice)
-// the rare kernel a tier gets (bitset_matrix): row-major once a record feeds
-// several pair increments
-inline bool rare_row_major(double incs, double records) { return incs >= 2.0 * records; }
-inline double rare_rate(double incs, double records) {
-    return rare_row_major(incs, records) ? kRareRowIncsPerS : kRareIncsPerS;
+// Cost model (seconds), calibrated on MI355X from per-kernel rocprofv3
+// averages (scripts/calib_rare.sh; profiles/r01/rare_model): bitset = dense
+// AND+popcount tiles + the rare tier; sorted = streaming hash join. Used by
+// METHOD_AUTO, the rare-threshold choice, the per-call rare kernel choice and
+// the cost-balanced row partition (gdist_sets_block_cost).
+constexpr double kDenseWordPairsPerS = 8.6e12;   // launched tile area; 0.87 of the measured and+bcnt ceiling (C2)
+constexpr double kDiagTileShare = 0.59;          // a DIAG-launch tile vs an off-diagonal one (C2)
+constexpr int kLongList = 64;                    // rare lists of this many sets are walked by a wave
+constexpr double kRareListIncsPerS = 2.6e10;     // list-major: pair increments in the block (lane-walked lists)
+constexpr double kRareLongIncsPerS = 8.5e9;      // list-major: pair increments of wave-walked long lists
+constexpr double kRareListScanPerS = 1.85e11;    // list-major: every list is opened once per call
+constexpr double kRareRowPerS = 7.5e10;          // row-major: (incs + records) x the block's share of rows
+constexpr double kRareOverlapExposed = 0.6;      // list-major beside the dense launch: the share not hidden
+// rare-tier totals the model reads
+struct RareTier {
+    double incs = 0, incs_long = 0, records = 0, lists = 0;
+};
+struct RareChoice {
+    double list_s = 0, row_s = 0;   // modelled kernel times for the block
+    bool row_major = false;
+    double cost() const { return row_major ? row_s : list_s * kRareOverlapExposed; }
+};
+// f_area: the block's share of the tier's pair increments (pairs in the
+// block / all pairs); f_rows: its share of the sets as rows. The list-major
+// kernel opens every list but walks pairs only from its rows; the row-major
+// kernel walks every list of each of its rows. The list-major kernel runs on
+// the side stream beside the dense tiles, so its exposed share is compared.
+inline RareChoice rare_choice(const RareTier& t, double f_area, double f_rows) {
+    RareChoice c;
+    if (t.lists <= 0) return c;
+    c.list_s = f_area * ((t.incs - t.incs_long) / kRareListIncsPerS + t.incs_long / kRareLongIncsPerS) +
+               t.lists / kRareListScanPerS;
+    c.row_s = f_rows * (t.incs + t.records) / kRareRowPerS;
+    c.row_major = c.row_s < c.list_s * kRareOverlapExposed;
+    return c;
 }
+RareTier rare_tier(const gdist_sets* s);
+// pairs of the block rows [r0, r1) x cols [c0, c1) (upper: only j > i)
+double block_pairs(int64_t r0, int64_t r1, int64_t c0, int64_t c1, bool upper);
+// modelled seconds of bitset_matrix on the block (dense + the rare kernel it picks)
+double bitset_block_cost_s(const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1, bool upper,
+                           bool* rare_row_major);
 constexpr double kSortedBytesPerS = 6.0e12;      // sorted_join_kernel streaming, C3
 double bitset_cost_s(const gdist_sets* s, double pairs);
 double sorted_cost_s(const gdist_sets* s, double pairs);

@@ -69,6 +69,7 @@ _SIGS = {
     "gdist_sets_build_bitsets": (C.c_int, [_setp, _u32]),
     "gdist_sets_build_bitsets_ex": (C.c_int, [_setp, _u32, _i64]),
     "gdist_sets_rare_info": (C.c_int, [_setp, _i64p, _i64p, _i64p]),
+    "gdist_sets_rare_stats": (C.c_int, [_setp, _i64p, _i64p]),
     "gdist_sets_bitset_info": (C.c_int, [_setp, _i64p, _i64p]),
     "gdist_sets_bitset_download": (C.c_int, [_setp, _u64p]),
     "gdist_sets_concat": (C.c_int, [_setp, _setp, C.POINTER(_setp)]),
@@ -87,6 +88,8 @@ _SIGS = {
     "gdist_sets_allgather": (C.c_int, [_ctxp, _setp, C.POINTER(_setp)]),
     "gdist_sets_allgather_bitsets": (C.c_int, [_ctxp, _setp, _u32, C.POINTER(_setp)]),
     "gdist_comm_allreduce_max": (C.c_int, [_ctxp, _dblp]),
+    "gdist_sets_block_cost": (C.c_int, [_setp, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_int,
+                                        C.POINTER(C.c_double), C.POINTER(C.c_int)]),
     "gdist_triangle_partition": (C.c_int, [_i64, C.c_int, _i64, _i64p]),
 }
 

@@ -273,11 +273,27 @@ class KmerSets(_Handle):
             return is_rep[:n], rep_of[:n], rep_d[:n]
         return is_rep[:n]
 
+    def block_cost(self, rows: tuple[int, int], cols: tuple[int, int] | None = None,
+                   upper: bool = True) -> tuple[float, int]:
+        """(modelled seconds, rare kernel: 0 list-major / 1 row-major / -1 none)
+        of one matrix call on the block (gdist_sets_block_cost)."""
+        c = cols if cols is not None else (0, len(self))
+        t, rk = C.c_double(), C.c_int()
+        L.check(L.lib.gdist_sets_block_cost(self.h, rows[0], rows[1], c[0], c[1], 1 if upper else 0, C.byref(t),
+                                            C.byref(rk)))
+        return t.value, rk.value
+
     def rare_info(self) -> tuple[int, int, int]:
         """(threshold T, posting lists, records) of the rare tier."""
         t, n, r = C.c_int64(), C.c_int64(), C.c_int64()
         L.check(L.lib.gdist_sets_rare_info(self.h, C.byref(t), C.byref(n), C.byref(r)))
         return t.value, n.value, r.value
+
+    def rare_stats(self) -> tuple[int, int]:
+        """(pair increments, longest posting list) of the rare tier."""
+        i, m = C.c_int64(), C.c_int64()
+        L.check(L.lib.gdist_sets_rare_stats(self.h, C.byref(i), C.byref(m)))
+        return i.value, m.value
 
     def bitsets(self) -> np.ndarray:
         """The dictionary-rank bitsets, (nsets, W) uint64."""

@@ -24,6 +24,48 @@ def triangle_bounds(n: int, nparts: int, align: int = 1) -> list[int]:
     return b
 
 
+def balanced_bounds(n: int, nparts: int, cost) -> list[int]:
+    """Row blocks [b[g], b[g+1]) of the upper triangle minimising the largest
+    modelled block time cost(r0, r1) (monotone: non-decreasing in r1,
+    non-increasing in r0), e.g. KmerSets.block_cost (gdist_sets_block_cost:
+    dense tiles by area, the rare kernel each block would pick by its rows and
+    pairs). Bisection on the target time; each block takes rows greedily
+    while it stays within the target. Exact integer rows; a cost proportional
+    to area gives the equal-area partition (up to a row)."""
+    if nparts <= 1 or n == 0:
+        return [0] + [n] * max(nparts, 1)
+
+    def cut(target: float) -> list[int] | None:
+        b = [0]
+        for _ in range(nparts - 1):
+            r0 = b[-1]
+            lo, hi = r0, n                         # largest r1 with cost(r0, r1) <= target
+            while lo < hi:
+                mid = (lo + hi + 1) // 2
+                if cost(r0, mid) <= target:
+                    lo = mid
+                else:
+                    hi = mid - 1
+            b.append(lo)
+            if lo == n:
+                break
+        b += [n] * (nparts + 1 - len(b))
+        return b if cost(b[-2], n) <= target else None
+
+    lo_t, hi_t = 0.0, cost(0, n)
+    best = cut(hi_t)
+    for _ in range(48):
+        mid = 0.5 * (lo_t + hi_t)
+        b = cut(mid)
+        if b is None:
+            lo_t = mid
+        else:
+            hi_t, best = mid, b
+        if hi_t - lo_t <= 1e-6 * hi_t:
+            break
+    return best
+
+
 def shard_of_sets(n: int, nparts: int) -> list[tuple[int, int]]:
     """Contiguous equal shards of set indices (who packs which genomes)."""
     q, r = divmod(n, nparts)

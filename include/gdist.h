@@ -146,6 +146,9 @@ int  gdist_sets_download(const gdist_sets* sets, int64_t* offsets, uint64_t* cod
 int  gdist_sets_build_bitsets(gdist_sets* sets, unsigned flags);
 int  gdist_sets_build_bitsets_ex(gdist_sets* sets, unsigned flags, int64_t rare_threshold);
 int  gdist_sets_rare_info(const gdist_sets* sets, int64_t* threshold, int64_t* lists, int64_t* records);
+/* Rare-tier statistics behind the cost model: pair increments (sum of
+ * m(m-1)/2 over the posting lists) and the longest list. */
+int  gdist_sets_rare_stats(const gdist_sets* sets, int64_t* pair_incs, int64_t* max_list);
 int  gdist_sets_bitset_info(const gdist_sets* sets, int64_t* dict_size, int64_t* words_per_set);
 /* Copy the bitsets (nsets x words_per_set uint64, row-major) to the host. */
 int  gdist_sets_bitset_download(const gdist_sets* sets, uint64_t* bits);
@@ -230,6 +233,15 @@ int  gdist_sets_allgather(gdist_ctx* ctx, const gdist_sets* local, gdist_sets** 
 int  gdist_sets_allgather_bitsets(gdist_ctx* ctx, const gdist_sets* local, unsigned flags, gdist_sets** out);
 /* Scalar max-reduction and barrier over the communicator (timing only). */
 int  gdist_comm_allreduce_max(gdist_ctx* ctx, double* value);
+
+/* The cost model's estimate (seconds) of one intersect-matrix call on the
+ * block rows [r0, r1) x columns [c0, c1) (upper: pairs j > i only): with
+ * bitsets built, dense tiles + the rare kernel the call would pick
+ * (*rare_kernel = 0 list-major, 1 row-major, -1 no rare tier); otherwise the
+ * sorted join (*rare_kernel = -1). For row partitions that balance modelled
+ * time rather than area (gdist.shard.balanced_bounds). */
+int  gdist_sets_block_cost(const gdist_sets* sets, int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper,
+                           double* seconds, int* rare_kernel);
 
 /* Row partition with equal upper-triangle area:
  * r_g = N (1 - sqrt(1 - g/G)), rounded to multiples of `align`. */

@@ -450,9 +450,10 @@ def test_reps_processors_java_semantics(ctx):
 
 
 def test_bitset_row_blocks_like_ranks(ctx):
-    """Row blocks as the multi-GPU partition hands them out (tile-aligned
-    r0 > 0, all columns, upper): the diagonal tiles of each block run the
-    trimmed variant and every pair is still exact; an unaligned block too."""
+    """Row blocks as the multi-GPU partition hands them out (r0 > 0, all
+    columns, upper; aligned to the 128-set tiles or not) and upper
+    rectangles with c0 > 0: the column tile grid starts at an origin
+    = r0 (mod 128) so diagonal tiles run the trimmed variant; every pair exact."""
     import gdist
     n = 700
     seqs = synth_sets(n, 3000, 0.01, 112)
@@ -460,10 +461,36 @@ def test_bitset_row_blocks_like_ranks(ctx):
     off, codes = oracle_pack(seqs, 21, 0, 0)
     eI, eD = oracle.matrix(off, codes, 0, n, 0, n)
     sets.build_bitsets()
-    for (r0, r1) in [(0, 256), (256, 512), (512, 700), (300, 450)]:
-        I, D = sets.matrix((r0, r1), (0, n), upper=True, method=gdist.METHOD_BITSET)
-        up = np.fromfunction(lambda a, b: b > (r0 + a), (r1 - r0, n))
-        assert np.array_equal(I[up], eI[r0:r1][up]) and bits_equal(D[up], eD[r0:r1][up]), (r0, r1)
+    for (r0, r1, c0, c1) in [(0, 256, 0, n), (256, 512, 0, n), (512, 700, 0, n), (300, 450, 0, n),
+                             (77, 301, 0, n), (100, 300, 50, 700), (400, 650, 133, 690), (5, 60, 0, 40)]:
+        I, D = sets.matrix((r0, r1), (c0, c1), upper=True, method=gdist.METHOD_BITSET)
+        up = np.fromfunction(lambda a, b: (c0 + b) > (r0 + a), (r1 - r0, c1 - c0))
+        assert np.array_equal(I[up], eI[r0:r1, c0:c1][up]), (r0, r1, c0, c1)
+        assert bits_equal(D[up], eD[r0:r1, c0:c1][up]), (r0, r1, c0, c1)
+
+
+def test_bitset_partial_row_tiles(ctx, monkeypatch):
+    """A block whose last row tile holds 1..127 rows runs it through the
+    launches instantiated for RR = ceil(rows / 16) accumulator rows: every RR
+    (1..7, RR = 7 enabled here) and its boundaries, upper (diagonal +
+    off-diagonal partial tiles) and full rectangles, exact against the oracle."""
+    import gdist
+    monkeypatch.setenv("GDIST_BITSET_PARTIAL_RR", "7")
+    n = 420
+    seqs = synth_sets(n, 2500, 0.01, 113)
+    sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
+    off, codes = oracle_pack(seqs, 21, 0, 0)
+    eI, eD = oracle.matrix(off, codes, 0, n, 0, n)
+    sets.build_bitsets()
+    for m in (1, 15, 16, 17, 33, 48, 63, 64, 65, 80, 97, 111, 112, 113, 127):
+        for (r0, up) in ((0, True), (3, True), (150, True), (131, False)):
+            r1 = min(n, r0 + 128 + m)
+            c0, c1 = (0, n) if up else (40, 400)
+            I, D = sets.matrix((r0, r1), (c0, c1), upper=up, method=gdist.METHOD_BITSET)
+            mask = (np.fromfunction(lambda a, b: (c0 + b) > (r0 + a), (r1 - r0, c1 - c0)) if up
+                    else np.ones((r1 - r0, c1 - c0), bool))
+            assert np.array_equal(I[mask], eI[r0:r1, c0:c1][mask]), (m, r0, up)
+            assert bits_equal(D[mask], eD[r0:r1, c0:c1][mask]), (m, r0, up)
 
 
 @pytest.mark.parametrize("strand", [0, 0x1, 0x2])
@@ -495,11 +522,15 @@ def test_k32_all_ones_code(ctx, strand):
 
 
 # ---------------------------------------------------------------- two-tier dictionary
+@pytest.mark.parametrize("kernel", ["0", "1"])
 @pytest.mark.parametrize("T", [0, 3, 8, 1000])
-def test_rare_tier_thresholds_exact(ctx, T):
+def test_rare_tier_thresholds_exact(ctx, T, kernel, monkeypatch):
     """Dense-only (T=0), mixed, and all-rare (T > N) dictionaries give the
-    same bit-exact counts and distances as the oracle."""
+    same bit-exact counts and distances as the oracle, through the list-major
+    (0) and the row-major (1) rare kernel. T > N puts lists of up to N members
+    in the rare tier: the wave-cooperative long-list walks."""
     import gdist
+    monkeypatch.setenv("GDIST_RARE_KERNEL", kernel)
     n = 200
     seqs = synth_sets(n, 6000, 0.01, 101)
     sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
@@ -510,6 +541,10 @@ def test_rare_tier_thresholds_exact(ctx, T):
         assert lists > 0 and recs >= 2 * lists
     else:
         assert lists == 0
+    incs, max_list = sets.rare_stats()
+    assert max_list <= max(T - 1, 0) and (incs > 0) == (lists > 0)
+    if T == 1000:
+        assert max_list >= 64          # long lists take the wave path
     off, codes = oracle_pack(seqs, 21, 0, 0)
     for (r0, r1, c0, c1, up) in [(0, n, 0, n, False), (0, n, 0, n, True), (17, 150, 3, 190, False),
                                  (60, 61, 0, n, False)]:

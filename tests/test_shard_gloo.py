@@ -86,3 +86,28 @@ def test_synth_shards_equal_whole():
     whole = synth.genomes(10, 500, 0.1, 3)
     parts = [synth.genomes(b - a, 500, 0.1, 3, first=a) for a, b in shard.shard_of_sets(10, 3)]
     assert np.array_equal(np.concatenate(parts), whole)
+
+
+def test_balanced_bounds():
+    """Min-max modelled time per rank: dense (area) + per-row costs, and a
+    cost with a fixed per-block term (list-major rare tier)."""
+    from gdist import shard
+    for n, G in ((1000, 2), (2000, 4), (2828, 8), (50, 8), (7, 3)):
+        tot = n * (n - 1) / 2
+        for dense, row, fixed in ((1.0, 0.0, 0.0), (1.0, 0.5, 0.0), (0.2, 1.0, 0.0), (0.0, 1.0, 0.0),
+                                  (1.0, 0.3, 0.05)):
+            def cost(r0, r1):
+                if r1 <= r0:
+                    return 0.0
+                return dense * shard.pairs_in_rows(n, r0, r1) / tot + row * (r1 - r0) / n + fixed
+            b = shard.balanced_bounds(n, G, cost)
+            assert len(b) == G + 1 and b[0] == 0 and b[-1] == n and all(x <= y for x, y in zip(b, b[1:]))
+            costs = [cost(b[g], b[g + 1]) for g in range(G)]
+            step = dense * (n - 1) / tot + row / n            # the most one row can add
+            assert max(costs) <= sum(costs) / G + step + 1e-9, (n, G, dense, row, b)
+            if (row, fixed) == (0.0, 0.0):                   # pure area: the equal-area partition
+                eq = shard.triangle_bounds(n, G, 1)
+                assert all(abs(x - y) <= 1 for x, y in zip(b, eq)), (b, eq)
+            # no partition has a smaller maximum than one more row can explain
+            eq_area = [cost(x, y) for x, y in zip(shard.triangle_bounds(n, G, 1), shard.triangle_bounds(n, G, 1)[1:])]
+            assert max(costs) <= max(eq_area) + 1e-9
