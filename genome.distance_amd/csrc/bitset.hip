@@ -155,22 +155,24 @@ __global__ void posting_sets_kernel(const uint64_t* __restrict__ recs, int64_t n
 // pairs (s = psets[x], t = psets[y]) for y in [y0, e) step dy, s < t
 __device__ __forceinline__ void rare_pair_walk(const uint32_t* __restrict__ psets, int64_t x, int64_t y0, int64_t e,
                                                int dy, int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper,
-                                               int32_t* __restrict__ I, int64_t ldI) {
+                                               int32_t w, int32_t* __restrict__ I, int64_t ldI) {
     const int64_t s = psets[x];
     const bool srow = s >= r0 && s < r1, scol = s >= c0 && s < c1;
     if (!srow && (upper || !scol)) return;
     for (int64_t y = y0; y < e; y += dy) {
         const int64_t t = psets[y];                  // t > s
-        if (srow && t >= c0 && t < c1) atomicAdd(I + (s - r0) * ldI + (t - c0), 1);
-        if (!upper && scol && t >= r0 && t < r1) atomicAdd(I + (t - r0) * ldI + (s - c0), 1);
+        if (srow && t >= c0 && t < c1) atomicAdd(I + (s - r0) * ldI + (t - c0), w);
+        if (!upper && scol && t >= r0 && t < r1) atomicAdd(I + (t - r0) * ldI + (s - c0), w);
     }
 }
 
-// Rare tier: every posting list (ascending set ids) adds 1 to each of its
-// m(m-1)/2 pairs that fall in the region. One lane per list; lists of
-// kLongList+ members are taken by the wave (trip counts are wave-uniform).
+// Rare tier: every posting list (ascending set ids) adds its weight (the
+// number of kmers sharing it) to each of its m(m-1)/2 pairs that fall in the
+// region. One lane per list; lists of kLongList+ members are taken by the
+// wave (trip counts are wave-uniform).
 __global__ __launch_bounds__(256) void rare_pairs_kernel(const int64_t* __restrict__ poff,
-                                                         const uint32_t* __restrict__ psets, int64_t nposts,
+                                                         const uint32_t* __restrict__ psets,
+                                                         const uint32_t* __restrict__ pw, int64_t nposts,
                                                          int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper,
                                                          int32_t* __restrict__ I, int64_t ldI) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -178,16 +180,19 @@ __global__ __launch_bounds__(256) void rare_pairs_kernel(const int64_t* __restri
     for (int64_t pb = (int64_t)blockIdx.x * blockDim.x; pb < nposts; pb += stride) {
         const int64_t p = pb + threadIdx.x;
         int64_t b = 0, e = 0;
-        if (p < nposts) { b = poff[p]; e = poff[p + 1]; }
+        int32_t w = 0;
+        if (p < nposts) { b = poff[p]; e = poff[p + 1]; w = (int32_t)pw[p]; }
         const bool lng = e - b >= kLongList;
         for (unsigned long long m = __ballot(lng); m; m &= m - 1) {
             const int l = __ffsll((long long)m) - 1;
             const int64_t lb = __shfl((long long)b, l, 64), le = __shfl((long long)e, l, 64);
+            const int32_t lw = __shfl(w, l, 64);
             for (int64_t x = lb; x < le - 1; x++)
-                rare_pair_walk(psets, x, x + 1 + lane, le, 64, r0, r1, c0, c1, upper, I, ldI);
+                rare_pair_walk(psets, x, x + 1 + lane, le, 64, r0, r1, c0, c1, upper, lw, I, ldI);
         }
         if (!lng)
-            for (int64_t x = b; x < e - 1; x++) rare_pair_walk(psets, x, x + 1, e, 1, r0, r1, c0, c1, upper, I, ldI);
+            for (int64_t x = b; x < e - 1; x++)
+                rare_pair_walk(psets, x, x + 1, e, 1, r0, r1, c0, c1, upper, w, I, ldI);
     }
 }
 
@@ -204,6 +209,7 @@ constexpr int RCH = 16384;   // max columns per LDS chunk (64 KiB of counters)
 // workgroups share a row chunk and flush with global atomics.
 __global__ __launch_bounds__(256) void rare_rows_kernel(const int64_t* __restrict__ soff,
                                                         const uint64_t* __restrict__ sent,
+                                                        const uint32_t* __restrict__ sw,
                                                         const uint32_t* __restrict__ psets, int64_t r0, int64_t r1,
                                                         int64_t c0, int64_t c1, int nch, int nsplit, int upper,
                                                         int32_t* __restrict__ I, int64_t ldI) {
@@ -227,21 +233,23 @@ __global__ __launch_bounds__(256) void rare_rows_kernel(const int64_t* __restric
     for (int64_t xbase = xb; xbase < xe; xbase += blockDim.x) {   // wave-uniform trip count
         const int64_t x = xbase + threadIdx.x;
         const uint64_t ent = x < xe ? sent[x] : 0ull;  // coalesced: no random bounds lookup
+        const int32_t w = x < xe ? (int32_t)sw[x] : 0;
         const int64_t b = (int64_t)(ent >> 24), e = b + (int64_t)(ent & 0xFFFFFFu);
         const bool lng = e - b >= kLongList;
         for (unsigned long long m = __ballot(lng); m; m &= m - 1) {   // long lists: the wave walks them
             const int l = __ffsll((long long)m) - 1;
             const int64_t lb = __shfl((long long)b, l, 64), le = __shfl((long long)e, l, 64);
+            const int32_t lw = __shfl(w, l, 64);
             for (int64_t y = lb + lane; y < le; y += 64) {
                 const int64_t t = psets[y];
-                if (t >= lo && t < ce && t != i) atomicAdd(&cnt[t - cb], 1);
+                if (t >= lo && t < ce && t != i) atomicAdd(&cnt[t - cb], lw);
             }
         }
         if (lng) continue;
 #pragma unroll 4
         for (int64_t y = b; y < e; y++) {
             const int64_t t = psets[y];
-            if (t >= lo && t < ce && t != i) atomicAdd(&cnt[t - cb], 1);
+            if (t >= lo && t < ce && t != i) atomicAdd(&cnt[t - cb], w);
         }
     }
     __syncthreads();
@@ -260,6 +268,7 @@ __global__ __launch_bounds__(256) void rare_rows_kernel(const int64_t* __restric
 // for every requested column position (duplicates included).
 __global__ __launch_bounds__(256) void rare_query_kernel(const int64_t* __restrict__ soff,
                                                          const uint64_t* __restrict__ sent,
+                                                         const uint32_t* __restrict__ sw,
                                                          const uint32_t* __restrict__ psets, int64_t q,
                                                          int32_t* __restrict__ cnt) {
     const int64_t xb = soff[q], xe = soff[q + 1];
@@ -268,20 +277,22 @@ __global__ __launch_bounds__(256) void rare_query_kernel(const int64_t* __restri
     for (int64_t xbase = xb + (int64_t)blockIdx.x * blockDim.x; xbase < xe; xbase += stride) {
         const int64_t x = xbase + threadIdx.x;
         const uint64_t ent = x < xe ? sent[x] : 0ull;
+        const int32_t w = x < xe ? (int32_t)sw[x] : 0;
         const int64_t b = (int64_t)(ent >> 24), e = b + (int64_t)(ent & 0xFFFFFFu);
         const bool lng = e - b >= kLongList;
         for (unsigned long long m = __ballot(lng); m; m &= m - 1) {
             const int l = __ffsll((long long)m) - 1;
             const int64_t lb = __shfl((long long)b, l, 64), le = __shfl((long long)e, l, 64);
+            const int32_t lw = __shfl(w, l, 64);
             for (int64_t y = lb + lane; y < le; y += 64) {
                 const int64_t t = psets[y];
-                if (t != q) atomicAdd(cnt + t, 1);
+                if (t != q) atomicAdd(cnt + t, lw);
             }
         }
         if (lng) continue;
         for (int64_t y = b; y < e; y++) {
             const int64_t t = psets[y];
-            if (t != q) atomicAdd(cnt + t, 1);
+            if (t != q) atomicAdd(cnt + t, w);
         }
     }
 }
@@ -660,7 +671,8 @@ void bitset_row(gdist_ctx* ctx, const gdist_sets* s, int64_t q, const int64_t* d
         DevBuf cnt(s->nsets * 4 + 4, ctx->stream);
         GD_HIP(hipMemsetAsync(cnt.p, 0, s->nsets * 4, ctx->stream));
         rare_query_kernel<<<256, 256, 0, ctx->stream>>>(s->srare_off.as<int64_t>(), s->srare_ent.as<uint64_t>(),
-                                                        s->post_sets.as<uint32_t>(), q, cnt.as<int32_t>());
+                                                        s->srare_w.as<uint32_t>(), s->post_sets.as<uint32_t>(), q,
+                                                        cnt.as<int32_t>());
         gather_add_kernel<<<(unsigned)ceil_div(ncols, 256), 256, 0, ctx->stream>>>(d_cols, ncols, cnt.as<int32_t>(),
                                                                                    d_I);
         GD_HIP(hipGetLastError());
@@ -1027,18 +1039,123 @@ void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_
     *rare_written = w;
 }
 
-// rare records (rank << 32 | set) -> posting lists CSR on `s`
+// ---- identical posting lists ------------------------------------------
+// Every kmer covering one variant that several sets share has the same
+// holders, so the rare tier is full of identical posting lists (C2: 42 per
+// shared substitution, 21 windows x 2 strands). Such lists are merged into
+// one list whose weight is their number: the kernels add the weight instead
+// of 1, and do the work of one list. Lists are grouped by a 64-bit content
+// hash and merged only after a member-by-member comparison with the group's
+// first list, so a hash collision costs compression, never exactness.
+namespace {
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ void list_hash_kernel(const int64_t* __restrict__ poff, const uint32_t* __restrict__ psets, int64_t nl,
+                                 uint64_t* __restrict__ h, int32_t* __restrict__ ids) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; l < nl; l += stride) {
+        const int64_t b = poff[l], e = poff[l + 1];
+        uint64_t x = mix64(0x9E3779B97F4A7C15ull * (uint64_t)(e - b + 1));
+        for (int64_t y = b; y < e; y++) x = mix64(x ^ (0x632BE59BD9B4E019ull + psets[y]));
+        h[l] = x;
+        ids[l] = (int32_t)l;
+    }
+}
+
+// sorted (hash, list) -> keep[list] = 0 if its contents equal the run's first
+// list (merged into it), else 1; weight[the list it counts for] += 1
+__global__ void list_merge_kernel(const int32_t* __restrict__ ids, const int32_t* __restrict__ flag,
+                                  const int64_t* __restrict__ pos, const int64_t* __restrict__ start, int64_t n,
+                                  const int64_t* __restrict__ poff, const uint32_t* __restrict__ psets,
+                                  int32_t* __restrict__ keep, uint32_t* __restrict__ weight) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const int64_t hd = start[pos[i] + flag[i] - 1];
+        const int32_t l = ids[i], h = ids[hd];
+        bool same = false;
+        if (i != hd) {
+            const int64_t lb = poff[l], le = poff[l + 1], hb = poff[h], he = poff[h + 1];
+            same = le - lb == he - hb;
+            for (int64_t y = 0; same && y < le - lb; y++) same = psets[lb + y] == psets[hb + y];
+        }
+        keep[l] = same ? 0 : 1;
+        atomicAdd(weight + (same ? h : l), 1u);
+    }
+}
+
+__global__ void record_keep_kernel(const uint64_t* __restrict__ recs, int64_t n, const int32_t* __restrict__ keep,
+                                   int32_t* __restrict__ rk) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t y = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; y < n; y += stride) rk[y] = keep[recs[y] >> 32];
+}
+
+// kept lists' records, renumbered: member sets in list order, and the same
+// records keyed by set (set << 32 | new list) for the set -> rare CSR
+__global__ void list_compact_kernel(const uint64_t* __restrict__ recs, int64_t n, const int32_t* __restrict__ keep,
+                                    const int64_t* __restrict__ newid, const int64_t* __restrict__ rpos,
+                                    uint32_t* __restrict__ out_sets, uint64_t* __restrict__ out_recs) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t y = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; y < n; y += stride) {
+        const int64_t l = (int64_t)(recs[y] >> 32);
+        if (!keep[l]) continue;
+        const uint32_t set = (uint32_t)recs[y];
+        out_sets[rpos[y]] = set;
+        out_recs[rpos[y]] = ((uint64_t)set << 32) | (uint64_t)newid[l];
+    }
+}
+
+__global__ void list_offsets_kernel(const int64_t* __restrict__ poff, int64_t nl, const int32_t* __restrict__ keep,
+                                    const int64_t* __restrict__ newid, const int64_t* __restrict__ rpos,
+                                    const uint32_t* __restrict__ weight, int64_t* __restrict__ out_off,
+                                    uint32_t* __restrict__ out_w) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; l < nl; l += stride)
+        if (keep[l]) { out_off[newid[l]] = rpos[poff[l]]; out_w[newid[l]] = weight[l]; }
+}
+
+__global__ void fill_u32_kernel(uint32_t* __restrict__ p, int64_t n, uint32_t v) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = v;
+}
+
+// set-side weights: the weight of each entry's list
+__global__ void entry_weights_kernel(const uint64_t* __restrict__ keys, int64_t n, const uint32_t* __restrict__ pw,
+                                     uint32_t* __restrict__ sw) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) sw[i] = pw[(uint32_t)keys[i]];
+}
+
+}  // namespace
+
+// rare records (rank << 32 | set) -> posting lists CSR on `s`, identical
+// lists merged (GDIST_RARE_DEDUP=0 keeps one list per kmer, A/B)
 void build_postings(gdist_ctx* ctx, gdist_sets* s, unsigned long long* recs, int64_t n, int64_t Ur) {
     hipStream_t st = ctx->stream;
+    Trace tr(st);
     s->n_rare = Ur;
+    s->rare_kmers = Ur;
+    s->rare_records = n;
     s->post_off.alloc((Ur + 1) * 8, st);
     s->post_sets.alloc(n * 4 + 4, st);
     s->rare_incs = s->rare_max_list = s->rare_incs_long = 0;
     if (Ur == 0 || n == 0) {
         GD_HIP(hipMemsetAsync(s->post_off.p, 0, (Ur + 1) * 8, st));
+        s->post_w.alloc(Ur * 4 + 4, st);
+        s->srare_off.alloc((s->nsets + 1) * 8, st);
+        GD_HIP(hipMemsetAsync(s->srare_off.p, 0, (s->nsets + 1) * 8, st));
+        s->srare_ent.alloc(8, st);
+        s->srare_w.alloc(4, st);
+        s->n_rare = 0;
+        s->rare_records = 0;
         GD_HIP(hipStreamSynchronize(st));
         return;
     }
+    GD_REQUIRE(Ur < (int64_t(1) << 31), "rare tier: too many lists");
     DevBuf alt(n * 8, st);
     uint64_t* keys = reinterpret_cast<uint64_t*>(recs);
     uint64_t* kalt = alt.as<uint64_t>();
@@ -1048,33 +1165,90 @@ void build_postings(gdist_ctx* ctx, gdist_sets* s, unsigned long long* recs, int
     posting_offsets_kernel<<<(int)ceil_div(Ur + 1, 256), 256, 0, st>>>(keys, n, Ur, s->post_off.as<int64_t>());
     posting_sets_kernel<<<grid_for(n), 256, 0, st>>>(keys, n, s->post_sets.as<uint32_t>());
     GD_HIP(hipGetLastError());
-    // the same records keyed by set: set -> rare CSR for the row-major kernels
-    swap_halves_kernel<<<grid_for(n), 256, 0, st>>>(keys, n, kalt);
-    GD_HIP(hipGetLastError());
+    tr.mark("postings: lists");
+    const char* dv = getenv("GDIST_RARE_DEDUP");
+    int64_t nl = Ur, nrec = n;
+    if (!(dv && atoi(dv) == 0)) {
+        DevBuf hA(Ur * 8, st), hB(Ur * 8, st), iA(Ur * 4, st), iB(Ur * 4, st);
+        list_hash_kernel<<<grid_for(Ur), 256, 0, st>>>(s->post_off.as<int64_t>(), s->post_sets.as<uint32_t>(), Ur,
+                                                       hA.as<uint64_t>(), iA.as<int32_t>());
+        GD_HIP(hipGetLastError());
+        uint64_t* hk = hA.as<uint64_t>(); uint64_t* hkalt = hB.as<uint64_t>();
+        int32_t* iv = iA.as<int32_t>(); int32_t* ivalt = iB.as<int32_t>();
+        sort_pairs_u64_i32(ctx, hk, hkalt, iv, ivalt, (size_t)Ur, 0, 64);
+        DevBuf flag, pos, uniq, start;
+        int64_t nruns = 0;
+        runs_of(ctx, hk, Ur, flag, pos, uniq, start, nruns);
+        DevBuf keep(Ur * 4 + 4, st), weight(Ur * 4 + 4, st), newid(Ur * 8 + 8, st);
+        GD_HIP(hipMemsetAsync(weight.p, 0, Ur * 4, st));
+        list_merge_kernel<<<grid_for(Ur), 256, 0, st>>>(iv, flag.as<int32_t>(), pos.as<int64_t>(), start.as<int64_t>(),
+                                                        Ur, s->post_off.as<int64_t>(), s->post_sets.as<uint32_t>(),
+                                                        keep.as<int32_t>(), weight.as<uint32_t>());
+        GD_HIP(hipGetLastError());
+        exclusive_scan_i32_to_i64(ctx, keep.as<int32_t>(), newid.as<int64_t>(), (size_t)Ur);
+        DevBuf rk(n * 4 + 4, st), rpos(n * 8 + 8, st);
+        record_keep_kernel<<<grid_for(n), 256, 0, st>>>(keys, n, keep.as<int32_t>(), rk.as<int32_t>());
+        GD_HIP(hipGetLastError());
+        exclusive_scan_i32_to_i64(ctx, rk.as<int32_t>(), rpos.as<int64_t>(), (size_t)n);
+        int64_t h[2];
+        int32_t hf[2];
+        d2h(&h[0], newid.as<int64_t>() + Ur - 1, 8, st);
+        d2h(&h[1], rpos.as<int64_t>() + n - 1, 8, st);
+        d2h(&hf[0], keep.as<int32_t>() + Ur - 1, 4, st);
+        d2h(&hf[1], rk.as<int32_t>() + n - 1, 4, st);
+        nl = h[0] + hf[0];
+        nrec = h[1] + hf[1];
+        DevBuf noff((nl + 1) * 8, st), nsets(nrec * 4 + 4, st);
+        s->post_w.alloc(nl * 4 + 4, st);
+        list_offsets_kernel<<<grid_for(Ur), 256, 0, st>>>(s->post_off.as<int64_t>(), Ur, keep.as<int32_t>(),
+                                                          newid.as<int64_t>(), rpos.as<int64_t>(),
+                                                          weight.as<uint32_t>(), noff.as<int64_t>(),
+                                                          s->post_w.as<uint32_t>());
+        list_compact_kernel<<<grid_for(n), 256, 0, st>>>(keys, n, keep.as<int32_t>(), newid.as<int64_t>(),
+                                                         rpos.as<int64_t>(), nsets.as<uint32_t>(), kalt);
+        GD_HIP(hipGetLastError());
+        h2d(noff.as<int64_t>() + nl, &nrec, 8, st);
+        s->post_off = std::move(noff);
+        s->post_sets = std::move(nsets);
+        tr.mark("postings: merge identical lists");
+    } else {
+        s->post_w.alloc(Ur * 4 + 4, st);
+        fill_u32_kernel<<<grid_for(Ur), 256, 0, st>>>(s->post_w.as<uint32_t>(), Ur, 1u);
+        // the same records keyed by set: set -> rare CSR for the row-major kernels
+        swap_halves_kernel<<<grid_for(n), 256, 0, st>>>(keys, n, kalt);
+        GD_HIP(hipGetLastError());
+    }
+    s->n_rare = nl;
+    s->rare_records = nrec;
+    // kalt: (set << 32 | list) records, sorted by set (into `keys`, then swapped back)
     int sbits = 1;
     while ((int64_t(1) << sbits) < s->nsets) sbits++;
-    sort_keys_u64(ctx, kalt, keys, (size_t)n, 0, std::min(64, 32 + sbits));
+    sort_keys_u64(ctx, kalt, keys, (size_t)nrec, 0, std::min(64, 32 + sbits));
     // packed entries: 40-bit list start, 24-bit length (a rare list has < T <= N + 1 sets)
-    GD_REQUIRE(n < (int64_t(1) << 40) && s->nsets < (int64_t(1) << 24), "rare tier too large for packed list entries");
+    GD_REQUIRE(nrec < (int64_t(1) << 40) && s->nsets < (int64_t(1) << 24), "rare tier too large for packed list entries");
     s->srare_off.alloc((s->nsets + 1) * 8, st);
-    s->srare_ent.alloc(n * 8 + 8, st);
-    posting_offsets_kernel<<<(int)ceil_div(s->nsets + 1, 256), 256, 0, st>>>(kalt, n, s->nsets,
+    s->srare_ent.alloc(nrec * 8 + 8, st);
+    s->srare_w.alloc(nrec * 4 + 4, st);
+    posting_offsets_kernel<<<(int)ceil_div(s->nsets + 1, 256), 256, 0, st>>>(kalt, nrec, s->nsets,
                                                                              s->srare_off.as<int64_t>());
-    rare_entries_kernel<<<grid_for(n), 256, 0, st>>>(kalt, n, s->post_off.as<int64_t>(),
-                                                     s->srare_ent.as<uint64_t>());
+    rare_entries_kernel<<<grid_for(nrec), 256, 0, st>>>(kalt, nrec, s->post_off.as<int64_t>(),
+                                                        s->srare_ent.as<uint64_t>());
+    entry_weights_kernel<<<grid_for(nrec), 256, 0, st>>>(kalt, nrec, s->post_w.as<uint32_t>(),
+                                                         s->srare_w.as<uint32_t>());
     GD_HIP(hipGetLastError());
     // pair increments of the tier (cost model, kernel choice)
     DevBuf d_incs(24, st);
     GD_HIP(hipMemsetAsync(d_incs.p, 0, 24, st));
-    rare_incs_kernel<<<grid_for(Ur, 256, 4096), 256, 0, st>>>(s->post_off.as<int64_t>(), Ur,
+    rare_incs_kernel<<<grid_for(nl, 256, 4096), 256, 0, st>>>(s->post_off.as<int64_t>(), nl,
                                                               d_incs.as<unsigned long long>());
     GD_HIP(hipGetLastError());
-    unsigned long long h[3] = {0, 0, 0};
-    d2h(h, d_incs.p, 24, st);
+    unsigned long long hi[3] = {0, 0, 0};
+    d2h(hi, d_incs.p, 24, st);
     GD_HIP(hipStreamSynchronize(st));
-    s->rare_incs = (int64_t)h[0];
-    s->rare_max_list = (int64_t)h[1];
-    s->rare_incs_long = (int64_t)h[2];
+    s->rare_incs = (int64_t)hi[0];
+    s->rare_max_list = (int64_t)hi[1];
+    s->rare_incs_long = (int64_t)hi[2];
+    tr.mark("postings: set side");
 }
 
 void build_bitsets(gdist_ctx* ctx, gdist_sets* s, unsigned flags, int64_t rare_threshold) {
@@ -1103,7 +1277,6 @@ void build_bitsets(gdist_ctx* ctx, gdist_sets* s, unsigned flags, int64_t rare_t
     s->W = W;
     s->dict_size = U;
     s->rare_T = T;
-    s->rare_records = written;
     s->bits_keep_singletons = keep;
 }
 
@@ -1188,8 +1361,13 @@ void free_bitsets(gdist_sets* s) {
     s->bits.release();
     s->post_off.release();
     s->post_sets.release();
+    s->post_w.release();
+    s->srare_off.release();
+    s->srare_ent.release();
+    s->srare_w.release();
     s->W = s->dict_size = 0;
     s->n_rare = s->rare_T = s->rare_records = s->rare_incs = s->rare_max_list = s->rare_incs_long = 0;
+    s->rare_kmers = 0;
 }
 
 void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1,
@@ -1238,8 +1416,8 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
         GD_HIP(hipEventRecord(ctx->ev_fork, st));
         GD_HIP(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
         rare_pairs_kernel<<<grid_for(s->n_rare, 256, 256 * 64), 256, 0, ctx->side>>>(
-            s->post_off.as<int64_t>(), s->post_sets.as<uint32_t>(), s->n_rare, r0, r1, c0, c1, upper ? 1 : 0, d_I,
-            ldI);
+            s->post_off.as<int64_t>(), s->post_sets.as<uint32_t>(), s->post_w.as<uint32_t>(), s->n_rare, r0, r1, c0,
+            c1, upper ? 1 : 0, d_I, ldI);
         GD_HIP(hipGetLastError());
         GD_HIP(hipEventRecord(ctx->ev_join, ctx->side));
     }
@@ -1332,8 +1510,8 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
             GD_HIP(hipStreamWaitEvent(st, ctx->ev_join, 0));
         } else if (list_major) {
             rare_pairs_kernel<<<grid_for(s->n_rare, 256, 256 * 64), 256, 0, st>>>(
-                s->post_off.as<int64_t>(), s->post_sets.as<uint32_t>(), s->n_rare, r0, r1, c0, c1, upper ? 1 : 0,
-                d_I, ldI);
+                s->post_off.as<int64_t>(), s->post_sets.as<uint32_t>(), s->post_w.as<uint32_t>(), s->n_rare, r0, r1,
+                c0, c1, upper ? 1 : 0, d_I, ldI);
         } else {
             const int nch = (int)ceil_div(nc, RCH);
             const int64_t units = nr * nch;
@@ -1343,6 +1521,7 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
             GD_REQUIRE(rgrid < (int64_t(1) << 31), "rare-tier grid too large");
             const size_t lds = (size_t)std::min<int64_t>(nc, RCH) * 4;
             rare_rows_kernel<<<(unsigned)rgrid, 256, lds, st>>>(s->srare_off.as<int64_t>(), s->srare_ent.as<uint64_t>(),
+                                                                s->srare_w.as<uint32_t>(),
                                                                 s->post_sets.as<uint32_t>(), r0, r1, c0, c1, nch,
                                                                 nsplit, upper ? 1 : 0, d_I, ldI);
         }

@@ -414,6 +414,13 @@ int gdist_sets_rare_info(const gdist_sets* s, int64_t* threshold, int64_t* lists
     });
 }
 
+int gdist_sets_rare_kmers(const gdist_sets* s, int64_t* kmers) {
+    return guard([&] {
+        check_sets(s);
+        if (kmers) *kmers = s->rare_kmers;
+    });
+}
+
 int gdist_sets_rare_stats(const gdist_sets* s, int64_t* pair_incs, int64_t* max_list) {
     return guard([&] {
         check_sets(s);
@@ -1028,7 +1035,6 @@ int gdist_sets_allgather_bitsets(gdist_ctx* ctx, const gdist_sets* local, unsign
             build_postings(ctx, s, lrec.as<unsigned long long>(), written, Ur);
         }
         s->rare_T = T;
-        s->rare_records = totw;
         GD_HIP(hipStreamSynchronize(st));
         *out = s;
     });

@@ -195,6 +195,12 @@ struct gdist_sets {
     gdist::DevBuf srare_off;              // int64 [nsets+1]: set -> its rare kmers (CSR)
     gdist::DevBuf srare_ent;              // uint64 [rare_records]: the set's rare lists as
                                           // (list start << 24 | list length), by rare rank
+    // Kmers whose posting lists are identical (every kmer covering one shared
+    // variant has the same holders) are one list of weight = their number:
+    // post_w[list], and srare_w[] aligned with srare_ent.
+    gdist::DevBuf post_w;                 // uint32 [n_rare]
+    gdist::DevBuf srare_w;                // uint32 [rare_records]
+    int64_t rare_kmers = 0;               // rare dictionary entries before identical lists merge
     bool auto_sorted = false;             // METHOD_AUTO measured the sorted join cheaper
 };
 

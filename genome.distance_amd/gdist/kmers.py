@@ -283,8 +283,14 @@ class KmerSets(_Handle):
                                             C.byref(rk)))
         return t.value, rk.value
 
+    def rare_kmers(self) -> int:
+        """Rare-tier kmers before identical posting lists were merged."""
+        n = C.c_int64()
+        L.check(L.lib.gdist_sets_rare_kmers(self.h, C.byref(n)))
+        return n.value
+
     def rare_info(self) -> tuple[int, int, int]:
-        """(threshold T, posting lists, records) of the rare tier."""
+        """(threshold T, distinct posting lists, their records) of the rare tier."""
         t, n, r = C.c_int64(), C.c_int64(), C.c_int64()
         L.check(L.lib.gdist_sets_rare_info(self.h, C.byref(t), C.byref(n), C.byref(r)))
         return t.value, n.value, r.value

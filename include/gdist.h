@@ -145,7 +145,12 @@ int  gdist_sets_download(const gdist_sets* sets, int64_t* offsets, uint64_t* cod
  * every distinct kmer. */
 int  gdist_sets_build_bitsets(gdist_sets* sets, unsigned flags);
 int  gdist_sets_build_bitsets_ex(gdist_sets* sets, unsigned flags, int64_t rare_threshold);
+/* Rare tier: threshold T, distinct posting lists and their member records.
+ * Kmers with identical posting lists (e.g. every kmer covering one shared
+ * variant) are one list weighted by their number (GDIST_RARE_DEDUP=0: one
+ * list per kmer); gdist_sets_rare_kmers gives the kmers before merging. */
 int  gdist_sets_rare_info(const gdist_sets* sets, int64_t* threshold, int64_t* lists, int64_t* records);
+int  gdist_sets_rare_kmers(const gdist_sets* sets, int64_t* kmers);
 /* Rare-tier statistics behind the cost model: pair increments (sum of
  * m(m-1)/2 over the posting lists) and the longest list. */
 int  gdist_sets_rare_stats(const gdist_sets* sets, int64_t* pair_incs, int64_t* max_list);

@@ -522,23 +522,32 @@ def test_k32_all_ones_code(ctx, strand):
 
 
 # ---------------------------------------------------------------- two-tier dictionary
+@pytest.mark.parametrize("dedup", ["1", "0"])
 @pytest.mark.parametrize("kernel", ["0", "1"])
 @pytest.mark.parametrize("T", [0, 3, 8, 1000])
-def test_rare_tier_thresholds_exact(ctx, T, kernel, monkeypatch):
+def test_rare_tier_thresholds_exact(ctx, T, kernel, dedup, monkeypatch):
     """Dense-only (T=0), mixed, and all-rare (T > N) dictionaries give the
     same bit-exact counts and distances as the oracle, through the list-major
-    (0) and the row-major (1) rare kernel. T > N puts lists of up to N members
-    in the rare tier: the wave-cooperative long-list walks."""
+    (0) and the row-major (1) rare kernel, with identical posting lists merged
+    into weighted lists (1) or one list per kmer (0). T > N puts lists of up
+    to N members in the rare tier: the wave-cooperative long-list walks."""
     import gdist
     monkeypatch.setenv("GDIST_RARE_KERNEL", kernel)
+    monkeypatch.setenv("GDIST_RARE_DEDUP", dedup)
     n = 200
     seqs = synth_sets(n, 6000, 0.01, 101)
     sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
     sets.build_bitsets(rare_threshold=T)
     thr, lists, recs = sets.rare_info()
     assert thr == T
+    kmers = sets.rare_kmers()
     if T > 2:
         assert lists > 0 and recs >= 2 * lists
+        # shared substitutions give every covering kmer the same holders
+        if dedup == "0":
+            assert lists == kmers
+        else:
+            assert lists < (kmers / 4 if T < n else kmers)
     else:
         assert lists == 0
     incs, max_list = sets.rare_stats()
