@@ -113,13 +113,14 @@ __global__ void scatter_bits_kernel(const int32_t* __restrict__ ids, const int32
                                     const int64_t* __restrict__ pos, const int64_t* __restrict__ rank, int64_t n,
                                     int64_t W, unsigned long long* __restrict__ bits, int64_t id_base,
                                     unsigned long long* __restrict__ rare_out, unsigned long long* __restrict__ rare_cnt,
-                                    int64_t rare_cap) {
+                                    int64_t rare_cap, const uint32_t* __restrict__ perm) {
     int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const int64_t run = pos[i] + flag[i] - 1;       // inclusive run index
         const int64_t r = rank[run];
         if (r >= 0) {
-            atomicOr(bits + (int64_t)ids[i] * W + (r >> 6), 1ull << (r & 63));
+            const int64_t b = perm ? (int64_t)perm[r] : r;   // bit position (locus order)
+            atomicOr(bits + (int64_t)ids[i] * W + (b >> 6), 1ull << (b & 63));
         } else if (r <= -2) {
             const unsigned long long slot = atomicAdd(rare_cnt, 1ull);
             if ((int64_t)slot < rare_cap)
@@ -994,7 +995,7 @@ int64_t choose_rare_threshold(const std::vector<uint64_t>& hist, int64_t nsets) 
 // run ranks, scatter); rare-tier records appended to rare_out (capacity cap)
 void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_t U, int64_t W,
                unsigned long long* bits, const uint64_t* rare, int64_t Ur, int64_t id_base,
-               unsigned long long* rare_out, int64_t rare_cap, int64_t* rare_written) {
+               unsigned long long* rare_out, int64_t rare_cap, int64_t* rare_written, const uint32_t* perm) {
     hipStream_t st = ctx->stream;
     const int cbits = std::min(64, code_bits(s->kind, s->k, s->flags));
     Trace tr(st);
@@ -1025,7 +1026,7 @@ void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_
                 tr.mark("fill: copy+sort+runs+rank");
                 scatter_bits_kernel<<<grid_for(n), 256, 0, st>>>(ids, flag.as<int32_t>(), pos.as<int64_t>(),
                                                                  rank.as<int64_t>(), n, W, bits, id_base, rare_out,
-                                                                 rcnt.as<unsigned long long>(), rare_cap);
+                                                                 rcnt.as<unsigned long long>(), rare_cap, perm);
                 GD_HIP(hipGetLastError());
                 GD_HIP(hipStreamSynchronize(st));
                 tr.mark("fill: scatter");
@@ -1264,12 +1265,19 @@ void build_bitsets(gdist_ctx* ctx, gdist_sets* s, unsigned flags, int64_t rare_t
                     dict, U, rare, Ur, mass);
     tr.mark("bitsets: dictionary");
     const int64_t W = bitset_words(U);
+    DevBuf perm;
+    if (s->n_guide > 0 && locus_order_enabled()) {
+        DevBuf key;
+        locus_keys(ctx, s, dict.as<uint64_t>(), U, 0, key);
+        locus_perm(ctx, key, U, perm);
+        tr.mark("bitsets: locus order");
+    }
     s->bits.alloc((size_t)s->nsets * W * 8 + 8, ctx->stream);
     DevBuf recs(mass * 8 + 8, ctx->stream);
     int64_t written = 0;
     tr.mark("bitsets: alloc");
     fill_bits(ctx, s, dict.as<uint64_t>(), U, W, s->bits.as<unsigned long long>(), rare.as<uint64_t>(), Ur, 0,
-              recs.as<unsigned long long>(), mass, &written);
+              recs.as<unsigned long long>(), mass, &written, perm.as<uint32_t>());
     tr.mark("bitsets: fill");
     GD_REQUIRE(written == mass, "rare-tier record count mismatch");
     build_postings(ctx, s, recs.as<unsigned long long>(), written, Ur);
@@ -1278,6 +1286,7 @@ void build_bitsets(gdist_ctx* ctx, gdist_sets* s, unsigned flags, int64_t rare_t
     s->dict_size = U;
     s->rare_T = T;
     s->bits_keep_singletons = keep;
+    build_sparse_words(ctx, s);
 }
 
 RareTier rare_tier(const gdist_sets* s) {
@@ -1341,14 +1350,20 @@ double bitset_block_cost_s(const gdist_sets* s, int64_t r0, int64_t r1, int64_t 
     if (rare_row_major) *rare_row_major = rc.row_major;
     double off, diag;
     dense_tiles(r0, r1, c0, c1, upper, &off, &diag);
-    return (off + kDiagTileShare * diag) * (double)(BT * BT) * (double)s->W / kDenseWordPairsPerS + rc.cost();
+    const double tW = s->sparse ? (double)s->Wd : (double)s->W;
+    // sparse tiles: ~ the block's pair area in 128 x 128 tiles, plus the partial ones on its row edge
+    const double sp_tiles = pairs / (double)(BT * BT) + (double)ceil_div(r1 - r0, BT);
+    return (off + kDiagTileShare * diag) * (double)(BT * BT) * tW / kDenseWordPairsPerS + rc.cost() +
+           sparse_block_cost_s(s, tot > 0 ? std::min(1.0, pairs / tot) : 1.0, sp_tiles);
 }
 
 double bitset_cost_s(const gdist_sets* s, double pairs) {
     // a region given only by its pair count: its share of the rows taken as its share of the pairs
     const double tot = 0.5 * (double)s->nsets * (double)(s->nsets - 1);
     const double frac = tot > 0 ? std::min(1.0, pairs / tot) : 1.0;
-    return pairs * (double)s->W / kDenseWordPairsPerS + rare_choice(rare_tier(s), frac, frac).cost();
+    const double tW = s->sparse ? (double)s->Wd : (double)s->W;
+    return pairs * tW / kDenseWordPairsPerS + rare_choice(rare_tier(s), frac, frac).cost() +
+           sparse_block_cost_s(s, frac, pairs / (double)(BT * BT) + std::sqrt(2.0 * pairs) / BT);
 }
 
 double sorted_cost_s(const gdist_sets* s, double pairs) {
@@ -1358,6 +1373,7 @@ double sorted_cost_s(const gdist_sets* s, double pairs) {
 }
 
 void free_bitsets(gdist_sets* s) {
+    free_sparse(s);
     s->bits.release();
     s->post_off.release();
     s->post_sets.release();
@@ -1386,7 +1402,11 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
             tiles.push_back(make_int2(a, b));
         }
     if (tiles.empty()) return;
-    const int64_t nchunks = s->W / KC;
+    // dense tile operands: every word, or only the dense words when the
+    // complement-sparse words run in their own kernel (sparse.hip)
+    const unsigned long long* tbits = s->sparse ? s->dbits.as<unsigned long long>() : s->bits.as<unsigned long long>();
+    const int64_t tW = s->sparse ? s->Wd : s->W;
+    const int64_t nchunks = tW / KC;
     // split the word dimension so the launch holds ≳ 8 workgroups per CU
     const int64_t target = (int64_t)ctx->cus * 8;
     int splits = (int)std::max<int64_t>(1, std::min<int64_t>(nchunks, ceil_div(target, (int64_t)tiles.size())));
@@ -1411,21 +1431,29 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     const bool list_major = rv ? atoi(rv) == 0 : !row_major;
     const char* ov = getenv("GDIST_RARE_OVERLAP");
     const bool overlap = s->n_rare > 0 && list_major && !(ov && atoi(ov) == 0);
+    // The sparse words and the list-major rare kernel add atomically, like
+    // the dense tiles, so they run on the side stream beside them.
+    const bool side = overlap || s->sparse;
+    DevBuf sp_tiles;
     GD_HIP(hipEventRecord(ctx->ev_k0, st));
-    if (overlap) {
+    if (side) {
         GD_HIP(hipEventRecord(ctx->ev_fork, st));
         GD_HIP(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
-        rare_pairs_kernel<<<grid_for(s->n_rare, 256, 256 * 64), 256, 0, ctx->side>>>(
-            s->post_off.as<int64_t>(), s->post_sets.as<uint32_t>(), s->post_w.as<uint32_t>(), s->n_rare, r0, r1, c0,
-            c1, upper ? 1 : 0, d_I, ldI);
+        if (s->sparse) sparse_matrix(ctx, s, r0, r1, c0, c1, upper, d_I, ldI, ctx->side, sp_tiles);
+        if (overlap)
+            rare_pairs_kernel<<<grid_for(s->n_rare, 256, 256 * 64), 256, 0, ctx->side>>>(
+                s->post_off.as<int64_t>(), s->post_sets.as<uint32_t>(), s->post_w.as<uint32_t>(), s->n_rare, r0, r1,
+                c0, c1, upper ? 1 : 0, d_I, ldI);
         GD_HIP(hipGetLastError());
         GD_HIP(hipEventRecord(ctx->ev_join, ctx->side));
     }
-    if (variant == 1) {
-        bitset_tile_kernel<<<(unsigned)grid, NT, 0, st>>>(s->bits.as<unsigned long long>(), s->W, dt.as<int2>(),
+    if (tW == 0) {
+        // no dense words: the sparse kernel holds the whole dense tier
+    } else if (variant == 1) {
+        bitset_tile_kernel<<<(unsigned)grid, NT, 0, st>>>(tbits, tW, dt.as<int2>(),
                                                            splits, nchunks, r0, r1, c0, c1, upper ? 1 : 0, d_I, ldI);
     } else {
-        const int64_t nch2 = s->W / KC2;
+        const int64_t nch2 = tW / KC2;
         // Diagonal tiles of an upper-triangle region (row0 == col0) get their
         // own launch of the DIAG variant, which skips the accumulators that
         // only hold pairs with j <= i (GDIST_BITSET_DIAG=0 keeps one launch).
@@ -1475,7 +1503,7 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
                 1, std::min<int64_t>(std::max<int64_t>(1, nch2 / min_kc), ceil_div(target2, (int64_t)nt)));
             const int64_t grid2 = (int64_t)nt * sp2;
             GD_REQUIRE(grid2 < (int64_t(1) << 31), "bitset matrix grid too large");
-            kern<<<(unsigned)grid2, NT, 0, st>>>(s->bits.as<unsigned long long>(), s->W, dtiles, (int)nt, sp2, nch2,
+            kern<<<(unsigned)grid2, NT, 0, st>>>(tbits, tW, dtiles, (int)nt, sp2, nch2,
                                                  r0, r1, c0, c1, corg, upper ? 1 : 0, d_I, ldI);
         };
         const int2* dg = dt2.as<int2>();
@@ -1505,9 +1533,9 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     }
     GD_HIP(hipGetLastError());
     ctx->last.launches = 1;
+    if (side) GD_HIP(hipStreamWaitEvent(st, ctx->ev_join, 0));
     if (s->n_rare > 0) {
         if (overlap) {
-            GD_HIP(hipStreamWaitEvent(st, ctx->ev_join, 0));
         } else if (list_major) {
             rare_pairs_kernel<<<grid_for(s->n_rare, 256, 256 * 64), 256, 0, st>>>(
                 s->post_off.as<int64_t>(), s->post_sets.as<uint32_t>(), s->post_w.as<uint32_t>(), s->n_rare, r0, r1,

@@ -414,6 +414,15 @@ int gdist_sets_rare_info(const gdist_sets* s, int64_t* threshold, int64_t* lists
     });
 }
 
+int gdist_sets_sparse_info(const gdist_sets* s, int64_t* sparse_words, int64_t* dense_words, int64_t* entries) {
+    return guard([&] {
+        check_sets(s);
+        if (sparse_words) *sparse_words = s->sparse ? s->Ws : 0;
+        if (dense_words) *dense_words = s->sparse ? s->Wd : s->W;
+        if (entries) *entries = s->sparse ? s->sp_entries : 0;
+    });
+}
+
 int gdist_sets_rare_kmers(const gdist_sets* s, int64_t* kmers) {
     return guard([&] {
         check_sets(s);
@@ -475,6 +484,17 @@ int gdist_sets_concat(const gdist_sets* a, const gdist_sets* b, gdist_sets** out
         if (b->total)
             GD_HIP(hipMemcpyAsync((char*)s->codes.p + a->total * es, b->codes.p, b->total * es,
                                   hipMemcpyDeviceToDevice, ctx->stream));
+        // locus guides: the first collection's (its sets come first), else the second's
+        const gdist_sets* g = a->n_guide ? a : b;
+        if (g->n_guide) {
+            s->guide_codes.alloc(g->n_guide * 8, ctx->stream);
+            s->guide_keys.alloc(g->n_guide * 8, ctx->stream);
+            GD_HIP(hipMemcpyAsync(s->guide_codes.p, g->guide_codes.p, g->n_guide * 8, hipMemcpyDeviceToDevice,
+                                  ctx->stream));
+            GD_HIP(hipMemcpyAsync(s->guide_keys.p, g->guide_keys.p, g->n_guide * 8, hipMemcpyDeviceToDevice,
+                                  ctx->stream));
+            s->n_guide = g->n_guide;
+        }
         GD_HIP(hipStreamSynchronize(ctx->stream));
         *out = s;
     });
@@ -965,11 +985,25 @@ int gdist_sets_allgather_bitsets(gdist_ctx* ctx, const gdist_sets* local, unsign
         int64_t id_base = 0;
         for (int r = 0; r < ctx->rank && R > 1; r++) id_base += hall[2 * r];
         const int64_t cap = local_rare_mass(ctx, sum, rare.as<uint64_t>(), Ur);
+        // locus order of the dense ranks: every rank keys them by its own
+        // guides (tagged with the rank, so rank 0's guides come first), one
+        // all-gather, the minimum over ranks -> the same permutation everywhere
+        DevBuf perm;
+        if (locus_order_enabled()) {
+            DevBuf key;
+            locus_keys(ctx, local, dict.as<uint64_t>(), U, (uint64_t)ctx->rank << 40, key);
+            if (R > 1) {
+                DevBuf allk((U * 8 + 8) * R, st);
+                allgather(ctx, key.p, allk.p, U * 8 + 8);
+                locus_keys_min(ctx, allk.as<uint64_t>(), U, U + 1, R, key);
+            }
+            locus_perm(ctx, key, U, perm);
+        }
         DevBuf lb((size_t)mxs * W * 8 + 8, st), lrec(cap * 8 + 8, st);
         int64_t written = 0;
         if (local->nsets)
             fill_bits(ctx, local, dict.as<uint64_t>(), U, W, lb.as<unsigned long long>(), rare.as<uint64_t>(), Ur,
-                      id_base, lrec.as<unsigned long long>(), cap, &written);
+                      id_base, lrec.as<unsigned long long>(), cap, &written, perm.as<uint32_t>());
         auto* s = new gdist_sets();
         s->ctx = ctx; s->kind = local->kind; s->k = local->k; s->flags = local->flags;
         s->nsets = N; s->has_codes = false;
@@ -1035,6 +1069,7 @@ int gdist_sets_allgather_bitsets(gdist_ctx* ctx, const gdist_sets* local, unsign
             build_postings(ctx, s, lrec.as<unsigned long long>(), written, Ur);
         }
         s->rare_T = T;
+        build_sparse_words(ctx, s);
         GD_HIP(hipStreamSynchronize(st));
         *out = s;
     });

@@ -201,6 +201,23 @@ struct gdist_sets {
     gdist::DevBuf post_w;                 // uint32 [n_rare]
     gdist::DevBuf srare_w;                // uint32 [rare_records]
     int64_t rare_kmers = 0;               // rare dictionary entries before identical lists merge
+    // locus guides (pack time, sparse.hip): the kmers of the first kGuides
+    // sequences with the position of their first window (window * strands +
+    // strand, guides in order), sorted by code
+    gdist::DevBuf guide_codes;            // uint64 [n_guide]
+    gdist::DevBuf guide_keys;             // uint64 [n_guide]
+    int64_t n_guide = 0;
+    // complement-sparse words of the dense tier (sparse.hip)
+    bool sparse = false;
+    gdist::DevBuf dbits;                  // uint64 [nsets][Wd]: the dense words only (tile kernels)
+    int64_t Wd = 0;                       // dense words, padded to 16 (0: none)
+    int64_t Ws = 0;                       // sparse words
+    gdist::DevBuf sp_off;                 // int64 [ceil(nsets/128) * Ws + 1]: (set block, sparse word) -> entries
+    gdist::DevBuf sp_word;                // uint64 [sp_entries]: complement word ~bits & valid
+    gdist::DevBuf sp_set;                 // uint8 [sp_entries]: set - 128 * block
+    gdist::DevBuf sp_nc;                  // int32 [nsets]: complement bits over the sparse words
+    int64_t sp_entries = 0, sp_U = 0;     // entries; valid bits of the sparse words
+    double sp_products = 0, sp_items = 0; // whole-triangle products / (tile, word) visits (cost model)
     bool auto_sorted = false;             // METHOD_AUTO measured the sorted join cheaper
 };
 
@@ -239,9 +256,11 @@ int64_t auto_rare_threshold(int64_t nsets);
 // cost-optimal rare threshold from hist[c] = number of kmers held by c sets
 // (c = 0..nsets); the chosen T is reported by gdist_sets_rare_info
 int64_t choose_rare_threshold(const std::vector<uint64_t>& hist, int64_t nsets);
+// perm (optional): bit position of each dense rank (locus order)
 void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_t U, int64_t W,
                unsigned long long* bits, const uint64_t* rare, int64_t Ur, int64_t id_base,
-               unsigned long long* rare_out, int64_t rare_cap, int64_t* rare_written);
+               unsigned long long* rare_out, int64_t rare_cap, int64_t* rare_written,
+               const uint32_t* perm = nullptr);
 void build_postings(gdist_ctx* ctx, gdist_sets* s, unsigned long long* recs, int64_t n, int64_t Ur);
 // Cost model (seconds), calibrated on MI355X from per-kernel rocprofv3
 // averages (scripts/calib_rare.sh; profiles/r01/rare_model): bitset = dense
@@ -292,6 +311,23 @@ void free_bitsets(gdist_sets* s);
 void build_bitsets(gdist_ctx* ctx, gdist_sets* s, unsigned flags, int64_t rare_threshold = -1);
 void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0,
                    int64_t c1, bool upper, int32_t* d_I, int64_t ldI);
+
+// sparse.hip — locus order of the dense dictionary, complement-sparse words
+constexpr int kGuides = 2;                       // guide sequences per packed collection
+constexpr double kSparseProductsPerS = 1.0e11;   // sparse tiles: complement-word products
+constexpr double kSparseItemsPerS = 2.0e10;      // sparse tiles: (tile, sparse word) visits
+bool locus_order_enabled();                      // GDIST_LOCUS_ORDER=0 keeps code order (A/B)
+// key[r] = tag | guide position of dense rank r (all ones where no guide holds it)
+void locus_keys(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_t U, uint64_t tag, DevBuf& key);
+// key[r] = min over R ranks' keys (all[q * stride_r + r])
+void locus_keys_min(gdist_ctx* ctx, const uint64_t* all, int64_t U, int64_t stride_r, int R, DevBuf& key);
+// perm[r] = bit position of dense rank r: ascending key, ties in rank order
+void locus_perm(gdist_ctx* ctx, DevBuf& key, int64_t U, DevBuf& perm);
+void build_sparse_words(gdist_ctx* ctx, gdist_sets* s);
+void free_sparse(gdist_sets* s);
+double sparse_block_cost_s(const gdist_sets* s, double f_area, double tiles);
+void sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1, bool upper,
+                   int32_t* d_I, int64_t ldI, hipStream_t st, DevBuf& dt);
 
 // sorted.hip
 void build_segments(gdist_ctx* ctx, gdist_sets* s);

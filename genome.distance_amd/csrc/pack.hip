@@ -194,7 +194,79 @@ inline int grid_for(int64_t n, int block = 256, int64_t cap = 256 * 32) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(g, cap));
 }
 
+__global__ void valid_flags_kernel(const int32_t* __restrict__ ids, int64_t n, int32_t invalid,
+                                   int32_t* __restrict__ flag) {
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        flag[i] = ids[i] != invalid ? 1 : 0;
+}
+
+// valid extracted entries -> (code, entry index); the index is the locus key
+__global__ void guide_compact_kernel(const uint64_t* __restrict__ keys, const int32_t* __restrict__ flag,
+                                     const int64_t* __restrict__ pos, int64_t n, uint64_t* __restrict__ codes,
+                                     int32_t* __restrict__ idx) {
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        if (flag[i]) { codes[pos[i]] = keys[i]; idx[pos[i]] = (int32_t)i; }
+}
+
+__global__ void code_heads_kernel(const uint64_t* __restrict__ codes, int64_t n, int32_t* __restrict__ flag) {
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        flag[i] = (i == 0 || codes[i] != codes[i - 1]) ? 1 : 0;
+}
+
+__global__ void guide_unique_kernel(const uint64_t* __restrict__ codes, const int32_t* __restrict__ idx,
+                                    const int32_t* __restrict__ flag, const int64_t* __restrict__ pos, int64_t n,
+                                    uint64_t* __restrict__ ucodes, uint64_t* __restrict__ ukeys) {
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        if (flag[i]) { ucodes[pos[i]] = codes[i]; ukeys[pos[i]] = (uint64_t)idx[i]; }
+}
+
 }  // namespace
+
+// Locus guides of a collection (sparse.hip): the first n extracted entries
+// (the windows of the first kGuides sequences, in window order; with both
+// strands entry 2w + strand) -> distinct codes with the index of their first
+// valid entry. The radix sort is stable, so the first entry of a code's run
+// is its first occurrence.
+static void guide_from_extract(gdist_ctx* ctx, const uint64_t* keys, const int32_t* ids, int64_t n, int32_t invalid,
+                               int cbits, gdist_sets* out) {
+    hipStream_t st = ctx->stream;
+    out->n_guide = 0;
+    if (n <= 0 || n >= (int64_t(1) << 31)) return;
+    DevBuf flag(n * 4 + 4, st), pos(n * 8 + 8, st);
+    valid_flags_kernel<<<grid_for(n), 256, 0, st>>>(ids, n, invalid, flag.as<int32_t>());
+    GD_HIP(hipGetLastError());
+    exclusive_scan_i32_to_i64(ctx, flag.as<int32_t>(), pos.as<int64_t>(), (size_t)n);
+    int64_t last = 0;
+    int32_t lf = 0;
+    d2h(&last, pos.as<int64_t>() + n - 1, 8, st);
+    d2h(&lf, flag.as<int32_t>() + n - 1, 4, st);
+    const int64_t nv = last + lf;
+    if (nv == 0) return;
+    DevBuf kA(nv * 8, st), kB(nv * 8, st), vA(nv * 4, st), vB(nv * 4, st);
+    guide_compact_kernel<<<grid_for(n), 256, 0, st>>>(keys, flag.as<int32_t>(), pos.as<int64_t>(), n,
+                                                      kA.as<uint64_t>(), vA.as<int32_t>());
+    GD_HIP(hipGetLastError());
+    uint64_t* k = kA.as<uint64_t>(); uint64_t* ka = kB.as<uint64_t>();
+    int32_t* v = vA.as<int32_t>(); int32_t* va = vB.as<int32_t>();
+    sort_pairs_u64_i32(ctx, k, ka, v, va, (size_t)nv, 0, std::min(64, cbits));
+    code_heads_kernel<<<grid_for(nv), 256, 0, st>>>(k, nv, flag.as<int32_t>());
+    GD_HIP(hipGetLastError());
+    exclusive_scan_i32_to_i64(ctx, flag.as<int32_t>(), pos.as<int64_t>(), (size_t)nv);
+    d2h(&last, pos.as<int64_t>() + nv - 1, 8, st);
+    d2h(&lf, flag.as<int32_t>() + nv - 1, 4, st);
+    const int64_t nu = last + lf;
+    out->guide_codes.alloc(nu * 8, st);
+    out->guide_keys.alloc(nu * 8, st);
+    guide_unique_kernel<<<grid_for(nv), 256, 0, st>>>(k, v, flag.as<int32_t>(), pos.as<int64_t>(), nv,
+                                                      out->guide_codes.as<uint64_t>(), out->guide_keys.as<uint64_t>());
+    GD_HIP(hipGetLastError());
+    GD_HIP(hipStreamSynchronize(st));
+    out->n_guide = nu;
+}
 
 void sort_pairs_u64_i32(gdist_ctx* ctx, uint64_t*& keys, uint64_t*& keys_alt, int32_t*& vals,
                         int32_t*& vals_alt, size_t n, int begin_bit, int end_bit) {
@@ -367,6 +439,9 @@ void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_se
             GD_HIP(hipGetLastError());
         }
         tr.mark("pack: alloc+extract");
+        if (s0 == 0 && nw > 0 && locus_order_enabled())
+            guide_from_extract(ctx, kA.as<uint64_t>(), vA.as<int32_t>(), hwo[std::min(nc, kGuides)] * mult, nc,
+                               cbits, out);
         uint64_t* keys = kA.as<uint64_t>(); uint64_t* keys_alt = kB.as<uint64_t>();
         int32_t* ids = vA.as<int32_t>(); int32_t* ids_alt = vB.as<int32_t>();
         PackDebug* dbg = (s0 == 0) ? g_pack_debug : nullptr;

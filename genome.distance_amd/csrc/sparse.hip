@@ -1,0 +1,409 @@
+// sparse.hip — locus order of the dense dictionary and the complement-sparse
+// words of the dense tier.
+//
+// The dense tier holds kmers most sets share (C2: the ancestral kmers, in
+// ~98 % of the genomes). A set lacks such a kmer only near its own variants,
+// and a substitution removes the k consecutive windows that cover it, on both
+// strands. Ranked in code order those absences are scattered over every word
+// of the bitset; ranked in LOCUS order (the window position of the kmer in a
+// guide sequence, strands interleaved) they fall into 1-2 words per variant.
+// The dictionary rank -> bit position map is therefore a permutation that
+// sorts the dense kmers by (guide, window, strand); kmers no guide holds keep
+// code order at the end. Any bijection gives the same popcounts, so this
+// changes only where work can be skipped, never a count.
+//
+// Then each 64-bit word w of the dense tier is classified by z_w, the number
+// of sets whose complement word c_i[w] = ~bits_i[w] & valid(w) is non-zero:
+//   * dense words (large z_w) stay bit columns for the AND+popcount tiles;
+//   * sparse words contribute, per pair,
+//       sum_w popc(a_w & b_w) = U_s - nc_i - nc_j + sum_{w in both lists} popc(c_i[w] & c_j[w])
+//     with U_s the valid bits of the sparse words and nc_i the complement
+//     bits of set i over them: only the words where BOTH sets lack something
+//     cost work. Entries are grouped by (128-set block, sparse word), so a tile
+//     of 128 x 128 pairs visits, per word, the few rows and columns that have
+//     an entry and adds their products into LDS counters.
+// C2 (1000 x 2 Mbp): 62.5 K words of which every one is sparse (z_w ~ 51 of
+// 1000), 95 M products per step instead of 31 G word pairs.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "gdist_internal.hpp"
+
+namespace gdist {
+namespace {
+
+inline int grid_for(int64_t n, int block = 256, int64_t cap = 256 * 32) {
+    int64_t g = ceil_div(n, block);
+    return (int)std::max<int64_t>(1, std::min<int64_t>(g, cap));
+}
+
+constexpr int SB = 128;                  // sets per block of the sparse entry index (tile edge)
+
+// ---- locus order -------------------------------------------------------
+__global__ void locus_key_kernel(const uint64_t* __restrict__ gcodes, const uint64_t* __restrict__ gkeys, int64_t ng,
+                                 const uint64_t* __restrict__ dict, int64_t U, uint64_t tag,
+                                 uint64_t* __restrict__ key) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < ng; g += stride) {
+        const uint64_t c = gcodes[g];
+        int64_t lo = 0, hi = U;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (dict[mid] < c) lo = mid + 1; else hi = mid;
+        }
+        if (lo < U && dict[lo] == c) key[lo] = tag | gkeys[g];   // guide codes are unique: one writer per rank
+    }
+}
+
+__global__ void fill_u64_kernel(uint64_t* __restrict__ p, int64_t n, uint64_t v) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = v;
+}
+
+__global__ void iota_i32_kernel(int32_t* __restrict__ p, int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = (int32_t)i;
+}
+
+__global__ void min_over_ranks_kernel(const uint64_t* __restrict__ all, int64_t U, int64_t stride_r, int R,
+                                      uint64_t* __restrict__ key) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < U; r += stride) {
+        uint64_t m = all[r];
+        for (int q = 1; q < R; q++) m = all[q * stride_r + r] < m ? all[q * stride_r + r] : m;
+        key[r] = m;
+    }
+}
+
+__global__ void invert_perm_kernel(const int32_t* __restrict__ order, int64_t U, uint32_t* __restrict__ perm) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < U; i += stride) perm[order[i]] = (uint32_t)i;
+}
+
+// ---- word classification ------------------------------------------------
+__device__ __forceinline__ unsigned long long valid_mask(int64_t w, int64_t U) {
+    const int64_t full = U >> 6;
+    if (w < full) return ~0ull;
+    if (w == full && (U & 63)) return (1ull << (U & 63)) - 1ull;
+    return 0ull;
+}
+
+// z[w] += number of sets in this block of rows whose complement word is non-zero
+__global__ __launch_bounds__(256) void word_z_kernel(const unsigned long long* __restrict__ bits, int64_t N, int64_t W,
+                                                     int64_t U, int64_t rows_per_block, int32_t* __restrict__ z) {
+    const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t i0 = (int64_t)blockIdx.y * rows_per_block;
+    const int64_t i1 = i0 + rows_per_block < N ? i0 + rows_per_block : N;
+    if (w >= W) return;
+    const unsigned long long m = valid_mask(w, U);
+    int c = 0;
+    for (int64_t i = i0; i < i1; i++) c += (bits[i * W + w] & m) != m;
+    if (c) atomicAdd(z + w, c);
+}
+
+__global__ void gather_words_kernel(const unsigned long long* __restrict__ bits, int64_t W,
+                                    const int32_t* __restrict__ dw, int64_t Wd, int64_t Wdp, int64_t N,
+                                    unsigned long long* __restrict__ out) {
+    const int64_t n = N * Wdp;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
+        const int64_t i = e / Wdp, d = e - i * Wdp;
+        out[e] = d < Wd ? bits[i * W + dw[d]] : 0ull;
+    }
+}
+
+// entries per (block b, sparse word s): sets of the block whose complement word is non-zero
+__global__ __launch_bounds__(256) void sparse_count_kernel(const unsigned long long* __restrict__ bits, int64_t N,
+                                                           int64_t W, int64_t U, const int32_t* __restrict__ sw,
+                                                           int64_t Ws, int32_t* __restrict__ cnt) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t b = blockIdx.y;
+    if (s >= Ws) return;
+    const int64_t w = sw[s];
+    const unsigned long long m = valid_mask(w, U);
+    const int64_t i1 = (b + 1) * SB < N ? (b + 1) * SB : N;
+    int c = 0;
+    for (int64_t i = b * SB; i < i1; i++) c += (bits[i * W + w] & m) != m;
+    cnt[b * Ws + s] = c;
+}
+
+__global__ __launch_bounds__(256) void sparse_fill_kernel(const unsigned long long* __restrict__ bits, int64_t N,
+                                                          int64_t W, int64_t U, const int32_t* __restrict__ sw,
+                                                          int64_t Ws, const int64_t* __restrict__ off,
+                                                          unsigned long long* __restrict__ word,
+                                                          uint8_t* __restrict__ set, int32_t* __restrict__ nc) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t b = blockIdx.y;
+    if (s >= Ws) return;
+    const int64_t w = sw[s];
+    const unsigned long long m = valid_mask(w, U);
+    const int64_t i1 = (b + 1) * SB < N ? (b + 1) * SB : N;
+    int64_t p = off[b * Ws + s];
+    for (int64_t i = b * SB; i < i1; i++) {
+        const unsigned long long c = ~bits[i * W + w] & m;
+        if (c) {
+            word[p] = c;
+            set[p] = (uint8_t)(i - b * SB);
+            p++;
+            atomicAdd(nc + i, (int32_t)__popcll(c));
+        }
+    }
+}
+
+// ---- the sparse tile kernel ---------------------------------------------
+// One workgroup per (128 x 128 tile of absolute set blocks (A, B), chunk of
+// the sparse words). Each wave takes 64 sparse words at a time: lane l loads
+// the (A, s) and (B, s) entry ranges of word s = base + l, the wave
+// prefix-sums their products r_s x c_s, and the 64 lanes then walk the
+// flattened products (word found by binary search over the prefix in LDS),
+// adding popc(c_i & c_j) to LDS counters. The flush adds the counters - and,
+// from chunk 0, the constant part U_s - nc_i - nc_j - to I with atomics.
+constexpr int SNT = 512;                 // threads per workgroup
+constexpr int SNW = SNT / 64;
+
+__global__ __launch_bounds__(SNT, 2) void sparse_tile_kernel(
+    const int64_t* __restrict__ off, const unsigned long long* __restrict__ word, const uint8_t* __restrict__ set,
+    const int32_t* __restrict__ nc, int64_t Us, int64_t Ws, const int2* __restrict__ tiles, int nchunks,
+    int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I, int64_t ldI) {
+    __shared__ int32_t cnt[SB * SB];                                       // 64 KiB
+    __shared__ int32_t pre[SNW][65];
+    __shared__ int64_t rbeg[SNW][64], cbeg[SNW][64];
+    __shared__ int32_t ncol[SNW][64];
+    const int tile = blockIdx.x / nchunks, ch = blockIdx.x % nchunks;
+    const int64_t A = tiles[tile].x, B = tiles[tile].y;
+    for (int t = threadIdx.x; t < SB * SB; t += SNT) cnt[t] = 0;
+    __syncthreads();
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t sb = Ws * ch / nchunks, se = Ws * (ch + 1) / nchunks;
+    const int64_t* offA = off + A * Ws;
+    const int64_t* offB = off + B * Ws;
+    for (int64_t base = sb + (int64_t)wv * 64; base < se; base += (int64_t)SNW * 64) {
+        const int64_t s = base + lane;
+        int64_t rb = 0, cb = 0;
+        int nr = 0, ncl = 0;
+        if (s < se) {
+            rb = offA[s]; nr = (int)(offA[s + 1] - rb);
+            cb = offB[s]; ncl = (int)(offB[s + 1] - cb);
+        }
+        int p = nr * ncl, incl = p;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += v;
+        }
+        pre[wv][lane + 1] = incl;
+        if (lane == 0) pre[wv][0] = 0;
+        rbeg[wv][lane] = rb;
+        cbeg[wv][lane] = cb;
+        ncol[wv][lane] = ncl;
+        const int total = __shfl(incl, 63, 64);
+        __builtin_amdgcn_wave_barrier();
+        for (int f = lane; f < total; f += 64) {
+            int lo = 0, hi = 64;                   // pre[lo] <= f < pre[hi]
+#pragma unroll
+            for (int step = 0; step < 6; step++) {
+                const int mid = (lo + hi) >> 1;
+                if (pre[wv][mid] <= f) lo = mid; else hi = mid;
+            }
+            const int q = f - pre[wv][lo];
+            const int n2 = ncol[wv][lo];
+            int x = (int)((float)q / (float)n2);
+            if (x * n2 > q) x--;
+            else if ((x + 1) * n2 <= q) x++;
+            const int y = q - x * n2;
+            const int64_t ri = rbeg[wv][lo] + x, ci = cbeg[wv][lo] + y;
+            const int v = __popcll(word[ri] & word[ci]);
+            if (v) atomicAdd(&cnt[(int)set[ri] * SB + (int)set[ci]], v);
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < SB * SB; t += SNT) {
+        const int64_t i = A * SB + (t >> 7), j = B * SB + (t & (SB - 1));
+        if (i < r0 || i >= r1 || j < c0 || j >= c1 || (upper && j <= i)) continue;
+        int v = cnt[t];
+        if (ch == 0) v += (int)Us - nc[i] - nc[j];
+        if (v) atomicAdd(I + (i - r0) * ldI + (j - c0), v);
+    }
+}
+
+}  // namespace
+
+// ---- host side ------------------------------------------------------------
+
+void locus_keys(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_t U, uint64_t tag, DevBuf& key) {
+    hipStream_t st = ctx->stream;
+    key.alloc(U * 8 + 8, st);
+    if (U == 0) return;
+    fill_u64_kernel<<<grid_for(U), 256, 0, st>>>(key.as<uint64_t>(), U, ~0ull);
+    if (s->n_guide > 0)
+        locus_key_kernel<<<grid_for(s->n_guide), 256, 0, st>>>(s->guide_codes.as<uint64_t>(),
+                                                               s->guide_keys.as<uint64_t>(), s->n_guide, dict, U, tag,
+                                                               key.as<uint64_t>());
+    GD_HIP(hipGetLastError());
+}
+
+void locus_keys_min(gdist_ctx* ctx, const uint64_t* all, int64_t U, int64_t stride_r, int R, DevBuf& key) {
+    hipStream_t st = ctx->stream;
+    key.alloc(U * 8 + 8, st);
+    if (U == 0) return;
+    min_over_ranks_kernel<<<grid_for(U), 256, 0, st>>>(all, U, stride_r, R, key.as<uint64_t>());
+    GD_HIP(hipGetLastError());
+}
+
+void locus_perm(gdist_ctx* ctx, DevBuf& key, int64_t U, DevBuf& perm) {
+    hipStream_t st = ctx->stream;
+    GD_REQUIRE(U < (int64_t(1) << 31), "dense dictionary too large for the locus order");
+    perm.alloc(U * 4 + 4, st);
+    if (U == 0) return;
+    DevBuf kB(U * 8, st), vA(U * 4, st), vB(U * 4, st);
+    iota_i32_kernel<<<grid_for(U), 256, 0, st>>>(vA.as<int32_t>(), U);
+    GD_HIP(hipGetLastError());
+    uint64_t* k = key.as<uint64_t>(); uint64_t* ka = kB.as<uint64_t>();
+    int32_t* v = vA.as<int32_t>(); int32_t* va = vB.as<int32_t>();
+    sort_pairs_u64_i32(ctx, k, ka, v, va, (size_t)U, 0, 64);   // stable: unkeyed ranks keep code order
+    invert_perm_kernel<<<grid_for(U), 256, 0, st>>>(v, U, perm.as<uint32_t>());
+    GD_HIP(hipGetLastError());
+    GD_HIP(hipStreamSynchronize(st));
+}
+
+bool locus_order_enabled() {
+    const char* e = getenv("GDIST_LOCUS_ORDER");
+    return !(e && atoi(e) == 0);
+}
+
+void free_sparse(gdist_sets* s) {
+    s->dbits.release();
+    s->sp_off.release();
+    s->sp_word.release();
+    s->sp_set.release();
+    s->sp_nc.release();
+    s->sparse = false;
+    s->Wd = s->Ws = s->sp_entries = s->sp_U = 0;
+    s->sp_products = s->sp_items = 0.0;
+}
+
+// Modelled seconds of the sparse words over a block: products (each pair's
+// common sparse words) and the (tile, word) visits of every launched tile.
+double sparse_block_cost_s(const gdist_sets* s, double f_area, double tiles) {
+    if (!s->sparse) return 0.0;
+    const double nb = (double)ceil_div(s->nsets, SB);
+    const double all_tiles = nb * (nb + 1) / 2;
+    return f_area * s->sp_products / kSparseProductsPerS + tiles / all_tiles * s->sp_items / kSparseItemsPerS;
+}
+
+void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
+    free_sparse(s);
+    const char* e = getenv("GDIST_SPARSE");
+    if ((e && atoi(e) == 0) || s->W == 0 || s->nsets < 2) return;
+    hipStream_t st = ctx->stream;
+    Trace tr(st);
+    const int64_t N = s->nsets, W = s->W, U = s->dict_size;
+    const int64_t Wv = ceil_div(U, 64);   // words holding dictionary bits
+    if (Wv == 0) return;
+    const unsigned long long* bits = s->bits.as<unsigned long long>();
+    DevBuf dz(W * 4, st);
+    GD_HIP(hipMemsetAsync(dz.p, 0, W * 4, st));
+    const int64_t rpb = 64;
+    dim3 g((unsigned)ceil_div(W, 256), (unsigned)ceil_div(N, rpb));
+    word_z_kernel<<<g, 256, 0, st>>>(bits, N, W, U, rpb, dz.as<int32_t>());
+    GD_HIP(hipGetLastError());
+    std::vector<int32_t> z(W);
+    d2h(z.data(), dz.p, W * 4, st);
+    tr.mark("sparse: word classes");
+    // A word is sparse when its products + visits cost less than its column
+    // of word pairs in the dense tiles (GDIST_SPARSE_ZMAX overrides).
+    const double n = (double)N, pairs = 0.5 * n * (n - 1.0);
+    const double nb = (double)ceil_div(N, SB), tiles = nb * (nb + 1) / 2;
+    const double dense_word_s = pairs / kDenseWordPairsPerS;
+    const char* zm = getenv("GDIST_SPARSE_ZMAX");
+    std::vector<int32_t> sw, dw;
+    double products = 0.0;
+    for (int64_t w = 0; w < Wv; w++) {
+        const double zz = (double)z[w];
+        const bool sparse = zm ? z[w] <= atoi(zm)
+                               : 0.5 * zz * zz / kSparseProductsPerS + tiles / kSparseItemsPerS < dense_word_s;
+        if (sparse) { sw.push_back((int32_t)w); products += 0.5 * zz * zz; }
+        else dw.push_back((int32_t)w);
+    }
+    const int64_t Ws = (int64_t)sw.size(), Wd = (int64_t)dw.size();
+    const int64_t Wdp = Wd ? ceil_div(Wd, 16) * 16 : 0;
+    // whole-triangle estimates: keep the split only if it beats the plain tiles
+    const double t_plain = pairs * (double)W / kDenseWordPairsPerS;
+    const double t_split = pairs * (double)Wdp / kDenseWordPairsPerS + products / kSparseProductsPerS +
+                           tiles * (double)Ws / kSparseItemsPerS;
+    if (Ws == 0 || !(zm || t_split < 0.8 * t_plain)) return;
+    const int64_t nblk = ceil_div(N, SB);
+    GD_REQUIRE((double)nblk * (double)Ws < 2e9, "sparse word index too large");
+    DevBuf dsw(Ws * 4, st), cnt(nblk * Ws * 4 + 4, st);
+    h2d(dsw.p, sw.data(), Ws * 4, st);
+    dim3 gs((unsigned)ceil_div(Ws, 256), (unsigned)nblk);
+    sparse_count_kernel<<<gs, 256, 0, st>>>(bits, N, W, U, dsw.as<int32_t>(), Ws, cnt.as<int32_t>());
+    GD_HIP(hipGetLastError());
+    GD_HIP(hipMemsetAsync(cnt.as<int32_t>() + nblk * Ws, 0, 4, st));
+    s->sp_off.alloc((nblk * Ws + 1) * 8, st);
+    exclusive_scan_i32_to_i64(ctx, cnt.as<int32_t>(), s->sp_off.as<int64_t>(), (size_t)(nblk * Ws + 1));
+    int64_t total = 0;
+    d2h(&total, s->sp_off.as<int64_t>() + nblk * Ws, 8, st);
+    s->sp_word.alloc(total * 8 + 8, st);
+    s->sp_set.alloc(total + 8, st);
+    s->sp_nc.alloc(N * 4, st);
+    GD_HIP(hipMemsetAsync(s->sp_nc.p, 0, N * 4, st));
+    sparse_fill_kernel<<<gs, 256, 0, st>>>(bits, N, W, U, dsw.as<int32_t>(), Ws, s->sp_off.as<int64_t>(),
+                                           s->sp_word.as<unsigned long long>(), s->sp_set.as<uint8_t>(),
+                                           s->sp_nc.as<int32_t>());
+    GD_HIP(hipGetLastError());
+    if (Wdp) {
+        DevBuf ddw(Wd * 4, st);
+        h2d(ddw.p, dw.data(), Wd * 4, st);
+        s->dbits.alloc((size_t)N * Wdp * 8, st);
+        gather_words_kernel<<<grid_for(N * Wdp), 256, 0, st>>>(bits, W, ddw.as<int32_t>(), Wd, Wdp, N,
+                                                               s->dbits.as<unsigned long long>());
+        GD_HIP(hipGetLastError());
+    }
+    int64_t Us = 0;
+    for (int32_t w : sw) Us += (w + 1) * 64 <= U ? 64 : U - (int64_t)w * 64;
+    GD_HIP(hipStreamSynchronize(st));
+    s->sparse = true;
+    s->Ws = Ws;
+    s->Wd = Wdp;
+    s->sp_entries = total;
+    s->sp_U = Us;
+    s->sp_products = products;
+    s->sp_items = tiles * (double)Ws;
+    tr.mark("sparse: entries + dense words");
+}
+
+// Adds the sparse words' share of |A ∩ B| to I over the region (atomics;
+// the caller zeroed I, the dense tiles add theirs).
+// Launched on `st`; `dt` (the caller's) holds the tile list until the launch completes.
+void sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1, bool upper,
+                   int32_t* d_I, int64_t ldI, hipStream_t st, DevBuf& dt) {
+    if (!s->sparse || r1 <= r0 || c1 <= c0) return;
+    std::vector<int2> tiles;
+    for (int64_t A = r0 / SB; A <= (r1 - 1) / SB; A++)
+        for (int64_t B = c0 / SB; B <= (c1 - 1) / SB; B++) {
+            const int64_t rmin = std::max(r0, A * SB);
+            const int64_t cmax = std::min(c1, (B + 1) * SB) - 1;
+            if (upper && cmax <= rmin) continue;
+            tiles.push_back(make_int2((int)A, (int)B));
+        }
+    if (tiles.empty()) return;
+    // enough workgroups to fill the chip, each over >= 512 sparse words
+    const char* cv = getenv("GDIST_SPARSE_WG_PER_CU");
+    const int64_t target = (int64_t)ctx->cus * (cv ? std::max(1, atoi(cv)) : 2);
+    const int nchunks = (int)std::max<int64_t>(
+        1, std::min<int64_t>(ceil_div(s->Ws, 512), ceil_div(target, (int64_t)tiles.size())));
+    dt.alloc(tiles.size() * sizeof(int2), st);
+    h2d(dt.p, tiles.data(), tiles.size() * sizeof(int2), st);
+    const int64_t grid = (int64_t)tiles.size() * nchunks;
+    GD_REQUIRE(grid < (int64_t(1) << 31), "sparse grid too large");
+    sparse_tile_kernel<<<(unsigned)grid, SNT, 0, st>>>(s->sp_off.as<int64_t>(), s->sp_word.as<unsigned long long>(),
+                                                       s->sp_set.as<uint8_t>(), s->sp_nc.as<int32_t>(), s->sp_U,
+                                                       s->Ws, dt.as<int2>(), nchunks, r0, r1, c0, c1, upper ? 1 : 0,
+                                                       d_I, ldI);
+    GD_HIP(hipGetLastError());
+}
+
+}  // namespace gdist

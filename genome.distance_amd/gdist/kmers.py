@@ -283,6 +283,12 @@ class KmerSets(_Handle):
                                             C.byref(rk)))
         return t.value, rk.value
 
+    def sparse_info(self) -> tuple[int, int, int]:
+        """(complement-sparse words, dense words left to the tiles, complement entries)."""
+        a, b, c = C.c_int64(), C.c_int64(), C.c_int64()
+        L.check(L.lib.gdist_sets_sparse_info(self.h, C.byref(a), C.byref(b), C.byref(c)))
+        return a.value, b.value, c.value
+
     def rare_kmers(self) -> int:
         """Rare-tier kmers before identical posting lists were merged."""
         n = C.c_int64()

@@ -155,6 +155,14 @@ int  gdist_sets_rare_kmers(const gdist_sets* sets, int64_t* kmers);
  * m(m-1)/2 over the posting lists) and the longest list. */
 int  gdist_sets_rare_stats(const gdist_sets* sets, int64_t* pair_incs, int64_t* max_list);
 int  gdist_sets_bitset_info(const gdist_sets* sets, int64_t* dict_size, int64_t* words_per_set);
+/* Complement-sparse words of the dense tier: the dense
+ * dictionary is ranked in locus order (the kmer's window in the collection's
+ * first sequences), and each bitset word that few sets lack anything in is
+ * counted from the sets' complement words instead of the AND+popcount tiles.
+ * Reports the sparse words, the dense words left to the tiles (padded) and
+ * the complement entries (0s when the split was not worth building).
+ * GDIST_SPARSE=0 / GDIST_LOCUS_ORDER=0 switch it off (A/B). */
+int  gdist_sets_sparse_info(const gdist_sets* sets, int64_t* sparse_words, int64_t* dense_words, int64_t* entries);
 /* Copy the bitsets (nsets x words_per_set uint64, row-major) to the host. */
 int  gdist_sets_bitset_download(const gdist_sets* sets, uint64_t* bits);
 /* Concatenate two collections (e.g. base genomes + comparison genomes). */

@@ -570,6 +570,45 @@ def test_rare_tier_thresholds_exact(ctx, T, kernel, dedup, monkeypatch):
     assert bits_equal(d, eD[0, cols])
 
 
+@pytest.mark.parametrize("mode", ["auto", "all_sparse", "mixed", "no_locus", "off"])
+def test_sparse_complement_words_exact(ctx, mode, monkeypatch):
+    """The dense tier in locus order with complement-sparse words: counts and
+    distances are bit-exact against the oracle over upper triangles,
+    rectangles, unaligned row blocks (as ranks get them) and row queries,
+    whether every word is sparse, words are split between the sparse kernel
+    and the tiles, the locus order is off (code order), or the split is off."""
+    import gdist
+    env = {"all_sparse": {"GDIST_SPARSE_ZMAX": "100000"}, "mixed": {"GDIST_SPARSE_ZMAX": "12"},
+           "no_locus": {"GDIST_LOCUS_ORDER": "0", "GDIST_SPARSE_ZMAX": "40"}, "off": {"GDIST_SPARSE": "0"}}
+    for k, v in env.get(mode, {}).items():
+        monkeypatch.setenv(k, v)
+    n = 300
+    seqs = synth_sets(n, 20000, 0.003, 105)
+    sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
+    _, W = sets.build_bitsets()
+    ws, wd, ent = sets.sparse_info()
+    if mode == "all_sparse":
+        assert ws > 0 and wd == 0 and ent > 0
+    elif mode == "mixed":
+        assert ws > 0 and wd > 0
+    elif mode == "off":
+        assert ws == 0 and wd == W
+    off, codes = oracle_pack(seqs, 21, 0, 0)
+    for (r0, r1, c0, c1, up) in [(0, n, 0, n, True), (0, n, 0, n, False), (37, 211, 5, 290, False),
+                                 (130, 259, 0, n, True), (299, 300, 0, n, False)]:
+        I, D = sets.matrix((r0, r1), (c0, c1), upper=up, method=gdist.METHOD_BITSET)
+        eI, eD = oracle.matrix(off, codes, r0, r1, c0, c1, flags=0x100 if up else 0)
+        if up:
+            mask = np.fromfunction(lambda a, b: (c0 + b) > (r0 + a), (r1 - r0, c1 - c0))
+            I, D, eI, eD = I[mask], D[mask], eI[mask], eD[mask]
+        assert np.array_equal(I, eI), (mode, r0, r1, c0, c1, up)
+        assert bits_equal(D, eD)
+    cols = [4, 299, 0, 150, 150]
+    d = sets.row_query(150, cols)
+    _, eD = oracle.matrix(off, codes, 150, 151, 0, n)
+    assert bits_equal(d, eD[0, cols])
+
+
 def test_auto_method_prepare(ctx):
     """METHOD_AUTO: small regions stay on the sorted join without building a
     dictionary; a large region of C3-like proteomes (two-tier structure) is
