@@ -135,6 +135,7 @@ def main():
     method = args.method or cfg["method"]
     width_words = 0
     rare = None
+    sparse_words = None
     auto = None
     if world > 1:
         if args.transport == "host":
@@ -167,6 +168,8 @@ def main():
             sets.build_bitsets()
         dict_size, width_words = sets.bitset_info()
         rare = dict(zip(("threshold", "lists", "records"), sets.rare_info()))
+        rare["kmers"] = sets.rare_kmers()
+        sparse_words = dict(zip(("sparse_words", "dense_words", "entries"), sets.sparse_info()))
         mflag = gdist.METHOD_BITSET
     elif method == "sorted":
         sets = local.allgather() if world > 1 else local
@@ -286,7 +289,7 @@ def main():
                        "k": cfg["k"], "pairs_per_step": pairs_all, "parallelism": f"rows{world}",
                        "bitset_words_per_set": width_words or None,
                        "dictionary_size": (dict_size if method == "bitset" else None),
-                       "method": method, "auto": auto, "rare_tier": rare},
+                       "method": method, "auto": auto, "rare_tier": rare, "complement_sparse": sparse_words},
             "roofline": roof,
             "verified": verified,
             "cpu_baseline": cpu,

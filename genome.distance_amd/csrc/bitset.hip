@@ -1434,7 +1434,7 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     // The sparse words and the list-major rare kernel add atomically, like
     // the dense tiles, so they run on the side stream beside them.
     const bool side = overlap || s->sparse;
-    DevBuf sp_tiles;
+    SparseScratch sp_tiles;
     GD_HIP(hipEventRecord(ctx->ev_k0, st));
     if (side) {
         GD_HIP(hipEventRecord(ctx->ev_fork, st));

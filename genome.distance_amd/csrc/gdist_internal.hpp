@@ -326,8 +326,11 @@ void locus_perm(gdist_ctx* ctx, DevBuf& key, int64_t U, DevBuf& perm);
 void build_sparse_words(gdist_ctx* ctx, gdist_sets* s);
 void free_sparse(gdist_sets* s);
 double sparse_block_cost_s(const gdist_sets* s, double f_area, double tiles);
+struct SparseScratch {
+    DevBuf tiles, part;   // tile list, per-chunk counters
+};
 void sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1, bool upper,
-                   int32_t* d_I, int64_t ldI, hipStream_t st, DevBuf& dt);
+                   int32_t* d_I, int64_t ldI, hipStream_t st, SparseScratch& sc);
 
 // sorted.hip
 void build_segments(gdist_ctx* ctx, gdist_sets* s);

@@ -157,21 +157,29 @@ __global__ __launch_bounds__(256) void sparse_fill_kernel(const unsigned long lo
 // the (A, s) and (B, s) entry ranges of word s = base + l, the wave
 // prefix-sums their products r_s x c_s, and the 64 lanes then walk the
 // flattened products (word found by binary search over the prefix in LDS),
-// adding popc(c_i & c_j) to LDS counters. The flush adds the counters - and,
-// from chunk 0, the constant part U_s - nc_i - nc_j - to I with atomics.
+// four per lane at a time so their loads overlap, adding popc(c_i & c_j) to
+// LDS counters. A diagonal tile (A == B) walks each word's pairs x < y of its
+// one entry list (and mirrors them when the region is not an upper triangle).
+// With one chunk per tile the counters go to I directly (atomics: the dense
+// tiles add into I concurrently), with the constant part U_s - nc_i - nc_j;
+// with several, each chunk stores its counters to `part` and
+// sparse_reduce_kernel sums them.
 constexpr int SNT = 512;                 // threads per workgroup
 constexpr int SNW = SNT / 64;
+constexpr int SUN = 4;                   // products per lane in flight
 
 __global__ __launch_bounds__(SNT, 2) void sparse_tile_kernel(
     const int64_t* __restrict__ off, const unsigned long long* __restrict__ word, const uint8_t* __restrict__ set,
     const int32_t* __restrict__ nc, int64_t Us, int64_t Ws, const int2* __restrict__ tiles, int nchunks,
-    int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I, int64_t ldI) {
+    int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I, int64_t ldI,
+    int32_t* __restrict__ part) {
     __shared__ int32_t cnt[SB * SB];                                       // 64 KiB
     __shared__ int32_t pre[SNW][65];
     __shared__ int64_t rbeg[SNW][64], cbeg[SNW][64];
     __shared__ int32_t ncol[SNW][64];
     const int tile = blockIdx.x / nchunks, ch = blockIdx.x % nchunks;
     const int64_t A = tiles[tile].x, B = tiles[tile].y;
+    const bool diag = A == B, mirror = diag && !upper;
     for (int t = threadIdx.x; t < SB * SB; t += SNT) cnt[t] = 0;
     __syncthreads();
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -186,7 +194,7 @@ __global__ __launch_bounds__(SNT, 2) void sparse_tile_kernel(
             rb = offA[s]; nr = (int)(offA[s + 1] - rb);
             cb = offB[s]; ncl = (int)(offB[s + 1] - cb);
         }
-        int p = nr * ncl, incl = p;
+        int incl = diag ? nr * (nr - 1) / 2 : nr * ncl;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const int v = __shfl_up(incl, o, 64);
@@ -199,33 +207,82 @@ __global__ __launch_bounds__(SNT, 2) void sparse_tile_kernel(
         ncol[wv][lane] = ncl;
         const int total = __shfl(incl, 63, 64);
         __builtin_amdgcn_wave_barrier();
-        for (int f = lane; f < total; f += 64) {
-            int lo = 0, hi = 64;                   // pre[lo] <= f < pre[hi]
+        for (int f0 = lane; f0 < total; f0 += 64 * SUN) {
+            int64_t ri[SUN], ci[SUN];
 #pragma unroll
-            for (int step = 0; step < 6; step++) {
-                const int mid = (lo + hi) >> 1;
-                if (pre[wv][mid] <= f) lo = mid; else hi = mid;
+            for (int u = 0; u < SUN; u++) {
+                const int f = f0 + 64 * u < total ? f0 + 64 * u : total - 1;
+                int lo = 0, hi = 64;                   // pre[lo] <= f < pre[hi]
+#pragma unroll
+                for (int step = 0; step < 6; step++) {
+                    const int mid = (lo + hi) >> 1;
+                    if (pre[wv][mid] <= f) lo = mid; else hi = mid;
+                }
+                const int q = f - pre[wv][lo];
+                int x, y;
+                if (diag) {                            // q -> pair (y, x), y < x: q = x(x-1)/2 + y
+                    x = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)q)) * 0.5f);
+                    if (x * (x - 1) / 2 > q) x--;
+                    else if ((x + 1) * x / 2 <= q) x++;
+                    y = q - x * (x - 1) / 2;
+                    ri[u] = rbeg[wv][lo] + y;
+                    ci[u] = rbeg[wv][lo] + x;
+                } else {
+                    const int n2 = ncol[wv][lo];
+                    x = (int)((float)q / (float)n2);
+                    if (x * n2 > q) x--;
+                    else if ((x + 1) * n2 <= q) x++;
+                    y = q - x * n2;
+                    ri[u] = rbeg[wv][lo] + x;
+                    ci[u] = cbeg[wv][lo] + y;
+                }
             }
-            const int q = f - pre[wv][lo];
-            const int n2 = ncol[wv][lo];
-            int x = (int)((float)q / (float)n2);
-            if (x * n2 > q) x--;
-            else if ((x + 1) * n2 <= q) x++;
-            const int y = q - x * n2;
-            const int64_t ri = rbeg[wv][lo] + x, ci = cbeg[wv][lo] + y;
-            const int v = __popcll(word[ri] & word[ci]);
-            if (v) atomicAdd(&cnt[(int)set[ri] * SB + (int)set[ci]], v);
+            unsigned long long wr[SUN], wc[SUN];
+            int sr[SUN], sc[SUN];
+#pragma unroll
+            for (int u = 0; u < SUN; u++) {
+                wr[u] = word[ri[u]]; wc[u] = word[ci[u]];
+                sr[u] = set[ri[u]]; sc[u] = set[ci[u]];
+            }
+#pragma unroll
+            for (int u = 0; u < SUN; u++) {
+                const int v = __popcll(wr[u] & wc[u]);
+                if (v && f0 + 64 * u < total) {
+                    atomicAdd(&cnt[sr[u] * SB + sc[u]], v);
+                    if (mirror) atomicAdd(&cnt[sc[u] * SB + sr[u]], v);
+                }
+            }
         }
         __builtin_amdgcn_wave_barrier();
     }
     __syncthreads();
+    if (part) {
+        int32_t* dst = part + ((int64_t)tile * nchunks + ch) * (SB * SB);
+        for (int t = threadIdx.x; t < SB * SB; t += SNT) dst[t] = cnt[t];
+        return;
+    }
     for (int t = threadIdx.x; t < SB * SB; t += SNT) {
         const int64_t i = A * SB + (t >> 7), j = B * SB + (t & (SB - 1));
         if (i < r0 || i >= r1 || j < c0 || j >= c1 || (upper && j <= i)) continue;
-        int v = cnt[t];
-        if (ch == 0) v += (int)Us - nc[i] - nc[j];
+        const int v = cnt[t] + (int)Us - nc[i] - nc[j];
         if (v) atomicAdd(I + (i - r0) * ldI + (j - c0), v);
     }
+}
+
+// the chunks' counters of each tile + the constant part, into I
+__global__ __launch_bounds__(256) void sparse_reduce_kernel(const int32_t* __restrict__ part, int nchunks,
+                                                            const int2* __restrict__ tiles,
+                                                            const int32_t* __restrict__ nc, int64_t Us, int64_t r0,
+                                                            int64_t r1, int64_t c0, int64_t c1, int upper,
+                                                            int32_t* __restrict__ I, int64_t ldI) {
+    const int tile = blockIdx.x / (SB * SB / 256);
+    const int t = (blockIdx.x % (SB * SB / 256)) * 256 + threadIdx.x;
+    const int64_t i = (int64_t)tiles[tile].x * SB + (t >> 7), j = (int64_t)tiles[tile].y * SB + (t & (SB - 1));
+    if (i < r0 || i >= r1 || j < c0 || j >= c1 || (upper && j <= i)) return;
+    int v = (int)Us - nc[i] - nc[j];
+    const int32_t* p = part + (int64_t)tile * nchunks * (SB * SB) + t;
+    for (int c = 0; c < nchunks; c++) v += p[(int64_t)c * (SB * SB)];
+    if (v) atomicAdd(I + (i - r0) * ldI + (j - c0), v);
 }
 
 }  // namespace
@@ -376,10 +433,10 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
 }
 
 // Adds the sparse words' share of |A ∩ B| to I over the region (atomics;
-// the caller zeroed I, the dense tiles add theirs).
-// Launched on `st`; `dt` (the caller's) holds the tile list until the launch completes.
+// the caller zeroed I, the dense tiles add theirs). Launched on `st`; the
+// caller's `sc` holds the tile list and chunk partials until it completes.
 void sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1, bool upper,
-                   int32_t* d_I, int64_t ldI, hipStream_t st, DevBuf& dt) {
+                   int32_t* d_I, int64_t ldI, hipStream_t st, SparseScratch& sc) {
     if (!s->sparse || r1 <= r0 || c1 <= c0) return;
     std::vector<int2> tiles;
     for (int64_t A = r0 / SB; A <= (r1 - 1) / SB; A++)
@@ -392,18 +449,27 @@ void sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     if (tiles.empty()) return;
     // enough workgroups to fill the chip, each over >= 512 sparse words
     const char* cv = getenv("GDIST_SPARSE_WG_PER_CU");
-    const int64_t target = (int64_t)ctx->cus * (cv ? std::max(1, atoi(cv)) : 2);
+    const int64_t target = (int64_t)ctx->cus * (cv ? std::max(1, atoi(cv)) : 4);
     const int nchunks = (int)std::max<int64_t>(
         1, std::min<int64_t>(ceil_div(s->Ws, 512), ceil_div(target, (int64_t)tiles.size())));
-    dt.alloc(tiles.size() * sizeof(int2), st);
-    h2d(dt.p, tiles.data(), tiles.size() * sizeof(int2), st);
-    const int64_t grid = (int64_t)tiles.size() * nchunks;
+    const int64_t nt = (int64_t)tiles.size();
+    sc.tiles.alloc(nt * sizeof(int2), st);
+    h2d(sc.tiles.p, tiles.data(), nt * sizeof(int2), st);
+    if (nchunks > 1) sc.part.alloc((size_t)nt * nchunks * SB * SB * 4, st);
+    const int64_t grid = nt * nchunks;
     GD_REQUIRE(grid < (int64_t(1) << 31), "sparse grid too large");
     sparse_tile_kernel<<<(unsigned)grid, SNT, 0, st>>>(s->sp_off.as<int64_t>(), s->sp_word.as<unsigned long long>(),
                                                        s->sp_set.as<uint8_t>(), s->sp_nc.as<int32_t>(), s->sp_U,
-                                                       s->Ws, dt.as<int2>(), nchunks, r0, r1, c0, c1, upper ? 1 : 0,
-                                                       d_I, ldI);
+                                                       s->Ws, sc.tiles.as<int2>(), nchunks, r0, r1, c0, c1,
+                                                       upper ? 1 : 0, d_I, ldI,
+                                                       nchunks > 1 ? sc.part.as<int32_t>() : nullptr);
     GD_HIP(hipGetLastError());
+    if (nchunks > 1) {
+        sparse_reduce_kernel<<<(unsigned)(nt * (SB * SB / 256)), 256, 0, st>>>(
+            sc.part.as<int32_t>(), nchunks, sc.tiles.as<int2>(), s->sp_nc.as<int32_t>(), s->sp_U, r0, r1, c0, c1,
+            upper ? 1 : 0, d_I, ldI);
+        GD_HIP(hipGetLastError());
+    }
 }
 
 }  // namespace gdist
