@@ -164,7 +164,7 @@ __global__ __launch_bounds__(256) void sparse_fill_kernel(const unsigned long lo
 // tiles add into I concurrently), with the constant part U_s - nc_i - nc_j;
 // with several, each chunk stores its counters to `part` and
 // sparse_reduce_kernel sums them.
-constexpr int SNT = 512;                 // threads per workgroup
+constexpr int SNT = 1024;                // threads per workgroup (2 per CU: 8 waves per SIMD)
 constexpr int SNW = SNT / 64;
 constexpr int SUN = 4;                   // products per lane in flight
 
@@ -175,8 +175,8 @@ __global__ __launch_bounds__(SNT, 2) void sparse_tile_kernel(
     int32_t* __restrict__ part) {
     __shared__ int32_t cnt[SB * SB];                                       // 64 KiB
     __shared__ int32_t pre[SNW][65];
-    __shared__ int64_t rbeg[SNW][64], cbeg[SNW][64];
-    __shared__ int32_t ncol[SNW][64];
+    __shared__ int32_t rbeg[SNW][64], cbeg[SNW][64];   // relative to the chunk's first entries
+    __shared__ uint8_t ncol[SNW][64];
     const int tile = blockIdx.x / nchunks, ch = blockIdx.x % nchunks;
     const int64_t A = tiles[tile].x, B = tiles[tile].y;
     const bool diag = A == B, mirror = diag && !upper;
@@ -186,6 +186,7 @@ __global__ __launch_bounds__(SNT, 2) void sparse_tile_kernel(
     const int64_t sb = Ws * ch / nchunks, se = Ws * (ch + 1) / nchunks;
     const int64_t* offA = off + A * Ws;
     const int64_t* offB = off + B * Ws;
+    const int64_t ra0 = offA[sb], cb0 = offB[sb];           // chunk bases (< 2^31 entries per chunk)
     for (int64_t base = sb + (int64_t)wv * 64; base < se; base += (int64_t)SNW * 64) {
         const int64_t s = base + lane;
         int64_t rb = 0, cb = 0;
@@ -202,9 +203,9 @@ __global__ __launch_bounds__(SNT, 2) void sparse_tile_kernel(
         }
         pre[wv][lane + 1] = incl;
         if (lane == 0) pre[wv][0] = 0;
-        rbeg[wv][lane] = rb;
-        cbeg[wv][lane] = cb;
-        ncol[wv][lane] = ncl;
+        rbeg[wv][lane] = (int32_t)(rb - ra0);
+        cbeg[wv][lane] = (int32_t)(cb - cb0);
+        ncol[wv][lane] = (uint8_t)ncl;
         const int total = __shfl(incl, 63, 64);
         __builtin_amdgcn_wave_barrier();
         for (int f0 = lane; f0 < total; f0 += 64 * SUN) {
@@ -225,16 +226,16 @@ __global__ __launch_bounds__(SNT, 2) void sparse_tile_kernel(
                     if (x * (x - 1) / 2 > q) x--;
                     else if ((x + 1) * x / 2 <= q) x++;
                     y = q - x * (x - 1) / 2;
-                    ri[u] = rbeg[wv][lo] + y;
-                    ci[u] = rbeg[wv][lo] + x;
+                    ri[u] = ra0 + rbeg[wv][lo] + y;
+                    ci[u] = ra0 + rbeg[wv][lo] + x;
                 } else {
                     const int n2 = ncol[wv][lo];
                     x = (int)((float)q / (float)n2);
                     if (x * n2 > q) x--;
                     else if ((x + 1) * n2 <= q) x++;
                     y = q - x * n2;
-                    ri[u] = rbeg[wv][lo] + x;
-                    ci[u] = cbeg[wv][lo] + y;
+                    ri[u] = ra0 + rbeg[wv][lo] + x;
+                    ci[u] = cb0 + cbeg[wv][lo] + y;
                 }
             }
             unsigned long long wr[SUN], wc[SUN];
