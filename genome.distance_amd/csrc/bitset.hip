@@ -1373,6 +1373,7 @@ double sorted_cost_s(const gdist_sets* s, double pairs) {
 }
 
 void free_bitsets(gdist_sets* s) {
+    s->plans.clear();
     free_sparse(s);
     s->bits.release();
     s->post_off.release();
@@ -1391,31 +1392,80 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     hipStream_t st = ctx->stream;
     const int64_t nr = r1 - r0, nc = c1 - c0;
     if (nr <= 0 || nc <= 0) return;
-    const int tr = (int)ceil_div(nr, BT), tc = (int)ceil_div(nc, BT);
-    std::vector<int2> tiles;
-    for (int a = 0; a < tr; a++)
-        for (int b = 0; b < tc; b++) {
-            // skip tiles holding no pair with j > i
-            const int64_t rmin = r0 + (int64_t)a * BT;
-            const int64_t cmax = std::min<int64_t>(c1, c0 + (int64_t)(b + 1) * BT) - 1;
-            if (upper && cmax <= rmin) continue;
-            tiles.push_back(make_int2(a, b));
-        }
-    if (tiles.empty()) return;
+    const int tr = (int)ceil_div(nr, BT);
     // dense tile operands: every word, or only the dense words when the
     // complement-sparse words run in their own kernel (sparse.hip)
     const unsigned long long* tbits = s->sparse ? s->dbits.as<unsigned long long>() : s->bits.as<unsigned long long>();
     const int64_t tW = s->sparse ? s->Wd : s->W;
-    const int64_t nchunks = tW / KC;
-    // split the word dimension so the launch holds ≳ 8 workgroups per CU
-    const int64_t target = (int64_t)ctx->cus * 8;
-    int splits = (int)std::max<int64_t>(1, std::min<int64_t>(nchunks, ceil_div(target, (int64_t)tiles.size())));
-    DevBuf dt(tiles.size() * sizeof(int2), st);
-    h2d(dt.p, tiles.data(), tiles.size() * sizeof(int2), st);
-    const int64_t grid = (int64_t)tiles.size() * splits;
-    GD_REQUIRE(grid < (int64_t(1) << 31), "bitset matrix grid too large");
     const char* ev = getenv("GDIST_BITSET_KERNEL");   // A/B selection (default: 3)
     const int variant = ev ? atoi(ev) : 3;
+    // Diagonal tiles of an upper-triangle region (row0 == col0) get their
+    // own launch of the DIAG variant, which skips the accumulators that
+    // only hold pairs with j <= i (GDIST_BITSET_DIAG=0 keeps one launch).
+    const char* dv = getenv("GDIST_BITSET_DIAG");
+    const bool split_diag = variant != 1 && upper && !(dv && atoi(dv) == 0);
+    // The last row tile of a block whose rows are not a multiple of BT
+    // holds nlast rows: its tiles get launches instantiated for
+    // RR = ceil(nlast / 16) accumulator rows, skipping the others' work.
+    // (GDIST_BITSET_PARTIAL_RR: the largest RR given its own launches, A/B)
+    const char* pv = getenv("GDIST_BITSET_PARTIAL_RR");
+    const int max_rr = pv ? atoi(pv) : kPartialMaxRR;
+
+    // ---- the region's launch plan (built once, then reused)
+    const std::vector<int64_t> key{r0, r1, c0, c1, upper ? 1 : 0, variant, split_diag ? 1 : 0, max_rr, tW};
+    auto it = s->plans.find(key);
+    if (it == s->plans.end()) {
+        if (s->plans.size() >= 8) s->plans.clear();   // row-block loops: keep the cache small
+        auto plan = std::make_unique<MatrixPlan>();
+        MatrixPlan& p = *plan;
+        if (variant == 1) {
+            const int tc = (int)ceil_div(nc, BT);
+            std::vector<int2> tiles;
+            for (int a = 0; a < tr; a++)
+                for (int b = 0; b < tc; b++) {
+                    // skip tiles holding no pair with j > i
+                    const int64_t rmin = r0 + (int64_t)a * BT;
+                    const int64_t cmax = std::min<int64_t>(c1, c0 + (int64_t)(b + 1) * BT) - 1;
+                    if (upper && cmax <= rmin) continue;
+                    tiles.push_back(make_int2(a, b));
+                }
+            p.ntiles = tiles.size();
+            // split the word dimension so the launch holds ≳ 8 workgroups per CU
+            const int64_t target = (int64_t)ctx->cus * 8;
+            p.splits = (int)std::max<int64_t>(
+                1, std::min<int64_t>(tW / KC, tiles.empty() ? 1 : ceil_div(target, (int64_t)tiles.size())));
+            p.tiles.alloc(tiles.size() * sizeof(int2) + 8, st);
+            if (!tiles.empty()) h2d(p.tiles.p, tiles.data(), tiles.size() * sizeof(int2), st);
+        } else {
+            // Upper-triangle regions tile their columns from an origin corg <= c0
+            // with corg = r0 (mod BT), so tiles lie exactly on the diagonal whatever
+            // r0 is (row-sharded ranks get exact equal-area row blocks); columns
+            // below c0 are loaded clamped and discarded. Diagonal tiles: col0 == row0.
+            p.corg = split_diag ? c0 - (((c0 - r0) % BT) + BT) % BT : c0;
+            const int64_t dlt_t = (r0 - p.corg) / BT;
+            const int64_t nlast = nr - (int64_t)(tr - 1) * BT;
+            p.rr = (int)ceil_div(nlast, 16);
+            p.part = p.rr <= max_rr;
+            std::vector<int2> grp[4];   // off-diagonal, diagonal, partial off-diagonal, partial diagonal
+            const int tc2 = (int)ceil_div(c1 - p.corg, BT);
+            for (int a = 0; a < tr; a++)
+                for (int b = 0; b < tc2; b++) {
+                    const int64_t rmin = r0 + (int64_t)a * BT;
+                    const int64_t cmax = std::min<int64_t>(c1, p.corg + (int64_t)(b + 1) * BT) - 1;
+                    if (cmax < c0 || (upper && cmax <= rmin)) continue;
+                    const int g = ((split_diag && (int64_t)b - a == dlt_t) ? 1 : 0) + ((p.part && a == tr - 1) ? 2 : 0);
+                    grp[g].push_back(make_int2(a, b));
+                }
+            for (int g = 0; g < 4; g++) p.at[g + 1] = p.at[g] + grp[g].size();
+            p.tiles.alloc(p.at[4] * sizeof(int2) + 8, st);
+            for (int g = 0; g < 4; g++)
+                if (!grp[g].empty()) h2d(p.tiles.as<int2>() + p.at[g], grp[g].data(), grp[g].size() * sizeof(int2), st);
+        }
+        it = s->plans.emplace(key, std::move(plan)).first;
+    }
+    MatrixPlan& p = *it->second;
+    if (variant == 1 ? p.ntiles == 0 : p.at[4] == 0) return;   // no pair in the region
+
     // Rare kernel per call from the cost model (rare_choice): list-major opens
     // every list and walks the pairs from this block's rows with global
     // atomics (short lists, blocks with few pairs per row: C2, the last rank
@@ -1434,12 +1484,11 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     // The sparse words and the list-major rare kernel add atomically, like
     // the dense tiles, so they run on the side stream beside them.
     const bool side = overlap || s->sparse;
-    SparseScratch sp_tiles;
     GD_HIP(hipEventRecord(ctx->ev_k0, st));
     if (side) {
         GD_HIP(hipEventRecord(ctx->ev_fork, st));
         GD_HIP(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
-        if (s->sparse) sparse_matrix(ctx, s, r0, r1, c0, c1, upper, d_I, ldI, ctx->side, sp_tiles);
+        if (s->sparse) sparse_matrix(ctx, s, r0, r1, c0, c1, upper, d_I, ldI, ctx->side, p.sparse);
         if (overlap)
             rare_pairs_kernel<<<grid_for(s->n_rare, 256, 256 * 64), 256, 0, ctx->side>>>(
                 s->post_off.as<int64_t>(), s->post_sets.as<uint32_t>(), s->post_w.as<uint32_t>(), s->n_rare, r0, r1,
@@ -1450,44 +1499,12 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     if (tW == 0) {
         // no dense words: the sparse kernel holds the whole dense tier
     } else if (variant == 1) {
-        bitset_tile_kernel<<<(unsigned)grid, NT, 0, st>>>(tbits, tW, dt.as<int2>(),
-                                                           splits, nchunks, r0, r1, c0, c1, upper ? 1 : 0, d_I, ldI);
+        const int64_t grid = (int64_t)p.ntiles * p.splits;
+        GD_REQUIRE(grid < (int64_t(1) << 31), "bitset matrix grid too large");
+        bitset_tile_kernel<<<(unsigned)grid, NT, 0, st>>>(tbits, tW, p.tiles.as<int2>(), p.splits, tW / KC, r0, r1, c0,
+                                                           c1, upper ? 1 : 0, d_I, ldI);
     } else {
         const int64_t nch2 = tW / KC2;
-        // Diagonal tiles of an upper-triangle region (row0 == col0) get their
-        // own launch of the DIAG variant, which skips the accumulators that
-        // only hold pairs with j <= i (GDIST_BITSET_DIAG=0 keeps one launch).
-        const char* dv = getenv("GDIST_BITSET_DIAG");
-        // Upper-triangle regions tile their columns from an origin corg <= c0
-        // with corg = r0 (mod BT), so tiles lie exactly on the diagonal whatever
-        // r0 is (row-sharded ranks get exact equal-area row blocks); columns
-        // below c0 are loaded clamped and discarded. Diagonal tiles: col0 == row0.
-        const bool split_diag = upper && !(dv && atoi(dv) == 0);
-        const int64_t corg = split_diag ? c0 - (((c0 - r0) % BT) + BT) % BT : c0;
-        const int64_t dlt_t = (r0 - corg) / BT;
-        // The last row tile of a block whose rows are not a multiple of BT
-        // holds nlast rows: its tiles get launches instantiated for
-        // RR = ceil(nlast / 16) accumulator rows, skipping the others' work.
-        // (GDIST_BITSET_PARTIAL_RR: the largest RR given its own launches, A/B)
-        const int64_t nlast = nr - (int64_t)(tr - 1) * BT;
-        const int rr = (int)ceil_div(nlast, 16);
-        const char* pv = getenv("GDIST_BITSET_PARTIAL_RR");
-        const bool part = rr <= (pv ? atoi(pv) : kPartialMaxRR);
-        std::vector<int2> grp[4];   // off-diagonal, diagonal, partial off-diagonal, partial diagonal
-        const int tc2 = (int)ceil_div(c1 - corg, BT);
-        for (int a = 0; a < tr; a++)
-            for (int b = 0; b < tc2; b++) {
-                const int64_t rmin = r0 + (int64_t)a * BT;
-                const int64_t cmax = std::min<int64_t>(c1, corg + (int64_t)(b + 1) * BT) - 1;
-                if (cmax < c0 || (upper && cmax <= rmin)) continue;
-                const int g = ((split_diag && (int64_t)b - a == dlt_t) ? 1 : 0) + ((part && a == tr - 1) ? 2 : 0);
-                grp[g].push_back(make_int2(a, b));
-            }
-        size_t at[5] = {0, 0, 0, 0, 0};
-        for (int g = 0; g < 4; g++) at[g + 1] = at[g] + grp[g].size();
-        DevBuf dt2(at[4] * sizeof(int2) + 8, st);
-        for (int g = 0; g < 4; g++)
-            if (!grp[g].empty()) h2d(dt2.as<int2>() + at[g], grp[g].data(), grp[g].size() * sizeof(int2), st);
         // workgroups per CU the K-split aims for (GDIST_BITSET_WG_PER_CU, A/B)
         const char* wv = getenv("GDIST_BITSET_WG_PER_CU");
         const int64_t wg_per_cu = wv ? std::max(1, atoi(wv)) : 16;
@@ -1496,6 +1513,7 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
         // (launches of few tiles: diagonal, partial; GDIST_BITSET_MIN_CHUNKS, A/B)
         const char* mv = getenv("GDIST_BITSET_MIN_CHUNKS");
         const int64_t min_kc = mv ? std::max(1, atoi(mv)) : 16;
+        const int64_t corg = p.corg;
         auto launch = [&](auto kern, const int2* dtiles, size_t nt) {
             if (nt == 0) return;
             const int64_t target2 = (int64_t)ctx->cus * wg_per_cu;
@@ -1506,7 +1524,8 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
             kern<<<(unsigned)grid2, NT, 0, st>>>(tbits, tW, dtiles, (int)nt, sp2, nch2,
                                                  r0, r1, c0, c1, corg, upper ? 1 : 0, d_I, ldI);
         };
-        const int2* dg = dt2.as<int2>();
+        const int2* dg = p.tiles.as<int2>();
+        const size_t* at = p.at;
         if (variant == 2) {   // A/B: ORDER 0, full-height tiles throughout
             launch(bitset_tile_kernel2<0, false>, dg, at[1]);
             launch(bitset_tile_kernel2<0, true>, dg + at[1], at[2] - at[1]);
@@ -1519,7 +1538,7 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
                 launch(off_k, dg + at[2], at[3] - at[2]);
                 launch(diag_k, dg + at[3], at[4] - at[3]);
             };
-            switch (part ? rr : 8) {
+            switch (p.part ? p.rr : 8) {
                 case 1: partial(bitset_tile_kernel2<1, false, 1>, bitset_tile_kernel2<1, true, 1>); break;
                 case 2: partial(bitset_tile_kernel2<1, false, 2>, bitset_tile_kernel2<1, true, 2>); break;
                 case 3: partial(bitset_tile_kernel2<1, false, 3>, bitset_tile_kernel2<1, true, 3>); break;

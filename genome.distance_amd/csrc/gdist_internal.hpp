@@ -9,6 +9,7 @@
 
 #include <cstdint>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -117,6 +118,27 @@ inline void d2h(void* dst, const void* src, size_t bytes, hipStream_t s) {
     GD_HIP(hipStreamSynchronize(s));
 }
 
+// Launch plan of one bitset_matrix region, cached on the collection: the
+// tile lists live on the device and the sparse chunk partials stay
+// allocated, so repeated calls over one region (the bench steps, row-block
+// loops) upload nothing and never wait on the host before their launches.
+struct SparseScratch {
+    bool ready = false;
+    DevBuf tiles, part;   // tile list, per-chunk counters
+    int nchunks = 0;
+    int64_t ntiles = 0;
+};
+struct MatrixPlan {
+    DevBuf tiles;                    // v1: the tile list; v2/v3: the four launch groups
+    size_t at[5] = {0, 0, 0, 0, 0};  // group bounds (v2/v3)
+    size_t ntiles = 0;               // v1
+    int splits = 1;                  // v1 K-split
+    int64_t corg = 0;
+    int rr = 8;
+    bool part = false;
+    SparseScratch sparse;
+};
+
 // ---------------------------------------------------------------------------
 struct Timing {
     double kernel_ms = 0.0, call_ms = 0.0;
@@ -219,6 +241,8 @@ struct gdist_sets {
     int64_t sp_entries = 0, sp_U = 0;     // entries; valid bits of the sparse words
     double sp_products = 0, sp_items = 0; // whole-triangle products / (tile, word) visits (cost model)
     bool auto_sorted = false;             // METHOD_AUTO measured the sorted join cheaper
+    // bitset_matrix launch plans by (region, kernel switches); cleared with the bitsets
+    mutable std::map<std::vector<int64_t>, std::unique_ptr<gdist::MatrixPlan>> plans;
 };
 
 namespace gdist {
@@ -326,9 +350,6 @@ void locus_perm(gdist_ctx* ctx, DevBuf& key, int64_t U, DevBuf& perm);
 void build_sparse_words(gdist_ctx* ctx, gdist_sets* s);
 void free_sparse(gdist_sets* s);
 double sparse_block_cost_s(const gdist_sets* s, double f_area, double tiles);
-struct SparseScratch {
-    DevBuf tiles, part;   // tile list, per-chunk counters
-};
 void sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1, bool upper,
                    int32_t* d_I, int64_t ldI, hipStream_t st, SparseScratch& sc);
 

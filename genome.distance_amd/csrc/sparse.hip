@@ -332,6 +332,7 @@ bool locus_order_enabled() {
 }
 
 void free_sparse(gdist_sets* s) {
+    s->plans.clear();
     s->dbits.release();
     s->sp_off.release();
     s->sp_word.release();
@@ -434,36 +435,42 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
 }
 
 // Adds the sparse words' share of |A ∩ B| to I over the region (atomics;
-// the caller zeroed I, the dense tiles add theirs). Launched on `st`; the
-// caller's `sc` holds the tile list and chunk partials until it completes.
+// the caller zeroed I, the dense tiles add theirs). Launched on `st`; `sc`
+// (the region's cached plan) holds the tile list and the chunk partials.
 void sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1, bool upper,
                    int32_t* d_I, int64_t ldI, hipStream_t st, SparseScratch& sc) {
     if (!s->sparse || r1 <= r0 || c1 <= c0) return;
-    std::vector<int2> tiles;
-    for (int64_t A = r0 / SB; A <= (r1 - 1) / SB; A++)
-        for (int64_t B = c0 / SB; B <= (c1 - 1) / SB; B++) {
-            const int64_t rmin = std::max(r0, A * SB);
-            const int64_t cmax = std::min(c1, (B + 1) * SB) - 1;
-            if (upper && cmax <= rmin) continue;
-            tiles.push_back(make_int2((int)A, (int)B));
+    if (!sc.ready) {
+        std::vector<int2> tiles;
+        for (int64_t A = r0 / SB; A <= (r1 - 1) / SB; A++)
+            for (int64_t B = c0 / SB; B <= (c1 - 1) / SB; B++) {
+                const int64_t rmin = std::max(r0, A * SB);
+                const int64_t cmax = std::min(c1, (B + 1) * SB) - 1;
+                if (upper && cmax <= rmin) continue;
+                tiles.push_back(make_int2((int)A, (int)B));
+            }
+        sc.ntiles = (int64_t)tiles.size();
+        // enough workgroups to fill the chip, each over >= 512 sparse words
+        const char* cv = getenv("GDIST_SPARSE_WG_PER_CU");
+        const int64_t target = (int64_t)ctx->cus * (cv ? std::max(1, atoi(cv)) : 4);
+        sc.nchunks = sc.ntiles ? (int)std::max<int64_t>(
+                                     1, std::min<int64_t>(ceil_div(s->Ws, 512), ceil_div(target, sc.ntiles)))
+                               : 0;
+        if (sc.ntiles) {
+            sc.tiles.alloc(sc.ntiles * sizeof(int2), st);
+            h2d(sc.tiles.p, tiles.data(), sc.ntiles * sizeof(int2), st);
         }
-    if (tiles.empty()) return;
-    // enough workgroups to fill the chip, each over >= 512 sparse words
-    const char* cv = getenv("GDIST_SPARSE_WG_PER_CU");
-    const int64_t target = (int64_t)ctx->cus * (cv ? std::max(1, atoi(cv)) : 4);
-    const int nchunks = (int)std::max<int64_t>(
-        1, std::min<int64_t>(ceil_div(s->Ws, 512), ceil_div(target, (int64_t)tiles.size())));
-    const int64_t nt = (int64_t)tiles.size();
-    sc.tiles.alloc(nt * sizeof(int2), st);
-    h2d(sc.tiles.p, tiles.data(), nt * sizeof(int2), st);
-    if (nchunks > 1) sc.part.alloc((size_t)nt * nchunks * SB * SB * 4, st);
-    const int64_t grid = nt * nchunks;
-    GD_REQUIRE(grid < (int64_t(1) << 31), "sparse grid too large");
-    sparse_tile_kernel<<<(unsigned)grid, SNT, 0, st>>>(s->sp_off.as<int64_t>(), s->sp_word.as<unsigned long long>(),
-                                                       s->sp_set.as<uint8_t>(), s->sp_nc.as<int32_t>(), s->sp_U,
-                                                       s->Ws, sc.tiles.as<int2>(), nchunks, r0, r1, c0, c1,
-                                                       upper ? 1 : 0, d_I, ldI,
-                                                       nchunks > 1 ? sc.part.as<int32_t>() : nullptr);
+        if (sc.nchunks > 1) sc.part.alloc((size_t)sc.ntiles * sc.nchunks * SB * SB * 4, st);
+        GD_REQUIRE(sc.ntiles * sc.nchunks < (int64_t(1) << 31), "sparse grid too large");
+        sc.ready = true;
+    }
+    if (sc.ntiles == 0) return;
+    const int nchunks = sc.nchunks;
+    const int64_t nt = sc.ntiles;
+    sparse_tile_kernel<<<(unsigned)(nt * nchunks), SNT, 0, st>>>(
+        s->sp_off.as<int64_t>(), s->sp_word.as<unsigned long long>(), s->sp_set.as<uint8_t>(), s->sp_nc.as<int32_t>(),
+        s->sp_U, s->Ws, sc.tiles.as<int2>(), nchunks, r0, r1, c0, c1, upper ? 1 : 0, d_I, ldI,
+        nchunks > 1 ? sc.part.as<int32_t>() : nullptr);
     GD_HIP(hipGetLastError());
     if (nchunks > 1) {
         sparse_reduce_kernel<<<(unsigned)(nt * (SB * SB / 256)), 256, 0, st>>>(
