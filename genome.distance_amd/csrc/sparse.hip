@@ -168,18 +168,29 @@ constexpr int SNT = 1024;                // threads per workgroup (2 per CU: 8 w
 constexpr int SNW = SNT / 64;
 constexpr int SUN = 4;                   // products per lane in flight
 
+// LDS counter of local pair (row a, column b): the column is rotated by the
+// row, so the products of one word (its rows x its columns, column fastest
+// across lanes) land on distinct banks instead of one bank per column
+__device__ __forceinline__ int cnt_index(int a, int b) { return a * SB + ((b + a) & (SB - 1)); }
+
 __global__ __launch_bounds__(SNT, 2) void sparse_tile_kernel(
     const int64_t* __restrict__ off, const unsigned long long* __restrict__ word, const uint8_t* __restrict__ set,
     const int32_t* __restrict__ nc, int64_t Us, int64_t Ws, const int2* __restrict__ tiles, int nchunks,
     int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I, int64_t ldI,
     int32_t* __restrict__ part) {
     __shared__ int32_t cnt[SB * SB];                                       // 64 KiB
-    __shared__ int32_t pre[SNW][65];
+    __shared__ int32_t pre[SNW][64];                    // first product of each word of the batch
     __shared__ int32_t rbeg[SNW][64], cbeg[SNW][64];   // relative to the chunk's first entries
     __shared__ uint8_t ncol[SNW][64];
     const int tile = blockIdx.x / nchunks, ch = blockIdx.x % nchunks;
     const int64_t A = tiles[tile].x, B = tiles[tile].y;
-    const bool diag = A == B, mirror = diag && !upper;
+    // rows of block A inside the region: a tile on a row-block edge (a rank's
+    // first or last rows) walks only those entries of each word's row list
+    const int rlo = (int)(r0 - A * SB > 0 ? r0 - A * SB : 0);
+    const int rhi = (int)(r1 - A * SB < SB ? r1 - A * SB : SB);
+    const bool rpart = rlo > 0 || rhi < SB;
+    // a whole diagonal tile walks each word's pairs x < y of its one list
+    const bool diag = A == B && !rpart, mirror = diag && !upper;
     for (int t = threadIdx.x; t < SB * SB; t += SNT) cnt[t] = 0;
     __syncthreads();
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -189,54 +200,71 @@ __global__ __launch_bounds__(SNT, 2) void sparse_tile_kernel(
     const int64_t ra0 = offA[sb], cb0 = offB[sb];           // chunk bases (< 2^31 entries per chunk)
     for (int64_t base = sb + (int64_t)wv * 64; base < se; base += (int64_t)SNW * 64) {
         const int64_t s = base + lane;
-        int64_t rb = 0, cb = 0;
+        int64_t rb = ra0, cb = cb0;
         int nr = 0, ncl = 0;
         if (s < se) {
             rb = offA[s]; nr = (int)(offA[s + 1] - rb);
             cb = offB[s]; ncl = (int)(offB[s + 1] - cb);
+            if (rpart) {                               // lists are sorted by set: trim both ends
+                int a = 0, e = nr;
+                for (int t = 0; t < nr; t++) {
+                    const int st = set[rb + t];
+                    a += st < rlo;
+                    e -= st >= rhi;
+                }
+                rb += a;
+                nr = e > a ? e - a : 0;
+            }
         }
-        int incl = diag ? nr * (nr - 1) / 2 : nr * ncl;
+        const int P = diag ? nr * (nr - 1) / 2 : nr * ncl;
+        int incl = P;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const int v = __shfl_up(incl, o, 64);
             if (lane >= o) incl += v;
         }
-        pre[wv][lane + 1] = incl;
-        if (lane == 0) pre[wv][0] = 0;
+        pre[wv][lane] = incl - P;
         rbeg[wv][lane] = (int32_t)(rb - ra0);
         cbeg[wv][lane] = (int32_t)(cb - cb0);
         ncol[wv][lane] = (uint8_t)ncl;
         const int total = __shfl(incl, 63, 64);
         __builtin_amdgcn_wave_barrier();
-        for (int f0 = lane; f0 < total; f0 += 64 * SUN) {
+        for (int fb = 0; fb < total; fb += 64 * SUN) {
             int64_t ri[SUN], ci[SUN];
+            bool ok[SUN];
 #pragma unroll
             for (int u = 0; u < SUN; u++) {
-                const int f = f0 + 64 * u < total ? f0 + 64 * u : total - 1;
-                int lo = 0, hi = 64;                   // pre[lo] <= f < pre[hi]
-#pragma unroll
-                for (int step = 0; step < 6; step++) {
-                    const int mid = (lo + hi) >> 1;
-                    if (pre[wv][mid] <= f) lo = mid; else hi = mid;
-                }
+                const int F = fb + 64 * u, f = F + lane;
+                ok[u] = f < total;
+                // the word holding product f: #{l : incl_l <= f}; incl ascends
+                // with l, so the words ending before F are a ballot prefix and
+                // the few ending inside [F, F + 63] are read from their lanes
+                const int w0 = __popcll(__ballot(incl <= F));
+                const int w1 = __popcll(__ballot(incl <= F + 63));
+                int lo = w0;
+                for (int l = w0; l < w1; l++) lo += __builtin_amdgcn_readlane(incl, l) <= f;
+                lo = lo < 63 ? lo : 63;
                 const int q = f - pre[wv][lo];
                 int x, y;
+                int64_t rr, cc;
                 if (diag) {                            // q -> pair (y, x), y < x: q = x(x-1)/2 + y
                     x = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)q)) * 0.5f);
                     if (x * (x - 1) / 2 > q) x--;
                     else if ((x + 1) * x / 2 <= q) x++;
                     y = q - x * (x - 1) / 2;
-                    ri[u] = ra0 + rbeg[wv][lo] + y;
-                    ci[u] = ra0 + rbeg[wv][lo] + x;
+                    rr = ra0 + rbeg[wv][lo] + y;
+                    cc = ra0 + rbeg[wv][lo] + x;
                 } else {
                     const int n2 = ncol[wv][lo];
-                    x = (int)((float)q / (float)n2);
+                    x = (int)((float)q * __builtin_amdgcn_rcpf((float)n2));
                     if (x * n2 > q) x--;
                     else if ((x + 1) * n2 <= q) x++;
                     y = q - x * n2;
-                    ri[u] = ra0 + rbeg[wv][lo] + x;
-                    ci[u] = cb0 + cbeg[wv][lo] + y;
+                    rr = ra0 + rbeg[wv][lo] + x;
+                    cc = cb0 + cbeg[wv][lo] + y;
                 }
+                ri[u] = ok[u] ? rr : ra0;
+                ci[u] = ok[u] ? cc : cb0;
             }
             unsigned long long wr[SUN], wc[SUN];
             int sr[SUN], sc[SUN];
@@ -248,9 +276,9 @@ __global__ __launch_bounds__(SNT, 2) void sparse_tile_kernel(
 #pragma unroll
             for (int u = 0; u < SUN; u++) {
                 const int v = __popcll(wr[u] & wc[u]);
-                if (v && f0 + 64 * u < total) {
-                    atomicAdd(&cnt[sr[u] * SB + sc[u]], v);
-                    if (mirror) atomicAdd(&cnt[sc[u] * SB + sr[u]], v);
+                if (v && ok[u]) {
+                    atomicAdd(&cnt[cnt_index(sr[u], sc[u])], v);
+                    if (mirror) atomicAdd(&cnt[cnt_index(sc[u], sr[u])], v);
                 }
             }
         }
@@ -263,7 +291,8 @@ __global__ __launch_bounds__(SNT, 2) void sparse_tile_kernel(
         return;
     }
     for (int t = threadIdx.x; t < SB * SB; t += SNT) {
-        const int64_t i = A * SB + (t >> 7), j = B * SB + (t & (SB - 1));
+        const int a = t >> 7, b = ((t & (SB - 1)) - a) & (SB - 1);
+        const int64_t i = A * SB + a, j = B * SB + b;
         if (i < r0 || i >= r1 || j < c0 || j >= c1 || (upper && j <= i)) continue;
         const int v = cnt[t] + (int)Us - nc[i] - nc[j];
         if (v) atomicAdd(I + (i - r0) * ldI + (j - c0), v);
@@ -277,8 +306,9 @@ __global__ __launch_bounds__(256) void sparse_reduce_kernel(const int32_t* __res
                                                             int64_t r1, int64_t c0, int64_t c1, int upper,
                                                             int32_t* __restrict__ I, int64_t ldI) {
     const int tile = blockIdx.x / (SB * SB / 256);
-    const int t = (blockIdx.x % (SB * SB / 256)) * 256 + threadIdx.x;
-    const int64_t i = (int64_t)tiles[tile].x * SB + (t >> 7), j = (int64_t)tiles[tile].y * SB + (t & (SB - 1));
+    const int t = (blockIdx.x % (SB * SB / 256)) * 256 + threadIdx.x;     // counter slot (cnt_index layout)
+    const int a = t >> 7, b = ((t & (SB - 1)) - a) & (SB - 1);
+    const int64_t i = (int64_t)tiles[tile].x * SB + a, j = (int64_t)tiles[tile].y * SB + b;
     if (i < r0 || i >= r1 || j < c0 || j >= c1 || (upper && j <= i)) return;
     int v = (int)Us - nc[i] - nc[j];
     const int32_t* p = part + (int64_t)tile * nchunks * (SB * SB) + t;
