@@ -179,9 +179,6 @@ __global__ __launch_bounds__(SNT, 2) void sparse_tile_kernel(
     int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I, int64_t ldI,
     int32_t* __restrict__ part) {
     __shared__ int32_t cnt[SB * SB];                                       // 64 KiB
-    __shared__ int32_t pre[SNW][64];                    // first product of each word of the batch
-    __shared__ int32_t rbeg[SNW][64], cbeg[SNW][64];   // relative to the chunk's first entries
-    __shared__ uint8_t ncol[SNW][64];
     const int tile = blockIdx.x / nchunks, ch = blockIdx.x % nchunks;
     const int64_t A = tiles[tile].x, B = tiles[tile].y;
     // rows of block A inside the region: a tile on a row-block edge (a rank's
@@ -223,12 +220,11 @@ __global__ __launch_bounds__(SNT, 2) void sparse_tile_kernel(
             const int v = __shfl_up(incl, o, 64);
             if (lane >= o) incl += v;
         }
-        pre[wv][lane] = incl - P;
-        rbeg[wv][lane] = (int32_t)(rb - ra0);
-        cbeg[wv][lane] = (int32_t)(cb - cb0);
-        ncol[wv][lane] = (uint8_t)ncl;
-        const int total = __shfl(incl, 63, 64);
-        __builtin_amdgcn_wave_barrier();
+        // word l of the batch: products [incl_l - P_l, incl_l); its list
+        // offsets relative to the chunk bases stay in lane l's registers
+        const int first = incl - P;
+        const int rrel = (int)(rb - ra0), crel = (int)(cb - cb0);
+        const int total = __builtin_amdgcn_readlane(incl, 63);
         for (int fb = 0; fb < total; fb += 64 * SUN) {
             int64_t ri[SUN], ci[SUN];
             bool ok[SUN];
@@ -236,15 +232,20 @@ __global__ __launch_bounds__(SNT, 2) void sparse_tile_kernel(
             for (int u = 0; u < SUN; u++) {
                 const int F = fb + 64 * u, f = F + lane;
                 ok[u] = f < total;
-                // the word holding product f: #{l : incl_l <= f}; incl ascends
-                // with l, so the words ending before F are a ballot prefix and
-                // the few ending inside [F, F + 63] are read from their lanes
-                const int w0 = __popcll(__ballot(incl <= F));
-                const int w1 = __popcll(__ballot(incl <= F + 63));
-                int lo = w0;
-                for (int l = w0; l < w1; l++) lo += __builtin_amdgcn_readlane(incl, l) <= f;
-                lo = lo < 63 ? lo : 63;
-                const int q = f - pre[wv][lo];
+                // the words holding products F .. F + 63 (incl ascends with
+                // l): from the first ending after F to the first ending after
+                // F + 63; each lane takes its word's fields from the owning
+                // lane with readlane - no LDS access before the counters
+                const int l0 = __popcll(__ballot(incl <= F));
+                int l1 = __popcll(__ballot(incl <= F + 63));
+                l1 = l1 < 63 ? l1 : 63;
+                int q = 0, xr = 0, xc = 0, n2 = 1;
+                for (int l = l0; l <= l1; l++) {
+                    const int st = __builtin_amdgcn_readlane(first, l), en = __builtin_amdgcn_readlane(incl, l);
+                    const int r_ = __builtin_amdgcn_readlane(rrel, l), c_ = __builtin_amdgcn_readlane(crel, l);
+                    const int n_ = __builtin_amdgcn_readlane(ncl, l);
+                    if (f >= st && f < en) { q = f - st; xr = r_; xc = c_; n2 = n_; }
+                }
                 int x, y;
                 int64_t rr, cc;
                 if (diag) {                            // q -> pair (y, x), y < x: q = x(x-1)/2 + y
@@ -252,16 +253,15 @@ __global__ __launch_bounds__(SNT, 2) void sparse_tile_kernel(
                     if (x * (x - 1) / 2 > q) x--;
                     else if ((x + 1) * x / 2 <= q) x++;
                     y = q - x * (x - 1) / 2;
-                    rr = ra0 + rbeg[wv][lo] + y;
-                    cc = ra0 + rbeg[wv][lo] + x;
+                    rr = ra0 + xr + y;
+                    cc = ra0 + xr + x;
                 } else {
-                    const int n2 = ncol[wv][lo];
                     x = (int)((float)q * __builtin_amdgcn_rcpf((float)n2));
                     if (x * n2 > q) x--;
                     else if ((x + 1) * n2 <= q) x++;
                     y = q - x * n2;
-                    rr = ra0 + rbeg[wv][lo] + x;
-                    cc = cb0 + cbeg[wv][lo] + y;
+                    rr = ra0 + xr + x;
+                    cc = cb0 + xc + y;
                 }
                 ri[u] = ok[u] ? rr : ra0;
                 ci[u] = ok[u] ? cc : cb0;
@@ -282,7 +282,6 @@ __global__ __launch_bounds__(SNT, 2) void sparse_tile_kernel(
                 }
             }
         }
-        __builtin_amdgcn_wave_barrier();
     }
     __syncthreads();
     if (part) {
