@@ -236,6 +236,7 @@ def main():
         algo_bytes = pairs_rank * bytes_per_pair
         achieved = algo_bytes / (k_avg_ms * 1e-3) / 1e9 if k_avg_ms > 0 else 0.0
         traffic = None
+        pmc = {}
         if os.path.exists(args.pmc_json):
             try:
                 with open(args.pmc_json) as f:
@@ -244,15 +245,52 @@ def main():
                     traffic = pmc.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
+        sparse = sparse_words if (method == "bitset" and sparse_words and sparse_words["sparse_words"] > 0) else None
         kname = {"bitset": "bitset_tile_kernel2<1> (+ rare_pairs_kernel)", "sorted": "sorted_join_kernel",
                  "sketch": "sketch_tile_kernel<16,24,LDS,K=2>"}[method]
-        if method == "bitset":
+        if sparse:
+            kname = "sparse_tile_kernel (+ bitset_tile_kernel2 on the dense words, rare_pairs_kernel, beside it)"
+        if traffic is not None and pmc.get("kernel", "").split()[0] != kname.split()[0]:
+            traffic = None                    # the PMC summary was taken on another kernel
+        valu_peak = VALU_WORDPAIR_PEAK * 4 / 1e12
+        if sparse:
+            # Complement-sparse dense tier: the step's work is
+            # the sparse tile kernel's products over (128-set block, sparse word)
+            # entry lists. Algorithmic bytes = what each launched tile must stream
+            # once: its row block's and column block's entries (8 B complement
+            # word + 1 B set) and their (block, word) offsets (2 x 8 B), one side
+            # for a whole diagonal tile.
+            nb = -(-N // 128)
+            side = sparse["entries"] / nb * 9.0 + sparse["sparse_words"] * 16.0
+            algo_sparse = 0.0
+            for A in range(r0 // 128, (r1 - 1) // 128 + 1):
+                rmin = max(r0, A * 128)
+                for B in range(nb):
+                    if min(N, (B + 1) * 128) - 1 <= rmin:
+                        continue
+                    whole_diag = A == B and A * 128 >= r0 and min(N, (A + 1) * 128) <= r1
+                    algo_sparse += side if whole_diag else 2.0 * side
+            ach = algo_sparse / (k_avg_ms * 1e-3) / 1e9 if k_avg_ms > 0 else 0.0
+            dense_ops = pairs_rank * width_words * 4 / (k_avg_ms * 1e-3) / 1e12 if k_avg_ms > 0 else 0.0
+            roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kname,
+                    "kernel_avg_ms": round(k_avg_ms, 4), "algo_bytes_per_launch": round(algo_sparse),
+                    "note": "algorithmic bytes = the complement entries + offsets each sparse tile streams once; "
+                            "the kernel is bound by its dependent load -> LDS-atomic chain, not by bandwidth "
+                            "(profiles/r01/sparse/ablation_c2.txt); kernel time = HIP-event span of the step's "
+                            "launches (sparse, dense-word tiles and rare tier run concurrently)",
+                    "dense_equivalent": {"lane_ops_per_s_T": round(dense_ops, 2),
+                                         "x_dense_valu_ceiling": round(dense_ops / valu_peak, 2),
+                                         "note": "the same pairs as AND+popcount over all W bitset words "
+                                                 "(4 lane-ops per word pair) in the step's kernel time, against the "
+                                                 "measured and+bcnt ceiling the dense tiles are bound by"}}
+        elif method == "bitset":
             # The tiles reuse each bitset from LDS across 128 partners, so the 16*W
             # B/pair streaming figure runs far past the HBM peak: the binding
             # resource is VALU issue. One 64-bit word pair = 4 lane-ops
             # (2 v_and_b32 + 2 v_bcnt_u32_b32); peak = the measured and+bcnt ceiling.
             wp = pairs_rank * width_words / (k_avg_ms * 1e-3) if k_avg_ms > 0 else 0.0
-            tops, tops_peak = wp * 4 / 1e12, VALU_WORDPAIR_PEAK * 4 / 1e12
+            tops, tops_peak = wp * 4 / 1e12, valu_peak
             roof = {"bound": "valu", "achieved": round(tops, 3), "peak": round(tops_peak, 3), "unit": "TOP/s",
                     "frac": round(tops / tops_peak, 4), "traffic": traffic, "kernel": kname,
                     "kernel_avg_ms": round(k_avg_ms, 4), "ops_per_pair": 4 * width_words,

@@ -609,6 +609,37 @@ def test_sparse_complement_words_exact(ctx, mode, monkeypatch):
     assert bits_equal(d, eD[0, cols])
 
 
+def test_sparse_equals_dense_at_size(ctx, monkeypatch):
+    """C2-shaped collection (shared core, sparse substitutions): the whole
+    triangle through the complement-sparse words equals the plain AND+popcount
+    tiles pair for pair, and the oracle on a corner block; row-sharded blocks
+    (unaligned, as ranks get them) agree too."""
+    import gdist
+    n = 420
+    seqs = synth_sets(n, 200_000, 0.002, 106)
+    sp = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
+    sp.build_bitsets()
+    ws, wd, ent = sp.sparse_info()
+    assert ws > 0 and ent > 0
+    I, D = sp.matrix(upper=True, method=gdist.METHOD_BITSET)
+    monkeypatch.setenv("GDIST_SPARSE", "0")
+    de = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
+    de.build_bitsets()
+    assert de.sparse_info()[0] == 0
+    eI, eD = de.matrix(upper=True, method=gdist.METHOD_BITSET)
+    iu = np.triu_indices(n, 1)
+    assert np.array_equal(I[iu], eI[iu]) and bits_equal(D[iu], eD[iu])
+    monkeypatch.delenv("GDIST_SPARSE")
+    for (r0, r1) in [(0, 77), (77, 200), (200, 331), (331, 420)]:
+        Ib, _ = sp.matrix((r0, r1), (0, n), upper=True, method=gdist.METHOD_BITSET)
+        mask = np.fromfunction(lambda a, b: b > (r0 + a), (r1 - r0, n))
+        assert np.array_equal(Ib[mask], eI[r0:r1][mask]), (r0, r1)
+    off, codes = oracle_pack(seqs[:12], 21, 0, 0)
+    oI, oD = oracle.matrix(off, codes, 0, 12, 0, 12, flags=0x100)
+    iu12 = np.triu_indices(12, 1)
+    assert np.array_equal(I[:12, :12][iu12], oI[iu12]) and bits_equal(D[:12, :12][iu12], oD[iu12])
+
+
 def test_auto_method_prepare(ctx):
     """METHOD_AUTO: small regions stay on the sorted join without building a
     dictionary; a large region of C3-like proteomes (two-tier structure) is
