@@ -164,21 +164,28 @@ __global__ __launch_bounds__(256) void sparse_fill_kernel(const unsigned long lo
 // tiles add into I concurrently), with the constant part U_s - nc_i - nc_j;
 // with several, each chunk stores its counters to `part` and
 // sparse_reduce_kernel sums them.
-constexpr int SNT = 1024;                // threads per workgroup (2 per CU: 8 waves per SIMD)
+constexpr int SNT = 1024;                // threads per workgroup
 constexpr int SNW = SNT / 64;
-constexpr int SUN = 4;                   // products per lane in flight
 
 // LDS counter of local pair (row a, column b): the column is rotated by the
 // row, so the products of one word (its rows x its columns, column fastest
 // across lanes) land on distinct banks instead of one bank per column
 __device__ __forceinline__ int cnt_index(int a, int b) { return a * SB + ((b + a) & (SB - 1)); }
 
-__global__ __launch_bounds__(SNT, 2) void sparse_tile_kernel(
+// 8 products per lane in flight: the kernel is bound by the latency of its
+// load -> add chain (measured 4 / 6 / 8 / 12 / 16: 0.385 / 0.366 / 0.359 /
+// 0.366 / 0.377 ms on C2; 8 runs one workgroup per CU, 83 VGPRs)
+constexpr int SUN = 8;
+
+__global__ __launch_bounds__(SNT) void sparse_tile_kernel(
     const int64_t* __restrict__ off, const unsigned long long* __restrict__ word, const uint8_t* __restrict__ set,
     const int32_t* __restrict__ nc, int64_t Us, int64_t Ws, const int2* __restrict__ tiles, int nchunks,
     int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I, int64_t ldI,
     int32_t* __restrict__ part) {
     __shared__ int32_t cnt[SB * SB];                                       // 64 KiB
+    __shared__ int32_t pre[SNW][64];                    // first product of each word of the batch
+    __shared__ int32_t rbeg[SNW][64], cbeg[SNW][64];   // relative to the chunk's first entries
+    __shared__ uint8_t ncol[SNW][64];
     const int tile = blockIdx.x / nchunks, ch = blockIdx.x % nchunks;
     const int64_t A = tiles[tile].x, B = tiles[tile].y;
     // rows of block A inside the region: a tile on a row-block edge (a rank's
@@ -195,6 +202,11 @@ __global__ __launch_bounds__(SNT, 2) void sparse_tile_kernel(
     const int64_t* offA = off + A * Ws;
     const int64_t* offB = off + B * Ws;
     const int64_t ra0 = offA[sb], cb0 = offB[sb];           // chunk bases (< 2^31 entries per chunk)
+    // the chunk's entries from its bases: 32-bit lane offsets on scalar bases
+    const unsigned long long* wA = word + ra0;
+    const unsigned long long* wB = word + cb0;
+    const uint8_t* sA = set + ra0;
+    const uint8_t* sB = set + cb0;
     for (int64_t base = sb + (int64_t)wv * 64; base < se; base += (int64_t)SNW * 64) {
         const int64_t s = base + lane;
         int64_t rb = ra0, cb = cb0;
@@ -220,58 +232,55 @@ __global__ __launch_bounds__(SNT, 2) void sparse_tile_kernel(
             const int v = __shfl_up(incl, o, 64);
             if (lane >= o) incl += v;
         }
-        // word l of the batch: products [incl_l - P_l, incl_l); its list
-        // offsets relative to the chunk bases stay in lane l's registers
-        const int first = incl - P;
-        const int rrel = (int)(rb - ra0), crel = (int)(cb - cb0);
-        const int total = __builtin_amdgcn_readlane(incl, 63);
+        pre[wv][lane] = incl - P;
+        rbeg[wv][lane] = (int32_t)(rb - ra0);
+        cbeg[wv][lane] = (int32_t)(cb - cb0);
+        ncol[wv][lane] = (uint8_t)ncl;
+        const int total = __shfl(incl, 63, 64);
+        __builtin_amdgcn_wave_barrier();
         for (int fb = 0; fb < total; fb += 64 * SUN) {
-            int64_t ri[SUN], ci[SUN];
+            int32_t ri[SUN], ci[SUN];
             bool ok[SUN];
 #pragma unroll
             for (int u = 0; u < SUN; u++) {
                 const int F = fb + 64 * u, f = F + lane;
                 ok[u] = f < total;
-                // the words holding products F .. F + 63 (incl ascends with
-                // l): from the first ending after F to the first ending after
-                // F + 63; each lane takes its word's fields from the owning
-                // lane with readlane - no LDS access before the counters
-                const int l0 = __popcll(__ballot(incl <= F));
-                int l1 = __popcll(__ballot(incl <= F + 63));
-                l1 = l1 < 63 ? l1 : 63;
-                int q = 0, xr = 0, xc = 0, n2 = 1;
-                for (int l = l0; l <= l1; l++) {
-                    const int st = __builtin_amdgcn_readlane(first, l), en = __builtin_amdgcn_readlane(incl, l);
-                    const int r_ = __builtin_amdgcn_readlane(rrel, l), c_ = __builtin_amdgcn_readlane(crel, l);
-                    const int n_ = __builtin_amdgcn_readlane(ncl, l);
-                    if (f >= st && f < en) { q = f - st; xr = r_; xc = c_; n2 = n_; }
-                }
+                // the word holding product f: #{l : incl_l <= f}; incl ascends
+                // with l, so the words ending before F are a ballot prefix and
+                // the few ending inside [F, F + 63] are read from their lanes
+                const int w0 = __popcll(__ballot(incl <= F));
+                const int w1 = __popcll(__ballot(incl <= F + 63));
+                int lo = w0;
+                for (int l = w0; l < w1; l++) lo += __builtin_amdgcn_readlane(incl, l) <= f;
+                lo = lo < 63 ? lo : 63;
+                const int q = f - pre[wv][lo];
                 int x, y;
-                int64_t rr, cc;
+                int32_t rr, cc;
                 if (diag) {                            // q -> pair (y, x), y < x: q = x(x-1)/2 + y
                     x = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)q)) * 0.5f);
                     if (x * (x - 1) / 2 > q) x--;
                     else if ((x + 1) * x / 2 <= q) x++;
                     y = q - x * (x - 1) / 2;
-                    rr = ra0 + xr + y;
-                    cc = ra0 + xr + x;
+                    rr = rbeg[wv][lo] + y;
+                    cc = rbeg[wv][lo] + x;
                 } else {
+                    const int n2 = ncol[wv][lo];
                     x = (int)((float)q * __builtin_amdgcn_rcpf((float)n2));
                     if (x * n2 > q) x--;
                     else if ((x + 1) * n2 <= q) x++;
                     y = q - x * n2;
-                    rr = ra0 + xr + x;
-                    cc = cb0 + xc + y;
+                    rr = rbeg[wv][lo] + x;
+                    cc = cbeg[wv][lo] + y;
                 }
-                ri[u] = ok[u] ? rr : ra0;
-                ci[u] = ok[u] ? cc : cb0;
+                ri[u] = ok[u] ? rr : 0;
+                ci[u] = ok[u] ? cc : 0;
             }
             unsigned long long wr[SUN], wc[SUN];
             int sr[SUN], sc[SUN];
 #pragma unroll
             for (int u = 0; u < SUN; u++) {
-                wr[u] = word[ri[u]]; wc[u] = word[ci[u]];
-                sr[u] = set[ri[u]]; sc[u] = set[ci[u]];
+                wr[u] = wA[(uint32_t)ri[u]]; wc[u] = (diag ? wA : wB)[(uint32_t)ci[u]];
+                sr[u] = sA[(uint32_t)ri[u]]; sc[u] = (diag ? sA : sB)[(uint32_t)ci[u]];
             }
 #pragma unroll
             for (int u = 0; u < SUN; u++) {
@@ -282,6 +291,7 @@ __global__ __launch_bounds__(SNT, 2) void sparse_tile_kernel(
                 }
             }
         }
+        __builtin_amdgcn_wave_barrier();
     }
     __syncthreads();
     if (part) {
