@@ -338,8 +338,8 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
 
 // sparse.hip — locus order of the dense dictionary, complement-sparse words
 constexpr int kGuides = 2;                       // guide sequences per packed collection
-constexpr double kSparseProductsPerS = 1.0e11;   // sparse tiles: complement-word products
-constexpr double kSparseItemsPerS = 2.0e10;      // sparse tiles: (tile, sparse word) visits
+constexpr double kSparseProductsPerS = 2.6e11;   // sparse tiles: complement-word products (C2)
+constexpr double kSparseItemsPerS = 6.0e10;      // sparse tiles: (tile, sparse word) visits (C2)
 bool locus_order_enabled();                      // GDIST_LOCUS_ORDER=0 keeps code order (A/B)
 // key[r] = tag | guide position of dense rank r (all ones where no guide holds it)
 void locus_keys(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_t U, uint64_t tag, DevBuf& key);

@@ -164,7 +164,11 @@ __global__ __launch_bounds__(256) void sparse_fill_kernel(const unsigned long lo
 // tiles add into I concurrently), with the constant part U_s - nc_i - nc_j;
 // with several, each chunk stores its counters to `part` and
 // sparse_reduce_kernel sums them.
-constexpr int SNT = 1024;                // threads per workgroup
+constexpr int SNT = 512;                 // threads per workgroup (3 per CU: 6 waves per SIMD)
+// Counters are 16-bit, two to an LDS dword: a chunk holds at most kChunkWords
+// sparse words, so a pair's count in one chunk is at most 64 x 1023 < 2^16
+// and a packed ds_add_u32 never carries into the neighbour (32 KiB per tile)
+constexpr int kChunkWords = 1023;
 constexpr int SNW = SNT / 64;
 
 // LDS counter of local pair (row a, column b): the column is rotated by the
@@ -172,17 +176,15 @@ constexpr int SNW = SNT / 64;
 // across lanes) land on distinct banks instead of one bank per column
 __device__ __forceinline__ int cnt_index(int a, int b) { return a * SB + ((b + a) & (SB - 1)); }
 
-// 8 products per lane in flight: the kernel is bound by the latency of its
-// load -> add chain (measured 4 / 6 / 8 / 12 / 16: 0.385 / 0.366 / 0.359 /
-// 0.366 / 0.377 ms on C2; 8 runs one workgroup per CU, 83 VGPRs)
-constexpr int SUN = 8;
 
-__global__ __launch_bounds__(SNT) void sparse_tile_kernel(
+// SUN products per lane in flight, OCC workgroups per CU
+template <int SUN, int OCC>
+__global__ __launch_bounds__(SNT, OCC) void sparse_tile_kernel(
     const int64_t* __restrict__ off, const unsigned long long* __restrict__ word, const uint8_t* __restrict__ set,
     const int32_t* __restrict__ nc, int64_t Us, int64_t Ws, const int2* __restrict__ tiles, int nchunks,
     int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I, int64_t ldI,
     int32_t* __restrict__ part) {
-    __shared__ int32_t cnt[SB * SB];                                       // 64 KiB
+    __shared__ uint32_t cnt[SB * SB / 2];                                  // 32 KiB, 16-bit counters
     __shared__ int32_t pre[SNW][64];                    // first product of each word of the batch
     __shared__ int32_t rbeg[SNW][64], cbeg[SNW][64];   // relative to the chunk's first entries
     __shared__ uint8_t ncol[SNW][64];
@@ -195,7 +197,7 @@ __global__ __launch_bounds__(SNT) void sparse_tile_kernel(
     const bool rpart = rlo > 0 || rhi < SB;
     // a whole diagonal tile walks each word's pairs x < y of its one list
     const bool diag = A == B && !rpart, mirror = diag && !upper;
-    for (int t = threadIdx.x; t < SB * SB; t += SNT) cnt[t] = 0;
+    for (int t = threadIdx.x; t < SB * SB / 2; t += SNT) cnt[t] = 0;
     __syncthreads();
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t sb = Ws * ch / nchunks, se = Ws * (ch + 1) / nchunks;
@@ -286,8 +288,12 @@ __global__ __launch_bounds__(SNT) void sparse_tile_kernel(
             for (int u = 0; u < SUN; u++) {
                 const int v = __popcll(wr[u] & wc[u]);
                 if (v && ok[u]) {
-                    atomicAdd(&cnt[cnt_index(sr[u], sc[u])], v);
-                    if (mirror) atomicAdd(&cnt[cnt_index(sc[u], sr[u])], v);
+                    const int t0 = cnt_index(sr[u], sc[u]);
+                    atomicAdd(&cnt[t0 >> 1], (uint32_t)v << ((t0 & 1) << 4));
+                    if (mirror) {
+                        const int t1 = cnt_index(sc[u], sr[u]);
+                        atomicAdd(&cnt[t1 >> 1], (uint32_t)v << ((t1 & 1) << 4));
+                    }
                 }
             }
         }
@@ -295,15 +301,15 @@ __global__ __launch_bounds__(SNT) void sparse_tile_kernel(
     }
     __syncthreads();
     if (part) {
-        int32_t* dst = part + ((int64_t)tile * nchunks + ch) * (SB * SB);
-        for (int t = threadIdx.x; t < SB * SB; t += SNT) dst[t] = cnt[t];
+        uint32_t* dst = reinterpret_cast<uint32_t*>(part) + ((int64_t)tile * nchunks + ch) * (SB * SB / 2);
+        for (int t = threadIdx.x; t < SB * SB / 2; t += SNT) dst[t] = cnt[t];
         return;
     }
     for (int t = threadIdx.x; t < SB * SB; t += SNT) {
         const int a = t >> 7, b = ((t & (SB - 1)) - a) & (SB - 1);
         const int64_t i = A * SB + a, j = B * SB + b;
         if (i < r0 || i >= r1 || j < c0 || j >= c1 || (upper && j <= i)) continue;
-        const int v = cnt[t] + (int)Us - nc[i] - nc[j];
+        const int v = (int)((cnt[t >> 1] >> ((t & 1) << 4)) & 0xFFFFu) + (int)Us - nc[i] - nc[j];
         if (v) atomicAdd(I + (i - r0) * ldI + (j - c0), v);
     }
 }
@@ -320,8 +326,8 @@ __global__ __launch_bounds__(256) void sparse_reduce_kernel(const int32_t* __res
     const int64_t i = (int64_t)tiles[tile].x * SB + a, j = (int64_t)tiles[tile].y * SB + b;
     if (i < r0 || i >= r1 || j < c0 || j >= c1 || (upper && j <= i)) return;
     int v = (int)Us - nc[i] - nc[j];
-    const int32_t* p = part + (int64_t)tile * nchunks * (SB * SB) + t;
-    for (int c = 0; c < nchunks; c++) v += p[(int64_t)c * (SB * SB)];
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(part) + (int64_t)tile * nchunks * (SB * SB / 2) + (t >> 1);
+    for (int c = 0; c < nchunks; c++) v += (int)((p[(int64_t)c * (SB * SB / 2)] >> ((t & 1) << 4)) & 0xFFFFu);
     if (v) atomicAdd(I + (i - r0) * ldI + (j - c0), v);
 }
 
@@ -492,21 +498,25 @@ void sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
         // enough workgroups to fill the chip, each over >= 512 sparse words
         const char* cv = getenv("GDIST_SPARSE_WG_PER_CU");
         const int64_t target = (int64_t)ctx->cus * (cv ? std::max(1, atoi(cv)) : 4);
-        sc.nchunks = sc.ntiles ? (int)std::max<int64_t>(
-                                     1, std::min<int64_t>(ceil_div(s->Ws, 512), ceil_div(target, sc.ntiles)))
+        // ... and each chunk within the 16-bit counters' bound
+        sc.nchunks = sc.ntiles ? (int)std::max<int64_t>(ceil_div(s->Ws, kChunkWords),
+                                                        std::min<int64_t>(ceil_div(s->Ws, 512), target / sc.ntiles))
                                : 0;
         if (sc.ntiles) {
             sc.tiles.alloc(sc.ntiles * sizeof(int2), st);
             h2d(sc.tiles.p, tiles.data(), sc.ntiles * sizeof(int2), st);
         }
-        if (sc.nchunks > 1) sc.part.alloc((size_t)sc.ntiles * sc.nchunks * SB * SB * 4, st);
+        if (sc.nchunks > 1) sc.part.alloc((size_t)sc.ntiles * sc.nchunks * SB * SB * 2, st);
         GD_REQUIRE(sc.ntiles * sc.nchunks < (int64_t(1) << 31), "sparse grid too large");
         sc.ready = true;
     }
     if (sc.ntiles == 0) return;
     const int nchunks = sc.nchunks;
     const int64_t nt = sc.ntiles;
-    sparse_tile_kernel<<<(unsigned)(nt * nchunks), SNT, 0, st>>>(
+    // 6 products per lane in flight at 3 workgroups (6 waves) per SIMD-quad:
+    // the kernel is bound by the latency of its load -> add chain (C2 sweep,
+    // profiles/r01/sparse/sweep_unroll_c2.txt)
+    sparse_tile_kernel<6, 3><<<(unsigned)(nt * nchunks), SNT, 0, st>>>(
         s->sp_off.as<int64_t>(), s->sp_word.as<unsigned long long>(), s->sp_set.as<uint8_t>(), s->sp_nc.as<int32_t>(),
         s->sp_U, s->Ws, sc.tiles.as<int2>(), nchunks, r0, r1, c0, c1, upper ? 1 : 0, d_I, ldI,
         nchunks > 1 ? sc.part.as<int32_t>() : nullptr);
