@@ -513,10 +513,15 @@ void sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     if (sc.ntiles == 0) return;
     const int nchunks = sc.nchunks;
     const int64_t nt = sc.ntiles;
-    // 6 products per lane in flight at 3 workgroups (6 waves) per SIMD-quad:
-    // the kernel is bound by the latency of its load -> add chain (C2 sweep,
-    // profiles/r01/sparse/sweep_unroll_c2.txt)
-    sparse_tile_kernel<6, 3><<<(unsigned)(nt * nchunks), SNT, 0, st>>>(
+    // 6 products per lane in flight (C2 sweep, profiles/r01/sparse/
+    // sweep_unroll_c2.txt): the kernel is bound by the latency of its
+    // load -> add chain. __launch_bounds__'s second argument is the minimum
+    // waves per SIMD: 8 holds the SGPRs under the 8-wave budget (4 workgroups
+    // per CU, LDS-limited) where 3 let them reach 112 (3 per CU): 0.310 ->
+    // 0.298 ms (profiles/r01/sparse/occ_{3,8}.json; GDIST_SPARSE_OCC=3 for A/B)
+    const char* ov = getenv("GDIST_SPARSE_OCC");
+    auto kern = (ov && atoi(ov) == 3) ? sparse_tile_kernel<6, 3> : sparse_tile_kernel<6, 8>;
+    kern<<<(unsigned)(nt * nchunks), SNT, 0, st>>>(
         s->sp_off.as<int64_t>(), s->sp_word.as<unsigned long long>(), s->sp_set.as<uint8_t>(), s->sp_nc.as<int32_t>(),
         s->sp_U, s->Ws, sc.tiles.as<int2>(), nchunks, r0, r1, c0, c1, upper ? 1 : 0, d_I, ldI,
         nchunks > 1 ? sc.part.as<int32_t>() : nullptr);
