@@ -520,7 +520,12 @@ void sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     // per CU, LDS-limited) where 3 let them reach 112 (3 per CU): 0.310 ->
     // 0.298 ms (profiles/r01/sparse/occ_{3,8}.json; GDIST_SPARSE_OCC=3 for A/B)
     const char* ov = getenv("GDIST_SPARSE_OCC");
-    auto kern = (ov && atoi(ov) == 3) ? sparse_tile_kernel<6, 3> : sparse_tile_kernel<6, 8>;
+    const char* uv = getenv("GDIST_SPARSE_SUN");
+    const int sun = uv ? atoi(uv) : 6;
+    auto kern = (ov && atoi(ov) == 3) ? sparse_tile_kernel<6, 3>
+                : sun == 4            ? sparse_tile_kernel<4, 8>
+                : sun == 8            ? sparse_tile_kernel<8, 8>
+                                      : sparse_tile_kernel<6, 8>;
     kern<<<(unsigned)(nt * nchunks), SNT, 0, st>>>(
         s->sp_off.as<int64_t>(), s->sp_word.as<unsigned long long>(), s->sp_set.as<uint8_t>(), s->sp_nc.as<int32_t>(),
         s->sp_U, s->Ws, sc.tiles.as<int2>(), nchunks, r0, r1, c0, c1, upper ? 1 : 0, d_I, ldI,
