@@ -1,7 +1,7 @@
 // bitset.hip — dictionary-rank bitsets and the tiled AND+popcount N×N kernel.
 //
 // Replaces the SequenceKmers.distance(other) loop over many pairs
-// (FastaDistanceProcessor.java:177-186, GenomeProcessor.java:336,
+// (FastaDistanceProcessor.java:177-186, GenomeProcessor.java:140,
 // WidthProcessor.java:159-165): |A∩B| = Σ_w popcount(a_w & b_w) over
 // per-set bitsets indexed by the rank of each kmer in a global dictionary.
 //

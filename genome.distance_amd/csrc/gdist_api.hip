@@ -711,14 +711,14 @@ int gdist_row_query(gdist_ctx* ctx, const gdist_sets* sets, int64_t q, const int
         }
         if (D_out) std::memcpy(D_out, d.data(), ncols * 8);
         if (mode == GDIST_QUERY_ANY_LE && hit) {
-            // anyMatch(x -> x.distance(kmers) <= maxDist), DistanceRepsProcessor.java:400
+            // anyMatch(x -> x.distance(kmers) <= maxDist), DistanceRepsProcessor.java:190
             int32_t h = 0;
             for (int64_t c = 0; c < ncols; c++) if (d[c] <= t) { h = 1; break; }
             *hit = h;
         }
         if (mode == GDIST_QUERY_ARGMIN) {
             // reduce(NULL_RESULT, (x,y) -> x.distance <= y.distance ? x : y),
-            // DistanceRepsProcessor.java:330-332,448-449: the 1.0 identity wins ties at 1.0
+            // DistanceRepsProcessor.java:108-122,238-239: the 1.0 identity wins ties at 1.0
             int64_t bi = -1;
             double bd = 1.0;
             for (int64_t c = 0; c < ncols; c++) if (d[c] < bd) { bd = d[c]; bi = c; }

@@ -1,7 +1,7 @@
 // pack.hip — device-side kmer extraction and packing into sorted unique
 // uint64 code sets (CSR).  Replaces KmerType.createKmers(seq, K)
 // (FastaDistanceProcessor.java:153,184), new GenomeKmers(genome)
-// (GenomeProcessor.java:305,335) and new ProteinKmers(seq)
+// (GenomeProcessor.java:109,139) and new ProteinKmers(seq)
 // (ProteinKmerReader.java:101), which build a HashSet<String> per sequence.
 //
 // Pipeline per chunk of sequences (bounded so keys+values fit comfortably):

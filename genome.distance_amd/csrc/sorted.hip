@@ -1,7 +1,7 @@
 // sorted.hip — exact |A∩B| over sorted uint64 kmer sets by LDS hash-join tiles.
 //
 // Same contract as bitset.hip (SequenceKmers.distance over many pairs,
-// FastaDistanceProcessor.java:177-186, GenomeProcessor.java:336), for set
+// FastaDistanceProcessor.java:177-186, GenomeProcessor.java:140), for set
 // collections whose shared-kmer dictionary would be too wide for bitsets
 // (diverse genomes / proteins: SURVEY §8d configs 3 and 4).
 //

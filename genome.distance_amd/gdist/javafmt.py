@@ -2,8 +2,8 @@
 
 Double.toString (JDK 19+ algorithm; the reference targets JDK 21, pom.xml:17)
 is what `"..." + distance` and TextStringBuilder.append(double) print at
-FastaDistanceProcessor.java:189-190, GenomeProcessor.java:340,
-DistanceRepsProcessor.java:460-461: the shortest decimal that rounds to the
+FastaDistanceProcessor.java:189-190, GenomeProcessor.java:144,
+DistanceRepsProcessor.java:250-251: the shortest decimal that rounds to the
 double (the closest such; a one-digit result is widened to the closest
 two-digit decimal), laid out plain for 1e-3 <= |d| < 1e7 and as d.dddE±n
 otherwise.

@@ -2,14 +2,15 @@
 
 The reference's `methods` command (MethodTableProcessor.java:166-308) drives
 this API: DistanceMethod.create(type) and parseParmString(parms) per line of
-the method file (:175-182), toString() as the output column header (:243),
-getMeasurer(genome1) once per first genome (:261-265,397-407),
-getDistance(measurer, genome2) from ForkJoin threads (:275) and close()
-(:304-306). The method classes themselves live in the un-vendored
+the method file (MethodTableProcessor.java:175-182), toString() as the output
+column header (MethodTableProcessor.java:243), getMeasurer(genome1) once per
+first genome (MethodTableProcessor.java:261-265,397-407),
+getDistance(measurer, genome2) from ForkJoin threads
+(MethodTableProcessor.java:275) and close() (MethodTableProcessor.java:304-306). The method classes themselves live in the un-vendored
 org.theseed:distance module; the kmer methods below restate the kmer
 distance of SURVEY §8a a1/a2 on the GPU path. A GPU Measurer keeps its
 genome packed in HBM; `getDistances` is the batched form the processor
-should call (GenomePairList.prepare groups pairs by id1, :240).
+should call (GenomePairList.prepare groups pairs by id1, MethodTableProcessor.java:240).
 """
 from __future__ import annotations
 
@@ -107,7 +108,7 @@ class _KmerMethod(DistanceMethod):
 
 
 class DnaKmerMethod(_KmerMethod):
-    """Contig DNA kmer distance (GenomeKmers, GenomeProcessor.java:305,336)."""
+    """Contig DNA kmer distance (GenomeKmers, GenomeProcessor.java:109,140)."""
     type_name = "kmer"
 
     def kmer_text(self, g: Genome) -> bytes:

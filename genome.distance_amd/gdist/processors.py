@@ -5,9 +5,9 @@ errors and output format, and replaces its per-pair Java loop with whole
 row-block / row-query calls on the device:
 
   fasta_distance   FastaDistanceProcessor  (fastaDist)  FastaDistanceProcessor.java:84-194
-  genome_distance  GenomeProcessor         (genomes)    GenomeProcessor.java:270-346
+  genome_distance  GenomeProcessor         (genomes)    GenomeProcessor.java:74-150
   fasta_reps       FastaDistanceRepsProcessor (fastaReps) FastaDistanceRepsProcessor.java:58-149
-  distance_reps    DistanceRepsProcessor   (distReps)   DistanceRepsProcessor.java:350-485
+  distance_reps    DistanceRepsProcessor   (distReps)   DistanceRepsProcessor.java:140-275
   width_processor  WidthProcessor          (width)      WidthProcessor.java:88-208
 
 Output rows are emitted in (row, column) order; the reference's fastaDist
@@ -52,12 +52,12 @@ def fasta_distance(records: Sequence[FastaRecord], out: TextIO, kmer_size: int =
                    kmer_type: KmerType = KmerType.DNA, flags: int = 0, method: int = L.METHOD_AUTO,
                    ctx: Context | None = None, row_block: int = 1024) -> int:
     """fastaDist: N×N upper triangle of kmer distances over FASTA records."""
-    k = kmer_size or kmer_type.getKmerSize()                       # :95-96
+    k = kmer_size or kmer_type.getKmerSize()                       # FastaDistanceProcessor.java:95-96
     if k < 2:
-        raise ParseFailureException("Kmer size must be at least 2.")   # :98-99
+        raise ParseFailureException("Kmer size must be at least 2.")   # FastaDistanceProcessor.java:98-99
     if batch < 1:
-        raise ParseFailureException("Batch size must be at least 1.")  # :101-102
-    out.write("seq1\tname1\tseq2\tname2\tdistance\n")                 # :139
+        raise ParseFailureException("Batch size must be at least 1.")  # FastaDistanceProcessor.java:101-102
+    out.write("seq1\tname1\tseq2\tname2\tdistance\n")                 # FastaDistanceProcessor.java:139
     n = len(records)
     if n < 2:
         return 0
@@ -82,21 +82,21 @@ def genome_distance(base: Sequence[Genome], others: Sequence[Sequence[Genome]], 
                     method: int = L.METHOD_AUTO, ctx: Context | None = None) -> int:
     """genomes: every comparison genome against every base genome."""
     if kmer_size < 4:
-        raise ParseFailureException("Kmer size cannot be less than 4.")          # GenomeProcessor.java:280-281
+        raise ParseFailureException("Kmer size cannot be less than 4.")          # GenomeProcessor.java:84-85
     if max_dist <= 0.0 or max_dist > 1.0:
-        raise ParseFailureException("Maximum distance must be > 0 and <= 1.")    # :285-286
-    out.write("genome1\tgenome2\tdistance\n")                                    # :317
+        raise ParseFailureException("Maximum distance must be > 0 and <= 1.")    # GenomeProcessor.java:89-90
+    out.write("genome1\tgenome2\tdistance\n")                                    # GenomeProcessor.java:121
     comps = [g for src in others for g in src]
     if not base or not comps:
         return 0
     allg = list(base) + comps
     sets = KmerSets.from_sequences([g.kmer_text() for g in allg], kmer_size, KmerType.DNA, flags, ctx)
     nb = len(base)
-    # one rectangle: rows = comparison genomes, cols = base genomes (:336)
+    # one rectangle: rows = comparison genomes, cols = base genomes (GenomeProcessor.java:140)
     _, D = sets.matrix((nb, len(allg)), (0, nb), method=method, want_I=False)
     n = 0
     for a, g in enumerate(comps):
-        for i, bg in enumerate(base):                                             # :339-341
+        for i, bg in enumerate(base):                                             # GenomeProcessor.java:143-144
             out.write(f"{g.id}\t{bg.id}\t{java_double(D[a, i])}\n")
             n += 1
     return n
@@ -111,22 +111,36 @@ def java_string_hash(s: str) -> int:
     return h - (1 << 32) if h & 0x80000000 else h
 
 
-def java_hashmap_order(keys: Sequence[str]) -> list[int]:
-    """Iteration order of a java.util.HashMap<String, V> into which `keys`
-    (distinct) were put in order: bucket (h ^ h >>> 16) & (cap - 1), cap the
-    table size after the 0.75-load resizes from 16; insertion order within a
-    bucket (resizes split bins keeping it). The reps processors iterate
-    repMap.values() in this order (DistanceRepsProcessor.java:190,236,
-    FastaDistanceRepsProcessor.java:124). Tree bins (>= 8 keys in one bucket
-    of a table >= 64) are not modelled."""
+def java_table_size_for(initial_capacity: int) -> int:
+    """java.util.HashMap.tableSizeFor: the power of two >= initial_capacity."""
+    cap = 1
+    while cap < initial_capacity:
+        cap *= 2
+    return max(cap, 1)
+
+
+def java_hashmap_order(keys: Sequence[str], initial_capacity: int = 16) -> list[int]:
+    """Iteration order of a java.util.HashMap<String, V> created with
+    `new HashMap<>(initial_capacity)` into which `keys` (distinct) were put in
+    order: bucket (h ^ h >>> 16) & (cap - 1), cap = tableSizeFor(initial
+    capacity), doubled whenever a put takes the size past 0.75 · cap;
+    insertion order within a bucket (resizes split bins keeping it). The reps
+    processors iterate repMap.values() in this order: distReps creates it with
+    capacity 500 (DistanceRepsProcessor.java:175, iterated at :190,238),
+    fastaReps with 100 (FastaDistanceRepsProcessor.java:90, iterated at :124).
+    Tree bins (>= 8 keys in one bucket of a table >= 64) are not modelled."""
     n = len(keys)
-    cap = 16
+    cap = java_table_size_for(initial_capacity)
     while n > cap * 3 // 4:
         cap *= 2
     def bucket(s):
         h = java_string_hash(s) & 0xFFFFFFFF
         return (h ^ (h >> 16)) & (cap - 1)
     return sorted(range(n), key=lambda i: (bucket(keys[i]), i))
+
+
+#: new HashMap<String, GenomeKmers>(500), DistanceRepsProcessor.java:175
+DISTREPS_REPMAP_CAPACITY = 500
 
 
 def _greedy_host(sets: KmerSets, keys: Sequence[str], max_dist: float) -> list[int]:
@@ -159,8 +173,8 @@ def fasta_reps(records: Sequence[FastaRecord], out: TextIO, kmer_size: int = 0, 
     (a repeated label re-enters repMap under its key and is printed again)."""
     k = kmer_size or kmer_type.getKmerSize()
     if k < 2:
-        raise ParseFailureException("Kmer size must be at least 2.")           # :96-97
-    out.write("seq\tname\n")                                                  # :121
+        raise ParseFailureException("Kmer size must be at least 2.")           # FastaDistanceRepsProcessor.java:84-85
+    out.write("seq\tname\n")                                                  # FastaDistanceRepsProcessor.java:115
     if not records:
         return []
     sets = KmerSets.from_sequences([r.sequence for r in records], k, kmer_type, flags, ctx)
@@ -179,27 +193,27 @@ def fasta_reps(records: Sequence[FastaRecord], out: TextIO, kmer_size: int = 0, 
             printed.append(i)
         reps = list(rep_of_key.values())
     for i in printed:
-        out.write(f"{records[i].label}\t{records[i].comment}\n")            # :139-141
+        out.write(f"{records[i].label}\t{records[i].comment}\n")            # FastaDistanceRepsProcessor.java:141-144
     return reps
 
 
 def distance_reps(genomes: Sequence[Genome], kmer_size: int = 9, max_dist: float = 0.97, flags: int = 0,
                   ctx: Context | None = None) -> tuple[str, str, str]:
-    """distReps (DistanceRepsProcessor.java:350-485): returns (file name
+    """distReps (DistanceRepsProcessor.java:140-275): returns (file name
     prefix, list.tbl text, stats.tbl text). Pass 1 picks representatives in
     input order; pass 2 assigns every genome its closest representative,
     ties to the earlier one in repMap's HashMap iteration order."""
     if kmer_size < 4:
-        raise ParseFailureException("Kmer size must be at least 4.")           # :366-367
+        raise ParseFailureException("Kmer size must be at least 4.")           # DistanceRepsProcessor.java:156-157
     if max_dist <= 0.0 or max_dist >= 1.0:
-        raise ParseFailureException("Distance must be strictly between 0 and 1.")  # :370-371
-    prefix = "rep%.4f_K%d" % (max_dist, kmer_size)                              # :422
+        raise ParseFailureException("Distance must be strictly between 0 and 1.")  # DistanceRepsProcessor.java:160-161
+    prefix = "rep%.4f_K%d" % (max_dist, kmer_size)                              # DistanceRepsProcessor.java:212
     sets = KmerSets.from_sequences([g.kmer_text() for g in genomes], kmer_size, KmerType.DNA, flags, ctx)
     ids = [g.id for g in genomes]
-    reps = _greedy(sets, ids, max_dist)                                         # pass 1 (:185-200)
+    reps = _greedy(sets, ids, max_dist)                                         # pass 1 (DistanceRepsProcessor.java:185-200)
     rep_set = set(reps)
     # repMap iteration order (keys = genome ids, put in pass-1 order)
-    order = java_hashmap_order([ids[r] for r in reps])
+    order = java_hashmap_order([ids[r] for r in reps], DISTREPS_REPMAP_CAPACITY)
     ordered_reps = [reps[o] for o in order]
     lines = ["genome_id\tgenome_name\trep_id\trep_name\tdistance"]
     counts: dict[int, int] = {}
@@ -209,7 +223,7 @@ def distance_reps(genomes: Sequence[Genome], kmer_size: int = 9, max_dist: float
         for pos, r in enumerate(ordered_reps):
             rank[r] = pos
         _, rep_of, rep_d = sets.greedy_reps(max_dist, assign=True, tie_rank=rank)
-    for i, g in enumerate(genomes):                                             # pass 2 (:227-262)
+    for i, g in enumerate(genomes):                                             # pass 2 (DistanceRepsProcessor.java:220-262)
         if i in rep_set:
             r, d = i, 0.0
         elif unique:
@@ -221,7 +235,7 @@ def distance_reps(genomes: Sequence[Genome], kmer_size: int = 9, max_dist: float
         lines.append(f"{g.id}\t{g.name}\t{rg.id}\t{rg.name}\t{java_double(d)}")
         counts[r] = counts.get(r, 0) + 1
     stats = ["rep_id\trep_name\tsize"]
-    for r, c in sorted(counts.items(), key=lambda kv: (-kv[1], genomes[kv[0]].id)):   # sortedCounts (:478)
+    for r, c in sorted(counts.items(), key=lambda kv: (-kv[1], genomes[kv[0]].id)):   # sortedCounts (DistanceRepsProcessor.java:268)
         stats.append(f"{genomes[r].id}\t{genomes[r].name}\t{c}")
     return prefix, "\n".join(lines) + "\n", "\n".join(stats) + "\n"
 

@@ -12,15 +12,15 @@
  * taken from the in-repo call sites):
  *
  *   gdist_sets_pack        KmerType.createKmers(seq, K)          FastaDistanceProcessor.java:153,184
- *                          new GenomeKmers(genome)               GenomeProcessor.java:305,335
+ *                          new GenomeKmers(genome)               GenomeProcessor.java:109,139
  *                          new ProteinKmers(seq)                 ProteinKmerReader.java:101
  *   gdist_sets_sizes       SequenceKmers.size()                  (used by distance())
  *   gdist_intersect_matrix SequenceKmers.distance(other) over the
  *                          N×N upper triangle                    FastaDistanceProcessor.java:177-186
- *                          M×N rectangle                         GenomeProcessor.java:336
+ *                          M×N rectangle                         GenomeProcessor.java:140
  *                          group all-pairs                       WidthProcessor.java:159-165
- *   gdist_row_query        anyMatch(d <= maxDist)                DistanceRepsProcessor.java:400
- *                          reduce(NULL_RESULT, merge) argmin     DistanceRepsProcessor.java:448-449
+ *   gdist_row_query        anyMatch(d <= maxDist)                DistanceRepsProcessor.java:190
+ *                          reduce(NULL_RESULT, merge) argmin     DistanceRepsProcessor.java:238-239
  *                          sequential early exit                 FastaDistanceRepsProcessor.java:117-128
  *   gdist_sketch_build     SequenceKmers.hashSet(width)          SketchProcessor.java:88, WidthProcessor.java:178
  *   gdist_sketch_matrix    Sketch.distance(other) all-pairs      WidthProcessor.java:183-185, TuningProcessor.java:131-133
@@ -205,7 +205,7 @@ int  gdist_greedy_reps(gdist_ctx* ctx, const gdist_sets* sets, int method, doubl
  *  ARGMIN: *best_idx = position in cols[] of the smallest distance (ties ->
  *          lowest position), *best_d = that distance; -1 / 1.0 when no
  *          distance is below 1.0 (the reference's NULL_RESULT identity wins
- *          ties at 1.0, DistanceRepsProcessor.java:318-332). */
+ *          ties at 1.0, DistanceRepsProcessor.java:108-122). */
 int  gdist_row_query(gdist_ctx* ctx, const gdist_sets* sets, int64_t q,
                      const int64_t* cols, int64_t ncols, int mode, double t,
                      double* D_out, int32_t* hit, int64_t* best_idx, double* best_d);

@@ -79,7 +79,7 @@ static int ambig_skip(int kind, unsigned flags) {
 
 /* ------------------------------------------------------------------ */
 /* kmer codes — KmerType.createKmers(seq, K) (FastaDistanceProcessor.java:153,184),
- * new GenomeKmers(genome) (GenomeProcessor.java:305), new ProteinKmers(seq)
+ * new GenomeKmers(genome) (GenomeProcessor.java:109), new ProteinKmers(seq)
  * (ProteinKmerReader.java:101). Set semantics: every length-k substring, once. */
 
 int64_t or_kmer_codes(int kind, int k, unsigned flags, const char* seq, int64_t len, uint64_t* out) {
@@ -184,7 +184,7 @@ double or_distance(int64_t inter, int64_t na, int64_t nb, unsigned flags) {
  * to d; when that is one digit long, the closest two-digit decimal.
  * Layout: plain for 1e-3 <= |d| < 1e7 (at least one fraction digit), else
  * d.dddE[-]n. Used at FastaDistanceProcessor.java:189-190,
- * GenomeProcessor.java:340, DistanceRepsProcessor.java:460-461. */
+ * GenomeProcessor.java:144, DistanceRepsProcessor.java:250-251. */
 int or_java_dtoa(double d, char* buf) {
     if (isnan(d)) return sprintf(buf, "NaN");
     if (isinf(d)) return sprintf(buf, d > 0 ? "Infinity" : "-Infinity");

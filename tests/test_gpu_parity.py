@@ -427,7 +427,7 @@ def test_reps_processors_java_semantics(ctx):
     for i in range(len(seqs)):
         if not any(pyref.set_distance(ks[r], ks[i]) <= 0.6 for r in reps):
             reps.append(i)
-    order = [reps[o] for o in P.java_hashmap_order([ids[r] for r in reps])]
+    order = [reps[o] for o in P.java_hashmap_order([ids[r] for r in reps], P.DISTREPS_REPMAP_CAPACITY)]
     rows = [l.split("\t") for l in lst.splitlines()[1:]]
     for i, row in enumerate(rows):
         if i in reps:

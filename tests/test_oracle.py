@@ -171,3 +171,31 @@ def test_java_string_hash_and_hashmap_order():
     assert java_hashmap_order(keys) == sorted(range(4), key=lambda i: ((java_string_hash(keys[i]) & 0xFFFFFFFF ^
                                                                          (java_string_hash(keys[i]) & 0xFFFFFFFF) >> 16) & 15, i))
     assert java_hashmap_order(["Aa", "BB"]) == [0, 1] and java_hashmap_order(["BB", "Aa"]) == [0, 1]
+
+
+def test_hashmap_order_initial_capacity():
+    """repMap is `new HashMap<>(500)` (DistanceRepsProcessor.java:175): a
+    512-bucket table from the first put, grown only past 384 keys. Hand
+    computed: String.hashCode of a one-char key is its char (a=97, b=98,
+    q=113), the spread h ^ h>>>16 leaves it, so with 16 buckets a and q share
+    bucket 1 (b is 2) and with 512 buckets they are 97, 98, 113."""
+    from gdist.processors import DISTREPS_REPMAP_CAPACITY, java_hashmap_order, java_table_size_for
+    assert java_table_size_for(500) == 512 and java_table_size_for(100) == 128 and java_table_size_for(16) == 16
+    keys = ["q", "b", "a"]
+    assert java_hashmap_order(keys) == [0, 2, 1]                                    # q(1) a(1) b(2)
+    assert java_hashmap_order(keys, DISTREPS_REPMAP_CAPACITY) == [2, 1, 0]          # a(97) b(98) q(113)
+    # 20 keys where bucket mod 16 and bucket mod 512 give different orders
+    many = [chr(ord("A") + i) + chr(ord("a") + (7 * i) % 26) for i in range(20)]
+    o16, o512 = java_hashmap_order(many), java_hashmap_order(many, 500)
+    assert o16 != o512 and sorted(o16) == sorted(o512) == list(range(20))
+    # two-char keys: hashCode = 31*c0 + c1 < 512*16, spread is the identity below 2^16
+    assert o512 == sorted(range(20), key=lambda i: ((31 * ord(many[i][0]) + ord(many[i][1])) & 511, i))
+    # growth: 384 keys stay in 512 buckets, the 385th put resizes to 1024
+    k385 = ["k%d" % i for i in range(385)]
+    def h(s):
+        x = 0
+        for ch in s:
+            x = (31 * x + ord(ch)) & 0xFFFFFFFF
+        return x ^ (x >> 16)
+    assert java_hashmap_order(k385[:384], 500) == sorted(range(384), key=lambda i: (h(k385[i]) & 511, i))
+    assert java_hashmap_order(k385, 500) == sorted(range(385), key=lambda i: (h(k385[i]) & 1023, i))
