@@ -80,7 +80,10 @@ def main():
                     help="multi-rank exchange: RCCL (default) or host-staged over gloo (ranks sharing a GPU)")
     ap.add_argument("--same-device", action="store_true",
                     help="testing: every rank uses device 0 (rehearse the multi-rank path on one GPU)")
-    ap.add_argument("--cpu-threads", type=int, default=8)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (default: this process's CPU share, see host_cpus())")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="context tuning option (gdist_ctx_set_option); GDIST_<NAME> variables are mapped too")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_c2.json"),
                     help="per-launch HBM traffic measured by rocprofv3 PMC passes (optional)")
     args = ap.parse_args()
@@ -102,7 +105,11 @@ def main():
     if args.length:
         cfg["length"] = args.length
     n_total = int(round(cfg["n"] * math.sqrt(world))) if world > 1 else cfg["n"]
-    ctx = gdist.Context(0 if args.same_device else local_rank)
+    options = gdist.options_from_env()
+    for kv in args.opt:
+        k, v = kv.split("=", 1)
+        options[k] = int(v)
+    ctx = gdist.Context(0 if args.same_device else local_rank, options)
 
     def barrier():
         ctx.synchronize()
@@ -217,6 +224,9 @@ def main():
     pairs_all = N * (N - 1) // 2
     value = pairs_all * args.steps / elapsed_max
     k_avg_ms = float(np.mean(kernel_ms)) if kernel_ms else 0.0
+    # end to end: the whole job for one pass over the collection = pack +
+    # represent (dictionary, bitsets / sketches) + one step, max over ranks
+    e2e_s = max_over_ranks(pack_s + represent_s + elapsed / max(args.steps, 1))
 
     verified = verify_sample(cfg, method, N, r0, r1, dI, dD, max_over_ranks)
     out = None
@@ -308,12 +318,14 @@ def main():
         # ---------------------------------------------------------------- CPU baseline
         cpu = None
         cpu_opt = None
+        host = host_cpus()
         if not args.no_cpu_baseline and world == 1:
-            cpu, cpu_opt = cpu_baselines(cfg, args.cpu_threads)
+            cpu, cpu_opt = cpu_baselines(cfg, args.cpu_threads or host["threads"], host)
         out = {
             "metric": "genome-pair distances/sec (N×N)",
             "value": round(value, 1),
             "unit": "pairs/s",
+            "end_to_end_pairs_per_s": round(pairs_all / e2e_s, 1),
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -327,13 +339,18 @@ def main():
                        "k": cfg["k"], "pairs_per_step": pairs_all, "parallelism": f"rows{world}",
                        "bitset_words_per_set": width_words or None,
                        "dictionary_size": (dict_size if method == "bitset" else None),
-                       "method": method, "auto": auto, "rare_tier": rare, "complement_sparse": sparse_words},
+                       "method": method, "auto": auto, "rare_tier": rare, "complement_sparse": sparse_words,
+                       "options": options or None},
             "roofline": roof,
             "verified": verified,
             "cpu_baseline": cpu,
             "cpu_optimized": cpu_opt,
             "setup_s": {"generate": round(gen_s, 2), "pack": round(pack_s, 2), "represent": round(represent_s, 2),
                         "total": round(setup_s, 2)},
+            "end_to_end": {"pairs_per_s": round(pairs_all / e2e_s, 1), "seconds": round(e2e_s, 3),
+                           "note": "one pass over the collection from FASTA bytes in host memory: pack (H2D + "
+                                   "kmer extraction + sort) + represent (dictionary, bitsets, sparse words) + one "
+                                   "step; synthetic-genome generation excluded; max over ranks"},
         }
         print(json.dumps(out), flush=True)
     if verified is not None and not verified["ok"]:
@@ -418,11 +435,37 @@ def verify_sample(cfg, method, N, r0, r1, dI, dD, max_over_ranks, npairs=4):
             "how": "independent numpy recount from regenerated genomes, bit-exact I and fp64 D"}
 
 
-def cpu_baselines(cfg, threads, target_s=10.0, cap=6000):
+def host_cpus() -> dict:
+    """The CPUs this process may use and what they are. On the GPU box
+    os.cpu_count() reports the whole machine while the job's share is set by
+    its affinity mask and OMP_NUM_THREADS (16 per GPU there), so the CPU legs
+    run on min(affinity, OMP_NUM_THREADS) threads and all three are recorded."""
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    threads = min(aff, int(omp)) if omp.isdigit() and int(omp) > 0 else aff
+    return {"model": model, "os_cpu_count": os.cpu_count(), "affinity": aff, "omp_num_threads": omp or None,
+            "threads": threads}
+
+
+def cpu_baselines(cfg, threads, host=None, target_s=10.0, cap=6000, batch=20):
     """The Java-faithful restatement (HashSet<String> + FastaDistanceProcessor
-    loop) on a bounded sample, plus the optimised sorted-merge CPU path.
-    Both samples are rows 0..T-1 against the later genomes of a prefix of the
-    workload; the prefix is calibrated so each leg runs ~target_s seconds."""
+    loop, the reference's default batch of 20 cached rows,
+    FastaDistanceProcessor.java:88) on a bounded sample — the rows of the
+    first batch against the later genomes of a prefix of the workload — plus
+    the optimised sorted-merge CPU path on rows 0..T-1. Each prefix is
+    calibrated so the leg runs ~target_s seconds."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     from gdist import synth
@@ -436,7 +479,7 @@ def cpu_baselines(cfg, threads, target_s=10.0, cap=6000):
     def faithful(n):
         seqs = genomes(n)
         t = time.perf_counter()
-        pairs, _ = oracle.faithful_fasta_dist(seqs, cfg["k"], kind, 0, batch=T, max_rows=T, nthreads=T)
+        pairs, _ = oracle.faithful_fasta_dist(seqs, cfg["k"], kind, 0, batch=batch, max_rows=batch, nthreads=T)
         return pairs, time.perf_counter() - t
 
     def optimised(n):
@@ -445,8 +488,8 @@ def cpu_baselines(cfg, threads, target_s=10.0, cap=6000):
         oracle.matrix(off, codes, 0, T, 0, n, flags=0x100, nthreads=T)
         return T * n - T * (T + 1) // 2, time.perf_counter() - t
 
-    def calibrated(run):
-        n = T + max(1, T // 2)
+    def calibrated(run, n0):
+        n = n0
         pairs, dt = run(n)
         for _ in range(4):          # fixed costs make small runs look slow: grow in steps
             if dt >= target_s / 2 or n >= cap:
@@ -455,12 +498,12 @@ def cpu_baselines(cfg, threads, target_s=10.0, cap=6000):
             pairs, dt = run(n)
         return n, pairs, dt
 
-    n1, p1, dt1 = calibrated(faithful)
-    fa = {"value": round(p1 / dt1, 3), "unit": "pairs/s", "cores": T, "kind": "port",
-          "sample": f"rows 0..{T - 1} x all later columns of the first {n1} genomes ({p1} pairs, "
-                    f"batch {T}: cached rows + per-pair rebuilt sets as FastaDistanceProcessor.java:150-186), "
-                    f"{dt1:.1f} s"}
-    n2, p2, dt2 = calibrated(optimised)
+    n1, p1, dt1 = calibrated(faithful, batch + max(1, batch // 2))
+    fa = {"value": round(p1 / dt1, 3), "unit": "pairs/s", "cores": T, "kind": "port", "host": host,
+          "sample": f"rows 0..{batch - 1} x all later columns of the first {n1} genomes ({p1} pairs, "
+                    f"batch {batch} as FastaDistanceProcessor.java:88: cached rows + per-pair rebuilt sets as "
+                    f":150-186, rows in parallel on {T} threads as :157-158), {dt1:.1f} s"}
+    n2, p2, dt2 = calibrated(optimised, T + max(1, T // 2))
     opt = {"value": round(p2 / dt2, 2), "unit": "pairs/s", "cores": T, "kind": "port-optimised",
            "sample": f"rows 0..{T - 1} x all later columns of the first {n2} genomes ({p2} pairs), "
                      f"sorted-uint64 merge, OpenMP, {dt2:.1f} s"}

@@ -835,8 +835,8 @@ void dictionary_from(gdist_ctx* ctx, const std::vector<SummaryView>& parts, bool
     const int64_t n = m.n;
     if (keep) T = 0;
     if (T < 0) {
-        if (const char* e = getenv("GDIST_RARE_T")) {
-            T = atoll(e);
+        if (ctx->has_option(OPT_RARE_T)) {
+            T = ctx->option(OPT_RARE_T, -1);
         } else {
             DevBuf dh((nsets + 1) * 8, st);
             GD_HIP(hipMemsetAsync(dh.p, 0, (nsets + 1) * 8, st));
@@ -998,7 +998,7 @@ void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_
                unsigned long long* rare_out, int64_t rare_cap, int64_t* rare_written, const uint32_t* perm) {
     hipStream_t st = ctx->stream;
     const int cbits = std::min(64, code_bits(s->kind, s->k, s->flags));
-    Trace tr(st);
+    Trace tr(st, ctx->trace());
     GD_HIP(hipMemsetAsync(bits, 0, (size_t)s->nsets * W * 8, st));
     DevBuf rcnt(8, st);
     GD_HIP(hipMemsetAsync(rcnt.p, 0, 8, st));
@@ -1137,7 +1137,7 @@ __global__ void entry_weights_kernel(const uint64_t* __restrict__ keys, int64_t 
 // lists merged (GDIST_RARE_DEDUP=0 keeps one list per kmer, A/B)
 void build_postings(gdist_ctx* ctx, gdist_sets* s, unsigned long long* recs, int64_t n, int64_t Ur) {
     hipStream_t st = ctx->stream;
-    Trace tr(st);
+    Trace tr(st, ctx->trace());
     s->n_rare = Ur;
     s->rare_kmers = Ur;
     s->rare_records = n;
@@ -1167,9 +1167,8 @@ void build_postings(gdist_ctx* ctx, gdist_sets* s, unsigned long long* recs, int
     posting_sets_kernel<<<grid_for(n), 256, 0, st>>>(keys, n, s->post_sets.as<uint32_t>());
     GD_HIP(hipGetLastError());
     tr.mark("postings: lists");
-    const char* dv = getenv("GDIST_RARE_DEDUP");
     int64_t nl = Ur, nrec = n;
-    if (!(dv && atoi(dv) == 0)) {
+    if (ctx->option(OPT_RARE_DEDUP, 1) != 0) {
         DevBuf hA(Ur * 8, st), hB(Ur * 8, st), iA(Ur * 4, st), iB(Ur * 4, st);
         list_hash_kernel<<<grid_for(Ur), 256, 0, st>>>(s->post_off.as<int64_t>(), s->post_sets.as<uint32_t>(), Ur,
                                                        hA.as<uint64_t>(), iA.as<int32_t>());
@@ -1255,7 +1254,7 @@ void build_postings(gdist_ctx* ctx, gdist_sets* s, unsigned long long* recs, int
 void build_bitsets(gdist_ctx* ctx, gdist_sets* s, unsigned flags, int64_t rare_threshold) {
     const bool keep = (flags & GDIST_BITSET_KEEP_SINGLETONS) != 0;
     int64_t T = keep ? 0 : rare_threshold;     // < 0: cost-optimal from the count histogram
-    Trace tr(ctx->stream);
+    Trace tr(ctx->stream, ctx->trace());
     Summary sum;
     local_summary(ctx, s, sum);
     tr.mark("bitsets: summary");
@@ -1266,7 +1265,7 @@ void build_bitsets(gdist_ctx* ctx, gdist_sets* s, unsigned flags, int64_t rare_t
     tr.mark("bitsets: dictionary");
     const int64_t W = bitset_words(U);
     DevBuf perm;
-    if (s->n_guide > 0 && locus_order_enabled()) {
+    if (s->n_guide > 0 && locus_order_enabled(ctx)) {
         DevBuf key;
         locus_keys(ctx, s, dict.as<uint64_t>(), U, 0, key);
         locus_perm(ctx, key, U, perm);
@@ -1397,19 +1396,16 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     // complement-sparse words run in their own kernel (sparse.hip)
     const unsigned long long* tbits = s->sparse ? s->dbits.as<unsigned long long>() : s->bits.as<unsigned long long>();
     const int64_t tW = s->sparse ? s->Wd : s->W;
-    const char* ev = getenv("GDIST_BITSET_KERNEL");   // A/B selection (default: 3)
-    const int variant = ev ? atoi(ev) : 3;
+    const int variant = (int)ctx->option(OPT_BITSET_KERNEL, 3);   // A/B selection
     // Diagonal tiles of an upper-triangle region (row0 == col0) get their
     // own launch of the DIAG variant, which skips the accumulators that
-    // only hold pairs with j <= i (GDIST_BITSET_DIAG=0 keeps one launch).
-    const char* dv = getenv("GDIST_BITSET_DIAG");
-    const bool split_diag = variant != 1 && upper && !(dv && atoi(dv) == 0);
+    // only hold pairs with j <= i (option bitset_diag = 0 keeps one launch).
+    const bool split_diag = variant != 1 && upper && ctx->option(OPT_BITSET_DIAG, 1) != 0;
     // The last row tile of a block whose rows are not a multiple of BT
     // holds nlast rows: its tiles get launches instantiated for
     // RR = ceil(nlast / 16) accumulator rows, skipping the others' work.
-    // (GDIST_BITSET_PARTIAL_RR: the largest RR given its own launches, A/B)
-    const char* pv = getenv("GDIST_BITSET_PARTIAL_RR");
-    const int max_rr = pv ? atoi(pv) : kPartialMaxRR;
+    // (option bitset_partial_rr: the largest RR given its own launches, A/B)
+    const int max_rr = (int)ctx->option(OPT_BITSET_PARTIAL_RR, kPartialMaxRR);
 
     // ---- the region's launch plan (built once, then reused)
     const std::vector<int64_t> key{r0, r1, c0, c1, upper ? 1 : 0, variant, split_diag ? 1 : 0, max_rr, tW};
@@ -1475,12 +1471,10 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     // list-major kernel uses atomics only, like the dense kernel, so it runs
     // beside the dense launch on the side stream (GDIST_RARE_OVERLAP=0 keeps
     // it in line).
-    const char* rv = getenv("GDIST_RARE_KERNEL");
     bool row_major = false;
     if (s->n_rare > 0) (void)bitset_block_cost_s(s, r0, r1, c0, c1, upper, &row_major);
-    const bool list_major = rv ? atoi(rv) == 0 : !row_major;
-    const char* ov = getenv("GDIST_RARE_OVERLAP");
-    const bool overlap = s->n_rare > 0 && list_major && !(ov && atoi(ov) == 0);
+    const bool list_major = ctx->has_option(OPT_RARE_KERNEL) ? ctx->option(OPT_RARE_KERNEL, 0) == 0 : !row_major;
+    const bool overlap = s->n_rare > 0 && list_major && ctx->option(OPT_RARE_OVERLAP, 1) != 0;
     // The sparse words and the list-major rare kernel add atomically, like
     // the dense tiles, so they run on the side stream beside them.
     const bool side = overlap || s->sparse;
@@ -1506,13 +1500,11 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     } else {
         const int64_t nch2 = tW / KC2;
         // workgroups per CU the K-split aims for (GDIST_BITSET_WG_PER_CU, A/B)
-        const char* wv = getenv("GDIST_BITSET_WG_PER_CU");
-        const int64_t wg_per_cu = wv ? std::max(1, atoi(wv)) : 16;
+        const int64_t wg_per_cu = std::max<int64_t>(1, ctx->option(OPT_BITSET_WG_PER_CU, 16));
         // ... but each workgroup streams at least min_kc chunks: a split's
         // prologue and its 16K accumulator atomics amortise over its chunks
         // (launches of few tiles: diagonal, partial; GDIST_BITSET_MIN_CHUNKS, A/B)
-        const char* mv = getenv("GDIST_BITSET_MIN_CHUNKS");
-        const int64_t min_kc = mv ? std::max(1, atoi(mv)) : 16;
+        const int64_t min_kc = std::max<int64_t>(1, ctx->option(OPT_BITSET_MIN_CHUNKS, 16));
         const int64_t corg = p.corg;
         auto launch = [&](auto kern, const int2* dtiles, size_t nt) {
             if (nt == 0) return;

@@ -19,6 +19,21 @@
 
 namespace gdist {
 
+const char* const kOptNames[OPT_COUNT] = {
+    "trace",           "rare_t",          "rare_dedup",      "rare_kernel",     "rare_overlap",
+    "bitset_kernel",   "bitset_diag",     "bitset_partial_rr", "bitset_wg_per_cu", "bitset_min_chunks",
+    "reps_block",      "locus_order",     "sparse",          "sparse_zmax",     "sparse_wg_per_cu",
+    "sparse_occ",      "sparse_sun",      "sketch_k",        "sketch_tile",     "sparse_part_budget",
+    "guides",
+};
+
+static int option_index(const char* name) {
+    GD_REQUIRE(name != nullptr, "null option name");
+    for (int i = 0; i < OPT_COUNT; i++)
+        if (strcmp(kOptNames[i], name) == 0) return i;
+    throw Error(GDIST_EINVAL, std::string("unknown option: ") + name);
+}
+
 static thread_local std::string g_last_error;
 
 void set_last_error(const std::string& msg) { g_last_error = msg; }
@@ -226,6 +241,34 @@ int gdist_ctx_synchronize(gdist_ctx* ctx) {
     return guard([&] {
         use_device(ctx);
         GD_HIP(hipStreamSynchronize(ctx->stream));
+    });
+}
+
+int gdist_ctx_set_option(gdist_ctx* ctx, const char* name, int64_t value) {
+    return guard([&] {
+        GD_REQUIRE(ctx, "null context");
+        const int i = option_index(name);
+        std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+        ctx->opt[i] = value == GDIST_OPTION_DEFAULT ? kOptUnset : value;
+        // launch plans cache per-call choices: drop none here (their keys
+        // carry the options they depend on), sets built later see the value
+    });
+}
+
+int gdist_ctx_get_option(gdist_ctx* ctx, const char* name, int64_t* value, int* is_set) {
+    return guard([&] {
+        GD_REQUIRE(ctx && value, "null argument");
+        const int i = option_index(name);
+        *value = ctx->opt[i] == kOptUnset ? GDIST_OPTION_DEFAULT : ctx->opt[i];
+        if (is_set) *is_set = ctx->opt[i] != kOptUnset;
+    });
+}
+
+int gdist_ctx_option_name(int index, const char** name) {
+    return guard([&] {
+        GD_REQUIRE(name, "null output");
+        GD_REQUIRE(index >= 0 && index < OPT_COUNT, "option index out of range");
+        *name = kOptNames[index];
     });
 }
 
@@ -989,7 +1032,7 @@ int gdist_sets_allgather_bitsets(gdist_ctx* ctx, const gdist_sets* local, unsign
         // guides (tagged with the rank, so rank 0's guides come first), one
         // all-gather, the minimum over ranks -> the same permutation everywhere
         DevBuf perm;
-        if (locus_order_enabled()) {
+        if (locus_order_enabled(ctx)) {
             DevBuf key;
             locus_keys(ctx, local, dict.as<uint64_t>(), U, (uint64_t)ctx->rank << 40, key);
             if (R > 1) {

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <climits>
 #include <cstdint>
 #include <map>
 #include <memory>
@@ -145,13 +146,45 @@ struct Timing {
     int64_t launches = 0;
 };
 
-// Stage timer for setup paths: GDIST_TRACE=1 prints "gdist: <stage> <ms>"
+// Tuning options of a context (gdist_ctx_set_option). These are the A/B
+// switches of DESIGN.md §5; each defaults to the measured best. The library
+// never reads the environment: a JNI host whose environment differs gets the
+// same kernels as the tests, and callers that share a context
+// (MethodTableProcessor.java:275, concurrent getDistance) share its options.
+enum Opt : int {
+    OPT_TRACE = 0,          // 1: setup stage timings on stderr
+    OPT_RARE_T,             // rare-tier threshold T (default: histogram cost model)
+    OPT_RARE_DEDUP,         // 0: one posting list per rare kmer
+    OPT_RARE_KERNEL,        // 0 list-major / 1 row-major (default: cost model per call)
+    OPT_RARE_OVERLAP,       // 0: list-major rare kernel in line
+    OPT_BITSET_KERNEL,      // tile kernel 1 / 2 / 3 (default 3)
+    OPT_BITSET_DIAG,        // 0: no separate trimmed launch for diagonal tiles
+    OPT_BITSET_PARTIAL_RR,  // largest RR whose partial row tile gets its own launches
+    OPT_BITSET_WG_PER_CU,   // K-split target (default 16)
+    OPT_BITSET_MIN_CHUNKS,  // fewest 8-word chunks per K-split workgroup (default 16)
+    OPT_REPS_BLOCK,         // greedy-reps row block (default: by memory)
+    OPT_LOCUS_ORDER,        // 0: dense ranks in code order
+    OPT_SPARSE,             // 0: no complement-sparse words
+    OPT_SPARSE_ZMAX,        // words with z_w <= ZMAX are sparse (forces the split)
+    OPT_SPARSE_WG_PER_CU,   // chunking target of the sparse tiles (default 4)
+    OPT_SPARSE_OCC,         // 3: sparse kernel built for 3 instead of 8 waves per SIMD
+    OPT_SPARSE_SUN,         // products per lane in flight (4 / 6 / 8, default 6)
+    OPT_SKETCH_K,           // sketch merge window (1 / 2 / 4 / 6, default 2)
+    OPT_SKETCH_TILE,        // 16: force the 16x16 sketch tile
+    OPT_SPARSE_PART_BUDGET, // bytes of sparse chunk partials one region may hold
+    OPT_GUIDES,             // guide sequences keyed at pack time (default kGuides)
+    OPT_COUNT
+};
+extern const char* const kOptNames[OPT_COUNT];
+constexpr int64_t kOptUnset = INT64_MIN;
+
+// Stage timer for setup paths: option "trace" = 1 prints "gdist: <stage> <ms>"
 // to stderr after synchronising the stream (off: no synchronisation, no cost).
 struct Trace {
     bool on;
     hipStream_t st;
     std::chrono::steady_clock::time_point t;
-    explicit Trace(hipStream_t s) : on(getenv("GDIST_TRACE") != nullptr), st(s), t(std::chrono::steady_clock::now()) {}
+    Trace(hipStream_t s, bool enabled) : on(enabled), st(s), t(std::chrono::steady_clock::now()) {}
     void mark(const char* stage) {
         if (!on) return;
         (void)hipStreamSynchronize(st);
@@ -180,6 +213,12 @@ struct gdist_ctx {
     gdist_allgather_fn host_ag = nullptr;   // host-staged transport (gdist_comm_init_host)
     void* host_user = nullptr;
     int nranks = 1, rank = 0;
+    // tuning options (gdist_ctx_set_option), kOptUnset = the default
+    int64_t opt[gdist::OPT_COUNT];
+    gdist_ctx() { for (auto& o : opt) o = gdist::kOptUnset; }
+    int64_t option(gdist::Opt o, int64_t dflt) const { return opt[o] == gdist::kOptUnset ? dflt : opt[o]; }
+    bool has_option(gdist::Opt o) const { return opt[o] != gdist::kOptUnset; }
+    bool trace() const { return option(gdist::OPT_TRACE, 0) != 0; }
 };
 
 // A collection of kmer sets resident in HBM.
@@ -340,7 +379,7 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
 constexpr int kGuides = 2;                       // guide sequences per packed collection
 constexpr double kSparseProductsPerS = 2.6e11;   // sparse tiles: complement-word products (C2)
 constexpr double kSparseItemsPerS = 6.0e10;      // sparse tiles: (tile, sparse word) visits (C2)
-bool locus_order_enabled();                      // GDIST_LOCUS_ORDER=0 keeps code order (A/B)
+bool locus_order_enabled(const gdist_ctx* ctx);  // option locus_order = 0 keeps code order (A/B)
 // key[r] = tag | guide position of dense rank r (all ones where no guide holds it)
 void locus_keys(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_t U, uint64_t tag, DevBuf& key);
 // key[r] = min over R ranks' keys (all[q * stride_r + r])

@@ -402,7 +402,7 @@ void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_se
     }
 
     // 2-4. chunks of sequences, at most kChunk entries each
-    Trace tr(st);
+    Trace tr(st, ctx->trace());
     tr.mark("pack: validate/fold");
     const int64_t kChunk = int64_t(1) << 30;
     std::vector<DevBuf> chunk_codes;
@@ -439,9 +439,9 @@ void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_se
             GD_HIP(hipGetLastError());
         }
         tr.mark("pack: alloc+extract");
-        if (s0 == 0 && nw > 0 && locus_order_enabled())
-            guide_from_extract(ctx, kA.as<uint64_t>(), vA.as<int32_t>(), hwo[std::min(nc, kGuides)] * mult, nc,
-                               cbits, out);
+        const int64_t nguides = std::min<int64_t>(nc, std::max<int64_t>(0, ctx->option(OPT_GUIDES, kGuides)));
+        if (s0 == 0 && nw > 0 && nguides > 0 && locus_order_enabled(ctx))
+            guide_from_extract(ctx, kA.as<uint64_t>(), vA.as<int32_t>(), hwo[nguides] * mult, nc, cbits, out);
         uint64_t* keys = kA.as<uint64_t>(); uint64_t* keys_alt = kB.as<uint64_t>();
         int32_t* ids = vA.as<int32_t>(); int32_t* ids_alt = vB.as<int32_t>();
         PackDebug* dbg = (s0 == 0) ? g_pack_debug : nullptr;

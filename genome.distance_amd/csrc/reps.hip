@@ -90,7 +90,7 @@ void greedy_reps(gdist_ctx* ctx, gdist_sets* s, int method, double t, const int6
     // row block: B x N counts + distances within ~1.5 GiB, a multiple of 128 rows
     int64_t B = std::max<int64_t>(128, std::min<int64_t>(4096, ((int64_t(1) << 27) / n) / 128 * 128));
     B = std::min<int64_t>(B, ceil_div(n, 128) * 128);
-    if (const char* e = getenv("GDIST_REPS_BLOCK")) B = std::max<int64_t>(1, atoll(e));   // tests: several blocks
+    if (ctx->has_option(OPT_REPS_BLOCK)) B = std::max<int64_t>(1, ctx->option(OPT_REPS_BLOCK, B));   // tests: several blocks
     DevBuf dI((size_t)B * n * 4 + 4, st), dD((size_t)B * n * 8 + 8, st), drep(n * 4 + 4, st), dcov(B * 4 + 4, st);
     GD_HIP(hipMemsetAsync(drep.p, 0, n * 4, st));
     std::vector<int32_t> cov(B);

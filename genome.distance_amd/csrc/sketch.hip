@@ -244,7 +244,7 @@ constexpr size_t sketch_meta_bytes() { return (size_t)(R + C) * (sizeof(int64_t)
 template <int R, int C>
 bool launch_sketch_tiles(hipStream_t st, const gdist_sets* sk, int width, int64_t r0, int64_t r1, int64_t c0,
                          int64_t c1, bool upper, int jac, int en, int32_t* d_common, double* d_D, int64_t ld,
-                         bool force_global) {
+                         bool force_global, int64_t kw_opt) {
     const int sw = sketch_stride(width);
     const size_t lds = (size_t)(R + C) * sw * 4 + LDS_SK_SLACK;
     const bool use_lds = !force_global && lds + sketch_meta_bytes<R, C>() <= (size_t)LDS_SK_MAX;
@@ -252,9 +252,8 @@ bool launch_sketch_tiles(hipStream_t st, const gdist_sets* sk, int width, int64_
     const int tr = (int)ceil_div(r1 - r0, R), tc = (int)ceil_div(c1 - c0, C);
     const int64_t grid = (int64_t)tr * tc;
     GD_REQUIRE(grid < (int64_t(1) << 31), "sketch grid too large");
-    // GDIST_SKETCH_K selects the merge window (1, 2, 4, 6; A/B measurements)
-    const char* env = getenv("GDIST_SKETCH_K");
-    const int kw = env ? atoi(env) : 2;
+    // option sketch_k selects the merge window (1, 2, 4, 6; A/B measurements)
+    const int kw = (int)kw_opt;
     const int32_t* sig = sk->codes.as<int32_t>();
     const int64_t* off = sk->off.as<int64_t>();
     if (!use_lds) {
@@ -371,14 +370,14 @@ void sketch_matrix(gdist_ctx* ctx, const gdist_sets* sk, int64_t r0, int64_t r1,
     const bool upper = (flags & GDIST_UPPER_TRIANGLE) != 0;
     const int jac = (flags & GDIST_SKETCH_JACCARD) ? 1 : 0, en = (flags & GDIST_EMPTY_NAN) ? 1 : 0;
     const int width = std::max(1, sk->width);
-    // GDIST_SKETCH_TILE=16 forces the 16x16 tile (A/B measurements)
-    const char* env = getenv("GDIST_SKETCH_TILE");
-    const bool only16 = env && atoi(env) == 16;
+    // option sketch_tile = 16 forces the 16x16 tile (A/B measurements)
+    const bool only16 = ctx->option(OPT_SKETCH_TILE, 0) == 16;
+    const int64_t kw = ctx->option(OPT_SKETCH_K, 2);
     GD_HIP(hipEventRecord(ctx->ev_k0, st));
     if (only16 || !launch_sketch_tiles<16, 24>(st, sk, width, r0, r1, c0, c1, upper, jac, en, d_common, d_D, ld,
-                                               false))
-        if (!launch_sketch_tiles<16, 16>(st, sk, width, r0, r1, c0, c1, upper, jac, en, d_common, d_D, ld, false))
-            launch_sketch_tiles<16, 16>(st, sk, width, r0, r1, c0, c1, upper, jac, en, d_common, d_D, ld, true);
+                                               false, kw))
+        if (!launch_sketch_tiles<16, 16>(st, sk, width, r0, r1, c0, c1, upper, jac, en, d_common, d_D, ld, false, kw))
+            launch_sketch_tiles<16, 16>(st, sk, width, r0, r1, c0, c1, upper, jac, en, d_common, d_D, ld, true, kw);
     GD_HIP(hipEventRecord(ctx->ev_k1, st));
     ctx->last.launches = 1;
 }

@@ -371,10 +371,7 @@ void locus_perm(gdist_ctx* ctx, DevBuf& key, int64_t U, DevBuf& perm) {
     GD_HIP(hipStreamSynchronize(st));
 }
 
-bool locus_order_enabled() {
-    const char* e = getenv("GDIST_LOCUS_ORDER");
-    return !(e && atoi(e) == 0);
-}
+bool locus_order_enabled(const gdist_ctx* ctx) { return ctx->option(OPT_LOCUS_ORDER, 1) != 0; }
 
 void free_sparse(gdist_sets* s) {
     s->plans.clear();
@@ -399,10 +396,9 @@ double sparse_block_cost_s(const gdist_sets* s, double f_area, double tiles) {
 
 void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
     free_sparse(s);
-    const char* e = getenv("GDIST_SPARSE");
-    if ((e && atoi(e) == 0) || s->W == 0 || s->nsets < 2) return;
+    if (ctx->option(OPT_SPARSE, 1) == 0 || s->W == 0 || s->nsets < 2) return;
     hipStream_t st = ctx->stream;
-    Trace tr(st);
+    Trace tr(st, ctx->trace());
     const int64_t N = s->nsets, W = s->W, U = s->dict_size;
     const int64_t Wv = ceil_div(U, 64);   // words holding dictionary bits
     if (Wv == 0) return;
@@ -417,16 +413,17 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
     d2h(z.data(), dz.p, W * 4, st);
     tr.mark("sparse: word classes");
     // A word is sparse when its products + visits cost less than its column
-    // of word pairs in the dense tiles (GDIST_SPARSE_ZMAX overrides).
+    // of word pairs in the dense tiles (option sparse_zmax overrides).
     const double n = (double)N, pairs = 0.5 * n * (n - 1.0);
     const double nb = (double)ceil_div(N, SB), tiles = nb * (nb + 1) / 2;
     const double dense_word_s = pairs / kDenseWordPairsPerS;
-    const char* zm = getenv("GDIST_SPARSE_ZMAX");
+    const bool zm = ctx->has_option(OPT_SPARSE_ZMAX);
+    const int64_t zmax = ctx->option(OPT_SPARSE_ZMAX, 0);
     std::vector<int32_t> sw, dw;
     double products = 0.0;
     for (int64_t w = 0; w < Wv; w++) {
         const double zz = (double)z[w];
-        const bool sparse = zm ? z[w] <= atoi(zm)
+        const bool sparse = zm ? z[w] <= zmax
                                : 0.5 * zz * zz / kSparseProductsPerS + tiles / kSparseItemsPerS < dense_word_s;
         if (sparse) { sw.push_back((int32_t)w); products += 0.5 * zz * zz; }
         else dw.push_back((int32_t)w);
@@ -496,8 +493,7 @@ void sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
             }
         sc.ntiles = (int64_t)tiles.size();
         // enough workgroups to fill the chip, each over >= 512 sparse words
-        const char* cv = getenv("GDIST_SPARSE_WG_PER_CU");
-        const int64_t target = (int64_t)ctx->cus * (cv ? std::max(1, atoi(cv)) : 4);
+        const int64_t target = (int64_t)ctx->cus * std::max<int64_t>(1, ctx->option(OPT_SPARSE_WG_PER_CU, 4));
         // ... and each chunk within the 16-bit counters' bound
         sc.nchunks = sc.ntiles ? (int)std::max<int64_t>(ceil_div(s->Ws, kChunkWords),
                                                         std::min<int64_t>(ceil_div(s->Ws, 512), target / sc.ntiles))
@@ -519,10 +515,8 @@ void sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     // waves per SIMD: 8 holds the SGPRs under the 8-wave budget (4 workgroups
     // per CU, LDS-limited) where 3 let them reach 112 (3 per CU): 0.310 ->
     // 0.298 ms (profiles/r01/sparse/occ_{3,8}.json; GDIST_SPARSE_OCC=3 for A/B)
-    const char* ov = getenv("GDIST_SPARSE_OCC");
-    const char* uv = getenv("GDIST_SPARSE_SUN");
-    const int sun = uv ? atoi(uv) : 6;
-    auto kern = (ov && atoi(ov) == 3) ? sparse_tile_kernel<6, 3>
+    const int sun = (int)ctx->option(OPT_SPARSE_SUN, 6);
+    auto kern = ctx->option(OPT_SPARSE_OCC, 8) == 3 ? sparse_tile_kernel<6, 3>
                 : sun == 4            ? sparse_tile_kernel<4, 8>
                 : sun == 8            ? sparse_tile_kernel<8, 8>
                                       : sparse_tile_kernel<6, 8>;

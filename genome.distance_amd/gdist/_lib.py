@@ -23,6 +23,7 @@ METHOD_AUTO, METHOD_SORTED, METHOD_BITSET = 0, 1, 2
 BITSET_KEEP_SINGLETONS = 0x1
 QUERY_ALL, QUERY_ANY_LE, QUERY_ARGMIN = 0, 1, 2
 UNIQUE_ID_BYTES = 128
+OPTION_DEFAULT = -(1 << 63)   # GDIST_OPTION_DEFAULT
 
 
 class GdistError(RuntimeError):
@@ -54,6 +55,9 @@ _SIGS = {
     "gdist_ctx_destroy": (C.c_int, [_ctxp]),
     "gdist_ctx_synchronize": (C.c_int, [_ctxp]),
     "gdist_ctx_last_timing": (C.c_int, [_ctxp, _dblp, _dblp, _i64p]),
+    "gdist_ctx_set_option": (C.c_int, [_ctxp, C.c_char_p, _i64]),
+    "gdist_ctx_get_option": (C.c_int, [_ctxp, C.c_char_p, _i64p, C.POINTER(C.c_int)]),
+    "gdist_ctx_option_name": (C.c_int, [C.c_int, C.POINTER(C.c_char_p)]),
     "gdist_dev_alloc": (C.c_int, [_ctxp, _i64, C.POINTER(_vp)]),
     "gdist_dev_free": (C.c_int, [_ctxp, _vp]),
     "gdist_memcpy_d2h": (C.c_int, [_ctxp, _vp, _vp, _i64]),

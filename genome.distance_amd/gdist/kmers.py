@@ -14,25 +14,75 @@ parity (one pair per call is a correctness path, not a fast path).
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import enum
-from typing import Iterable, Sequence
+import os
+from typing import Iterable, Mapping, Sequence
 
 import numpy as np
 
 from . import _lib as L
 
 
+def option_names() -> list[str]:
+    """Every tuning option of gdist_ctx_set_option (include/gdist.h)."""
+    names, i = [], 0
+    while True:
+        p = C.c_char_p()
+        if L.lib.gdist_ctx_option_name(i, C.byref(p)) != L.OK:
+            return names
+        names.append(p.value.decode())
+        i += 1
+
+
+def options_from_env(environ: Mapping[str, str] | None = None) -> dict[str, int]:
+    """GDIST_<NAME>=<int> variables of a host program's environment as an
+    options dict. The library itself never reads the environment; A/B
+    launchers (bench.py, scripts/) map it explicitly with this."""
+    env = os.environ if environ is None else environ
+    out = {}
+    for name in option_names():
+        v = env.get("GDIST_" + name.upper())
+        if v is not None and v != "":
+            out[name] = int(v)
+    return out
+
+
 class Context:
-    """One HIP device + stream (gdist_ctx)."""
+    """One HIP device + stream (gdist_ctx) and its tuning options."""
 
     _defaults: dict[int, "Context"] = {}
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, options: Mapping[str, int] | None = None):
         h = C.c_void_p()
         L.check(L.lib.gdist_ctx_create(device, C.byref(h)))
         self.h = h
         self.device = device
+        for k, v in (options or {}).items():
+            self.set_option(k, v)
+
+    def set_option(self, name: str, value: int | None) -> None:
+        """gdist_ctx_set_option; None restores the default."""
+        L.check(L.lib.gdist_ctx_set_option(self.h, name.encode(), L.OPTION_DEFAULT if value is None else int(value)))
+
+    def option(self, name: str) -> int | None:
+        """The option's value, None when it is at its default."""
+        v, is_set = C.c_int64(), C.c_int()
+        L.check(L.lib.gdist_ctx_get_option(self.h, name.encode(), C.byref(v), C.byref(is_set)))
+        return int(v.value) if is_set.value else None
+
+    @contextlib.contextmanager
+    def options(self, **opts: int | None):
+        """Set options for the duration of a with-block, then restore them."""
+        old = {k: self.option(k) for k in opts}
+        try:
+            for k, v in opts.items():
+                self.set_option(k, v)
+            yield self
+        finally:
+            for k, v in old.items():
+                self.set_option(k, v)
 
     @classmethod
     def default(cls, device: int = 0) -> "Context":

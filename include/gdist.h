@@ -115,6 +115,19 @@ int  gdist_ctx_synchronize(gdist_ctx* ctx);
 /* HIP-event time of the last intersect/sketch matrix call's main kernel(s)
  * and of the whole call, in ms (recorded on the stream they run on). */
 int  gdist_ctx_last_timing(gdist_ctx* ctx, double* kernel_ms, double* call_ms, int64_t* launches);
+/* Tuning options of a context: the A/B switches of DESIGN.md §5 by name
+ * ("rare_t", "bitset_kernel", "sparse", "sparse_zmax", "sketch_k", ...;
+ * gdist_ctx_option_name enumerates them, EINVAL past the last). Every option
+ * defaults to the measured best; GDIST_OPTION_DEFAULT restores it. The
+ * library never reads the environment, so every host (JNI, ctypes) sharing a
+ * context gets the same kernels (concurrent getDistance callers,
+ * MethodTableProcessor.java:275). Options read at build time (rare_t,
+ * rare_dedup, locus_order, sparse, sparse_zmax, guides) apply to collections
+ * packed or built after the call. */
+#define GDIST_OPTION_DEFAULT INT64_MIN
+int  gdist_ctx_set_option(gdist_ctx* ctx, const char* name, int64_t value);
+int  gdist_ctx_get_option(gdist_ctx* ctx, const char* name, int64_t* value, int* is_set);
+int  gdist_ctx_option_name(int index, const char** name);
 int  gdist_dev_alloc(gdist_ctx* ctx, int64_t bytes, void** dptr);
 int  gdist_dev_free(gdist_ctx* ctx, void* dptr);
 int  gdist_memcpy_d2h(gdist_ctx* ctx, void* dst, const void* src, int64_t bytes);

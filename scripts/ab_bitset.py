@@ -21,7 +21,7 @@ ref = None
 times = {v: [] for v in variants}
 for rnd in range(rounds):
     for v in variants:
-        os.environ["GDIST_BITSET_KERNEL"] = v
+        ctx.set_option("bitset_kernel", int(v))
         sets.matrix_device(dI.ptr, dD.ptr, n, (0, n), (0, n), upper=True, method=gdist.METHOD_BITSET)
         k_ms, call_ms, _ = ctx.last_timing()
         times[v].append(k_ms)

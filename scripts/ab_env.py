@@ -1,4 +1,4 @@
-"""In-process A/B of environment switches read per matrix call (GDIST_*):
+"""In-process A/B of context options (gdist_ctx_set_option, named GDIST_<OPTION> here):
 interleaved rounds on one collection; every setting's counts must equal the
 first one's. AB_ENVS="K=V,K=V;K=V;..." (";" separates settings, "" = defaults),
 AB_N sets (C2-like 2 Mbp genomes), AB_BLOCKS="r0:r1 ..." row blocks (default
@@ -30,22 +30,23 @@ if os.environ.get("AB_RANKS"):
 rows = max(c - a for a, c in blocks)
 dI, dD = ctx.alloc(rows * n * 4), ctx.alloc(rows * n * 8)
 print(f"n={n} blocks={blocks}", flush=True)
+def opt_name(kv):
+    return kv[len("GDIST_"):].lower() if kv.startswith("GDIST_") else kv.lower()
+
+
 base = {}
 for kv in set(k for s in settings for k in [x.split("=")[0] for x in s.split(",") if x]):
-    base[kv] = os.environ.get(kv)
+    base[kv] = ctx.option(opt_name(kv))
 times = {s: {b: [] for b in blocks} for s in settings}
 ref = {}
 for rnd in range(rounds):
     for s in settings:
         for kv, v in base.items():
-            if v is None:
-                os.environ.pop(kv, None)
-            else:
-                os.environ[kv] = v
+            ctx.set_option(opt_name(kv), v)
         for x in s.split(","):
             if x:
                 kk, vv = x.split("=")
-                os.environ[kk] = vv
+                ctx.set_option(opt_name(kk), int(vv))
         for b in blocks:
             sets.matrix_device(dI.ptr, dD.ptr, n, b, (0, n), upper=True, method=gdist.METHOD_BITSET)
             ctx.synchronize()

@@ -17,13 +17,13 @@ check_rows = min(n, 2048)
 
 
 def apply(v):
-    os.environ.pop("GDIST_SKETCH_TILE", None)
-    os.environ.pop("GDIST_SKETCH_K", None)
+    ctx.set_option("sketch_tile", None)
+    ctx.set_option("sketch_k", None)
     for part in v.split("+"):
         if part.startswith("k"):
-            os.environ["GDIST_SKETCH_K"] = part[1:]
+            ctx.set_option("sketch_k", int(part[1:]))
         elif part.startswith("t"):
-            os.environ["GDIST_SKETCH_TILE"] = part[1:]
+            ctx.set_option("sketch_tile", int(part[1:]))
 
 
 

@@ -36,10 +36,10 @@ incs, max_list = sets.rare_stats()
 a, b = (float(x) for x in os.environ.get("CAL_ROWS", "0:1").split(":"))
 r0, r1 = int(round(a * N)), int(round(b * N))
 dI, dD = ctx.alloc((r1 - r0) * N * 4), ctx.alloc((r1 - r0) * N * 8)
-os.environ["GDIST_RARE_OVERLAP"] = "0"
+ctx.set_option("rare_overlap", 0)
 ms = {}
 for kern in ("0", "1"):
-    os.environ["GDIST_RARE_KERNEL"] = kern
+    ctx.set_option("rare_kernel", int(kern))
     for _ in range(4):
         sets.matrix_device(dI.ptr, dD.ptr, N, (r0, r1), (0, N), upper=True, method=gdist.METHOD_BITSET)
     ctx.synchronize()

@@ -32,10 +32,7 @@ max_rows = max(bounds[k + 1] - bounds[k] for k in range(G))      # the last rank
 dI, dD = ctx.alloc(max_rows * N * 4), ctx.alloc(max_rows * N * 8)
 print(f"row blocks {bounds} (max {max_rows} rows; buffers {max_rows * N * 12 / 1e9:.2f} GB)", flush=True)
 for kern in os.environ.get("EMU_KERNELS", ",0,1").split(","):   # "" = the model's per-block choice
-    if kern:
-        os.environ["GDIST_RARE_KERNEL"] = kern
-    else:
-        os.environ.pop("GDIST_RARE_KERNEL", None)
+    ctx.set_option("rare_kernel", int(kern) if kern else None)
     times = []
     for rk in range(G):
         r0, r1 = bounds[rk], bounds[rk + 1]

@@ -24,3 +24,19 @@ def pytest_configure(config):
 def ctx():
     import gdist
     return gdist.Context.default(0)
+
+
+@pytest.fixture
+def opts(ctx):
+    """opts(name=value, ...) sets tuning options of the shared context
+    (gdist_ctx_set_option) for one test; they are restored at teardown."""
+    old = {}
+
+    def set_(**kw):
+        for k, v in kw.items():
+            if k not in old:
+                old[k] = ctx.option(k)
+            ctx.set_option(k, v)
+    yield set_
+    for k, v in old.items():
+        ctx.set_option(k, v)

@@ -1,0 +1,65 @@
+"""Tuning options live in the context (gdist_ctx_set_option), never in the
+environment: a JNI host with a different environment runs the same kernels
+(callers sharing one context, MethodTableProcessor.java:275)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def test_option_roundtrip_and_errors(ctx):
+    import gdist
+    names = gdist.option_names()
+    for n in ("rare_t", "rare_kernel", "bitset_kernel", "sparse", "sparse_zmax", "sketch_k", "reps_block",
+              "locus_order", "guides", "sparse_part_budget"):
+        assert n in names
+    c = gdist.Context(0)
+    try:
+        assert c.option("sparse") is None
+        c.set_option("sparse", 0)
+        assert c.option("sparse") == 0
+        with c.options(sparse=1, rare_t=7):
+            assert c.option("sparse") == 1 and c.option("rare_t") == 7
+        assert c.option("sparse") == 0 and c.option("rare_t") is None
+        c.set_option("sparse", None)
+        assert c.option("sparse") is None
+        with pytest.raises(ValueError):
+            c.set_option("no_such_option", 1)
+    finally:
+        c.close()
+
+
+def test_environment_does_not_change_kernels(monkeypatch):
+    """GDIST_* variables in the process environment are ignored by the
+    library: the sparse split and the rare threshold follow the context."""
+    import gdist
+    from gdist import synth
+    seqs = [bytes(r) for r in synth.genomes(160, 20000, 0.003, 7)]
+    monkeypatch.setenv("GDIST_SPARSE", "0")
+    monkeypatch.setenv("GDIST_RARE_T", "3")
+    c = gdist.Context(0)
+    try:
+        a = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, c)
+        a.build_bitsets()
+        t_env = a.rare_info()[0]
+        monkeypatch.delenv("GDIST_RARE_T")
+        a.build_bitsets()
+        assert a.rare_info()[0] == t_env, "GDIST_RARE_T in the environment must not change T"
+        monkeypatch.setenv("GDIST_RARE_T", "3")
+        c.set_option("sparse_zmax", 100000)           # force the split through the context
+        b = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, c)
+        b.build_bitsets()
+        assert b.sparse_info()[0] > 0, "GDIST_SPARSE=0 in the environment must not switch the split off"
+        c.set_option("sparse", 0)
+        d = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, c)
+        d.build_bitsets()
+        assert d.sparse_info()[0] == 0
+        c.set_option("rare_t", 5)
+        d.build_bitsets()
+        assert d.rare_info()[0] == 5
+        I1, _ = b.matrix(upper=True, method=gdist.METHOD_BITSET)
+        I2, _ = d.matrix(upper=True, method=gdist.METHOD_BITSET)
+        iu = np.triu_indices(len(seqs), 1)
+        assert np.array_equal(I1[iu], I2[iu])
+    finally:
+        c.close()

@@ -380,14 +380,14 @@ def test_genome_and_reps_processors(ctx):
 
 
 @pytest.mark.parametrize("block", [None, "100", "37"])
-def test_greedy_reps_device(ctx, block, monkeypatch):
+def test_greedy_reps_device(ctx, block, opts):
     """gdist_greedy_reps: pass 1 equals the sequential loop of row queries
     (DistanceRepsProcessor.java:185-200) for one block and several; pass 2
     equals the argmin over representatives of the exact distances, ties to
     the lowest tie rank, on a collection with duplicated genomes (exact ties)."""
     import gdist
     if block:
-        monkeypatch.setenv("GDIST_REPS_BLOCK", block)
+        opts(reps_block=int(block))
     base = synth_sets(150, 3000, 0.15, 109)
     seqs = base + [base[i] for i in (3, 17, 40, 41, 99)]           # duplicates -> ties
     n = len(seqs)
@@ -469,13 +469,13 @@ def test_bitset_row_blocks_like_ranks(ctx):
         assert bits_equal(D[up], eD[r0:r1, c0:c1][up]), (r0, r1, c0, c1)
 
 
-def test_bitset_partial_row_tiles(ctx, monkeypatch):
+def test_bitset_partial_row_tiles(ctx, opts):
     """A block whose last row tile holds 1..127 rows runs it through the
     launches instantiated for RR = ceil(rows / 16) accumulator rows: every RR
     (1..7, RR = 7 enabled here) and its boundaries, upper (diagonal +
     off-diagonal partial tiles) and full rectangles, exact against the oracle."""
     import gdist
-    monkeypatch.setenv("GDIST_BITSET_PARTIAL_RR", "7")
+    opts(bitset_partial_rr=7)
     n = 420
     seqs = synth_sets(n, 2500, 0.01, 113)
     sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
@@ -525,15 +525,14 @@ def test_k32_all_ones_code(ctx, strand):
 @pytest.mark.parametrize("dedup", ["1", "0"])
 @pytest.mark.parametrize("kernel", ["0", "1"])
 @pytest.mark.parametrize("T", [0, 3, 8, 1000])
-def test_rare_tier_thresholds_exact(ctx, T, kernel, dedup, monkeypatch):
+def test_rare_tier_thresholds_exact(ctx, T, kernel, dedup, opts):
     """Dense-only (T=0), mixed, and all-rare (T > N) dictionaries give the
     same bit-exact counts and distances as the oracle, through the list-major
     (0) and the row-major (1) rare kernel, with identical posting lists merged
     into weighted lists (1) or one list per kmer (0). T > N puts lists of up
     to N members in the rare tier: the wave-cooperative long-list walks."""
     import gdist
-    monkeypatch.setenv("GDIST_RARE_KERNEL", kernel)
-    monkeypatch.setenv("GDIST_RARE_DEDUP", dedup)
+    opts(rare_kernel=int(kernel), rare_dedup=int(dedup))
     n = 200
     seqs = synth_sets(n, 6000, 0.01, 101)
     sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
@@ -571,17 +570,16 @@ def test_rare_tier_thresholds_exact(ctx, T, kernel, dedup, monkeypatch):
 
 
 @pytest.mark.parametrize("mode", ["auto", "all_sparse", "mixed", "no_locus", "off"])
-def test_sparse_complement_words_exact(ctx, mode, monkeypatch):
+def test_sparse_complement_words_exact(ctx, mode, opts):
     """The dense tier in locus order with complement-sparse words: counts and
     distances are bit-exact against the oracle over upper triangles,
     rectangles, unaligned row blocks (as ranks get them) and row queries,
     whether every word is sparse, words are split between the sparse kernel
     and the tiles, the locus order is off (code order), or the split is off."""
     import gdist
-    env = {"all_sparse": {"GDIST_SPARSE_ZMAX": "100000"}, "mixed": {"GDIST_SPARSE_ZMAX": "12"},
-           "no_locus": {"GDIST_LOCUS_ORDER": "0", "GDIST_SPARSE_ZMAX": "40"}, "off": {"GDIST_SPARSE": "0"}}
-    for k, v in env.get(mode, {}).items():
-        monkeypatch.setenv(k, v)
+    settings = {"all_sparse": {"sparse_zmax": 100000}, "mixed": {"sparse_zmax": 12},
+                "no_locus": {"locus_order": 0, "sparse_zmax": 40}, "off": {"sparse": 0}}
+    opts(**settings.get(mode, {}))
     n = 300
     seqs = synth_sets(n, 20000, 0.003, 105)
     sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
@@ -609,7 +607,7 @@ def test_sparse_complement_words_exact(ctx, mode, monkeypatch):
     assert bits_equal(d, eD[0, cols])
 
 
-def test_sparse_equals_dense_at_size(ctx, monkeypatch):
+def test_sparse_equals_dense_at_size(ctx, opts):
     """C2-shaped collection (shared core, sparse substitutions): the whole
     triangle through the complement-sparse words equals the plain AND+popcount
     tiles pair for pair, and the oracle on a corner block; row-sharded blocks
@@ -622,14 +620,14 @@ def test_sparse_equals_dense_at_size(ctx, monkeypatch):
     ws, wd, ent = sp.sparse_info()
     assert ws > 0 and ent > 0
     I, D = sp.matrix(upper=True, method=gdist.METHOD_BITSET)
-    monkeypatch.setenv("GDIST_SPARSE", "0")
+    opts(sparse=0)
     de = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
     de.build_bitsets()
     assert de.sparse_info()[0] == 0
     eI, eD = de.matrix(upper=True, method=gdist.METHOD_BITSET)
     iu = np.triu_indices(n, 1)
     assert np.array_equal(I[iu], eI[iu]) and bits_equal(D[iu], eD[iu])
-    monkeypatch.delenv("GDIST_SPARSE")
+    opts(sparse=None)
     for (r0, r1) in [(0, 77), (77, 200), (200, 331), (331, 420)]:
         Ib, _ = sp.matrix((r0, r1), (0, n), upper=True, method=gdist.METHOD_BITSET)
         mask = np.fromfunction(lambda a, b: b > (r0 + a), (r1 - r0, n))
