@@ -24,7 +24,7 @@ const char* const kOptNames[OPT_COUNT] = {
     "bitset_kernel",   "bitset_diag",     "bitset_partial_rr", "bitset_wg_per_cu", "bitset_min_chunks",
     "reps_block",      "locus_order",     "sparse",          "sparse_zmax",     "sparse_wg_per_cu",
     "sparse_occ",      "sparse_sun",      "sketch_k",        "sketch_tile",     "sparse_part_budget",
-    "guides",
+    "guides",          "force_exchange",
 };
 
 static int option_index(const char* name) {
@@ -240,6 +240,7 @@ int gdist_ctx_destroy(gdist_ctx* ctx) {
 int gdist_ctx_synchronize(gdist_ctx* ctx) {
     return guard([&] {
         use_device(ctx);
+        std::lock_guard<std::recursive_mutex> lk_(ctx->mu);
         GD_HIP(hipStreamSynchronize(ctx->stream));
     });
 }
@@ -284,6 +285,7 @@ int gdist_ctx_last_timing(gdist_ctx* ctx, double* kernel_ms, double* call_ms, in
 int gdist_dev_alloc(gdist_ctx* ctx, int64_t bytes, void** dptr) {
     return guard([&] {
         use_device(ctx);
+        std::lock_guard<std::recursive_mutex> lk_(ctx->mu);
         GD_REQUIRE(dptr && bytes >= 0, "bad allocation request");
         *dptr = nullptr;
         if (bytes) GD_HIP(hipMalloc(dptr, (size_t)bytes));
@@ -293,6 +295,7 @@ int gdist_dev_alloc(gdist_ctx* ctx, int64_t bytes, void** dptr) {
 int gdist_dev_free(gdist_ctx* ctx, void* dptr) {
     return guard([&] {
         use_device(ctx);
+        std::lock_guard<std::recursive_mutex> lk_(ctx->mu);
         GD_HIP(hipStreamSynchronize(ctx->stream));
         if (dptr) GD_HIP(hipFree(dptr));
     });
@@ -301,6 +304,7 @@ int gdist_dev_free(gdist_ctx* ctx, void* dptr) {
 int gdist_memcpy_d2h(gdist_ctx* ctx, void* dst, const void* src, int64_t bytes) {
     return guard([&] {
         use_device(ctx);
+        std::lock_guard<std::recursive_mutex> lk_(ctx->mu);
         if (bytes <= 0) return;
         d2h(dst, src, (size_t)bytes, ctx->stream);
         GD_HIP(hipStreamSynchronize(ctx->stream));
@@ -310,6 +314,7 @@ int gdist_memcpy_d2h(gdist_ctx* ctx, void* dst, const void* src, int64_t bytes) 
 int gdist_memcpy_h2d(gdist_ctx* ctx, void* dst, const void* src, int64_t bytes) {
     return guard([&] {
         use_device(ctx);
+        std::lock_guard<std::recursive_mutex> lk_(ctx->mu);
         if (bytes <= 0) return;
         h2d(dst, src, (size_t)bytes, ctx->stream);
         GD_HIP(hipStreamSynchronize(ctx->stream));
@@ -429,6 +434,7 @@ int gdist_sets_download(const gdist_sets* s, int64_t* offsets, uint64_t* codes) 
         check_sets(s);
         GD_REQUIRE(s->kind != GDIST_SKETCH, "use gdist_sketch_download for sketches");
         use_device(s->ctx);
+        std::lock_guard<std::recursive_mutex> lk_(s->ctx->mu);
         if (offsets) std::memcpy(offsets, s->h_off.data(), (s->nsets + 1) * 8);
         if (codes && s->total)
             d2h(codes, s->codes.p, s->total * 8, s->ctx->stream);
@@ -495,6 +501,7 @@ int gdist_sets_bitset_download(const gdist_sets* s, uint64_t* bits) {
         GD_REQUIRE(s->bits.p, "no bitsets built");
         GD_REQUIRE(bits, "null output");
         use_device(s->ctx);
+        std::lock_guard<std::recursive_mutex> lk_(s->ctx->mu);
         d2h(bits, s->bits.p, (size_t)s->nsets * s->W * 8, s->ctx->stream);
         GD_HIP(hipStreamSynchronize(s->ctx->stream));
     });
@@ -579,6 +586,7 @@ int gdist_sets_prepare(gdist_ctx* ctx, gdist_sets* sets, int method, double pair
                        double* cost_bitset_s, double* cost_sorted_s) {
     return guard([&] {
         use_device(ctx);
+        std::lock_guard<std::recursive_mutex> lk_(ctx->mu);
         check_sets(sets);
         GD_REQUIRE(sets->ctx == ctx, "sets belong to another context");
         GD_REQUIRE(sets->kind != GDIST_SKETCH, "sketch collections have one method");
@@ -656,6 +664,7 @@ int gdist_intersect_matrix(gdist_ctx* ctx, const gdist_sets* sets, int64_t r0, i
                            int method, unsigned flags, int32_t* I_out, double* D_out, int64_t ld) {
     return guard([&] {
         use_device(ctx);
+        std::lock_guard<std::recursive_mutex> lk_(ctx->mu);
         check_sets(sets);
         GD_REQUIRE(sets->ctx == ctx, "sets belong to another context");
         GD_REQUIRE(sets->kind != GDIST_SKETCH, "use gdist_sketch_matrix for sketches");
@@ -709,6 +718,7 @@ int gdist_greedy_reps(gdist_ctx* ctx, const gdist_sets* sets, int method, double
                       int32_t* is_rep, int64_t* rep_of, double* rep_dist, int64_t* nreps) {
     return guard([&] {
         use_device(ctx);
+        std::lock_guard<std::recursive_mutex> lk_(ctx->mu);
         check_sets(sets);
         GD_REQUIRE(sets->ctx == ctx, "sets belong to another context");
         GD_REQUIRE(sets->kind != GDIST_SKETCH, "representatives are chosen on kmer sets");
@@ -727,6 +737,7 @@ int gdist_row_query(gdist_ctx* ctx, const gdist_sets* sets, int64_t q, const int
                     double t, double* D_out, int32_t* hit, int64_t* best_idx, double* best_d) {
     return guard([&] {
         use_device(ctx);
+        std::lock_guard<std::recursive_mutex> lk_(ctx->mu);
         check_sets(sets);
         GD_REQUIRE(sets->ctx == ctx, "sets belong to another context");
         GD_REQUIRE(sets->kind != GDIST_SKETCH, "row queries run on kmer sets");
@@ -775,6 +786,7 @@ int gdist_row_query(gdist_ctx* ctx, const gdist_sets* sets, int64_t q, const int
 int gdist_sketch_build(gdist_ctx* ctx, const gdist_sets* sets, int width, gdist_sets** out) {
     return guard([&] {
         use_device(ctx);
+        std::lock_guard<std::recursive_mutex> lk_(ctx->mu);
         check_sets(sets);
         GD_REQUIRE(out, "null output");
         *out = nullptr;
@@ -795,6 +807,7 @@ int gdist_sketch_upload(gdist_ctx* ctx, int width, int64_t nsets, const int64_t*
                         gdist_sets** out) {
     return guard([&] {
         use_device(ctx);
+        std::lock_guard<std::recursive_mutex> lk_(ctx->mu);
         GD_REQUIRE(out && nsets >= 0 && offsets && width > 0, "bad sketch upload arguments");
         *out = nullptr;
         GD_REQUIRE(offsets[0] == 0, "offsets[0] must be 0");
@@ -823,6 +836,7 @@ int gdist_sketch_download(const gdist_sets* sk, int64_t* offsets, int32_t* sigs)
         check_sets(sk);
         GD_REQUIRE(sk->kind == GDIST_SKETCH, "not a sketch collection");
         use_device(sk->ctx);
+        std::lock_guard<std::recursive_mutex> lk_(sk->ctx->mu);
         if (offsets) std::memcpy(offsets, sk->h_off.data(), (sk->nsets + 1) * 8);
         if (sigs && sk->total)
             d2h(sigs, sk->codes.p, sk->total * 4, sk->ctx->stream);
@@ -834,6 +848,7 @@ int gdist_sketch_matrix(gdist_ctx* ctx, const gdist_sets* sk, int64_t r0, int64_
                         unsigned flags, int32_t* common_out, double* D_out, int64_t ld) {
     return guard([&] {
         use_device(ctx);
+        std::lock_guard<std::recursive_mutex> lk_(ctx->mu);
         check_sets(sk);
         GD_REQUIRE(sk->ctx == ctx, "sketches belong to another context");
         GD_REQUIRE(sk->kind == GDIST_SKETCH, "not a sketch collection");
@@ -885,6 +900,7 @@ int gdist_comm_unique_id(char id[GDIST_UNIQUE_ID_BYTES]) {
 int gdist_comm_init(gdist_ctx* ctx, const char id[GDIST_UNIQUE_ID_BYTES], int nranks, int rank) {
     return guard([&] {
         use_device(ctx);
+        std::lock_guard<std::recursive_mutex> lk_(ctx->mu);
         GD_REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank / world size");
         ncclUniqueId u;
         std::memcpy(&u, id, sizeof(u));
@@ -899,6 +915,7 @@ int gdist_comm_init(gdist_ctx* ctx, const char id[GDIST_UNIQUE_ID_BYTES], int nr
 int gdist_comm_init_host(gdist_ctx* ctx, int nranks, int rank, gdist_allgather_fn fn, void* user) {
     return guard([&] {
         use_device(ctx);
+        std::lock_guard<std::recursive_mutex> lk_(ctx->mu);
         GD_REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank / world size");
         GD_REQUIRE(fn != nullptr, "null all-gather callback");
         if (ctx->comm) { (void)ncclCommDestroy(ctx->comm); ctx->comm = nullptr; }
@@ -912,6 +929,7 @@ int gdist_comm_init_host(gdist_ctx* ctx, int nranks, int rank, gdist_allgather_f
 int gdist_comm_destroy(gdist_ctx* ctx) {
     return guard([&] {
         use_device(ctx);
+        std::lock_guard<std::recursive_mutex> lk_(ctx->mu);
         if (ctx->comm) GD_NCCL(ncclCommDestroy(ctx->comm));
         ctx->comm = nullptr;
         ctx->host_ag = nullptr;
@@ -924,6 +942,7 @@ int gdist_comm_destroy(gdist_ctx* ctx) {
 int gdist_sets_allgather(gdist_ctx* ctx, const gdist_sets* local, gdist_sets** out) {
     return guard([&] {
         use_device(ctx);
+        std::lock_guard<std::recursive_mutex> lk_(ctx->mu);
         check_sets(local);
         GD_REQUIRE(out, "null output");
         if (!has_comm(ctx)) throw ::gdist::Error(GDIST_ECOMM, "communicator not initialised (gdist_comm_init)");
@@ -977,12 +996,17 @@ int gdist_sets_allgather(gdist_ctx* ctx, const gdist_sets* local, gdist_sets** o
 int gdist_sets_allgather_bitsets(gdist_ctx* ctx, const gdist_sets* local, unsigned flags, gdist_sets** out) {
     return guard([&] {
         use_device(ctx);
+        std::lock_guard<std::recursive_mutex> lk_(ctx->mu);
         check_sets(local);
         GD_REQUIRE(out, "null output");
         GD_REQUIRE(local->kind != GDIST_SKETCH && local->has_codes, "local kmer sets with codes required");
         std::lock_guard<std::recursive_mutex> lk(ctx->mu);
         hipStream_t st = ctx->stream;
         const int R = has_comm(ctx) ? ctx->nranks : 1;
+        // every exchange runs when there are peers, or on a one-rank
+        // communicator with option force_exchange (runs the RCCL calls on a
+        // one-GPU box; the result must equal the local build)
+        const bool xchg = R > 1 || (has_comm(ctx) && ctx->option(OPT_FORCE_EXCHANGE, 0) != 0);
         const bool keep = (flags & GDIST_BITSET_KEEP_SINGLETONS) != 0;
         // 1. local dictionary summary
         Summary sum;
@@ -990,7 +1014,7 @@ int gdist_sets_allgather_bitsets(gdist_ctx* ctx, const gdist_sets* local, unsign
         // 2. every rank's (nsets, summary length)
         std::vector<int64_t> hall(2 * R);
         hall[0] = local->nsets; hall[1] = sum.n;
-        if (R > 1) {
+        if (xchg) {
             DevBuf mine(16, st), all(16 * R, st);
             h2d(mine.p, hall.data(), 16, st);
             allgather(ctx, mine.p, all.p, 16);
@@ -1002,7 +1026,7 @@ int gdist_sets_allgather_bitsets(gdist_ctx* ctx, const gdist_sets* local, unsign
         // 3. all-gather the summaries (padded), merge into the global dictionary
         DevBuf gc, gn;
         std::vector<SummaryView> parts;
-        if (R > 1) {
+        if (xchg) {
             DevBuf sc(mxn * 8 + 8, st), sn(mxn * 4 + 4, st);
             if (sum.n) {
                 GD_HIP(hipMemcpyAsync(sc.p, sum.codes.p, sum.n * 8, hipMemcpyDeviceToDevice, st));
@@ -1026,7 +1050,7 @@ int gdist_sets_allgather_bitsets(gdist_ctx* ctx, const gdist_sets* local, unsign
         const int64_t W = bitset_words(U);
         // 4. local bitsets (padded to the largest shard) + local rare-tier records
         int64_t id_base = 0;
-        for (int r = 0; r < ctx->rank && R > 1; r++) id_base += hall[2 * r];
+        for (int r = 0; r < ctx->rank && xchg; r++) id_base += hall[2 * r];
         const int64_t cap = local_rare_mass(ctx, sum, rare.as<uint64_t>(), Ur);
         // locus order of the dense ranks: every rank keys them by its own
         // guides (tagged with the rank, so rank 0's guides come first), one
@@ -1035,7 +1059,7 @@ int gdist_sets_allgather_bitsets(gdist_ctx* ctx, const gdist_sets* local, unsign
         if (locus_order_enabled(ctx)) {
             DevBuf key;
             locus_keys(ctx, local, dict.as<uint64_t>(), U, (uint64_t)ctx->rank << 40, key);
-            if (R > 1) {
+            if (xchg) {
                 DevBuf allk((U * 8 + 8) * R, st);
                 allgather(ctx, key.p, allk.p, U * 8 + 8);
                 locus_keys_min(ctx, allk.as<uint64_t>(), U, U + 1, R, key);
@@ -1051,7 +1075,7 @@ int gdist_sets_allgather_bitsets(gdist_ctx* ctx, const gdist_sets* local, unsign
         s->ctx = ctx; s->kind = local->kind; s->k = local->k; s->flags = local->flags;
         s->nsets = N; s->has_codes = false;
         s->bits.alloc((size_t)N * W * 8 + 8, st);
-        if (R > 1) {
+        if (xchg) {
             DevBuf gb((size_t)mxs * W * 8 * R + 8, st);
             allgather(ctx, lb.p, gb.p, (size_t)mxs * W * 8);
             int64_t at = 0;
@@ -1068,7 +1092,7 @@ int gdist_sets_allgather_bitsets(gdist_ctx* ctx, const gdist_sets* local, unsign
         // 5. set sizes of all ranks (one all-gather of the padded size arrays)
         std::vector<int64_t> sizes(mxs + 1, 0), allsz((mxs + 1) * R, 0);
         for (int64_t i = 0; i < local->nsets; i++) sizes[i] = local->h_off[i + 1] - local->h_off[i];
-        if (R > 1) {
+        if (xchg) {
             DevBuf ds((mxs + 1) * 8, st), da((mxs + 1) * 8 * R, st);
             h2d(ds.p, sizes.data(), (mxs + 1) * 8, st);
             allgather(ctx, ds.p, da.p, (mxs + 1) * 8);
@@ -1089,7 +1113,7 @@ int gdist_sets_allgather_bitsets(gdist_ctx* ctx, const gdist_sets* local, unsign
         std::vector<int64_t> wr(R, 0);
         wr[0] = written;
         int64_t mxw = written, totw = written;
-        if (R > 1) {
+        if (xchg) {
             DevBuf mw(8, st), aw(8 * R, st);
             h2d(mw.p, &written, 8, st);
             allgather(ctx, mw.p, aw.p, 8);
@@ -1121,6 +1145,7 @@ int gdist_sets_allgather_bitsets(gdist_ctx* ctx, const gdist_sets* local, unsign
 int gdist_comm_allreduce_max(gdist_ctx* ctx, double* value) {
     return guard([&] {
         use_device(ctx);
+        std::lock_guard<std::recursive_mutex> lk_(ctx->mu);
         GD_REQUIRE(value, "null value");
         if (!has_comm(ctx)) return;
         DevBuf d(8, ctx->stream), all(8 * ctx->nranks, ctx->stream);

@@ -173,6 +173,7 @@ enum Opt : int {
     OPT_SKETCH_TILE,        // 16: force the 16x16 sketch tile
     OPT_SPARSE_PART_BUDGET, // bytes of sparse chunk partials one region may hold
     OPT_GUIDES,             // guide sequences keyed at pack time (default kGuides)
+    OPT_FORCE_EXCHANGE,     // 1: a one-rank communicator runs every collective (tests)
     OPT_COUNT
 };
 extern const char* const kOptNames[OPT_COUNT];

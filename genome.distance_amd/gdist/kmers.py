@@ -18,6 +18,7 @@ import contextlib
 import ctypes as C
 import enum
 import os
+import weakref
 from typing import Iterable, Mapping, Sequence
 
 import numpy as np
@@ -59,6 +60,7 @@ class Context:
         L.check(L.lib.gdist_ctx_create(device, C.byref(h)))
         self.h = h
         self.device = device
+        self._handles = weakref.WeakSet()     # live collections: freed before the context
         for k, v in (options or {}).items():
             self.set_option(k, v)
 
@@ -91,7 +93,11 @@ class Context:
         return cls._defaults[device]
 
     def close(self):
+        """gdist_ctx_destroy, after freeing every collection still alive on it
+        (a collection must not outlive its context)."""
         if self.h:
+            for hd in list(self._handles):
+                hd.free()
             L.lib.gdist_ctx_destroy(self.h)
             self.h = None
 
@@ -150,6 +156,7 @@ class DeviceBuffer:
         p = C.c_void_p()
         L.check(L.lib.gdist_dev_alloc(ctx.h, int(nbytes), C.byref(p)))
         self.ctx, self.ptr, self.nbytes = ctx, p.value or 0, int(nbytes)
+        ctx._handles.add(self)
 
     def to_host(self, dtype, count: int | None = None, offset: int = 0) -> np.ndarray:
         """`count` elements of `dtype` starting at element `offset`."""
@@ -206,6 +213,7 @@ def _as_bytes(s) -> bytes:
 class _Handle:
     def __init__(self, ctx: Context, h: C.c_void_p):
         self.ctx, self.h = ctx, h
+        ctx._handles.add(self)
 
     def free(self):
         if getattr(self, "h", None):

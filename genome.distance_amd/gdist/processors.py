@@ -33,10 +33,14 @@ class ParseFailureException(ValueError):
 
 @dataclasses.dataclass
 class Genome:
-    """The part of org.theseed.genome.Genome the distance path reads."""
+    """The part of org.theseed.genome.Genome the distance path reads: contig
+    DNA (GenomeKmers), protein sequences (ProteinKmers, the `prot` method)
+    and the taxonomic lineage rank -> taxon (TaxonDistanceMethod)."""
     id: str
     name: str
     contigs: list[str]
+    proteins: list[str] = dataclasses.field(default_factory=list)
+    lineage: dict = dataclasses.field(default_factory=dict)
 
     def kmer_text(self) -> bytes:
         # contigs joined by the 0x00 separator: one set, no kmer spans contigs

@@ -1,8 +1,17 @@
 """Worker of tests/test_multirank_gpu.py, one process per rank (launched by
 torch.distributed.run, gloo): the row-sharded multi-rank path on ranks that
-share one GPU through the host-staged transport. Each rank packs its shard,
-all-gathers (bitsets and plain sets), computes its triangle rows, and rank 0
-compares every rank's rows with a single-process matrix over all sets."""
+share one GPU through the host-staged transport. For every case each rank
+packs its shard, all-gathers (bitsets, plain sets, sketches), computes its
+triangle rows, and rank 0 compares every rank's rows bit-exactly with the CPU
+oracle over all sets.
+
+Cases:
+  base    301 x 6 kbp, p 0.01: bitset, sorted and sketch (C5's exchange) legs
+  sparse  C2-shaped (shared core, p <= 0.002): the complement-sparse words
+          must be active on every rank, so the rank-tagged locus keys are
+          all-gathered and min-reduced (gdist_sets_allgather_bitsets)
+  c4      C4-shaped (100 kbp, p <= 0.05, DNA k=21) at small N, METHOD_AUTO
+"""
 import os
 import sys
 
@@ -12,14 +21,78 @@ import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "genome.distance_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
 import gdist  # noqa: E402
+import oracle  # noqa: E402  (test infrastructure: the checker)
 from gdist import shard, synth  # noqa: E402
+
+CASES = {
+    "base": dict(n=301, L=6000, p=0.01, cfg=11, legs=("bitset", "sorted", "sketch")),
+    "sparse": dict(n=300, L=150_000, p=0.002, cfg=12, legs=("bitset",), sparse=True),
+    "c4": dict(n=200, L=100_000, p=0.05, cfg=4, legs=("auto", "sorted")),
+}
+SKETCH_W = 200
+
+
+def run_case(name, c, ctx, rank, world):
+    n = c["n"]
+    seqs = [bytes(r) for r in synth.genomes(n, c["L"], c["p"], c["cfg"])]
+    s0, s1 = shard.shard_of_sets(n, world)[rank]
+    local = gdist.KmerSets.from_sequences(seqs[s0:s1], 21, gdist.KmerType.DNA, 0, ctx)
+    bounds = shard.triangle_bounds(n, world, 16)
+    r0, r1 = bounds[rank], bounds[rank + 1]
+    results = {}
+    info = {}
+    for leg in c["legs"]:
+        if leg in ("bitset", "auto"):
+            gb = local.allgather_bitsets()
+            assert len(gb) == n
+            if c.get("sparse"):
+                ws, wd, ent = gb.sparse_info()
+                assert ws > 0 and ent > 0, f"rank {rank}: complement-sparse words not active"
+                info["sparse"] = (ws, wd, ent)
+            results[leg] = gb.matrix((r0, r1), (0, n), upper=True, method=gdist.METHOD_BITSET)
+        elif leg == "sorted":
+            gs = local.allgather()
+            assert len(gs) == n
+            results[leg] = gs.matrix((r0, r1), (0, n), upper=True, method=gdist.METHOD_SORTED)
+        elif leg == "sketch":
+            sk = local.sketches(SKETCH_W).allgather()
+            assert len(sk) == n
+            so, sv = sk.download()
+            results[leg] = sk.matrix((r0, r1), (0, n), upper=True)
+            info["sketch_sigs"] = [sv[so[i]:so[i + 1]].tolist() for i in range(n)]
+    gathered = [None] * world
+    dist.all_gather_object(gathered, (r0, r1, {m: (I.tolist(), D.tolist()) for m, (I, D) in results.items()},
+                                      info))
+    if rank != 0:
+        return
+    off, codes = oracle.pack(seqs, 21, 0, 0)
+    eI, eD = oracle.matrix(off, codes, 0, n, 0, n, flags=0x100, nthreads=8)
+    esk = [oracle.sketch(codes[off[i]:off[i + 1]], 21, 0, SKETCH_W) for i in range(n)] \
+        if "sketch" in c["legs"] else None
+    rows = 0
+    for (a, b, res, inf) in gathered:
+        up = np.fromfunction(lambda x, y: y > (a + x), (b - a, n))
+        for m, (I, D) in res.items():
+            I, D = np.array(I, dtype=np.int32), np.array(D, dtype=np.float64)
+            if m == "sketch":
+                assert inf["sketch_sigs"] == [s.tolist() for s in esk], (name, "sketch signatures")
+                for i in range(a, b):
+                    for j in range(i + 1, n):
+                        d, common = oracle.sketch_distance(esk[i], esk[j], SKETCH_W)
+                        assert I[i - a, j] == common and D[i - a, j] == d, (name, m, i, j)
+                continue
+            assert np.array_equal(I[up], eI[a:b][up]), (name, m, a, b)
+            assert np.array_equal(D[up].view(np.uint64), eD[a:b][up].view(np.uint64)), (name, m, a, b)
+        rows += b - a
+    assert rows == n
+    print(f"CASE_OK {name} {world} {gathered[0][3].get('sparse', '')}", flush=True)
 
 
 def main():
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
-    n, L = int(os.environ.get("MR_N", "301")), int(os.environ.get("MR_LEN", "6000"))
     ctx = gdist.Context(0)
 
     def ag(a):
@@ -30,33 +103,11 @@ def main():
 
     ctx.comm_init_host(world, rank, ag)
     assert ctx.allreduce_max(float(rank)) == float(world - 1)
-    g = synth.genomes(n, L, 0.01, 11)
-    seqs = [bytes(r) for r in g]
-    s0, s1 = shard.shard_of_sets(n, world)[rank]
-    local = gdist.KmerSets.from_sequences(seqs[s0:s1], 21, gdist.KmerType.DNA, 0, ctx)
-    bounds = shard.triangle_bounds(n, world, 16)
-    r0, r1 = bounds[rank], bounds[rank + 1]
-    results = {}
-    gb = local.allgather_bitsets()
-    assert len(gb) == n
-    results["bitset"] = gb.matrix((r0, r1), (0, n), upper=True, method=gdist.METHOD_BITSET)
-    gs = local.allgather()
-    assert len(gs) == n and np.array_equal(gs.sizes(), gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx).sizes())
-    results["sorted"] = gs.matrix((r0, r1), (0, n), upper=True, method=gdist.METHOD_SORTED)
-    gathered = [None] * world
-    dist.all_gather_object(gathered, (r0, r1, {m: (I.tolist(), D.tolist()) for m, (I, D) in results.items()}))
+    names = os.environ.get("MR_CASES", ",".join(CASES)).split(",")
+    for name in names:
+        run_case(name, CASES[name], ctx, rank, world)
+        dist.barrier()
     if rank == 0:
-        full = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
-        eI, eD = full.matrix(upper=True, method=gdist.METHOD_SORTED)
-        rows = 0
-        for (a, b, res) in gathered:
-            up = np.fromfunction(lambda x, y: y > (a + x), (b - a, n))
-            for m, (I, D) in res.items():
-                I, D = np.array(I, dtype=np.int32), np.array(D, dtype=np.float64)
-                assert np.array_equal(I[up], eI[a:b][up]), (m, a, b)
-                assert np.array_equal(D[up].view(np.uint64), eD[a:b][up].view(np.uint64)), (m, a, b)
-            rows += b - a
-        assert rows == n
         print("MULTIRANK_OK", world, flush=True)
     ctx.comm_destroy()
     dist.destroy_process_group()

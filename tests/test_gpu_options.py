@@ -62,4 +62,4 @@ def test_environment_does_not_change_kernels(monkeypatch):
         iu = np.triu_indices(len(seqs), 1)
         assert np.array_equal(I1[iu], I2[iu])
     finally:
-        c.close()
+        c.close()            # frees a, b, d first (a collection must not outlive its context)

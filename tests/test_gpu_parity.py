@@ -267,7 +267,8 @@ def test_row_queries(ctx):
     import gdist
     seqs = synth_sets(80, 3000, 0.2, 96)
     sets = gdist.KmerSets.from_sequences(seqs, 11, gdist.KmerType.DNA, 0, ctx)
-    _, D = sets.matrix(method=gdist.METHOD_SORTED)
+    off, codes = oracle_pack(seqs, 11, 0, 0)
+    _, D = oracle.matrix(off, codes, 0, 80, 0, 80)          # expectations from the CPU oracle
     cols = [5, 17, 3, 60, 22, 79]
     for use_bits in (False, True):
         if use_bits:
@@ -364,7 +365,11 @@ def test_genome_and_reps_processors(ctx):
     assert n == 20 * 10
     lines = buf.getvalue().splitlines()
     ks = [pyref.kmer_set("\0".join(g.contigs), 12) for g in gens]
-    assert lines[1] == f"g10\tg0\t{pyref.java_double_str(pyref.set_distance(ks[10], ks[0]))}"
+    # every line, in the reference's order: comparison genomes in directory
+    # order, each against every base genome (GenomeProcessor.java:119-146)
+    exp = [f"g{j}\tg{i}\t{pyref.java_double_str(pyref.set_distance(ks[j], ks[i]))}"
+           for j in range(10, 30) for i in range(10)]
+    assert lines[1:] == exp
     prefix, lst, stats = processors.distance_reps(gens, kmer_size=12, max_dist=0.5, ctx=ctx)
     assert prefix == "rep0.5000_K12"
     reps = []
@@ -392,7 +397,8 @@ def test_greedy_reps_device(ctx, block, opts):
     seqs = base + [base[i] for i in (3, 17, 40, 41, 99)]           # duplicates -> ties
     n = len(seqs)
     sets = gdist.KmerSets.from_sequences(seqs, 15, gdist.KmerType.DNA, 0, ctx)
-    _, D = sets.matrix(method=gdist.METHOD_SORTED)
+    off, codes = oracle_pack(seqs, 15, 0, 0)
+    _, D = oracle.matrix(off, codes, 0, n, 0, n)             # expectations from the CPU oracle
     for t in (0.3, 0.6):
         reps = []
         for k in range(n):
