@@ -81,6 +81,13 @@ __global__ void compact_u64_kernel(const uint64_t* __restrict__ v, const int32_t
         if (flag[i]) out[pos[i]] = v[i];
 }
 
+__global__ void compact_u32_kernel(const uint32_t* __restrict__ v, const int32_t* __restrict__ flag,
+                                   const int64_t* __restrict__ pos, int64_t n, uint32_t* __restrict__ out) {
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        if (flag[i]) out[pos[i]] = v[i];
+}
+
 __global__ void widen_u32_kernel(const uint32_t* __restrict__ in, int64_t n, int64_t* __restrict__ out) {
     int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) out[i] = in[i];
@@ -824,7 +831,7 @@ __global__ void count_hist_kernel(const uint32_t* __restrict__ cnt, int64_t n, i
 // (all codes with keep_singletons), rare = codes held by 2..T-1 sets.
 // rare_mass = number of (code, set) records the rare tier will produce.
 void dictionary_from(gdist_ctx* ctx, const std::vector<SummaryView>& parts, bool keep, int64_t& T, int64_t nsets,
-                     DevBuf& dict, int64_t& U, DevBuf& rare, int64_t& Ur, int64_t& rare_mass) {
+                     DevBuf& dict, int64_t& U, DevBuf& rare, int64_t& Ur, int64_t& rare_mass, DevBuf* dcounts) {
     hipStream_t st = ctx->stream;
     Summary all;
     SummaryView m = parts.size() == 1 ? parts[0] : SummaryView{nullptr, nullptr, 0};
@@ -875,9 +882,13 @@ void dictionary_from(gdist_ctx* ctx, const std::vector<SummaryView>& parts, bool
     }
     dict.alloc(U * 8 + 8, st);
     rare.alloc(Ur * 8 + 8, st);
+    if (dcounts) dcounts->alloc(U * 4 + 4, st);
     if (n) {
         compact_u64_kernel<<<grid_for(n), 256, 0, st>>>(m.codes, df.as<int32_t>(), dpos.as<int64_t>(), n,
                                                         dict.as<uint64_t>());
+        if (dcounts)
+            compact_u32_kernel<<<grid_for(n), 256, 0, st>>>(m.counts, df.as<int32_t>(), dpos.as<int64_t>(), n,
+                                                            dcounts->as<uint32_t>());
         compact_u64_kernel<<<grid_for(n), 256, 0, st>>>(m.codes, rf.as<int32_t>(), rpos.as<int64_t>(), n,
                                                         rare.as<uint64_t>());
         GD_HIP(hipGetLastError());
@@ -1258,16 +1269,16 @@ void build_bitsets(gdist_ctx* ctx, gdist_sets* s, unsigned flags, int64_t rare_t
     Summary sum;
     local_summary(ctx, s, sum);
     tr.mark("bitsets: summary");
-    DevBuf dict, rare;
+    DevBuf dict, rare, dcnt;
     int64_t U = 0, Ur = 0, mass = 0;
     dictionary_from(ctx, {SummaryView{sum.codes.as<uint64_t>(), sum.counts.as<uint32_t>(), sum.n}}, keep, T, s->nsets,
-                    dict, U, rare, Ur, mass);
+                    dict, U, rare, Ur, mass, &dcnt);
     tr.mark("bitsets: dictionary");
     const int64_t W = bitset_words(U);
     DevBuf perm;
     if (s->n_guide > 0 && locus_order_enabled(ctx)) {
         DevBuf key;
-        locus_keys(ctx, s, dict.as<uint64_t>(), U, 0, key);
+        locus_keys(ctx, s, dict.as<uint64_t>(), dcnt.as<uint32_t>(), U, 0, key);
         locus_perm(ctx, key, U, perm);
         tr.mark("bitsets: locus order");
     }
@@ -1349,7 +1360,7 @@ double bitset_block_cost_s(const gdist_sets* s, int64_t r0, int64_t r1, int64_t 
     if (rare_row_major) *rare_row_major = rc.row_major;
     double off, diag;
     dense_tiles(r0, r1, c0, c1, upper, &off, &diag);
-    const double tW = s->sparse ? (double)s->Wd : (double)s->W;
+    const double tW = s->sparse ? (s->sp_fold_dense ? 0.0 : (double)s->Wd) : (double)s->W;
     // sparse tiles: ~ the block's pair area in 128 x 128 tiles, plus the partial ones on its row edge
     const double sp_tiles = pairs / (double)(BT * BT) + (double)ceil_div(r1 - r0, BT);
     return (off + kDiagTileShare * diag) * (double)(BT * BT) * tW / kDenseWordPairsPerS + rc.cost() +
@@ -1360,7 +1371,7 @@ double bitset_cost_s(const gdist_sets* s, double pairs) {
     // a region given only by its pair count: its share of the rows taken as its share of the pairs
     const double tot = 0.5 * (double)s->nsets * (double)(s->nsets - 1);
     const double frac = tot > 0 ? std::min(1.0, pairs / tot) : 1.0;
-    const double tW = s->sparse ? (double)s->Wd : (double)s->W;
+    const double tW = s->sparse ? (s->sp_fold_dense ? 0.0 : (double)s->Wd) : (double)s->W;
     return pairs * tW / kDenseWordPairsPerS + rare_choice(rare_tier(s), frac, frac).cost() +
            sparse_block_cost_s(s, frac, pairs / (double)(BT * BT) + std::sqrt(2.0 * pairs) / BT);
 }
@@ -1490,8 +1501,8 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
         GD_HIP(hipGetLastError());
         GD_HIP(hipEventRecord(ctx->ev_join, ctx->side));
     }
-    if (tW == 0) {
-        // no dense words: the sparse kernel holds the whole dense tier
+    if (tW == 0 || (s->sparse && s->sp_fold_dense)) {
+        // no dense words, or so few that the sparse flush counts them
     } else if (variant == 1) {
         const int64_t grid = (int64_t)p.ntiles * p.splits;
         GD_REQUIRE(grid < (int64_t(1) << 31), "bitset matrix grid too large");

@@ -24,7 +24,7 @@ const char* const kOptNames[OPT_COUNT] = {
     "bitset_kernel",   "bitset_diag",     "bitset_partial_rr", "bitset_wg_per_cu", "bitset_min_chunks",
     "reps_block",      "locus_order",     "sparse",          "sparse_zmax",     "sparse_wg_per_cu",
     "sparse_occ",      "sparse_sun",      "sketch_k",        "sketch_tile",     "sparse_part_budget",
-    "guides",          "force_exchange",
+    "guides",          "force_exchange",  "sparse_kernel",   "sparse_chunks",   "fold_dense_words", "sparse_abl",
 };
 
 static int option_index(const char* name) {
@@ -469,6 +469,14 @@ int gdist_sets_sparse_info(const gdist_sets* s, int64_t* sparse_words, int64_t* 
         if (sparse_words) *sparse_words = s->sparse ? s->Ws : 0;
         if (dense_words) *dense_words = s->sparse ? s->Wd : s->W;
         if (entries) *entries = s->sparse ? s->sp_entries : 0;
+    });
+}
+
+int gdist_sets_sparse_sides(const gdist_sets* s, int64_t* complement_words, int64_t* positive_words) {
+    return guard([&] {
+        check_sets(s);
+        if (complement_words) *complement_words = s->sparse ? s->Ws - s->sp_pos_words : 0;
+        if (positive_words) *positive_words = s->sparse ? s->sp_pos_words : 0;
     });
 }
 
@@ -1042,10 +1050,10 @@ int gdist_sets_allgather_bitsets(gdist_ctx* ctx, const gdist_sets* local, unsign
         } else {
             parts.push_back({sum.codes.as<uint64_t>(), sum.counts.as<uint32_t>(), sum.n});
         }
-        DevBuf dict, rare;
+        DevBuf dict, rare, dcnt;
         int64_t U = 0, Ur = 0, mass_all = 0;
         int64_t T = keep ? 0 : -1;                 // cost-optimal from the global count histogram
-        dictionary_from(ctx, parts, keep, T, N, dict, U, rare, Ur, mass_all);
+        dictionary_from(ctx, parts, keep, T, N, dict, U, rare, Ur, mass_all, &dcnt);
         gc.release(); gn.release();
         const int64_t W = bitset_words(U);
         // 4. local bitsets (padded to the largest shard) + local rare-tier records
@@ -1058,7 +1066,7 @@ int gdist_sets_allgather_bitsets(gdist_ctx* ctx, const gdist_sets* local, unsign
         DevBuf perm;
         if (locus_order_enabled(ctx)) {
             DevBuf key;
-            locus_keys(ctx, local, dict.as<uint64_t>(), U, (uint64_t)ctx->rank << 40, key);
+            locus_keys(ctx, local, dict.as<uint64_t>(), dcnt.as<uint32_t>(), U, (uint64_t)ctx->rank << 40, key);
             if (xchg) {
                 DevBuf allk((U * 8 + 8) * R, st);
                 allgather(ctx, key.p, allk.p, U * 8 + 8);

@@ -127,6 +127,7 @@ struct SparseScratch {
     bool ready = false;
     DevBuf tiles, part;   // tile list, per-chunk counters
     int nchunks = 0;
+    bool use_part = false;   // chunks store partials (else flush with atomics)
     int64_t ntiles = 0;
 };
 struct MatrixPlan {
@@ -174,6 +175,10 @@ enum Opt : int {
     OPT_SPARSE_PART_BUDGET, // bytes of sparse chunk partials one region may hold
     OPT_GUIDES,             // guide sequences keyed at pack time (default kGuides)
     OPT_FORCE_EXCHANGE,     // 1: a one-rank communicator runs every collective (tests)
+    OPT_SPARSE_KERNEL,      // sparse tile kernel 1 (word + byte loads, default) / 2 (LDS-staged) / 3 (16-byte records)
+    OPT_SPARSE_CHUNKS,      // chunks of the sparse words per tile (tests; default: parallelism and memory)
+    OPT_FOLD_DENSE_WORDS,   // at most this many (padded) dense words are folded into the sparse flush
+    OPT_SPARSE_ABL,         // timing ablations of the sparse kernel v2 (results wrong; never in tests)
     OPT_COUNT
 };
 extern const char* const kOptNames[OPT_COUNT];
@@ -277,8 +282,15 @@ struct gdist_sets {
     gdist::DevBuf sp_off;                 // int64 [ceil(nsets/128) * Ws + 1]: (set block, sparse word) -> entries
     gdist::DevBuf sp_word;                // uint64 [sp_entries]: complement word ~bits & valid
     gdist::DevBuf sp_set;                 // uint8 [sp_entries]: set - 128 * block
+    gdist::DevBuf sp_ent;                 // {word, set} 16-byte records [sp_entries] (v3 tile kernel)
     gdist::DevBuf sp_nc;                  // int32 [nsets]: complement bits over the sparse words
     int64_t sp_entries = 0, sp_U = 0;     // entries; valid bits of the sparse words
+    int sp_win = 0;                       // v2 kernel window (aligned sparse words), 0: v1 only
+    int64_t sp_pos_words = 0;             // sparse words counted from their set bits (positive-sparse)
+    bool sp_fold_dense = false;           // the dense words are counted in the sparse flush (no tile launch)
+    gdist::DevBuf sp_dT;                  // uint64 [Wd][nsets]: the dense words word-major, for the fold
+    std::vector<int32_t> sp_bucket_bits;  // [nsets][sp_nbk]: complement bits per set and 1024 sparse words
+    int64_t sp_nbk = 0;
     double sp_products = 0, sp_items = 0; // whole-triangle products / (tile, word) visits (cost model)
     bool auto_sorted = false;             // METHOD_AUTO measured the sorted join cheaper
     // bitset_matrix launch plans by (region, kernel switches); cleared with the bitsets
@@ -312,8 +324,10 @@ struct SummaryView {
 void local_summary(gdist_ctx* ctx, const gdist_sets* s, Summary& out);
 // T (in/out): rare-tier threshold; T < 0 picks the cost-optimal one for a
 // collection of nsets sets from the histogram of kmer counts
+// dcounts (optional): the number of sets holding each dense dictionary kmer
 void dictionary_from(gdist_ctx* ctx, const std::vector<SummaryView>& parts, bool keep, int64_t& T, int64_t nsets,
-                     DevBuf& dict, int64_t& U, DevBuf& rare, int64_t& Ur, int64_t& rare_mass);
+                     DevBuf& dict, int64_t& U, DevBuf& rare, int64_t& Ur, int64_t& rare_mass,
+                     DevBuf* dcounts = nullptr);
 int64_t bitset_words(int64_t dict_size);
 int64_t local_rare_mass(gdist_ctx* ctx, const Summary& local, const uint64_t* rare, int64_t Ur);
 int64_t auto_rare_threshold(int64_t nsets);
@@ -377,12 +391,18 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
                    int64_t c1, bool upper, int32_t* d_I, int64_t ldI);
 
 // sparse.hip — locus order of the dense dictionary, complement-sparse words
-constexpr int kGuides = 2;                       // guide sequences per packed collection
+constexpr int kGuides = 4;                       // guide sequences per packed collection
+constexpr int kSparseStageEntries = 640;         // sparse v2: entries per side a window may hold
+constexpr int kFoldDenseWords = 0;               // dense words folded into the sparse flush: off (the
+                                                 // tile launch overlaps the sparse kernel; the fold runs after it)
 constexpr double kSparseProductsPerS = 2.6e11;   // sparse tiles: complement-word products (C2)
 constexpr double kSparseItemsPerS = 6.0e10;      // sparse tiles: (tile, sparse word) visits (C2)
+constexpr double kDenseLaunchFixedS = 6.0e-5;    // a dense-word tile launch beside the sparse kernel (C2: 64 words 0.09 ms)
 bool locus_order_enabled(const gdist_ctx* ctx);  // option locus_order = 0 keeps code order (A/B)
-// key[r] = tag | guide position of dense rank r (all ones where no guide holds it)
-void locus_keys(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_t U, uint64_t tag, DevBuf& key);
+// key[r] = tag | guide position of dense rank r; kmers no guide holds sort
+// after every guide key by the number of sets holding them (dcounts)
+void locus_keys(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, const uint32_t* dcounts, int64_t U,
+                uint64_t tag, DevBuf& key);
 // key[r] = min over R ranks' keys (all[q * stride_r + r])
 void locus_keys_min(gdist_ctx* ctx, const uint64_t* all, int64_t U, int64_t stride_r, int R, DevBuf& key);
 // perm[r] = bit position of dense rank r: ascending key, ties in rank order

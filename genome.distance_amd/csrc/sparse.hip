@@ -39,6 +39,7 @@ inline int grid_for(int64_t n, int block = 256, int64_t cap = 256 * 32) {
 }
 
 constexpr int SB = 128;                  // sets per block of the sparse entry index (tile edge)
+constexpr int kBucketShift = 10;         // sparse words per complement-bit bucket: 1024
 
 // ---- locus order -------------------------------------------------------
 __global__ void locus_key_kernel(const uint64_t* __restrict__ gcodes, const uint64_t* __restrict__ gkeys, int64_t ng,
@@ -56,9 +57,14 @@ __global__ void locus_key_kernel(const uint64_t* __restrict__ gcodes, const uint
     }
 }
 
-__global__ void fill_u64_kernel(uint64_t* __restrict__ p, int64_t n, uint64_t v) {
+// kmers no guide holds: after every guide key (rank tags < 2^48), ordered by
+// the number of sets holding them, so the words they fill are homogeneous:
+// rarely held kmers (positive-sparse words) apart from commonly held ones
+// (complement-sparse words); the same on every rank (global counts)
+__global__ void unkeyed_kernel(uint64_t* __restrict__ p, const uint32_t* __restrict__ cnt, int64_t n) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = v;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        p[i] = (0xFFull << 56) | (cnt ? (uint64_t)cnt[i] : 0xFFFFFFFFull);
 }
 
 __global__ void iota_i32_kernel(int32_t* __restrict__ p, int64_t n) {
@@ -89,17 +95,24 @@ __device__ __forceinline__ unsigned long long valid_mask(int64_t w, int64_t U) {
     return 0ull;
 }
 
-// z[w] += number of sets in this block of rows whose complement word is non-zero
+// z[w] += sets of this block of rows whose complement word is non-zero,
+// zp[w] += sets whose word is non-zero
 __global__ __launch_bounds__(256) void word_z_kernel(const unsigned long long* __restrict__ bits, int64_t N, int64_t W,
-                                                     int64_t U, int64_t rows_per_block, int32_t* __restrict__ z) {
+                                                     int64_t U, int64_t rows_per_block, int32_t* __restrict__ z,
+                                                     int32_t* __restrict__ zp) {
     const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t i0 = (int64_t)blockIdx.y * rows_per_block;
     const int64_t i1 = i0 + rows_per_block < N ? i0 + rows_per_block : N;
     if (w >= W) return;
     const unsigned long long m = valid_mask(w, U);
-    int c = 0;
-    for (int64_t i = i0; i < i1; i++) c += (bits[i * W + w] & m) != m;
+    int c = 0, p = 0;
+    for (int64_t i = i0; i < i1; i++) {
+        const unsigned long long b = bits[i * W + w] & m;
+        c += b != m;
+        p += b != 0;
+    }
     if (c) atomicAdd(z + w, c);
+    if (p) atomicAdd(zp + w, p);
 }
 
 __global__ void gather_words_kernel(const unsigned long long* __restrict__ bits, int64_t W,
@@ -113,42 +126,62 @@ __global__ void gather_words_kernel(const unsigned long long* __restrict__ bits,
     }
 }
 
-// entries per (block b, sparse word s): sets of the block whose complement word is non-zero
+// the entry word of set word b: the complement (complement-sparse words) or
+// the word itself (positive-sparse words: few sets hold any of its kmers)
+__device__ __forceinline__ unsigned long long entry_word(unsigned long long b, unsigned long long m, bool pos) {
+    return pos ? (b & m) : (~b & m);
+}
+
+// entries per (block b, sparse word s): sets of the block whose entry word is non-zero
 __global__ __launch_bounds__(256) void sparse_count_kernel(const unsigned long long* __restrict__ bits, int64_t N,
                                                            int64_t W, int64_t U, const int32_t* __restrict__ sw,
-                                                           int64_t Ws, int32_t* __restrict__ cnt) {
+                                                           const uint8_t* __restrict__ spos, int64_t Ws,
+                                                           int32_t* __restrict__ cnt) {
     const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t b = blockIdx.y;
     if (s >= Ws) return;
     const int64_t w = sw[s];
+    const bool pos = spos[s] != 0;
     const unsigned long long m = valid_mask(w, U);
     const int64_t i1 = (b + 1) * SB < N ? (b + 1) * SB : N;
     int c = 0;
-    for (int64_t i = b * SB; i < i1; i++) c += (bits[i * W + w] & m) != m;
+    for (int64_t i = b * SB; i < i1; i++) c += entry_word(bits[i * W + w], m, pos) != 0;
     cnt[b * Ws + s] = c;
 }
 
 __global__ __launch_bounds__(256) void sparse_fill_kernel(const unsigned long long* __restrict__ bits, int64_t N,
                                                           int64_t W, int64_t U, const int32_t* __restrict__ sw,
+                                                          const uint8_t* __restrict__ spos,
                                                           int64_t Ws, const int64_t* __restrict__ off,
                                                           unsigned long long* __restrict__ word,
-                                                          uint8_t* __restrict__ set, int32_t* __restrict__ nc) {
+                                                          uint8_t* __restrict__ set, int32_t* __restrict__ nc,
+                                                          int32_t* __restrict__ bucket_bits, int64_t nbk) {
     const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t b = blockIdx.y;
     if (s >= Ws) return;
     const int64_t w = sw[s];
+    const bool pos = spos[s] != 0;
     const unsigned long long m = valid_mask(w, U);
     const int64_t i1 = (b + 1) * SB < N ? (b + 1) * SB : N;
     int64_t p = off[b * Ws + s];
     for (int64_t i = b * SB; i < i1; i++) {
-        const unsigned long long c = ~bits[i * W + w] & m;
+        const unsigned long long c = entry_word(bits[i * W + w], m, pos);
         if (c) {
             word[p] = c;
             set[p] = (uint8_t)(i - b * SB);
             p++;
-            atomicAdd(nc + i, (int32_t)__popcll(c));
+            if (!pos) atomicAdd(nc + i, (int32_t)__popcll(c));     // constant part: complement words only
+            atomicAdd(bucket_bits + i * nbk + (s >> kBucketShift), (int32_t)__popcll(c));
         }
     }
+}
+
+// 16-byte {complement word, set} records of the entries (E16 tile kernels)
+__global__ void sparse_records_kernel(const unsigned long long* __restrict__ word, const uint8_t* __restrict__ set,
+                                      int64_t n, ulonglong2* __restrict__ ent) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride)
+        ent[e] = make_ulonglong2(word[e], (unsigned long long)set[e]);
 }
 
 // ---- the sparse tile kernel ---------------------------------------------
@@ -176,14 +209,39 @@ constexpr int SNW = SNT / 64;
 // across lanes) land on distinct banks instead of one bank per column
 __device__ __forceinline__ int cnt_index(int a, int b) { return a * SB + ((b + a) & (SB - 1)); }
 
+// The dense words folded into the flush (a few words): their
+// AND+popcount for one pair, from the dense words stored word-major
+// [Wdp][N] (consecutive threads hold consecutive columns j: coalesced;
+// the row i is shared by the workgroup's threads; L2-resident)
+__device__ __forceinline__ int dense_pair(const unsigned long long* __restrict__ dT, int64_t Wdp, int64_t N,
+                                          int64_t i, int64_t j) {
+    int v = 0;
+    if (dT)
+        for (int64_t d = 0; d < Wdp; d++) v += __popcll(dT[d * N + i] & dT[d * N + j]);
+    return v;
+}
 
-// SUN products per lane in flight, OCC workgroups per CU
-template <int SUN, int OCC>
+__global__ void transpose_words_kernel(const unsigned long long* __restrict__ dbits, int64_t N, int64_t Wdp,
+                                       unsigned long long* __restrict__ dT) {
+    const int64_t n = N * Wdp;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
+        const int64_t d = e / N, i = e - d * N;
+        dT[e] = dbits[i * Wdp + d];
+    }
+}
+
+
+// SUN products per lane in flight, OCC workgroups per CU. E16: the entries
+// are read as 16-byte {complement word, set} records (one load per side and
+// product instead of a word load and a byte load)
+template <int SUN, int OCC, bool E16 = false>
 __global__ __launch_bounds__(SNT, OCC) void sparse_tile_kernel(
     const int64_t* __restrict__ off, const unsigned long long* __restrict__ word, const uint8_t* __restrict__ set,
+    const ulonglong2* __restrict__ ent,
     const int32_t* __restrict__ nc, int64_t Us, int64_t Ws, const int2* __restrict__ tiles, int nchunks,
     int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I, int64_t ldI,
-    int32_t* __restrict__ part) {
+    int32_t* __restrict__ part, const unsigned long long* __restrict__ dbits, int64_t Wdp, int64_t N) {
     __shared__ uint32_t cnt[SB * SB / 2];                                  // 32 KiB, 16-bit counters
     __shared__ int32_t pre[SNW][64];                    // first product of each word of the batch
     __shared__ int32_t rbeg[SNW][64], cbeg[SNW][64];   // relative to the chunk's first entries
@@ -209,6 +267,8 @@ __global__ __launch_bounds__(SNT, OCC) void sparse_tile_kernel(
     const unsigned long long* wB = word + cb0;
     const uint8_t* sA = set + ra0;
     const uint8_t* sB = set + cb0;
+    const ulonglong2* eA = ent + ra0;
+    const ulonglong2* eB = ent + cb0;
     for (int64_t base = sb + (int64_t)wv * 64; base < se; base += (int64_t)SNW * 64) {
         const int64_t s = base + lane;
         int64_t rb = ra0, cb = cb0;
@@ -281,8 +341,14 @@ __global__ __launch_bounds__(SNT, OCC) void sparse_tile_kernel(
             int sr[SUN], sc[SUN];
 #pragma unroll
             for (int u = 0; u < SUN; u++) {
-                wr[u] = wA[(uint32_t)ri[u]]; wc[u] = (diag ? wA : wB)[(uint32_t)ci[u]];
-                sr[u] = sA[(uint32_t)ri[u]]; sc[u] = (diag ? sA : sB)[(uint32_t)ci[u]];
+                if (E16) {
+                    const ulonglong2 er = eA[(uint32_t)ri[u]], ec = (diag ? eA : eB)[(uint32_t)ci[u]];
+                    wr[u] = er.x; wc[u] = ec.x;
+                    sr[u] = (int)er.y; sc[u] = (int)ec.y;
+                } else {
+                    wr[u] = wA[(uint32_t)ri[u]]; wc[u] = (diag ? wA : wB)[(uint32_t)ci[u]];
+                    sr[u] = sA[(uint32_t)ri[u]]; sc[u] = (diag ? sA : sB)[(uint32_t)ci[u]];
+                }
             }
 #pragma unroll
             for (int u = 0; u < SUN; u++) {
@@ -309,7 +375,357 @@ __global__ __launch_bounds__(SNT, OCC) void sparse_tile_kernel(
         const int a = t >> 7, b = ((t & (SB - 1)) - a) & (SB - 1);
         const int64_t i = A * SB + a, j = B * SB + b;
         if (i < r0 || i >= r1 || j < c0 || j >= c1 || (upper && j <= i)) continue;
-        const int v = (int)((cnt[t >> 1] >> ((t & 1) << 4)) & 0xFFFFu) + (int)Us - nc[i] - nc[j];
+        // the constant part once per pair: by chunk 0 (chunks flush with atomics)
+        const int v = (int)((cnt[t >> 1] >> ((t & 1) << 4)) & 0xFFFFu) +
+                      (ch == 0 ? (int)Us - nc[i] - nc[j] + dense_pair(dbits, Wdp, N, i, j) : 0);
+        if (v) atomicAdd(I + (i - r0) * ldI + (j - c0), v);
+    }
+}
+
+// ---- the LDS-staged sparse tile kernel (v2) --------------------------------
+// Same work and flattened-product walk as sparse_tile_kernel, other data
+// path. v1 loads a product's two complement words and set bytes from global
+// memory: a dependent chain of four loads whose L2/MALL latency bounds it
+// (every tile of a block row and column re-reads the chunk's entries, ~30 MB
+// per launch on C2, beyond an XCD's 4 MiB L2). v2 walks the chunk in
+// windows of `win` consecutive sparse words (aligned to multiples of win;
+// the build guarantees a window holds <= S2E entries per block, sp_win):
+//   * the window's entries (both lists, contiguous in the CSR) and offsets
+//     were loaded into registers while the previous window was walked, and
+//     are written to LDS between two barriers;
+//   * every wave prefix-sums the window's products (lane = word) and walks
+//     its eighth of them, SUN per lane in flight (ballot word search, rcp
+//     decode), reading the complement words and set bytes from LDS;
+//   * meanwhile the next window's loads are in flight.
+// A whole diagonal tile walks x < y of its one list, as v1.
+constexpr int S2T = 512;                 // threads per workgroup (8 waves)
+constexpr int S2NW = S2T / 64;
+constexpr int S2E = kSparseStageEntries;   // staged entries per side and window (<= 2 per thread)
+
+// ABL (timing ablations only, results wrong): 1 = no product walk, 2 = no
+// global fetch after the first window
+template <int SUN, int OCC, int ABL = 0>
+__global__ __launch_bounds__(S2T, OCC) void sparse_tile_kernel2(
+    const int64_t* __restrict__ off, const unsigned long long* __restrict__ word, const uint8_t* __restrict__ set,
+    const int32_t* __restrict__ nc, int64_t Us, int64_t Ws, int win, const int2* __restrict__ tiles, int nchunks,
+    int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I, int64_t ldI,
+    int32_t* __restrict__ part, const unsigned long long* __restrict__ dbits, int64_t Wdp, int64_t N) {
+    __shared__ uint32_t cnt[SB * SB / 2];                  // 32 KiB, 16-bit counters (cnt_index layout)
+    __shared__ unsigned long long wA[S2E], wB[S2E];        // 10 KiB: staged complement words
+    __shared__ uint8_t sA[S2E], sB[S2E];                   // their set bytes
+    __shared__ int16_t oA[65], oB[65];                    // window word -> first staged entry
+    __shared__ int32_t pre[S2NW][64];                      // per wave: first product of each word
+    __shared__ int16_t rbeg[S2NW][64], cbeg[S2NW][64];
+    __shared__ uint8_t ncol[S2NW][64];
+    const int tile = blockIdx.x / nchunks, ch = blockIdx.x % nchunks;
+    const int64_t A = tiles[tile].x, B = tiles[tile].y;
+    const int rlo = (int)(r0 - A * SB > 0 ? r0 - A * SB : 0);
+    const int rhi = (int)(r1 - A * SB < SB ? r1 - A * SB : SB);
+    const bool rpart = rlo > 0 || rhi < SB;
+    const bool diag = A == B && !rpart, mirror = diag && !upper;
+    for (int t = threadIdx.x; t < SB * SB / 2; t += S2T) cnt[t] = 0;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t sb = Ws * ch / nchunks, se = Ws * (ch + 1) / nchunks;
+    const int64_t* offA = off + A * Ws;
+    const int64_t* offB = off + B * Ws;
+    const unsigned long long* cw = diag ? wA : wB;
+    const uint8_t* cs = diag ? sA : sB;
+    const int16_t* co = diag ? oA : oB;
+    // registers holding the next window: offsets (threads 0..64) and two
+    // entries per side per thread
+    int64_t ra_off = 0, rb_off = 0;
+    unsigned long long ewA[2], ewB[2];
+    uint8_t esA[2], esB[2];
+    int na = 0, nb = 0, nw = 0;
+    auto fetch = [&](int64_t s0, int64_t s1) {
+        nw = (int)(s1 - s0);
+        const int64_t a0 = offA[s0], b0 = offB[s0];
+        na = (int)(offA[s1] - a0);
+        nb = diag ? 0 : (int)(offB[s1] - b0);
+        if (threadIdx.x <= nw) {
+            ra_off = offA[s0 + threadIdx.x] - a0;
+            if (!diag) rb_off = offB[s0 + threadIdx.x] - b0;
+        }
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+            const int t = threadIdx.x + e * S2T;
+            if (t < na) { ewA[e] = word[a0 + t]; esA[e] = set[a0 + t]; }
+            if (t < nb) { ewB[e] = word[b0 + t]; esB[e] = set[b0 + t]; }
+        }
+    };
+    int64_t s0 = sb;
+    int64_t s1 = std::min<int64_t>(se, (sb / win + 1) * win);
+    if (s0 < se) fetch(s0, s1);
+    while (s0 < se) {
+        __syncthreads();                               // the previous window's walk is done
+        if (threadIdx.x <= nw) {
+            oA[threadIdx.x] = (int16_t)ra_off;
+            if (!diag) oB[threadIdx.x] = (int16_t)rb_off;
+        }
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+            const int t = threadIdx.x + e * S2T;
+            if (t < na) { wA[t] = ewA[e]; sA[t] = esA[e]; }
+            if (t < nb) { wB[t] = ewB[e]; sB[t] = esB[e]; }
+        }
+        __syncthreads();
+        const int cur_nw = nw;
+        const int64_t n0 = s1, n1 = std::min<int64_t>(se, s1 + win);
+        if (n0 < se && !(ABL == 2 && s0 != sb)) fetch(n0, n1);   // in flight during the walk
+        // every wave: the window's products, lane = word
+        int P = 0, rb = 0, cb = 0, ncl = 0;
+        if (lane < cur_nw) {
+            rb = oA[lane];
+            int nr = oA[lane + 1] - rb;
+            cb = co[lane]; ncl = co[lane + 1] - cb;
+            if (rpart) {                               // lists are sorted by set: trim both ends
+                int a = 0, e = nr;
+                for (int t = 0; t < nr; t++) {
+                    const int st = sA[rb + t];
+                    a += st < rlo;
+                    e -= st >= rhi;
+                }
+                rb += a;
+                nr = e > a ? e - a : 0;
+            }
+            P = diag ? nr * (nr - 1) / 2 : nr * ncl;
+        }
+        int incl = P;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += v;
+        }
+        pre[wv][lane] = incl - P;
+        rbeg[wv][lane] = (int16_t)rb;
+        cbeg[wv][lane] = (int16_t)cb;
+        ncol[wv][lane] = (uint8_t)ncl;
+        const int total = __shfl(incl, 63, 64);
+        __builtin_amdgcn_wave_barrier();
+        const int f0 = (int)((int64_t)total * wv / S2NW);
+        const int f1 = ABL == 1 ? f0 : (int)((int64_t)total * (wv + 1) / S2NW);
+        for (int fb = f0; fb < f1; fb += 64 * SUN) {
+            int ri[SUN], ci[SUN];
+            bool ok[SUN];
+#pragma unroll
+            for (int u = 0; u < SUN; u++) {
+                const int F = fb + 64 * u, f = F + lane;
+                ok[u] = f < f1;
+                const int q0 = __popcll(__ballot(incl <= F));
+                const int q1 = __popcll(__ballot(incl <= F + 63));
+                int lo = q0;
+                for (int l = q0; l < q1; l++) lo += __builtin_amdgcn_readlane(incl, l) <= f;
+                lo = lo < 63 ? lo : 63;
+                const int q = f - pre[wv][lo];
+                int x, y, rr, cc;
+                if (diag) {                            // q -> pair (y, x), y < x: q = x(x-1)/2 + y
+                    x = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)q)) * 0.5f);
+                    if (x * (x - 1) / 2 > q) x--;
+                    else if ((x + 1) * x / 2 <= q) x++;
+                    y = q - x * (x - 1) / 2;
+                    rr = rbeg[wv][lo] + y;
+                    cc = rbeg[wv][lo] + x;
+                } else {
+                    const int n2 = ncol[wv][lo];
+                    x = (int)((float)q * __builtin_amdgcn_rcpf((float)n2));
+                    if (x * n2 > q) x--;
+                    else if ((x + 1) * n2 <= q) x++;
+                    y = q - x * n2;
+                    rr = rbeg[wv][lo] + x;
+                    cc = cbeg[wv][lo] + y;
+                }
+                ri[u] = ok[u] ? rr : 0;
+                ci[u] = ok[u] ? cc : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < SUN; u++) {
+                const int v = __popcll(wA[ri[u]] & cw[ci[u]]);
+                if (v && ok[u]) {
+                    const int sr = sA[ri[u]], sc = cs[ci[u]];
+                    const int t0 = cnt_index(sr, sc);
+                    atomicAdd(&cnt[t0 >> 1], (uint32_t)v << ((t0 & 1) << 4));
+                    if (mirror) {
+                        const int t1 = cnt_index(sc, sr);
+                        atomicAdd(&cnt[t1 >> 1], (uint32_t)v << ((t1 & 1) << 4));
+                    }
+                }
+            }
+        }
+        s0 = n0;
+        s1 = n1;
+    }
+    __syncthreads();
+    if (part) {
+        uint32_t* dst = reinterpret_cast<uint32_t*>(part) + ((int64_t)tile * nchunks + ch) * (SB * SB / 2);
+        for (int t = threadIdx.x; t < SB * SB / 2; t += S2T) dst[t] = cnt[t];
+        return;
+    }
+    for (int t = threadIdx.x; t < SB * SB; t += S2T) {
+        const int a = t >> 7, b = ((t & (SB - 1)) - a) & (SB - 1);
+        const int64_t i = A * SB + a, j = B * SB + b;
+        if (i < r0 || i >= r1 || j < c0 || j >= c1 || (upper && j <= i)) continue;
+        // the constant part once per pair: by chunk 0 (chunks flush with atomics)
+        const int v = (int)((cnt[t >> 1] >> ((t & 1) << 4)) & 0xFFFFu) +
+                      (ch == 0 ? (int)Us - nc[i] - nc[j] + dense_pair(dbits, Wdp, N, i, j) : 0);
+        if (v) atomicAdd(I + (i - r0) * ldI + (j - c0), v);
+    }
+}
+
+// ---- v4: the v2 windows, walked as an 8 x 8 grid per word ----------------
+// The staging of v2, but no flattened-product search: a wave takes the
+// window's words w = wave, wave + 8, ... one at a time, lane (i, j) =
+// (row entry ib + i, column entry jb + j), blocks of 8 x 8 over longer
+// lists. All indexing is wave-uniform; a product is two broadcast
+// ds_read_b64, two byte reads, the AND + popcount and the counter add.
+// U words are in flight per wave step.
+template <int U, int OCC>
+__global__ __launch_bounds__(S2T, OCC) void sparse_tile_kernel4(
+    const int64_t* __restrict__ off, const unsigned long long* __restrict__ word, const uint8_t* __restrict__ set,
+    const int32_t* __restrict__ nc, int64_t Us, int64_t Ws, int win, const int2* __restrict__ tiles, int nchunks,
+    int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I, int64_t ldI,
+    int32_t* __restrict__ part, const unsigned long long* __restrict__ dbits, int64_t Wdp, int64_t N) {
+    __shared__ uint32_t cnt[SB * SB / 2];                  // 32 KiB, 16-bit counters (cnt_index layout)
+    __shared__ unsigned long long wA[S2E], wB[S2E];        // 10 KiB: staged complement words
+    __shared__ uint8_t sA[S2E], sB[S2E];                   // their set bytes
+    __shared__ int16_t oA[65], oB[65];                    // window word -> first staged entry
+    const int tile = blockIdx.x / nchunks, ch = blockIdx.x % nchunks;
+    const int64_t A = tiles[tile].x, B = tiles[tile].y;
+    const int rlo = (int)(r0 - A * SB > 0 ? r0 - A * SB : 0);
+    const int rhi = (int)(r1 - A * SB < SB ? r1 - A * SB : SB);
+    const bool rpart = rlo > 0 || rhi < SB;
+    const bool diag = A == B && !rpart, mirror = diag && !upper;
+    for (int t = threadIdx.x; t < SB * SB / 2; t += S2T) cnt[t] = 0;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t sb = Ws * ch / nchunks, se = Ws * (ch + 1) / nchunks;
+    const int64_t* offA = off + A * Ws;
+    const int64_t* offB = off + B * Ws;
+    const unsigned long long* cw = diag ? wA : wB;
+    const uint8_t* cs = diag ? sA : sB;
+    const int16_t* co = diag ? oA : oB;
+    // registers holding the next window: offsets (threads 0..64) and two
+    // entries per side per thread
+    int64_t ra_off = 0, rb_off = 0;
+    unsigned long long ewA[2], ewB[2];
+    uint8_t esA[2], esB[2];
+    int na = 0, nb = 0, nw = 0;
+    auto fetch = [&](int64_t s0, int64_t s1) {
+        nw = (int)(s1 - s0);
+        const int64_t a0 = offA[s0], b0 = offB[s0];
+        na = (int)(offA[s1] - a0);
+        nb = diag ? 0 : (int)(offB[s1] - b0);
+        if (threadIdx.x <= nw) {
+            ra_off = offA[s0 + threadIdx.x] - a0;
+            if (!diag) rb_off = offB[s0 + threadIdx.x] - b0;
+        }
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+            const int t = threadIdx.x + e * S2T;
+            if (t < na) { ewA[e] = word[a0 + t]; esA[e] = set[a0 + t]; }
+            if (t < nb) { ewB[e] = word[b0 + t]; esB[e] = set[b0 + t]; }
+        }
+    };
+    int64_t s0 = sb;
+    int64_t s1 = std::min<int64_t>(se, (sb / win + 1) * win);
+    if (s0 < se) fetch(s0, s1);
+    while (s0 < se) {
+        __syncthreads();                               // the previous window's walk is done
+        if (threadIdx.x <= nw) {
+            oA[threadIdx.x] = (int16_t)ra_off;
+            if (!diag) oB[threadIdx.x] = (int16_t)rb_off;
+        }
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+            const int t = threadIdx.x + e * S2T;
+            if (t < na) { wA[t] = ewA[e]; sA[t] = esA[e]; }
+            if (t < nb) { wB[t] = ewB[e]; sB[t] = esB[e]; }
+        }
+        __syncthreads();
+        const int cur_nw = nw;
+        const int64_t n0 = s1, n1 = std::min<int64_t>(se, s1 + win);
+        if (n0 < se) fetch(n0, n1);                    // in flight during the walk
+        const int gi = lane >> 3, gj = lane & 7;
+        for (int w0 = wv; w0 < cur_nw; w0 += S2NW * U) {
+            int ra[U], nr[U], cb[U], ncl[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const int w = w0 + u * S2NW;
+                const bool has = w < cur_nw;
+                ra[u] = has ? oA[w] : 0;
+                nr[u] = has ? oA[w + 1] - ra[u] : 0;
+                cb[u] = has ? co[w] : 0;
+                ncl[u] = has ? co[w + 1] - cb[u] : 0;
+            }
+            // the common case: every list of the U words within one 8 x 8 block
+            bool small = true;
+#pragma unroll
+            for (int u = 0; u < U; u++) small = small && nr[u] <= 8 && ncl[u] <= 8;
+            if (small) {
+                unsigned long long wx[U], wy[U];
+                int sx[U], sy[U];
+                bool on[U];
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    on[u] = gi < nr[u] && gj < ncl[u] && (!diag || gj > gi);
+                    const int xi = on[u] ? ra[u] + gi : 0, yi = on[u] ? cb[u] + gj : 0;
+                    wx[u] = wA[xi]; wy[u] = cw[yi];
+                    sx[u] = sA[xi]; sy[u] = cs[yi];
+                    on[u] = on[u] && (!rpart || (sx[u] >= rlo && sx[u] < rhi));
+                }
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const int v = __popcll(wx[u] & wy[u]);
+                    if (on[u] && v) {
+                        const int t0 = cnt_index(sx[u], sy[u]);
+                        atomicAdd(&cnt[t0 >> 1], (uint32_t)v << ((t0 & 1) << 4));
+                        if (mirror) {
+                            const int t1 = cnt_index(sy[u], sx[u]);
+                            atomicAdd(&cnt[t1 >> 1], (uint32_t)v << ((t1 & 1) << 4));
+                        }
+                    }
+                }
+                continue;
+            }
+#pragma unroll 1
+            for (int u = 0; u < U; u++) {
+                for (int ib = 0; ib < nr[u]; ib += 8) {
+                    const int x = ib + gi;
+                    const bool xo = x < nr[u];
+                    const unsigned long long wx = xo ? wA[ra[u] + x] : 0ull;
+                    const int sx = xo ? sA[ra[u] + x] : 0;
+                    const bool xin = xo && (!rpart || (sx >= rlo && sx < rhi));
+                    for (int jb = diag ? ib : 0; jb < ncl[u]; jb += 8) {
+                        const int y = jb + gj;
+                        if (!xin || y >= ncl[u] || (diag && y <= x)) continue;
+                        const int v = __popcll(wx & cw[cb[u] + y]);
+                        if (v) {
+                            const int sy = cs[cb[u] + y];
+                            const int t0 = cnt_index(sx, sy);
+                            atomicAdd(&cnt[t0 >> 1], (uint32_t)v << ((t0 & 1) << 4));
+                            if (mirror) {
+                                const int t1 = cnt_index(sy, sx);
+                                atomicAdd(&cnt[t1 >> 1], (uint32_t)v << ((t1 & 1) << 4));
+                            }
+                        }
+                    }
+                }
+            }
+        }
+        s0 = n0;
+        s1 = n1;
+    }
+    __syncthreads();
+    if (part) {
+        uint32_t* dst = reinterpret_cast<uint32_t*>(part) + ((int64_t)tile * nchunks + ch) * (SB * SB / 2);
+        for (int t = threadIdx.x; t < SB * SB / 2; t += S2T) dst[t] = cnt[t];
+        return;
+    }
+    for (int t = threadIdx.x; t < SB * SB; t += S2T) {
+        const int a = t >> 7, b = ((t & (SB - 1)) - a) & (SB - 1);
+        const int64_t i = A * SB + a, j = B * SB + b;
+        if (i < r0 || i >= r1 || j < c0 || j >= c1 || (upper && j <= i)) continue;
+        // the constant part once per pair: by chunk 0 (chunks flush with atomics)
+        const int v = (int)((cnt[t >> 1] >> ((t & 1) << 4)) & 0xFFFFu) +
+                      (ch == 0 ? (int)Us - nc[i] - nc[j] + dense_pair(dbits, Wdp, N, i, j) : 0);
         if (v) atomicAdd(I + (i - r0) * ldI + (j - c0), v);
     }
 }
@@ -319,13 +735,15 @@ __global__ __launch_bounds__(256) void sparse_reduce_kernel(const int32_t* __res
                                                             const int2* __restrict__ tiles,
                                                             const int32_t* __restrict__ nc, int64_t Us, int64_t r0,
                                                             int64_t r1, int64_t c0, int64_t c1, int upper,
-                                                            int32_t* __restrict__ I, int64_t ldI) {
+                                                            int32_t* __restrict__ I, int64_t ldI,
+                                                            const unsigned long long* __restrict__ dbits,
+                                                            int64_t Wdp, int64_t N) {
     const int tile = blockIdx.x / (SB * SB / 256);
     const int t = (blockIdx.x % (SB * SB / 256)) * 256 + threadIdx.x;     // counter slot (cnt_index layout)
     const int a = t >> 7, b = ((t & (SB - 1)) - a) & (SB - 1);
     const int64_t i = (int64_t)tiles[tile].x * SB + a, j = (int64_t)tiles[tile].y * SB + b;
     if (i < r0 || i >= r1 || j < c0 || j >= c1 || (upper && j <= i)) return;
-    int v = (int)Us - nc[i] - nc[j];
+    int v = (int)Us - nc[i] - nc[j] + dense_pair(dbits, Wdp, N, i, j);
     const uint32_t* p = reinterpret_cast<const uint32_t*>(part) + (int64_t)tile * nchunks * (SB * SB / 2) + (t >> 1);
     for (int c = 0; c < nchunks; c++) v += (int)((p[(int64_t)c * (SB * SB / 2)] >> ((t & 1) << 4)) & 0xFFFFu);
     if (v) atomicAdd(I + (i - r0) * ldI + (j - c0), v);
@@ -335,11 +753,12 @@ __global__ __launch_bounds__(256) void sparse_reduce_kernel(const int32_t* __res
 
 // ---- host side ------------------------------------------------------------
 
-void locus_keys(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_t U, uint64_t tag, DevBuf& key) {
+void locus_keys(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, const uint32_t* dcounts, int64_t U,
+                uint64_t tag, DevBuf& key) {
     hipStream_t st = ctx->stream;
     key.alloc(U * 8 + 8, st);
     if (U == 0) return;
-    fill_u64_kernel<<<grid_for(U), 256, 0, st>>>(key.as<uint64_t>(), U, ~0ull);
+    unkeyed_kernel<<<grid_for(U), 256, 0, st>>>(key.as<uint64_t>(), dcounts, U);
     if (s->n_guide > 0)
         locus_key_kernel<<<grid_for(s->n_guide), 256, 0, st>>>(s->guide_codes.as<uint64_t>(),
                                                                s->guide_keys.as<uint64_t>(), s->n_guide, dict, U, tag,
@@ -379,9 +798,16 @@ void free_sparse(gdist_sets* s) {
     s->sp_off.release();
     s->sp_word.release();
     s->sp_set.release();
+    s->sp_ent.release();
     s->sp_nc.release();
     s->sparse = false;
     s->Wd = s->Ws = s->sp_entries = s->sp_U = 0;
+    s->sp_bucket_bits.clear();
+    s->sp_nbk = 0;
+    s->sp_pos_words = 0;
+    s->sp_fold_dense = false;
+    s->sp_dT.release();
+    s->sp_win = 0;
     s->sp_products = s->sp_items = 0.0;
 }
 
@@ -403,14 +829,23 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
     const int64_t Wv = ceil_div(U, 64);   // words holding dictionary bits
     if (Wv == 0) return;
     const unsigned long long* bits = s->bits.as<unsigned long long>();
-    DevBuf dz(W * 4, st);
-    GD_HIP(hipMemsetAsync(dz.p, 0, W * 4, st));
+    DevBuf dz(W * 8, st);
+    GD_HIP(hipMemsetAsync(dz.p, 0, W * 8, st));
     const int64_t rpb = 64;
     dim3 g((unsigned)ceil_div(W, 256), (unsigned)ceil_div(N, rpb));
-    word_z_kernel<<<g, 256, 0, st>>>(bits, N, W, U, rpb, dz.as<int32_t>());
+    word_z_kernel<<<g, 256, 0, st>>>(bits, N, W, U, rpb, dz.as<int32_t>(), dz.as<int32_t>() + W);
     GD_HIP(hipGetLastError());
-    std::vector<int32_t> z(W);
-    d2h(z.data(), dz.p, W * 4, st);
+    std::vector<int32_t> zc(W), zp(W), z(W);
+    d2h(zc.data(), dz.p, W * 4, st);
+    d2h(zp.data(), dz.as<int32_t>() + W, W * 4, st);
+    // each word is counted from the side fewer sets have entries on: the
+    // complement (sets lacking a common kmer) or the word itself (sets
+    // holding a rare one); the option sparse_zmax forces the complement side
+    std::vector<uint8_t> wpos(W, 0);
+    for (int64_t w = 0; w < W; w++) {
+        wpos[w] = !ctx->has_option(OPT_SPARSE_ZMAX) && zp[w] < zc[w];
+        z[w] = wpos[w] ? zp[w] : zc[w];
+    }
     tr.mark("sparse: word classes");
     // A word is sparse when its products + visits cost less than its column
     // of word pairs in the dense tiles (option sparse_zmax overrides).
@@ -437,10 +872,14 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
     if (Ws == 0 || !(zm || t_split < 0.8 * t_plain)) return;
     const int64_t nblk = ceil_div(N, SB);
     GD_REQUIRE((double)nblk * (double)Ws < 2e9, "sparse word index too large");
-    DevBuf dsw(Ws * 4, st), cnt(nblk * Ws * 4 + 4, st);
+    std::vector<uint8_t> spos(Ws);
+    for (int64_t k = 0; k < Ws; k++) spos[k] = wpos[sw[k]];
+    DevBuf dsw(Ws * 4, st), dsp(Ws + 8, st), cnt(nblk * Ws * 4 + 4, st);
     h2d(dsw.p, sw.data(), Ws * 4, st);
+    h2d(dsp.p, spos.data(), Ws, st);
     dim3 gs((unsigned)ceil_div(Ws, 256), (unsigned)nblk);
-    sparse_count_kernel<<<gs, 256, 0, st>>>(bits, N, W, U, dsw.as<int32_t>(), Ws, cnt.as<int32_t>());
+    sparse_count_kernel<<<gs, 256, 0, st>>>(bits, N, W, U, dsw.as<int32_t>(), dsp.as<uint8_t>(), Ws,
+                                            cnt.as<int32_t>());
     GD_HIP(hipGetLastError());
     GD_HIP(hipMemsetAsync(cnt.as<int32_t>() + nblk * Ws, 0, 4, st));
     s->sp_off.alloc((nblk * Ws + 1) * 8, st);
@@ -451,9 +890,26 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
     s->sp_set.alloc(total + 8, st);
     s->sp_nc.alloc(N * 4, st);
     GD_HIP(hipMemsetAsync(s->sp_nc.p, 0, N * 4, st));
-    sparse_fill_kernel<<<gs, 256, 0, st>>>(bits, N, W, U, dsw.as<int32_t>(), Ws, s->sp_off.as<int64_t>(),
+    const int64_t nbk = ceil_div(Ws, int64_t(1) << kBucketShift);
+    DevBuf dbb((size_t)N * nbk * 4, st);
+    GD_HIP(hipMemsetAsync(dbb.p, 0, (size_t)N * nbk * 4, st));
+    sparse_fill_kernel<<<gs, 256, 0, st>>>(bits, N, W, U, dsw.as<int32_t>(), dsp.as<uint8_t>(), Ws,
+                                           s->sp_off.as<int64_t>(),
                                            s->sp_word.as<unsigned long long>(), s->sp_set.as<uint8_t>(),
-                                           s->sp_nc.as<int32_t>());
+                                           s->sp_nc.as<int32_t>(), dbb.as<int32_t>(), nbk);
+    GD_HIP(hipGetLastError());
+    {   // complement bits of every set per bucket of 1024 sparse words, kept
+        // on the host for the chunk bound of sparse_matrix
+        s->sp_nbk = nbk;
+        s->sp_bucket_bits.assign((size_t)N * nbk, 0);
+        d2h(s->sp_bucket_bits.data(), dbb.p, (size_t)N * nbk * 4, st);
+    }
+    GD_HIP(hipGetLastError());
+    s->sp_ent.alloc(total * 16 + 16, st);
+    if (total)
+        sparse_records_kernel<<<grid_for(total), 256, 0, st>>>(s->sp_word.as<unsigned long long>(),
+                                                                s->sp_set.as<uint8_t>(), total,
+                                                                s->sp_ent.as<ulonglong2>());
     GD_HIP(hipGetLastError());
     if (Wdp) {
         DevBuf ddw(Wd * 4, st);
@@ -463,8 +919,41 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
                                                                s->dbits.as<unsigned long long>());
         GD_HIP(hipGetLastError());
     }
-    int64_t Us = 0;
-    for (int32_t w : sw) Us += (w + 1) * 64 <= U ? 64 : U - (int64_t)w * 64;
+    // v2 windows: the most aligned consecutive sparse words (64, 32, ... 4)
+    // whose entries fit the staging arrays in every block (a word holds at
+    // most 128 entries per block, so 4 words always fit)
+    {
+        std::vector<int64_t> ho(nblk * Ws + 1);
+        d2h(ho.data(), s->sp_off.as<int64_t>(), (nblk * Ws + 1) * 8, st);
+        s->sp_win = 0;
+        for (int win = 64; win >= 4 && !s->sp_win; win >>= 1) {
+            int64_t mx = 0;
+            for (int64_t b = 0; b < nblk; b++)
+                for (int64_t m = 0; m < Ws; m += win) {
+                    const int64_t e = std::min<int64_t>(Ws, m + win);
+                    mx = std::max(mx, ho[b * Ws + e] - ho[b * Ws + m]);
+                }
+            if (mx <= kSparseStageEntries) s->sp_win = win;
+        }
+    }
+    int64_t Us = 0;                       // valid bits of the complement-sparse words
+    int64_t npos = 0;
+    for (int32_t w : sw) {
+        if (wpos[w]) { npos++; continue; }
+        Us += (w + 1) * 64 <= U ? 64 : U - (int64_t)w * 64;
+    }
+    s->sp_pos_words = npos;
+    // A few dense words are counted in the flush of the sparse counters
+    // instead of a dense tile launch: the launch's per-tile accumulator flush
+    // cost C2's 16-64 dense words 0.09-0.15 ms beside the sparse kernel, the
+    // fold reads 2 x Wdp words per pair from L2 (option fold_dense_words)
+    s->sp_fold_dense = Wdp > 0 && Wdp <= ctx->option(OPT_FOLD_DENSE_WORDS, kFoldDenseWords);
+    if (s->sp_fold_dense) {
+        s->sp_dT.alloc((size_t)N * Wdp * 8, st);
+        transpose_words_kernel<<<grid_for(N * Wdp), 256, 0, st>>>(s->dbits.as<unsigned long long>(), N, Wdp,
+                                                                 s->sp_dT.as<unsigned long long>());
+        GD_HIP(hipGetLastError());
+    }
     GD_HIP(hipStreamSynchronize(st));
     s->sparse = true;
     s->Ws = Ws;
@@ -494,15 +983,65 @@ void sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
         sc.ntiles = (int64_t)tiles.size();
         // enough workgroups to fill the chip, each over >= 512 sparse words
         const int64_t target = (int64_t)ctx->cus * std::max<int64_t>(1, ctx->option(OPT_SPARSE_WG_PER_CU, 4));
-        // ... and each chunk within the 16-bit counters' bound
-        sc.nchunks = sc.ntiles ? (int)std::max<int64_t>(ceil_div(s->Ws, kChunkWords),
-                                                        std::min<int64_t>(ceil_div(s->Ws, 512), target / sc.ntiles))
-                               : 0;
+        // chunks of <= kChunkWords words keep the 16-bit counters exact for
+        // any sets; more chunks only while they add parallelism
+        int64_t nch = sc.ntiles ? std::max<int64_t>(ceil_div(s->Ws, kChunkWords),
+                                                    std::min<int64_t>(ceil_div(s->Ws, 512), ceil_div(target, sc.ntiles)))
+                                : 0;
+        const int64_t budget = ctx->option(OPT_SPARSE_PART_BUDGET, int64_t(1) << 30);
+        const int64_t tile_bytes = SB * SB * 2;
+        // ... and every chunk within the 16-bit counters' bound: a pair's
+        // count in a chunk is at most either set's complement bits there, so
+        // a chunk is exact when the SECOND largest set total over the buckets
+        // covering it is <= 65535 (one set may hold more: a guide lacks every
+        // kmer the later guides key, C2's sets 0-3). sp_bucket_bits holds the
+        // totals per set and bucket of 1024 sparse words.
+        auto chunk_ok = [&](int64_t n) {
+            const int64_t N = s->nsets, nbk = s->sp_nbk;
+            for (int64_t c = 0; c < n; c++) {
+                const int64_t b0 = s->Ws * c / n, b1 = s->Ws * (c + 1) / n;
+                if (b1 <= b0) continue;
+                if (b1 - b0 <= kChunkWords) continue;          // 64 x 1023 < 2^16 whatever the sets
+                if ((int64_t)s->sp_bucket_bits.size() != N * nbk) return false;
+                int64_t m1 = 0, m2 = 0;
+                for (int64_t i = 0; i < N; i++) {
+                    int64_t t = 0;
+                    for (int64_t k = b0 >> kBucketShift; k <= (b1 - 1) >> kBucketShift; k++)
+                        t += s->sp_bucket_bits[i * nbk + k];
+                    if (t > m1) { m2 = m1; m1 = t; } else if (t > m2) m2 = t;
+                }
+                if (m2 > 65535) return false;
+            }
+            return true;
+        };
+        // Past the partial budget (many tiles: N >> 1000), fewer and longer
+        // chunks where the complement bits allow it (chunk_ok), so that the
+        // partials fit; otherwise the chunks flush with atomics.
+        if (sc.ntiles && sc.ntiles * nch * tile_bytes > budget) {
+            int64_t fewer = std::max<int64_t>(1, budget / (sc.ntiles * tile_bytes));
+            while (fewer < nch && !chunk_ok(fewer)) fewer = std::min<int64_t>(nch, fewer * 2);
+            nch = std::min(nch, fewer);
+        }
+        if (ctx->has_option(OPT_SPARSE_CHUNKS))       // tests: a given chunk count (exactness still checked)
+            nch = std::max<int64_t>(1, std::min<int64_t>(s->Ws, ctx->option(OPT_SPARSE_CHUNKS, 1)));
+        GD_REQUIRE(nch == 0 || chunk_ok(nch), "sparse chunks exceed the 16-bit counter bound");
+        sc.nchunks = (int)nch;
         if (sc.ntiles) {
             sc.tiles.alloc(sc.ntiles * sizeof(int2), st);
             h2d(sc.tiles.p, tiles.data(), sc.ntiles * sizeof(int2), st);
         }
-        if (sc.nchunks > 1) sc.part.alloc((size_t)sc.ntiles * sc.nchunks * SB * SB * 2, st);
+        // chunk partials (16-bit counters, 32 KiB per tile and chunk) within a
+        // byte budget (option sparse_part_budget, default 1 GiB); past it the
+        // chunks flush their counters with global atomics instead
+        const int64_t part_bytes = sc.ntiles * sc.nchunks * tile_bytes;
+        sc.use_part = sc.nchunks > 1 && part_bytes <= budget;
+        if (sc.use_part) sc.part.alloc((size_t)part_bytes, st);
+        if (ctx->trace())
+            fprintf(stderr, "gdist: sparse plan rows [%lld,%lld) cols [%lld,%lld): %lld tiles x %d chunks, %s, win %d, "
+                            "%lld of %lld sparse words positive\n",
+                    (long long)r0, (long long)r1, (long long)c0, (long long)c1, (long long)sc.ntiles, sc.nchunks,
+                    sc.use_part ? "partials" : "atomic flush", s->sp_win, (long long)s->sp_pos_words,
+                    (long long)s->Ws);
         GD_REQUIRE(sc.ntiles * sc.nchunks < (int64_t(1) << 31), "sparse grid too large");
         sc.ready = true;
     }
@@ -516,19 +1055,41 @@ void sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     // per CU, LDS-limited) where 3 let them reach 112 (3 per CU): 0.310 ->
     // 0.298 ms (profiles/r01/sparse/occ_{3,8}.json; GDIST_SPARSE_OCC=3 for A/B)
     const int sun = (int)ctx->option(OPT_SPARSE_SUN, 6);
+    int version = (int)ctx->option(OPT_SPARSE_KERNEL, 1);
+    const unsigned long long* fold = s->sp_fold_dense ? s->sp_dT.as<unsigned long long>() : nullptr;
+    if ((version == 2 || version == 4) && s->sp_win == 0) version = 1;
     auto kern = ctx->option(OPT_SPARSE_OCC, 8) == 3 ? sparse_tile_kernel<6, 3>
                 : sun == 4            ? sparse_tile_kernel<4, 8>
                 : sun == 8            ? sparse_tile_kernel<8, 8>
                                       : sparse_tile_kernel<6, 8>;
+    if (version == 3)                  // v1 over 16-byte records
+        kern = sun == 4 ? sparse_tile_kernel<4, 8, true>
+               : sun == 8 ? sparse_tile_kernel<8, 8, true>
+                          : sparse_tile_kernel<6, 8, true>;
+    const int abl = (int)ctx->option(OPT_SPARSE_ABL, 0);
+    if (version == 4 && s->sp_win > 0)
+        (sun == 4 ? sparse_tile_kernel4<4, 6> : sun == 1 ? sparse_tile_kernel4<1, 6> : sparse_tile_kernel4<2, 6>)<<<
+            (unsigned)(nt * nchunks), S2T, 0, st>>>(
+            s->sp_off.as<int64_t>(), s->sp_word.as<unsigned long long>(), s->sp_set.as<uint8_t>(),
+            s->sp_nc.as<int32_t>(), s->sp_U, s->Ws, s->sp_win, sc.tiles.as<int2>(), nchunks, r0, r1, c0, c1,
+            upper ? 1 : 0, d_I, ldI, sc.use_part ? sc.part.as<int32_t>() : nullptr, fold, s->Wd, s->nsets);
+    else if (version == 2)
+        (abl == 1 ? sparse_tile_kernel2<4, 6, 1> : abl == 2 ? sparse_tile_kernel2<4, 6, 2> : sparse_tile_kernel2<4, 6, 0>)<<<(unsigned)(nt * nchunks), S2T, 0, st>>>(
+            s->sp_off.as<int64_t>(), s->sp_word.as<unsigned long long>(), s->sp_set.as<uint8_t>(),
+            s->sp_nc.as<int32_t>(), s->sp_U, s->Ws, s->sp_win, sc.tiles.as<int2>(), nchunks, r0, r1, c0, c1,
+            upper ? 1 : 0,
+            d_I, ldI, sc.use_part ? sc.part.as<int32_t>() : nullptr, fold, s->Wd, s->nsets);
+    else
     kern<<<(unsigned)(nt * nchunks), SNT, 0, st>>>(
-        s->sp_off.as<int64_t>(), s->sp_word.as<unsigned long long>(), s->sp_set.as<uint8_t>(), s->sp_nc.as<int32_t>(),
+        s->sp_off.as<int64_t>(), s->sp_word.as<unsigned long long>(), s->sp_set.as<uint8_t>(),
+        s->sp_ent.as<ulonglong2>(), s->sp_nc.as<int32_t>(),
         s->sp_U, s->Ws, sc.tiles.as<int2>(), nchunks, r0, r1, c0, c1, upper ? 1 : 0, d_I, ldI,
-        nchunks > 1 ? sc.part.as<int32_t>() : nullptr);
+        sc.use_part ? sc.part.as<int32_t>() : nullptr, fold, s->Wd, s->nsets);
     GD_HIP(hipGetLastError());
-    if (nchunks > 1) {
+    if (sc.use_part) {
         sparse_reduce_kernel<<<(unsigned)(nt * (SB * SB / 256)), 256, 0, st>>>(
             sc.part.as<int32_t>(), nchunks, sc.tiles.as<int2>(), s->sp_nc.as<int32_t>(), s->sp_U, r0, r1, c0, c1,
-            upper ? 1 : 0, d_I, ldI);
+            upper ? 1 : 0, d_I, ldI, fold, s->Wd, s->nsets);
         GD_HIP(hipGetLastError());
     }
 }

@@ -347,6 +347,12 @@ class KmerSets(_Handle):
         L.check(L.lib.gdist_sets_sparse_info(self.h, C.byref(a), C.byref(b), C.byref(c)))
         return a.value, b.value, c.value
 
+    def sparse_sides(self) -> tuple[int, int]:
+        """(complement-sparse words, positive-sparse words)."""
+        a, b = C.c_int64(), C.c_int64()
+        L.check(L.lib.gdist_sets_sparse_sides(self.h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
     def rare_kmers(self) -> int:
         """Rare-tier kmers before identical posting lists were merged."""
         n = C.c_int64()

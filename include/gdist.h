@@ -176,6 +176,10 @@ int  gdist_sets_bitset_info(const gdist_sets* sets, int64_t* dict_size, int64_t*
  * the complement entries (0s when the split was not worth building).
  * GDIST_SPARSE=0 / GDIST_LOCUS_ORDER=0 switch it off (A/B). */
 int  gdist_sets_sparse_info(const gdist_sets* sets, int64_t* sparse_words, int64_t* dense_words, int64_t* entries);
+/* The sparse words by side: counted from the sets' complement words (sets
+ * lacking a commonly held kmer) or from their words (sets holding a rarely
+ * held one: positive-sparse). */
+int  gdist_sets_sparse_sides(const gdist_sets* sets, int64_t* complement_words, int64_t* positive_words);
 /* Copy the bitsets (nsets x words_per_set uint64, row-major) to the host. */
 int  gdist_sets_bitset_download(const gdist_sets* sets, uint64_t* bits);
 /* Concatenate two collections (e.g. base genomes + comparison genomes). */

@@ -575,7 +575,9 @@ def test_rare_tier_thresholds_exact(ctx, T, kernel, dedup, opts):
     assert bits_equal(d, eD[0, cols])
 
 
-@pytest.mark.parametrize("mode", ["auto", "all_sparse", "mixed", "no_locus", "off"])
+@pytest.mark.parametrize("mode", ["auto", "all_sparse", "mixed", "no_locus", "off", "atomic_flush", "kernel_v1",
+                                  "kernel_v2", "many_chunks", "two_sided", "mixed_fold", "mixed_fold_1chunk",
+                                  "kernel_v4", "kernel_v4_rows"])
 def test_sparse_complement_words_exact(ctx, mode, opts):
     """The dense tier in locus order with complement-sparse words: counts and
     distances are bit-exact against the oracle over upper triangles,
@@ -584,19 +586,37 @@ def test_sparse_complement_words_exact(ctx, mode, opts):
     and the tiles, the locus order is off (code order), or the split is off."""
     import gdist
     settings = {"all_sparse": {"sparse_zmax": 100000}, "mixed": {"sparse_zmax": 12},
-                "no_locus": {"locus_order": 0, "sparse_zmax": 40}, "off": {"sparse": 0}}
+                "no_locus": {"locus_order": 0, "sparse_zmax": 40}, "off": {"sparse": 0},
+                # chunks flush with atomics (no partials within a zero budget)
+                "atomic_flush": {"sparse_zmax": 100000, "sparse_part_budget": 0, "sparse_chunks": 5},
+                "kernel_v1": {"sparse_zmax": 100000, "sparse_kernel": 1},
+                "kernel_v2": {"sparse_zmax": 100000, "sparse_kernel": 2},
+                "kernel_v4": {"sparse_zmax": 100000, "sparse_kernel": 4},
+                "kernel_v4_rows": {"sparse_zmax": 40, "sparse_kernel": 4, "sparse_sun": 4},
+                "many_chunks": {"sparse_zmax": 100000, "sparse_chunks": 37},
+                # words counted from either side (complement / positive), model's choice
+                # a dense-only dictionary: the substitution kmers two or more
+                # sets share are dense too, and their words are counted from
+                # the set bits (positive-sparse) beside the complement words
+                "two_sided": {"rare_t": 2},
+                # the dense words counted in the sparse flush (reduce kernel / one chunk's atomics)
+                "mixed_fold": {"sparse_zmax": 12, "fold_dense_words": 100000, "sparse_chunks": 3},
+                "mixed_fold_1chunk": {"sparse_zmax": 12, "fold_dense_words": 100000, "sparse_chunks": 1}}
     opts(**settings.get(mode, {}))
     n = 300
     seqs = synth_sets(n, 20000, 0.003, 105)
     sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
     _, W = sets.build_bitsets()
     ws, wd, ent = sets.sparse_info()
-    if mode == "all_sparse":
+    if mode in ("all_sparse", "atomic_flush", "kernel_v1", "kernel_v2", "many_chunks", "kernel_v4"):
         assert ws > 0 and wd == 0 and ent > 0
-    elif mode == "mixed":
+    elif mode in ("mixed", "mixed_fold", "mixed_fold_1chunk"):
         assert ws > 0 and wd > 0
     elif mode == "off":
         assert ws == 0 and wd == W
+    elif mode == "two_sided":
+        cw, pw = sets.sparse_sides()
+        assert ws > 0 and cw > 0 and pw > 0 and cw + pw == ws
     off, codes = oracle_pack(seqs, 21, 0, 0)
     for (r0, r1, c0, c1, up) in [(0, n, 0, n, True), (0, n, 0, n, False), (37, 211, 5, 290, False),
                                  (130, 259, 0, n, True), (299, 300, 0, n, False)]:
