@@ -50,6 +50,9 @@ CONFIGS = {
     # name: (n_genomes, length, p_max, kind, k, method, cfg index for the seed)
     "c2": dict(n=1000, length=2_000_000, p_max=0.002, protein=False, k=21, method="bitset", cfg=2,
                desc="1000 synthetic 2 Mbp genomes, DNA k=21 both strands, dictionary-rank bitsets"),
+    "c2r": dict(n=1000, length=2_000_000, p_max=0.002, protein=False, k=21, method="bitset", cfg=2, realistic=True,
+                desc="C2-realistic: 1000 synthetic ~2 Mbp genomes in 8 clades with short indels and segment "
+                     "moves / inversions (gdist.synth.realistic_genome), DNA k=21 both strands, bitsets"),
     "c3": dict(n=10000, length=33_333, p_max=0.10, protein=True, k=8, method="auto", cfg=3,
                desc="10000 synthetic 33,333-aa proteomes, protein k=8, sorted uint64 sets "
                     "(METHOD_AUTO: two-tier bitsets built from them, or the LDS hash-join)"),
@@ -128,9 +131,16 @@ def main():
     t_setup = time.time()
     s0, s1 = shard.shard_of_sets(n_total, world)[rank]
     t = time.time()
-    genomes = synth.genomes(s1 - s0, cfg["length"], cfg["p_max"], cfg["cfg"], protein=cfg["protein"], first=s0)
-    blob, off = synth.to_blob(genomes)
-    del genomes
+    if cfg.get("realistic"):
+        rs = synth.realistic_genomes(s1 - s0, cfg["length"], cfg["p_max"], cfg["cfg"], first=s0)
+        blob = b"".join(rs)
+        off = np.zeros(len(rs) + 1, dtype=np.int64)
+        off[1:] = np.cumsum([len(x) for x in rs])
+        del rs
+    else:
+        genomes = synth.genomes(s1 - s0, cfg["length"], cfg["p_max"], cfg["cfg"], protein=cfg["protein"], first=s0)
+        blob, off = synth.to_blob(genomes)
+        del genomes
     gen_s = time.time() - t
     kt = gdist.KmerType.PROT if cfg["protein"] else gdist.KmerType.DNA
     t = time.time()
@@ -415,7 +425,11 @@ def verify_sample(cfg, method, N, r0, r1, dI, dD, max_over_ranks, npairs=4):
 
     def codes(g):
         if g not in cache:
-            s = bytes(synth.genomes(1, cfg["length"], cfg["p_max"], cfg["cfg"], protein=cfg["protein"], first=g)[0])
+            if cfg.get("realistic"):
+                s = synth.realistic_genome(g, cfg["length"], cfg["p_max"], cfg["cfg"])
+            else:
+                s = bytes(synth.genomes(1, cfg["length"], cfg["p_max"], cfg["cfg"], protein=cfg["protein"],
+                                        first=g)[0])
             cache[g] = _kmer_codes(s, cfg["k"], cfg["protein"])
         return cache[g]
 
@@ -474,6 +488,8 @@ def cpu_baselines(cfg, threads, host=None, target_s=10.0, cap=6000, batch=20):
     cap = max(T + 2, min(cap, int(2e8 // cfg["length"])))    # bound the sample's residues too
 
     def genomes(n):
+        if cfg.get("realistic"):
+            return synth.realistic_genomes(n, cfg["length"], cfg["p_max"], cfg["cfg"])
         return [bytes(r) for r in synth.genomes(n, cfg["length"], cfg["p_max"], cfg["cfg"], protein=cfg["protein"])]
 
     def faithful(n):

@@ -895,6 +895,45 @@ int gdist_sketch_matrix(gdist_ctx* ctx, const gdist_sets* sk, int64_t r0, int64_
 }
 
 // ---------------------------------------------------------------------------
+int gdist_lsh_build(gdist_ctx* ctx, const gdist_sets* sketches, int stages, int buckets, uint64_t seed,
+                    gdist_lsh** out) {
+    return guard([&] {
+        use_device(ctx);
+        std::lock_guard<std::recursive_mutex> lk_(ctx->mu);
+        check_sets(sketches);
+        GD_REQUIRE(out, "null output");
+        *out = nullptr;
+        auto* L = new gdist_lsh();
+        try {
+            gdist::lsh_build(ctx, sketches, stages, buckets, seed, L);
+        } catch (...) {
+            delete L;
+            throw;
+        }
+        *out = L;
+    });
+}
+
+int gdist_lsh_free(gdist_lsh* lsh) {
+    return guard([&] {
+        if (!lsh) return;
+        (void)hipSetDevice(lsh->ctx->device);
+        delete lsh;
+    });
+}
+
+int gdist_lsh_closest(gdist_ctx* ctx, const gdist_lsh* lsh, const gdist_sets* queries, int n, double max_dist,
+                      int64_t* idx_out, double* d_out, int32_t* count_out) {
+    return guard([&] {
+        use_device(ctx);
+        std::lock_guard<std::recursive_mutex> lk_(ctx->mu);
+        GD_REQUIRE(lsh && lsh->ctx == ctx, "index of another context");
+        check_sets(queries);
+        GD_REQUIRE(count_out && (n == 0 || (idx_out && d_out)), "null output");
+        gdist::lsh_closest(ctx, lsh, queries, n, max_dist, idx_out, d_out, count_out);
+    });
+}
+
 int gdist_comm_unique_id(char id[GDIST_UNIQUE_ID_BYTES]) {
     return guard([&] {
         static_assert(sizeof(ncclUniqueId) <= GDIST_UNIQUE_ID_BYTES, "unique id size");

@@ -297,6 +297,17 @@ struct gdist_sets {
     mutable std::map<std::vector<int64_t>, std::unique_ptr<gdist::MatrixPlan>> plans;
 };
 
+// LSH index of a sketch collection (lsh.hip)
+struct gdist_lsh {
+    gdist_ctx* ctx = nullptr;
+    const gdist_sets* sk = nullptr;       // the indexed sketches (must outlive the index)
+    int stages = 0, buckets = 0;
+    uint64_t seed = 0;
+    gdist::DevBuf salts;                  // uint64 [stages]
+    gdist::DevBuf off;                    // int64 [stages * buckets + 1]: bucket -> members
+    gdist::DevBuf members;                // int32 [nsets * stages], by (stage, bucket), ascending set
+};
+
 namespace gdist {
 
 // pack.hip
@@ -435,6 +446,11 @@ void zero_counts(gdist_ctx* ctx, int64_t r0, int64_t r1, int64_t c0, int64_t c1,
 void distance_epilogue(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0,
                        int64_t c1, bool upper, unsigned flags, const int32_t* d_I, int64_t ldI,
                        double* d_D, int64_t ldD);
+
+// lsh.hip
+void lsh_build(gdist_ctx* ctx, const gdist_sets* sk, int stages, int buckets, uint64_t seed, gdist_lsh* L);
+void lsh_closest(gdist_ctx* ctx, const gdist_lsh* L, const gdist_sets* qs, int nbest, double max_dist,
+                 int64_t* idx_out, double* d_out, int32_t* count_out);
 
 // sketch.hip
 void sketch_build(gdist_ctx* ctx, const gdist_sets* s, int width, gdist_sets* out);

@@ -88,6 +88,9 @@ _SIGS = {
     "gdist_sketch_upload": (C.c_int, [_ctxp, C.c_int, _i64, _i64p, _i32p, C.POINTER(_setp)]),
     "gdist_sketch_download": (C.c_int, [_setp, _i64p, _i32p]),
     "gdist_sketch_matrix": (C.c_int, [_ctxp, _setp, _i64, _i64, _i64, _i64, _u32, _vp, _vp, _i64]),
+    "gdist_lsh_build": (C.c_int, [_ctxp, _setp, C.c_int, C.c_int, C.c_uint64, C.POINTER(C.c_void_p)]),
+    "gdist_lsh_free": (C.c_int, [C.c_void_p]),
+    "gdist_lsh_closest": (C.c_int, [_ctxp, C.c_void_p, _setp, C.c_int, _dbl, _i64p, _dblp, _i32p]),
     "gdist_comm_unique_id": (C.c_int, [C.c_char_p]),
     "gdist_comm_init": (C.c_int, [_ctxp, C.c_char_p, C.c_int, C.c_int]),
     "gdist_comm_init_host": (C.c_int, [_ctxp, C.c_int, C.c_int, C.c_void_p, _vp]),

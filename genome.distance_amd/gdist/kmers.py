@@ -522,6 +522,38 @@ class SketchSets(_Handle):
                                           d_D, ld))
 
 
+class LSHIndex:
+    """LSHMemSeqHash over a SketchSets collection (gdist_lsh_build):
+    getClosest(queries, n, maxDist) per query sketch."""
+
+    def __init__(self, sketches: "SketchSets", stages: int, buckets: int, seed: int = 0x5EED):
+        h = C.c_void_p()
+        L.check(L.lib.gdist_lsh_build(sketches.ctx.h, sketches.h, int(stages), int(buckets), int(seed), C.byref(h)))
+        self.ctx, self.h, self.sketches = sketches.ctx, h, sketches      # the index keeps its sketches alive
+        self.ctx._handles.add(self)
+
+    def free(self):
+        if getattr(self, "h", None):
+            L.lib.gdist_lsh_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+    def getClosest(self, queries: "SketchSets", n: int, max_dist: float) -> list[list[tuple[int, float]]]:
+        """For each query: [(indexed set, distance)] nearest first, at most n, distance <= max_dist."""
+        nq = len(queries)
+        idx = np.zeros(max(nq * n, 1), dtype=np.int64)
+        d = np.zeros(max(nq * n, 1), dtype=np.float64)
+        cnt = np.zeros(max(nq, 1), dtype=np.int32)
+        L.check(L.lib.gdist_lsh_closest(self.ctx.h, self.h, queries.h, int(n), float(max_dist),
+                                        L.ptr(idx, C.c_int64), L.ptr(d, C.c_double), L.ptr(cnt, C.c_int32)))
+        return [[(int(idx[q * n + r]), float(d[q * n + r])) for r in range(cnt[q])] for q in range(nq)]
+
+
 def triangle_partition(n: int, nparts: int, align: int = 1) -> list[int]:
     """Row bounds with equal upper-triangle area per part."""
     b = np.zeros(nparts + 1, dtype=np.int64)

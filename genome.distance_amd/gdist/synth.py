@@ -63,3 +63,83 @@ def to_blob(arr: np.ndarray) -> tuple[bytes, np.ndarray]:
     n, length = arr.shape
     off = np.arange(n + 1, dtype=np.int64) * length
     return arr.tobytes(), off
+
+
+_ANCESTORS: dict = {}
+_COMP = np.zeros(256, dtype=np.uint8)
+for _a, _b in zip(b"ACGT", b"TGCA"):
+    _COMP[_a] = _b
+
+
+def realistic_genome(g: int, length: int, p_max: float, cfg: int, clades: int = 8, p_clade: float = 0.004,
+                     indel_rate: float = 2e-5, blocks: int = 16, p_rearrange: float = 0.5) -> bytes:
+    """Genome g of a collection that is NOT one ancestor plus independent
+    substitutions (the structure the locus order was tuned on):
+      * clades: the ancestor gets p_clade substitutions per clade (genome g
+        belongs to clade g mod `clades`), so genomes share variants in groups
+        and the first sequences (the guides) are ordinary clade members;
+      * substitutions of its own at p_g ~ U[0, p_max];
+      * short indels (1-10 bp, rate indel_rate per site each way), so genome
+        lengths and kmer windows shift;
+      * with probability p_rearrange, 1-3 moves of one of `blocks` equal
+        segments to another position, reverse-complemented half the time.
+    Deterministic per (cfg, g): splitmix64 substreams as genomes()."""
+    seed = master_seed(cfg) ^ 0x5EA1
+    c = g % clades
+    with np.errstate(over="ignore"):
+        sc = int(np.uint64(seed) ^ (np.uint64(0xC1ADE + c) * GOLDEN))
+        sg = int(np.uint64(seed) ^ (np.uint64(g) * GOLDEN))
+    key = (seed, length)
+    if key not in _ANCESTORS:
+        _ANCESTORS.clear()
+        _ANCESTORS[key] = (splitmix64(seed, length) % np.uint64(4)).astype(np.uint8)
+    idx = _ANCESTORS[key].copy()
+
+    def substitute(idx, s, m, start):
+        if m <= 0:
+            return
+        x = splitmix64(s, 2 * m, start=start)
+        pos = (x[:m] % np.uint64(len(idx))).astype(np.int64)
+        idx[pos] = (idx[pos] + (x[m:] % np.uint64(3)).astype(np.uint8) + 1) % 4
+
+    substitute(idx, sc, int(round(p_clade * length)), 1)
+    p = float(_uniform(splitmix64(sg, 1))[0]) * p_max
+    substitute(idx, sg, int(round(p * length)), 1)
+    seq = DNA_ALPHA[idx]
+    # indels at distinct sorted positions: even events delete 1-10 bp, odd
+    # events insert 1-10 random bp; assembled in one pass
+    ne = int(round(indel_rate * length))
+    if ne:
+        x = splitmix64(sg, 4 * ne, start=1 << 40)
+        pos = np.unique((x[:2 * ne] % np.uint64(length)).astype(np.int64))
+        lens = (x[2 * ne:2 * ne + len(pos)] % np.uint64(10)).astype(np.int64) + 1
+        pieces, at = [], 0
+        for k, q in enumerate(pos):
+            if q < at:
+                continue
+            pieces.append(seq[at:q])
+            ln = int(lens[k])
+            if k % 2 == 0:
+                at = q + ln                                   # deletion
+            else:
+                pieces.append(DNA_ALPHA[(splitmix64(sg ^ 0x1D, ln, start=int(q)) % np.uint64(4)).astype(np.uint8)])
+                at = q
+        pieces.append(seq[at:])
+        seq = np.concatenate(pieces)
+    # rearrangements: move (and maybe reverse-complement) whole segments
+    r = splitmix64(sg, 8, start=1 << 41)
+    if _uniform(r[:1])[0] < p_rearrange:
+        segs = np.array_split(seq, blocks)
+        for t in range(1 + int(r[1] % np.uint64(3))):
+            a = int(r[2 + t] % np.uint64(len(segs)))
+            b = int((r[2 + t] >> np.uint64(20)) % np.uint64(len(segs)))
+            s = segs.pop(a)
+            if (r[2 + t] >> np.uint64(40)) & np.uint64(1):
+                s = _COMP[s[::-1]]
+            segs.insert(b, s)
+        seq = np.concatenate(segs)
+    return seq.tobytes()
+
+
+def realistic_genomes(n: int, length: int, p_max: float, cfg: int, first: int = 0, **kw) -> list[bytes]:
+    return [realistic_genome(first + r, length, p_max, cfg, **kw) for r in range(n)]

@@ -103,6 +103,7 @@ extern "C" {
 
 typedef struct gdist_ctx  gdist_ctx;
 typedef struct gdist_sets gdist_sets;
+typedef struct gdist_lsh  gdist_lsh;
 
 /* ---- library / context ---------------------------------------------- */
 const char* gdist_version(void);
@@ -237,6 +238,22 @@ int  gdist_sketch_download(const gdist_sets* sk, int64_t* offsets, int32_t* sigs
 int  gdist_sketch_matrix(gdist_ctx* ctx, const gdist_sets* sk,
                          int64_t r0, int64_t r1, int64_t c0, int64_t c1, unsigned flags,
                          int32_t* common_out, double* D_out, int64_t ld);
+
+/* ---- LSH bucket query (MashProcessor / FindProcessor) ------------------ */
+/* Index of a sketch collection: new LSHMemSeqHash(width, stages, buckets)
+ * + add() per subject (MashProcessor.java:110,130; BuildProcessor.java:131,148).
+ * Stage t files a sketch in bucket (min over its signature of a salted
+ * splitmix64 mix) mod buckets; seed picks the salts. The sketches must
+ * outlive the index. (Restated: the LSH classes are un-vendored.) */
+int  gdist_lsh_build(gdist_ctx* ctx, const gdist_sets* sketches, int stages, int buckets, uint64_t seed,
+                     gdist_lsh** out);
+int  gdist_lsh_free(gdist_lsh* lsh);
+/* getClosest(kmers, n, maxDist) for every query sketch (MashProcessor.java:150,
+ * FindProcessor.java:110): among the indexed sets sharing a bucket with the
+ * query in any stage, those at sketch distance <= max_dist, nearest first
+ * (ties by index), at most n: idx_out[q*n + r], d_out[q*n + r], count_out[q]. */
+int  gdist_lsh_closest(gdist_ctx* ctx, const gdist_lsh* lsh, const gdist_sets* queries, int n, double max_dist,
+                       int64_t* idx_out, double* d_out, int32_t* count_out);
 
 /* ---- multi-GPU (RCCL over xGMI) -------------------------------------- */
 #define GDIST_UNIQUE_ID_BYTES 128

@@ -129,3 +129,53 @@ def faithful_fasta_dist(seqs: list[bytes], k: int, kind: int = 0, flags: int = 0
     pairs = lib().or_faithful_fasta_dist(kind, k, flags, blob, _p(off, C.c_int64), n, batch, max_rows,
                                          _p(D, C.c_double), nthreads)
     return int(pairs), D
+
+
+# ---------------------------------------------------------------- LSH (restated)
+_M64 = (1 << 64) - 1
+
+
+def _mix64(z: int) -> int:
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _M64
+    return z ^ (z >> 31)
+
+
+def lsh_salts(stages: int, seed: int) -> list[int]:
+    """Stage salts of gdist_lsh_build (csrc/lsh.hip)."""
+    return [_mix64((seed + 0x9E3779B97F4A7C15 * (t + 1)) & _M64) for t in range(stages)]
+
+
+def lsh_buckets(sig, stages: int, buckets: int, seed: int) -> list[int]:
+    """Stage t's bucket of one signature: min over x of mix(uint32(x) ^ salt_t) mod buckets."""
+    out = []
+    for salt in lsh_salts(stages, seed):
+        m = min((_mix64((int(x) & 0xFFFFFFFF) ^ salt) for x in sig), default=_M64)
+        out.append(m % buckets)
+    return out
+
+
+def lsh_closest(subject_sigs, query_sigs, width: int, stages: int, buckets: int, seed: int, n: int,
+                max_dist: float):
+    """getClosest(kmers, n, maxDist) (MashProcessor.java:150, FindProcessor.java:110)
+    restated over the LSH of csrc/lsh.hip: candidates share a bucket with the
+    query in some stage; sketch distance <= max_dist; nearest first, ties by
+    index; at most n. Test infrastructure (parity unpinned: the reference's
+    LSH classes are un-vendored)."""
+    index = {}
+    for i, s in enumerate(subject_sigs):
+        for t, b in enumerate(lsh_buckets(s, stages, buckets, seed)):
+            index.setdefault((t, b), []).append(i)
+    res = []
+    for q in query_sigs:
+        cand = set()
+        for t, b in enumerate(lsh_buckets(q, stages, buckets, seed)):
+            cand.update(index.get((t, b), []))
+        scored = []
+        for c in sorted(cand):
+            d, _ = sketch_distance(np.asarray(q, np.int32), np.asarray(subject_sigs[c], np.int32), width)
+            if d <= max_dist:
+                scored.append((d, c))
+        scored.sort()
+        res.append([(c, d) for d, c in scored[:n]])
+    return res

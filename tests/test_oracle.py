@@ -199,3 +199,15 @@ def test_hashmap_order_initial_capacity():
         return x ^ (x >> 16)
     assert java_hashmap_order(k385[:384], 500) == sorted(range(384), key=lambda i: (h(k385[i]) & 511, i))
     assert java_hashmap_order(k385, 500) == sorted(range(385), key=lambda i: (h(k385[i]) & 1023, i))
+
+
+def test_lsh_oracle_known_answer():
+    """oracle.lsh_closest (the restated bucket search): with one bucket per
+    stage every indexed sketch is a candidate; distances are the Mash
+    bottom-s distances, nearest first, ties by index, capped at n."""
+    s = [np.array([1, 5, 9, 12], np.int32), np.array([1, 5, 9, 13], np.int32), np.array([100, 200], np.int32)]
+    assert oracle.lsh_closest(s, [s[0]], 8, 3, 1, 1, 5, 1.0) == [[(0, 0.0), (1, 0.4), (2, 1.0)]]
+    assert oracle.lsh_closest(s, [s[0]], 8, 3, 1, 1, 2, 1.0) == [[(0, 0.0), (1, 0.4)]]
+    assert oracle.lsh_closest(s, [s[0]], 8, 3, 1, 1, 5, 0.3) == [[(0, 0.0)]]
+    b = oracle.lsh_buckets(s[0], 4, 1000, 7)
+    assert len(b) == 4 and all(0 <= x < 1000 for x in b) and b == oracle.lsh_buckets(list(s[0]), 4, 1000, 7)
