@@ -270,7 +270,7 @@ def main():
                  "sketch": "sketch_tile_kernel<16,24,LDS,K=2>"}[method]
         if sparse:
             kname = "sparse_tile_kernel (+ bitset_tile_kernel2 on the dense words, rare_pairs_kernel, beside it)"
-        if traffic is not None and pmc.get("kernel", "").split()[0] != kname.split()[0]:
+        if traffic is not None and not pmc.get("kernel", "").startswith(kname.split()[0]):
             traffic = None                    # the PMC summary was taken on another kernel
         valu_peak = VALU_WORDPAIR_PEAK * 4 / 1e12
         if sparse:
@@ -295,10 +295,14 @@ def main():
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kname,
                     "kernel_avg_ms": round(k_avg_ms, 4), "algo_bytes_per_launch": round(algo_sparse),
-                    "note": "algorithmic bytes = the complement entries + offsets each sparse tile streams once; "
-                            "the kernel is bound by its dependent load -> LDS-atomic chain, not by bandwidth "
-                            "(profiles/r01/sparse/ablation_c2.txt); kernel time = HIP-event span of the step's "
-                            "launches (sparse, dense-word tiles and rare tier run concurrently)",
+                    "limiter": "instruction issue and the dependent load -> LDS-atomic chain, not HBM bandwidth: "
+                               "~100 wave-instructions per 64 products (word search, decode, 4 loads, the add), "
+                               "SQ_ACTIVE_INST_ANY ~ the kernel's cycles per SIMD, TA busy ~50 % "
+                               "(profiles/r02/sparse/pmc_v1.txt); LDS-staged variants measured slower "
+                               "(DESIGN.md §4)",
+                    "note": "algorithmic bytes = the sparse entries + offsets each sparse tile streams once; "
+                            "kernel time = HIP-event span of the step's launches (sparse tiles with their chunk "
+                            "reduce, the dense-word tiles and the rare tier run concurrently)",
                     "dense_equivalent": {"lane_ops_per_s_T": round(dense_ops, 2),
                                          "x_dense_valu_ceiling": round(dense_ops / valu_peak, 2),
                                          "note": "the same pairs as AND+popcount over all W bitset words "

@@ -402,7 +402,7 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
                    int64_t c1, bool upper, int32_t* d_I, int64_t ldI);
 
 // sparse.hip — locus order of the dense dictionary, complement-sparse words
-constexpr int kGuides = 4;                       // guide sequences per packed collection
+constexpr int kGuides = 2;                       // guide sequences per packed collection
 constexpr int kSparseStageEntries = 640;         // sparse v2: entries per side a window may hold
 constexpr int kFoldDenseWords = 0;               // dense words folded into the sparse flush: off (the
                                                  // tile launch overlaps the sparse kernel; the fold runs after it)
