@@ -197,7 +197,7 @@ __global__ void sparse_records_kernel(const unsigned long long* __restrict__ wor
 // tiles add into I concurrently), with the constant part U_s - nc_i - nc_j;
 // with several, each chunk stores its counters to `part` and
 // sparse_reduce_kernel sums them.
-constexpr int SNT = 512;                 // threads per workgroup (3 per CU: 6 waves per SIMD)
+constexpr int SNT = 512;                 // threads per workgroup (4 per CU, LDS-limited: 8 waves per SIMD)
 // Counters are 16-bit, two to an LDS dword: a chunk holds at most kChunkWords
 // sparse words, so a pair's count in one chunk is at most 64 x 1023 < 2^16
 // and a packed ds_add_u32 never carries into the neighbour (32 KiB per tile)
@@ -1058,6 +1058,7 @@ void sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     int version = (int)ctx->option(OPT_SPARSE_KERNEL, 1);
     const unsigned long long* fold = s->sp_fold_dense ? s->sp_dT.as<unsigned long long>() : nullptr;
     if ((version == 2 || version == 4) && s->sp_win == 0) version = 1;
+    // (option sparse_occ = 3 exists for SUN = 6 only: the A/B that chose OCC 8)
     auto kern = ctx->option(OPT_SPARSE_OCC, 8) == 3 ? sparse_tile_kernel<6, 3>
                 : sun == 4            ? sparse_tile_kernel<4, 8>
                 : sun == 8            ? sparse_tile_kernel<8, 8>
