@@ -223,13 +223,14 @@ def main():
     for _ in range(args.warmup):
         step()
     barrier()
-    kernel_ms = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
-        kernel_ms.append(ctx.last_timing()[0])
+        step()                       # device outputs: returns once queued
     barrier()
     elapsed = time.perf_counter() - t0
+    # the timed steps' kernel times (HIP events on the library's streams,
+    # recorded per step inside the timed region, read after it)
+    kernel_ms = ctx.recent_timings(args.steps)
     elapsed_max = max_over_ranks(elapsed)
     pairs_all = N * (N - 1) // 2
     value = pairs_all * args.steps / elapsed_max

@@ -1383,6 +1383,7 @@ double sorted_cost_s(const gdist_sets* s, double pairs) {
 }
 
 void free_bitsets(gdist_sets* s) {
+    s->graphs.clear();
     s->plans.clear();
     free_sparse(s);
     s->bits.release();
@@ -1422,7 +1423,10 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     const std::vector<int64_t> key{r0, r1, c0, c1, upper ? 1 : 0, variant, split_diag ? 1 : 0, max_rr, tW};
     auto it = s->plans.find(key);
     if (it == s->plans.end()) {
-        if (s->plans.size() >= 8) s->plans.clear();   // row-block loops: keep the cache small
+        if (s->plans.size() >= 8) {   // row-block loops: keep the cache small
+            s->graphs.clear();        // (captured steps hold the plans' buffers)
+            s->plans.clear();
+        }
         auto plan = std::make_unique<MatrixPlan>();
         MatrixPlan& p = *plan;
         if (variant == 1) {
@@ -1489,12 +1493,15 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     // The sparse words and the list-major rare kernel add atomically, like
     // the dense tiles, so they run on the side stream beside them.
     const bool side = overlap || s->sparse;
-    GD_HIP(hipEventRecord(ctx->ev_k0, st));
+    if (!ctx->capturing) GD_HIP(hipEventRecord(ctx->ev_k0, st));
     if (side) {
         GD_HIP(hipEventRecord(ctx->ev_fork, st));
         GD_HIP(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
         if (s->sparse) sparse_matrix(ctx, s, r0, r1, c0, c1, upper, d_I, ldI, ctx->side, p.sparse);
-        if (overlap)
+        // beside the sparse kernel the list-major rare kernel goes to the main
+        // stream after the dense tiles (the side stream is busy until the
+        // sparse tiles and their reduce end: C2 0.0185 ms in line there)
+        if (overlap && !s->sparse)
             rare_pairs_kernel<<<grid_for(s->n_rare, 256, 256 * 64), 256, 0, ctx->side>>>(
                 s->post_off.as<int64_t>(), s->post_sets.as<uint32_t>(), s->post_w.as<uint32_t>(), s->n_rare, r0, r1,
                 c0, c1, upper ? 1 : 0, d_I, ldI);
@@ -1553,6 +1560,10 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
             }
         }
     }
+    if (overlap && s->sparse)
+        rare_pairs_kernel<<<grid_for(s->n_rare, 256, 256 * 64), 256, 0, st>>>(
+            s->post_off.as<int64_t>(), s->post_sets.as<uint32_t>(), s->post_w.as<uint32_t>(), s->n_rare, r0, r1, c0,
+            c1, upper ? 1 : 0, d_I, ldI);
     GD_HIP(hipGetLastError());
     ctx->last.launches = 1;
     if (side) GD_HIP(hipStreamWaitEvent(st, ctx->ev_join, 0));
@@ -1578,7 +1589,7 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
         GD_HIP(hipGetLastError());
         ctx->last.launches = 2;
     }
-    GD_HIP(hipEventRecord(ctx->ev_k1, st));
+    if (!ctx->capturing) GD_HIP(hipEventRecord(ctx->ev_k1, st));
     const int64_t lo = std::max(r0, c0), hi = std::min(r1, c1);
     if (!upper && hi > lo) {
         self_pairs_kernel<<<(unsigned)ceil_div(hi - lo, 256), 256, 0, st>>>(s->off.as<int64_t>(), lo, hi, r0, c0, d_I,

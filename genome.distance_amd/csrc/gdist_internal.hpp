@@ -130,6 +130,14 @@ struct SparseScratch {
     bool use_part = false;   // chunks store partials (else flush with atomics)
     int64_t ntiles = 0;
 };
+// One captured step: zero counts, the tile / sparse / rare launches on both
+// streams, the epilogue (gdist_intersect_matrix, option graph)
+struct StepGraph {
+    hipGraphExec_t exec = nullptr;
+    int calls = 0;          // uncaptured calls so far (the first builds the launch plans)
+    bool failed = false;    // capture refused: this key runs uncaptured
+    ~StepGraph() { if (exec) (void)hipGraphExecDestroy(exec); }
+};
 struct MatrixPlan {
     DevBuf tiles;                    // v1: the tile list; v2/v3: the four launch groups
     size_t at[5] = {0, 0, 0, 0, 0};  // group bounds (v2/v3)
@@ -179,6 +187,7 @@ enum Opt : int {
     OPT_SPARSE_CHUNKS,      // chunks of the sparse words per tile (tests; default: parallelism and memory)
     OPT_FOLD_DENSE_WORDS,   // at most this many (padded) dense words are folded into the sparse flush
     OPT_SPARSE_ABL,         // timing ablations of the sparse kernel v2 (results wrong; never in tests)
+    OPT_GRAPH,              // 0: no hipGraph replay of repeated matrix calls
     OPT_COUNT
 };
 extern const char* const kOptNames[OPT_COUNT];
@@ -221,6 +230,15 @@ struct gdist_ctx {
     int nranks = 1, rank = 0;
     // tuning options (gdist_ctx_set_option), kOptUnset = the default
     int64_t opt[gdist::OPT_COUNT];
+    bool capturing = false;                  // a step is being captured into a hipGraph
+    // kernel-time events of the recent matrix calls (a ring): ev_k0 / ev_k1
+    // point at the current call's pair; calls into device outputs return
+    // without waiting, their times are read later (gdist_ctx_recent_timings)
+    static constexpr int kTimingRing = 256;
+    hipEvent_t ring0[kTimingRing] = {}, ring1[kTimingRing] = {};
+    int64_t ring_n = 0;                      // calls whose kernel events were recorded
+    bool pending = false;                    // the last call's times are not read yet
+    bool last_kernel = false;
     gdist_ctx() { for (auto& o : opt) o = gdist::kOptUnset; }
     int64_t option(gdist::Opt o, int64_t dflt) const { return opt[o] == gdist::kOptUnset ? dflt : opt[o]; }
     bool has_option(gdist::Opt o) const { return opt[o] != gdist::kOptUnset; }
@@ -295,6 +313,9 @@ struct gdist_sets {
     bool auto_sorted = false;             // METHOD_AUTO measured the sorted join cheaper
     // bitset_matrix launch plans by (region, kernel switches); cleared with the bitsets
     mutable std::map<std::vector<int64_t>, std::unique_ptr<gdist::MatrixPlan>> plans;
+    // captured steady-state steps (gdist_intersect_matrix into device outputs):
+    // a region's launches replayed as one hipGraph; cleared with the plans
+    mutable std::map<std::vector<int64_t>, std::unique_ptr<gdist::StepGraph>> graphs;
 };
 
 // LSH index of a sketch collection (lsh.hip)

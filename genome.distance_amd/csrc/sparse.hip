@@ -793,6 +793,7 @@ void locus_perm(gdist_ctx* ctx, DevBuf& key, int64_t U, DevBuf& perm) {
 bool locus_order_enabled(const gdist_ctx* ctx) { return ctx->option(OPT_LOCUS_ORDER, 1) != 0; }
 
 void free_sparse(gdist_sets* s) {
+    s->graphs.clear();
     s->plans.clear();
     s->dbits.release();
     s->sp_off.release();

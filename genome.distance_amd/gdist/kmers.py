@@ -109,6 +109,13 @@ class Context:
         L.check(L.lib.gdist_ctx_last_timing(self.h, C.byref(k), C.byref(c), C.byref(n)))
         return k.value, c.value, n.value
 
+    def recent_timings(self, n: int) -> list[float]:
+        """Kernel ms of the last n matrix calls, oldest first (waits for them)."""
+        out = np.zeros(max(n, 1), dtype=np.float64)
+        cnt = C.c_int()
+        L.check(L.lib.gdist_ctx_recent_timings(self.h, int(n), L.ptr(out, C.c_double), C.byref(cnt)))
+        return [float(x) for x in out[:cnt.value]]
+
     def alloc(self, nbytes: int) -> "DeviceBuffer":
         return DeviceBuffer(self, nbytes)
 

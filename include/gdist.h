@@ -80,7 +80,10 @@ extern "C" {
 
 /* distance / matrix flags */
 #define GDIST_UPPER_TRIANGLE 0x100u /* only pairs with global col > global row */
-#define GDIST_OUT_DEVICE     0x200u /* I_out / D_out are device pointers (gdist_dev_alloc) */
+#define GDIST_OUT_DEVICE     0x200u /* I_out / D_out are device pointers (gdist_dev_alloc); the call
+                                       returns once its work is queued on the context's stream:
+                                       gdist_ctx_synchronize, gdist_memcpy_d2h or the next call that
+                                       reads results waits for it */
 #define GDIST_EMPTY_NAN      0x400u /* |A|+|B| == 0 -> NaN instead of 1.0 */
 #define GDIST_SKETCH_JACCARD 0x800u /* sketch distance: plain Jaccard of the two signatures
                                        (default: Mash bottom-s of the union) */
@@ -116,6 +119,9 @@ int  gdist_ctx_synchronize(gdist_ctx* ctx);
 /* HIP-event time of the last intersect/sketch matrix call's main kernel(s)
  * and of the whole call, in ms (recorded on the stream they run on). */
 int  gdist_ctx_last_timing(gdist_ctx* ctx, double* kernel_ms, double* call_ms, int64_t* launches);
+/* Kernel times (ms, HIP events on the stream they ran on) of the last
+ * min(max, 256) matrix calls, oldest first, *count of them; waits for them. */
+int  gdist_ctx_recent_timings(gdist_ctx* ctx, int max, double* kernel_ms, int* count);
 /* Tuning options of a context: the A/B switches of DESIGN.md §5 by name
  * ("rare_t", "bitset_kernel", "sparse", "sparse_zmax", "sketch_k", ...;
  * gdist_ctx_option_name enumerates them, EINVAL past the last). Every option

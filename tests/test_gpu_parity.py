@@ -598,7 +598,7 @@ def test_sparse_complement_words_exact(ctx, mode, opts):
                 # a dense-only dictionary: the substitution kmers two or more
                 # sets share are dense too, and their words are counted from
                 # the set bits (positive-sparse) beside the complement words
-                "two_sided": {"rare_t": 2},
+                "two_sided": {"rare_t": 2, "guides": 4},
                 # the dense words counted in the sparse flush (reduce kernel / one chunk's atomics)
                 "mixed_fold": {"sparse_zmax": 12, "fold_dense_words": 100000, "sparse_chunks": 3},
                 "mixed_fold_1chunk": {"sparse_zmax": 12, "fold_dense_words": 100000, "sparse_chunks": 1}}
@@ -765,3 +765,33 @@ def test_width_processor_vs_restatement(ctx):
         tgt = max(tgt, good)
     assert out.getvalue().splitlines() == exp
     assert target == tgt
+
+
+@pytest.mark.parametrize("sparse", [True, False])
+def test_graph_replay_of_repeated_steps(ctx, opts, sparse):
+    """Repeated matrix calls into the same device outputs replay the step as
+    a hipGraph (option graph): the second call is captured, later calls
+    launch the graph. Every call — including after the outputs were
+    overwritten — equals the oracle, and equals the uncaptured path."""
+    import gdist
+    n = 300
+    seqs = synth_sets(n, 20000, 0.003, 107)
+    opts(sparse_zmax=100000 if sparse else None, sparse=None if sparse else 0)
+    sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
+    sets.build_bitsets()
+    assert (sets.sparse_info()[0] > 0) == sparse
+    off, codes = oracle_pack(seqs, 21, 0, 0)
+    for (r0, r1) in [(0, n), (37, 211)]:
+        eI, eD = oracle.matrix(off, codes, r0, r1, 0, n, flags=0x100)
+        nr = r1 - r0
+        dI, dD = ctx.alloc(nr * n * 4), ctx.alloc(nr * n * 8)
+        mask = np.fromfunction(lambda a, b: b > (r0 + a), (nr, n))
+        for call in range(4):
+            dI.from_host(np.full(nr * n, -7, np.int32))
+            dD.from_host(np.full(nr * n, 42.5))
+            sets.matrix_device(dI.ptr, dD.ptr, n, (r0, r1), (0, n), upper=True, method=gdist.METHOD_BITSET)
+            I = dI.to_host(np.int32).reshape(nr, n)
+            D = dD.to_host(np.float64).reshape(nr, n)
+            assert np.array_equal(I[mask], eI[mask]) and bits_equal(D[mask], eD[mask]), (r0, call)
+            assert np.all(I[~mask] == -7), (r0, call)           # below the diagonal untouched
+        dI.free(); dD.free()
