@@ -25,6 +25,7 @@ const char* const kOptNames[OPT_COUNT] = {
     "reps_block",      "locus_order",     "sparse",          "sparse_zmax",     "sparse_wg_per_cu",
     "sparse_occ",      "sparse_sun",      "sketch_k",        "sketch_tile",     "sparse_part_budget",
     "guides",          "force_exchange",  "sparse_kernel",   "sparse_chunks",   "fold_dense_words", "sparse_abl",      "graph",
+    "sparse_shape",    "sparse_absorb",   "sparse_balance",  "sparse_fold",
 };
 
 static int option_index(const char* name) {

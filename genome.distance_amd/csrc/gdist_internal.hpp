@@ -126,6 +126,7 @@ inline void d2h(void* dst, const void* src, size_t bytes, hipStream_t s) {
 struct SparseScratch {
     bool ready = false;
     DevBuf tiles, part;   // tile list, per-chunk counters
+    DevBuf bounds;        // int32 [nchunks + 1]: first sparse word of each chunk (cost-balanced)
     int nchunks = 0;
     bool use_part = false;   // chunks store partials (else flush with atomics)
     int64_t ntiles = 0;
@@ -177,17 +178,23 @@ enum Opt : int {
     OPT_SPARSE_ZMAX,        // words with z_w <= ZMAX are sparse (forces the split)
     OPT_SPARSE_WG_PER_CU,   // chunking target of the sparse tiles (default 4)
     OPT_SPARSE_OCC,         // 3: sparse kernel built for 3 instead of 8 waves per SIMD
-    OPT_SPARSE_SUN,         // products per lane in flight (4 / 6 / 8, default 6)
+    OPT_SPARSE_SUN,         // product slots per lane in flight (v1: 4 / 6 / 8, default 6; v5: 4 / 6; v6: 2 / 3 / 4, default 3)
     OPT_SKETCH_K,           // sketch merge window (1 / 2 / 4 / 6, default 2)
     OPT_SKETCH_TILE,        // 16: force the 16x16 sketch tile
     OPT_SPARSE_PART_BUDGET, // bytes of sparse chunk partials one region may hold
     OPT_GUIDES,             // guide sequences keyed at pack time (default kGuides)
     OPT_FORCE_EXCHANGE,     // 1: a one-rank communicator runs every collective (tests)
-    OPT_SPARSE_KERNEL,      // sparse tile kernel 1 (word + byte loads, default) / 2 (LDS-staged) / 3 (16-byte records)
+    OPT_SPARSE_KERNEL,      // sparse tile kernel 1 (word + byte loads) / 2 (LDS-staged) / 3 (16-byte records) /
+                            // 4 (LDS grid) / 5 (v1 walk re-laid) / 6 (micro-tiles, default)
     OPT_SPARSE_CHUNKS,      // chunks of the sparse words per tile (tests; default: parallelism and memory)
     OPT_FOLD_DENSE_WORDS,   // at most this many (padded) dense words are folded into the sparse flush
     OPT_SPARSE_ABL,         // timing ablations of the sparse kernel v2 (results wrong; never in tests)
     OPT_GRAPH,              // 0: no hipGraph replay of repeated matrix calls
+    OPT_SPARSE_SHAPE,       // v6 micro-tile rows x columns: 12 (default) / 14 / 22
+    OPT_SPARSE_ABSORB,      // 1: every word sparse (no dense-word launch; default 0)
+    OPT_SPARSE_BALANCE,     // 1: chunk bounds at equal modelled cost, words dealt to waves one at a time
+    OPT_SPARSE_FOLD,        // at most this many (padded) dense words counted inside the v5 / v6 tile kernel
+                            // (8 per chunk; default 64, 0: the dense-word tile launch)
     OPT_COUNT
 };
 extern const char* const kOptNames[OPT_COUNT];
@@ -305,9 +312,12 @@ struct gdist_sets {
     int64_t sp_entries = 0, sp_U = 0;     // entries; valid bits of the sparse words
     int sp_win = 0;                       // v2 kernel window (aligned sparse words), 0: v1 only
     int64_t sp_pos_words = 0;             // sparse words counted from their set bits (positive-sparse)
-    bool sp_fold_dense = false;           // the dense words are counted in the sparse flush (no tile launch)
+    bool sp_fold_dense = false;           // the dense words are counted by the sparse kernels (no tile launch):
+    int sp_fold_slabs = 0;                // ... in the tile kernel (v5 / v6), 8 words per chunk, when > 0;
+                                          // else in the flush / reduce (option fold_dense_words, sp_dT)
     gdist::DevBuf sp_dT;                  // uint64 [Wd][nsets]: the dense words word-major, for the fold
     std::vector<int32_t> sp_bucket_bits;  // [nsets][sp_nbk]: complement bits per set and 1024 sparse words
+    std::vector<double> sp_cost;          // [Ws + 1]: prefix of each sparse word's modelled cost over all tiles
     int64_t sp_nbk = 0;
     double sp_products = 0, sp_items = 0; // whole-triangle products / (tile, word) visits (cost model)
     bool auto_sorted = false;             // METHOD_AUTO measured the sorted join cheaper
@@ -427,9 +437,10 @@ constexpr int kGuides = 2;                       // guide sequences per packed c
 constexpr int kSparseStageEntries = 640;         // sparse v2: entries per side a window may hold
 constexpr int kFoldDenseWords = 0;               // dense words folded into the sparse flush: off (the
                                                  // tile launch overlaps the sparse kernel; the fold runs after it)
-constexpr double kSparseProductsPerS = 2.6e11;   // sparse tiles: complement-word products (C2)
-constexpr double kSparseItemsPerS = 6.0e10;      // sparse tiles: (tile, sparse word) visits (C2)
-constexpr double kDenseLaunchFixedS = 6.0e-5;    // a dense-word tile launch beside the sparse kernel (C2: 64 words 0.09 ms)
+constexpr double kSparseProductsPerS = 6.5e11;   // sparse tiles (v6): complement-word products (C2)
+constexpr double kSparseItemsPerS = 1.0e11;      // sparse tiles (v6): (tile, sparse word) visits (C2)
+constexpr double kDenseLaunchFixedS = 6.0e-5;    // a dense-word tile launch beside the sparse kernel (C2: 64 words
+                                                 // 0.09 + 0.04 ms of tiles sharing the CUs with the sparse kernel)
 bool locus_order_enabled(const gdist_ctx* ctx);  // option locus_order = 0 keeps code order (A/B)
 // key[r] = tag | guide position of dense rank r; kmers no guide holds sort
 // after every guide key by the number of sets holding them (dcounts)

@@ -202,6 +202,10 @@ constexpr int SNT = 512;                 // threads per workgroup (4 per CU, LDS
 // sparse words, so a pair's count in one chunk is at most 64 x 1023 < 2^16
 // and a packed ds_add_u32 never carries into the neighbour (32 KiB per tile)
 constexpr int kChunkWords = 1023;
+// dense words per in-kernel fold slab (v5 / v6): a pair gains at most
+// 64 x 8 in the chunk that folds a slab, so such chunks hold at most
+// kChunkWords - kFoldSlabWords sparse words
+constexpr int kFoldSlabWords = 8;
 constexpr int SNW = SNT / 64;
 
 // LDS counter of local pair (row a, column b): the column is rotated by the
@@ -239,7 +243,7 @@ template <int SUN, int OCC, bool E16 = false>
 __global__ __launch_bounds__(SNT, OCC) void sparse_tile_kernel(
     const int64_t* __restrict__ off, const unsigned long long* __restrict__ word, const uint8_t* __restrict__ set,
     const ulonglong2* __restrict__ ent,
-    const int32_t* __restrict__ nc, int64_t Us, int64_t Ws, const int2* __restrict__ tiles, int nchunks,
+    const int32_t* __restrict__ nc, int64_t Us, int64_t Ws, const int2* __restrict__ tiles, const int32_t* __restrict__ cbnd, int nchunks,
     int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I, int64_t ldI,
     int32_t* __restrict__ part, const unsigned long long* __restrict__ dbits, int64_t Wdp, int64_t N) {
     __shared__ uint32_t cnt[SB * SB / 2];                                  // 32 KiB, 16-bit counters
@@ -258,7 +262,7 @@ __global__ __launch_bounds__(SNT, OCC) void sparse_tile_kernel(
     for (int t = threadIdx.x; t < SB * SB / 2; t += SNT) cnt[t] = 0;
     __syncthreads();
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t sb = Ws * ch / nchunks, se = Ws * (ch + 1) / nchunks;
+    const int64_t sb = cbnd[ch], se = cbnd[ch + 1];          // the chunk's sparse words
     const int64_t* offA = off + A * Ws;
     const int64_t* offB = off + B * Ws;
     const int64_t ra0 = offA[sb], cb0 = offB[sb];           // chunk bases (< 2^31 entries per chunk)
@@ -407,7 +411,7 @@ constexpr int S2E = kSparseStageEntries;   // staged entries per side and window
 template <int SUN, int OCC, int ABL = 0>
 __global__ __launch_bounds__(S2T, OCC) void sparse_tile_kernel2(
     const int64_t* __restrict__ off, const unsigned long long* __restrict__ word, const uint8_t* __restrict__ set,
-    const int32_t* __restrict__ nc, int64_t Us, int64_t Ws, int win, const int2* __restrict__ tiles, int nchunks,
+    const int32_t* __restrict__ nc, int64_t Us, int64_t Ws, int win, const int2* __restrict__ tiles, const int32_t* __restrict__ cbnd, int nchunks,
     int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I, int64_t ldI,
     int32_t* __restrict__ part, const unsigned long long* __restrict__ dbits, int64_t Wdp, int64_t N) {
     __shared__ uint32_t cnt[SB * SB / 2];                  // 32 KiB, 16-bit counters (cnt_index layout)
@@ -425,7 +429,7 @@ __global__ __launch_bounds__(S2T, OCC) void sparse_tile_kernel2(
     const bool diag = A == B && !rpart, mirror = diag && !upper;
     for (int t = threadIdx.x; t < SB * SB / 2; t += S2T) cnt[t] = 0;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t sb = Ws * ch / nchunks, se = Ws * (ch + 1) / nchunks;
+    const int64_t sb = cbnd[ch], se = cbnd[ch + 1];          // the chunk's sparse words
     const int64_t* offA = off + A * Ws;
     const int64_t* offB = off + B * Ws;
     const unsigned long long* cw = diag ? wA : wB;
@@ -581,7 +585,7 @@ __global__ __launch_bounds__(S2T, OCC) void sparse_tile_kernel2(
 template <int U, int OCC>
 __global__ __launch_bounds__(S2T, OCC) void sparse_tile_kernel4(
     const int64_t* __restrict__ off, const unsigned long long* __restrict__ word, const uint8_t* __restrict__ set,
-    const int32_t* __restrict__ nc, int64_t Us, int64_t Ws, int win, const int2* __restrict__ tiles, int nchunks,
+    const int32_t* __restrict__ nc, int64_t Us, int64_t Ws, int win, const int2* __restrict__ tiles, const int32_t* __restrict__ cbnd, int nchunks,
     int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I, int64_t ldI,
     int32_t* __restrict__ part, const unsigned long long* __restrict__ dbits, int64_t Wdp, int64_t N) {
     __shared__ uint32_t cnt[SB * SB / 2];                  // 32 KiB, 16-bit counters (cnt_index layout)
@@ -596,7 +600,7 @@ __global__ __launch_bounds__(S2T, OCC) void sparse_tile_kernel4(
     const bool diag = A == B && !rpart, mirror = diag && !upper;
     for (int t = threadIdx.x; t < SB * SB / 2; t += S2T) cnt[t] = 0;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t sb = Ws * ch / nchunks, se = Ws * (ch + 1) / nchunks;
+    const int64_t sb = cbnd[ch], se = cbnd[ch + 1];          // the chunk's sparse words
     const int64_t* offA = off + A * Ws;
     const int64_t* offB = off + B * Ws;
     const unsigned long long* cw = diag ? wA : wB;
@@ -730,7 +734,299 @@ __global__ __launch_bounds__(S2T, OCC) void sparse_tile_kernel4(
     }
 }
 
-// the chunks' counters of each tile + the constant part, into I
+// ---- v5 / v6: v1's flattened walk, laid out for issue --------------------
+// The products and the walk of v1; what changes is the instruction stream
+// per product (round-2 ISA of v1: the diagonal/off-diagonal choice and the
+// +-1 correction of the quotient compiled to exec-mask branches inside every
+// product slot, four dependent LDS reads per slot, quarter-rate 32-bit
+// multiplies, and the set-byte loads sunk behind the counter branch):
+//   * diagonal and off-diagonal tiles run separate instantiations of the
+//     walk (one uniform branch per batch);
+//   * a word's walk fields are one 16-byte LDS record {pre | ncol << 24,
+//     row start, column start, 1 / ncol}: one ds_read_b128 per slot, all
+//     SUN slots' reads issued before any is used;
+//   * the quotient correction is select-only, multiplies are 24-bit;
+//   * an entry is one 16-byte {word, set} record (one load per side, scalar
+//     base + 32-bit offset);
+//   * the counter add is unconditional (a zero product adds 0), so no slot
+//     waits on another's branch; idle slots (f >= total) read the zero
+//     sentinel record past the last entry instead of being masked.
+// v5 keeps one product per slot; v6 (below) walks micro-tiles.
+struct SparseWalk {
+    const ulonglong2* eA;                 // the chunk's row-side records
+    const ulonglong2* eB;                 // ... and column-side records
+};
+
+// Word of product (slot) f: #{l : incl_l <= f} (v1's search). Words w0 and
+// w0 + 1 unconditionally (a word past w1 ends after f: it adds 0), the rest
+// (more than two words ending inside the slot group) in a loop.
+__device__ __forceinline__ int slot_word(int incl, int F, int f) {
+    const int w0 = __builtin_amdgcn_readfirstlane(__popcll(__ballot(incl <= F)));
+    const int w1 = __builtin_amdgcn_readfirstlane(__popcll(__ballot(incl <= F + 63)));
+    const int l1 = w0 < 63 ? w0 + 1 : 63;
+    int lo = w0 + (__builtin_amdgcn_readlane(incl, w0 < 63 ? w0 : 63) <= f) +
+             (__builtin_amdgcn_readlane(incl, l1) <= f);
+    for (int l = w0 + 2; l < w1; l++) lo += __builtin_amdgcn_readlane(incl, l) <= f;
+    return lo < 63 ? lo : 63;
+}
+
+// zc: the sentinel record relative to the column side's base
+template <int SUN, bool DIAG>
+__device__ __forceinline__ void sparse_walk5(const int4* __restrict__ rec, int incl, int total, int lane,
+                                             const SparseWalk& e, uint32_t zc, uint32_t* __restrict__ cnt,
+                                             bool mirror) {
+    const char* beA = reinterpret_cast<const char*>(e.eA);
+    const char* beB = reinterpret_cast<const char*>(DIAG ? e.eA : e.eB);
+    for (int fb = 0; fb < total; fb += 64 * SUN) {
+        int4 r[SUN];
+        int f[SUN];
+#pragma unroll
+        for (int u = 0; u < SUN; u++) {
+            f[u] = fb + 64 * u + lane;
+            r[u] = rec[slot_word(incl, fb + 64 * u, f[u])];
+        }
+        uint32_t ri[SUN], ci[SUN];
+#pragma unroll
+        for (int u = 0; u < SUN; u++) {
+            const bool ok = f[u] < total;
+            const int q = f[u] - (r[u].x & 0xFFFFFF);
+            int rr, cc;
+            if (DIAG) {                        // q -> pair (y, x), y < x: q = x(x-1)/2 + y
+                int x = (int)((1.0f + __builtin_amdgcn_sqrtf(1.0f + 8.0f * (float)q)) * 0.5f);
+                const int t = (int)(__umul24(x, x - 1) >> 1);
+                // x -= 1 when t > q, x += 1 when (x + 1) x / 2 <= q: arithmetic, not branches
+                const int dn = (int)(t > q), up = (int)(t + x <= q);
+                const int xc = x + up - dn;
+                const int tc = t + __mul24(up, x) - __mul24(dn, x - 1);
+                rr = r[u].y + (q - tc);
+                cc = r[u].y + xc;
+            } else {
+                const int n2 = (int)((uint32_t)r[u].x >> 24);
+                const int x = (int)((float)q * __int_as_float(r[u].w));
+                const int t = (int)__umul24(x, n2);
+                const int adj = (int)(t + n2 <= q) - (int)(t > q);   // the quotient's +-1, select-free
+                const int xc = x + adj;
+                const int tc = (int)__umul24(xc, n2);
+                rr = r[u].y + xc;
+                cc = r[u].z + (q - tc);
+            }
+            ri[u] = ok ? (uint32_t)rr : 0u;
+            ci[u] = ok ? (uint32_t)cc : zc;
+        }
+        ulonglong2 a[SUN], b[SUN];
+#pragma unroll
+        for (int u = 0; u < SUN; u++) {
+            a[u] = *reinterpret_cast<const ulonglong2*>(beA + (ri[u] << 4));
+            b[u] = *reinterpret_cast<const ulonglong2*>(beB + (ci[u] << 4));
+        }
+#pragma unroll
+        for (int u = 0; u < SUN; u++) {
+            const uint32_t sr = (uint32_t)a[u].y, sc = (uint32_t)b[u].y;
+            const uint32_t v = (uint32_t)__popcll(a[u].x & b[u].x);
+            const uint32_t t0 = sr * SB + ((sc + sr) & (SB - 1));
+            atomicAdd(&cnt[t0 >> 1], v << ((t0 & 1) << 4));
+            if (DIAG && mirror) {
+                const uint32_t t1 = sc * SB + ((sr + sc) & (SB - 1));
+                atomicAdd(&cnt[t1 >> 1], v << ((t1 & 1) << 4));
+            }
+        }
+    }
+}
+
+// v6 (off-diagonal tiles): a product slot is a micro-tile of RW adjacent
+// rows x CW adjacent columns of one word: nrp = ceil(nr / RW) x ncp =
+// ceil(ncol / CW) slots per word. One search and quotient per RW x CW
+// products; the records of a slot's rows (and columns) are adjacent, one
+// offset each, immediates +16 for the rest. Rows / columns past a list's end
+// read the next records (or the zero sentinels past the last one) and add 0.
+// Record: {pre | ncol << 24, row start, column start, 1 / ncp with nr in the
+// low 8 mantissa bits} (the quotient tolerates the 2^-15 error, q < 2^14).
+template <int SUN, int RW, int CW>
+__device__ __forceinline__ void sparse_walk6(const int4* __restrict__ rec, int incl, int total, int lane,
+                                             const SparseWalk& e, uint32_t zc, uint32_t* __restrict__ cnt) {
+    const char* beA = reinterpret_cast<const char*>(e.eA);
+    const char* beB = reinterpret_cast<const char*>(e.eB);
+    for (int fb = 0; fb < total; fb += 64 * SUN) {
+        int4 r[SUN];
+        int f[SUN];
+#pragma unroll
+        for (int u = 0; u < SUN; u++) {
+            f[u] = fb + 64 * u + lane;
+            r[u] = rec[slot_word(incl, fb + 64 * u, f[u])];
+        }
+        uint32_t ri[SUN], ci[SUN];
+        int nrow[SUN], ncol[SUN];                      // valid rows / columns of the slot
+#pragma unroll
+        for (int u = 0; u < SUN; u++) {
+            const bool ok = f[u] < total;
+            const int q = f[u] - (r[u].x & 0xFFFFFF);
+            const int ncl = (int)((uint32_t)r[u].x >> 24);
+            const int ncp = (ncl + CW - 1) / CW;
+            const int x = (int)((float)q * __int_as_float(r[u].w));
+            const int t = (int)__umul24(x, ncp);
+            const int adj = (int)(t + ncp <= q) - (int)(t > q);
+            const int xc = x + adj;
+            const int yc = (q - (int)__umul24(xc, ncp)) * CW;
+            ncol[u] = ncl - yc;
+            nrow[u] = RW > 1 ? (r[u].w & 0xFF) - xc * RW : 1;
+            ri[u] = ok ? (uint32_t)(r[u].y + xc * RW) : 0u;
+            ci[u] = ok ? (uint32_t)(r[u].z + yc) : zc;
+        }
+        ulonglong2 a[SUN][RW], b[SUN][CW];
+#pragma unroll
+        for (int u = 0; u < SUN; u++) {
+            const char* pa = beA + (ri[u] << 4);
+            const char* pb = beB + (ci[u] << 4);
+#pragma unroll
+            for (int i = 0; i < RW; i++) a[u][i] = *reinterpret_cast<const ulonglong2*>(pa + 16 * i);
+#pragma unroll
+            for (int j = 0; j < CW; j++) b[u][j] = *reinterpret_cast<const ulonglong2*>(pb + 16 * j);
+        }
+#pragma unroll
+        for (int u = 0; u < SUN; u++)
+#pragma unroll
+            for (int i = 0; i < RW; i++) {
+                const uint32_t sr = (uint32_t)a[u][i].y;
+#pragma unroll
+                for (int j = 0; j < CW; j++) {
+                    const bool in = (i == 0 || i < nrow[u]) && (j == 0 || j < ncol[u]);
+                    const uint32_t v = in ? (uint32_t)__popcll(a[u][i].x & b[u][j].x) : 0u;
+                    const uint32_t t0 = sr * SB + (((uint32_t)b[u][j].y + sr) & (SB - 1));
+                    atomicAdd(&cnt[t0 >> 1], v << ((t0 & 1) << 4));
+                }
+            }
+    }
+}
+
+// RW = CW = 0: v5 (one product per slot); otherwise v6 with RW x CW
+// micro-tiles on the off-diagonal tiles (diagonal tiles walk v5's pairs)
+template <int SUN, int OCC, int RW = 0, int CW = 0>
+__global__ __launch_bounds__(SNT, OCC) void sparse_tile_kernel5(
+    const int64_t* __restrict__ off, const uint8_t* __restrict__ set, const ulonglong2* __restrict__ ent,
+    const int32_t* __restrict__ nc, int64_t Us, int64_t Ws, const int2* __restrict__ tiles, const int32_t* __restrict__ cbnd, int nchunks,
+    int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I, int64_t ldI,
+    int32_t* __restrict__ part, const unsigned long long* __restrict__ dbits, int64_t Wdp, int64_t N, int il,
+    const unsigned long long* __restrict__ slab_bits, int slabs) {
+    // dbits: the flush-fold dense words (word-major, option fold_dense_words);
+    // slab_bits / slabs: the in-kernel fold's dense words (set-major [N][Wdp])
+    __shared__ uint32_t cnt[SB * SB / 2];                  // 32 KiB, 16-bit counters (cnt_index layout)
+    __shared__ int4 rec[SNW][64];                          // 8 KiB: the batch's walk records
+    const int tile = blockIdx.x / nchunks, ch = blockIdx.x % nchunks;
+    const int64_t A = tiles[tile].x, B = tiles[tile].y;
+    const int rlo = (int)(r0 - A * SB > 0 ? r0 - A * SB : 0);
+    const int rhi = (int)(r1 - A * SB < SB ? r1 - A * SB : SB);
+    const bool rpart = rlo > 0 || rhi < SB;
+    const bool diag = A == B && !rpart, mirror = diag && !upper;
+    for (int t = threadIdx.x; t < SB * SB / 2; t += SNT) cnt[t] = 0;
+    __syncthreads();
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int64_t sb = cbnd[ch], se = cbnd[ch + 1];          // the chunk's sparse words
+    const int64_t* offA = off + A * Ws;
+    const int64_t* offB = off + B * Ws;
+    const int64_t ra0 = offA[sb], cb0 = offB[sb];           // chunk bases (< 2^31 entries per chunk)
+    const SparseWalk e{ent + ra0, ent + cb0};
+    const int64_t ntot = off[(int64_t)ceil_div(N, SB) * Ws];         // entries of every block: the sentinel
+    const uint32_t zA = (uint32_t)(ntot - ra0), zB = (uint32_t)(ntot - cb0);
+    // batches of 64 consecutive words per wave, or (il, option
+    // sparse_balance) the words dealt to the waves one at a time (word
+    // sb + 8 j + wv, j = 64 k + lane), so that a run of heavy words spreads
+    // over all eight waves instead of one wave's batch
+    const int64_t wfirst = il ? wv : (int64_t)wv * 64, lstride = il ? SNW : 1;
+    for (int64_t k0 = 0; sb + k0 * SNW + wfirst < se; k0 += 64) {
+        const int64_t s = sb + k0 * SNW + wfirst + lane * lstride;
+        int64_t rb = ra0, cb = cb0;
+        int nr = 0, ncl = 0;
+        if (s < se) {
+            rb = offA[s]; nr = (int)(offA[s + 1] - rb);
+            cb = offB[s]; ncl = (int)(offB[s + 1] - cb);
+            if (rpart) {                               // lists are sorted by set: trim both ends
+                int a = 0, en = nr;
+                for (int t = 0; t < nr; t++) {
+                    const int st = set[rb + t];
+                    a += st < rlo;
+                    en -= st >= rhi;
+                }
+                rb += a;
+                nr = en > a ? en - a : 0;
+            }
+        }
+        // v6: slots per row group / row groups (micro-tiles of RW x CW)
+        const int ncd = CW && !diag ? (ncl + CW - 1) / (CW ? CW : 1) : ncl;
+        const int nrd = RW && !diag ? (nr + RW - 1) / (RW ? RW : 1) : nr;
+        const int P = diag ? nr * (nr - 1) / 2 : nrd * ncd;
+        int incl = P;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += v;
+        }
+        // pre < 2^24 (64 words x 128 x 128 products), ncol <= 128
+        const int rcp = __float_as_int(ncd ? __builtin_amdgcn_rcpf((float)ncd) : 0.0f);
+        rec[wv][lane] = make_int4((incl - P) | (ncl << 24), (int32_t)(rb - ra0), (int32_t)(cb - cb0),
+                                  RW > 1 && !diag ? (rcp & ~0xFF) | nr : rcp);
+        const int total = __builtin_amdgcn_readlane(incl, 63);      // uniform: the walk's loop stays scalar
+        __builtin_amdgcn_wave_barrier();
+        if (diag) sparse_walk5<SUN, true>(rec[wv], incl, total, lane, e, zA, cnt, mirror);
+        else if (CW) sparse_walk6<SUN, RW ? RW : 1, CW ? CW : 1>(rec[wv], incl, total, lane, e, zB, cnt);
+        else sparse_walk5<SUN, false>(rec[wv], incl, total, lane, e, zB, cnt, false);
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (ch < slabs) {
+        // dense words [8 ch, 8 ch + 8) of the tile's 128 x 128 pairs: the
+        // rows' words staged in the record area (8 KiB), a thread holds one
+        // column's 8 words and walks 32 rows (broadcast LDS reads)
+        __syncthreads();                                   // every wave is done with its records
+        unsigned long long* As = reinterpret_cast<unsigned long long*>(&rec[0][0]);
+        const int64_t w0 = (int64_t)ch * kFoldSlabWords;
+        for (int t = threadIdx.x; t < SB * kFoldSlabWords; t += SNT) {
+            const int64_t i = A * SB + (t >> 3);
+            As[t] = i < N ? slab_bits[i * Wdp + w0 + (t & 7)] : 0ull;
+        }
+        __syncthreads();
+        const int b = threadIdx.x & (SB - 1), rg = threadIdx.x >> 7;
+        const int64_t j = B * SB + b;
+        if (j < N) {
+            unsigned long long bw[kFoldSlabWords];
+#pragma unroll
+            for (int k = 0; k < kFoldSlabWords; k++) bw[k] = slab_bits[j * Wdp + w0 + k];
+            for (int a = rg * (SB / 4); a < (rg + 1) * (SB / 4); a++) {
+                const ulonglong2* ar = reinterpret_cast<const ulonglong2*>(As + a * kFoldSlabWords);
+                uint32_t v = 0;
+#pragma unroll
+                for (int k = 0; k < kFoldSlabWords / 2; k++) {
+                    const ulonglong2 x = ar[k];
+                    v += (uint32_t)__popcll(x.x & bw[2 * k]) + (uint32_t)__popcll(x.y & bw[2 * k + 1]);
+                }
+                const int t0 = cnt_index(a, b);
+                atomicAdd(&cnt[t0 >> 1], v << ((t0 & 1) << 4));
+            }
+        }
+    }
+    __syncthreads();
+    if (part) {
+        uint32_t* dst = reinterpret_cast<uint32_t*>(part) + ((int64_t)tile * nchunks + ch) * (SB * SB / 2);
+        for (int t = threadIdx.x; t < SB * SB / 2; t += SNT) dst[t] = cnt[t];
+        return;
+    }
+    for (int t = threadIdx.x; t < SB * SB; t += SNT) {
+        const int a = t >> 7, b = ((t & (SB - 1)) - a) & (SB - 1);
+        const int64_t i = A * SB + a, j = B * SB + b;
+        if (i < r0 || i >= r1 || j < c0 || j >= c1 || (upper && j <= i)) continue;
+        const int v = (int)((cnt[t >> 1] >> ((t & 1) << 4)) & 0xFFFFu) +
+                      (ch == 0 ? (int)Us - nc[i] - nc[j] + dense_pair(dbits, Wdp, N, i, j) : 0);
+        if (v) atomicAdd(I + (i - r0) * ldI + (j - c0), v);
+    }
+}
+
+// the chunks' counters of each tile + the constant part, into I. A lane
+// owns 8 counters (one 16-byte word of a chunk's partial); the four waves of
+// a workgroup take every fourth chunk of the same 64 words (independent
+// 16-byte loads, several in flight per lane), sum through LDS, and wave 0
+// adds the 512 counters into I. 32 workgroups per tile: the loads of the
+// whole grid in flight cover the latency of the partials' read (round 2: one
+// workgroup per CU, 62 loads per lane in a chain, ran at ~2 TB/s).
+constexpr int kReduceCnt = 8;
+constexpr int kReduceGroups = 64;                            // 16-byte groups per workgroup
 __global__ __launch_bounds__(256) void sparse_reduce_kernel(const int32_t* __restrict__ part, int nchunks,
                                                             const int2* __restrict__ tiles,
                                                             const int32_t* __restrict__ nc, int64_t Us, int64_t r0,
@@ -738,15 +1034,42 @@ __global__ __launch_bounds__(256) void sparse_reduce_kernel(const int32_t* __res
                                                             int32_t* __restrict__ I, int64_t ldI,
                                                             const unsigned long long* __restrict__ dbits,
                                                             int64_t Wdp, int64_t N) {
-    const int tile = blockIdx.x / (SB * SB / 256);
-    const int t = (blockIdx.x % (SB * SB / 256)) * 256 + threadIdx.x;     // counter slot (cnt_index layout)
-    const int a = t >> 7, b = ((t & (SB - 1)) - a) & (SB - 1);
-    const int64_t i = (int64_t)tiles[tile].x * SB + a, j = (int64_t)tiles[tile].y * SB + b;
-    if (i < r0 || i >= r1 || j < c0 || j >= c1 || (upper && j <= i)) return;
-    int v = (int)Us - nc[i] - nc[j] + dense_pair(dbits, Wdp, N, i, j);
-    const uint32_t* p = reinterpret_cast<const uint32_t*>(part) + (int64_t)tile * nchunks * (SB * SB / 2) + (t >> 1);
-    for (int c = 0; c < nchunks; c++) v += (int)((p[(int64_t)c * (SB * SB / 2)] >> ((t & 1) << 4)) & 0xFFFFu);
-    if (v) atomicAdd(I + (i - r0) * ldI + (j - c0), v);
+    constexpr int per_tile = SB * SB / kReduceCnt / kReduceGroups;       // workgroups per tile
+    __shared__ uint32_t sum[4][kReduceCnt][kReduceGroups];               // 8 KiB
+    const int tile = blockIdx.x / per_tile;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int g = (blockIdx.x % per_tile) * kReduceGroups + lane;        // 16-byte group of the tile's counters
+    const uint4* p = reinterpret_cast<const uint4*>(part) + (int64_t)tile * nchunks * (SB * SB / 8) + g;
+    uint32_t acc[kReduceCnt] = {0, 0, 0, 0, 0, 0, 0, 0};
+    auto add = [&](const uint4& v) {
+        acc[0] += v.x & 0xFFFFu; acc[1] += v.x >> 16;
+        acc[2] += v.y & 0xFFFFu; acc[3] += v.y >> 16;
+        acc[4] += v.z & 0xFFFFu; acc[5] += v.z >> 16;
+        acc[6] += v.w & 0xFFFFu; acc[7] += v.w >> 16;
+    };
+    int c = wv;
+    for (; c + 12 < nchunks; c += 16) {
+        uint4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) v[k] = p[(int64_t)(c + 4 * k) * (SB * SB / 8)];
+#pragma unroll
+        for (int k = 0; k < 4; k++) add(v[k]);
+    }
+    for (; c < nchunks; c += 4) add(p[(int64_t)c * (SB * SB / 8)]);
+#pragma unroll
+    for (int k = 0; k < kReduceCnt; k++) sum[wv][k][lane] = acc[k];
+    __syncthreads();
+    // 512 counters per workgroup: each thread finalizes two
+    for (int e = threadIdx.x; e < kReduceCnt * kReduceGroups; e += 256) {
+        const int gl = e / kReduceCnt, k = e % kReduceCnt;               // consecutive threads: consecutive counters
+        const uint32_t tot = sum[0][k][gl] + sum[1][k][gl] + sum[2][k][gl] + sum[3][k][gl];
+        const int t = ((blockIdx.x % per_tile) * kReduceGroups + gl) * kReduceCnt + k;   // cnt_index layout
+        const int a = t >> 7, b = ((t & (SB - 1)) - a) & (SB - 1);
+        const int64_t i = (int64_t)tiles[tile].x * SB + a, j = (int64_t)tiles[tile].y * SB + b;
+        if (i < r0 || i >= r1 || j < c0 || j >= c1 || (upper && j <= i)) continue;
+        const int v = (int)Us - nc[i] - nc[j] + dense_pair(dbits, Wdp, N, i, j) + (int)tot;
+        if (v) atomicAdd(I + (i - r0) * ldI + (j - c0), v);
+    }
 }
 
 }  // namespace
@@ -804,9 +1127,11 @@ void free_sparse(gdist_sets* s) {
     s->sparse = false;
     s->Wd = s->Ws = s->sp_entries = s->sp_U = 0;
     s->sp_bucket_bits.clear();
+    s->sp_cost.clear();
     s->sp_nbk = 0;
     s->sp_pos_words = 0;
     s->sp_fold_dense = false;
+    s->sp_fold_slabs = 0;
     s->sp_dT.release();
     s->sp_win = 0;
     s->sp_products = s->sp_items = 0.0;
@@ -864,7 +1189,41 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
         if (sparse) { sw.push_back((int32_t)w); products += 0.5 * zz * zz; }
         else dw.push_back((int32_t)w);
     }
+    // Absorbing the dense words into the sparse tier (option sparse_absorb =
+    // 1) removes their tile launch (C2: 49 words, z 277-998, 0.08 + 0.05 ms
+    // of tiles beside the sparse kernel) at the price of their products. On
+    // C2 that lost (step 0.279 vs 0.251 ms, profiles/r02/sparse6/): the
+    // launch overlaps the sparse kernel, and the modelled fixed cost below
+    // overstates it, so absorbing is opt-in; the model is reported by trace.
+    if (!dw.empty() && ctx->option(OPT_SPARSE_ABSORB, 0) != 0) {
+        double absorb_s = 0.0, absorb_products = 0.0;
+        for (int32_t w : dw) {
+            const double zz = (double)z[w];
+            absorb_products += 0.5 * zz * zz;
+            absorb_s += 0.5 * zz * zz / kSparseProductsPerS + tiles / kSparseItemsPerS;
+        }
+        const double keep_s = kDenseLaunchFixedS + pairs * (double)ceil_div((int64_t)dw.size(), 16) * 16.0 /
+                                                       kDenseWordPairsPerS;
+        if (ctx->trace())
+            fprintf(stderr, "gdist: absorbing %zu dense words: modelled %.1f us of products vs %.1f us launch\n",
+                    dw.size(), absorb_s * 1e6, keep_s * 1e6);
+        {
+            sw.clear();
+            for (int64_t w = 0; w < Wv; w++) sw.push_back((int32_t)w);
+            dw.clear();
+            products += absorb_products;
+        }
+    }
     const int64_t Ws = (int64_t)sw.size(), Wd = (int64_t)dw.size();
+    if (ctx->trace() && Wd) {
+        std::vector<int32_t> zd;
+        for (int32_t w : dw) zd.push_back(z[w]);
+        std::sort(zd.begin(), zd.end());
+        fprintf(stderr, "gdist: %lld dense words, z min %d median %d max %d (of %lld sets), word indices %d..%d of %lld; "
+                        "words past the valid bits %lld\n",
+                (long long)Wd, zd.front(), zd[zd.size() / 2], zd.back(), (long long)N, dw.front(), dw.back(),
+                (long long)Wv, (long long)(W - Wv));
+    }
     const int64_t Wdp = Wd ? ceil_div(Wd, 16) * 16 : 0;
     // whole-triangle estimates: keep the split only if it beats the plain tiles
     const double t_plain = pairs * (double)W / kDenseWordPairsPerS;
@@ -887,8 +1246,12 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
     exclusive_scan_i32_to_i64(ctx, cnt.as<int32_t>(), s->sp_off.as<int64_t>(), (size_t)(nblk * Ws + 1));
     int64_t total = 0;
     d2h(&total, s->sp_off.as<int64_t>() + nblk * Ws, 8, st);
+    GD_REQUIRE(total < (int64_t(1) << 32), "sparse entries exceed 32-bit offsets");
     s->sp_word.alloc(total * 8 + 8, st);
     s->sp_set.alloc(total + 8, st);
+    // word[total] = 0: the sentinel entry v5's idle product slots read
+    GD_HIP(hipMemsetAsync(s->sp_word.as<unsigned long long>() + total, 0, 8, st));
+    GD_HIP(hipMemsetAsync(s->sp_set.as<uint8_t>() + total, 0, 8, st));
     s->sp_nc.alloc(N * 4, st);
     GD_HIP(hipMemsetAsync(s->sp_nc.p, 0, N * 4, st));
     const int64_t nbk = ceil_div(Ws, int64_t(1) << kBucketShift);
@@ -906,7 +1269,8 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
         d2h(s->sp_bucket_bits.data(), dbb.p, (size_t)N * nbk * 4, st);
     }
     GD_HIP(hipGetLastError());
-    s->sp_ent.alloc(total * 16 + 16, st);
+    s->sp_ent.alloc(total * 16 + 64, st);
+    GD_HIP(hipMemsetAsync(s->sp_ent.as<ulonglong2>() + total, 0, 64, st));      // the sentinel records
     if (total)
         sparse_records_kernel<<<grid_for(total), 256, 0, st>>>(s->sp_word.as<unsigned long long>(),
                                                                 s->sp_set.as<uint8_t>(), total,
@@ -936,6 +1300,37 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
                 }
             if (mx <= kSparseStageEntries) s->sp_win = win;
         }
+        // each word's modelled cost over all tiles, in products: the pair
+        // products of its lists (diagonal tiles: pairs within one list) and
+        // the tile visits; sparse_matrix cuts chunks at equal cost
+        s->sp_cost.assign(Ws + 1, 0.0);
+        const double visit = (double)nblk * (double)(nblk + 1) / 2 * kSparseProductsPerS / kSparseItemsPerS;
+        for (int64_t m = 0; m < Ws; m++) {
+            double se1 = 0.0;
+            for (int64_t b = 0; b < nblk; b++) se1 += (double)(ho[b * Ws + m + 1] - ho[b * Ws + m]);
+            // sum_{a<b} e_a e_b + sum_a e_a (e_a - 1) / 2 = (se1^2 - se1) / 2
+            s->sp_cost[m + 1] = s->sp_cost[m] + 0.5 * (se1 * se1 - se1) + visit;
+        }
+        if (ctx->trace()) {               // entries per (block, word): the shape of the tile walk
+            int64_t h[34] = {0};
+            double pr = 0.0, cells8 = 0.0;
+            for (int64_t b = 0; b < nblk; b++)
+                for (int64_t m = 0; m < Ws; m++) {
+                    const int64_t e = ho[b * Ws + m + 1] - ho[b * Ws + m];
+                    h[e <= 32 ? e : 33]++;
+                }
+            for (int64_t m = 0; m < Ws; m++)
+                for (int64_t a = 0; a < nblk; a++)
+                    for (int64_t b = a + 1; b < nblk; b++) {
+                        const int64_t ea = ho[a * Ws + m + 1] - ho[a * Ws + m];
+                        const int64_t eb = ho[b * Ws + m + 1] - ho[b * Ws + m];
+                        pr += (double)ea * eb;
+                        cells8 += 64.0 * (double)((ea + 7) / 8) * (double)((eb + 7) / 8);
+                    }
+            fprintf(stderr, "gdist: sparse entries per (block, word):");
+            for (int k = 0; k < 34; k++) fprintf(stderr, " %lld", (long long)h[k]);
+            fprintf(stderr, "\ngdist: off-diagonal products %.4g, 8x8 grid lanes %.4g\n", pr, cells8);
+        }
     }
     int64_t Us = 0;                       // valid bits of the complement-sparse words
     int64_t npos = 0;
@@ -948,8 +1343,19 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
     // instead of a dense tile launch: the launch's per-tile accumulator flush
     // cost C2's 16-64 dense words 0.09-0.15 ms beside the sparse kernel, the
     // fold reads 2 x Wdp words per pair from L2 (option fold_dense_words)
-    s->sp_fold_dense = Wdp > 0 && Wdp <= ctx->option(OPT_FOLD_DENSE_WORDS, kFoldDenseWords);
-    if (s->sp_fold_dense) {
+    // The dense words counted inside the v5 / v6 tile kernel (option
+    // sparse_fold, default up to 64 words): chunk c < Wdp / 8 of every tile
+    // adds words [8c, 8c + 8) of its 128 x 128 pairs into its LDS counters
+    // (~2 us per such workgroup), so no dense-word tile launch shares the
+    // CUs with the sparse kernel (C2: 0.09 + 0.04 ms of tiles beside it)
+    const int sk = (int)ctx->option(OPT_SPARSE_KERNEL, 6);
+    if (Wdp > 0 && (sk == 5 || sk == 6) && Wdp <= ctx->option(OPT_SPARSE_FOLD, 64) &&
+        !(Wdp <= ctx->option(OPT_FOLD_DENSE_WORDS, kFoldDenseWords))) {
+        s->sp_fold_dense = true;
+        s->sp_fold_slabs = (int)(Wdp / kFoldSlabWords);
+    }
+    if (!s->sp_fold_dense) s->sp_fold_dense = Wdp > 0 && Wdp <= ctx->option(OPT_FOLD_DENSE_WORDS, kFoldDenseWords);
+    if (s->sp_fold_dense && s->sp_fold_slabs == 0) {
         s->sp_dT.alloc((size_t)N * Wdp * 8, st);
         transpose_words_kernel<<<grid_for(N * Wdp), 256, 0, st>>>(s->dbits.as<unsigned long long>(), N, Wdp,
                                                                  s->sp_dT.as<unsigned long long>());
@@ -984,25 +1390,50 @@ void sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
         sc.ntiles = (int64_t)tiles.size();
         // enough workgroups to fill the chip, each over >= 512 sparse words
         const int64_t target = (int64_t)ctx->cus * std::max<int64_t>(1, ctx->option(OPT_SPARSE_WG_PER_CU, 4));
-        // chunks of <= kChunkWords words keep the 16-bit counters exact for
-        // any sets; more chunks only while they add parallelism
-        int64_t nch = sc.ntiles ? std::max<int64_t>(ceil_div(s->Ws, kChunkWords),
-                                                    std::min<int64_t>(ceil_div(s->Ws, 512), ceil_div(target, sc.ntiles)))
-                                : 0;
         const int64_t budget = ctx->option(OPT_SPARSE_PART_BUDGET, int64_t(1) << 30);
         const int64_t tile_bytes = SB * SB * 2;
-        // ... and every chunk within the 16-bit counters' bound: a pair's
-        // count in a chunk is at most either set's complement bits there, so
-        // a chunk is exact when the SECOND largest set total over the buckets
-        // covering it is <= 65535 (one set may hold more: a guide lacks every
-        // kmer the later guides key, C2's sets 0-3). sp_bucket_bits holds the
-        // totals per set and bucket of 1024 sparse words.
-        auto chunk_ok = [&](int64_t n) {
+        // Chunk bounds: equal word counts, or (option sparse_balance) equal
+        // modelled cost (sp_cost: each word's products over all tiles +
+        // visits), so that a run of heavy words (C2 with sparse_absorb: the
+        // ~50 words half the sets lack, at the end of the locus order) gets
+        // narrow chunks instead of one chunk many times the others' work; at
+        // most `cap` words per chunk. On C2 as built (no absorb) the equal
+        // split is faster: the cost split makes 110 smaller chunks (kernel
+        // 0.145 vs 0.136 ms, reduce 0.029 vs 0.034; profiles/r02/sparse6/).
+        const bool balance = ctx->option(OPT_SPARSE_BALANCE, 0) != 0;
+        // chunks that fold a dense-word slab (the first sp_fold_slabs) hold
+        // at most kChunkWords - kFoldSlabWords words: every chunk does
+        const int64_t cap = s->sp_fold_slabs ? kChunkWords - kFoldSlabWords : kChunkWords;
+        auto make_bounds = [&](int64_t n, int64_t wcap) {
+            const int64_t Ws = s->Ws;
+            const bool costed = balance && (int64_t)s->sp_cost.size() == Ws + 1 && s->sp_cost[Ws] > 0.0;
+            auto cum = [&](int64_t m) { return costed ? s->sp_cost[m] : (double)m; };
+            const double step = cum(Ws) / (double)n;
+            std::vector<int32_t> b{0};
+            double next = step;
+            for (int64_t m = 0; m + 1 < Ws; m++) {            // close after word m at the quantile or the cap
+                const double end = cum(m + 1);
+                if (end >= next || m + 1 - b.back() >= wcap) {
+                    b.push_back((int32_t)(m + 1));
+                    while (next <= end) next += step;
+                }
+            }
+            b.push_back((int32_t)Ws);
+            return b;
+        };
+        // A chunk is exact when it holds <= kChunkWords words (64 x 1023 <
+        // 2^16 whatever the sets) or when the SECOND largest set total of
+        // complement bits over the buckets covering it is <= 65535 (one set
+        // may hold more: a guide lacks every kmer the later guides key, C2's
+        // sets 0-3); sp_bucket_bits holds the totals per set and bucket of
+        // 1024 sparse words.
+        auto bounds_ok = [&](const std::vector<int32_t>& b) {
             const int64_t N = s->nsets, nbk = s->sp_nbk;
-            for (int64_t c = 0; c < n; c++) {
-                const int64_t b0 = s->Ws * c / n, b1 = s->Ws * (c + 1) / n;
-                if (b1 <= b0) continue;
-                if (b1 - b0 <= kChunkWords) continue;          // 64 x 1023 < 2^16 whatever the sets
+            if ((int64_t)b.size() - 1 < s->sp_fold_slabs) return false;    // a chunk per slab
+            for (size_t c = 0; c + 1 < b.size(); c++) {
+                const int64_t b0 = b[c], b1 = b[c + 1];
+                const int64_t fold = (int64_t)c < s->sp_fold_slabs ? 64 * kFoldSlabWords : 0;
+                if (b1 - b0 <= cap) continue;
                 if ((int64_t)s->sp_bucket_bits.size() != N * nbk) return false;
                 int64_t m1 = 0, m2 = 0;
                 for (int64_t i = 0; i < N; i++) {
@@ -1011,25 +1442,40 @@ void sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
                         t += s->sp_bucket_bits[i * nbk + k];
                     if (t > m1) { m2 = m1; m1 = t; } else if (t > m2) m2 = t;
                 }
-                if (m2 > 65535) return false;
+                if (m2 + fold > 65535) return false;
             }
             return true;
         };
-        // Past the partial budget (many tiles: N >> 1000), fewer and longer
-        // chunks where the complement bits allow it (chunk_ok), so that the
-        // partials fit; otherwise the chunks flush with atomics.
-        if (sc.ntiles && sc.ntiles * nch * tile_bytes > budget) {
-            int64_t fewer = std::max<int64_t>(1, budget / (sc.ntiles * tile_bytes));
-            while (fewer < nch && !chunk_ok(fewer)) fewer = std::min<int64_t>(nch, fewer * 2);
-            nch = std::min(nch, fewer);
+        std::vector<int32_t> bnd;
+        if (sc.ntiles) {
+            const int64_t n0 = std::max<int64_t>(std::max<int64_t>(ceil_div(s->Ws, cap), s->sp_fold_slabs),
+                                                 std::min<int64_t>(ceil_div(s->Ws, 512), ceil_div(target, sc.ntiles)));
+            if (balance) bnd = make_bounds(n0, cap);
+            else
+                for (int64_t c = 0; c <= n0; c++) bnd.push_back((int32_t)(s->Ws * c / n0));
+            // Past the partial budget (many tiles: N >> 1000), fewer and
+            // longer chunks where the complement bits allow it (bounds_ok), so
+            // that the partials fit; otherwise the chunks flush with atomics.
+            const int64_t nb0 = (int64_t)bnd.size() - 1;
+            if (sc.ntiles * nb0 * tile_bytes > budget) {
+                for (int64_t fewer = std::max<int64_t>(1, budget / (sc.ntiles * tile_bytes)); fewer < nb0; fewer *= 2) {
+                    auto b = make_bounds(fewer, INT64_MAX);
+                    if (bounds_ok(b)) { bnd = b; break; }
+                }
+            }
+            if (ctx->has_option(OPT_SPARSE_CHUNKS))   // tests: a given chunk count (exactness still checked)
+                bnd = make_bounds(std::max<int64_t>(s->sp_fold_slabs,
+                                                    std::max<int64_t>(1, std::min<int64_t>(s->Ws, ctx->option(OPT_SPARSE_CHUNKS, 1)))),
+                                  INT64_MAX);
+            GD_REQUIRE(bounds_ok(bnd), "sparse chunks exceed the 16-bit counter bound");
         }
-        if (ctx->has_option(OPT_SPARSE_CHUNKS))       // tests: a given chunk count (exactness still checked)
-            nch = std::max<int64_t>(1, std::min<int64_t>(s->Ws, ctx->option(OPT_SPARSE_CHUNKS, 1)));
-        GD_REQUIRE(nch == 0 || chunk_ok(nch), "sparse chunks exceed the 16-bit counter bound");
+        const int64_t nch = sc.ntiles ? (int64_t)bnd.size() - 1 : 0;
         sc.nchunks = (int)nch;
         if (sc.ntiles) {
             sc.tiles.alloc(sc.ntiles * sizeof(int2), st);
             h2d(sc.tiles.p, tiles.data(), sc.ntiles * sizeof(int2), st);
+            sc.bounds.alloc(bnd.size() * 4, st);
+            h2d(sc.bounds.p, bnd.data(), bnd.size() * 4, st);
         }
         // chunk partials (16-bit counters, 32 KiB per tile and chunk) within a
         // byte budget (option sparse_part_budget, default 1 GiB); past it the
@@ -1037,6 +1483,16 @@ void sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
         const int64_t part_bytes = sc.ntiles * sc.nchunks * tile_bytes;
         sc.use_part = sc.nchunks > 1 && part_bytes <= budget;
         if (sc.use_part) sc.part.alloc((size_t)part_bytes, st);
+        if (ctx->trace() && sc.ntiles) {
+            double cmax = 0.0, csum = 0.0;
+            for (size_t c = 0; c + 1 < bnd.size(); c++) {
+                const double cc = s->sp_cost.empty() ? 0.0 : s->sp_cost[bnd[c + 1]] - s->sp_cost[bnd[c]];
+                cmax = std::max(cmax, cc);
+                csum += cc;
+            }
+            fprintf(stderr, "gdist: sparse chunks: %lld, modelled cost max / mean %.2f\n", (long long)nch,
+                    csum > 0 ? cmax / (csum / (double)nch) : 0.0);
+        }
         if (ctx->trace())
             fprintf(stderr, "gdist: sparse plan rows [%lld,%lld) cols [%lld,%lld): %lld tiles x %d chunks, %s, win %d, "
                             "%lld of %lld sparse words positive\n",
@@ -1049,17 +1505,20 @@ void sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     if (sc.ntiles == 0) return;
     const int nchunks = sc.nchunks;
     const int64_t nt = sc.ntiles;
-    // 6 products per lane in flight (C2 sweep, profiles/r01/sparse/
-    // sweep_unroll_c2.txt): the kernel is bound by the latency of its
-    // load -> add chain. __launch_bounds__'s second argument is the minimum
-    // waves per SIMD: 8 holds the SGPRs under the 8-wave budget (4 workgroups
-    // per CU, LDS-limited) where 3 let them reach 112 (3 per CU): 0.310 ->
-    // 0.298 ms (profiles/r01/sparse/occ_{3,8}.json; GDIST_SPARSE_OCC=3 for A/B)
-    const int sun = (int)ctx->option(OPT_SPARSE_SUN, 6);
-    int version = (int)ctx->option(OPT_SPARSE_KERNEL, 1);
-    const unsigned long long* fold = s->sp_fold_dense ? s->sp_dT.as<unsigned long long>() : nullptr;
+    // Kernel 6 (default): v5's walk over 1 x 2 micro-tiles, 3 slots (6
+    // products) per lane in flight (C2 A/B, profiles/r02/sparse6/). v1: 6
+    // products per lane in flight (profiles/r01/sparse/sweep_unroll_c2.txt).
+    // __launch_bounds__'s second argument is the minimum waves per SIMD: 8
+    // holds the registers under the 8-wave budget (4 workgroups per CU,
+    // LDS-limited) where 3 let the SGPRs reach 112 (3 per CU): v1 0.310 ->
+    // 0.298 ms (profiles/r01/sparse/occ_{3,8}.json; option sparse_occ = 3).
+    int version = (int)ctx->option(OPT_SPARSE_KERNEL, 6);
+    const int sun = (int)ctx->option(OPT_SPARSE_SUN, version == 6 ? 3 : version == 5 ? 4 : 6);
+    const unsigned long long* fold =
+        s->sp_fold_dense && s->sp_fold_slabs == 0 ? s->sp_dT.as<unsigned long long>() : nullptr;
+    GD_REQUIRE(s->sp_fold_slabs == 0 || version == 5 || version == 6,
+               "dense words folded into the v5 / v6 tile kernel (option sparse_fold): build with that kernel");
     if ((version == 2 || version == 4) && s->sp_win == 0) version = 1;
-    // (option sparse_occ = 3 exists for SUN = 6 only: the A/B that chose OCC 8)
     auto kern = ctx->option(OPT_SPARSE_OCC, 8) == 3 ? sparse_tile_kernel<6, 3>
                 : sun == 4            ? sparse_tile_kernel<4, 8>
                 : sun == 8            ? sparse_tile_kernel<8, 8>
@@ -1073,23 +1532,40 @@ void sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
         (sun == 4 ? sparse_tile_kernel4<4, 6> : sun == 1 ? sparse_tile_kernel4<1, 6> : sparse_tile_kernel4<2, 6>)<<<
             (unsigned)(nt * nchunks), S2T, 0, st>>>(
             s->sp_off.as<int64_t>(), s->sp_word.as<unsigned long long>(), s->sp_set.as<uint8_t>(),
-            s->sp_nc.as<int32_t>(), s->sp_U, s->Ws, s->sp_win, sc.tiles.as<int2>(), nchunks, r0, r1, c0, c1,
+            s->sp_nc.as<int32_t>(), s->sp_U, s->Ws, s->sp_win, sc.tiles.as<int2>(), sc.bounds.as<int32_t>(), nchunks, r0, r1, c0, c1,
             upper ? 1 : 0, d_I, ldI, sc.use_part ? sc.part.as<int32_t>() : nullptr, fold, s->Wd, s->nsets);
+    else if (version == 5 || version == 6) {
+        const int shape = (int)ctx->option(OPT_SPARSE_SHAPE, 12);
+        GD_REQUIRE(version == 5 || shape == 12 || shape == 14 || shape == 22, "sparse_shape: 12, 14 or 22");
+        GD_REQUIRE(version == 6 ? sun >= 2 && sun <= (shape == 12 ? 4 : 3) : sun == 4 || sun == 6,
+                   "sparse_sun out of range for the kernel");
+        auto k5 = version == 5 ? (sun == 4 ? sparse_tile_kernel5<4, 8> : sparse_tile_kernel5<6, 8>)
+                  : shape == 14 ? (sun == 2 ? sparse_tile_kernel5<2, 8, 1, 4> : sparse_tile_kernel5<3, 8, 1, 4>)
+                  : shape == 22 ? (sun == 2 ? sparse_tile_kernel5<2, 8, 2, 2> : sparse_tile_kernel5<3, 8, 2, 2>)
+                  : sun == 2    ? sparse_tile_kernel5<2, 8, 1, 2>
+                  : sun == 4    ? sparse_tile_kernel5<4, 8, 1, 2>
+                                : sparse_tile_kernel5<3, 8, 1, 2>;
+        k5<<<(unsigned)(nt * nchunks), SNT, 0, st>>>(
+            s->sp_off.as<int64_t>(), s->sp_set.as<uint8_t>(), s->sp_ent.as<ulonglong2>(), s->sp_nc.as<int32_t>(),
+            s->sp_U, s->Ws, sc.tiles.as<int2>(), sc.bounds.as<int32_t>(), nchunks, r0, r1, c0, c1, upper ? 1 : 0, d_I, ldI,
+            sc.use_part ? sc.part.as<int32_t>() : nullptr, fold, s->Wd, s->nsets,
+            ctx->option(OPT_SPARSE_BALANCE, 0) != 0 ? 1 : 0, s->dbits.as<unsigned long long>(), s->sp_fold_slabs);
+    }
     else if (version == 2)
         (abl == 1 ? sparse_tile_kernel2<4, 6, 1> : abl == 2 ? sparse_tile_kernel2<4, 6, 2> : sparse_tile_kernel2<4, 6, 0>)<<<(unsigned)(nt * nchunks), S2T, 0, st>>>(
             s->sp_off.as<int64_t>(), s->sp_word.as<unsigned long long>(), s->sp_set.as<uint8_t>(),
-            s->sp_nc.as<int32_t>(), s->sp_U, s->Ws, s->sp_win, sc.tiles.as<int2>(), nchunks, r0, r1, c0, c1,
+            s->sp_nc.as<int32_t>(), s->sp_U, s->Ws, s->sp_win, sc.tiles.as<int2>(), sc.bounds.as<int32_t>(), nchunks, r0, r1, c0, c1,
             upper ? 1 : 0,
             d_I, ldI, sc.use_part ? sc.part.as<int32_t>() : nullptr, fold, s->Wd, s->nsets);
     else
     kern<<<(unsigned)(nt * nchunks), SNT, 0, st>>>(
         s->sp_off.as<int64_t>(), s->sp_word.as<unsigned long long>(), s->sp_set.as<uint8_t>(),
         s->sp_ent.as<ulonglong2>(), s->sp_nc.as<int32_t>(),
-        s->sp_U, s->Ws, sc.tiles.as<int2>(), nchunks, r0, r1, c0, c1, upper ? 1 : 0, d_I, ldI,
+        s->sp_U, s->Ws, sc.tiles.as<int2>(), sc.bounds.as<int32_t>(), nchunks, r0, r1, c0, c1, upper ? 1 : 0, d_I, ldI,
         sc.use_part ? sc.part.as<int32_t>() : nullptr, fold, s->Wd, s->nsets);
     GD_HIP(hipGetLastError());
     if (sc.use_part) {
-        sparse_reduce_kernel<<<(unsigned)(nt * (SB * SB / 256)), 256, 0, st>>>(
+        sparse_reduce_kernel<<<(unsigned)(nt * (SB * SB / kReduceCnt / kReduceGroups)), 256, 0, st>>>(
             sc.part.as<int32_t>(), nchunks, sc.tiles.as<int2>(), s->sp_nc.as<int32_t>(), s->sp_U, r0, r1, c0, c1,
             upper ? 1 : 0, d_I, ldI, fold, s->Wd, s->nsets);
         GD_HIP(hipGetLastError());

@@ -577,7 +577,10 @@ def test_rare_tier_thresholds_exact(ctx, T, kernel, dedup, opts):
 
 @pytest.mark.parametrize("mode", ["auto", "all_sparse", "mixed", "no_locus", "off", "atomic_flush", "kernel_v1",
                                   "kernel_v2", "many_chunks", "two_sided", "mixed_fold", "mixed_fold_1chunk",
-                                  "kernel_v4", "kernel_v4_rows"])
+                                  "kernel_v4", "kernel_v4_rows", "kernel_v5", "kernel_v5_rows", "kernel_v5_sun6",
+                                  "kernel_v5_atomic", "kernel_v6_rows", "kernel_v6_sun4", "kernel_v6_quads",
+                                  "kernel_v6_2x2", "kernel_v6_2x2_rows", "kernel_v6_atomic", "absorb",
+                                  "mixed_slabs", "mixed_slabs_atomic", "mixed_tiles"])
 def test_sparse_complement_words_exact(ctx, mode, opts):
     """The dense tier in locus order with complement-sparse words: counts and
     distances are bit-exact against the oracle over upper triangles,
@@ -593,6 +596,25 @@ def test_sparse_complement_words_exact(ctx, mode, opts):
                 "kernel_v2": {"sparse_zmax": 100000, "sparse_kernel": 2},
                 "kernel_v4": {"sparse_zmax": 100000, "sparse_kernel": 4},
                 "kernel_v4_rows": {"sparse_zmax": 40, "sparse_kernel": 4, "sparse_sun": 4},
+                "kernel_v5": {"sparse_zmax": 100000, "sparse_kernel": 5},
+                "kernel_v5_rows": {"sparse_zmax": 40, "sparse_kernel": 5},
+                "kernel_v5_sun6": {"sparse_zmax": 100000, "sparse_kernel": 5, "sparse_sun": 6, "sparse_chunks": 7},
+                "kernel_v5_atomic": {"sparse_zmax": 100000, "sparse_kernel": 5, "sparse_part_budget": 0,
+                                     "sparse_chunks": 3},
+                # kernel 6 (the default): micro-tiles of 1 x 2 / 1 x 4 / 2 x 2 entries per slot
+                "kernel_v6_rows": {"sparse_zmax": 40, "sparse_sun": 2},
+                "kernel_v6_sun4": {"sparse_zmax": 100000, "sparse_sun": 4, "sparse_chunks": 7},
+                "kernel_v6_quads": {"sparse_zmax": 100000, "sparse_shape": 14},
+                "kernel_v6_2x2": {"sparse_zmax": 100000, "sparse_shape": 22},
+                "kernel_v6_2x2_rows": {"sparse_zmax": 40, "sparse_shape": 22, "sparse_sun": 2},
+                "kernel_v6_atomic": {"sparse_zmax": 100000, "sparse_part_budget": 0, "sparse_chunks": 3},
+                # the dense words absorbed into the sparse tier (no dense-word launch)
+                "absorb": {"sparse_zmax": 12, "sparse_absorb": 1},
+                # the dense words counted inside the tile kernel, 8 per chunk (partials / atomic flush),
+                # or by their own tile launch
+                "mixed_slabs": {"sparse_zmax": 12, "sparse_fold": 100000},
+                "mixed_slabs_atomic": {"sparse_zmax": 12, "sparse_fold": 100000, "sparse_part_budget": 0},
+                "mixed_tiles": {"sparse_zmax": 12, "sparse_fold": 0},
                 "many_chunks": {"sparse_zmax": 100000, "sparse_chunks": 37},
                 # words counted from either side (complement / positive), model's choice
                 # a dense-only dictionary: the substitution kmers two or more
@@ -608,9 +630,11 @@ def test_sparse_complement_words_exact(ctx, mode, opts):
     sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
     _, W = sets.build_bitsets()
     ws, wd, ent = sets.sparse_info()
-    if mode in ("all_sparse", "atomic_flush", "kernel_v1", "kernel_v2", "many_chunks", "kernel_v4"):
+    if mode in ("all_sparse", "atomic_flush", "kernel_v1", "kernel_v2", "many_chunks", "kernel_v4", "kernel_v5",
+                "kernel_v5_sun6", "kernel_v5_atomic", "kernel_v6_sun4", "kernel_v6_quads", "kernel_v6_2x2",
+                "kernel_v6_atomic", "absorb"):
         assert ws > 0 and wd == 0 and ent > 0
-    elif mode in ("mixed", "mixed_fold", "mixed_fold_1chunk"):
+    elif mode in ("mixed", "mixed_fold", "mixed_fold_1chunk", "mixed_slabs", "mixed_slabs_atomic", "mixed_tiles"):
         assert ws > 0 and wd > 0
     elif mode == "off":
         assert ws == 0 and wd == W
