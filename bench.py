@@ -36,6 +36,10 @@ sys.path.insert(0, os.path.join(ROOT, "genome.distance_amd"))
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0               # MI355X_MICROARCH.md chip table (spec)
+# what bounds the sparse tile kernel (v6), from its PMC passes (profiles/r02/sparse6/)
+SPARSE_LIMITER = ("vector-memory issue and latency of the product walk, not HBM bandwidth: v6 walks 1x2 "
+                  "micro-tiles (one search + quotient per two products, 3 record loads), see "
+                  "profiles/r02/sparse6/pmc_v6.txt and DESIGN.md §4")
 # VALU ceiling of the bitset inner step, MEASURED (scripts/microbench/valu_popc.hip,
 # profiles/r01/valu_microbench.txt): an interleaved v_and_b32 + v_bcnt_u32_b32 stream
 # issues at most 6.17e11 wave-instructions/s chip-wide (v_bcnt is half rate:
@@ -232,6 +236,20 @@ def main():
     # recorded per step inside the timed region, read after it)
     kernel_ms = ctx.recent_timings(args.steps)
     elapsed_max = max_over_ranks(elapsed)
+    # The sparse tile kernel alone, after the timed region (roofline): HIP
+    # events around its launch on the stream it runs on (option time_sparse;
+    # such calls run unreplayed, one event pair per call)
+    sparse_k_ms = None
+    if method == "bitset" and sparse_words and sparse_words["sparse_words"] > 0:
+        prev = ctx.option("time_sparse")
+        ctx.set_option("time_sparse", 1)
+        ts = []
+        for _ in range(max(3, min(args.steps, 20))):
+            step()
+            ts.append(ctx.sparse_kernel_ms())
+        ctx.set_option("time_sparse", prev)
+        ts = [t for t in ts[1:] if t > 0]                 # the first call builds nothing new, but warms
+        sparse_k_ms = float(np.mean(ts)) if ts else None
     pairs_all = N * (N - 1) // 2
     value = pairs_all * args.steps / elapsed_max
     k_avg_ms = float(np.mean(kernel_ms)) if kernel_ms else 0.0
@@ -270,8 +288,8 @@ def main():
         kname = {"bitset": "bitset_tile_kernel2<1> (+ rare_pairs_kernel)", "sorted": "sorted_join_kernel",
                  "sketch": "sketch_tile_kernel<16,24,LDS,K=2>"}[method]
         if sparse:
-            kname = "sparse_tile_kernel (+ bitset_tile_kernel2 on the dense words, rare_pairs_kernel, beside it)"
-        if traffic is not None and not pmc.get("kernel", "").startswith(kname.split()[0]):
+            kname = "sparse_tile_kernel5<3, 8, 1, 2> (v6: 1x2 micro-tiles, the dense words folded in)"
+        if traffic is not None and not pmc.get("kernel", "").startswith(kname.split(" (")[0]):
             traffic = None                    # the PMC summary was taken on another kernel
         valu_peak = VALU_WORDPAIR_PEAK * 4 / 1e12
         if sparse:
@@ -291,19 +309,19 @@ def main():
                         continue
                     whole_diag = A == B and A * 128 >= r0 and min(N, (A + 1) * 128) <= r1
                     algo_sparse += side if whole_diag else 2.0 * side
-            ach = algo_sparse / (k_avg_ms * 1e-3) / 1e9 if k_avg_ms > 0 else 0.0
+            kms = sparse_k_ms if sparse_k_ms else k_avg_ms
+            ach = algo_sparse / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
             dense_ops = pairs_rank * width_words * 4 / (k_avg_ms * 1e-3) / 1e12 if k_avg_ms > 0 else 0.0
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kname,
-                    "kernel_avg_ms": round(k_avg_ms, 4), "algo_bytes_per_launch": round(algo_sparse),
-                    "limiter": "instruction issue and the dependent load -> LDS-atomic chain, not HBM bandwidth: "
-                               "~100 wave-instructions per 64 products (word search, decode, 4 loads, the add), "
-                               "SQ_ACTIVE_INST_ANY ~ the kernel's cycles per SIMD, TA busy ~50 % "
-                               "(profiles/r02/sparse/pmc_v1.txt); LDS-staged variants measured slower "
-                               "(DESIGN.md §4)",
-                    "note": "algorithmic bytes = the sparse entries + offsets each sparse tile streams once; "
-                            "kernel time = HIP-event span of the step's launches (sparse tiles with their chunk "
-                            "reduce, the dense-word tiles and the rare tier run concurrently)",
+                    "kernel_avg_ms": round(kms, 4), "step_kernel_span_ms": round(k_avg_ms, 4),
+                    "algo_bytes_per_launch": round(algo_sparse),
+                    "limiter": SPARSE_LIMITER,
+                    "note": "algorithmic bytes = the sparse entries (8 B word + 1 B set) + offsets each sparse "
+                            "tile streams once; kernel_avg_ms = HIP events around the sparse tile kernel alone "
+                            "(option time_sparse, after the timed region); step_kernel_span_ms = HIP-event span "
+                            "of the timed steps' launches (zeroing, sparse tiles, chunk reduce, rare tier "
+                            "beside them, epilogue)",
                     "dense_equivalent": {"lane_ops_per_s_T": round(dense_ops, 2),
                                          "x_dense_valu_ceiling": round(dense_ops / valu_peak, 2),
                                          "note": "the same pairs as AND+popcount over all W bitset words "

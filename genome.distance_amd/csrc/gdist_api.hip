@@ -25,7 +25,7 @@ const char* const kOptNames[OPT_COUNT] = {
     "reps_block",      "locus_order",     "sparse",          "sparse_zmax",     "sparse_wg_per_cu",
     "sparse_occ",      "sparse_sun",      "sketch_k",        "sketch_tile",     "sparse_part_budget",
     "guides",          "force_exchange",  "sparse_kernel",   "sparse_chunks",   "fold_dense_words", "sparse_abl",      "graph",
-    "sparse_shape",    "sparse_absorb",   "sparse_balance",  "sparse_fold",
+    "sparse_shape",    "sparse_absorb",   "sparse_balance",  "time_sparse",     "sparse_xcd",      "sparse_fold",
 };
 
 static int option_index(const char* name) {
@@ -230,6 +230,8 @@ int gdist_ctx_create(int device, gdist_ctx** out) {
         GD_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
         GD_HIP(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
         GD_HIP(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+        GD_HIP(hipEventCreate(&c->ev_sp0));
+        GD_HIP(hipEventCreate(&c->ev_sp1));
         GD_HIP(hipEventCreateWithFlags(&c->ev_stage[0], hipEventDisableTiming));
         GD_HIP(hipEventCreateWithFlags(&c->ev_stage[1], hipEventDisableTiming));
         GD_HIP(hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device));
@@ -252,6 +254,8 @@ int gdist_ctx_destroy(gdist_ctx* ctx) {
         (void)hipStreamSynchronize(ctx->side);
         (void)hipEventDestroy(ctx->ev_fork);
         (void)hipEventDestroy(ctx->ev_join);
+        (void)hipEventDestroy(ctx->ev_sp0);
+        (void)hipEventDestroy(ctx->ev_sp1);
         (void)hipStreamDestroy(ctx->side);
         (void)hipEventDestroy(ctx->ev_stage[0]);
         (void)hipEventDestroy(ctx->ev_stage[1]);
@@ -313,6 +317,20 @@ int gdist_ctx_recent_timings(gdist_ctx* ctx, int max, double* kernel_ms, int* co
             kernel_ms[i] = km;
         }
         *count = (int)n;
+    });
+}
+
+int gdist_ctx_sparse_kernel_ms(gdist_ctx* ctx, double* ms) {
+    return guard([&] {
+        GD_REQUIRE(ctx && ms, "null argument");
+        use_device(ctx);
+        std::lock_guard<std::recursive_mutex> lk_(ctx->mu);
+        *ms = -1.0;
+        if (!ctx->sp_timed) return;
+        GD_HIP(hipEventSynchronize(ctx->ev_sp1));
+        float t = 0.f;
+        GD_HIP(hipEventElapsedTime(&t, ctx->ev_sp0, ctx->ev_sp1));
+        *ms = t;
     });
 }
 
@@ -760,7 +778,8 @@ int gdist_intersect_matrix(gdist_ctx* ctx, const gdist_sets* sets, int64_t r0, i
         // epilogue without host round trips between them. The first call
         // runs uncaptured (it builds the launch plans), the second is
         // captured; a refused capture leaves the key uncaptured.
-        if (dev && I_out && m == GDIST_METHOD_BITSET && ctx->option(OPT_GRAPH, 1) != 0) {
+        if (dev && I_out && m == GDIST_METHOD_BITSET && ctx->option(OPT_GRAPH, 1) != 0 &&
+            ctx->option(OPT_TIME_SPARSE, 0) == 0) {
             std::vector<int64_t> key{r0, r1, c0, c1, (int64_t)flags, (int64_t)(intptr_t)I_out,
                                      (int64_t)(intptr_t)D_out, ld};
             key.insert(key.end(), ctx->opt, ctx->opt + OPT_COUNT);

@@ -193,6 +193,8 @@ enum Opt : int {
     OPT_SPARSE_SHAPE,       // v6 micro-tile rows x columns: 12 (default) / 14 / 22
     OPT_SPARSE_ABSORB,      // 1: every word sparse (no dense-word launch; default 0)
     OPT_SPARSE_BALANCE,     // 1: chunk bounds at equal modelled cost, words dealt to waves one at a time
+    OPT_TIME_SPARSE,        // 1: HIP events around the sparse tile kernel (no hipGraph replay; bench roofline)
+    OPT_SPARSE_XCD,         // 1: chunk c of every tile on XCD c mod 8 (default 0: tile-major order; A/B lost)
     OPT_SPARSE_FOLD,        // at most this many (padded) dense words counted inside the v5 / v6 tile kernel
                             // (8 per chunk; default 64, 0: the dense-word tile launch)
     OPT_COUNT
@@ -228,6 +230,9 @@ struct gdist_ctx {
     size_t pinned_bytes = 0;
     hipEvent_t ev_stage[2] = {nullptr, nullptr};
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // option time_sparse: the sparse tile kernel alone (uncaptured calls)
+    hipEvent_t ev_sp0 = nullptr, ev_sp1 = nullptr;
+    bool sp_timed = false;
     gdist::Timing last;
     int cus = 256;
     // RCCL communicator (multi-GPU row sharding)

@@ -906,12 +906,28 @@ __global__ __launch_bounds__(SNT, OCC) void sparse_tile_kernel5(
     const int32_t* __restrict__ nc, int64_t Us, int64_t Ws, const int2* __restrict__ tiles, const int32_t* __restrict__ cbnd, int nchunks,
     int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I, int64_t ldI,
     int32_t* __restrict__ part, const unsigned long long* __restrict__ dbits, int64_t Wdp, int64_t N, int il,
-    const unsigned long long* __restrict__ slab_bits, int slabs) {
+    const unsigned long long* __restrict__ slab_bits, int slabs, int ntiles, int xmap) {
     // dbits: the flush-fold dense words (word-major, option fold_dense_words);
     // slab_bits / slabs: the in-kernel fold's dense words (set-major [N][Wdp])
     __shared__ uint32_t cnt[SB * SB / 2];                  // 32 KiB, 16-bit counters (cnt_index layout)
     __shared__ int4 rec[SNW][64];                          // 8 KiB: the batch's walk records
-    const int tile = blockIdx.x / nchunks, ch = blockIdx.x % nchunks;
+    // xmap (option sparse_xcd): workgroup b = 8 (t + ntiles g) + x runs chunk
+    // 8 g + x of tile t. Blocks b and b + 8 share an XCD (round-robin
+    // dispatch), so chunk c of EVERY tile runs on one XCD, and the groups of 8
+    // chunks are dispatched in turn: an XCD's L2 holds the few chunks it is
+    // working on for all the tiles that read them (C2: ~0.85 MB of records
+    // per chunk over the 8 blocks), instead of every workgroup fetching its
+    // own rows and columns past L2 (tile-major order: 0.5 GB per launch).
+    int tile, ch;
+    if (xmap) {
+        const int per_g = ntiles * 8;
+        tile = (blockIdx.x % per_g) >> 3;
+        ch = (blockIdx.x / per_g) * 8 + (blockIdx.x & 7);
+        if (ch >= nchunks) return;
+    } else {
+        tile = blockIdx.x / nchunks;
+        ch = blockIdx.x % nchunks;
+    }
     const int64_t A = tiles[tile].x, B = tiles[tile].y;
     const int rlo = (int)(r0 - A * SB > 0 ? r0 - A * SB : 0);
     const int rhi = (int)(r1 - A * SB < SB ? r1 - A * SB : SB);
@@ -1448,8 +1464,12 @@ void sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
         };
         std::vector<int32_t> bnd;
         if (sc.ntiles) {
-            const int64_t n0 = std::max<int64_t>(std::max<int64_t>(ceil_div(s->Ws, cap), s->sp_fold_slabs),
-                                                 std::min<int64_t>(ceil_div(s->Ws, 512), ceil_div(target, sc.ntiles)));
+            int64_t n0 = std::max<int64_t>(std::max<int64_t>(ceil_div(s->Ws, cap), s->sp_fold_slabs),
+                                           std::min<int64_t>(ceil_div(s->Ws, 512), ceil_div(target, sc.ntiles)));
+            // whole groups of 8 chunks for the XCD-mapped v5 / v6 launch
+            const int sk = (int)ctx->option(OPT_SPARSE_KERNEL, 6);
+            if ((sk == 5 || sk == 6) && ctx->option(OPT_SPARSE_XCD, 0) != 0 && n0 > 8)
+                n0 = ceil_div(n0, 8) * 8;                // (empty chunks are allowed)
             if (balance) bnd = make_bounds(n0, cap);
             else
                 for (int64_t c = 0; c <= n0; c++) bnd.push_back((int32_t)(s->Ws * c / n0));
@@ -1528,6 +1548,8 @@ void sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
                : sun == 8 ? sparse_tile_kernel<8, 8, true>
                           : sparse_tile_kernel<6, 8, true>;
     const int abl = (int)ctx->option(OPT_SPARSE_ABL, 0);
+    const bool timed = ctx->option(OPT_TIME_SPARSE, 0) != 0 && !ctx->capturing;
+    if (timed) GD_HIP(hipEventRecord(ctx->ev_sp0, st));
     if (version == 4 && s->sp_win > 0)
         (sun == 4 ? sparse_tile_kernel4<4, 6> : sun == 1 ? sparse_tile_kernel4<1, 6> : sparse_tile_kernel4<2, 6>)<<<
             (unsigned)(nt * nchunks), S2T, 0, st>>>(
@@ -1545,11 +1567,15 @@ void sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
                   : sun == 2    ? sparse_tile_kernel5<2, 8, 1, 2>
                   : sun == 4    ? sparse_tile_kernel5<4, 8, 1, 2>
                                 : sparse_tile_kernel5<3, 8, 1, 2>;
-        k5<<<(unsigned)(nt * nchunks), SNT, 0, st>>>(
+        const bool xmap = ctx->option(OPT_SPARSE_XCD, 0) != 0;
+        const int64_t grid = xmap ? ceil_div(nchunks, 8) * 8 * nt : nt * nchunks;
+        GD_REQUIRE(grid < (int64_t(1) << 31), "sparse grid too large");
+        k5<<<(unsigned)grid, SNT, 0, st>>>(
             s->sp_off.as<int64_t>(), s->sp_set.as<uint8_t>(), s->sp_ent.as<ulonglong2>(), s->sp_nc.as<int32_t>(),
             s->sp_U, s->Ws, sc.tiles.as<int2>(), sc.bounds.as<int32_t>(), nchunks, r0, r1, c0, c1, upper ? 1 : 0, d_I, ldI,
             sc.use_part ? sc.part.as<int32_t>() : nullptr, fold, s->Wd, s->nsets,
-            ctx->option(OPT_SPARSE_BALANCE, 0) != 0 ? 1 : 0, s->dbits.as<unsigned long long>(), s->sp_fold_slabs);
+            ctx->option(OPT_SPARSE_BALANCE, 0) != 0 ? 1 : 0, s->dbits.as<unsigned long long>(), s->sp_fold_slabs,
+            (int)nt, xmap ? 1 : 0);
     }
     else if (version == 2)
         (abl == 1 ? sparse_tile_kernel2<4, 6, 1> : abl == 2 ? sparse_tile_kernel2<4, 6, 2> : sparse_tile_kernel2<4, 6, 0>)<<<(unsigned)(nt * nchunks), S2T, 0, st>>>(
@@ -1564,6 +1590,10 @@ void sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
         s->sp_U, s->Ws, sc.tiles.as<int2>(), sc.bounds.as<int32_t>(), nchunks, r0, r1, c0, c1, upper ? 1 : 0, d_I, ldI,
         sc.use_part ? sc.part.as<int32_t>() : nullptr, fold, s->Wd, s->nsets);
     GD_HIP(hipGetLastError());
+    if (timed) {
+        GD_HIP(hipEventRecord(ctx->ev_sp1, st));
+        ctx->sp_timed = true;
+    }
     if (sc.use_part) {
         sparse_reduce_kernel<<<(unsigned)(nt * (SB * SB / kReduceCnt / kReduceGroups)), 256, 0, st>>>(
             sc.part.as<int32_t>(), nchunks, sc.tiles.as<int2>(), s->sp_nc.as<int32_t>(), s->sp_U, r0, r1, c0, c1,

@@ -109,6 +109,13 @@ class Context:
         L.check(L.lib.gdist_ctx_last_timing(self.h, C.byref(k), C.byref(c), C.byref(n)))
         return k.value, c.value, n.value
 
+    def sparse_kernel_ms(self) -> float:
+        """HIP-event ms of the sparse tile kernel in the last call made with
+        option time_sparse = 1 (-1: none timed)."""
+        v = C.c_double()
+        L.check(L.lib.gdist_ctx_sparse_kernel_ms(self.h, C.byref(v)))
+        return v.value
+
     def recent_timings(self, n: int) -> list[float]:
         """Kernel ms of the last n matrix calls, oldest first (waits for them)."""
         out = np.zeros(max(n, 1), dtype=np.float64)

@@ -122,6 +122,10 @@ int  gdist_ctx_last_timing(gdist_ctx* ctx, double* kernel_ms, double* call_ms, i
 /* Kernel times (ms, HIP events on the stream they ran on) of the last
  * min(max, 256) matrix calls, oldest first, *count of them; waits for them. */
 int  gdist_ctx_recent_timings(gdist_ctx* ctx, int max, double* kernel_ms, int* count);
+/* HIP-event time (ms) of the sparse tile kernel alone in the last matrix call
+ * made with option "time_sparse" = 1 (such calls are not graph-replayed);
+ * -1 when none was timed. Waits for it. */
+int  gdist_ctx_sparse_kernel_ms(gdist_ctx* ctx, double* ms);
 /* Tuning options of a context: the A/B switches of DESIGN.md §5 by name
  * ("rare_t", "bitset_kernel", "sparse", "sparse_zmax", "sketch_k", ...;
  * gdist_ctx_option_name enumerates them, EINVAL past the last). Every option
