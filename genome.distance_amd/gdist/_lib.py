@@ -41,6 +41,34 @@ def _load():
 
 lib = _load()
 
+_PKG = os.path.dirname(_HERE)
+_REPO = os.path.dirname(_PKG)
+
+
+def tree_source_hash() -> str:
+    """sha256 prefix of the library's sources in this tree, in the Makefile's
+    order (csrc/*.hip by name, csrc/gdist_internal.hpp, include/gdist.h)."""
+    import glob
+    import hashlib
+    files = sorted(glob.glob(os.path.join(_PKG, "csrc", "*.hip")))
+    files += [os.path.join(_PKG, "csrc", "gdist_internal.hpp"), os.path.join(_REPO, "include", "gdist.h")]
+    h = hashlib.sha256()
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def check_build() -> str:
+    """Raises when the loaded libgdist.so was built from other sources than
+    this tree's (a stale in-tree build); returns the hash."""
+    built = lib.gdist_source_hash().decode()
+    tree = tree_source_hash()
+    if built != tree:
+        raise ImportError(f"libgdist.so is stale: built from sources {built}, this tree is {tree}; "
+                          "rebuild with `make -C genome.distance_amd`")
+    return built
+
 _i64, _i32, _u32, _dbl = C.c_int64, C.c_int32, C.c_uint, C.c_double
 _vp, _i64p, _i32p, _u64p, _dblp = (C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int32),
                                    C.POINTER(C.c_uint64), C.POINTER(C.c_double))
@@ -48,6 +76,7 @@ _ctxp, _setp = C.c_void_p, C.c_void_p
 
 _SIGS = {
     "gdist_version": (C.c_char_p, []),
+    "gdist_source_hash": (C.c_char_p, []),
     "gdist_abi_version": (C.c_int, []),
     "gdist_last_error": (C.c_char_p, []),
     "gdist_device_count": (C.c_int, [C.POINTER(C.c_int)]),

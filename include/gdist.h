@@ -110,6 +110,10 @@ typedef struct gdist_lsh  gdist_lsh;
 
 /* ---- library / context ---------------------------------------------- */
 const char* gdist_version(void);
+/* sha256 prefix (16 hex) of the sources the library was built from
+ * (csrc/ *.hip in name order, csrc/gdist_internal.hpp, include/gdist.h):
+ * a stale build is detectable against the tree it runs from. */
+const char* gdist_source_hash(void);
 int  gdist_abi_version(void);
 const char* gdist_last_error(void);                 /* thread-local */
 int  gdist_device_count(int* n);

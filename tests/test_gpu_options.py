@@ -7,6 +7,13 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
+def test_gpu_box_library_matches_tree():
+    """On the GPU box: the library these tests load was built from the
+    sources of the snapshot they run from."""
+    from gdist import _lib
+    _lib.check_build()
+
+
 def test_option_roundtrip_and_errors(ctx):
     import gdist
     names = gdist.option_names()

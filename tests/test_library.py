@@ -26,6 +26,14 @@ def test_library_exports_every_declared_symbol():
     assert set(syms) == set(_lib.EXPORTED), "Python binding out of sync with include/gdist.h"
 
 
+def test_library_built_from_this_tree():
+    """The in-tree libgdist.so was built from these sources (the Makefile's
+    compiled-in hash vs the tree's): a stale binary fails here, on the CPU
+    and on the GPU box alike (test_gpu_options repeats it there)."""
+    from gdist import _lib
+    assert _lib.check_build() == _lib.tree_source_hash()
+
+
 def test_abi_version_and_errors():
     from gdist import _lib
     assert _lib.lib.gdist_abi_version() == 1
