@@ -1398,15 +1398,15 @@ void free_bitsets(gdist_sets* s) {
     s->rare_kmers = 0;
 }
 
-void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1,
-                   bool upper, int32_t* d_I, int64_t ldI) {
+// The region's launch plan (tile groups, K-split, the sparse plan's slot),
+// built once per region and option set, then reused
+static MatrixPlan& matrix_plan(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1,
+                               bool upper) {
     hipStream_t st = ctx->stream;
     const int64_t nr = r1 - r0, nc = c1 - c0;
-    if (nr <= 0 || nc <= 0) return;
     const int tr = (int)ceil_div(nr, BT);
     // dense tile operands: every word, or only the dense words when the
     // complement-sparse words run in their own kernel (sparse.hip)
-    const unsigned long long* tbits = s->sparse ? s->dbits.as<unsigned long long>() : s->bits.as<unsigned long long>();
     const int64_t tW = s->sparse ? s->Wd : s->W;
     const int variant = (int)ctx->option(OPT_BITSET_KERNEL, 3);   // A/B selection
     // Diagonal tiles of an upper-triangle region (row0 == col0) get their
@@ -1474,7 +1474,20 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
         }
         it = s->plans.emplace(key, std::move(plan)).first;
     }
-    MatrixPlan& p = *it->second;
+    return *it->second;
+}
+
+void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1,
+                   bool upper, int32_t* d_I, int64_t ldI) {
+    hipStream_t st = ctx->stream;
+    const int64_t nr = r1 - r0, nc = c1 - c0;
+    if (nr <= 0 || nc <= 0) return;
+    const unsigned long long* tbits = s->sparse ? s->dbits.as<unsigned long long>() : s->bits.as<unsigned long long>();
+    const int64_t tW = s->sparse ? s->Wd : s->W;
+    const int variant = (int)ctx->option(OPT_BITSET_KERNEL, 3);   // A/B selection
+    const bool split_diag = variant != 1 && upper && ctx->option(OPT_BITSET_DIAG, 1) != 0;
+    (void)split_diag;
+    MatrixPlan& p = matrix_plan(ctx, s, r0, r1, c0, c1, upper);
     if (variant == 1 ? p.ntiles == 0 : p.at[4] == 0) return;   // no pair in the region
 
     // Rare kernel per call from the cost model (rare_choice): list-major opens
@@ -1493,11 +1506,12 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     // The sparse words and the list-major rare kernel add atomically, like
     // the dense tiles, so they run on the side stream beside them.
     const bool side = overlap || s->sparse;
+    bool rare_done = false;               // the sparse chunk reduce added the rare pairs
     if (!ctx->capturing) GD_HIP(hipEventRecord(ctx->ev_k0, st));
     if (side) {
         GD_HIP(hipEventRecord(ctx->ev_fork, st));
         GD_HIP(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
-        if (s->sparse) sparse_matrix(ctx, s, r0, r1, c0, c1, upper, d_I, ldI, ctx->side, p.sparse);
+        if (s->sparse) rare_done = sparse_matrix(ctx, s, r0, r1, c0, c1, upper, d_I, ldI, ctx->side, p.sparse);
         // beside the sparse kernel the list-major rare kernel goes to the main
         // stream after the dense tiles (the side stream is busy until the
         // sparse tiles and their reduce end: C2 0.0185 ms in line there)
@@ -1560,14 +1574,14 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
             }
         }
     }
-    if (overlap && s->sparse)
+    if (overlap && s->sparse && !rare_done)
         rare_pairs_kernel<<<grid_for(s->n_rare, 256, 256 * 64), 256, 0, st>>>(
             s->post_off.as<int64_t>(), s->post_sets.as<uint32_t>(), s->post_w.as<uint32_t>(), s->n_rare, r0, r1, c0,
             c1, upper ? 1 : 0, d_I, ldI);
     GD_HIP(hipGetLastError());
     ctx->last.launches = 1;
     if (side) GD_HIP(hipStreamWaitEvent(st, ctx->ev_join, 0));
-    if (s->n_rare > 0) {
+    if (s->n_rare > 0 && !rare_done) {
         if (overlap) {
         } else if (list_major) {
             rare_pairs_kernel<<<grid_for(s->n_rare, 256, 256 * 64), 256, 0, st>>>(
@@ -1596,6 +1610,31 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
                                                                              ldI);
         GD_HIP(hipGetLastError());
     }
+}
+
+bool bitset_matrix_fused(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1,
+                         bool upper, unsigned flags, int32_t* d_I, int64_t ldI, double* d_D, int64_t ldD) {
+    // One stream, two launches: the sparse tile kernel (dense words folded
+    // in) and its chunk reduce, which adds the rare pairs, STORES I (no
+    // zeroing) and writes D (no epilogue launch). Only when every count of
+    // the region comes from that reduce: sparse tier, no dense-word launch,
+    // chunk partials, the rare pairs in its table (or no rare tier).
+    if (!s->sparse || !d_D || ctx->option(OPT_SPARSE_FUSED, 1) == 0) return false;
+    if (r1 <= r0 || c1 <= c0 || !(s->sp_fold_dense || s->Wd == 0)) return false;
+    MatrixPlan& p = matrix_plan(ctx, s, r0, r1, c0, c1, upper);
+    sparse_plan(ctx, s, r0, r1, c0, c1, upper, ctx->stream, p.sparse);
+    if (p.sparse.ntiles == 0 || !p.sparse.use_part || (s->n_rare > 0 && !p.sparse.rare_in)) return false;
+    SparseEpilogue ep;
+    ep.D = d_D;
+    ep.ldD = ldD;
+    ep.off = s->off.as<int64_t>();
+    ep.empty_nan = (flags & GDIST_EMPTY_NAN) ? 1 : 0;
+    hipStream_t st = ctx->stream;
+    if (!ctx->capturing) GD_HIP(hipEventRecord(ctx->ev_k0, st));
+    sparse_matrix(ctx, s, r0, r1, c0, c1, upper, d_I, ldI, st, p.sparse, &ep);
+    if (!ctx->capturing) GD_HIP(hipEventRecord(ctx->ev_k1, st));
+    ctx->last.launches = 1;
+    return true;
 }
 
 namespace {

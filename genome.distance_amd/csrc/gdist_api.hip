@@ -25,7 +25,8 @@ const char* const kOptNames[OPT_COUNT] = {
     "reps_block",      "locus_order",     "sparse",          "sparse_zmax",     "sparse_wg_per_cu",
     "sparse_occ",      "sparse_sun",      "sketch_k",        "sketch_tile",     "sparse_part_budget",
     "guides",          "force_exchange",  "sparse_kernel",   "sparse_chunks",   "fold_dense_words", "sparse_abl",      "graph",
-    "sparse_shape",    "sparse_absorb",   "sparse_balance",  "time_sparse",     "sparse_xcd",      "sparse_fold",
+    "sparse_shape",    "sparse_absorb",   "sparse_balance",  "time_sparse",     "sparse_xcd",      "sparse_rare",     "sparse_fused",
+    "sparse_fold",
 };
 
 static int option_index(const char* name) {
@@ -795,9 +796,11 @@ int gdist_intersect_matrix(gdist_ctx* ctx, const gdist_sets* sets, int64_t r0, i
                 ctx->capturing = true;
                 bool ok = true;
                 try {
-                    zero_counts(ctx, r0, r1, c0, c1, upper, dI, ldI);
-                    bitset_matrix(ctx, s, r0, r1, c0, c1, upper, dI, ldI);
-                    if (D_out) distance_epilogue(ctx, s, r0, r1, c0, c1, upper, flags, dI, ldI, D_out, ld);
+                    if (!bitset_matrix_fused(ctx, s, r0, r1, c0, c1, upper, flags, dI, ldI, D_out, ld)) {
+                        zero_counts(ctx, r0, r1, c0, c1, upper, dI, ldI);
+                        bitset_matrix(ctx, s, r0, r1, c0, c1, upper, dI, ldI);
+                        if (D_out) distance_epilogue(ctx, s, r0, r1, c0, c1, upper, flags, dI, ldI, D_out, ld);
+                    }
                 } catch (...) {
                     ok = false;
                 }
@@ -820,19 +823,24 @@ int gdist_intersect_matrix(gdist_ctx* ctx, const gdist_sets* sets, int64_t r0, i
             }
             g.calls++;
         }
-        if (m == GDIST_METHOD_BITSET)   // accumulated with atomics
-            zero_counts(ctx, r0, r1, c0, c1, upper && dev, dI, ldI);
-        if (m == GDIST_METHOD_BITSET) bitset_matrix(ctx, s, r0, r1, c0, c1, upper, dI, ldI);
-        else sorted_matrix(ctx, s, r0, r1, c0, c1, upper, dI, ldI);
         DevBuf tD;
+        double* dD = nullptr;
+        int64_t ldD = 0;
         if (D_out) {
-            double* dD;
-            int64_t ldD;
             if (dev) { dD = D_out; ldD = ld; }
             else { tD.alloc((size_t)nr * nc * 8, st); dD = tD.as<double>(); ldD = nc; }
-            distance_epilogue(ctx, s, r0, r1, c0, c1, upper, flags, dI, ldI, dD, ldD);
-            if (!dev) copy_out_rows(ctx, dD, 8, nr, nc, r0, c0, upper, D_out, ld);
         }
+        // the fused sparse step writes I and D itself (bitset.hip)
+        const bool fused = m == GDIST_METHOD_BITSET && dD &&
+                           bitset_matrix_fused(ctx, s, r0, r1, c0, c1, upper, flags, dI, ldI, dD, ldD);
+        if (!fused) {
+            if (m == GDIST_METHOD_BITSET)   // accumulated with atomics
+                zero_counts(ctx, r0, r1, c0, c1, upper && dev, dI, ldI);
+            if (m == GDIST_METHOD_BITSET) bitset_matrix(ctx, s, r0, r1, c0, c1, upper, dI, ldI);
+            else sorted_matrix(ctx, s, r0, r1, c0, c1, upper, dI, ldI);
+            if (D_out) distance_epilogue(ctx, s, r0, r1, c0, c1, upper, flags, dI, ldI, dD, ldD);
+        }
+        if (D_out && !dev) copy_out_rows(ctx, dD, 8, nr, nc, r0, c0, upper, D_out, ld);
         if (I_out && !dev) copy_out_rows(ctx, dI, 4, nr, nc, r0, c0, upper, I_out, ld);
         gdist::finish_timing(ctx, true, dev);
     });

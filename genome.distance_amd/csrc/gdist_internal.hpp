@@ -127,6 +127,10 @@ struct SparseScratch {
     bool ready = false;
     DevBuf tiles, part;   // tile list, per-chunk counters
     DevBuf bounds;        // int32 [nchunks + 1]: first sparse word of each chunk (cost-balanced)
+    // the rare tier's pairs of the region, added by the chunk reduce (no rare
+    // kernel): keys tile << 14 | counter slot, weights, CSR over (tile, 512-slot group)
+    DevBuf rp_key, rp_w, rp_off;
+    bool rare_in = false;
     int nchunks = 0;
     bool use_part = false;   // chunks store partials (else flush with atomics)
     int64_t ntiles = 0;
@@ -195,6 +199,8 @@ enum Opt : int {
     OPT_SPARSE_BALANCE,     // 1: chunk bounds at equal modelled cost, words dealt to waves one at a time
     OPT_TIME_SPARSE,        // 1: HIP events around the sparse tile kernel (no hipGraph replay; bench roofline)
     OPT_SPARSE_XCD,         // 1: chunk c of every tile on XCD c mod 8 (default 0: tile-major order; A/B lost)
+    OPT_SPARSE_RARE,        // 0: the rare tier's pairs by the rare kernel, not the sparse chunk reduce
+    OPT_SPARSE_FUSED,       // 0: no fused reduce + epilogue (zeroing, rare kernel, epilogue launched apart)
     OPT_SPARSE_FOLD,        // at most this many (padded) dense words counted inside the v5 / v6 tile kernel
                             // (8 per chunk; default 64, 0: the dense-word tile launch)
     OPT_COUNT
@@ -436,9 +442,15 @@ void free_bitsets(gdist_sets* s);
 void build_bitsets(gdist_ctx* ctx, gdist_sets* s, unsigned flags, int64_t rare_threshold = -1);
 void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0,
                    int64_t c1, bool upper, int32_t* d_I, int64_t ldI);
+// the fused sparse step (sparse tiles + reduce storing I and D): true when it
+// ran, false when the region needs zeroing + bitset_matrix + epilogue
+bool bitset_matrix_fused(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1,
+                         bool upper, unsigned flags, int32_t* d_I, int64_t ldI, double* d_D, int64_t ldD);
 
 // sparse.hip — locus order of the dense dictionary, complement-sparse words
-constexpr int kGuides = 2;                       // guide sequences per packed collection
+constexpr int kGuides = 8;                       // guide sequences per packed collection (C2-realistic, 8
+                                                 // clades: 2 -> 8 guides took the step 4.60 -> 3.25 ms; C2 and
+                                                 // pack time unchanged, profiles/r02/realistic/guides.txt)
 constexpr int kSparseStageEntries = 640;         // sparse v2: entries per side a window may hold
 constexpr int kFoldDenseWords = 0;               // dense words folded into the sparse flush: off (the
                                                  // tile launch overlaps the sparse kernel; the fold runs after it)
@@ -458,8 +470,19 @@ void locus_perm(gdist_ctx* ctx, DevBuf& key, int64_t U, DevBuf& perm);
 void build_sparse_words(gdist_ctx* ctx, gdist_sets* s);
 void free_sparse(gdist_sets* s);
 double sparse_block_cost_s(const gdist_sets* s, double f_area, double tiles);
-void sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1, bool upper,
-                   int32_t* d_I, int64_t ldI, hipStream_t st, SparseScratch& sc);
+// Fused epilogue of a sparse step (bitset_matrix_fused): the chunk reduce
+// stores I (no zeroing) and writes D, the rare pairs come with it
+struct SparseEpilogue {
+    double* D = nullptr;
+    int64_t ldD = 0;
+    const int64_t* off = nullptr;         // set offsets: sizes n_i
+    int empty_nan = 0;
+};
+void sparse_plan(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1, bool upper,
+                 hipStream_t st, SparseScratch& sc);
+// returns true when the rare tier's pairs were added with the sparse words
+bool sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1, bool upper,
+                   int32_t* d_I, int64_t ldI, hipStream_t st, SparseScratch& sc, const SparseEpilogue* ep = nullptr);
 
 // sorted.hip
 void build_segments(gdist_ctx* ctx, gdist_sets* s);

@@ -1049,7 +1049,12 @@ __global__ __launch_bounds__(256) void sparse_reduce_kernel(const int32_t* __res
                                                             int64_t r1, int64_t c0, int64_t c1, int upper,
                                                             int32_t* __restrict__ I, int64_t ldI,
                                                             const unsigned long long* __restrict__ dbits,
-                                                            int64_t Wdp, int64_t N) {
+                                                            int64_t Wdp, int64_t N, const uint32_t* __restrict__ rp_key,
+                                                            const uint32_t* __restrict__ rp_w,
+                                                            const int64_t* __restrict__ rp_off,
+                                                            double* __restrict__ D, int64_t ldD,
+                                                            const int64_t* __restrict__ soff, int empty_nan) {
+#pragma clang fp contract(off)
     constexpr int per_tile = SB * SB / kReduceCnt / kReduceGroups;       // workgroups per tile
     __shared__ uint32_t sum[4][kReduceCnt][kReduceGroups];               // 8 KiB
     const int tile = blockIdx.x / per_tile;
@@ -1075,6 +1080,14 @@ __global__ __launch_bounds__(256) void sparse_reduce_kernel(const int32_t* __res
 #pragma unroll
     for (int k = 0; k < kReduceCnt; k++) sum[wv][k][lane] = acc[k];
     __syncthreads();
+    if (rp_off) {                            // the rare tier's pairs of this group's 512 slots
+        const int64_t grp = (int64_t)tile * per_tile + (blockIdx.x % per_tile);
+        for (int64_t p = rp_off[grp] + threadIdx.x; p < rp_off[grp + 1]; p += 256) {
+            const int c = (int)(rp_key[p] & 511);
+            atomicAdd(&sum[0][c % kReduceCnt][c / kReduceCnt], rp_w[p]);
+        }
+        __syncthreads();
+    }
     // 512 counters per workgroup: each thread finalizes two
     for (int e = threadIdx.x; e < kReduceCnt * kReduceGroups; e += 256) {
         const int gl = e / kReduceCnt, k = e % kReduceCnt;               // consecutive threads: consecutive counters
@@ -1083,8 +1096,18 @@ __global__ __launch_bounds__(256) void sparse_reduce_kernel(const int32_t* __res
         const int a = t >> 7, b = ((t & (SB - 1)) - a) & (SB - 1);
         const int64_t i = (int64_t)tiles[tile].x * SB + a, j = (int64_t)tiles[tile].y * SB + b;
         if (i < r0 || i >= r1 || j < c0 || j >= c1 || (upper && j <= i)) continue;
-        const int v = (int)Us - nc[i] - nc[j] + dense_pair(dbits, Wdp, N, i, j) + (int)tot;
-        if (v) atomicAdd(I + (i - r0) * ldI + (j - c0), v);
+        int v = (int)Us - nc[i] - nc[j] + dense_pair(dbits, Wdp, N, i, j) + (int)tot;
+        if (D && i == j) v = (int)(soff[i + 1] - soff[i]);        // a set with itself (self_pairs_kernel)
+        if (D) {                             // fused: the only writer of I over the region, then D
+            I[(i - r0) * ldI + (j - c0)] = v;
+            const int64_t na = soff[i + 1] - soff[i], nb = soff[j + 1] - soff[j];
+            double d;
+            if (v > 0) d = 1.0 - (double)v / (double)(na + nb - v);      // as epilogue_kernel (bitset.hip)
+            else d = (empty_nan && na + nb == 0) ? __builtin_nan("") : 1.0;
+            D[(i - r0) * ldD + (j - c0)] = d;
+        } else if (v) {
+            atomicAdd(I + (i - r0) * ldI + (j - c0), v);
+        }
     }
 }
 
@@ -1245,6 +1268,9 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
     const double t_plain = pairs * (double)W / kDenseWordPairsPerS;
     const double t_split = pairs * (double)Wdp / kDenseWordPairsPerS + products / kSparseProductsPerS +
                            tiles * (double)Ws / kSparseItemsPerS;
+    if (ctx->trace())
+        fprintf(stderr, "gdist: sparse split model: plain tiles %.3f ms, split %.3f ms (%lld sparse words, %.3g products)\n",
+                t_plain * 1e3, t_split * 1e3, (long long)Ws, products);
     if (Ws == 0 || !(zm || t_split < 0.8 * t_plain)) return;
     const int64_t nblk = ceil_div(N, SB);
     GD_REQUIRE((double)nblk * (double)Ws < 2e9, "sparse word index too large");
@@ -1391,8 +1417,76 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
 // Adds the sparse words' share of |A ∩ B| to I over the region (atomics;
 // the caller zeroed I, the dense tiles add theirs). Launched on `st`; `sc`
 // (the region's cached plan) holds the tile list and the chunk partials.
-void sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1, bool upper,
-                   int32_t* d_I, int64_t ldI, hipStream_t st, SparseScratch& sc) {
+// The rare tier's pairs of a region, for the chunk reduce: every posting
+// list adds its weight to each of its pairs in the region (the semantics of
+// rare_pairs_kernel, bitset.hip), here expanded once per region plan on the
+// host, keyed by (tile, counter slot in the cnt_index layout), merged and
+// bucketed by (tile, 512-slot reduce group). Lists are few and short when the
+// sparse tier runs (C2: 0.2 M lists, ~0.3 M pairs); past kRarePairsMax pairs
+// the rare kernel keeps them.
+constexpr int64_t kRarePairsMax = int64_t(1) << 25;
+static void rare_pair_table(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1,
+                            bool upper, const std::vector<int2>& tiles, hipStream_t st, SparseScratch& sc) {
+    sc.rare_in = false;
+    if (s->n_rare == 0) return;
+    if (ctx->option(OPT_SPARSE_RARE, 1) == 0 || s->rare_records > kRarePairsMax) return;
+    std::vector<int64_t> poff(s->n_rare + 1);
+    std::vector<uint32_t> psets(s->rare_records), pw(s->n_rare);
+    d2h(poff.data(), s->post_off.p, poff.size() * 8, st);
+    d2h(psets.data(), s->post_sets.p, psets.size() * 4, st);
+    d2h(pw.data(), s->post_w.p, pw.size() * 4, st);
+    double npairs = 0.0;
+    for (int64_t l = 0; l < s->n_rare; l++) {
+        const double m = (double)(poff[l + 1] - poff[l]);
+        npairs += 0.5 * m * (m - 1.0) * (upper ? 1.0 : 2.0);
+    }
+    if (npairs > (double)kRarePairsMax) return;
+    const int64_t nb = ceil_div(s->nsets, SB);
+    std::vector<int32_t> tile_of((size_t)nb * nb, -1);
+    for (size_t t = 0; t < tiles.size(); t++) tile_of[(size_t)tiles[t].x * nb + tiles[t].y] = (int32_t)t;
+    std::vector<std::pair<uint32_t, uint32_t>> kv;
+    kv.reserve((size_t)npairs);
+    bool missing = false;
+    auto emit = [&](int64_t i, int64_t j, uint32_t w) {
+        const int32_t t = tile_of[(size_t)(i / SB) * nb + (j / SB)];
+        if (t < 0) { missing = true; return; }
+        const int a = (int)(i % SB), b = (int)(j % SB);
+        kv.emplace_back(((uint32_t)t << 14) | (uint32_t)(a * SB + ((b + a) & (SB - 1))), w);
+    };
+    for (int64_t l = 0; l < s->n_rare; l++)
+        for (int64_t x = poff[l]; x < poff[l + 1]; x++) {
+            const int64_t a = psets[x];
+            for (int64_t y = x + 1; y < poff[l + 1]; y++) {
+                const int64_t b = psets[y];          // b > a
+                if (a >= r0 && a < r1 && b >= c0 && b < c1) emit(a, b, pw[l]);
+                if (!upper && b >= r0 && b < r1 && a >= c0 && a < c1) emit(b, a, pw[l]);
+            }
+        }
+    GD_REQUIRE(!missing, "rare pair outside the sparse plan's tiles");
+    GD_REQUIRE(tiles.size() < (size_t(1) << 18), "too many tiles for the rare pair keys");
+    std::sort(kv.begin(), kv.end());
+    std::vector<uint32_t> keys, ws;
+    for (const auto& e : kv) {
+        if (!keys.empty() && keys.back() == e.first) ws.back() += e.second;
+        else { keys.push_back(e.first); ws.push_back(e.second); }
+    }
+    const int64_t ngroups = (int64_t)tiles.size() * (SB * SB / 512);
+    std::vector<int64_t> goff(ngroups + 1, 0);
+    for (uint32_t k : keys) goff[(k >> 9) + 1]++;
+    for (int64_t g = 0; g < ngroups; g++) goff[g + 1] += goff[g];
+    sc.rp_key.alloc(keys.size() * 4 + 4, st);
+    sc.rp_w.alloc(ws.size() * 4 + 4, st);
+    sc.rp_off.alloc(goff.size() * 8, st);
+    if (!keys.empty()) {
+        h2d(sc.rp_key.p, keys.data(), keys.size() * 4, st);
+        h2d(sc.rp_w.p, ws.data(), ws.size() * 4, st);
+    }
+    h2d(sc.rp_off.p, goff.data(), goff.size() * 8, st);
+    sc.rare_in = true;
+}
+
+void sparse_plan(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1, bool upper,
+                 hipStream_t st, SparseScratch& sc) {
     if (!s->sparse || r1 <= r0 || c1 <= c0) return;
     if (!sc.ready) {
         std::vector<int2> tiles;
@@ -1520,9 +1614,17 @@ void sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
                     sc.use_part ? "partials" : "atomic flush", s->sp_win, (long long)s->sp_pos_words,
                     (long long)s->Ws);
         GD_REQUIRE(sc.ntiles * sc.nchunks < (int64_t(1) << 31), "sparse grid too large");
+        if (sc.use_part) rare_pair_table(ctx, s, r0, r1, c0, c1, upper, tiles, st, sc);
         sc.ready = true;
     }
-    if (sc.ntiles == 0) return;
+}
+
+bool sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1, bool upper,
+                   int32_t* d_I, int64_t ldI, hipStream_t st, SparseScratch& sc, const SparseEpilogue* ep) {
+    if (!s->sparse || r1 <= r0 || c1 <= c0) return false;
+    sparse_plan(ctx, s, r0, r1, c0, c1, upper, st, sc);
+    GD_REQUIRE(!ep || (sc.use_part && (s->n_rare == 0 || sc.rare_in)), "fused sparse epilogue without its plan");
+    if (sc.ntiles == 0) return false;
     const int nchunks = sc.nchunks;
     const int64_t nt = sc.ntiles;
     // Kernel 6 (default): v5's walk over 1 x 2 micro-tiles, 3 slots (6
@@ -1597,9 +1699,13 @@ void sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     if (sc.use_part) {
         sparse_reduce_kernel<<<(unsigned)(nt * (SB * SB / kReduceCnt / kReduceGroups)), 256, 0, st>>>(
             sc.part.as<int32_t>(), nchunks, sc.tiles.as<int2>(), s->sp_nc.as<int32_t>(), s->sp_U, r0, r1, c0, c1,
-            upper ? 1 : 0, d_I, ldI, fold, s->Wd, s->nsets);
+            upper ? 1 : 0, d_I, ldI, fold, s->Wd, s->nsets,
+            sc.rare_in ? sc.rp_key.as<uint32_t>() : nullptr, sc.rare_in ? sc.rp_w.as<uint32_t>() : nullptr,
+            sc.rare_in ? sc.rp_off.as<int64_t>() : nullptr, ep ? ep->D : nullptr, ep ? ep->ldD : 0,
+            ep ? ep->off : nullptr, ep ? ep->empty_nan : 0);
         GD_HIP(hipGetLastError());
     }
+    return sc.use_part && sc.rare_in;
 }
 
 }  // namespace gdist

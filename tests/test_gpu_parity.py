@@ -580,7 +580,8 @@ def test_rare_tier_thresholds_exact(ctx, T, kernel, dedup, opts):
                                   "kernel_v4", "kernel_v4_rows", "kernel_v5", "kernel_v5_rows", "kernel_v5_sun6",
                                   "kernel_v5_atomic", "kernel_v6_rows", "kernel_v6_sun4", "kernel_v6_quads",
                                   "kernel_v6_2x2", "kernel_v6_2x2_rows", "kernel_v6_atomic", "absorb",
-                                  "mixed_slabs", "mixed_slabs_atomic", "mixed_tiles"])
+                                  "mixed_slabs", "mixed_slabs_atomic", "mixed_tiles", "unfused", "rare_kernel",
+                                  "unfused_rare_kernel"])
 def test_sparse_complement_words_exact(ctx, mode, opts):
     """The dense tier in locus order with complement-sparse words: counts and
     distances are bit-exact against the oracle over upper triangles,
@@ -615,6 +616,11 @@ def test_sparse_complement_words_exact(ctx, mode, opts):
                 "mixed_slabs": {"sparse_zmax": 12, "sparse_fold": 100000},
                 "mixed_slabs_atomic": {"sparse_zmax": 12, "sparse_fold": 100000, "sparse_part_budget": 0},
                 "mixed_tiles": {"sparse_zmax": 12, "sparse_fold": 0},
+                # the default step is fused (tiles + a reduce that adds the rare pairs and
+                # stores I and D); the same counts with zeroing + rare kernel + epilogue apart
+                "unfused": {"sparse_fused": 0},
+                "rare_kernel": {"sparse_rare": 0},
+                "unfused_rare_kernel": {"sparse_fused": 0, "sparse_rare": 0},
                 "many_chunks": {"sparse_zmax": 100000, "sparse_chunks": 37},
                 # words counted from either side (complement / positive), model's choice
                 # a dense-only dictionary: the substitution kmers two or more
