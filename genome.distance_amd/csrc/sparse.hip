@@ -176,12 +176,42 @@ __global__ __launch_bounds__(256) void sparse_fill_kernel(const unsigned long lo
     }
 }
 
-// 16-byte {complement word, set} records of the entries (E16 tile kernels)
+// LDS counter of local pair (row a, column b), as a 16-bit slot t (dword
+// t >> 1, half t & 1): row a owns dwords [64 a, 64 a + 64); column b sits in
+// dword (b >> 1) ^ (a & 63) of it, half b & 1. The XOR rotation by the row
+// spreads the products of one word (its rows x its columns) over the banks.
+// The records carry the two halves of the address precomputed (entry_codes):
+// a row entry's byte base with its rotation key, a column entry's byte offset
+// and half shift, so a product's counter costs one XOR and one shift.
+__host__ __device__ __forceinline__ int cnt_index(int a, int b) {
+    return ((a * 64 + ((b >> 1) ^ (a & 63))) << 1) | (b & 1);
+}
+__host__ __device__ __forceinline__ void cnt_pair(int t, int& a, int& b) {
+    const int d = t >> 1;
+    a = d >> 6;
+    b = (((d & 63) ^ (a & 63)) << 1) | (t & 1);
+}
+// record codes of set s (0..127): row role = byte address of its row with the
+// rotation key in bits 2-7 (row bytes 256 s, keys < 256); column role = shift
+// (s & 1) << 4 in bits 0-4 and its dword's byte offset (s >> 1) << 2 in bits 16+
+__host__ __device__ __forceinline__ uint32_t row_code(int s) { return ((uint32_t)s << 8) | ((uint32_t)(s & 63) << 2); }
+__host__ __device__ __forceinline__ uint32_t col_code(int s) {
+    return ((uint32_t)(s & 1) << 4) | (((uint32_t)(s >> 1) << 2) << 16);
+}
+// the counter add of a product of row code r and column code c (byte address r ^ c >> 16)
+__device__ __forceinline__ void cnt_add(uint32_t* cnt, uint32_t r, uint32_t c, uint32_t v) {
+    atomicAdd(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(cnt) + (r ^ (c >> 16))), v << (c & 31));
+}
+
+// 16-byte records of the entries (E16 / v5 / v6 tile kernels): {complement
+// word, row_code(set) | col_code(set) << 32}
 __global__ void sparse_records_kernel(const unsigned long long* __restrict__ word, const uint8_t* __restrict__ set,
                                       int64_t n, ulonglong2* __restrict__ ent) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride)
-        ent[e] = make_ulonglong2(word[e], (unsigned long long)set[e]);
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
+        const int st = set[e];
+        ent[e] = make_ulonglong2(word[e], (unsigned long long)row_code(st) | ((unsigned long long)col_code(st) << 32));
+    }
 }
 
 // ---- the sparse tile kernel ---------------------------------------------
@@ -208,10 +238,6 @@ constexpr int kChunkWords = 1023;
 constexpr int kFoldSlabWords = 8;
 constexpr int SNW = SNT / 64;
 
-// LDS counter of local pair (row a, column b): the column is rotated by the
-// row, so the products of one word (its rows x its columns, column fastest
-// across lanes) land on distinct banks instead of one bank per column
-__device__ __forceinline__ int cnt_index(int a, int b) { return a * SB + ((b + a) & (SB - 1)); }
 
 // The dense words folded into the flush (a few words): their
 // AND+popcount for one pair, from the dense words stored word-major
@@ -348,7 +374,9 @@ __global__ __launch_bounds__(SNT, OCC) void sparse_tile_kernel(
                 if (E16) {
                     const ulonglong2 er = eA[(uint32_t)ri[u]], ec = (diag ? eA : eB)[(uint32_t)ci[u]];
                     wr[u] = er.x; wc[u] = ec.x;
-                    sr[u] = (int)er.y; sc[u] = (int)ec.y;
+                    sr[u] = (int)((uint32_t)er.y >> 8);                               // row code -> set
+                    const uint32_t cc = (uint32_t)(ec.y >> 32);                        // column code -> set
+                    sc[u] = (int)(((cc >> 18) << 1) | ((cc >> 4) & 1));
                 } else {
                     wr[u] = wA[(uint32_t)ri[u]]; wc[u] = (diag ? wA : wB)[(uint32_t)ci[u]];
                     sr[u] = sA[(uint32_t)ri[u]]; sc[u] = (diag ? sA : sB)[(uint32_t)ci[u]];
@@ -376,7 +404,8 @@ __global__ __launch_bounds__(SNT, OCC) void sparse_tile_kernel(
         return;
     }
     for (int t = threadIdx.x; t < SB * SB; t += SNT) {
-        const int a = t >> 7, b = ((t & (SB - 1)) - a) & (SB - 1);
+        int a, b;
+        cnt_pair(t, a, b);
         const int64_t i = A * SB + a, j = B * SB + b;
         if (i < r0 || i >= r1 || j < c0 || j >= c1 || (upper && j <= i)) continue;
         // the constant part once per pair: by chunk 0 (chunks flush with atomics)
@@ -565,7 +594,8 @@ __global__ __launch_bounds__(S2T, OCC) void sparse_tile_kernel2(
         return;
     }
     for (int t = threadIdx.x; t < SB * SB; t += S2T) {
-        const int a = t >> 7, b = ((t & (SB - 1)) - a) & (SB - 1);
+        int a, b;
+        cnt_pair(t, a, b);
         const int64_t i = A * SB + a, j = B * SB + b;
         if (i < r0 || i >= r1 || j < c0 || j >= c1 || (upper && j <= i)) continue;
         // the constant part once per pair: by chunk 0 (chunks flush with atomics)
@@ -724,7 +754,8 @@ __global__ __launch_bounds__(S2T, OCC) void sparse_tile_kernel4(
         return;
     }
     for (int t = threadIdx.x; t < SB * SB; t += S2T) {
-        const int a = t >> 7, b = ((t & (SB - 1)) - a) & (SB - 1);
+        int a, b;
+        cnt_pair(t, a, b);
         const int64_t i = A * SB + a, j = B * SB + b;
         if (i < r0 || i >= r1 || j < c0 || j >= c1 || (upper && j <= i)) continue;
         // the constant part once per pair: by chunk 0 (chunks flush with atomics)
@@ -821,14 +852,9 @@ __device__ __forceinline__ void sparse_walk5(const int4* __restrict__ rec, int i
         }
 #pragma unroll
         for (int u = 0; u < SUN; u++) {
-            const uint32_t sr = (uint32_t)a[u].y, sc = (uint32_t)b[u].y;
             const uint32_t v = (uint32_t)__popcll(a[u].x & b[u].x);
-            const uint32_t t0 = sr * SB + ((sc + sr) & (SB - 1));
-            atomicAdd(&cnt[t0 >> 1], v << ((t0 & 1) << 4));
-            if (DIAG && mirror) {
-                const uint32_t t1 = sc * SB + ((sr + sc) & (SB - 1));
-                atomicAdd(&cnt[t1 >> 1], v << ((t1 & 1) << 4));
-            }
+            cnt_add(cnt, (uint32_t)a[u].y, (uint32_t)(b[u].y >> 32), v);
+            if (DIAG && mirror) cnt_add(cnt, (uint32_t)b[u].y, (uint32_t)(a[u].y >> 32), v);
         }
     }
 }
@@ -886,13 +912,12 @@ __device__ __forceinline__ void sparse_walk6(const int4* __restrict__ rec, int i
         for (int u = 0; u < SUN; u++)
 #pragma unroll
             for (int i = 0; i < RW; i++) {
-                const uint32_t sr = (uint32_t)a[u][i].y;
+                const uint32_t rc = (uint32_t)a[u][i].y;
 #pragma unroll
                 for (int j = 0; j < CW; j++) {
                     const bool in = (i == 0 || i < nrow[u]) && (j == 0 || j < ncol[u]);
                     const uint32_t v = in ? (uint32_t)__popcll(a[u][i].x & b[u][j].x) : 0u;
-                    const uint32_t t0 = sr * SB + (((uint32_t)b[u][j].y + sr) & (SB - 1));
-                    atomicAdd(&cnt[t0 >> 1], v << ((t0 & 1) << 4));
+                    cnt_add(cnt, rc, (uint32_t)(b[u][j].y >> 32), v);
                 }
             }
     }
@@ -1025,7 +1050,8 @@ __global__ __launch_bounds__(SNT, OCC) void sparse_tile_kernel5(
         return;
     }
     for (int t = threadIdx.x; t < SB * SB; t += SNT) {
-        const int a = t >> 7, b = ((t & (SB - 1)) - a) & (SB - 1);
+        int a, b;
+        cnt_pair(t, a, b);
         const int64_t i = A * SB + a, j = B * SB + b;
         if (i < r0 || i >= r1 || j < c0 || j >= c1 || (upper && j <= i)) continue;
         const int v = (int)((cnt[t >> 1] >> ((t & 1) << 4)) & 0xFFFFu) +
@@ -1093,7 +1119,8 @@ __global__ __launch_bounds__(256) void sparse_reduce_kernel(const int32_t* __res
         const int gl = e / kReduceCnt, k = e % kReduceCnt;               // consecutive threads: consecutive counters
         const uint32_t tot = sum[0][k][gl] + sum[1][k][gl] + sum[2][k][gl] + sum[3][k][gl];
         const int t = ((blockIdx.x % per_tile) * kReduceGroups + gl) * kReduceCnt + k;   // cnt_index layout
-        const int a = t >> 7, b = ((t & (SB - 1)) - a) & (SB - 1);
+        int a, b;
+        cnt_pair(t, a, b);
         const int64_t i = (int64_t)tiles[tile].x * SB + a, j = (int64_t)tiles[tile].y * SB + b;
         if (i < r0 || i >= r1 || j < c0 || j >= c1 || (upper && j <= i)) continue;
         int v = (int)Us - nc[i] - nc[j] + dense_pair(dbits, Wdp, N, i, j) + (int)tot;
@@ -1451,7 +1478,7 @@ static void rare_pair_table(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int
         const int32_t t = tile_of[(size_t)(i / SB) * nb + (j / SB)];
         if (t < 0) { missing = true; return; }
         const int a = (int)(i % SB), b = (int)(j % SB);
-        kv.emplace_back(((uint32_t)t << 14) | (uint32_t)(a * SB + ((b + a) & (SB - 1))), w);
+        kv.emplace_back(((uint32_t)t << 14) | (uint32_t)cnt_index(a, b), w);
     };
     for (int64_t l = 0; l < s->n_rare; l++)
         for (int64_t x = poff[l]; x < poff[l + 1]; x++) {
