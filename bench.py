@@ -232,10 +232,19 @@ def main():
         step()                       # device outputs: returns once queued
     barrier()
     elapsed = time.perf_counter() - t0
-    # the timed steps' kernel times (HIP events on the library's streams,
-    # recorded per step inside the timed region, read after it)
-    kernel_ms = ctx.recent_timings(args.steps)
     elapsed_max = max_over_ranks(elapsed)
+    # Kernel times, after the timed region: replayed steps record no timing
+    # events by default (they cost 13-18 us a step), so a short loop with
+    # option step_timing = 1 reads the steps' HIP-event spans (on the
+    # library's streams), and for the sparse tier a loop with time_sparse = 1
+    # the sparse tile kernel alone
+    kt = max(3, min(args.steps, 20))
+    prev_st = ctx.option("step_timing")
+    ctx.set_option("step_timing", 1)
+    for _ in range(kt):
+        step()
+    kernel_ms = ctx.recent_timings(kt)
+    ctx.set_option("step_timing", prev_st)
     # The sparse tile kernel alone, after the timed region (roofline): HIP
     # events around its launch on the stream it runs on (option time_sparse;
     # such calls run unreplayed, one event pair per call)

@@ -199,6 +199,7 @@ enum Opt : int {
     OPT_SPARSE_BALANCE,     // 1: chunk bounds at equal modelled cost, words dealt to waves one at a time
     OPT_TIME_SPARSE,        // 1: HIP events around the sparse tile kernel (no hipGraph replay; bench roofline)
     OPT_SPARSE_XCD,         // 1: chunk c of every tile on XCD c mod 8 (default 0: tile-major order; A/B lost)
+    OPT_STEP_TIMING,        // 1: graph-replayed steps record timing events too (default 0: they cost 13-18 us a step)
     OPT_SPARSE_RARE,        // 0: the rare tier's pairs by the rare kernel, not the sparse chunk reduce
     OPT_SPARSE_FUSED,       // 0: no fused reduce + epilogue (zeroing, rare kernel, epilogue launched apart)
     OPT_SPARSE_FOLD,        // at most this many (padded) dense words counted inside the v5 / v6 tile kernel
