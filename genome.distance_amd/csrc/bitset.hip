@@ -1361,9 +1361,22 @@ double bitset_block_cost_s(const gdist_sets* s, int64_t r0, int64_t r1, int64_t 
     double off, diag;
     dense_tiles(r0, r1, c0, c1, upper, &off, &diag);
     const double tW = s->sparse ? (s->sp_fold_dense ? 0.0 : (double)s->Wd) : (double)s->W;
-    // sparse tiles: ~ the block's pair area in 128 x 128 tiles, plus the partial ones on its row edge
-    const double sp_tiles = pairs / (double)(BT * BT) + (double)ceil_div(r1 - r0, BT);
-    return (off + kDiagTileShare * diag) * (double)(BT * BT) * tW / kDenseWordPairsPerS + rc.cost() +
+    // sparse tiles: exactly the tiles the block's sparse plan launches (a
+    // thin, unaligned row block still visits every word in each of its row
+    // blocks' tiles: round-2 G = 8 emulation, balance 0.76 with the area estimate)
+    double sp_tiles = 0.0;
+    if (s->sparse && r1 > r0 && c1 > c0)
+        for (int64_t A = r0 / BT; A <= (r1 - 1) / BT; A++)
+            for (int64_t B = c0 / BT; B <= (c1 - 1) / BT; B++) {
+                const int64_t rmin = std::max(r0, A * BT);
+                const int64_t cmax = std::min(c1, (B + 1) * BT) - 1;
+                if (!(upper && cmax <= rmin)) sp_tiles += 1.0;
+            }
+    // the rare tier's pairs ride in the sparse chunk reduce (sparse.hip,
+    // rare_pair_table) when the lists are few: no rare kernel then
+    const bool rare_in_reduce = s->sparse && s->n_rare > 0 && s->rare_records <= (int64_t(1) << 25);
+    return (off + kDiagTileShare * diag) * (double)(BT * BT) * tW / kDenseWordPairsPerS +
+           (rare_in_reduce ? 0.0 : rc.cost()) +
            sparse_block_cost_s(s, tot > 0 ? std::min(1.0, pairs / tot) : 1.0, sp_tiles);
 }
 
