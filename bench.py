@@ -148,8 +148,9 @@ def main():
     gen_s = time.time() - t
     kt = gdist.KmerType.PROT if cfg["protein"] else gdist.KmerType.DNA
     t = time.time()
-    local = gdist.KmerSets.from_sequences([blob[off[i]:off[i + 1]] for i in range(len(off) - 1)], cfg["k"], kt,
-                                          0, ctx)
+    # the genomes as FASTA bytes in host memory: one buffer + offsets, handed
+    # to gdist_sets_pack as they are (no per-genome copies)
+    local = gdist.KmerSets.from_blob(blob, off, cfg["k"], kt, 0, ctx)
     del blob
     pack_s = time.time() - t
     t = time.time()

@@ -1002,8 +1002,65 @@ int64_t choose_rare_threshold(const std::vector<uint64_t>& hist, int64_t nsets) 
     return bestT;
 }
 
-// bits of sets [0, nsets) against the dense dictionary (chunked pairs sort,
-// run ranks, scatter); rare-tier records appended to rare_out (capacity cap)
+// The fill without a sort: each set's codes are sorted (pack), and so are
+// the dense dictionary and the rare codes, so a wave takes a segment of
+// kFillSeg consecutive codes of ONE set, finds the segment's window in the
+// dictionary and in the rare codes (four binary searches, one lane each),
+// and each lane then searches its codes inside those windows (L1-resident).
+// Dense codes set their bit (locus position through perm), rare codes append
+// a (rare rank << 32 | set) record; singletons are skipped. Segments that
+// straddle a set boundary are cut there, so a window is always monotone.
+constexpr int kFillSeg = 2048;
+__device__ __forceinline__ int64_t lower_bound_u64(const uint64_t* __restrict__ a, int64_t lo, int64_t hi, uint64_t k) {
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (a[mid] < k) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+__global__ __launch_bounds__(256) void fill_search_kernel(
+    const uint64_t* __restrict__ codes, const int64_t* __restrict__ off, const int64_t* __restrict__ seg,
+    int64_t nseg, const uint64_t* __restrict__ dict, int64_t U, const uint64_t* __restrict__ rare, int64_t Ur,
+    int64_t W, unsigned long long* __restrict__ bits, int64_t id_base, unsigned long long* __restrict__ rare_out,
+    unsigned long long* __restrict__ rare_cnt, int64_t rare_cap, const uint32_t* __restrict__ perm) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (wave >= nseg) return;
+    // segment: (set << 40 | first code index) packed, its end the next segment's start or its set's end
+    const uint64_t sd = (uint64_t)seg[wave];
+    const int64_t set = (int64_t)(sd >> 40), b = (int64_t)(sd & ((1ull << 40) - 1));
+    const int64_t e = std::min<int64_t>(b + kFillSeg, off[set + 1]);
+    if (e <= b) return;
+    const uint64_t kfirst = codes[b], klast = codes[e - 1];
+    // lanes 0-3: the windows [lower_bound(first), upper_bound(last)) in dict and rare
+    int64_t w = 0;
+    if (lane == 0) w = lower_bound_u64(dict, 0, U, kfirst);
+    else if (lane == 1) w = lower_bound_u64(dict, 0, U, klast + 1 == 0 ? klast : klast + 1) + (klast == ~0ull);
+    else if (lane == 2) w = lower_bound_u64(rare, 0, Ur, kfirst);
+    else if (lane == 3) w = lower_bound_u64(rare, 0, Ur, klast + 1 == 0 ? klast : klast + 1) + (klast == ~0ull);
+    const int64_t dlo = __shfl((long long)w, 0, 64), dhi = std::min<int64_t>(U, __shfl((long long)w, 1, 64));
+    const int64_t rlo = __shfl((long long)w, 2, 64), rhi = std::min<int64_t>(Ur, __shfl((long long)w, 3, 64));
+    unsigned long long* row = bits + set * W;
+    for (int64_t i = b + lane; i < e; i += 64) {
+        const uint64_t k = codes[i];
+        const int64_t r = lower_bound_u64(dict, dlo, dhi, k);
+        if (r < dhi && dict[r] == k) {
+            const int64_t pos = perm ? (int64_t)perm[r] : r;     // bit position (locus order)
+            atomicOr(row + (pos >> 6), 1ull << (pos & 63));
+            continue;
+        }
+        const int64_t q = lower_bound_u64(rare, rlo, rhi, k);
+        if (q < rhi && rare[q] == k) {
+            const unsigned long long slot = atomicAdd(rare_cnt, 1ull);
+            if ((int64_t)slot < rare_cap)
+                rare_out[slot] = ((unsigned long long)q << 32) | (unsigned long long)(uint32_t)(set + id_base);
+        }
+    }
+}
+
+// bits of sets [0, nsets) against the dense dictionary (windowed searches,
+// or, option fill_sort, the chunked pairs sort + run ranks + scatter);
+// rare-tier records appended to rare_out (capacity cap)
 void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_t U, int64_t W,
                unsigned long long* bits, const uint64_t* rare, int64_t Ur, int64_t id_base,
                unsigned long long* rare_out, int64_t rare_cap, int64_t* rare_written, const uint32_t* perm) {
@@ -1013,7 +1070,26 @@ void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_
     GD_HIP(hipMemsetAsync(bits, 0, (size_t)s->nsets * W * 8, st));
     DevBuf rcnt(8, st);
     GD_HIP(hipMemsetAsync(rcnt.p, 0, 8, st));
-    if (U + Ur > 0) {
+    if (U + Ur > 0 && ctx->option(OPT_FILL_SORT, 0) == 0) {
+        // segments of <= kFillSeg codes inside one set, built on the host from the offsets
+        GD_REQUIRE(s->nsets < (int64_t(1) << 23) && s->h_off[s->nsets] < (int64_t(1) << 40),
+                   "collection too large for packed fill segments");
+        std::vector<int64_t> seg;
+        for (int64_t i = 0; i < s->nsets; i++)
+            for (int64_t b = s->h_off[i]; b < s->h_off[i + 1]; b += kFillSeg) seg.push_back((i << 40) | b);
+        const int64_t nseg = (int64_t)seg.size();
+        if (nseg) {
+            DevBuf dseg(nseg * 8, st);
+            h2d(dseg.p, seg.data(), nseg * 8, st);
+            const int64_t threads = nseg * 64;
+            fill_search_kernel<<<(unsigned)ceil_div(threads, 256), 256, 0, st>>>(
+                s->codes.as<uint64_t>(), s->off.as<int64_t>(), dseg.as<int64_t>(), nseg, dict, U, rare, Ur, W, bits,
+                id_base, rare_out, rcnt.as<unsigned long long>(), rare_cap, perm);
+            GD_HIP(hipGetLastError());
+            GD_HIP(hipStreamSynchronize(st));
+        }
+        tr.mark("fill: windowed searches + scatter");
+    } else if (U + Ur > 0) {
         int64_t s0 = 0;
         while (s0 < s->nsets) {
             int64_t s1 = s0 + 1;

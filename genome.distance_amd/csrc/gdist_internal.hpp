@@ -204,6 +204,7 @@ enum Opt : int {
     OPT_SPARSE_FUSED,       // 0: no fused reduce + epilogue (zeroing, rare kernel, epilogue launched apart)
     OPT_SPARSE_FOLD,        // at most this many (padded) dense words counted inside the v5 / v6 tile kernel
                             // (8 per chunk; default 64, 0: the dense-word tile launch)
+    OPT_FILL_SORT,          // 1: bitset fill by a (code, set) sort + run ranks (default 0: windowed searches)
     OPT_COUNT
 };
 extern const char* const kOptNames[OPT_COUNT];

@@ -274,6 +274,26 @@ class KmerSets(_Handle):
         return cls(ctx, h)
 
     @classmethod
+    def from_blob(cls, blob, offsets, k: int, kmer_type: KmerType = KmerType.DNA, flags: int = 0,
+                  ctx: Context | None = None) -> "KmerSets":
+        """Sequences already laid out as one byte buffer (bytes / bytearray /
+        uint8 array) with int64 offsets (n + 1): passed to gdist_sets_pack as
+        they are, no per-sequence copies (FASTA bytes read into memory)."""
+        ctx = ctx or Context.default()
+        off = np.ascontiguousarray(offsets, dtype=np.int64)
+        n = len(off) - 1
+        if isinstance(blob, np.ndarray):
+            buf = np.ascontiguousarray(blob, dtype=np.uint8)
+            ptr = buf.ctypes.data_as(C.c_char_p) if buf.size else b"\0"
+        else:
+            buf = blob if len(blob) else b"\0"
+            ptr = buf if isinstance(buf, bytes) else (C.c_char * len(buf)).from_buffer(buf)
+        h = C.c_void_p()
+        L.check(L.lib.gdist_sets_pack(ctx.h, kmer_type.kind, int(k), flags, ptr, L.ptr(off, C.c_int64), n,
+                                      C.byref(h)))
+        return cls(ctx, h)
+
+    @classmethod
     def from_device(cls, ctx: Context, d_seqs: int, d_off: int, nseqs: int, total_bytes: int, k: int,
                     kmer_type: KmerType = KmerType.DNA, flags: int = 0) -> "KmerSets":
         h = C.c_void_p()

@@ -581,7 +581,7 @@ def test_rare_tier_thresholds_exact(ctx, T, kernel, dedup, opts):
                                   "kernel_v5_atomic", "kernel_v6_rows", "kernel_v6_sun4", "kernel_v6_quads",
                                   "kernel_v6_2x2", "kernel_v6_2x2_rows", "kernel_v6_atomic", "absorb",
                                   "mixed_slabs", "mixed_slabs_atomic", "mixed_tiles", "unfused", "rare_kernel",
-                                  "unfused_rare_kernel"])
+                                  "unfused_rare_kernel", "fill_sort"])
 def test_sparse_complement_words_exact(ctx, mode, opts):
     """The dense tier in locus order with complement-sparse words: counts and
     distances are bit-exact against the oracle over upper triangles,
@@ -621,6 +621,8 @@ def test_sparse_complement_words_exact(ctx, mode, opts):
                 "unfused": {"sparse_fused": 0},
                 "rare_kernel": {"sparse_rare": 0},
                 "unfused_rare_kernel": {"sparse_fused": 0, "sparse_rare": 0},
+                # the bitset fill by the (code, set) sort + run ranks instead of windowed searches
+                "fill_sort": {"fill_sort": 1},
                 "many_chunks": {"sparse_zmax": 100000, "sparse_chunks": 37},
                 # words counted from either side (complement / positive), model's choice
                 # a dense-only dictionary: the substitution kmers two or more
@@ -825,3 +827,22 @@ def test_graph_replay_of_repeated_steps(ctx, opts, sparse):
             assert np.array_equal(I[mask], eI[mask]) and bits_equal(D[mask], eD[mask]), (r0, call)
             assert np.all(I[~mask] == -7), (r0, call)           # below the diagonal untouched
         dI.free(); dD.free()
+
+
+def test_from_blob_equals_from_sequences(ctx):
+    """KmerSets.from_blob (one buffer + offsets, as bytes, bytearray or a
+    uint8 array; what bench.py packs from) gives the same collection as
+    from_sequences: identical counts and distances."""
+    import gdist
+    seqs = synth_sets(40, 3000, 0.02, 77)
+    seqs[5] = b""                                            # an empty sequence in the middle
+    off = np.zeros(len(seqs) + 1, dtype=np.int64)
+    off[1:] = np.cumsum([len(s) for s in seqs])
+    blob = b"".join(seqs)
+    ref = gdist.KmerSets.from_sequences(seqs, 15, gdist.KmerType.DNA, 0, ctx)
+    eI, eD = ref.matrix(method=gdist.METHOD_SORTED)
+    for b in (blob, bytearray(blob), np.frombuffer(blob, dtype=np.uint8)):
+        s = gdist.KmerSets.from_blob(b, off, 15, gdist.KmerType.DNA, 0, ctx)
+        assert np.array_equal(s.sizes(), ref.sizes())
+        I, D = s.matrix(method=gdist.METHOD_SORTED)
+        assert np.array_equal(I, eI) and bits_equal(D, eD)
