@@ -933,20 +933,98 @@ __device__ __forceinline__ void sparse_walk6_range(const int4* __restrict__ rec,
     }
 }
 
+// v6 with CONSECUTIVE slots per lane (option sparse_shape = 112): lane l of a
+// group takes slots fb + SUN l ... fb + SUN l + SUN - 1 of the batch. One
+// search and one quotient give the first; each next slot is one column pair
+// further (a new row after ncp pairs, the next word with slots after nr
+// rows: a short divergent step that reads that word's record), so SUN slots
+// cost one search + one quotient instead of SUN of each. The search spans
+// the words ending inside the group's 64 SUN slots (a uniform readlane loop).
+// Records carry nr in the low 8 mantissa bits of 1 / ncp (as RW > 1).
+template <int SUN>
+__device__ __forceinline__ void sparse_walk6c_range(const int4* __restrict__ rec, int incl, int total, int lane,
+                                                    const SparseWalk& e, uint32_t zc, uint32_t* __restrict__ cnt,
+                                                    int fb0, int fb1) {
+    const char* beA = reinterpret_cast<const char*>(e.eA);
+    const char* beB = reinterpret_cast<const char*>(e.eB);
+    for (int fb = fb0; fb < fb1; fb += 64 * SUN) {
+        const int f0 = fb + SUN * lane;
+        const int w0 = __builtin_amdgcn_readfirstlane(__popcll(__ballot(incl <= fb)));
+        const int w1 = __builtin_amdgcn_readfirstlane(__popcll(__ballot(incl <= fb + 64 * SUN - 1)));
+        int lo = w0;
+        for (int l = w0; l < w1; l++) lo += __builtin_amdgcn_readlane(incl, l) <= f0;
+        lo = lo < 63 ? lo : 63;
+        int4 r = rec[lo];
+        int ncl = (int)((uint32_t)r.x >> 24), ncp = (ncl + 1) >> 1, nr = r.w & 0xFF;
+        int xr, yc;
+        {
+            const int q = f0 - (r.x & 0xFFFFFF);
+            const int x = (int)((float)q * __int_as_float(r.w));
+            const int t = (int)__umul24(x, ncp);
+            const int adj = (int)(t + ncp <= q) - (int)(t > q);
+            xr = x + adj;
+            yc = q - (int)__umul24(xr, ncp);
+        }
+        uint32_t ri[SUN], ci[SUN];
+        bool two[SUN];
+#pragma unroll
+        for (int u = 0; u < SUN; u++) {
+            const bool ok = f0 + u < total;
+            ri[u] = ok ? (uint32_t)(r.y + xr) : 0u;
+            ci[u] = ok ? (uint32_t)(r.z + 2 * yc) : zc;
+            two[u] = 2 * yc + 1 < ncl;
+            if (u + 1 < SUN) {                         // one slot further
+                yc++;
+                const bool wrap = yc == ncp;
+                yc = wrap ? 0 : yc;
+                xr += wrap ? 1 : 0;
+                if (xr >= nr && ok) {                  // past the word: the next word with slots
+                    do {
+                        lo++;
+                        r = rec[lo < 63 ? lo : 63];
+                        ncl = (int)((uint32_t)r.x >> 24);
+                        ncp = (ncl + 1) >> 1;
+                        nr = r.w & 0xFF;
+                    } while (lo < 63 && nr * ncp == 0);
+                    xr = 0;
+                    yc = 0;
+                }
+            }
+        }
+        ulonglong2 a[SUN], b0[SUN], b1[SUN];
+#pragma unroll
+        for (int u = 0; u < SUN; u++) {
+            a[u] = *reinterpret_cast<const ulonglong2*>(beA + (ri[u] << 4));
+            const char* pb = beB + (ci[u] << 4);
+            b0[u] = *reinterpret_cast<const ulonglong2*>(pb);
+            b1[u] = *reinterpret_cast<const ulonglong2*>(pb + 16);
+        }
+#pragma unroll
+        for (int u = 0; u < SUN; u++) {
+            const uint32_t rc = (uint32_t)a[u].y;
+            const uint32_t v0 = (uint32_t)__popcll(a[u].x & b0[u].x);
+            const uint32_t v1 = two[u] ? (uint32_t)__popcll(a[u].x & b1[u].x) : 0u;
+            cnt_add(cnt, rc, (uint32_t)(b0[u].y >> 32), v0);
+            cnt_add(cnt, rc, (uint32_t)(b1[u].y >> 32), v1);
+        }
+    }
+}
+
 // SUN slots per lane while whole groups of 64 SUN slots remain, then one
 // 64-slot group at a time: a batch's last iteration no longer walks up to
 // 64 (SUN - 1) idle slots (~7 % of C2's slots at SUN = 3)
-template <int SUN, int RW, int CW>
+template <int SUN, int RW, int CW, bool CONSEC = false>
 __device__ __forceinline__ void sparse_walk6(const int4* __restrict__ rec, int incl, int total, int lane,
                                              const SparseWalk& e, uint32_t zc, uint32_t* __restrict__ cnt) {
     const int full = total / (64 * SUN) * (64 * SUN);
-    sparse_walk6_range<SUN, RW, CW>(rec, incl, total, lane, e, zc, cnt, 0, full);
+    if (CONSEC) sparse_walk6c_range<SUN>(rec, incl, total, lane, e, zc, cnt, 0, full);
+    else sparse_walk6_range<SUN, RW, CW>(rec, incl, total, lane, e, zc, cnt, 0, full);
     if (SUN > 1) sparse_walk6_range<1, RW, CW>(rec, incl, total, lane, e, zc, cnt, full, total);
 }
 
 // RW = CW = 0: v5 (one product per slot); otherwise v6 with RW x CW
 // micro-tiles on the off-diagonal tiles (diagonal tiles walk v5's pairs)
-template <int SUN, int OCC, int RW = 0, int CW = 0>
+template <int SUN, int OCC, int RW = 0, int CW = 0, bool CONSEC = false>
 __global__ __launch_bounds__(SNT, OCC) void sparse_tile_kernel5(
     const int64_t* __restrict__ off, const uint8_t* __restrict__ set, const ulonglong2* __restrict__ ent,
     const int32_t* __restrict__ nc, int64_t Us, int64_t Ws, const int2* __restrict__ tiles, const int32_t* __restrict__ cbnd, int nchunks,
@@ -1025,11 +1103,11 @@ __global__ __launch_bounds__(SNT, OCC) void sparse_tile_kernel5(
         // pre < 2^24 (64 words x 128 x 128 products), ncol <= 128
         const int rcp = __float_as_int(ncd ? __builtin_amdgcn_rcpf((float)ncd) : 0.0f);
         rec[wv][lane] = make_int4((incl - P) | (ncl << 24), (int32_t)(rb - ra0), (int32_t)(cb - cb0),
-                                  RW > 1 && !diag ? (rcp & ~0xFF) | nr : rcp);
+                                  (RW > 1 || CONSEC) && !diag ? (rcp & ~0xFF) | nr : rcp);
         const int total = __builtin_amdgcn_readlane(incl, 63);      // uniform: the walk's loop stays scalar
         __builtin_amdgcn_wave_barrier();
         if (diag) sparse_walk5<SUN, true>(rec[wv], incl, total, lane, e, zA, cnt, mirror);
-        else if (CW) sparse_walk6<SUN, RW ? RW : 1, CW ? CW : 1>(rec[wv], incl, total, lane, e, zB, cnt);
+        else if (CW) sparse_walk6<SUN, RW ? RW : 1, CW ? CW : 1, CONSEC>(rec[wv], incl, total, lane, e, zB, cnt);
         else sparse_walk5<SUN, false>(rec[wv], incl, total, lane, e, zB, cnt, false);
         __builtin_amdgcn_wave_barrier();
     }
@@ -1708,12 +1786,16 @@ bool sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
             upper ? 1 : 0, d_I, ldI, sc.use_part ? sc.part.as<int32_t>() : nullptr, fold, s->Wd, s->nsets);
     else if (version == 5 || version == 6) {
         const int shape = (int)ctx->option(OPT_SPARSE_SHAPE, 12);
-        GD_REQUIRE(version == 5 || shape == 12 || shape == 14 || shape == 22, "sparse_shape: 12, 14 or 22");
+        GD_REQUIRE(version == 5 || shape == 12 || shape == 14 || shape == 22 || shape == 112,
+                   "sparse_shape: 12, 14, 22 or 112");
         GD_REQUIRE(version == 6 ? sun >= 2 && sun <= (shape == 12 ? 4 : 3) : sun == 4 || sun == 6,
                    "sparse_sun out of range for the kernel");
         auto k5 = version == 5 ? (sun == 4 ? sparse_tile_kernel5<4, 8> : sparse_tile_kernel5<6, 8>)
                   : shape == 14 ? (sun == 2 ? sparse_tile_kernel5<2, 8, 1, 4> : sparse_tile_kernel5<3, 8, 1, 4>)
                   : shape == 22 ? (sun == 2 ? sparse_tile_kernel5<2, 8, 2, 2> : sparse_tile_kernel5<3, 8, 2, 2>)
+                  : shape == 112 ? (sun == 2 ? sparse_tile_kernel5<2, 8, 1, 2, true>
+                                   : sun == 4 ? sparse_tile_kernel5<4, 8, 1, 2, true>
+                                              : sparse_tile_kernel5<3, 8, 1, 2, true>)
                   : sun == 2    ? sparse_tile_kernel5<2, 8, 1, 2>
                   : sun == 4    ? sparse_tile_kernel5<4, 8, 1, 2>
                                 : sparse_tile_kernel5<3, 8, 1, 2>;

@@ -581,7 +581,8 @@ def test_rare_tier_thresholds_exact(ctx, T, kernel, dedup, opts):
                                   "kernel_v5_atomic", "kernel_v6_rows", "kernel_v6_sun4", "kernel_v6_quads",
                                   "kernel_v6_2x2", "kernel_v6_2x2_rows", "kernel_v6_atomic", "absorb",
                                   "mixed_slabs", "mixed_slabs_atomic", "mixed_tiles", "unfused", "rare_kernel",
-                                  "unfused_rare_kernel", "fill_sort"])
+                                  "unfused_rare_kernel", "fill_sort", "kernel_v6_consec", "kernel_v6_consec_rows",
+                                  "kernel_v6_consec_sun4"])
 def test_sparse_complement_words_exact(ctx, mode, opts):
     """The dense tier in locus order with complement-sparse words: counts and
     distances are bit-exact against the oracle over upper triangles,
@@ -609,6 +610,10 @@ def test_sparse_complement_words_exact(ctx, mode, opts):
                 "kernel_v6_2x2": {"sparse_zmax": 100000, "sparse_shape": 22},
                 "kernel_v6_2x2_rows": {"sparse_zmax": 40, "sparse_shape": 22, "sparse_sun": 2},
                 "kernel_v6_atomic": {"sparse_zmax": 100000, "sparse_part_budget": 0, "sparse_chunks": 3},
+                # consecutive slots per lane (one search + quotient per lane and group)
+                "kernel_v6_consec": {"sparse_zmax": 100000, "sparse_shape": 112},
+                "kernel_v6_consec_rows": {"sparse_zmax": 40, "sparse_shape": 112, "sparse_sun": 2},
+                "kernel_v6_consec_sun4": {"sparse_zmax": 100000, "sparse_shape": 112, "sparse_sun": 4},
                 # the dense words absorbed into the sparse tier (no dense-word launch)
                 "absorb": {"sparse_zmax": 12, "sparse_absorb": 1},
                 # the dense words counted inside the tile kernel, 8 per chunk (partials / atomic flush),
@@ -640,7 +645,7 @@ def test_sparse_complement_words_exact(ctx, mode, opts):
     ws, wd, ent = sets.sparse_info()
     if mode in ("all_sparse", "atomic_flush", "kernel_v1", "kernel_v2", "many_chunks", "kernel_v4", "kernel_v5",
                 "kernel_v5_sun6", "kernel_v5_atomic", "kernel_v6_sun4", "kernel_v6_quads", "kernel_v6_2x2",
-                "kernel_v6_atomic", "absorb"):
+                "kernel_v6_atomic", "absorb", "kernel_v6_consec", "kernel_v6_consec_sun4"):
         assert ws > 0 and wd == 0 and ent > 0
     elif mode in ("mixed", "mixed_fold", "mixed_fold_1chunk", "mixed_slabs", "mixed_slabs_atomic", "mixed_tiles"):
         assert ws > 0 and wd > 0
