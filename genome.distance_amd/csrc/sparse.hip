@@ -1788,7 +1788,7 @@ bool sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
         const int shape = (int)ctx->option(OPT_SPARSE_SHAPE, 12);
         GD_REQUIRE(version == 5 || shape == 12 || shape == 14 || shape == 22 || shape == 112,
                    "sparse_shape: 12, 14, 22 or 112");
-        GD_REQUIRE(version == 6 ? sun >= 2 && sun <= (shape == 12 ? 4 : 3) : sun == 4 || sun == 6,
+        GD_REQUIRE(version == 6 ? sun >= 2 && sun <= (shape == 12 || shape == 112 ? 4 : 3) : sun == 4 || sun == 6,
                    "sparse_sun out of range for the kernel");
         auto k5 = version == 5 ? (sun == 4 ? sparse_tile_kernel5<4, 8> : sparse_tile_kernel5<6, 8>)
                   : shape == 14 ? (sun == 2 ? sparse_tile_kernel5<2, 8, 1, 4> : sparse_tile_kernel5<3, 8, 1, 4>)
