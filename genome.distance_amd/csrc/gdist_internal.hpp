@@ -205,6 +205,7 @@ enum Opt : int {
     OPT_SPARSE_FOLD,        // at most this many (padded) dense words counted inside the v5 / v6 tile kernel
                             // (8 per chunk; default 64, 0: the dense-word tile launch)
     OPT_FILL_SORT,          // 1: bitset fill by a (code, set) sort + run ranks (default 0: windowed searches)
+    OPT_SPARSE_TILE_ORDER,  // 1: sparse tiles heaviest first (default 0: row-major order; C2 neutral)
     OPT_COUNT
 };
 extern const char* const kOptNames[OPT_COUNT];

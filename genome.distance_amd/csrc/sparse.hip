@@ -1623,6 +1623,23 @@ void sparse_plan(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, in
                 if (upper && cmax <= rmin) continue;
                 tiles.push_back(make_int2((int)A, (int)B));
             }
+        // Heaviest tiles first (workgroups are dispatched in blockIdx order,
+        // tile-major): whole off-diagonal tiles, then row-partial ones, then
+        // the diagonal tiles (pairs x < y of one list, ~0.45 of a tile), so
+        // the last dispatch round is made of the light ones (option
+        // sparse_tile_order = 1; measured neutral on C2, 0.126 vs 0.124 ms,
+        // so row-major order stays the default)
+        if (ctx->option(OPT_SPARSE_TILE_ORDER, 0) != 0) {
+            auto weight = [&](const int2& t) {
+                const int64_t A = t.x, B = t.y;
+                const double rows = (double)(std::min(r1, (A + 1) * SB) - std::max(r0, A * SB));
+                const double cols = (double)(std::min(c1, (B + 1) * SB) - std::max(c0, B * SB));
+                const bool diag = A == B && rows == (double)std::min<int64_t>(SB, s->nsets - A * SB);
+                return rows * cols * (diag ? 0.45 : 1.0);
+            };
+            std::stable_sort(tiles.begin(), tiles.end(),
+                             [&](const int2& a, const int2& b) { return weight(a) > weight(b); });
+        }
         sc.ntiles = (int64_t)tiles.size();
         // enough workgroups to fill the chip, each over >= 512 sparse words
         const int64_t target = (int64_t)ctx->cus * std::max<int64_t>(1, ctx->option(OPT_SPARSE_WG_PER_CU, 4));
