@@ -876,7 +876,7 @@ __device__ __forceinline__ void sparse_walk5(const int4* __restrict__ rec, int i
 // read the next records (or the zero sentinels past the last one) and add 0.
 // Record: {pre | ncol << 24, row start, column start, 1 / ncp with nr in the
 // low 8 mantissa bits} (the quotient tolerates the 2^-15 error, q < 2^14).
-template <int SUN, int RW, int CW>
+template <int SUN, int RW, int CW, bool EXQ>
 __device__ __forceinline__ void sparse_walk6_range(const int4* __restrict__ rec, int incl, int total, int lane,
                                                    const SparseWalk& e, uint32_t zc, uint32_t* __restrict__ cnt,
                                                    int fb0, int fb1) {
@@ -898,10 +898,19 @@ __device__ __forceinline__ void sparse_walk6_range(const int4* __restrict__ rec,
             const int q = f[u] - (r[u].x & 0xFFFFFF);
             const int ncl = (int)((uint32_t)r[u].x >> 24);
             const int ncp = (ncl + CW - 1) / CW;
-            const int x = (int)((float)q * __int_as_float(r[u].w));
-            const int t = (int)__umul24(x, ncp);
-            const int adj = (int)(t + ncp <= q) - (int)(t > q);
-            const int xc = x + adj;
+            int xc;
+            if (EXQ) {
+                // exact without a correction: rec.w = 1 / (2 ncp), and
+                // (2q + 1) / (2 ncp) = q / ncp + (q mod ncp + 1/2) / ncp stays
+                // >= 1/(2 ncp) >= 1/128 from an integer, while the float error
+                // is <= (q + 1/2) / ncp * 2^-22 < 0.002 (q < 128 x 64)
+                xc = (int)((float)(2 * q + 1) * __int_as_float(r[u].w));
+            } else {
+                const int x = (int)((float)q * __int_as_float(r[u].w));
+                const int t = (int)__umul24(x, ncp);
+                const int adj = (int)(t + ncp <= q) - (int)(t > q);
+                xc = x + adj;
+            }
             const int yc = (q - (int)__umul24(xc, ncp)) * CW;
             ncol[u] = ncl - yc;
             nrow[u] = RW > 1 ? (r[u].w & 0xFF) - xc * RW : 1;
@@ -1016,10 +1025,12 @@ __device__ __forceinline__ void sparse_walk6c_range(const int4* __restrict__ rec
 template <int SUN, int RW, int CW, bool CONSEC = false>
 __device__ __forceinline__ void sparse_walk6(const int4* __restrict__ rec, int incl, int total, int lane,
                                              const SparseWalk& e, uint32_t zc, uint32_t* __restrict__ cnt) {
+    // EXQ: the correction-free quotient, records holding 1 / (2 ncp) (one row per slot, not CONSEC)
+    constexpr bool EXQ = RW == 1 && !CONSEC;
     const int full = total / (64 * SUN) * (64 * SUN);
     if (CONSEC) sparse_walk6c_range<SUN>(rec, incl, total, lane, e, zc, cnt, 0, full);
-    else sparse_walk6_range<SUN, RW, CW>(rec, incl, total, lane, e, zc, cnt, 0, full);
-    if (SUN > 1) sparse_walk6_range<1, RW, CW>(rec, incl, total, lane, e, zc, cnt, full, total);
+    else sparse_walk6_range<SUN, RW, CW, EXQ>(rec, incl, total, lane, e, zc, cnt, 0, full);
+    if (SUN > 1) sparse_walk6_range<1, RW, CW, EXQ>(rec, incl, total, lane, e, zc, cnt, full, total);
 }
 
 // RW = CW = 0: v5 (one product per slot); otherwise v6 with RW x CW
@@ -1101,7 +1112,9 @@ __global__ __launch_bounds__(SNT, OCC) void sparse_tile_kernel5(
             if (lane >= o) incl += v;
         }
         // pre < 2^24 (64 words x 128 x 128 products), ncol <= 128
-        const int rcp = __float_as_int(ncd ? __builtin_amdgcn_rcpf((float)ncd) : 0.0f);
+        // 1 / ncd; v6 with one row per slot: 1 / (2 ncd) for the correction-free quotient
+        const float rden = CW && RW <= 1 && !CONSEC && !diag ? 2.0f * (float)ncd : (float)ncd;
+        const int rcp = __float_as_int(ncd ? __builtin_amdgcn_rcpf(rden) : 0.0f);
         rec[wv][lane] = make_int4((incl - P) | (ncl << 24), (int32_t)(rb - ra0), (int32_t)(cb - cb0),
                                   (RW > 1 || CONSEC) && !diag ? (rcp & ~0xFF) | nr : rcp);
         const int total = __builtin_amdgcn_readlane(incl, 63);      // uniform: the walk's loop stays scalar
