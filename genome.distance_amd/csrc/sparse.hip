@@ -203,14 +203,24 @@ __device__ __forceinline__ void cnt_add(uint32_t* cnt, uint32_t r, uint32_t c, u
     atomicAdd(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(cnt) + (r ^ (c >> 16))), v << (c & 31));
 }
 
-// 16-byte records of the entries (E16 / v5 / v6 tile kernels): {complement
-// word, row_code(set) | col_code(set) << 32}
+// 16-byte records of the entries (E16 / v5 / v6 tile kernels), as four
+// dwords {row_code(set), word lo, word hi, col_code(set)}: a row needs the
+// first 12 bytes, a column the last 12, so v6 loads 12 per entry
+// (global_load_dwordx3) instead of 16
+struct Rec3 {
+    uint32_t a, b, c;
+};
+__device__ __forceinline__ unsigned long long rec_word(const ulonglong2& r) { return (r.x >> 32) | (r.y << 32); }
+__device__ __forceinline__ uint32_t rec_row(const ulonglong2& r) { return (uint32_t)r.x; }
+__device__ __forceinline__ uint32_t rec_col(const ulonglong2& r) { return (uint32_t)(r.y >> 32); }
 __global__ void sparse_records_kernel(const unsigned long long* __restrict__ word, const uint8_t* __restrict__ set,
                                       int64_t n, ulonglong2* __restrict__ ent) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
         const int st = set[e];
-        ent[e] = make_ulonglong2(word[e], (unsigned long long)row_code(st) | ((unsigned long long)col_code(st) << 32));
+        const unsigned long long w = word[e];
+        ent[e] = make_ulonglong2((unsigned long long)row_code(st) | (w << 32),
+                                 (w >> 32) | ((unsigned long long)col_code(st) << 32));
     }
 }
 
@@ -373,9 +383,9 @@ __global__ __launch_bounds__(SNT, OCC) void sparse_tile_kernel(
             for (int u = 0; u < SUN; u++) {
                 if (E16) {
                     const ulonglong2 er = eA[(uint32_t)ri[u]], ec = (diag ? eA : eB)[(uint32_t)ci[u]];
-                    wr[u] = er.x; wc[u] = ec.x;
-                    sr[u] = (int)((uint32_t)er.y >> 8);                               // row code -> set
-                    const uint32_t cc = (uint32_t)(ec.y >> 32);                        // column code -> set
+                    wr[u] = rec_word(er); wc[u] = rec_word(ec);
+                    sr[u] = (int)(rec_row(er) >> 8);                                  // row code -> set
+                    const uint32_t cc = rec_col(ec);                                   // column code -> set
                     sc[u] = (int)(((cc >> 18) << 1) | ((cc >> 4) & 1));
                 } else {
                     wr[u] = wA[(uint32_t)ri[u]]; wc[u] = (diag ? wA : wB)[(uint32_t)ci[u]];
@@ -852,9 +862,9 @@ __device__ __forceinline__ void sparse_walk5_range(const int4* __restrict__ rec,
         }
 #pragma unroll
         for (int u = 0; u < SUN; u++) {
-            const uint32_t v = (uint32_t)__popcll(a[u].x & b[u].x);
-            cnt_add(cnt, (uint32_t)a[u].y, (uint32_t)(b[u].y >> 32), v);
-            if (DIAG && mirror) cnt_add(cnt, (uint32_t)b[u].y, (uint32_t)(a[u].y >> 32), v);
+            const uint32_t v = (uint32_t)__popcll(rec_word(a[u]) & rec_word(b[u]));
+            cnt_add(cnt, rec_row(a[u]), rec_col(b[u]), v);
+            if (DIAG && mirror) cnt_add(cnt, rec_row(b[u]), rec_col(a[u]), v);
         }
     }
 }
@@ -917,26 +927,26 @@ __device__ __forceinline__ void sparse_walk6_range(const int4* __restrict__ rec,
             ri[u] = ok ? (uint32_t)(r[u].y + xc * RW) : 0u;
             ci[u] = ok ? (uint32_t)(r[u].z + yc) : zc;
         }
-        ulonglong2 a[SUN][RW], b[SUN][CW];
+        Rec3 a[SUN][RW], b[SUN][CW];          // rows {row code, word}, columns {word, column code}
 #pragma unroll
         for (int u = 0; u < SUN; u++) {
             const char* pa = beA + (ri[u] << 4);
-            const char* pb = beB + (ci[u] << 4);
+            const char* pb = beB + (ci[u] << 4) + 4;
 #pragma unroll
-            for (int i = 0; i < RW; i++) a[u][i] = *reinterpret_cast<const ulonglong2*>(pa + 16 * i);
+            for (int i = 0; i < RW; i++) a[u][i] = *reinterpret_cast<const Rec3*>(pa + 16 * i);
 #pragma unroll
-            for (int j = 0; j < CW; j++) b[u][j] = *reinterpret_cast<const ulonglong2*>(pb + 16 * j);
+            for (int j = 0; j < CW; j++) b[u][j] = *reinterpret_cast<const Rec3*>(pb + 16 * j);
         }
 #pragma unroll
         for (int u = 0; u < SUN; u++)
 #pragma unroll
             for (int i = 0; i < RW; i++) {
-                const uint32_t rc = (uint32_t)a[u][i].y;
+                const uint32_t rc = a[u][i].a;
 #pragma unroll
                 for (int j = 0; j < CW; j++) {
                     const bool in = (i == 0 || i < nrow[u]) && (j == 0 || j < ncol[u]);
-                    const uint32_t v = in ? (uint32_t)__popcll(a[u][i].x & b[u][j].x) : 0u;
-                    cnt_add(cnt, rc, (uint32_t)(b[u][j].y >> 32), v);
+                    const uint32_t v = in ? (uint32_t)(__popc(a[u][i].b & b[u][j].a) + __popc(a[u][i].c & b[u][j].b)) : 0u;
+                    cnt_add(cnt, rc, b[u][j].c, v);
                 }
             }
     }
@@ -1000,21 +1010,21 @@ __device__ __forceinline__ void sparse_walk6c_range(const int4* __restrict__ rec
                 }
             }
         }
-        ulonglong2 a[SUN], b0[SUN], b1[SUN];
+        Rec3 a[SUN], b0[SUN], b1[SUN];
 #pragma unroll
         for (int u = 0; u < SUN; u++) {
-            a[u] = *reinterpret_cast<const ulonglong2*>(beA + (ri[u] << 4));
-            const char* pb = beB + (ci[u] << 4);
-            b0[u] = *reinterpret_cast<const ulonglong2*>(pb);
-            b1[u] = *reinterpret_cast<const ulonglong2*>(pb + 16);
+            a[u] = *reinterpret_cast<const Rec3*>(beA + (ri[u] << 4));
+            const char* pb = beB + (ci[u] << 4) + 4;
+            b0[u] = *reinterpret_cast<const Rec3*>(pb);
+            b1[u] = *reinterpret_cast<const Rec3*>(pb + 16);
         }
 #pragma unroll
         for (int u = 0; u < SUN; u++) {
-            const uint32_t rc = (uint32_t)a[u].y;
-            const uint32_t v0 = (uint32_t)__popcll(a[u].x & b0[u].x);
-            const uint32_t v1 = two[u] ? (uint32_t)__popcll(a[u].x & b1[u].x) : 0u;
-            cnt_add(cnt, rc, (uint32_t)(b0[u].y >> 32), v0);
-            cnt_add(cnt, rc, (uint32_t)(b1[u].y >> 32), v1);
+            const uint32_t rc = a[u].a;
+            const uint32_t v0 = (uint32_t)(__popc(a[u].b & b0[u].a) + __popc(a[u].c & b0[u].b));
+            const uint32_t v1 = two[u] ? (uint32_t)(__popc(a[u].b & b1[u].a) + __popc(a[u].c & b1[u].b)) : 0u;
+            cnt_add(cnt, rc, b0[u].c, v0);
+            cnt_add(cnt, rc, b1[u].c, v1);
         }
     }
 }
