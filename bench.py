@@ -298,7 +298,7 @@ def main():
         kname = {"bitset": "bitset_tile_kernel2<1> (+ rare_pairs_kernel)", "sorted": "sorted_join_kernel",
                  "sketch": "sketch_tile_kernel<16,24,LDS,K=2>"}[method]
         if sparse:
-            kname = "sparse_tile_kernel5<3, 8, 1, 2> (v6: 1x2 micro-tiles, the dense words folded in)"
+            kname = "sparse_tile_kernel5<3, 8, 1, 2, false> (v6: 1x2 micro-tiles, the dense words folded in)"
         if traffic is not None and not pmc.get("kernel", "").startswith(kname.split(" (")[0]):
             traffic = None                    # the PMC summary was taken on another kernel
         valu_peak = VALU_WORDPAIR_PEAK * 4 / 1e12
