@@ -1058,8 +1058,273 @@ __global__ __launch_bounds__(256) void fill_search_kernel(
     }
 }
 
-// bits of sets [0, nsets) against the dense dictionary (windowed searches,
-// or, option fill_sort, the chunked pairs sort + run ranks + scatter);
+// The default fill, in two passes so that no bit is set by a global atomic
+// (a wave's 64 atomicOr land in 64 different rows' cache lines, the slow
+// case of the L2 atomic unit: the one-pass fill above spends 0.27 s of C2's
+// setup on them).
+// Pass 1 (fill_window_kernel + fill_pos_kernel): segments of up to kPosSeg
+// consecutive codes of one set (shorter for sets much smaller than the
+// dictionary, so that a segment's window fits in LDS). One thread per
+// (segment, bound) finds the segment's windows [dlo, dhi) in the dense codes
+// and [rlo, rhi) in the rare codes and writes them beside the segment's
+// bounds - independent searches, instead of a dependent chain inside the
+// wave that uses them. A wave (one per block) then stages its dense window in
+// LDS with coalesced loads (codes and their bit positions perm[]), loads its
+// codes up front, and each lane binary-searches its codes in LDS. Misses
+// (about 1 code in 100 on C2) are listed in LDS and looked up together after
+// the dense pass: a search over LDS fences (every 8th rare code of the
+// window) and one 64-byte load of the 8-code bucket, so a segment waits on
+// one global latency for its rare codes, not one per round. Each code's bit
+// position (u32; ~0 outside the dense tier) goes to a position array
+// parallel to the codes; rare-tier codes append their records (one atomic
+// per wave and round). A window over the LDS caps (a set sparse against the
+// dictionary) falls back to a wave walk over global memory.
+// (The one-pass fill's per-lane binary searches in global memory chain ~20
+// dependent loads per code: it is latency-bound at 0.27 s for C2.)
+// Pass 2 (pos_bits_kernel): a workgroup owns one set's row slice of
+// kPosSlice 32-bit words in LDS, streams the set's positions, ORs the ones in
+// its slice into LDS (ds_or) and stores the slice whole: every row word is
+// written once, coalesced, and the row needs no memset.
+constexpr int kPosSeg = 512;       // codes per segment (at most)
+constexpr int kWinDense = 768;     // LDS dense-window cap (entries)
+constexpr int kRareBucket = 8;     // rare codes per LDS fence
+constexpr int kRareFences = 256;   // LDS fence cap (a rare window of up to 2048 codes)
+constexpr int kPosSlice = 32768;   // 32-bit row words per workgroup (128 KiB of LDS)
+constexpr int64_t kFillPosChunk = int64_t(1) << 30;   // codes per position-array chunk (4 GiB)
+
+__device__ __forceinline__ int64_t upper_bound_u64(const uint64_t* __restrict__ a, int64_t lo, int64_t hi, uint64_t k) {
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (a[mid] <= k) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+// per segment 8 int64: dlo, dhi, rlo, rhi, (set << 40 | b), e
+__global__ __launch_bounds__(256) void fill_window_kernel(const uint64_t* __restrict__ codes,
+                                                          const int64_t* __restrict__ off, const int64_t* __restrict__ seg,
+                                                          int64_t ns, const uint64_t* __restrict__ dict, int64_t U,
+                                                          const uint64_t* __restrict__ rare, int64_t Ur,
+                                                          int64_t* __restrict__ win) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ns * 4) return;
+    const int64_t sg = t >> 2;
+    const uint64_t sd = (uint64_t)seg[sg];
+    const int64_t set = (int64_t)(sd >> 40), b = (int64_t)(sd & ((1ull << 40) - 1));
+    int64_t e = off[set + 1];   // the next segment's start within the set
+    if (sg + 1 < ns) {
+        const uint64_t nx = (uint64_t)seg[sg + 1];
+        if ((int64_t)(nx >> 40) == set) e = (int64_t)(nx & ((1ull << 40) - 1));
+    }
+    const int which = (int)(t & 3);
+    const uint64_t* a = which < 2 ? dict : rare;
+    const int64_t n = which < 2 ? U : Ur;
+    win[sg * 8 + which] = (which & 1) ? upper_bound_u64(a, 0, n, codes[e - 1]) : lower_bound_u64(a, 0, n, codes[b]);
+    if (which == 0) {
+        win[sg * 8 + 4] = (int64_t)sd;
+        win[sg * 8 + 5] = e;
+    }
+}
+
+// Ranks of the active lanes' codes k (sorted across lanes) in a[P, hi) of
+// global memory (the fallback walk): rk = lower bound, hit = a[rk] == k. P is
+// uniform and only moves forward; on return it is the largest active rank.
+__device__ __forceinline__ void wave_rank(const uint64_t* __restrict__ a, int64_t& P, int64_t hi, uint64_t k,
+                                          bool active, int64_t& rk, bool& hit) {
+    const int lane = threadIdx.x & 63;
+    bool pend = active;
+    rk = hi;
+    hit = false;
+    for (int round = 0; __ballot(pend); round++) {
+        const int nb = (int)std::min<int64_t>(64, hi - P);
+        if (nb <= 0) break;   // pending lanes: past the end (rk = hi, no hit)
+        const uint64_t B = lane < nb ? a[P + lane] : ~0ull;
+        int c = 0;   // # block codes < k
+#pragma unroll
+        for (int st = 32; st >= 1; st >>= 1) {
+            const uint64_t v = (uint64_t)__shfl((long long)B, c + st - 1, 64);
+            if (c + st <= nb && v < k) c += st;
+        }
+        const uint64_t v = (uint64_t)__shfl((long long)B, c & 63, 64);
+        if (c < nb && v < k) c++;
+        const uint64_t m = (uint64_t)__shfl((long long)B, c & 63, 64);
+        if (pend && (c < nb || P + nb >= hi)) {
+            rk = P + c;
+            hit = c < nb && m == k;
+            pend = false;
+        }
+        const unsigned long long left = __ballot(pend);
+        if (!left) break;
+        const uint64_t kmin = (uint64_t)__shfl((long long)k, __ffsll((long long)left) - 1, 64);
+        P += nb;
+        if (round >= 1) P = lower_bound_u64(a, P, hi, kmin);   // uniform: a gap, search it
+    }
+    const unsigned long long act = __ballot(active);
+    if (act) P = __shfl((long long)rk, 63 - __clzll((long long)act), 64);
+}
+
+// lower bound of k in LDS a[0, n)
+__device__ __forceinline__ int lds_lower_bound(const uint64_t* a, int n, uint64_t k) {
+    int lo = 0;
+    for (int len = n; len > 0;) {
+        const int half = len >> 1;
+        if (a[lo + half] < k) { lo += half + 1; len -= half + 1; } else len = half;
+    }
+    return lo;
+}
+
+// rare-tier records of the lanes with rhit: one atomic per wave
+__device__ __forceinline__ void append_rare(bool rhit, int64_t q, int64_t set, int64_t id_base,
+                                            unsigned long long* __restrict__ rare_out,
+                                            unsigned long long* __restrict__ rare_cnt, int64_t rare_cap) {
+    const unsigned long long m = __ballot(rhit);
+    if (!m) return;
+    const int lane = threadIdx.x & 63;
+    unsigned long long b0 = 0;
+    if (lane == __ffsll((long long)m) - 1) b0 = atomicAdd(rare_cnt, (unsigned long long)__popcll(m));
+    b0 = (unsigned long long)__shfl((long long)b0, __ffsll((long long)m) - 1, 64);
+    if (rhit) {
+        const unsigned long long slot = b0 + __popcll(m & ((1ull << lane) - 1));
+        if ((int64_t)slot < rare_cap)
+            rare_out[slot] = ((unsigned long long)q << 32) | (unsigned long long)(uint32_t)(set + id_base);
+    }
+}
+
+// one wave per block and segment
+__global__ __launch_bounds__(64) void fill_pos_kernel(
+    const uint64_t* __restrict__ codes, const int64_t* __restrict__ win, const uint64_t* __restrict__ dict,
+    const uint64_t* __restrict__ rare, int64_t base, uint32_t* __restrict__ pos_out, int64_t id_base,
+    unsigned long long* __restrict__ rare_out, unsigned long long* __restrict__ rare_cnt, int64_t rare_cap,
+    const uint32_t* __restrict__ perm) {
+    __shared__ uint64_t s_d[kWinDense];
+    __shared__ uint32_t s_p[kWinDense];
+    __shared__ uint64_t s_f[kRareFences];
+    __shared__ uint64_t s_mk[kPosSeg];
+    const int lane = threadIdx.x;
+    const int64_t sg = blockIdx.x;
+    const int64_t wv = lane < 6 ? win[sg * 8 + lane] : 0;
+    int64_t dlo = __shfl((long long)wv, 0, 64), dhi = __shfl((long long)wv, 1, 64);
+    int64_t rlo = __shfl((long long)wv, 2, 64), rhi = __shfl((long long)wv, 3, 64);
+    const uint64_t sd = (uint64_t)__shfl((long long)wv, 4, 64);
+    const int64_t e = __shfl((long long)wv, 5, 64);
+    const int64_t set = (int64_t)(sd >> 40), b = (int64_t)(sd & ((1ull << 40) - 1));
+    const int64_t nd = dhi - dlo, nr = rhi - rlo, nf = (nr + kRareBucket - 1) / kRareBucket;
+    if (nd <= kWinDense && nf <= kRareFences) {
+        uint64_t kk[kPosSeg / 64];
+#pragma unroll
+        for (int j = 0; j < kPosSeg / 64; j++) kk[j] = b + 64 * j + lane < e ? codes[b + 64 * j + lane] : 0;
+        for (int j = lane; j < nd; j += 64) {
+            s_d[j] = dict[dlo + j];
+            s_p[j] = perm ? perm[dlo + j] : (uint32_t)(dlo + j);
+        }
+        for (int j = lane; j < nf; j += 64) s_f[j] = rare[rlo + (int64_t)j * kRareBucket];
+        __syncthreads();
+        int nm = 0;   // misses listed (uniform)
+#pragma unroll
+        for (int j = 0; j < kPosSeg / 64; j++) {
+            if (b + 64 * j >= e) break;
+            const int64_t i = b + 64 * j + lane;
+            const bool valid = i < e;
+            bool miss = false;
+            if (valid) {
+                const uint64_t k = kk[j];
+                const int r = lds_lower_bound(s_d, (int)nd, k);
+                const bool hit = r < nd && s_d[r] == k;
+                pos_out[i - base] = hit ? s_p[r] : ~0u;
+                miss = !hit;
+            }
+            const unsigned long long m = __ballot(miss);
+            if (miss) s_mk[nm + __popcll(m & ((1ull << lane) - 1))] = kk[j];
+            nm += __popcll(m);
+        }
+        __syncthreads();
+        for (int t0 = 0; t0 < nm; t0 += 64) {
+            bool rhit = false;
+            int64_t q = 0;
+            if (t0 + lane < nm && nf > 0) {
+                const uint64_t k = s_mk[t0 + lane];
+                const int g = lds_lower_bound(s_f, (int)nf, k + 1) - 1;   // last fence <= k (k = ~0: the last fence)
+                if (g >= 0 || k == ~0ull) {
+                    const int gg = g >= 0 ? g : (int)nf - 1;
+                    const int64_t q0 = rlo + (int64_t)gg * kRareBucket;
+                    uint64_t v[kRareBucket];
+#pragma unroll
+                    for (int u = 0; u < kRareBucket; u++) v[u] = q0 + u < rhi ? rare[q0 + u] : 0;
+#pragma unroll
+                    for (int u = 0; u < kRareBucket; u++)
+                        if (q0 + u < rhi && v[u] == k) { rhit = true; q = q0 + u; }
+                }
+            }
+            append_rare(rhit, q, set, id_base, rare_out, rare_cnt, rare_cap);
+        }
+        return;
+    }
+    // fallback: walk the windows in global memory
+    for (int64_t i0 = b; i0 < e; i0 += 64) {
+        const int64_t i = i0 + lane;
+        const bool valid = i < e;
+        const uint64_t k = valid ? codes[i] : 0;
+        int64_t r;
+        bool hit;
+        wave_rank(dict, dlo, dhi, k, valid, r, hit);
+        if (valid) pos_out[i - base] = hit ? (perm ? perm[r] : (uint32_t)r) : ~0u;
+        const bool miss = valid && !hit;
+        if (__ballot(miss) && rlo < rhi) {
+            int64_t q;
+            bool rhit;
+            wave_rank(rare, rlo, rhi, k, miss, q, rhit);
+            append_rare(rhit, q, set, id_base, rare_out, rare_cnt, rare_cap);
+        }
+    }
+}
+
+__device__ __forceinline__ void pos_or(uint32_t* lds, uint32_t p, uint32_t sb) {
+    const uint32_t x = (p >> 5) - sb;   // ~0 positions and other slices wrap to >= kPosSlice
+    if (x < (uint32_t)kPosSlice) atomicOr(lds + x, 1u << (p & 31));
+}
+
+// grid (slices, sets of the chunk); block 1024
+__global__ __launch_bounds__(1024) void pos_bits_kernel(const uint32_t* __restrict__ pos, const int64_t* __restrict__ off,
+                                                        int64_t s0, int64_t base, int64_t W, uint32_t* __restrict__ bits) {
+    __shared__ uint32_t lds[kPosSlice];
+    const int64_t set = s0 + blockIdx.y;
+    const int64_t words = 2 * W;
+    const uint32_t sb = blockIdx.x * (uint32_t)kPosSlice;
+    const int n32 = (int)std::min<int64_t>(kPosSlice, words - sb);
+    for (int j = threadIdx.x; j < kPosSlice; j += 1024) lds[j] = 0;
+    __syncthreads();
+    int64_t ob = off[set] - base;
+    const int64_t oe = off[set + 1] - base;
+    // head up to a 16-byte boundary, then 4 x uint4 per thread per pass, then the tail
+    const int64_t ha = std::min<int64_t>(oe, (ob + 3) & ~int64_t(3));
+    if (ob + threadIdx.x < ha) pos_or(lds, pos[ob + threadIdx.x], sb);
+    ob = ha;
+    const int64_t nv = (oe - ob) >> 2;   // whole uint4 in [ob, oe)
+    const uint4* v = reinterpret_cast<const uint4*>(pos + ob);
+    int64_t j = threadIdx.x;
+    for (; j + 3 * 1024 < nv; j += 4 * 1024) {
+        uint4 a[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) a[u] = v[j + u * 1024];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            pos_or(lds, a[u].x, sb); pos_or(lds, a[u].y, sb); pos_or(lds, a[u].z, sb); pos_or(lds, a[u].w, sb);
+        }
+    }
+    for (; j < nv; j += 1024) {
+        const uint4 a = v[j];
+        pos_or(lds, a.x, sb); pos_or(lds, a.y, sb); pos_or(lds, a.z, sb); pos_or(lds, a.w, sb);
+    }
+    const int64_t t = ob + nv * 4 + threadIdx.x;
+    if (t < oe) pos_or(lds, pos[t], sb);
+    __syncthreads();
+    uint32_t* row = bits + set * words + sb;
+    for (int x = threadIdx.x; x < n32; x += 1024) row[x] = lds[x];
+}
+
+// bits of sets [0, nsets) against the dense dictionary (default: merged
+// positions + LDS slices; option fill_sort 1: the chunked pairs sort + run
+// ranks + scatter; 2: the one-pass windowed searches with global atomics);
 // rare-tier records appended to rare_out (capacity cap)
 void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_t U, int64_t W,
                unsigned long long* bits, const uint64_t* rare, int64_t Ur, int64_t id_base,
@@ -1070,7 +1335,56 @@ void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_
     GD_HIP(hipMemsetAsync(bits, 0, (size_t)s->nsets * W * 8, st));
     DevBuf rcnt(8, st);
     GD_HIP(hipMemsetAsync(rcnt.p, 0, 8, st));
-    if (U + Ur > 0 && ctx->option(OPT_FILL_SORT, 0) == 0) {
+    const int64_t mode = ctx->option(OPT_FILL_SORT, 0);
+    if (U + Ur > 0 && mode == 0) {
+        GD_REQUIRE(s->nsets < (int64_t(1) << 23) && s->h_off[s->nsets] < (int64_t(1) << 40),
+                   "collection too large for packed fill segments");
+        GD_REQUIRE(U <= (int64_t(1) << 31), "dense tier too large for u32 positions");   // keeps ~0 out of every row
+        // segment length per set: its windows should fit the LDS caps (window ~ length x dictionary / set size)
+        std::vector<int64_t> seg, first(s->nsets + 1, 0);
+        for (int64_t i = 0; i < s->nsets; i++) {
+            first[i] = (int64_t)seg.size();
+            const double ni = (double)(s->h_off[i + 1] - s->h_off[i]);
+            const double fit = 0.8 * std::min(kWinDense * ni / (double)std::max<int64_t>(1, U),
+                                              kRareFences * kRareBucket * ni / (double)std::max<int64_t>(1, Ur));
+            const int64_t L = std::max<int64_t>(64, std::min<int64_t>(kPosSeg, (int64_t)(fit / 64) * 64));
+            for (int64_t b = s->h_off[i]; b < s->h_off[i + 1]; b += L) seg.push_back((i << 40) | b);
+        }
+        first[s->nsets] = (int64_t)seg.size();
+        DevBuf dseg(std::max<int64_t>(1, (int64_t)seg.size()) * 8, st);
+        if (!seg.empty()) h2d(dseg.p, seg.data(), seg.size() * 8, st);
+        const unsigned nslice = (unsigned)ceil_div(2 * W, kPosSlice);
+        int64_t s0 = 0;
+        while (s0 < s->nsets) {
+            int64_t s1 = s0 + 1;
+            while (s1 < s->nsets && s->h_off[s1 + 1] - s->h_off[s0] <= kFillPosChunk) s1++;
+            const int64_t base = s->h_off[s0], n = s->h_off[s1] - base, ns = first[s1] - first[s0];
+            DevBuf pos(std::max<int64_t>(1, n) * 4 + 16, st);
+            if (ns) {
+                const int64_t* sg = dseg.as<int64_t>() + first[s0];
+                DevBuf win(ns * 8 * 8, st);
+                fill_window_kernel<<<(unsigned)ceil_div(ns * 4, 256), 256, 0, st>>>(
+                    s->codes.as<uint64_t>(), s->off.as<int64_t>(), sg, ns, dict, U, rare, Ur, win.as<int64_t>());
+                GD_HIP(hipGetLastError());
+                GD_REQUIRE(ns < (int64_t(1) << 31), "too many fill segments in one chunk");
+                fill_pos_kernel<<<(unsigned)ns, 64, 0, st>>>(s->codes.as<uint64_t>(), win.as<int64_t>(), dict, rare,
+                                                             base, pos.as<uint32_t>(),
+                                                             id_base, rare_out, rcnt.as<unsigned long long>(),
+                                                             rare_cap, perm);
+                GD_HIP(hipGetLastError());
+            }
+            tr.mark("fill: merged positions");
+            for (int64_t c0 = s0; c0 < s1; c0 += 65535) {
+                const unsigned ny = (unsigned)std::min<int64_t>(65535, s1 - c0);
+                pos_bits_kernel<<<dim3(nslice, ny), 1024, 0, st>>>(pos.as<uint32_t>(), s->off.as<int64_t>(), c0, base,
+                                                                    W, reinterpret_cast<uint32_t*>(bits));
+                GD_HIP(hipGetLastError());
+            }
+            GD_HIP(hipStreamSynchronize(st));
+            tr.mark("fill: LDS row slices");
+            s0 = s1;
+        }
+    } else if (U + Ur > 0 && mode == 2) {
         // segments of <= kFillSeg codes inside one set, built on the host from the offsets
         GD_REQUIRE(s->nsets < (int64_t(1) << 23) && s->h_off[s->nsets] < (int64_t(1) << 40),
                    "collection too large for packed fill segments");

@@ -192,6 +192,40 @@ def test_large_segments_and_sentinel_code(ctx):
     assert np.array_equal(I2, eI) and bits_equal(D2, eD)
 
 
+@pytest.mark.parametrize("fill", [0, 1, 2])
+@pytest.mark.parametrize("keep", [False, True])
+def test_bitset_fill_ragged_sets(ctx, opts, fill, keep):
+    """The three bitset fills (merged positions + LDS row slices, the sort,
+    the one-pass atomics) on ragged sets: empty sets, two-code sets that span
+    the whole dictionary (the merge gallops), sets far larger than a fill
+    segment at unaligned offsets, and the all-ones code."""
+    import gdist
+    opts(fill_sort=fill)
+    rng = np.random.default_rng(17 + fill)
+    base = np.unique(rng.integers(0, 2 ** 63, 40000, dtype=np.uint64))
+    sets_codes = []
+    for t in range(23):
+        if t % 7 == 3:
+            c = np.zeros(0, np.uint64)
+        elif t % 7 == 5:
+            c = np.array([base[1], base[-2]], np.uint64)
+        else:
+            c = base[rng.random(len(base)) < rng.uniform(0.05, 0.95)]
+            c = c[: len(c) - int(rng.integers(0, 5))]
+        if t % 4 == 0:
+            c = np.concatenate([c, np.array([~np.uint64(0)], np.uint64)])
+        sets_codes.append(np.unique(c))
+    off = np.zeros(len(sets_codes) + 1, np.int64)
+    off[1:] = np.cumsum([len(c) for c in sets_codes])
+    flat = np.concatenate(sets_codes)
+    sets = gdist.KmerSets.from_codes(off, flat, 8, gdist.KmerType.PROT, ctx)
+    sets.build_bitsets(keep_singletons=keep)
+    n = len(sets_codes)
+    I, D = sets.matrix(method=gdist.METHOD_BITSET)
+    eI, eD = oracle.matrix(off, flat, 0, n, 0, n)
+    assert np.array_equal(I, eI) and bits_equal(D, eD)
+
+
 # ---------------------------------------------------------------- properties at size
 def test_full_size_properties_bitset(ctx):
     """Size-independent properties on a larger collection: symmetry,
@@ -581,7 +615,7 @@ def test_rare_tier_thresholds_exact(ctx, T, kernel, dedup, opts):
                                   "kernel_v5_atomic", "kernel_v6_rows", "kernel_v6_sun4", "kernel_v6_quads",
                                   "kernel_v6_2x2", "kernel_v6_2x2_rows", "kernel_v6_atomic", "absorb",
                                   "mixed_slabs", "mixed_slabs_atomic", "mixed_tiles", "unfused", "rare_kernel",
-                                  "unfused_rare_kernel", "fill_sort", "kernel_v6_consec", "kernel_v6_consec_rows",
+                                  "unfused_rare_kernel", "fill_sort", "fill_direct", "kernel_v6_consec", "kernel_v6_consec_rows",
                                   "kernel_v6_consec_sun4"])
 def test_sparse_complement_words_exact(ctx, mode, opts):
     """The dense tier in locus order with complement-sparse words: counts and
@@ -626,8 +660,10 @@ def test_sparse_complement_words_exact(ctx, mode, opts):
                 "unfused": {"sparse_fused": 0},
                 "rare_kernel": {"sparse_rare": 0},
                 "unfused_rare_kernel": {"sparse_fused": 0, "sparse_rare": 0},
-                # the bitset fill by the (code, set) sort + run ranks instead of windowed searches
+                # the bitset fill by the (code, set) sort + run ranks, or by the one-pass
+                # windowed searches with global atomics, instead of merged positions + LDS slices
                 "fill_sort": {"fill_sort": 1},
+                "fill_direct": {"fill_sort": 2},
                 "many_chunks": {"sparse_zmax": 100000, "sparse_chunks": 37},
                 # words counted from either side (complement / positive), model's choice
                 # a dense-only dictionary: the substitution kmers two or more
