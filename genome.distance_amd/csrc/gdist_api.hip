@@ -26,7 +26,7 @@ const char* const kOptNames[OPT_COUNT] = {
     "sparse_occ",      "sparse_sun",      "sketch_k",        "sketch_tile",     "sparse_part_budget",
     "guides",          "force_exchange",  "sparse_kernel",   "sparse_chunks",   "fold_dense_words", "sparse_abl",      "graph",
     "sparse_shape",    "sparse_absorb",   "sparse_balance",  "time_sparse",     "sparse_xcd",      "step_timing",     "sparse_rare",     "sparse_fused",
-    "sparse_fold",     "fill_sort",       "sparse_tile_order",
+    "sparse_fold",     "fill_sort",       "sparse_tile_order", "pack_sort",
 };
 
 static int option_index(const char* name) {

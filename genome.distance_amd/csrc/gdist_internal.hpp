@@ -204,8 +204,10 @@ enum Opt : int {
     OPT_SPARSE_FUSED,       // 0: no fused reduce + epilogue (zeroing, rare kernel, epilogue launched apart)
     OPT_SPARSE_FOLD,        // at most this many (padded) dense words counted inside the v5 / v6 tile kernel
                             // (8 per chunk; default 64, 0: the dense-word tile launch)
-    OPT_FILL_SORT,          // 1: bitset fill by a (code, set) sort + run ranks (default 0: windowed searches)
+    OPT_FILL_SORT,          // bitset fill: 0 merged positions + LDS row slices (default), 1 (code, set) sort +
+                            // run ranks, 2 one-pass windowed searches with global atomics
     OPT_SPARSE_TILE_ORDER,  // 1: sparse tiles heaviest first (default 0: row-major order; C2 neutral)
+    OPT_PACK_SORT,          // 1: pack sorts (code, set) pairs twice (default 0: one sort of packed set|code keys when they fit 64 bits)
     OPT_COUNT
 };
 extern const char* const kOptNames[OPT_COUNT];

@@ -174,6 +174,25 @@ __global__ void compact_kernel(const uint64_t* __restrict__ codes, const int32_t
         if (flag[i]) out[pos[i]] = codes[i];
 }
 
+// (set, code) pairs <-> one key set << cbits | code (cbits + set bits <= 64)
+__global__ void pack_keys_kernel(const uint64_t* __restrict__ codes, const int32_t* __restrict__ ids, int64_t n,
+                                 int cbits, uint64_t* __restrict__ keys) {
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        keys[i] = cbits < 64 ? ((uint64_t)(uint32_t)ids[i] << cbits) | codes[i] : codes[i];
+}
+
+__global__ void unpack_keys_kernel(const uint64_t* __restrict__ keys, int64_t n, int cbits,
+                                   uint64_t* __restrict__ codes, int32_t* __restrict__ ids) {
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const uint64_t mask = cbits < 64 ? (uint64_t(1) << cbits) - 1 : ~0ull;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t k = keys[i];
+        codes[i] = k & mask;
+        ids[i] = cbits < 64 ? (int32_t)(k >> cbits) : 0;
+    }
+}
+
 // off[s] = pos[lower_bound(ids, s)] (or the unique total past the end).
 __global__ void set_offsets_kernel(const int32_t* __restrict__ ids, const int64_t* __restrict__ pos,
                                    const int32_t* __restrict__ flag, int64_t n, int nsets,
@@ -446,13 +465,30 @@ void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_se
         int32_t* ids = vA.as<int32_t>(); int32_t* ids_alt = vB.as<int32_t>();
         PackDebug* dbg = (s0 == 0) ? g_pack_debug : nullptr;
         if (dbg) { dbg->n = n; d2h(dbg->k_extract, keys, n * 8, st); d2h(dbg->v_extract, ids, n * 4, st); }
-        sort_pairs_u64_i32(ctx, keys, keys_alt, ids, ids_alt, (size_t)n, 0, std::min(64, cbits));
-        if (dbg) { d2h(dbg->k_sort1, keys, n * 8, st); d2h(dbg->v_sort1, ids, n * 4, st); }
         int idbits = 1;
         while ((int64_t(1) << idbits) <= nc) idbits++;
-        sort_pairs_i32_u64(ctx, ids, ids_alt, keys, keys_alt, (size_t)n, idbits);
-        if (dbg) { d2h(dbg->k_sort2, keys, n * 8, st); d2h(dbg->v_sort2, ids, n * 4, st); }
-        tr.mark("pack: sort by code, by set");
+        if (!dbg && cbits + idbits <= 64 && ctx->option(OPT_PACK_SORT, 0) == 0) {
+            // one sort of (set << cbits | code) keys: 8-byte records instead of two
+            // 12-byte pair sorts (C2: 52-bit keys, 7 digit passes instead of 6 + 2)
+            if (n > 0) {
+                pack_keys_kernel<<<grid_for(n), 256, 0, st>>>(keys, ids, n, cbits, keys_alt);
+                GD_HIP(hipGetLastError());
+            }
+            std::swap(keys, keys_alt);
+            sort_keys_u64(ctx, keys, keys_alt, (size_t)n, 0, cbits + idbits);
+            if (n > 0) {
+                unpack_keys_kernel<<<grid_for(n), 256, 0, st>>>(keys, n, cbits, keys_alt, ids);
+                GD_HIP(hipGetLastError());
+            }
+            std::swap(keys, keys_alt);
+            tr.mark("pack: sort by set|code");
+        } else {
+            sort_pairs_u64_i32(ctx, keys, keys_alt, ids, ids_alt, (size_t)n, 0, std::min(64, cbits));
+            if (dbg) { d2h(dbg->k_sort1, keys, n * 8, st); d2h(dbg->v_sort1, ids, n * 4, st); }
+            sort_pairs_i32_u64(ctx, ids, ids_alt, keys, keys_alt, (size_t)n, idbits);
+            if (dbg) { d2h(dbg->k_sort2, keys, n * 8, st); d2h(dbg->v_sort2, ids, n * 4, st); }
+            tr.mark("pack: sort by code, by set");
+        }
 
         DevBuf flag(n * 4 + 4, st), pos(n * 8 + 8, st);
         if (n > 0) {

@@ -615,7 +615,7 @@ def test_rare_tier_thresholds_exact(ctx, T, kernel, dedup, opts):
                                   "kernel_v5_atomic", "kernel_v6_rows", "kernel_v6_sun4", "kernel_v6_quads",
                                   "kernel_v6_2x2", "kernel_v6_2x2_rows", "kernel_v6_atomic", "absorb",
                                   "mixed_slabs", "mixed_slabs_atomic", "mixed_tiles", "unfused", "rare_kernel",
-                                  "unfused_rare_kernel", "fill_sort", "fill_direct", "kernel_v6_consec", "kernel_v6_consec_rows",
+                                  "unfused_rare_kernel", "fill_sort", "fill_direct", "pack_pairs", "kernel_v6_consec", "kernel_v6_consec_rows",
                                   "kernel_v6_consec_sun4"])
 def test_sparse_complement_words_exact(ctx, mode, opts):
     """The dense tier in locus order with complement-sparse words: counts and
@@ -664,6 +664,8 @@ def test_sparse_complement_words_exact(ctx, mode, opts):
                 # windowed searches with global atomics, instead of merged positions + LDS slices
                 "fill_sort": {"fill_sort": 1},
                 "fill_direct": {"fill_sort": 2},
+                # the pack's two (code, set) pair sorts instead of one sort of set|code keys
+                "pack_pairs": {"pack_sort": 1},
                 "many_chunks": {"sparse_zmax": 100000, "sparse_chunks": 37},
                 # words counted from either side (complement / positive), model's choice
                 # a dense-only dictionary: the substitution kmers two or more
