@@ -1359,7 +1359,9 @@ void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_
             int64_t s1 = s0 + 1;
             while (s1 < s->nsets && s->h_off[s1 + 1] - s->h_off[s0] <= kFillPosChunk) s1++;
             const int64_t base = s->h_off[s0], n = s->h_off[s1] - base, ns = first[s1] - first[s0];
-            DevBuf pos(std::max<int64_t>(1, n) * 4 + 16, st);
+            // sized like the summary's per-chunk key buffers (8 B a code) so that the caching
+            // allocator hands back one of those blocks: a fresh 4 GiB block costs ~25 ms
+            DevBuf pos(std::max<int64_t>(1, n) * 8 + 8, st);
             if (ns) {
                 const int64_t* sg = dseg.as<int64_t>() + first[s0];
                 DevBuf win(ns * 8 * 8, st);
