@@ -730,7 +730,7 @@ void runs_of(gdist_ctx* ctx, const uint64_t* keys, int64_t n, DevBuf& flag, DevB
 }
 
 // merge (codes, counts) parts into one summary
-void merge_parts(gdist_ctx* ctx, const std::vector<SummaryView>& parts, Summary& out) {
+void merge_parts(gdist_ctx* ctx, const std::vector<SummaryView>& parts, Summary& out, int end_bit = 64) {
     hipStream_t st = ctx->stream;
     int64_t m = 0;
     for (auto& p : parts) m += p.n;
@@ -745,7 +745,7 @@ void merge_parts(gdist_ctx* ctx, const std::vector<SummaryView>& parts, Summary&
     }
     uint64_t* keys = kA.as<uint64_t>(); uint64_t* kalt = kB.as<uint64_t>();
     int32_t* vals = vA.as<int32_t>(); int32_t* valt = vB.as<int32_t>();
-    if (parts.size() > 1) sort_pairs_u64_i32(ctx, keys, kalt, vals, valt, (size_t)m, 0, 64);
+    if (parts.size() > 1) sort_pairs_u64_i32(ctx, keys, kalt, vals, valt, (size_t)m, 0, end_bit);
     DevBuf flag, pos, start;
     runs_of(ctx, keys, m, flag, pos, out.codes, start, out.n);
     // per-run sum of counts via prefix sums of the counts
@@ -771,6 +771,25 @@ void merge_parts(gdist_ctx* ctx, const std::vector<SummaryView>& parts, Summary&
 void local_summary(gdist_ctx* ctx, const gdist_sets* s, Summary& out) {
     hipStream_t st = ctx->stream;
     const int cbits = std::min(64, code_bits(s->kind, s->k, s->flags));
+    if (!s->pack_sum.empty()) {
+        // the pack's chunk summaries (code-major pack sort): merge, no code sort
+        if (s->pack_sum.size() == 1) {
+            const Summary& p = s->pack_sum[0];
+            out.n = p.n;
+            out.codes.alloc(p.n * 8 + 8, st);
+            out.counts.alloc(p.n * 4 + 4, st);
+            if (p.n) {
+                GD_HIP(hipMemcpyAsync(out.codes.p, p.codes.p, p.n * 8, hipMemcpyDeviceToDevice, st));
+                GD_HIP(hipMemcpyAsync(out.counts.p, p.counts.p, p.n * 4, hipMemcpyDeviceToDevice, st));
+            }
+            GD_HIP(hipStreamSynchronize(st));
+            return;
+        }
+        std::vector<SummaryView> parts;
+        for (auto& p : s->pack_sum) parts.push_back({p.codes.as<uint64_t>(), p.counts.as<uint32_t>(), p.n});
+        merge_parts(ctx, parts, out, cbits);
+        return;
+    }
     std::vector<Summary> chunks;
     int64_t s0 = 0;
     while (s0 < s->nsets) {

@@ -26,7 +26,7 @@ const char* const kOptNames[OPT_COUNT] = {
     "sparse_occ",      "sparse_sun",      "sketch_k",        "sketch_tile",     "sparse_part_budget",
     "guides",          "force_exchange",  "sparse_kernel",   "sparse_chunks",   "fold_dense_words", "sparse_abl",      "graph",
     "sparse_shape",    "sparse_absorb",   "sparse_balance",  "time_sparse",     "sparse_xcd",      "step_timing",     "sparse_rare",     "sparse_fused",
-    "sparse_fold",     "fill_sort",       "sparse_tile_order", "pack_sort",
+    "sparse_fold",     "fill_sort",       "sparse_tile_order", "pack_sort",       "pack_summary",    "pack_overlap",    "pack_chunk",
 };
 
 static int option_index(const char* name) {
@@ -408,13 +408,15 @@ int gdist_sets_pack(gdist_ctx* ctx, int kind, int k, unsigned flags, const char*
         for (int64_t s = 0; s <= nseqs; s++) h[s] = (nseqs ? seq_off[s] : 0) - base;
         for (int64_t s = 0; s < nseqs; s++) GD_REQUIRE(h[s + 1] >= h[s], "sequence offsets must be non-decreasing");
         const int64_t bytes = h[nseqs];
+        Trace tr(ctx->stream, ctx->trace());
         DevBuf dseq(bytes + 1, ctx->stream), doff((nseqs + 1) * 8, ctx->stream);
-        if (bytes) h2d(dseq.p, seqs + base, bytes, ctx->stream);
         h2d(doff.p, h.data(), (nseqs + 1) * 8, ctx->stream);
+        tr.mark("pack: byte buffer");
         auto* s = new gdist_sets();
         s->ctx = ctx;
         try {
-            pack_sets(ctx, kind, k, flags, dseq.as<char>(), doff.as<int64_t>(), h, s);
+            // the bytes move to dseq during the pack, chunk by chunk
+            pack_sets(ctx, kind, k, flags, dseq.as<char>(), doff.as<int64_t>(), h, s, seqs + base);
         } catch (...) {
             delete s;
             throw;

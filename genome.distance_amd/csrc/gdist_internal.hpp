@@ -208,6 +208,11 @@ enum Opt : int {
                             // run ranks, 2 one-pass windowed searches with global atomics
     OPT_SPARSE_TILE_ORDER,  // 1: sparse tiles heaviest first (default 0: row-major order; C2 neutral)
     OPT_PACK_SORT,          // 1: pack sorts (code, set) pairs twice (default 0: one sort of packed set|code keys when they fit 64 bits)
+    OPT_PACK_SUMMARY,       // 0: pack sorts set|code keys and the bitset build re-sorts every code for the
+                            // dictionary summary (default 1: code|set keys, the chunk summaries kept from the pack)
+    OPT_PACK_OVERLAP,       // 0: gdist_sets_pack uploads every sequence byte before packing (default 1: chunk
+                            // c + 1 uploads from a host thread while chunk c packs)
+    OPT_PACK_CHUNK,         // kmer windows per pack chunk (default 2^30; small values test the chunked paths)
     OPT_COUNT
 };
 extern const char* const kOptNames[OPT_COUNT];
@@ -227,6 +232,14 @@ struct Trace {
         fprintf(stderr, "gdist: %-28s %9.1f ms\n", stage, std::chrono::duration<double, std::milli>(n - t).count());
         t = n;
     }
+};
+
+// Dictionary summary: sorted distinct codes + the number of sets holding each
+// (bitset.hip; pack.hip keeps one per pack chunk, gdist_sets::pack_sum)
+struct Summary {
+    DevBuf codes;    // uint64 [n]
+    DevBuf counts;   // uint32 [n]
+    int64_t n = 0;
 };
 
 }  // namespace gdist
@@ -335,6 +348,10 @@ struct gdist_sets {
     std::vector<int32_t> sp_bucket_bits;  // [nsets][sp_nbk]: complement bits per set and 1024 sparse words
     std::vector<double> sp_cost;          // [Ws + 1]: prefix of each sparse word's modelled cost over all tiles
     int64_t sp_nbk = 0;
+    // summaries of the pack chunks (option pack_summary): the code-major pack
+    // sort leaves each chunk's codes in code order, so their runs are that
+    // chunk's summary; local_summary merges them instead of re-sorting codes
+    std::vector<gdist::Summary> pack_sum;
     double sp_products = 0, sp_items = 0; // whole-triangle products / (tile, word) visits (cost model)
     bool auto_sorted = false;             // METHOD_AUTO measured the sorted join cheaper
     // bitset_matrix launch plans by (region, kernel switches); cleared with the bitsets
@@ -358,8 +375,11 @@ struct gdist_lsh {
 namespace gdist {
 
 // pack.hip
+// h_seqs (optional): the bytes are still on the host; d_seqs is then the
+// caller's device buffer of the same extent, filled chunk by chunk during the pack
 void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_seqs,
-               const int64_t* d_seq_off, const std::vector<int64_t>& h_seq_off, gdist_sets* out);
+               const int64_t* d_seq_off, const std::vector<int64_t>& h_seq_off, gdist_sets* out,
+               const char* h_seqs = nullptr);
 void sort_pairs_u64_i32(gdist_ctx* ctx, uint64_t*& keys, uint64_t*& keys_alt, int32_t*& vals,
                         int32_t*& vals_alt, size_t n, int begin_bit, int end_bit);
 void sort_keys_u64(gdist_ctx* ctx, uint64_t*& keys, uint64_t*& keys_alt, size_t n, int begin_bit,
@@ -368,12 +388,7 @@ void exclusive_scan_i64(gdist_ctx* ctx, const int64_t* in, int64_t* out, size_t 
 void exclusive_scan_i32_to_i64(gdist_ctx* ctx, const int32_t* in, int64_t* out, size_t n);
 int code_bits(int kind, int k, unsigned flags);
 
-// bitset.hip — dictionary summaries: sorted distinct codes + number of sets holding each
-struct Summary {
-    DevBuf codes;    // uint64 [n]
-    DevBuf counts;   // uint32 [n]
-    int64_t n = 0;
-};
+// bitset.hip — dictionary summaries (struct Summary above gdist_sets)
 struct SummaryView {
     const uint64_t* codes;
     const uint32_t* counts;

@@ -8,14 +8,20 @@
 //   1. validate   — unencodable chars in keep / 5-bit modes -> EINVAL
 //   2. extract    — one thread per window: code (fwd, rc or canonical),
 //                   value = set id, or the "invalid" id for skipped windows
-//   3. radix sort by code (code bits only), then stable radix sort by set id
+//   3. radix sort of code|set keys (the chunk's dictionary summary is the
+//      runs of codes), then a stable radix sort on the set bits alone
 //   4. unique flags + exclusive scan -> compacted CSR codes, offsets by
-//      lower_bound of each set id in the sorted id array
+//      lower_bound of each set id in the sorted keys
+// From host bytes (gdist_sets_pack) a host thread uploads chunk c + 1 while
+// the device works on chunk c (ChunkUploader).
 // The alphabet maps are order preserving, so code order == Java String order.
 #include <cstring>
 #include <rocprim/rocprim.hpp>
 
 #include <algorithm>
+#include <atomic>
+#include <future>
+#include <thread>
 
 #include "gdist_internal.hpp"
 
@@ -208,6 +214,74 @@ __global__ void set_offsets_kernel(const int32_t* __restrict__ ids, const int64_
     off[s] = base + (lo < n ? pos[lo] : total);
 }
 
+// Code-major keys (option pack_summary): code << idbits | set, the set field
+// nsets marking an invalid window. Sorted, equal keys are one set's repeats of
+// a kmer, and the runs of equal codes (one key per holding set after the
+// unique) are the chunk's dictionary summary; a stable sort on the set bits
+// alone then gives the set-major CSR with each set's codes still ascending.
+__global__ void pack_keys_cm_kernel(const uint64_t* __restrict__ codes, const int32_t* __restrict__ ids, int64_t n,
+                                    int idbits, uint64_t* __restrict__ keys) {
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        keys[i] = (codes[i] << idbits) | (uint32_t)ids[i];
+}
+
+// flag word: bit 0 = the first key of its (code, set) pair and a valid
+// window; bit 32 = that, and the first of its code (invalid windows carry
+// the largest set field, so they sort after a code's valid keys and never
+// sit between two of them)
+__global__ void cm_flags_kernel(const uint64_t* __restrict__ keys, int64_t n, uint64_t smask, uint64_t invalid,
+                                int idbits, int64_t* __restrict__ flag) {
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t k = keys[i];
+        const uint64_t p = i ? keys[i - 1] : ~k;
+        const bool u = (k & smask) != invalid && k != p;
+        const bool h = u && (i == 0 || (k >> idbits) != (p >> idbits));
+        flag[i] = (int64_t)u | ((int64_t)h << 32);
+    }
+}
+
+// unique keys to u[], each code's first to the summary (code, start in u[])
+__global__ void cm_emit_kernel(const uint64_t* __restrict__ keys, const int64_t* __restrict__ flag,
+                               const int64_t* __restrict__ pos, int64_t n, int idbits, uint64_t* __restrict__ u,
+                               uint64_t* __restrict__ codes, int64_t* __restrict__ start) {
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const int64_t f = flag[i];
+        if (!(f & 1)) continue;
+        const uint64_t k = keys[i];
+        const int64_t p = pos[i], at = p & 0xFFFFFFFFll;
+        u[at] = k;
+        if (f >> 32) { codes[p >> 32] = k >> idbits; start[p >> 32] = at; }
+    }
+}
+
+__global__ void cm_run_counts_kernel(const int64_t* __restrict__ start, int64_t nruns, int64_t n,
+                                     uint32_t* __restrict__ counts) {
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nruns; r += stride)
+        counts[r] = (uint32_t)((r + 1 < nruns ? start[r + 1] : n) - start[r]);
+}
+
+__global__ void cm_codes_kernel(const uint64_t* __restrict__ u, int64_t n, int idbits, uint64_t* __restrict__ codes) {
+    int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) codes[i] = u[i] >> idbits;
+}
+
+// off[s] = base + lower_bound(u & smask, s) over the set-major unique keys
+__global__ void cm_set_offsets_kernel(const uint64_t* __restrict__ u, int64_t n, uint64_t smask, int nsets,
+                                      int64_t base, int64_t* __restrict__ off) {
+    int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s > nsets) return;
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if ((int64_t)(u[mid] & smask) < s) lo = mid + 1; else hi = mid;
+    }
+    off[s] = base + lo;
+}
+
 inline int grid_for(int64_t n, int block = 256, int64_t cap = 256 * 32) {
     int64_t g = ceil_div(n, block);
     return (int)std::max<int64_t>(1, std::min<int64_t>(g, cap));
@@ -348,6 +422,57 @@ void exclusive_scan_i32_to_i64(gdist_ctx* ctx, const int32_t* in, int64_t* out, 
                                    ctx->stream));
 }
 
+// Overlapped upload of host sequence bytes: a host thread copies each pack
+// chunk's byte range on its own stream in 64 MiB pieces (the runtime's
+// pageable path: ~25 GB/s on the box, ahead of our own pinned staging with a
+// CPU memcpy, measured 5-7 GB/s), synchronises, then signals the chunk; the
+// pack waits for chunk c's signal before its extraction, so chunk c + 1's
+// bytes move while chunk c sorts (chunk 0's wait is the part left on the
+// clock). Pieces, not one copy per chunk, so that the pack's own small
+// read-backs interleave with the upload.
+class ChunkUploader {
+  public:
+    ChunkUploader(int device, const char* h, char* d, std::vector<std::pair<int64_t, int64_t>> ranges)
+        : ready_(ranges.size()) {
+        for (auto& p : ready_) got_.push_back(p.get_future());
+        th_ = std::thread([this, device, h, d, ranges] { run(device, h, d, ranges); });
+    }
+    ~ChunkUploader() {
+        stop_ = true;
+        if (th_.joinable()) th_.join();
+    }
+    void wait(size_t c) { got_[c].get(); }   // rethrows the uploader's error
+
+  private:
+    static constexpr int64_t kPiece = int64_t(64) << 20;
+    void run(int device, const char* h, char* d, const std::vector<std::pair<int64_t, int64_t>>& ranges) {
+        size_t c = 0;
+        hipStream_t us = nullptr;
+        try {
+            GD_HIP(hipSetDevice(device));
+            GD_HIP(hipStreamCreateWithFlags(&us, hipStreamNonBlocking));
+            for (; c < ranges.size() && !stop_; c++) {
+                for (int64_t o = ranges[c].first; o < ranges[c].second; o += kPiece) {
+                    const size_t len = (size_t)std::min(kPiece, ranges[c].second - o);
+                    GD_HIP(hipMemcpyWithStream(d + o, h + o, len, hipMemcpyHostToDevice, us));
+                }
+                GD_HIP(hipStreamSynchronize(us));
+                ready_[c].set_value();
+            }
+        } catch (...) {
+            for (; c < ranges.size(); c++) ready_[c].set_exception(std::current_exception());
+        }
+        if (us) {
+            (void)hipStreamSynchronize(us);
+            (void)hipStreamDestroy(us);
+        }
+    }
+    std::vector<std::promise<void>> ready_;
+    std::vector<std::future<void>> got_;
+    std::atomic<bool> stop_{false};
+    std::thread th_;
+};
+
 // Debug hook (diagnostics only): host copies of each stage of the first chunk.
 struct PackDebug {
     uint64_t* k_extract; int32_t* v_extract;
@@ -359,7 +484,8 @@ static PackDebug* g_pack_debug = nullptr;
 
 // Pack sequences [0, nseq) (device bytes + device/host offsets) into `out`.
 void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_seqs,
-               const int64_t* d_seq_off, const std::vector<int64_t>& h_seq_off, gdist_sets* out) {
+               const int64_t* d_seq_off, const std::vector<int64_t>& h_seq_off, gdist_sets* out,
+               const char* h_seqs) {
     const int64_t nseq = (int64_t)h_seq_off.size() - 1;
     GD_REQUIRE(kind == GDIST_DNA || kind == GDIST_PROT, "kind must be GDIST_DNA or GDIST_PROT");
     unsigned am = flags & GDIST_AMBIG_MASK;
@@ -384,9 +510,38 @@ void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_se
 
     out->kind = kind; out->k = k; out->flags = flags; out->nsets = nseq;
 
-    // 1. validation of the whole byte range (keep modes; 5-bit protein)
     const int64_t total_bytes = h_seq_off.back() - h_seq_off.front();
     bool need_validate = dna_keep || (kind == GDIST_PROT && bits == 5);
+    // windows per sequence
+    std::vector<int64_t> nwin(nseq);
+    for (int64_t s = 0; s < nseq; s++) {
+        int64_t len = h_seq_off[s + 1] - h_seq_off[s];
+        GD_REQUIRE(len >= 0, "sequence offsets must be non-decreasing");
+        nwin[s] = std::max<int64_t>(0, len - k + 1);
+    }
+    // chunks of sequences, at most kChunk entries each (the first sequence of a chunk always fits)
+    const int64_t kChunk = std::max<int64_t>(1, ctx->option(OPT_PACK_CHUNK, int64_t(1) << 30));
+    std::vector<std::pair<int64_t, int64_t>> chunks;   // [s0, s1)
+    for (int64_t s0 = 0, s1; s0 < nseq; s0 = s1) {
+        int64_t entries = 0;
+        for (s1 = s0; s1 < nseq && (s1 == s0 || entries + nwin[s1] * mult <= kChunk); s1++) entries += nwin[s1] * mult;
+        chunks.push_back({s0, s1});
+    }
+    // host bytes: whole-range passes (validation, folding) need every byte
+    // first; otherwise chunk c + 1 uploads while chunk c is packed
+    std::unique_ptr<ChunkUploader> up;
+    if (h_seqs && total_bytes > 0) {
+        char* dst = const_cast<char*>(d_seqs);         // the caller's upload buffer (gdist_sets_pack)
+        if (need_validate || (raw8 && alh.fold) || chunks.size() < 2 || ctx->option(OPT_PACK_OVERLAP, 1) == 0) {
+            h2d(dst + h_seq_off.front(), h_seqs + h_seq_off.front(), total_bytes, st);
+        } else {
+            std::vector<std::pair<int64_t, int64_t>> ranges;
+            for (auto& c : chunks) ranges.push_back({h_seq_off[c.first], h_seq_off[c.second]});
+            up.reset(new ChunkUploader(ctx->device, h_seqs, dst, std::move(ranges)));
+        }
+    }
+
+    // 1. validation of the whole byte range (keep modes; 5-bit protein)
     if (need_validate && total_bytes > 0) {
         DevBuf bad(sizeof(int), st);
         GD_HIP(hipMemsetAsync(bad.p, 0, sizeof(int), st));
@@ -412,24 +567,22 @@ void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_se
         src = folded.as<unsigned char>();
     }
 
-    // windows per sequence
-    std::vector<int64_t> nwin(nseq);
-    for (int64_t s = 0; s < nseq; s++) {
-        int64_t len = h_seq_off[s + 1] - h_seq_off[s];
-        GD_REQUIRE(len >= 0, "sequence offsets must be non-decreasing");
-        nwin[s] = std::max<int64_t>(0, len - k + 1);
-    }
-
-    // 2-4. chunks of sequences, at most kChunk entries each
+    // 2-4. the chunks
     Trace tr(st, ctx->trace());
     tr.mark("pack: validate/fold");
-    const int64_t kChunk = int64_t(1) << 30;
-    std::vector<DevBuf> chunk_codes;
-    std::vector<int64_t> chunk_total;
+    size_t ci = 0;
+    // every chunk compacts its unique codes straight into one buffer sized
+    // for every window (an upper bound; trimmed below when far too large)
+    int64_t cap = 0;
+    for (int64_t s = 0; s < nseq; s++) cap += nwin[s] * mult;
+    DevBuf all_codes(cap * 8 + 8, st);
     std::vector<int64_t> h_off(nseq + 1, 0);
     DevBuf d_off((nseq + 1) * sizeof(int64_t), st);
     int64_t base = 0;
     int64_t s0 = 0;
+    bool want_sum = ctx->option(OPT_PACK_SUMMARY, 1) != 0, sum_ok = true;
+    std::vector<Summary> pack_sum;
+    int64_t sum_runs = 0;
     while (s0 < nseq || (nseq == 0 && s0 == 0)) {
         if (nseq == 0) break;
         int64_t s1 = s0, entries = 0;
@@ -437,6 +590,9 @@ void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_se
             entries += nwin[s1] * mult;
             s1++;
         }
+        GD_REQUIRE(ci < chunks.size() && chunks[ci].first == s0 && chunks[ci].second == s1, "pack: chunk plan");
+        if (up) up->wait(ci);                            // this chunk's bytes are on the device
+        ci++;
         const int nc = (int)(s1 - s0);
         std::vector<int64_t> hwo(nc + 1, 0);
         for (int i = 0; i < nc; i++) hwo[i + 1] = hwo[i] + nwin[s0 + i];
@@ -467,6 +623,78 @@ void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_se
         if (dbg) { dbg->n = n; d2h(dbg->k_extract, keys, n * 8, st); d2h(dbg->v_extract, ids, n * 4, st); }
         int idbits = 1;
         while ((int64_t(1) << idbits) <= nc) idbits++;
+        if (want_sum && !dbg && cbits + idbits <= 64 && n < (int64_t(1) << 31) && ctx->option(OPT_PACK_SORT, 0) == 0) {
+            // code-major keys: the chunk's summary falls out of the same sort
+            const uint64_t smask = (uint64_t(1) << idbits) - 1;
+            if (n > 0) {
+                pack_keys_cm_kernel<<<grid_for(n), 256, 0, st>>>(keys, ids, n, idbits, keys_alt);
+                GD_HIP(hipGetLastError());
+            }
+            std::swap(keys, keys_alt);
+            sort_keys_u64(ctx, keys, keys_alt, (size_t)n, 0, cbits + idbits);
+            tr.mark("pack: sort by code|set");
+            // one flag word per key: bit 0 = first key of its (code, set)
+            // (valid), bit 32 = first valid key of its code; one scan gives
+            // both the unique positions (low half) and the run index (high)
+            DevBuf flag(n * 8 + 8, st), pos(n * 8 + 8, st);
+            int64_t uniq = 0, nruns = 0;
+            if (n > 0) {
+                cm_flags_kernel<<<grid_for(n), 256, 0, st>>>(keys, n, smask, (uint64_t)nc, idbits,
+                                                             flag.as<int64_t>());
+                GD_HIP(hipGetLastError());
+                exclusive_scan_i64(ctx, flag.as<int64_t>(), pos.as<int64_t>(), (size_t)n);
+                int64_t last = 0, lf = 0;
+                d2h(&last, pos.as<int64_t>() + n - 1, 8, st);
+                d2h(&lf, flag.as<int64_t>() + n - 1, 8, st);
+                GD_HIP(hipStreamSynchronize(st));
+                uniq = (last + lf) & 0xFFFFFFFFll;
+                nruns = (last + lf) >> 32;
+            }
+            Summary sum;
+            sum.codes.alloc(nruns * 8 + 8, st);
+            sum.counts.alloc(nruns * 4 + 4, st);
+            sum.n = nruns;
+            if (uniq > 0) {
+                DevBuf start(nruns * 8 + 8, st);
+                cm_emit_kernel<<<grid_for(n), 256, 0, st>>>(keys, flag.as<int64_t>(), pos.as<int64_t>(), n, idbits,
+                                                            keys_alt, sum.codes.as<uint64_t>(), start.as<int64_t>());
+                GD_HIP(hipGetLastError());
+                std::swap(keys, keys_alt);                      // keys: the unique code|set keys
+                cm_run_counts_kernel<<<grid_for(nruns), 256, 0, st>>>(start.as<int64_t>(), nruns, uniq,
+                                                                       sum.counts.as<uint32_t>());
+                GD_HIP(hipGetLastError());
+                // set-major: a stable sort on the set bits keeps each set's codes ascending
+                sort_keys_u64(ctx, keys, keys_alt, (size_t)uniq, 0, idbits);
+                GD_HIP(hipStreamSynchronize(st));
+            }
+            tr.mark("pack: unique+summary+by set");
+            if (uniq > 0) {
+                cm_codes_kernel<<<grid_for(uniq), 256, 0, st>>>(keys, uniq, idbits, all_codes.as<uint64_t>() + base);
+                GD_HIP(hipGetLastError());
+            }
+            cm_set_offsets_kernel<<<(int)ceil_div(nc + 1, 256), 256, 0, st>>>(keys, uniq, smask, nc, base,
+                                                                               d_off.as<int64_t>() + s0);
+            GD_HIP(hipGetLastError());
+            std::vector<int64_t> co(nc + 1);
+            d2h(co.data(), d_off.as<int64_t>() + s0, (nc + 1) * sizeof(int64_t), st);
+            GD_HIP(hipStreamSynchronize(st));
+            GD_REQUIRE(co[nc] - base == uniq, "pack: set offsets disagree with the unique count");
+            for (int i = 0; i <= nc; i++) h_off[s0 + i] = co[i];
+            tr.mark("pack: codes+offsets");
+            // keep the summaries only while they are much smaller than the
+            // codes (shared kmers); otherwise the bitset build sorts the codes
+            sum_runs += nruns;
+            if (sum_runs * 4 > base + uniq) {
+                want_sum = false;
+                pack_sum.clear();
+            } else {
+                pack_sum.push_back(std::move(sum));
+            }
+            base += uniq;
+            s0 = s1;
+            continue;
+        }
+        sum_ok = false;                                        // a chunk without a summary
         if (!dbg && cbits + idbits <= 64 && ctx->option(OPT_PACK_SORT, 0) == 0) {
             // one sort of (set << cbits | code) keys: 8-byte records instead of two
             // 12-byte pair sorts (C2: 52-bit keys, 7 digit passes instead of 6 + 2)
@@ -504,41 +732,35 @@ void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_se
         d2h(co.data(), d_off.as<int64_t>() + s0, (nc + 1) * sizeof(int64_t), st);
         GD_HIP(hipStreamSynchronize(st));
         const int64_t uniq = co[nc] - base;
-        DevBuf cc(uniq * 8 + 8, st);
         if (n > 0) {
             compact_kernel<<<grid_for(n), 256, 0, st>>>(keys, flag.as<int32_t>(), pos.as<int64_t>(), n,
-                                                         cc.as<uint64_t>());
+                                                         all_codes.as<uint64_t>() + base);
             GD_HIP(hipGetLastError());
         }
         for (int i = 0; i <= nc; i++) h_off[s0 + i] = co[i];
         tr.mark("pack: unique+compact");
-        chunk_codes.push_back(std::move(cc));
-        chunk_total.push_back(uniq);
         base += uniq;
         s0 = s1;
     }
     out->h_off = h_off;
     out->total = base;
+    out->pack_sum.clear();
+    if (want_sum && sum_ok && nseq > 0) out->pack_sum = std::move(pack_sum);
     out->off = std::move(d_off);
     if (nseq == 0) {
         out->off.alloc(sizeof(int64_t), st);
         GD_HIP(hipMemsetAsync(out->off.p, 0, sizeof(int64_t), st));
         out->h_off.assign(1, 0);
     }
-    if (chunk_codes.size() == 1) {
-        out->codes = std::move(chunk_codes[0]);
-    } else {
+    if (base < cap / 2 && (cap - base) * 8 > (int64_t(64) << 20)) {
+        // mostly repeated windows: keep an exact-size copy instead of the bound
         out->codes.alloc(base * 8 + 8, st);
-        int64_t at = 0;
-        for (size_t c = 0; c < chunk_codes.size(); c++) {
-            if (chunk_total[c])
-                GD_HIP(hipMemcpyAsync(out->codes.as<uint64_t>() + at, chunk_codes[c].p, chunk_total[c] * 8,
-                                      hipMemcpyDeviceToDevice, st));
-            at += chunk_total[c];
-        }
+        if (base) GD_HIP(hipMemcpyAsync(out->codes.p, all_codes.p, base * 8, hipMemcpyDeviceToDevice, st));
+    } else {
+        out->codes = std::move(all_codes);
     }
     GD_HIP(hipStreamSynchronize(st));
-    tr.mark("pack: concat");
+    tr.mark("pack: codes");
 }
 
 }  // namespace gdist

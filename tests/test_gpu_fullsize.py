@@ -36,7 +36,7 @@ def _threads():
 
 
 @pytest.mark.timeout(900)
-def test_c2_full_size_rows_vs_oracle(ctx):
+def test_c2_full_size_rows_vs_oracle(ctx, opts):
     import gdist
     from gdist import synth
     n, L = 1000, 2_000_000
@@ -66,6 +66,16 @@ def test_c2_full_size_rows_vs_oracle(ctx):
         assert bits_equal(D[i], eD), i
     # the whole triangle is symmetric (rows and columns of one pair agree)
     assert np.array_equal(I, I.T)
+    # the default pack keeps its four chunks' summaries for the dictionary; the
+    # set-major pack (option pack_summary 0) leaves the bitset build to sort
+    # every code: the same dictionary, sparse plan and counts
+    info = (sets.build_bitsets(), sets.sparse_info())
+    del sets
+    opts(pack_summary=0)
+    s0 = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
+    assert (s0.build_bitsets(), s0.sparse_info()) == info
+    I0, _ = s0.matrix((0, 200), (0, n), upper=False, method=gdist.METHOD_BITSET)
+    assert np.array_equal(I0, I[:200])
 
 
 def test_pack_after_bitset_workload_regression(ctx):

@@ -59,9 +59,22 @@ def test_golden_through_device(ctx, case):
 
 
 # ---------------------------------------------------------------- packing
+PACK_MODES = {"default": {}, "set_major": {"pack_summary": 0},
+              # chunks of ~1,000 windows: many chunk summaries, the upload of
+              # chunk c + 1 overlapped with chunk c (or not)
+              "chunked": {"pack_chunk": 1000}, "chunked_set_major": {"pack_chunk": 1000, "pack_summary": 0},
+              "chunked_no_overlap": {"pack_chunk": 1000, "pack_overlap": 0}}
+
+
+@pytest.mark.parametrize("mode", sorted(PACK_MODES))
 @pytest.mark.parametrize("seed", range(6))
-def test_pack_random_modes(ctx, seed):
+def test_pack_random_modes(ctx, opts, seed, mode):
+    """Codes and offsets against the oracle: the code-major pack sort that
+    keeps each chunk's dictionary summary (option pack_summary 1, the
+    default), the set-major one (0), and both over many small chunks whose
+    bytes upload while the previous chunk packs."""
     import gdist
+    opts(**PACK_MODES[mode])
     rng = random.Random(seed)
     for _ in range(12):
         kind = rng.choice([0, 1])
@@ -84,6 +97,25 @@ def test_pack_random_modes(ctx, seed):
         sets = gdist.KmerSets.from_sequences(seqs, k, kt, flags, ctx)
         off, codes = sets.download()
         assert np.array_equal(off, eo) and np.array_equal(codes, ec), (kind, k, flags)
+
+
+@pytest.mark.parametrize("mode", ["chunked", "chunked_set_major", "chunked_no_overlap"])
+def test_chunked_pack_bitset_matrix(ctx, opts, mode):
+    """A collection packed in ~20 chunks (chunk summaries merged for the
+    dictionary, uploads overlapped): codes, then the bitset matrix, equal the
+    oracle's."""
+    import gdist
+    opts(**PACK_MODES[mode])
+    opts(pack_chunk=40000)
+    seqs = synth_sets(120, 4000, 0.01, 77)
+    eo, ec = oracle_pack(seqs, 21, 0, 0)
+    sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
+    off, codes = sets.download()
+    assert np.array_equal(off, eo) and np.array_equal(codes, ec)
+    sets.build_bitsets()
+    I, D = sets.matrix(method=gdist.METHOD_BITSET)
+    eI, eD = oracle.matrix(eo, ec, 0, 120, 0, 120)
+    assert np.array_equal(I, eI) and bits_equal(D, eD)
 
 
 def test_pack_rejects_unencodable_and_bad_k(ctx):
@@ -615,7 +647,7 @@ def test_rare_tier_thresholds_exact(ctx, T, kernel, dedup, opts):
                                   "kernel_v5_atomic", "kernel_v6_rows", "kernel_v6_sun4", "kernel_v6_quads",
                                   "kernel_v6_2x2", "kernel_v6_2x2_rows", "kernel_v6_atomic", "absorb",
                                   "mixed_slabs", "mixed_slabs_atomic", "mixed_tiles", "unfused", "rare_kernel",
-                                  "unfused_rare_kernel", "fill_sort", "fill_direct", "pack_pairs", "kernel_v6_consec", "kernel_v6_consec_rows",
+                                  "unfused_rare_kernel", "fill_sort", "fill_direct", "pack_pairs", "pack_nosummary", "kernel_v6_consec", "kernel_v6_consec_rows",
                                   "kernel_v6_consec_sun4"])
 def test_sparse_complement_words_exact(ctx, mode, opts):
     """The dense tier in locus order with complement-sparse words: counts and
@@ -666,6 +698,8 @@ def test_sparse_complement_words_exact(ctx, mode, opts):
                 "fill_direct": {"fill_sort": 2},
                 # the pack's two (code, set) pair sorts instead of one sort of set|code keys
                 "pack_pairs": {"pack_sort": 1},
+                # the pack without chunk summaries: the bitset build sorts every code for its dictionary
+                "pack_nosummary": {"pack_summary": 0},
                 "many_chunks": {"sparse_zmax": 100000, "sparse_chunks": 37},
                 # words counted from either side (complement / positive), model's choice
                 # a dense-only dictionary: the substitution kmers two or more
