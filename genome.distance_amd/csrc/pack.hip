@@ -432,8 +432,10 @@ void exclusive_scan_i32_to_i64(gdist_ctx* ctx, const int32_t* in, int64_t* out, 
 // read-backs interleave with the upload.
 class ChunkUploader {
   public:
-    ChunkUploader(int device, const char* h, char* d, std::vector<std::pair<int64_t, int64_t>> ranges)
-        : ready_(ranges.size()) {
+    // pin: register each chunk's host range (page-locked, one DMA) instead of
+    // the runtime's staged pageable copies (option pack_overlap 2)
+    ChunkUploader(int device, const char* h, char* d, std::vector<std::pair<int64_t, int64_t>> ranges, bool pin)
+        : ready_(ranges.size()), pin_(pin) {
         for (auto& p : ready_) got_.push_back(p.get_future());
         th_ = std::thread([this, device, h, d, ranges] { run(device, h, d, ranges); });
     }
@@ -452,11 +454,22 @@ class ChunkUploader {
             GD_HIP(hipSetDevice(device));
             GD_HIP(hipStreamCreateWithFlags(&us, hipStreamNonBlocking));
             for (; c < ranges.size() && !stop_; c++) {
-                for (int64_t o = ranges[c].first; o < ranges[c].second; o += kPiece) {
-                    const size_t len = (size_t)std::min(kPiece, ranges[c].second - o);
-                    GD_HIP(hipMemcpyWithStream(d + o, h + o, len, hipMemcpyHostToDevice, us));
+                const int64_t b0 = ranges[c].first, b1 = ranges[c].second;
+                // chunks are registered one at a time: adjacent ranges share a page
+                bool reg = pin_ && b1 > b0 &&
+                           hipHostRegister(const_cast<char*>(h) + b0, (size_t)(b1 - b0), hipHostRegisterDefault) ==
+                               hipSuccess;
+                if (pin_ && !reg) (void)hipGetLastError();
+                if (reg) {
+                    GD_HIP(hipMemcpyAsync(d + b0, h + b0, (size_t)(b1 - b0), hipMemcpyHostToDevice, us));
+                } else {
+                    for (int64_t o = b0; o < b1; o += kPiece) {
+                        const size_t len = (size_t)std::min(kPiece, b1 - o);
+                        GD_HIP(hipMemcpyWithStream(d + o, h + o, len, hipMemcpyHostToDevice, us));
+                    }
                 }
                 GD_HIP(hipStreamSynchronize(us));
+                if (reg) GD_HIP(hipHostUnregister(const_cast<char*>(h) + b0));
                 ready_[c].set_value();
             }
         } catch (...) {
@@ -469,6 +482,7 @@ class ChunkUploader {
     }
     std::vector<std::promise<void>> ready_;
     std::vector<std::future<void>> got_;
+    bool pin_ = false;
     std::atomic<bool> stop_{false};
     std::thread th_;
 };
@@ -537,7 +551,7 @@ void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_se
         } else {
             std::vector<std::pair<int64_t, int64_t>> ranges;
             for (auto& c : chunks) ranges.push_back({h_seq_off[c.first], h_seq_off[c.second]});
-            up.reset(new ChunkUploader(ctx->device, h_seqs, dst, std::move(ranges)));
+            up.reset(new ChunkUploader(ctx->device, h_seqs, dst, std::move(ranges), ctx->option(OPT_PACK_OVERLAP, 1) == 2));
         }
     }
 

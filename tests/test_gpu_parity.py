@@ -63,7 +63,8 @@ PACK_MODES = {"default": {}, "set_major": {"pack_summary": 0},
               # chunks of ~1,000 windows: many chunk summaries, the upload of
               # chunk c + 1 overlapped with chunk c (or not)
               "chunked": {"pack_chunk": 1000}, "chunked_set_major": {"pack_chunk": 1000, "pack_summary": 0},
-              "chunked_no_overlap": {"pack_chunk": 1000, "pack_overlap": 0}}
+              "chunked_no_overlap": {"pack_chunk": 1000, "pack_overlap": 0},
+              "chunked_pinned": {"pack_chunk": 1000, "pack_overlap": 2}}
 
 
 @pytest.mark.parametrize("mode", sorted(PACK_MODES))
@@ -99,7 +100,7 @@ def test_pack_random_modes(ctx, opts, seed, mode):
         assert np.array_equal(off, eo) and np.array_equal(codes, ec), (kind, k, flags)
 
 
-@pytest.mark.parametrize("mode", ["chunked", "chunked_set_major", "chunked_no_overlap"])
+@pytest.mark.parametrize("mode", ["chunked", "chunked_set_major", "chunked_no_overlap", "chunked_pinned"])
 def test_chunked_pack_bitset_matrix(ctx, opts, mode):
     """A collection packed in ~20 chunks (chunk summaries merged for the
     dictionary, uploads overlapped): codes, then the bitset matrix, equal the
