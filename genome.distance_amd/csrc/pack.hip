@@ -424,8 +424,9 @@ void exclusive_scan_i32_to_i64(gdist_ctx* ctx, const int32_t* in, int64_t* out, 
 
 // Overlapped upload of host sequence bytes: a host thread copies each pack
 // chunk's byte range on its own stream in 64 MiB pieces (the runtime's
-// pageable path: ~25 GB/s on the box, ahead of our own pinned staging with a
-// CPU memcpy, measured 5-7 GB/s), synchronises, then signals the chunk; the
+// pageable path, ~6 GB/s on the box: faster than our own pinned staging with
+// a CPU memcpy and than registering the range, both measured),
+// synchronises, then signals the chunk; the
 // pack waits for chunk c's signal before its extraction, so chunk c + 1's
 // bytes move while chunk c sorts (chunk 0's wait is the part left on the
 // clock). Pieces, not one copy per chunk, so that the pack's own small
