@@ -395,7 +395,8 @@ def main():
             "end_to_end": {"pairs_per_s": round(pairs_all / e2e_s, 1), "seconds": round(e2e_s, 3),
                            "note": "one pass over the collection from FASTA bytes in host memory: pack (H2D + "
                                    "kmer extraction + sort) + represent (dictionary, bitsets, sparse words) + one "
-                                   "step; synthetic-genome generation excluded; max over ranks"},
+                                   "step; synthetic-genome generation and the release of the caller's host buffer "
+                                   "(setup_s.host_free) excluded; max over ranks"},
         }
         print(json.dumps(out), flush=True)
     if verified is not None and not verified["ok"]:
