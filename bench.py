@@ -78,7 +78,9 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
-    ap.add_argument("--n", type=int, default=0, help="override genome count (testing)")
+    ap.add_argument("--n", "--genomes", dest="n", type=int, default=0,
+                    help="override genome count (testing; --genomes under torch.distributed.run, whose own "
+                         "options make --n ambiguous)")
     ap.add_argument("--length", type=int, default=0, help="override genome length (testing)")
     ap.add_argument("--method", default="", choices=["", "auto", "bitset", "sorted"],
                     help="override the config's kernel family (experiments; the config's own is the bench line)")
