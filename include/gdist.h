@@ -150,7 +150,10 @@ int  gdist_memcpy_h2d(gdist_ctx* ctx, void* dst, const void* src, int64_t bytes)
 
 /* ---- kmer sets ------------------------------------------------------- */
 /* Build kmer sets of nseqs sequences on the device. seqs is the byte
- * concatenation, sequence s = seqs[seq_off[s] .. seq_off[s+1]). */
+ * concatenation, sequence s = seqs[seq_off[s] .. seq_off[s+1]). The call
+ * is synchronous; inside it a short-lived host thread of the library
+ * uploads the bytes of pack chunk c + 1 while chunk c is packed (option
+ * "pack_overlap"), so seqs is read until the call returns. */
 int  gdist_sets_pack(gdist_ctx* ctx, int kind, int k, unsigned flags,
                      const char* seqs, const int64_t* seq_off, int64_t nseqs,
                      gdist_sets** out);
