@@ -213,7 +213,7 @@ enum Opt : int {
     OPT_PACK_OVERLAP,       // 0: gdist_sets_pack uploads every sequence byte before packing (default 1: chunk
                             // c + 1 uploads from a host thread while chunk c packs; 2: the same from
                             // registered (page-locked) host ranges)
-    OPT_PACK_CHUNK,         // kmer windows per pack chunk (default 2^30; small values test the chunked paths)
+    OPT_PACK_CHUNK,         // kmer windows per pack chunk (default 2^28; small values test the chunked paths)
     OPT_COUNT
 };
 extern const char* const kOptNames[OPT_COUNT];

@@ -535,7 +535,7 @@ void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_se
         nwin[s] = std::max<int64_t>(0, len - k + 1);
     }
     // chunks of sequences, at most kChunk entries each (the first sequence of a chunk always fits)
-    const int64_t kChunk = std::max<int64_t>(1, ctx->option(OPT_PACK_CHUNK, int64_t(1) << 30));
+    const int64_t kChunk = std::max<int64_t>(1, ctx->option(OPT_PACK_CHUNK, int64_t(1) << 28));
     std::vector<std::pair<int64_t, int64_t>> chunks;   // [s0, s1)
     for (int64_t s0 = 0, s1; s0 < nseq; s0 = s1) {
         int64_t entries = 0;
