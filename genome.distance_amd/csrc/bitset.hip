@@ -348,15 +348,8 @@ constexpr int BT = 128;                 // tile edge (sets)
 // its own launches with RR accumulator rows (RR = 7 saves less than the two
 // launches cost: C2, 104 rows, 4.51 vs 4.27 ms)
 constexpr int kPartialMaxRR = 6;
-constexpr int KC = 16;                  // 64-bit words per staged chunk
-constexpr int ROWB = KC * 8;            // 128 B per set row in LDS
-constexpr int TILE_BYTES = BT * ROWB;   // 16 KiB per operand per chunk
+constexpr int KC = 16;                  // bitsets are padded to whole multiples of KC words
 constexpr int NT = 256;
-
-// LDS image: row g, logical 16-B slot q stored at slot q ^ ((g >> 1) & 7):
-// the 16 lanes of a ds_read_b128 group read 16 consecutive rows at one
-// logical slot and land on 16 distinct 4-bank groups.
-__device__ __forceinline__ int lds_off(int g, int q) { return g * ROWB + ((q ^ ((g >> 1) & 7)) << 4); }
 
 // v_bcnt_u32_b32 d, x, acc = popcount(x) + acc. Written as asm because hipcc
 // otherwise reassociates the sums into extra v_add3_u32 (10 VALU ops per
@@ -367,87 +360,8 @@ __device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc) {
     return r;
 }
 
-__device__ __forceinline__ uint32_t and_popc(uint4 a, uint4 b, uint32_t acc) {
-    acc = bcnt_acc(a.x & b.x, acc);
-    acc = bcnt_acc(a.y & b.y, acc);
-    acc = bcnt_acc(a.z & b.z, acc);
-    acc = bcnt_acc(a.w & b.w, acc);
-    return acc;
-}
-
-__global__ __launch_bounds__(NT, 2) void bitset_tile_kernel(
-    const unsigned long long* __restrict__ bits, int64_t W, const int2* __restrict__ tiles, int splits,
-    int64_t nchunks, int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I,
-    int64_t ldI) {
-    __shared__ __attribute__((aligned(16))) unsigned char lds[2 * TILE_BYTES];
-    unsigned char* ldsA = lds;
-    unsigned char* ldsB = lds + TILE_BYTES;
-
-    const int tile = blockIdx.x / splits;
-    const int split = blockIdx.x % splits;
-    const int2 t = tiles[tile];
-    if (t.x < 0 || t.y < 0) return;   // defensive: never address outside the region
-    const int64_t row0 = r0 + (int64_t)t.x * BT;
-    const int64_t col0 = c0 + (int64_t)t.y * BT;
-    const int64_t kc_per = ceil_div(nchunks, splits);
-    const int64_t kc0 = (int64_t)split * kc_per;
-    const int64_t kc1 = kc0 + kc_per < nchunks ? kc0 + kc_per : nchunks;
-
-    const int tid = threadIdx.x;
-    const int tx = tid & 15, ty = tid >> 4;
-
-    uint32_t acc[8][8];
-#pragma unroll
-    for (int r = 0; r < 8; r++)
-#pragma unroll
-        for (int c = 0; c < 8; c++) acc[r][c] = 0;
-
-    for (int64_t kc = kc0; kc < kc1; kc++) {
-        // stage: 128 rows × 8 slots of 16 B per operand = 1024 pieces, 4 per thread
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const int piece = tid + NT * q;
-            const int g = piece >> 3, slot = piece & 7;
-            const int64_t wofs = kc * KC + slot * 2;
-            const int64_t ra = row0 + g, cb = col0 + g;
-            uint4 va = make_uint4(0, 0, 0, 0), vb = make_uint4(0, 0, 0, 0);
-            if (ra < r1) va = *reinterpret_cast<const uint4*>(bits + ra * W + wofs);
-            if (cb < c1) vb = *reinterpret_cast<const uint4*>(bits + cb * W + wofs);
-            *reinterpret_cast<uint4*>(ldsA + lds_off(g, slot)) = va;
-            *reinterpret_cast<uint4*>(ldsB + lds_off(g, slot)) = vb;
-        }
-        __syncthreads();
-#pragma unroll 2
-        for (int q = 0; q < 8; q++) {
-            uint4 a[8];
-#pragma unroll
-            for (int r = 0; r < 8; r++) a[r] = *reinterpret_cast<const uint4*>(ldsA + lds_off(ty + 16 * r, q));
-#pragma unroll
-            for (int c = 0; c < 8; c++) {
-                const uint4 b = *reinterpret_cast<const uint4*>(ldsB + lds_off(tx + 16 * c, q));
-#pragma unroll
-                for (int r = 0; r < 8; r++) acc[r][c] = and_popc(a[r], b, acc[r][c]);
-            }
-        }
-        __syncthreads();
-    }
-
-    // exact integer reduction of the K-slices
-#pragma unroll
-    for (int r = 0; r < 8; r++) {
-        const int64_t i = row0 + ty + 16 * r;
-        if (i >= r1) continue;
-#pragma unroll
-        for (int c = 0; c < 8; c++) {
-            const int64_t j = col0 + tx + 16 * c;
-            if (j >= c1 || (upper && j <= i)) continue;
-            if (acc[r][c]) atomicAdd(I + (i - r0) * ldI + (j - c0), (int32_t)acc[r][c]);
-        }
-    }
-}
-
-// ---- v2: LDS-DMA double buffering, split-major XCD-aware order -------------
-// 256 threads, 128×128 tile, 8×8 counts per thread as in v1, but
+// ---- dense tiles: LDS-DMA double buffering, split-major XCD-aware order ----
+// 256 threads own a 128×128 tile, 8×8 counts per thread;
 //  * chunks of KC2 = 8 words are moved HBM/L2 -> LDS by global_load_lds_dwordx4
 //    (no register staging, so ≤ 128 VGPRs and 4 waves per SIMD), double
 //    buffered: chunk k+1 is in flight while chunk k is computed;
@@ -484,17 +398,15 @@ __device__ __forceinline__ void dma_chunk(const unsigned long long* __restrict__
     }
 }
 
-// ORDER 0: per column fragment, the 4 dwords of one pair back to back (a
-// dependent chain per accumulator). ORDER 1: two column fragments at once,
-// dword-outer, so consecutive v_and/v_bcnt pairs belong to 16 different
-// accumulators and no instruction waits on its predecessor.
 // One staged chunk (KC2 words of 128 row sets and 128 column sets) into the
-// thread's 8x8 accumulators. DIAG: the tile sits on the diagonal of an
+// thread's 8x8 accumulators, two column fragments at once, dword-outer, so
+// consecutive v_and/v_bcnt pairs belong to 16 different accumulators and no
+// instruction waits on its predecessor. DIAG: the tile sits on the diagonal of an
 // upper-triangle region, where accumulator (r, c) holds pairs with j > i only
 // when c >= r (rows ty + 16r, columns tx + 16c): the c < r ones (28 of 64) are
 // never computed. RR: only accumulator rows r < RR hold rows of the block (a
 // partial row tile at a block's end); the others are never computed.
-template <int ORDER, bool DIAG, int RR = 8>
+template <bool DIAG, int RR = 8>
 __device__ __forceinline__ void chunk_pairs(const unsigned char* A, const unsigned char* B, int ty, int tx,
                                             uint32_t (&acc)[8][8]) {
 #pragma unroll 1
@@ -502,29 +414,19 @@ __device__ __forceinline__ void chunk_pairs(const unsigned char* A, const unsign
         uint4 a[8];
 #pragma unroll
         for (int r = 0; r < RR; r++) a[r] = *reinterpret_cast<const uint4*>(A + lds_off2(ty + 16 * r, q));
-        if (ORDER == 0) {
 #pragma unroll
-            for (int c = 0; c < 8; c++) {
-                const uint4 bv = *reinterpret_cast<const uint4*>(B + lds_off2(tx + 16 * c, q));
+        for (int c = 0; c < 8; c += 2) {
+            const uint4 b0 = *reinterpret_cast<const uint4*>(B + lds_off2(tx + 16 * c, q));
+            const uint4 b1 = *reinterpret_cast<const uint4*>(B + lds_off2(tx + 16 * (c + 1), q));
+            const uint32_t bw0[4] = {b0.x, b0.y, b0.z, b0.w};
+            const uint32_t bw1[4] = {b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
-                for (int r = 0; r < RR; r++)
-                    if (!DIAG || c >= r) acc[r][c] = and_popc(a[r], bv, acc[r][c]);
-            }
-        } else {
+            for (int d = 0; d < 4; d++) {
 #pragma unroll
-            for (int c = 0; c < 8; c += 2) {
-                const uint4 b0 = *reinterpret_cast<const uint4*>(B + lds_off2(tx + 16 * c, q));
-                const uint4 b1 = *reinterpret_cast<const uint4*>(B + lds_off2(tx + 16 * (c + 1), q));
-                const uint32_t bw0[4] = {b0.x, b0.y, b0.z, b0.w};
-                const uint32_t bw1[4] = {b1.x, b1.y, b1.z, b1.w};
-#pragma unroll
-                for (int d = 0; d < 4; d++) {
-#pragma unroll
-                    for (int r = 0; r < RR; r++) {
-                        const uint32_t ad = d == 0 ? a[r].x : d == 1 ? a[r].y : d == 2 ? a[r].z : a[r].w;
-                        if (!DIAG || c >= r) acc[r][c] = bcnt_acc(ad & bw0[d], acc[r][c]);
-                        if (!DIAG || c + 1 >= r) acc[r][c + 1] = bcnt_acc(ad & bw1[d], acc[r][c + 1]);
-                    }
+                for (int r = 0; r < RR; r++) {
+                    const uint32_t ad = d == 0 ? a[r].x : d == 1 ? a[r].y : d == 2 ? a[r].z : a[r].w;
+                    if (!DIAG || c >= r) acc[r][c] = bcnt_acc(ad & bw0[d], acc[r][c]);
+                    if (!DIAG || c + 1 >= r) acc[r][c + 1] = bcnt_acc(ad & bw1[d], acc[r][c + 1]);
                 }
             }
         }
@@ -535,7 +437,7 @@ __device__ __forceinline__ void chunk_pairs(const unsigned char* A, const unsign
 // region (bitset_matrix launches those tiles separately). RR < 8: every tile
 // of the launch is the partial last row tile of the block, with at most 16 RR
 // rows (rows ty + 16r with r >= RR are past r1 for every thread).
-template <int ORDER, bool DIAG, int RR = 8>
+template <bool DIAG, int RR = 8>
 __global__ __launch_bounds__(NT, 4) void bitset_tile_kernel2(
     const unsigned long long* __restrict__ bits, int64_t W, const int2* __restrict__ tiles, int ntiles, int splits,
     int64_t nchunks, int64_t r0, int64_t r1, int64_t c0, int64_t c1, int64_t corg, int upper,
@@ -581,7 +483,7 @@ __global__ __launch_bounds__(NT, 4) void bitset_tile_kernel2(
         } else {
             asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
         }
-        chunk_pairs<ORDER, DIAG, RR>(A, B, ty, tx, acc);
+        chunk_pairs<DIAG, RR>(A, B, ty, tx, acc);
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // stage free for the next DMA
     }
 
@@ -1827,16 +1729,15 @@ void free_bitsets(gdist_sets* s) {
 static MatrixPlan& matrix_plan(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1,
                                bool upper) {
     hipStream_t st = ctx->stream;
-    const int64_t nr = r1 - r0, nc = c1 - c0;
+    const int64_t nr = r1 - r0;
     const int tr = (int)ceil_div(nr, BT);
     // dense tile operands: every word, or only the dense words when the
     // complement-sparse words run in their own kernel (sparse.hip)
     const int64_t tW = s->sparse ? s->Wd : s->W;
-    const int variant = (int)ctx->option(OPT_BITSET_KERNEL, 3);   // A/B selection
     // Diagonal tiles of an upper-triangle region (row0 == col0) get their
     // own launch of the DIAG variant, which skips the accumulators that
     // only hold pairs with j <= i (option bitset_diag = 0 keeps one launch).
-    const bool split_diag = variant != 1 && upper && ctx->option(OPT_BITSET_DIAG, 1) != 0;
+    const bool split_diag = upper && ctx->option(OPT_BITSET_DIAG, 1) != 0;
     // The last row tile of a block whose rows are not a multiple of BT
     // holds nlast rows: its tiles get launches instantiated for
     // RR = ceil(nlast / 16) accumulator rows, skipping the others' work.
@@ -1844,7 +1745,11 @@ static MatrixPlan& matrix_plan(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, 
     const int max_rr = (int)ctx->option(OPT_BITSET_PARTIAL_RR, kPartialMaxRR);
 
     // ---- the region's launch plan (built once, then reused)
-    const std::vector<int64_t> key{r0, r1, c0, c1, upper ? 1 : 0, variant, split_diag ? 1 : 0, max_rr, tW};
+    // the key holds every option the plan (and the sparse plan in it) reads,
+    // so that changing one builds a new plan instead of reusing a stale one
+    const std::vector<int64_t> key{r0, r1, c0, c1, upper ? 1 : 0, split_diag ? 1 : 0, max_rr, tW,
+                                   ctx->option(OPT_SPARSE_RARE, 1), ctx->option(OPT_SPARSE_CHUNKS, -1),
+                                   ctx->option(OPT_SPARSE_PART_BUDGET, -1), ctx->option(OPT_SPARSE_WG_PER_CU, -1)};
     auto it = s->plans.find(key);
     if (it == s->plans.end()) {
         if (s->plans.size() >= 8) {   // row-block loops: keep the cache small
@@ -1853,49 +1758,29 @@ static MatrixPlan& matrix_plan(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, 
         }
         auto plan = std::make_unique<MatrixPlan>();
         MatrixPlan& p = *plan;
-        if (variant == 1) {
-            const int tc = (int)ceil_div(nc, BT);
-            std::vector<int2> tiles;
-            for (int a = 0; a < tr; a++)
-                for (int b = 0; b < tc; b++) {
-                    // skip tiles holding no pair with j > i
-                    const int64_t rmin = r0 + (int64_t)a * BT;
-                    const int64_t cmax = std::min<int64_t>(c1, c0 + (int64_t)(b + 1) * BT) - 1;
-                    if (upper && cmax <= rmin) continue;
-                    tiles.push_back(make_int2(a, b));
-                }
-            p.ntiles = tiles.size();
-            // split the word dimension so the launch holds ≳ 8 workgroups per CU
-            const int64_t target = (int64_t)ctx->cus * 8;
-            p.splits = (int)std::max<int64_t>(
-                1, std::min<int64_t>(tW / KC, tiles.empty() ? 1 : ceil_div(target, (int64_t)tiles.size())));
-            p.tiles.alloc(tiles.size() * sizeof(int2) + 8, st);
-            if (!tiles.empty()) h2d(p.tiles.p, tiles.data(), tiles.size() * sizeof(int2), st);
-        } else {
-            // Upper-triangle regions tile their columns from an origin corg <= c0
-            // with corg = r0 (mod BT), so tiles lie exactly on the diagonal whatever
-            // r0 is (row-sharded ranks get exact equal-area row blocks); columns
-            // below c0 are loaded clamped and discarded. Diagonal tiles: col0 == row0.
-            p.corg = split_diag ? c0 - (((c0 - r0) % BT) + BT) % BT : c0;
-            const int64_t dlt_t = (r0 - p.corg) / BT;
-            const int64_t nlast = nr - (int64_t)(tr - 1) * BT;
-            p.rr = (int)ceil_div(nlast, 16);
-            p.part = p.rr <= max_rr;
-            std::vector<int2> grp[4];   // off-diagonal, diagonal, partial off-diagonal, partial diagonal
-            const int tc2 = (int)ceil_div(c1 - p.corg, BT);
-            for (int a = 0; a < tr; a++)
-                for (int b = 0; b < tc2; b++) {
-                    const int64_t rmin = r0 + (int64_t)a * BT;
-                    const int64_t cmax = std::min<int64_t>(c1, p.corg + (int64_t)(b + 1) * BT) - 1;
-                    if (cmax < c0 || (upper && cmax <= rmin)) continue;
-                    const int g = ((split_diag && (int64_t)b - a == dlt_t) ? 1 : 0) + ((p.part && a == tr - 1) ? 2 : 0);
-                    grp[g].push_back(make_int2(a, b));
-                }
-            for (int g = 0; g < 4; g++) p.at[g + 1] = p.at[g] + grp[g].size();
-            p.tiles.alloc(p.at[4] * sizeof(int2) + 8, st);
-            for (int g = 0; g < 4; g++)
-                if (!grp[g].empty()) h2d(p.tiles.as<int2>() + p.at[g], grp[g].data(), grp[g].size() * sizeof(int2), st);
-        }
+        // Upper-triangle regions tile their columns from an origin corg <= c0
+        // with corg = r0 (mod BT), so tiles lie exactly on the diagonal whatever
+        // r0 is (row-sharded ranks get exact equal-area row blocks); columns
+        // below c0 are loaded clamped and discarded. Diagonal tiles: col0 == row0.
+        p.corg = split_diag ? c0 - (((c0 - r0) % BT) + BT) % BT : c0;
+        const int64_t dlt_t = (r0 - p.corg) / BT;
+        const int64_t nlast = nr - (int64_t)(tr - 1) * BT;
+        p.rr = (int)ceil_div(nlast, 16);
+        p.part = p.rr <= max_rr;
+        std::vector<int2> grp[4];   // off-diagonal, diagonal, partial off-diagonal, partial diagonal
+        const int tc2 = (int)ceil_div(c1 - p.corg, BT);
+        for (int a = 0; a < tr; a++)
+            for (int b = 0; b < tc2; b++) {
+                const int64_t rmin = r0 + (int64_t)a * BT;
+                const int64_t cmax = std::min<int64_t>(c1, p.corg + (int64_t)(b + 1) * BT) - 1;
+                if (cmax < c0 || (upper && cmax <= rmin)) continue;
+                const int g = ((split_diag && (int64_t)b - a == dlt_t) ? 1 : 0) + ((p.part && a == tr - 1) ? 2 : 0);
+                grp[g].push_back(make_int2(a, b));
+            }
+        for (int g = 0; g < 4; g++) p.at[g + 1] = p.at[g] + grp[g].size();
+        p.tiles.alloc(p.at[4] * sizeof(int2) + 8, st);
+        for (int g = 0; g < 4; g++)
+            if (!grp[g].empty()) h2d(p.tiles.as<int2>() + p.at[g], grp[g].data(), grp[g].size() * sizeof(int2), st);
         it = s->plans.emplace(key, std::move(plan)).first;
     }
     return *it->second;
@@ -1908,11 +1793,8 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     if (nr <= 0 || nc <= 0) return;
     const unsigned long long* tbits = s->sparse ? s->dbits.as<unsigned long long>() : s->bits.as<unsigned long long>();
     const int64_t tW = s->sparse ? s->Wd : s->W;
-    const int variant = (int)ctx->option(OPT_BITSET_KERNEL, 3);   // A/B selection
-    const bool split_diag = variant != 1 && upper && ctx->option(OPT_BITSET_DIAG, 1) != 0;
-    (void)split_diag;
     MatrixPlan& p = matrix_plan(ctx, s, r0, r1, c0, c1, upper);
-    if (variant == 1 ? p.ntiles == 0 : p.at[4] == 0) return;   // no pair in the region
+    if (p.at[4] == 0) return;   // no pair in the region
 
     // Rare kernel per call from the cost model (rare_choice): list-major opens
     // every list and walks the pairs from this block's rows with global
@@ -1948,11 +1830,6 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     }
     if (tW == 0 || (s->sparse && s->sp_fold_dense)) {
         // no dense words, or so few that the sparse flush counts them
-    } else if (variant == 1) {
-        const int64_t grid = (int64_t)p.ntiles * p.splits;
-        GD_REQUIRE(grid < (int64_t(1) << 31), "bitset matrix grid too large");
-        bitset_tile_kernel<<<(unsigned)grid, NT, 0, st>>>(tbits, tW, p.tiles.as<int2>(), p.splits, tW / KC, r0, r1, c0,
-                                                           c1, upper ? 1 : 0, d_I, ldI);
     } else {
         const int64_t nch2 = tW / KC2;
         // workgroups per CU the K-split aims for (GDIST_BITSET_WG_PER_CU, A/B)
@@ -1974,26 +1851,21 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
         };
         const int2* dg = p.tiles.as<int2>();
         const size_t* at = p.at;
-        if (variant == 2) {   // A/B: ORDER 0, full-height tiles throughout
-            launch(bitset_tile_kernel2<0, false>, dg, at[1]);
-            launch(bitset_tile_kernel2<0, true>, dg + at[1], at[2] - at[1]);
-            launch(bitset_tile_kernel2<0, false>, dg + at[2], at[3] - at[2]);
-            launch(bitset_tile_kernel2<0, true>, dg + at[3], at[4] - at[3]);
-        } else {
-            launch(bitset_tile_kernel2<1, false>, dg, at[1]);
-            launch(bitset_tile_kernel2<1, true>, dg + at[1], at[2] - at[1]);
+        {
+            launch(bitset_tile_kernel2<false>, dg, at[1]);
+            launch(bitset_tile_kernel2<true>, dg + at[1], at[2] - at[1]);
             auto partial = [&](auto off_k, auto diag_k) {
                 launch(off_k, dg + at[2], at[3] - at[2]);
                 launch(diag_k, dg + at[3], at[4] - at[3]);
             };
             switch (p.part ? p.rr : 8) {
-                case 1: partial(bitset_tile_kernel2<1, false, 1>, bitset_tile_kernel2<1, true, 1>); break;
-                case 2: partial(bitset_tile_kernel2<1, false, 2>, bitset_tile_kernel2<1, true, 2>); break;
-                case 3: partial(bitset_tile_kernel2<1, false, 3>, bitset_tile_kernel2<1, true, 3>); break;
-                case 4: partial(bitset_tile_kernel2<1, false, 4>, bitset_tile_kernel2<1, true, 4>); break;
-                case 5: partial(bitset_tile_kernel2<1, false, 5>, bitset_tile_kernel2<1, true, 5>); break;
-                case 6: partial(bitset_tile_kernel2<1, false, 6>, bitset_tile_kernel2<1, true, 6>); break;
-                case 7: partial(bitset_tile_kernel2<1, false, 7>, bitset_tile_kernel2<1, true, 7>); break;
+                case 1: partial(bitset_tile_kernel2<false, 1>, bitset_tile_kernel2<true, 1>); break;
+                case 2: partial(bitset_tile_kernel2<false, 2>, bitset_tile_kernel2<true, 2>); break;
+                case 3: partial(bitset_tile_kernel2<false, 3>, bitset_tile_kernel2<true, 3>); break;
+                case 4: partial(bitset_tile_kernel2<false, 4>, bitset_tile_kernel2<true, 4>); break;
+                case 5: partial(bitset_tile_kernel2<false, 5>, bitset_tile_kernel2<true, 5>); break;
+                case 6: partial(bitset_tile_kernel2<false, 6>, bitset_tile_kernel2<true, 6>); break;
+                case 7: partial(bitset_tile_kernel2<false, 7>, bitset_tile_kernel2<true, 7>); break;
                 default: break;   // no partial row tile
             }
         }

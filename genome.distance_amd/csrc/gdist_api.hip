@@ -20,13 +20,9 @@
 namespace gdist {
 
 const char* const kOptNames[OPT_COUNT] = {
-    "trace",           "rare_t",          "rare_dedup",      "rare_kernel",     "rare_overlap",
-    "bitset_kernel",   "bitset_diag",     "bitset_partial_rr", "bitset_wg_per_cu", "bitset_min_chunks",
-    "reps_block",      "locus_order",     "sparse",          "sparse_zmax",     "sparse_wg_per_cu",
-    "sparse_occ",      "sparse_sun",      "sketch_k",        "sketch_tile",     "sparse_part_budget",
-    "guides",          "force_exchange",  "sparse_kernel",   "sparse_chunks",   "fold_dense_words", "sparse_abl",      "graph",
-    "sparse_shape",    "sparse_absorb",   "sparse_balance",  "time_sparse",     "sparse_xcd",      "step_timing",     "sparse_rare",     "sparse_fused",
-    "sparse_fold",     "fill_sort",       "sparse_tile_order", "pack_sort",       "pack_summary",    "pack_overlap",    "pack_chunk",
+#define GDIST_OPT_NAME(id, name) name,
+    GDIST_OPTIONS(GDIST_OPT_NAME)
+#undef GDIST_OPT_NAME
 };
 
 static int option_index(const char* name) {
@@ -175,7 +171,7 @@ static void settle_timing(gdist_ctx* ctx) {
     float ms = 0.f;
     GD_HIP(hipEventElapsedTime(&ms, ctx->ev_call0, ctx->ev_call1));
     ctx->last.call_ms = ms;
-    ctx->last.kernel_ms = 0.0;
+    ctx->last.kernel_ms = __builtin_nan("");
     if (ctx->last_kernel) {
         float km = 0.f;
         GD_HIP(hipEventElapsedTime(&km, ctx->ev_k0, ctx->ev_k1));
@@ -297,6 +293,7 @@ int gdist_ctx_get_option(gdist_ctx* ctx, const char* name, int64_t* value, int* 
     return guard([&] {
         GD_REQUIRE(ctx && value, "null argument");
         const int i = option_index(name);
+        std::lock_guard<std::recursive_mutex> lk(ctx->mu);      // set_option writes under the lock
         *value = ctx->opt[i] == kOptUnset ? GDIST_OPTION_DEFAULT : ctx->opt[i];
         if (is_set) *is_set = ctx->opt[i] != kOptUnset;
     });

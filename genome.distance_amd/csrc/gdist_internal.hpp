@@ -144,10 +144,8 @@ struct StepGraph {
     ~StepGraph() { if (exec) (void)hipGraphExecDestroy(exec); }
 };
 struct MatrixPlan {
-    DevBuf tiles;                    // v1: the tile list; v2/v3: the four launch groups
-    size_t at[5] = {0, 0, 0, 0, 0};  // group bounds (v2/v3)
-    size_t ntiles = 0;               // v1
-    int splits = 1;                  // v1 K-split
+    DevBuf tiles;                    // the four launch groups' tiles
+    size_t at[5] = {0, 0, 0, 0, 0};  // group bounds
     int64_t corg = 0;
     int rr = 8;
     bool part = false;
@@ -155,8 +153,10 @@ struct MatrixPlan {
 };
 
 // ---------------------------------------------------------------------------
+// NaN: the call recorded no timing events (a graph-replayed step without
+// option step_timing, or no kernel time of its own)
 struct Timing {
-    double kernel_ms = 0.0, call_ms = 0.0;
+    double kernel_ms = __builtin_nan(""), call_ms = __builtin_nan("");
     int64_t launches = 0;
 };
 
@@ -165,55 +165,47 @@ struct Timing {
 // never reads the environment: a JNI host whose environment differs gets the
 // same kernels as the tests, and callers that share a context
 // (MethodTableProcessor.java:275, concurrent getDistance) share its options.
+// Every option preserves results: each only picks among exact kernels,
+// tilings, thresholds or setup paths, and the parity tests run each non-default
+// value against the oracle (tests/test_gpu_parity.py, test_gpu_options.py).
+#define GDIST_OPTIONS(X)                                                                                       \
+    X(TRACE, "trace")                         /* 1: setup stage timings and plans on stderr */                 \
+    X(RARE_T, "rare_t")                       /* rare-tier threshold T (default: histogram cost model) */      \
+    X(RARE_DEDUP, "rare_dedup")               /* 0: one posting list per rare kmer */                          \
+    X(RARE_KERNEL, "rare_kernel")             /* 0 list-major / 1 row-major (default: cost model per call) */  \
+    X(RARE_OVERLAP, "rare_overlap")           /* 0: list-major rare kernel in line */                          \
+    X(BITSET_DIAG, "bitset_diag")             /* 0: no separate trimmed launch for diagonal tiles */           \
+    X(BITSET_PARTIAL_RR, "bitset_partial_rr") /* largest RR whose partial row tile gets its own launches */    \
+    X(BITSET_WG_PER_CU, "bitset_wg_per_cu")   /* K-split target (default 16) */                                \
+    X(BITSET_MIN_CHUNKS, "bitset_min_chunks") /* fewest 8-word chunks per K-split workgroup (default 16) */     \
+    X(REPS_BLOCK, "reps_block")               /* greedy-reps row block (default: by memory) */                 \
+    X(LOCUS_ORDER, "locus_order")             /* 0: dense ranks in code order */                               \
+    X(SPARSE, "sparse")                       /* 0: no sparse words */                                         \
+    X(SPARSE_ZMAX, "sparse_zmax")             /* words with z_w <= ZMAX are sparse (forces the split) */       \
+    X(SPARSE_WG_PER_CU, "sparse_wg_per_cu")   /* chunking target of the sparse tiles (default 4) */            \
+    X(SPARSE_SUN, "sparse_sun")               /* slots per lane in flight: 2 / 3 / 4 (default 3) */            \
+    X(SKETCH_K, "sketch_k")                   /* sketch merge window (1 / 2 / 4 / 6, default 2) */             \
+    X(SKETCH_TILE, "sketch_tile")             /* 16: force the 16x16 sketch tile */                            \
+    X(SPARSE_PART_BUDGET, "sparse_part_budget") /* bytes of sparse chunk partials one region may hold */       \
+    X(GUIDES, "guides")                       /* guide sequences keyed at pack time (default kGuides) */       \
+    X(FORCE_EXCHANGE, "force_exchange")       /* 1: a one-rank communicator runs every collective (tests) */   \
+    X(SPARSE_CHUNKS, "sparse_chunks")         /* chunks of the sparse words per tile (tests) */                \
+    X(GRAPH, "graph")                         /* 0: no hipGraph replay of repeated matrix calls */             \
+    X(TIME_SPARSE, "time_sparse")             /* 1: HIP events around the sparse tile kernel (no replay) */    \
+    X(STEP_TIMING, "step_timing")             /* 1: graph-replayed steps record timing events too */           \
+    X(SPARSE_RARE, "sparse_rare")             /* 0: the rare pairs by the rare kernel, not the chunk reduce */ \
+    X(SPARSE_FUSED, "sparse_fused")           /* 0: zeroing, rare kernel and epilogue as their own launches */ \
+    X(SPARSE_FOLD, "sparse_fold")             /* most (padded) dense words counted in the sparse tile kernel */\
+    X(FILL_SORT, "fill_sort")                 /* bitset fill: 0 positions + LDS slices, 1 sort, 2 atomics */   \
+    X(PACK_SORT, "pack_sort")                 /* 1: two (code, set) pair sorts instead of packed keys */       \
+    X(PACK_SUMMARY, "pack_summary")           /* 0: set|code pack keys, the bitset build re-sorts codes */     \
+    X(PACK_OVERLAP, "pack_overlap")           /* 0: upload first / 1: overlapped host thread / 2: registered */\
+    X(PACK_CHUNK, "pack_chunk")               /* kmer windows per pack chunk (default 2^28) */
+
 enum Opt : int {
-    OPT_TRACE = 0,          // 1: setup stage timings on stderr
-    OPT_RARE_T,             // rare-tier threshold T (default: histogram cost model)
-    OPT_RARE_DEDUP,         // 0: one posting list per rare kmer
-    OPT_RARE_KERNEL,        // 0 list-major / 1 row-major (default: cost model per call)
-    OPT_RARE_OVERLAP,       // 0: list-major rare kernel in line
-    OPT_BITSET_KERNEL,      // tile kernel 1 / 2 / 3 (default 3)
-    OPT_BITSET_DIAG,        // 0: no separate trimmed launch for diagonal tiles
-    OPT_BITSET_PARTIAL_RR,  // largest RR whose partial row tile gets its own launches
-    OPT_BITSET_WG_PER_CU,   // K-split target (default 16)
-    OPT_BITSET_MIN_CHUNKS,  // fewest 8-word chunks per K-split workgroup (default 16)
-    OPT_REPS_BLOCK,         // greedy-reps row block (default: by memory)
-    OPT_LOCUS_ORDER,        // 0: dense ranks in code order
-    OPT_SPARSE,             // 0: no complement-sparse words
-    OPT_SPARSE_ZMAX,        // words with z_w <= ZMAX are sparse (forces the split)
-    OPT_SPARSE_WG_PER_CU,   // chunking target of the sparse tiles (default 4)
-    OPT_SPARSE_OCC,         // 3: sparse kernel built for 3 instead of 8 waves per SIMD
-    OPT_SPARSE_SUN,         // product slots per lane in flight (v1: 4 / 6 / 8, default 6; v5: 4 / 6; v6: 2 / 3 / 4, default 3)
-    OPT_SKETCH_K,           // sketch merge window (1 / 2 / 4 / 6, default 2)
-    OPT_SKETCH_TILE,        // 16: force the 16x16 sketch tile
-    OPT_SPARSE_PART_BUDGET, // bytes of sparse chunk partials one region may hold
-    OPT_GUIDES,             // guide sequences keyed at pack time (default kGuides)
-    OPT_FORCE_EXCHANGE,     // 1: a one-rank communicator runs every collective (tests)
-    OPT_SPARSE_KERNEL,      // sparse tile kernel 1 (word + byte loads) / 2 (LDS-staged) / 3 (16-byte records) /
-                            // 4 (LDS grid) / 5 (v1 walk re-laid) / 6 (micro-tiles, default)
-    OPT_SPARSE_CHUNKS,      // chunks of the sparse words per tile (tests; default: parallelism and memory)
-    OPT_FOLD_DENSE_WORDS,   // at most this many (padded) dense words are folded into the sparse flush
-    OPT_SPARSE_ABL,         // timing ablations of the sparse kernel v2 (results wrong; never in tests)
-    OPT_GRAPH,              // 0: no hipGraph replay of repeated matrix calls
-    OPT_SPARSE_SHAPE,       // v6 micro-tile rows x columns: 12 (default) / 14 / 22
-    OPT_SPARSE_ABSORB,      // 1: every word sparse (no dense-word launch; default 0)
-    OPT_SPARSE_BALANCE,     // 1: chunk bounds at equal modelled cost, words dealt to waves one at a time
-    OPT_TIME_SPARSE,        // 1: HIP events around the sparse tile kernel (no hipGraph replay; bench roofline)
-    OPT_SPARSE_XCD,         // 1: chunk c of every tile on XCD c mod 8 (default 0: tile-major order; A/B lost)
-    OPT_STEP_TIMING,        // 1: graph-replayed steps record timing events too (default 0: they cost 13-18 us a step)
-    OPT_SPARSE_RARE,        // 0: the rare tier's pairs by the rare kernel, not the sparse chunk reduce
-    OPT_SPARSE_FUSED,       // 0: no fused reduce + epilogue (zeroing, rare kernel, epilogue launched apart)
-    OPT_SPARSE_FOLD,        // at most this many (padded) dense words counted inside the v5 / v6 tile kernel
-                            // (8 per chunk; default 64, 0: the dense-word tile launch)
-    OPT_FILL_SORT,          // bitset fill: 0 merged positions + LDS row slices (default), 1 (code, set) sort +
-                            // run ranks, 2 one-pass windowed searches with global atomics
-    OPT_SPARSE_TILE_ORDER,  // 1: sparse tiles heaviest first (default 0: row-major order; C2 neutral)
-    OPT_PACK_SORT,          // 1: pack sorts (code, set) pairs twice (default 0: one sort of packed set|code keys when they fit 64 bits)
-    OPT_PACK_SUMMARY,       // 0: pack sorts set|code keys and the bitset build re-sorts every code for the
-                            // dictionary summary (default 1: code|set keys, the chunk summaries kept from the pack)
-    OPT_PACK_OVERLAP,       // 0: gdist_sets_pack uploads every sequence byte before packing (default 1: chunk
-                            // c + 1 uploads from a host thread while chunk c packs; 2: the same from
-                            // registered (page-locked) host ranges)
-    OPT_PACK_CHUNK,         // kmer windows per pack chunk (default 2^28; small values test the chunked paths)
+#define GDIST_OPT_ENUM(id, name) OPT_##id,
+    GDIST_OPTIONS(GDIST_OPT_ENUM)
+#undef GDIST_OPT_ENUM
     OPT_COUNT
 };
 extern const char* const kOptNames[OPT_COUNT];
@@ -335,19 +327,13 @@ struct gdist_sets {
     int64_t Wd = 0;                       // dense words, padded to 16 (0: none)
     int64_t Ws = 0;                       // sparse words
     gdist::DevBuf sp_off;                 // int64 [ceil(nsets/128) * Ws + 1]: (set block, sparse word) -> entries
-    gdist::DevBuf sp_word;                // uint64 [sp_entries]: complement word ~bits & valid
-    gdist::DevBuf sp_set;                 // uint8 [sp_entries]: set - 128 * block
-    gdist::DevBuf sp_ent;                 // {word, set} 16-byte records [sp_entries] (v3 tile kernel)
+    gdist::DevBuf sp_ent;                 // 16-byte records {row code, word, column code} [sp_entries + 4]
     gdist::DevBuf sp_nc;                  // int32 [nsets]: complement bits over the sparse words
     int64_t sp_entries = 0, sp_U = 0;     // entries; valid bits of the sparse words
-    int sp_win = 0;                       // v2 kernel window (aligned sparse words), 0: v1 only
     int64_t sp_pos_words = 0;             // sparse words counted from their set bits (positive-sparse)
-    bool sp_fold_dense = false;           // the dense words are counted by the sparse kernels (no tile launch):
-    int sp_fold_slabs = 0;                // ... in the tile kernel (v5 / v6), 8 words per chunk, when > 0;
-                                          // else in the flush / reduce (option fold_dense_words, sp_dT)
-    gdist::DevBuf sp_dT;                  // uint64 [Wd][nsets]: the dense words word-major, for the fold
+    bool sp_fold_dense = false;           // the dense words are counted by the sparse tile kernel (no tile launch),
+    int sp_fold_slabs = 0;                // 8 words per chunk in the first sp_fold_slabs chunks
     std::vector<int32_t> sp_bucket_bits;  // [nsets][sp_nbk]: complement bits per set and 1024 sparse words
-    std::vector<double> sp_cost;          // [Ws + 1]: prefix of each sparse word's modelled cost over all tiles
     int64_t sp_nbk = 0;
     // summaries of the pack chunks (option pack_summary): the code-major pack
     // sort leaves each chunk's codes in code order, so their runs are that
@@ -472,13 +458,8 @@ bool bitset_matrix_fused(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_
 constexpr int kGuides = 8;                       // guide sequences per packed collection (C2-realistic, 8
                                                  // clades: 2 -> 8 guides took the step 4.60 -> 3.25 ms; C2 and
                                                  // pack time unchanged, profiles/r02/realistic/guides.txt)
-constexpr int kSparseStageEntries = 640;         // sparse v2: entries per side a window may hold
-constexpr int kFoldDenseWords = 0;               // dense words folded into the sparse flush: off (the
-                                                 // tile launch overlaps the sparse kernel; the fold runs after it)
 constexpr double kSparseProductsPerS = 6.5e11;   // sparse tiles (v6): complement-word products (C2)
 constexpr double kSparseItemsPerS = 1.0e11;      // sparse tiles (v6): (tile, sparse word) visits (C2)
-constexpr double kDenseLaunchFixedS = 6.0e-5;    // a dense-word tile launch beside the sparse kernel (C2: 64 words
-                                                 // 0.09 + 0.04 ms of tiles sharing the CUs with the sparse kernel)
 bool locus_order_enabled(const gdist_ctx* ctx);  // option locus_order = 0 keeps code order (A/B)
 // key[r] = tag | guide position of dense rank r; kmers no guide holds sort
 // after every guide key by the number of sets holding them (dcounts)

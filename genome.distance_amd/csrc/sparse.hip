@@ -228,579 +228,48 @@ __global__ void sparse_records_kernel(const unsigned long long* __restrict__ wor
 // One workgroup per (128 x 128 tile of absolute set blocks (A, B), chunk of
 // the sparse words). Each wave takes 64 sparse words at a time: lane l loads
 // the (A, s) and (B, s) entry ranges of word s = base + l, the wave
-// prefix-sums their products r_s x c_s, and the 64 lanes then walk the
-// flattened products (word found by binary search over the prefix in LDS),
-// four per lane at a time so their loads overlap, adding popc(c_i & c_j) to
-// LDS counters. A diagonal tile (A == B) walks each word's pairs x < y of its
-// one entry list (and mirrors them when the region is not an upper triangle).
-// With one chunk per tile the counters go to I directly (atomics: the dense
-// tiles add into I concurrently), with the constant part U_s - nc_i - nc_j;
-// with several, each chunk stores its counters to `part` and
-// sparse_reduce_kernel sums them.
+// prefix-sums the word's product slots, parks the walk fields in LDS, and the
+// 64 lanes then walk the flattened slots, SUN per lane in flight so their
+// loads overlap, adding popc(c_i & c_j) to LDS counters. A diagonal tile
+// (A == B) walks each word's pairs x < y of its one entry list (mirrored
+// when the region is not an upper triangle). With one chunk per tile the
+// counters go to I directly (atomics) with the constant part
+// U_s - nc_i - nc_j; with several, each chunk stores its counters to `part`
+// and sparse_reduce_kernel sums them.
+//
+// The instruction stream per slot (round-2 ISA work):
+//   * diagonal and off-diagonal tiles run separate instantiations of the
+//     walk (one uniform branch per batch);
+//   * a word's walk fields are one 16-byte LDS record {first slot | ncol << 24,
+//     row start, column start, 1 / (2 ncp)}: one ds_read_b128 per slot;
+//   * an off-diagonal slot is a 1 x 2 micro-tile: one row entry and a PAIR of
+//     adjacent column entries of one word, so one search and one quotient
+//     serve two products (an odd list's last pair reads the next record and
+//     adds 0); the quotient is exact without a correction step;
+//   * an entry is one 16-byte record {row code, word, column code}: a row
+//     loads its first 12 bytes, a column its last 12 (global_load_dwordx3);
+//   * the counter add is unconditional (a zero product adds 0), so no slot
+//     waits on another's branch; idle slots read the zero sentinel record
+//     past the last entry instead of being masked.
 constexpr int SNT = 512;                 // threads per workgroup (4 per CU, LDS-limited: 8 waves per SIMD)
 // Counters are 16-bit, two to an LDS dword: a chunk holds at most kChunkWords
 // sparse words, so a pair's count in one chunk is at most 64 x 1023 < 2^16
 // and a packed ds_add_u32 never carries into the neighbour (32 KiB per tile)
 constexpr int kChunkWords = 1023;
-// dense words per in-kernel fold slab (v5 / v6): a pair gains at most
-// 64 x 8 in the chunk that folds a slab, so such chunks hold at most
-// kChunkWords - kFoldSlabWords sparse words
+// dense words per in-kernel fold slab: a pair gains at most 64 x 8 in the
+// chunk that folds a slab, so such chunks hold at most kChunkWords -
+// kFoldSlabWords sparse words
 constexpr int kFoldSlabWords = 8;
 constexpr int SNW = SNT / 64;
 
-
-// The dense words folded into the flush (a few words): their
-// AND+popcount for one pair, from the dense words stored word-major
-// [Wdp][N] (consecutive threads hold consecutive columns j: coalesced;
-// the row i is shared by the workgroup's threads; L2-resident)
-__device__ __forceinline__ int dense_pair(const unsigned long long* __restrict__ dT, int64_t Wdp, int64_t N,
-                                          int64_t i, int64_t j) {
-    int v = 0;
-    if (dT)
-        for (int64_t d = 0; d < Wdp; d++) v += __popcll(dT[d * N + i] & dT[d * N + j]);
-    return v;
-}
-
-__global__ void transpose_words_kernel(const unsigned long long* __restrict__ dbits, int64_t N, int64_t Wdp,
-                                       unsigned long long* __restrict__ dT) {
-    const int64_t n = N * Wdp;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
-        const int64_t d = e / N, i = e - d * N;
-        dT[e] = dbits[i * Wdp + d];
-    }
-}
-
-
-// SUN products per lane in flight, OCC workgroups per CU. E16: the entries
-// are read as 16-byte {complement word, set} records (one load per side and
-// product instead of a word load and a byte load)
-template <int SUN, int OCC, bool E16 = false>
-__global__ __launch_bounds__(SNT, OCC) void sparse_tile_kernel(
-    const int64_t* __restrict__ off, const unsigned long long* __restrict__ word, const uint8_t* __restrict__ set,
-    const ulonglong2* __restrict__ ent,
-    const int32_t* __restrict__ nc, int64_t Us, int64_t Ws, const int2* __restrict__ tiles, const int32_t* __restrict__ cbnd, int nchunks,
-    int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I, int64_t ldI,
-    int32_t* __restrict__ part, const unsigned long long* __restrict__ dbits, int64_t Wdp, int64_t N) {
-    __shared__ uint32_t cnt[SB * SB / 2];                                  // 32 KiB, 16-bit counters
-    __shared__ int32_t pre[SNW][64];                    // first product of each word of the batch
-    __shared__ int32_t rbeg[SNW][64], cbeg[SNW][64];   // relative to the chunk's first entries
-    __shared__ uint8_t ncol[SNW][64];
-    const int tile = blockIdx.x / nchunks, ch = blockIdx.x % nchunks;
-    const int64_t A = tiles[tile].x, B = tiles[tile].y;
-    // rows of block A inside the region: a tile on a row-block edge (a rank's
-    // first or last rows) walks only those entries of each word's row list
-    const int rlo = (int)(r0 - A * SB > 0 ? r0 - A * SB : 0);
-    const int rhi = (int)(r1 - A * SB < SB ? r1 - A * SB : SB);
-    const bool rpart = rlo > 0 || rhi < SB;
-    // a whole diagonal tile walks each word's pairs x < y of its one list
-    const bool diag = A == B && !rpart, mirror = diag && !upper;
-    for (int t = threadIdx.x; t < SB * SB / 2; t += SNT) cnt[t] = 0;
-    __syncthreads();
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t sb = cbnd[ch], se = cbnd[ch + 1];          // the chunk's sparse words
-    const int64_t* offA = off + A * Ws;
-    const int64_t* offB = off + B * Ws;
-    const int64_t ra0 = offA[sb], cb0 = offB[sb];           // chunk bases (< 2^31 entries per chunk)
-    // the chunk's entries from its bases: 32-bit lane offsets on scalar bases
-    const unsigned long long* wA = word + ra0;
-    const unsigned long long* wB = word + cb0;
-    const uint8_t* sA = set + ra0;
-    const uint8_t* sB = set + cb0;
-    const ulonglong2* eA = ent + ra0;
-    const ulonglong2* eB = ent + cb0;
-    for (int64_t base = sb + (int64_t)wv * 64; base < se; base += (int64_t)SNW * 64) {
-        const int64_t s = base + lane;
-        int64_t rb = ra0, cb = cb0;
-        int nr = 0, ncl = 0;
-        if (s < se) {
-            rb = offA[s]; nr = (int)(offA[s + 1] - rb);
-            cb = offB[s]; ncl = (int)(offB[s + 1] - cb);
-            if (rpart) {                               // lists are sorted by set: trim both ends
-                int a = 0, e = nr;
-                for (int t = 0; t < nr; t++) {
-                    const int st = set[rb + t];
-                    a += st < rlo;
-                    e -= st >= rhi;
-                }
-                rb += a;
-                nr = e > a ? e - a : 0;
-            }
-        }
-        const int P = diag ? nr * (nr - 1) / 2 : nr * ncl;
-        int incl = P;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int v = __shfl_up(incl, o, 64);
-            if (lane >= o) incl += v;
-        }
-        pre[wv][lane] = incl - P;
-        rbeg[wv][lane] = (int32_t)(rb - ra0);
-        cbeg[wv][lane] = (int32_t)(cb - cb0);
-        ncol[wv][lane] = (uint8_t)ncl;
-        const int total = __shfl(incl, 63, 64);
-        __builtin_amdgcn_wave_barrier();
-        for (int fb = 0; fb < total; fb += 64 * SUN) {
-            int32_t ri[SUN], ci[SUN];
-            bool ok[SUN];
-#pragma unroll
-            for (int u = 0; u < SUN; u++) {
-                const int F = fb + 64 * u, f = F + lane;
-                ok[u] = f < total;
-                // the word holding product f: #{l : incl_l <= f}; incl ascends
-                // with l, so the words ending before F are a ballot prefix and
-                // the few ending inside [F, F + 63] are read from their lanes
-                const int w0 = __popcll(__ballot(incl <= F));
-                const int w1 = __popcll(__ballot(incl <= F + 63));
-                int lo = w0;
-                for (int l = w0; l < w1; l++) lo += __builtin_amdgcn_readlane(incl, l) <= f;
-                lo = lo < 63 ? lo : 63;
-                const int q = f - pre[wv][lo];
-                int x, y;
-                int32_t rr, cc;
-                if (diag) {                            // q -> pair (y, x), y < x: q = x(x-1)/2 + y
-                    x = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)q)) * 0.5f);
-                    if (x * (x - 1) / 2 > q) x--;
-                    else if ((x + 1) * x / 2 <= q) x++;
-                    y = q - x * (x - 1) / 2;
-                    rr = rbeg[wv][lo] + y;
-                    cc = rbeg[wv][lo] + x;
-                } else {
-                    const int n2 = ncol[wv][lo];
-                    x = (int)((float)q * __builtin_amdgcn_rcpf((float)n2));
-                    if (x * n2 > q) x--;
-                    else if ((x + 1) * n2 <= q) x++;
-                    y = q - x * n2;
-                    rr = rbeg[wv][lo] + x;
-                    cc = cbeg[wv][lo] + y;
-                }
-                ri[u] = ok[u] ? rr : 0;
-                ci[u] = ok[u] ? cc : 0;
-            }
-            unsigned long long wr[SUN], wc[SUN];
-            int sr[SUN], sc[SUN];
-#pragma unroll
-            for (int u = 0; u < SUN; u++) {
-                if (E16) {
-                    const ulonglong2 er = eA[(uint32_t)ri[u]], ec = (diag ? eA : eB)[(uint32_t)ci[u]];
-                    wr[u] = rec_word(er); wc[u] = rec_word(ec);
-                    sr[u] = (int)(rec_row(er) >> 8);                                  // row code -> set
-                    const uint32_t cc = rec_col(ec);                                   // column code -> set
-                    sc[u] = (int)(((cc >> 18) << 1) | ((cc >> 4) & 1));
-                } else {
-                    wr[u] = wA[(uint32_t)ri[u]]; wc[u] = (diag ? wA : wB)[(uint32_t)ci[u]];
-                    sr[u] = sA[(uint32_t)ri[u]]; sc[u] = (diag ? sA : sB)[(uint32_t)ci[u]];
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < SUN; u++) {
-                const int v = __popcll(wr[u] & wc[u]);
-                if (v && ok[u]) {
-                    const int t0 = cnt_index(sr[u], sc[u]);
-                    atomicAdd(&cnt[t0 >> 1], (uint32_t)v << ((t0 & 1) << 4));
-                    if (mirror) {
-                        const int t1 = cnt_index(sc[u], sr[u]);
-                        atomicAdd(&cnt[t1 >> 1], (uint32_t)v << ((t1 & 1) << 4));
-                    }
-                }
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-    }
-    __syncthreads();
-    if (part) {
-        uint32_t* dst = reinterpret_cast<uint32_t*>(part) + ((int64_t)tile * nchunks + ch) * (SB * SB / 2);
-        for (int t = threadIdx.x; t < SB * SB / 2; t += SNT) dst[t] = cnt[t];
-        return;
-    }
-    for (int t = threadIdx.x; t < SB * SB; t += SNT) {
-        int a, b;
-        cnt_pair(t, a, b);
-        const int64_t i = A * SB + a, j = B * SB + b;
-        if (i < r0 || i >= r1 || j < c0 || j >= c1 || (upper && j <= i)) continue;
-        // the constant part once per pair: by chunk 0 (chunks flush with atomics)
-        const int v = (int)((cnt[t >> 1] >> ((t & 1) << 4)) & 0xFFFFu) +
-                      (ch == 0 ? (int)Us - nc[i] - nc[j] + dense_pair(dbits, Wdp, N, i, j) : 0);
-        if (v) atomicAdd(I + (i - r0) * ldI + (j - c0), v);
-    }
-}
-
-// ---- the LDS-staged sparse tile kernel (v2) --------------------------------
-// Same work and flattened-product walk as sparse_tile_kernel, other data
-// path. v1 loads a product's two complement words and set bytes from global
-// memory: a dependent chain of four loads whose L2/MALL latency bounds it
-// (every tile of a block row and column re-reads the chunk's entries, ~30 MB
-// per launch on C2, beyond an XCD's 4 MiB L2). v2 walks the chunk in
-// windows of `win` consecutive sparse words (aligned to multiples of win;
-// the build guarantees a window holds <= S2E entries per block, sp_win):
-//   * the window's entries (both lists, contiguous in the CSR) and offsets
-//     were loaded into registers while the previous window was walked, and
-//     are written to LDS between two barriers;
-//   * every wave prefix-sums the window's products (lane = word) and walks
-//     its eighth of them, SUN per lane in flight (ballot word search, rcp
-//     decode), reading the complement words and set bytes from LDS;
-//   * meanwhile the next window's loads are in flight.
-// A whole diagonal tile walks x < y of its one list, as v1.
-constexpr int S2T = 512;                 // threads per workgroup (8 waves)
-constexpr int S2NW = S2T / 64;
-constexpr int S2E = kSparseStageEntries;   // staged entries per side and window (<= 2 per thread)
-
-// ABL (timing ablations only, results wrong): 1 = no product walk, 2 = no
-// global fetch after the first window
-template <int SUN, int OCC, int ABL = 0>
-__global__ __launch_bounds__(S2T, OCC) void sparse_tile_kernel2(
-    const int64_t* __restrict__ off, const unsigned long long* __restrict__ word, const uint8_t* __restrict__ set,
-    const int32_t* __restrict__ nc, int64_t Us, int64_t Ws, int win, const int2* __restrict__ tiles, const int32_t* __restrict__ cbnd, int nchunks,
-    int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I, int64_t ldI,
-    int32_t* __restrict__ part, const unsigned long long* __restrict__ dbits, int64_t Wdp, int64_t N) {
-    __shared__ uint32_t cnt[SB * SB / 2];                  // 32 KiB, 16-bit counters (cnt_index layout)
-    __shared__ unsigned long long wA[S2E], wB[S2E];        // 10 KiB: staged complement words
-    __shared__ uint8_t sA[S2E], sB[S2E];                   // their set bytes
-    __shared__ int16_t oA[65], oB[65];                    // window word -> first staged entry
-    __shared__ int32_t pre[S2NW][64];                      // per wave: first product of each word
-    __shared__ int16_t rbeg[S2NW][64], cbeg[S2NW][64];
-    __shared__ uint8_t ncol[S2NW][64];
-    const int tile = blockIdx.x / nchunks, ch = blockIdx.x % nchunks;
-    const int64_t A = tiles[tile].x, B = tiles[tile].y;
-    const int rlo = (int)(r0 - A * SB > 0 ? r0 - A * SB : 0);
-    const int rhi = (int)(r1 - A * SB < SB ? r1 - A * SB : SB);
-    const bool rpart = rlo > 0 || rhi < SB;
-    const bool diag = A == B && !rpart, mirror = diag && !upper;
-    for (int t = threadIdx.x; t < SB * SB / 2; t += S2T) cnt[t] = 0;
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t sb = cbnd[ch], se = cbnd[ch + 1];          // the chunk's sparse words
-    const int64_t* offA = off + A * Ws;
-    const int64_t* offB = off + B * Ws;
-    const unsigned long long* cw = diag ? wA : wB;
-    const uint8_t* cs = diag ? sA : sB;
-    const int16_t* co = diag ? oA : oB;
-    // registers holding the next window: offsets (threads 0..64) and two
-    // entries per side per thread
-    int64_t ra_off = 0, rb_off = 0;
-    unsigned long long ewA[2], ewB[2];
-    uint8_t esA[2], esB[2];
-    int na = 0, nb = 0, nw = 0;
-    auto fetch = [&](int64_t s0, int64_t s1) {
-        nw = (int)(s1 - s0);
-        const int64_t a0 = offA[s0], b0 = offB[s0];
-        na = (int)(offA[s1] - a0);
-        nb = diag ? 0 : (int)(offB[s1] - b0);
-        if (threadIdx.x <= nw) {
-            ra_off = offA[s0 + threadIdx.x] - a0;
-            if (!diag) rb_off = offB[s0 + threadIdx.x] - b0;
-        }
-#pragma unroll
-        for (int e = 0; e < 2; e++) {
-            const int t = threadIdx.x + e * S2T;
-            if (t < na) { ewA[e] = word[a0 + t]; esA[e] = set[a0 + t]; }
-            if (t < nb) { ewB[e] = word[b0 + t]; esB[e] = set[b0 + t]; }
-        }
-    };
-    int64_t s0 = sb;
-    int64_t s1 = std::min<int64_t>(se, (sb / win + 1) * win);
-    if (s0 < se) fetch(s0, s1);
-    while (s0 < se) {
-        __syncthreads();                               // the previous window's walk is done
-        if (threadIdx.x <= nw) {
-            oA[threadIdx.x] = (int16_t)ra_off;
-            if (!diag) oB[threadIdx.x] = (int16_t)rb_off;
-        }
-#pragma unroll
-        for (int e = 0; e < 2; e++) {
-            const int t = threadIdx.x + e * S2T;
-            if (t < na) { wA[t] = ewA[e]; sA[t] = esA[e]; }
-            if (t < nb) { wB[t] = ewB[e]; sB[t] = esB[e]; }
-        }
-        __syncthreads();
-        const int cur_nw = nw;
-        const int64_t n0 = s1, n1 = std::min<int64_t>(se, s1 + win);
-        if (n0 < se && !(ABL == 2 && s0 != sb)) fetch(n0, n1);   // in flight during the walk
-        // every wave: the window's products, lane = word
-        int P = 0, rb = 0, cb = 0, ncl = 0;
-        if (lane < cur_nw) {
-            rb = oA[lane];
-            int nr = oA[lane + 1] - rb;
-            cb = co[lane]; ncl = co[lane + 1] - cb;
-            if (rpart) {                               // lists are sorted by set: trim both ends
-                int a = 0, e = nr;
-                for (int t = 0; t < nr; t++) {
-                    const int st = sA[rb + t];
-                    a += st < rlo;
-                    e -= st >= rhi;
-                }
-                rb += a;
-                nr = e > a ? e - a : 0;
-            }
-            P = diag ? nr * (nr - 1) / 2 : nr * ncl;
-        }
-        int incl = P;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int v = __shfl_up(incl, o, 64);
-            if (lane >= o) incl += v;
-        }
-        pre[wv][lane] = incl - P;
-        rbeg[wv][lane] = (int16_t)rb;
-        cbeg[wv][lane] = (int16_t)cb;
-        ncol[wv][lane] = (uint8_t)ncl;
-        const int total = __shfl(incl, 63, 64);
-        __builtin_amdgcn_wave_barrier();
-        const int f0 = (int)((int64_t)total * wv / S2NW);
-        const int f1 = ABL == 1 ? f0 : (int)((int64_t)total * (wv + 1) / S2NW);
-        for (int fb = f0; fb < f1; fb += 64 * SUN) {
-            int ri[SUN], ci[SUN];
-            bool ok[SUN];
-#pragma unroll
-            for (int u = 0; u < SUN; u++) {
-                const int F = fb + 64 * u, f = F + lane;
-                ok[u] = f < f1;
-                const int q0 = __popcll(__ballot(incl <= F));
-                const int q1 = __popcll(__ballot(incl <= F + 63));
-                int lo = q0;
-                for (int l = q0; l < q1; l++) lo += __builtin_amdgcn_readlane(incl, l) <= f;
-                lo = lo < 63 ? lo : 63;
-                const int q = f - pre[wv][lo];
-                int x, y, rr, cc;
-                if (diag) {                            // q -> pair (y, x), y < x: q = x(x-1)/2 + y
-                    x = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)q)) * 0.5f);
-                    if (x * (x - 1) / 2 > q) x--;
-                    else if ((x + 1) * x / 2 <= q) x++;
-                    y = q - x * (x - 1) / 2;
-                    rr = rbeg[wv][lo] + y;
-                    cc = rbeg[wv][lo] + x;
-                } else {
-                    const int n2 = ncol[wv][lo];
-                    x = (int)((float)q * __builtin_amdgcn_rcpf((float)n2));
-                    if (x * n2 > q) x--;
-                    else if ((x + 1) * n2 <= q) x++;
-                    y = q - x * n2;
-                    rr = rbeg[wv][lo] + x;
-                    cc = cbeg[wv][lo] + y;
-                }
-                ri[u] = ok[u] ? rr : 0;
-                ci[u] = ok[u] ? cc : 0;
-            }
-#pragma unroll
-            for (int u = 0; u < SUN; u++) {
-                const int v = __popcll(wA[ri[u]] & cw[ci[u]]);
-                if (v && ok[u]) {
-                    const int sr = sA[ri[u]], sc = cs[ci[u]];
-                    const int t0 = cnt_index(sr, sc);
-                    atomicAdd(&cnt[t0 >> 1], (uint32_t)v << ((t0 & 1) << 4));
-                    if (mirror) {
-                        const int t1 = cnt_index(sc, sr);
-                        atomicAdd(&cnt[t1 >> 1], (uint32_t)v << ((t1 & 1) << 4));
-                    }
-                }
-            }
-        }
-        s0 = n0;
-        s1 = n1;
-    }
-    __syncthreads();
-    if (part) {
-        uint32_t* dst = reinterpret_cast<uint32_t*>(part) + ((int64_t)tile * nchunks + ch) * (SB * SB / 2);
-        for (int t = threadIdx.x; t < SB * SB / 2; t += S2T) dst[t] = cnt[t];
-        return;
-    }
-    for (int t = threadIdx.x; t < SB * SB; t += S2T) {
-        int a, b;
-        cnt_pair(t, a, b);
-        const int64_t i = A * SB + a, j = B * SB + b;
-        if (i < r0 || i >= r1 || j < c0 || j >= c1 || (upper && j <= i)) continue;
-        // the constant part once per pair: by chunk 0 (chunks flush with atomics)
-        const int v = (int)((cnt[t >> 1] >> ((t & 1) << 4)) & 0xFFFFu) +
-                      (ch == 0 ? (int)Us - nc[i] - nc[j] + dense_pair(dbits, Wdp, N, i, j) : 0);
-        if (v) atomicAdd(I + (i - r0) * ldI + (j - c0), v);
-    }
-}
-
-// ---- v4: the v2 windows, walked as an 8 x 8 grid per word ----------------
-// The staging of v2, but no flattened-product search: a wave takes the
-// window's words w = wave, wave + 8, ... one at a time, lane (i, j) =
-// (row entry ib + i, column entry jb + j), blocks of 8 x 8 over longer
-// lists. All indexing is wave-uniform; a product is two broadcast
-// ds_read_b64, two byte reads, the AND + popcount and the counter add.
-// U words are in flight per wave step.
-template <int U, int OCC>
-__global__ __launch_bounds__(S2T, OCC) void sparse_tile_kernel4(
-    const int64_t* __restrict__ off, const unsigned long long* __restrict__ word, const uint8_t* __restrict__ set,
-    const int32_t* __restrict__ nc, int64_t Us, int64_t Ws, int win, const int2* __restrict__ tiles, const int32_t* __restrict__ cbnd, int nchunks,
-    int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I, int64_t ldI,
-    int32_t* __restrict__ part, const unsigned long long* __restrict__ dbits, int64_t Wdp, int64_t N) {
-    __shared__ uint32_t cnt[SB * SB / 2];                  // 32 KiB, 16-bit counters (cnt_index layout)
-    __shared__ unsigned long long wA[S2E], wB[S2E];        // 10 KiB: staged complement words
-    __shared__ uint8_t sA[S2E], sB[S2E];                   // their set bytes
-    __shared__ int16_t oA[65], oB[65];                    // window word -> first staged entry
-    const int tile = blockIdx.x / nchunks, ch = blockIdx.x % nchunks;
-    const int64_t A = tiles[tile].x, B = tiles[tile].y;
-    const int rlo = (int)(r0 - A * SB > 0 ? r0 - A * SB : 0);
-    const int rhi = (int)(r1 - A * SB < SB ? r1 - A * SB : SB);
-    const bool rpart = rlo > 0 || rhi < SB;
-    const bool diag = A == B && !rpart, mirror = diag && !upper;
-    for (int t = threadIdx.x; t < SB * SB / 2; t += S2T) cnt[t] = 0;
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t sb = cbnd[ch], se = cbnd[ch + 1];          // the chunk's sparse words
-    const int64_t* offA = off + A * Ws;
-    const int64_t* offB = off + B * Ws;
-    const unsigned long long* cw = diag ? wA : wB;
-    const uint8_t* cs = diag ? sA : sB;
-    const int16_t* co = diag ? oA : oB;
-    // registers holding the next window: offsets (threads 0..64) and two
-    // entries per side per thread
-    int64_t ra_off = 0, rb_off = 0;
-    unsigned long long ewA[2], ewB[2];
-    uint8_t esA[2], esB[2];
-    int na = 0, nb = 0, nw = 0;
-    auto fetch = [&](int64_t s0, int64_t s1) {
-        nw = (int)(s1 - s0);
-        const int64_t a0 = offA[s0], b0 = offB[s0];
-        na = (int)(offA[s1] - a0);
-        nb = diag ? 0 : (int)(offB[s1] - b0);
-        if (threadIdx.x <= nw) {
-            ra_off = offA[s0 + threadIdx.x] - a0;
-            if (!diag) rb_off = offB[s0 + threadIdx.x] - b0;
-        }
-#pragma unroll
-        for (int e = 0; e < 2; e++) {
-            const int t = threadIdx.x + e * S2T;
-            if (t < na) { ewA[e] = word[a0 + t]; esA[e] = set[a0 + t]; }
-            if (t < nb) { ewB[e] = word[b0 + t]; esB[e] = set[b0 + t]; }
-        }
-    };
-    int64_t s0 = sb;
-    int64_t s1 = std::min<int64_t>(se, (sb / win + 1) * win);
-    if (s0 < se) fetch(s0, s1);
-    while (s0 < se) {
-        __syncthreads();                               // the previous window's walk is done
-        if (threadIdx.x <= nw) {
-            oA[threadIdx.x] = (int16_t)ra_off;
-            if (!diag) oB[threadIdx.x] = (int16_t)rb_off;
-        }
-#pragma unroll
-        for (int e = 0; e < 2; e++) {
-            const int t = threadIdx.x + e * S2T;
-            if (t < na) { wA[t] = ewA[e]; sA[t] = esA[e]; }
-            if (t < nb) { wB[t] = ewB[e]; sB[t] = esB[e]; }
-        }
-        __syncthreads();
-        const int cur_nw = nw;
-        const int64_t n0 = s1, n1 = std::min<int64_t>(se, s1 + win);
-        if (n0 < se) fetch(n0, n1);                    // in flight during the walk
-        const int gi = lane >> 3, gj = lane & 7;
-        for (int w0 = wv; w0 < cur_nw; w0 += S2NW * U) {
-            int ra[U], nr[U], cb[U], ncl[U];
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                const int w = w0 + u * S2NW;
-                const bool has = w < cur_nw;
-                ra[u] = has ? oA[w] : 0;
-                nr[u] = has ? oA[w + 1] - ra[u] : 0;
-                cb[u] = has ? co[w] : 0;
-                ncl[u] = has ? co[w + 1] - cb[u] : 0;
-            }
-            // the common case: every list of the U words within one 8 x 8 block
-            bool small = true;
-#pragma unroll
-            for (int u = 0; u < U; u++) small = small && nr[u] <= 8 && ncl[u] <= 8;
-            if (small) {
-                unsigned long long wx[U], wy[U];
-                int sx[U], sy[U];
-                bool on[U];
-#pragma unroll
-                for (int u = 0; u < U; u++) {
-                    on[u] = gi < nr[u] && gj < ncl[u] && (!diag || gj > gi);
-                    const int xi = on[u] ? ra[u] + gi : 0, yi = on[u] ? cb[u] + gj : 0;
-                    wx[u] = wA[xi]; wy[u] = cw[yi];
-                    sx[u] = sA[xi]; sy[u] = cs[yi];
-                    on[u] = on[u] && (!rpart || (sx[u] >= rlo && sx[u] < rhi));
-                }
-#pragma unroll
-                for (int u = 0; u < U; u++) {
-                    const int v = __popcll(wx[u] & wy[u]);
-                    if (on[u] && v) {
-                        const int t0 = cnt_index(sx[u], sy[u]);
-                        atomicAdd(&cnt[t0 >> 1], (uint32_t)v << ((t0 & 1) << 4));
-                        if (mirror) {
-                            const int t1 = cnt_index(sy[u], sx[u]);
-                            atomicAdd(&cnt[t1 >> 1], (uint32_t)v << ((t1 & 1) << 4));
-                        }
-                    }
-                }
-                continue;
-            }
-#pragma unroll 1
-            for (int u = 0; u < U; u++) {
-                for (int ib = 0; ib < nr[u]; ib += 8) {
-                    const int x = ib + gi;
-                    const bool xo = x < nr[u];
-                    const unsigned long long wx = xo ? wA[ra[u] + x] : 0ull;
-                    const int sx = xo ? sA[ra[u] + x] : 0;
-                    const bool xin = xo && (!rpart || (sx >= rlo && sx < rhi));
-                    for (int jb = diag ? ib : 0; jb < ncl[u]; jb += 8) {
-                        const int y = jb + gj;
-                        if (!xin || y >= ncl[u] || (diag && y <= x)) continue;
-                        const int v = __popcll(wx & cw[cb[u] + y]);
-                        if (v) {
-                            const int sy = cs[cb[u] + y];
-                            const int t0 = cnt_index(sx, sy);
-                            atomicAdd(&cnt[t0 >> 1], (uint32_t)v << ((t0 & 1) << 4));
-                            if (mirror) {
-                                const int t1 = cnt_index(sy, sx);
-                                atomicAdd(&cnt[t1 >> 1], (uint32_t)v << ((t1 & 1) << 4));
-                            }
-                        }
-                    }
-                }
-            }
-        }
-        s0 = n0;
-        s1 = n1;
-    }
-    __syncthreads();
-    if (part) {
-        uint32_t* dst = reinterpret_cast<uint32_t*>(part) + ((int64_t)tile * nchunks + ch) * (SB * SB / 2);
-        for (int t = threadIdx.x; t < SB * SB / 2; t += S2T) dst[t] = cnt[t];
-        return;
-    }
-    for (int t = threadIdx.x; t < SB * SB; t += S2T) {
-        int a, b;
-        cnt_pair(t, a, b);
-        const int64_t i = A * SB + a, j = B * SB + b;
-        if (i < r0 || i >= r1 || j < c0 || j >= c1 || (upper && j <= i)) continue;
-        // the constant part once per pair: by chunk 0 (chunks flush with atomics)
-        const int v = (int)((cnt[t >> 1] >> ((t & 1) << 4)) & 0xFFFFu) +
-                      (ch == 0 ? (int)Us - nc[i] - nc[j] + dense_pair(dbits, Wdp, N, i, j) : 0);
-        if (v) atomicAdd(I + (i - r0) * ldI + (j - c0), v);
-    }
-}
-
-// ---- v5 / v6: v1's flattened walk, laid out for issue --------------------
-// The products and the walk of v1; what changes is the instruction stream
-// per product (round-2 ISA of v1: the diagonal/off-diagonal choice and the
-// +-1 correction of the quotient compiled to exec-mask branches inside every
-// product slot, four dependent LDS reads per slot, quarter-rate 32-bit
-// multiplies, and the set-byte loads sunk behind the counter branch):
-//   * diagonal and off-diagonal tiles run separate instantiations of the
-//     walk (one uniform branch per batch);
-//   * a word's walk fields are one 16-byte LDS record {pre | ncol << 24,
-//     row start, column start, 1 / ncol}: one ds_read_b128 per slot, all
-//     SUN slots' reads issued before any is used;
-//   * the quotient correction is select-only, multiplies are 24-bit;
-//   * an entry is one 16-byte {word, set} record (one load per side, scalar
-//     base + 32-bit offset);
-//   * the counter add is unconditional (a zero product adds 0), so no slot
-//     waits on another's branch; idle slots (f >= total) read the zero
-//     sentinel record past the last entry instead of being masked.
-// v5 keeps one product per slot; v6 (below) walks micro-tiles.
 struct SparseWalk {
     const ulonglong2* eA;                 // the chunk's row-side records
     const ulonglong2* eB;                 // ... and column-side records
 };
 
-// Word of product (slot) f: #{l : incl_l <= f} (v1's search). Words w0 and
-// w0 + 1 unconditionally (a word past w1 ends after f: it adds 0), the rest
-// (more than two words ending inside the slot group) in a loop.
+// Word of slot f: #{l : incl_l <= f}. Words w0 and w0 + 1 unconditionally
+// (a word past w1 ends after f: it adds 0), the rest (more than two words
+// ending inside the slot group) in a loop.
 __device__ __forceinline__ int slot_word(int incl, int F, int f) {
     const int w0 = __builtin_amdgcn_readfirstlane(__popcll(__ballot(incl <= F)));
     const int w1 = __builtin_amdgcn_readfirstlane(__popcll(__ballot(incl <= F + 63)));
@@ -811,13 +280,13 @@ __device__ __forceinline__ int slot_word(int incl, int F, int f) {
     return lo < 63 ? lo : 63;
 }
 
-// zc: the sentinel record relative to the column side's base
-template <int SUN, bool DIAG>
-__device__ __forceinline__ void sparse_walk5_range(const int4* __restrict__ rec, int incl, int total, int lane,
-                                                   const SparseWalk& e, uint32_t zc, uint32_t* __restrict__ cnt,
-                                                   bool mirror, int fb0, int fb1) {
-    const char* beA = reinterpret_cast<const char*>(e.eA);
-    const char* beB = reinterpret_cast<const char*>(DIAG ? e.eA : e.eB);
+// Diagonal tiles: slot q of a word is its pair (y, x), y < x, q = x(x-1)/2 + y.
+// zc: the sentinel record relative to the side's base.
+template <int SUN>
+__device__ __forceinline__ void sparse_walk_diag(const int4* __restrict__ rec, int incl, int total, int lane,
+                                                 const SparseWalk& e, uint32_t zc, uint32_t* __restrict__ cnt,
+                                                 bool mirror, int fb0, int fb1) {
+    const char* be = reinterpret_cast<const char*>(e.eA);
     for (int fb = fb0; fb < fb1; fb += 64 * SUN) {
         int4 r[SUN];
         int f[SUN];
@@ -831,65 +300,40 @@ __device__ __forceinline__ void sparse_walk5_range(const int4* __restrict__ rec,
         for (int u = 0; u < SUN; u++) {
             const bool ok = f[u] < total;
             const int q = f[u] - (r[u].x & 0xFFFFFF);
-            int rr, cc;
-            if (DIAG) {                        // q -> pair (y, x), y < x: q = x(x-1)/2 + y
-                int x = (int)((1.0f + __builtin_amdgcn_sqrtf(1.0f + 8.0f * (float)q)) * 0.5f);
-                const int t = (int)(__umul24(x, x - 1) >> 1);
-                // x -= 1 when t > q, x += 1 when (x + 1) x / 2 <= q: arithmetic, not branches
-                const int dn = (int)(t > q), up = (int)(t + x <= q);
-                const int xc = x + up - dn;
-                const int tc = t + __mul24(up, x) - __mul24(dn, x - 1);
-                rr = r[u].y + (q - tc);
-                cc = r[u].y + xc;
-            } else {
-                const int n2 = (int)((uint32_t)r[u].x >> 24);
-                const int x = (int)((float)q * __int_as_float(r[u].w));
-                const int t = (int)__umul24(x, n2);
-                const int adj = (int)(t + n2 <= q) - (int)(t > q);   // the quotient's +-1, select-free
-                const int xc = x + adj;
-                const int tc = (int)__umul24(xc, n2);
-                rr = r[u].y + xc;
-                cc = r[u].z + (q - tc);
-            }
-            ri[u] = ok ? (uint32_t)rr : 0u;
-            ci[u] = ok ? (uint32_t)cc : zc;
+            int x = (int)((1.0f + __builtin_amdgcn_sqrtf(1.0f + 8.0f * (float)q)) * 0.5f);
+            const int t = (int)(__umul24(x, x - 1) >> 1);
+            // x -= 1 when t > q, x += 1 when (x + 1) x / 2 <= q: arithmetic, not branches
+            const int dn = (int)(t > q), up = (int)(t + x <= q);
+            const int xc = x + up - dn;
+            const int tc = t + __mul24(up, x) - __mul24(dn, x - 1);
+            ri[u] = ok ? (uint32_t)(r[u].y + (q - tc)) : 0u;
+            ci[u] = ok ? (uint32_t)(r[u].y + xc) : zc;
         }
         ulonglong2 a[SUN], b[SUN];
 #pragma unroll
         for (int u = 0; u < SUN; u++) {
-            a[u] = *reinterpret_cast<const ulonglong2*>(beA + (ri[u] << 4));
-            b[u] = *reinterpret_cast<const ulonglong2*>(beB + (ci[u] << 4));
+            a[u] = *reinterpret_cast<const ulonglong2*>(be + (ri[u] << 4));
+            b[u] = *reinterpret_cast<const ulonglong2*>(be + (ci[u] << 4));
         }
 #pragma unroll
         for (int u = 0; u < SUN; u++) {
             const uint32_t v = (uint32_t)__popcll(rec_word(a[u]) & rec_word(b[u]));
             cnt_add(cnt, rec_row(a[u]), rec_col(b[u]), v);
-            if (DIAG && mirror) cnt_add(cnt, rec_row(b[u]), rec_col(a[u]), v);
+            if (mirror) cnt_add(cnt, rec_row(b[u]), rec_col(a[u]), v);
         }
     }
 }
 
-template <int SUN, bool DIAG>
-__device__ __forceinline__ void sparse_walk5(const int4* __restrict__ rec, int incl, int total, int lane,
-                                             const SparseWalk& e, uint32_t zc, uint32_t* __restrict__ cnt,
-                                             bool mirror) {
-    const int full = total / (64 * SUN) * (64 * SUN);
-    sparse_walk5_range<SUN, DIAG>(rec, incl, total, lane, e, zc, cnt, mirror, 0, full);
-    if (SUN > 1) sparse_walk5_range<1, DIAG>(rec, incl, total, lane, e, zc, cnt, mirror, full, total);
-}
-
-// v6 (off-diagonal tiles): a product slot is a micro-tile of RW adjacent
-// rows x CW adjacent columns of one word: nrp = ceil(nr / RW) x ncp =
-// ceil(ncol / CW) slots per word. One search and quotient per RW x CW
-// products; the records of a slot's rows (and columns) are adjacent, one
-// offset each, immediates +16 for the rest. Rows / columns past a list's end
-// read the next records (or the zero sentinels past the last one) and add 0.
-// Record: {pre | ncol << 24, row start, column start, 1 / ncp with nr in the
-// low 8 mantissa bits} (the quotient tolerates the 2^-15 error, q < 2^14).
-template <int SUN, int RW, int CW, bool EXQ>
-__device__ __forceinline__ void sparse_walk6_range(const int4* __restrict__ rec, int incl, int total, int lane,
-                                                   const SparseWalk& e, uint32_t zc, uint32_t* __restrict__ cnt,
-                                                   int fb0, int fb1) {
+// Off-diagonal tiles: 1 x 2 micro-tiles, ncp = ceil(ncol / 2) slots per row
+// entry. rec.w = 1 / (2 ncp): (2q + 1) / (2 ncp) = q / ncp + (q mod ncp +
+// 1/2) / ncp stays >= 1/(2 ncp) >= 1/128 from an integer, while the float
+// error is <= (q + 1/2) / ncp * 2^-22 < 0.002 (q < 128 x 64), so the
+// truncation is the exact quotient (checked exhaustively with +-2-ulp
+// reciprocals).
+template <int SUN>
+__device__ __forceinline__ void sparse_walk_off(const int4* __restrict__ rec, int incl, int total, int lane,
+                                                const SparseWalk& e, uint32_t zc, uint32_t* __restrict__ cnt,
+                                                int fb0, int fb1) {
     const char* beA = reinterpret_cast<const char*>(e.eA);
     const char* beB = reinterpret_cast<const char*>(e.eB);
     for (int fb = fb0; fb < fb1; fb += 64 * SUN) {
@@ -901,120 +345,24 @@ __device__ __forceinline__ void sparse_walk6_range(const int4* __restrict__ rec,
             r[u] = rec[slot_word(incl, fb + 64 * u, f[u])];
         }
         uint32_t ri[SUN], ci[SUN];
-        int nrow[SUN], ncol[SUN];                      // valid rows / columns of the slot
+        int ncol[SUN];                                 // valid columns from the slot's first
 #pragma unroll
         for (int u = 0; u < SUN; u++) {
             const bool ok = f[u] < total;
             const int q = f[u] - (r[u].x & 0xFFFFFF);
             const int ncl = (int)((uint32_t)r[u].x >> 24);
-            const int ncp = (ncl + CW - 1) / CW;
-            int xc;
-            if (EXQ) {
-                // exact without a correction: rec.w = 1 / (2 ncp), and
-                // (2q + 1) / (2 ncp) = q / ncp + (q mod ncp + 1/2) / ncp stays
-                // >= 1/(2 ncp) >= 1/128 from an integer, while the float error
-                // is <= (q + 1/2) / ncp * 2^-22 < 0.002 (q < 128 x 64)
-                xc = (int)((float)(2 * q + 1) * __int_as_float(r[u].w));
-            } else {
-                const int x = (int)((float)q * __int_as_float(r[u].w));
-                const int t = (int)__umul24(x, ncp);
-                const int adj = (int)(t + ncp <= q) - (int)(t > q);
-                xc = x + adj;
-            }
-            const int yc = (q - (int)__umul24(xc, ncp)) * CW;
+            const int ncp = (ncl + 1) >> 1;
+            const int xc = (int)((float)(2 * q + 1) * __int_as_float(r[u].w));
+            const int yc = (q - (int)__umul24(xc, ncp)) * 2;
             ncol[u] = ncl - yc;
-            nrow[u] = RW > 1 ? (r[u].w & 0xFF) - xc * RW : 1;
-            ri[u] = ok ? (uint32_t)(r[u].y + xc * RW) : 0u;
+            ri[u] = ok ? (uint32_t)(r[u].y + xc) : 0u;
             ci[u] = ok ? (uint32_t)(r[u].z + yc) : zc;
         }
-        Rec3 a[SUN][RW], b[SUN][CW];          // rows {row code, word}, columns {word, column code}
+        Rec3 a[SUN], b0[SUN], b1[SUN];                 // row {row code, word}, columns {word, column code}
 #pragma unroll
         for (int u = 0; u < SUN; u++) {
-            const char* pa = beA + (ri[u] << 4);
             const char* pb = beB + (ci[u] << 4) + 4;
-#pragma unroll
-            for (int i = 0; i < RW; i++) a[u][i] = *reinterpret_cast<const Rec3*>(pa + 16 * i);
-#pragma unroll
-            for (int j = 0; j < CW; j++) b[u][j] = *reinterpret_cast<const Rec3*>(pb + 16 * j);
-        }
-#pragma unroll
-        for (int u = 0; u < SUN; u++)
-#pragma unroll
-            for (int i = 0; i < RW; i++) {
-                const uint32_t rc = a[u][i].a;
-#pragma unroll
-                for (int j = 0; j < CW; j++) {
-                    const bool in = (i == 0 || i < nrow[u]) && (j == 0 || j < ncol[u]);
-                    const uint32_t v = in ? (uint32_t)(__popc(a[u][i].b & b[u][j].a) + __popc(a[u][i].c & b[u][j].b)) : 0u;
-                    cnt_add(cnt, rc, b[u][j].c, v);
-                }
-            }
-    }
-}
-
-// v6 with CONSECUTIVE slots per lane (option sparse_shape = 112): lane l of a
-// group takes slots fb + SUN l ... fb + SUN l + SUN - 1 of the batch. One
-// search and one quotient give the first; each next slot is one column pair
-// further (a new row after ncp pairs, the next word with slots after nr
-// rows: a short divergent step that reads that word's record), so SUN slots
-// cost one search + one quotient instead of SUN of each. The search spans
-// the words ending inside the group's 64 SUN slots (a uniform readlane loop).
-// Records carry nr in the low 8 mantissa bits of 1 / ncp (as RW > 1).
-template <int SUN>
-__device__ __forceinline__ void sparse_walk6c_range(const int4* __restrict__ rec, int incl, int total, int lane,
-                                                    const SparseWalk& e, uint32_t zc, uint32_t* __restrict__ cnt,
-                                                    int fb0, int fb1) {
-    const char* beA = reinterpret_cast<const char*>(e.eA);
-    const char* beB = reinterpret_cast<const char*>(e.eB);
-    for (int fb = fb0; fb < fb1; fb += 64 * SUN) {
-        const int f0 = fb + SUN * lane;
-        const int w0 = __builtin_amdgcn_readfirstlane(__popcll(__ballot(incl <= fb)));
-        const int w1 = __builtin_amdgcn_readfirstlane(__popcll(__ballot(incl <= fb + 64 * SUN - 1)));
-        int lo = w0;
-        for (int l = w0; l < w1; l++) lo += __builtin_amdgcn_readlane(incl, l) <= f0;
-        lo = lo < 63 ? lo : 63;
-        int4 r = rec[lo];
-        int ncl = (int)((uint32_t)r.x >> 24), ncp = (ncl + 1) >> 1, nr = r.w & 0xFF;
-        int xr, yc;
-        {
-            const int q = f0 - (r.x & 0xFFFFFF);
-            const int x = (int)((float)q * __int_as_float(r.w));
-            const int t = (int)__umul24(x, ncp);
-            const int adj = (int)(t + ncp <= q) - (int)(t > q);
-            xr = x + adj;
-            yc = q - (int)__umul24(xr, ncp);
-        }
-        uint32_t ri[SUN], ci[SUN];
-        bool two[SUN];
-#pragma unroll
-        for (int u = 0; u < SUN; u++) {
-            const bool ok = f0 + u < total;
-            ri[u] = ok ? (uint32_t)(r.y + xr) : 0u;
-            ci[u] = ok ? (uint32_t)(r.z + 2 * yc) : zc;
-            two[u] = 2 * yc + 1 < ncl;
-            if (u + 1 < SUN) {                         // one slot further
-                yc++;
-                const bool wrap = yc == ncp;
-                yc = wrap ? 0 : yc;
-                xr += wrap ? 1 : 0;
-                if (xr >= nr && ok) {                  // past the word: the next word with slots
-                    do {
-                        lo++;
-                        r = rec[lo < 63 ? lo : 63];
-                        ncl = (int)((uint32_t)r.x >> 24);
-                        ncp = (ncl + 1) >> 1;
-                        nr = r.w & 0xFF;
-                    } while (lo < 63 && nr * ncp == 0);
-                    xr = 0;
-                    yc = 0;
-                }
-            }
-        }
-        Rec3 a[SUN], b0[SUN], b1[SUN];
-#pragma unroll
-        for (int u = 0; u < SUN; u++) {
             a[u] = *reinterpret_cast<const Rec3*>(beA + (ri[u] << 4));
-            const char* pb = beB + (ci[u] << 4) + 4;
             b0[u] = *reinterpret_cast<const Rec3*>(pb);
             b1[u] = *reinterpret_cast<const Rec3*>(pb + 16);
         }
@@ -1022,7 +370,7 @@ __device__ __forceinline__ void sparse_walk6c_range(const int4* __restrict__ rec
         for (int u = 0; u < SUN; u++) {
             const uint32_t rc = a[u].a;
             const uint32_t v0 = (uint32_t)(__popc(a[u].b & b0[u].a) + __popc(a[u].c & b0[u].b));
-            const uint32_t v1 = two[u] ? (uint32_t)(__popc(a[u].b & b1[u].a) + __popc(a[u].c & b1[u].b)) : 0u;
+            const uint32_t v1 = ncol[u] > 1 ? (uint32_t)(__popc(a[u].b & b1[u].a) + __popc(a[u].c & b1[u].b)) : 0u;
             cnt_add(cnt, rc, b0[u].c, v0);
             cnt_add(cnt, rc, b1[u].c, v1);
         }
@@ -1032,47 +380,30 @@ __device__ __forceinline__ void sparse_walk6c_range(const int4* __restrict__ rec
 // SUN slots per lane while whole groups of 64 SUN slots remain, then one
 // 64-slot group at a time: a batch's last iteration no longer walks up to
 // 64 (SUN - 1) idle slots (~7 % of C2's slots at SUN = 3)
-template <int SUN, int RW, int CW, bool CONSEC = false>
-__device__ __forceinline__ void sparse_walk6(const int4* __restrict__ rec, int incl, int total, int lane,
-                                             const SparseWalk& e, uint32_t zc, uint32_t* __restrict__ cnt) {
-    // EXQ: the correction-free quotient, records holding 1 / (2 ncp) (one row per slot, not CONSEC)
-    constexpr bool EXQ = RW == 1 && !CONSEC;
+template <int SUN, bool DIAG>
+__device__ __forceinline__ void sparse_walk(const int4* __restrict__ rec, int incl, int total, int lane,
+                                            const SparseWalk& e, uint32_t zc, uint32_t* __restrict__ cnt,
+                                            bool mirror) {
     const int full = total / (64 * SUN) * (64 * SUN);
-    if (CONSEC) sparse_walk6c_range<SUN>(rec, incl, total, lane, e, zc, cnt, 0, full);
-    else sparse_walk6_range<SUN, RW, CW, EXQ>(rec, incl, total, lane, e, zc, cnt, 0, full);
-    if (SUN > 1) sparse_walk6_range<1, RW, CW, EXQ>(rec, incl, total, lane, e, zc, cnt, full, total);
+    if (DIAG) {
+        sparse_walk_diag<SUN>(rec, incl, total, lane, e, zc, cnt, mirror, 0, full);
+        if (SUN > 1) sparse_walk_diag<1>(rec, incl, total, lane, e, zc, cnt, mirror, full, total);
+    } else {
+        sparse_walk_off<SUN>(rec, incl, total, lane, e, zc, cnt, 0, full);
+        if (SUN > 1) sparse_walk_off<1>(rec, incl, total, lane, e, zc, cnt, full, total);
+    }
 }
 
-// RW = CW = 0: v5 (one product per slot); otherwise v6 with RW x CW
-// micro-tiles on the off-diagonal tiles (diagonal tiles walk v5's pairs)
-template <int SUN, int OCC, int RW = 0, int CW = 0, bool CONSEC = false>
-__global__ __launch_bounds__(SNT, OCC) void sparse_tile_kernel5(
-    const int64_t* __restrict__ off, const uint8_t* __restrict__ set, const ulonglong2* __restrict__ ent,
-    const int32_t* __restrict__ nc, int64_t Us, int64_t Ws, const int2* __restrict__ tiles, const int32_t* __restrict__ cbnd, int nchunks,
-    int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I, int64_t ldI,
-    int32_t* __restrict__ part, const unsigned long long* __restrict__ dbits, int64_t Wdp, int64_t N, int il,
-    const unsigned long long* __restrict__ slab_bits, int slabs, int ntiles, int xmap) {
-    // dbits: the flush-fold dense words (word-major, option fold_dense_words);
+template <int SUN>
+__global__ __launch_bounds__(SNT, 8) void sparse_tile_kernel(
+    const int64_t* __restrict__ off, const ulonglong2* __restrict__ ent, const int32_t* __restrict__ nc, int64_t Us,
+    int64_t Ws, const int2* __restrict__ tiles, const int32_t* __restrict__ cbnd, int nchunks, int64_t r0, int64_t r1,
+    int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I, int64_t ldI, int32_t* __restrict__ part, int64_t Wdp,
+    int64_t N, const unsigned long long* __restrict__ slab_bits, int slabs) {
     // slab_bits / slabs: the in-kernel fold's dense words (set-major [N][Wdp])
     __shared__ uint32_t cnt[SB * SB / 2];                  // 32 KiB, 16-bit counters (cnt_index layout)
     __shared__ int4 rec[SNW][64];                          // 8 KiB: the batch's walk records
-    // xmap (option sparse_xcd): workgroup b = 8 (t + ntiles g) + x runs chunk
-    // 8 g + x of tile t. Blocks b and b + 8 share an XCD (round-robin
-    // dispatch), so chunk c of EVERY tile runs on one XCD, and the groups of 8
-    // chunks are dispatched in turn: an XCD's L2 holds the few chunks it is
-    // working on for all the tiles that read them (C2: ~0.85 MB of records
-    // per chunk over the 8 blocks), instead of every workgroup fetching its
-    // own rows and columns past L2 (tile-major order: 0.5 GB per launch).
-    int tile, ch;
-    if (xmap) {
-        const int per_g = ntiles * 8;
-        tile = (blockIdx.x % per_g) >> 3;
-        ch = (blockIdx.x / per_g) * 8 + (blockIdx.x & 7);
-        if (ch >= nchunks) return;
-    } else {
-        tile = blockIdx.x / nchunks;
-        ch = blockIdx.x % nchunks;
-    }
+    const int tile = blockIdx.x / nchunks, ch = blockIdx.x % nchunks;
     const int64_t A = tiles[tile].x, B = tiles[tile].y;
     const int rlo = (int)(r0 - A * SB > 0 ? r0 - A * SB : 0);
     const int rhi = (int)(r1 - A * SB < SB ? r1 - A * SB : SB);
@@ -1088,13 +419,9 @@ __global__ __launch_bounds__(SNT, OCC) void sparse_tile_kernel5(
     const SparseWalk e{ent + ra0, ent + cb0};
     const int64_t ntot = off[(int64_t)ceil_div(N, SB) * Ws];         // entries of every block: the sentinel
     const uint32_t zA = (uint32_t)(ntot - ra0), zB = (uint32_t)(ntot - cb0);
-    // batches of 64 consecutive words per wave, or (il, option
-    // sparse_balance) the words dealt to the waves one at a time (word
-    // sb + 8 j + wv, j = 64 k + lane), so that a run of heavy words spreads
-    // over all eight waves instead of one wave's batch
-    const int64_t wfirst = il ? wv : (int64_t)wv * 64, lstride = il ? SNW : 1;
-    for (int64_t k0 = 0; sb + k0 * SNW + wfirst < se; k0 += 64) {
-        const int64_t s = sb + k0 * SNW + wfirst + lane * lstride;
+    // batches of 64 consecutive words per wave
+    for (int64_t k0 = 0; sb + k0 * SNW + (int64_t)wv * 64 < se; k0 += 64) {
+        const int64_t s = sb + k0 * SNW + (int64_t)wv * 64 + lane;
         int64_t rb = ra0, cb = cb0;
         int nr = 0, ncl = 0;
         if (s < se) {
@@ -1103,7 +430,7 @@ __global__ __launch_bounds__(SNT, OCC) void sparse_tile_kernel5(
             if (rpart) {                               // lists are sorted by set: trim both ends
                 int a = 0, en = nr;
                 for (int t = 0; t < nr; t++) {
-                    const int st = set[rb + t];
+                    const int st = (int)(rec_row(ent[rb + t]) >> 8);   // row code: set << 8 | rotation key
                     a += st < rlo;
                     en -= st >= rhi;
                 }
@@ -1111,27 +438,21 @@ __global__ __launch_bounds__(SNT, OCC) void sparse_tile_kernel5(
                 nr = en > a ? en - a : 0;
             }
         }
-        // v6: slots per row group / row groups (micro-tiles of RW x CW)
-        const int ncd = CW && !diag ? (ncl + CW - 1) / (CW ? CW : 1) : ncl;
-        const int nrd = RW && !diag ? (nr + RW - 1) / (RW ? RW : 1) : nr;
-        const int P = diag ? nr * (nr - 1) / 2 : nrd * ncd;
+        const int ncd = diag ? ncl : (ncl + 1) >> 1;   // column pairs per row (off-diagonal micro-tiles)
+        const int P = diag ? nr * (nr - 1) / 2 : nr * ncd;
         int incl = P;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const int v = __shfl_up(incl, o, 64);
             if (lane >= o) incl += v;
         }
-        // pre < 2^24 (64 words x 128 x 128 products), ncol <= 128
-        // 1 / ncd; v6 with one row per slot: 1 / (2 ncd) for the correction-free quotient
-        const float rden = CW && RW <= 1 && !CONSEC && !diag ? 2.0f * (float)ncd : (float)ncd;
-        const int rcp = __float_as_int(ncd ? __builtin_amdgcn_rcpf(rden) : 0.0f);
-        rec[wv][lane] = make_int4((incl - P) | (ncl << 24), (int32_t)(rb - ra0), (int32_t)(cb - cb0),
-                                  (RW > 1 || CONSEC) && !diag ? (rcp & ~0xFF) | nr : rcp);
+        // first slot < 2^24 (64 words x 128 x 128 products), ncol <= 128
+        const int rcp = __float_as_int(ncd ? __builtin_amdgcn_rcpf(2.0f * (float)ncd) : 0.0f);
+        rec[wv][lane] = make_int4((incl - P) | (ncl << 24), (int32_t)(rb - ra0), (int32_t)(cb - cb0), rcp);
         const int total = __builtin_amdgcn_readlane(incl, 63);      // uniform: the walk's loop stays scalar
         __builtin_amdgcn_wave_barrier();
-        if (diag) sparse_walk5<SUN, true>(rec[wv], incl, total, lane, e, zA, cnt, mirror);
-        else if (CW) sparse_walk6<SUN, RW ? RW : 1, CW ? CW : 1, CONSEC>(rec[wv], incl, total, lane, e, zB, cnt);
-        else sparse_walk5<SUN, false>(rec[wv], incl, total, lane, e, zB, cnt, false);
+        if (diag) sparse_walk<SUN, true>(rec[wv], incl, total, lane, e, zA, cnt, mirror);
+        else sparse_walk<SUN, false>(rec[wv], incl, total, lane, e, zB, cnt, false);
         __builtin_amdgcn_wave_barrier();
     }
     if (ch < slabs) {
@@ -1176,8 +497,8 @@ __global__ __launch_bounds__(SNT, OCC) void sparse_tile_kernel5(
         cnt_pair(t, a, b);
         const int64_t i = A * SB + a, j = B * SB + b;
         if (i < r0 || i >= r1 || j < c0 || j >= c1 || (upper && j <= i)) continue;
-        const int v = (int)((cnt[t >> 1] >> ((t & 1) << 4)) & 0xFFFFu) +
-                      (ch == 0 ? (int)Us - nc[i] - nc[j] + dense_pair(dbits, Wdp, N, i, j) : 0);
+        // the constant part once per pair: by chunk 0 (chunks flush with atomics)
+        const int v = (int)((cnt[t >> 1] >> ((t & 1) << 4)) & 0xFFFFu) + (ch == 0 ? (int)Us - nc[i] - nc[j] : 0);
         if (v) atomicAdd(I + (i - r0) * ldI + (j - c0), v);
     }
 }
@@ -1196,8 +517,7 @@ __global__ __launch_bounds__(256) void sparse_reduce_kernel(const int32_t* __res
                                                             const int32_t* __restrict__ nc, int64_t Us, int64_t r0,
                                                             int64_t r1, int64_t c0, int64_t c1, int upper,
                                                             int32_t* __restrict__ I, int64_t ldI,
-                                                            const unsigned long long* __restrict__ dbits,
-                                                            int64_t Wdp, int64_t N, const uint32_t* __restrict__ rp_key,
+                                                            const uint32_t* __restrict__ rp_key,
                                                             const uint32_t* __restrict__ rp_w,
                                                             const int64_t* __restrict__ rp_off,
                                                             double* __restrict__ D, int64_t ldD,
@@ -1245,7 +565,7 @@ __global__ __launch_bounds__(256) void sparse_reduce_kernel(const int32_t* __res
         cnt_pair(t, a, b);
         const int64_t i = (int64_t)tiles[tile].x * SB + a, j = (int64_t)tiles[tile].y * SB + b;
         if (i < r0 || i >= r1 || j < c0 || j >= c1 || (upper && j <= i)) continue;
-        int v = (int)Us - nc[i] - nc[j] + dense_pair(dbits, Wdp, N, i, j) + (int)tot;
+        int v = (int)Us - nc[i] - nc[j] + (int)tot;
         if (D && i == j) v = (int)(soff[i + 1] - soff[i]);        // a set with itself (self_pairs_kernel)
         if (D) {                             // fused: the only writer of I over the region, then D
             I[(i - r0) * ldI + (j - c0)] = v;
@@ -1308,20 +628,15 @@ void free_sparse(gdist_sets* s) {
     s->plans.clear();
     s->dbits.release();
     s->sp_off.release();
-    s->sp_word.release();
-    s->sp_set.release();
     s->sp_ent.release();
     s->sp_nc.release();
     s->sparse = false;
     s->Wd = s->Ws = s->sp_entries = s->sp_U = 0;
     s->sp_bucket_bits.clear();
-    s->sp_cost.clear();
     s->sp_nbk = 0;
     s->sp_pos_words = 0;
     s->sp_fold_dense = false;
     s->sp_fold_slabs = 0;
-    s->sp_dT.release();
-    s->sp_win = 0;
     s->sp_products = s->sp_items = 0.0;
 }
 
@@ -1377,31 +692,6 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
         if (sparse) { sw.push_back((int32_t)w); products += 0.5 * zz * zz; }
         else dw.push_back((int32_t)w);
     }
-    // Absorbing the dense words into the sparse tier (option sparse_absorb =
-    // 1) removes their tile launch (C2: 49 words, z 277-998, 0.08 + 0.05 ms
-    // of tiles beside the sparse kernel) at the price of their products. On
-    // C2 that lost (step 0.279 vs 0.251 ms, profiles/r02/sparse6/): the
-    // launch overlaps the sparse kernel, and the modelled fixed cost below
-    // overstates it, so absorbing is opt-in; the model is reported by trace.
-    if (!dw.empty() && ctx->option(OPT_SPARSE_ABSORB, 0) != 0) {
-        double absorb_s = 0.0, absorb_products = 0.0;
-        for (int32_t w : dw) {
-            const double zz = (double)z[w];
-            absorb_products += 0.5 * zz * zz;
-            absorb_s += 0.5 * zz * zz / kSparseProductsPerS + tiles / kSparseItemsPerS;
-        }
-        const double keep_s = kDenseLaunchFixedS + pairs * (double)ceil_div((int64_t)dw.size(), 16) * 16.0 /
-                                                       kDenseWordPairsPerS;
-        if (ctx->trace())
-            fprintf(stderr, "gdist: absorbing %zu dense words: modelled %.1f us of products vs %.1f us launch\n",
-                    dw.size(), absorb_s * 1e6, keep_s * 1e6);
-        {
-            sw.clear();
-            for (int64_t w = 0; w < Wv; w++) sw.push_back((int32_t)w);
-            dw.clear();
-            products += absorb_products;
-        }
-    }
     const int64_t Ws = (int64_t)sw.size(), Wd = (int64_t)dw.size();
     if (ctx->trace() && Wd) {
         std::vector<int32_t> zd;
@@ -1438,11 +728,8 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
     int64_t total = 0;
     d2h(&total, s->sp_off.as<int64_t>() + nblk * Ws, 8, st);
     GD_REQUIRE(total < (int64_t(1) << 32), "sparse entries exceed 32-bit offsets");
-    s->sp_word.alloc(total * 8 + 8, st);
-    s->sp_set.alloc(total + 8, st);
-    // word[total] = 0: the sentinel entry v5's idle product slots read
-    GD_HIP(hipMemsetAsync(s->sp_word.as<unsigned long long>() + total, 0, 8, st));
-    GD_HIP(hipMemsetAsync(s->sp_set.as<uint8_t>() + total, 0, 8, st));
+    // the entries' words and set bytes, turned into the kernel's records below
+    DevBuf sp_word(total * 8 + 8, st), sp_set(total + 8, st);
     s->sp_nc.alloc(N * 4, st);
     GD_HIP(hipMemsetAsync(s->sp_nc.p, 0, N * 4, st));
     const int64_t nbk = ceil_div(Ws, int64_t(1) << kBucketShift);
@@ -1450,7 +737,7 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
     GD_HIP(hipMemsetAsync(dbb.p, 0, (size_t)N * nbk * 4, st));
     sparse_fill_kernel<<<gs, 256, 0, st>>>(bits, N, W, U, dsw.as<int32_t>(), dsp.as<uint8_t>(), Ws,
                                            s->sp_off.as<int64_t>(),
-                                           s->sp_word.as<unsigned long long>(), s->sp_set.as<uint8_t>(),
+                                           sp_word.as<unsigned long long>(), sp_set.as<uint8_t>(),
                                            s->sp_nc.as<int32_t>(), dbb.as<int32_t>(), nbk);
     GD_HIP(hipGetLastError());
     {   // complement bits of every set per bucket of 1024 sparse words, kept
@@ -1463,8 +750,8 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
     s->sp_ent.alloc(total * 16 + 64, st);
     GD_HIP(hipMemsetAsync(s->sp_ent.as<ulonglong2>() + total, 0, 64, st));      // the sentinel records
     if (total)
-        sparse_records_kernel<<<grid_for(total), 256, 0, st>>>(s->sp_word.as<unsigned long long>(),
-                                                                s->sp_set.as<uint8_t>(), total,
+        sparse_records_kernel<<<grid_for(total), 256, 0, st>>>(sp_word.as<unsigned long long>(),
+                                                                sp_set.as<uint8_t>(), total,
                                                                 s->sp_ent.as<ulonglong2>());
     GD_HIP(hipGetLastError());
     if (Wdp) {
@@ -1475,54 +762,6 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
                                                                s->dbits.as<unsigned long long>());
         GD_HIP(hipGetLastError());
     }
-    // v2 windows: the most aligned consecutive sparse words (64, 32, ... 4)
-    // whose entries fit the staging arrays in every block (a word holds at
-    // most 128 entries per block, so 4 words always fit)
-    {
-        std::vector<int64_t> ho(nblk * Ws + 1);
-        d2h(ho.data(), s->sp_off.as<int64_t>(), (nblk * Ws + 1) * 8, st);
-        s->sp_win = 0;
-        for (int win = 64; win >= 4 && !s->sp_win; win >>= 1) {
-            int64_t mx = 0;
-            for (int64_t b = 0; b < nblk; b++)
-                for (int64_t m = 0; m < Ws; m += win) {
-                    const int64_t e = std::min<int64_t>(Ws, m + win);
-                    mx = std::max(mx, ho[b * Ws + e] - ho[b * Ws + m]);
-                }
-            if (mx <= kSparseStageEntries) s->sp_win = win;
-        }
-        // each word's modelled cost over all tiles, in products: the pair
-        // products of its lists (diagonal tiles: pairs within one list) and
-        // the tile visits; sparse_matrix cuts chunks at equal cost
-        s->sp_cost.assign(Ws + 1, 0.0);
-        const double visit = (double)nblk * (double)(nblk + 1) / 2 * kSparseProductsPerS / kSparseItemsPerS;
-        for (int64_t m = 0; m < Ws; m++) {
-            double se1 = 0.0;
-            for (int64_t b = 0; b < nblk; b++) se1 += (double)(ho[b * Ws + m + 1] - ho[b * Ws + m]);
-            // sum_{a<b} e_a e_b + sum_a e_a (e_a - 1) / 2 = (se1^2 - se1) / 2
-            s->sp_cost[m + 1] = s->sp_cost[m] + 0.5 * (se1 * se1 - se1) + visit;
-        }
-        if (ctx->trace()) {               // entries per (block, word): the shape of the tile walk
-            int64_t h[34] = {0};
-            double pr = 0.0, cells8 = 0.0;
-            for (int64_t b = 0; b < nblk; b++)
-                for (int64_t m = 0; m < Ws; m++) {
-                    const int64_t e = ho[b * Ws + m + 1] - ho[b * Ws + m];
-                    h[e <= 32 ? e : 33]++;
-                }
-            for (int64_t m = 0; m < Ws; m++)
-                for (int64_t a = 0; a < nblk; a++)
-                    for (int64_t b = a + 1; b < nblk; b++) {
-                        const int64_t ea = ho[a * Ws + m + 1] - ho[a * Ws + m];
-                        const int64_t eb = ho[b * Ws + m + 1] - ho[b * Ws + m];
-                        pr += (double)ea * eb;
-                        cells8 += 64.0 * (double)((ea + 7) / 8) * (double)((eb + 7) / 8);
-                    }
-            fprintf(stderr, "gdist: sparse entries per (block, word):");
-            for (int k = 0; k < 34; k++) fprintf(stderr, " %lld", (long long)h[k]);
-            fprintf(stderr, "\ngdist: off-diagonal products %.4g, 8x8 grid lanes %.4g\n", pr, cells8);
-        }
-    }
     int64_t Us = 0;                       // valid bits of the complement-sparse words
     int64_t npos = 0;
     for (int32_t w : sw) {
@@ -1530,27 +769,15 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
         Us += (w + 1) * 64 <= U ? 64 : U - (int64_t)w * 64;
     }
     s->sp_pos_words = npos;
-    // A few dense words are counted in the flush of the sparse counters
-    // instead of a dense tile launch: the launch's per-tile accumulator flush
-    // cost C2's 16-64 dense words 0.09-0.15 ms beside the sparse kernel, the
-    // fold reads 2 x Wdp words per pair from L2 (option fold_dense_words)
-    // The dense words counted inside the v5 / v6 tile kernel (option
-    // sparse_fold, default up to 64 words): chunk c < Wdp / 8 of every tile
-    // adds words [8c, 8c + 8) of its 128 x 128 pairs into its LDS counters
-    // (~2 us per such workgroup), so no dense-word tile launch shares the
-    // CUs with the sparse kernel (C2: 0.09 + 0.04 ms of tiles beside it)
-    const int sk = (int)ctx->option(OPT_SPARSE_KERNEL, 6);
-    if (Wdp > 0 && (sk == 5 || sk == 6) && Wdp <= ctx->option(OPT_SPARSE_FOLD, 64) &&
-        !(Wdp <= ctx->option(OPT_FOLD_DENSE_WORDS, kFoldDenseWords))) {
+    // The dense words counted inside the tile kernel (option sparse_fold,
+    // default up to 64 words): chunk c < Wdp / 8 of every tile adds words
+    // [8c, 8c + 8) of its 128 x 128 pairs into its LDS counters (~2 us per
+    // such workgroup), so no dense-word tile launch shares the CUs with the
+    // sparse kernel (C2: 0.09 + 0.04 ms of tiles beside it); past the option
+    // the dense words get their own tile launch (bitset_matrix)
+    if (Wdp > 0 && Wdp <= ctx->option(OPT_SPARSE_FOLD, 64)) {
         s->sp_fold_dense = true;
         s->sp_fold_slabs = (int)(Wdp / kFoldSlabWords);
-    }
-    if (!s->sp_fold_dense) s->sp_fold_dense = Wdp > 0 && Wdp <= ctx->option(OPT_FOLD_DENSE_WORDS, kFoldDenseWords);
-    if (s->sp_fold_dense && s->sp_fold_slabs == 0) {
-        s->sp_dT.alloc((size_t)N * Wdp * 8, st);
-        transpose_words_kernel<<<grid_for(N * Wdp), 256, 0, st>>>(s->dbits.as<unsigned long long>(), N, Wdp,
-                                                                 s->sp_dT.as<unsigned long long>());
-        GD_HIP(hipGetLastError());
     }
     GD_HIP(hipStreamSynchronize(st));
     s->sparse = true;
@@ -1646,55 +873,18 @@ void sparse_plan(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, in
                 if (upper && cmax <= rmin) continue;
                 tiles.push_back(make_int2((int)A, (int)B));
             }
-        // Heaviest tiles first (workgroups are dispatched in blockIdx order,
-        // tile-major): whole off-diagonal tiles, then row-partial ones, then
-        // the diagonal tiles (pairs x < y of one list, ~0.45 of a tile), so
-        // the last dispatch round is made of the light ones (option
-        // sparse_tile_order = 1; measured neutral on C2, 0.126 vs 0.124 ms,
-        // so row-major order stays the default)
-        if (ctx->option(OPT_SPARSE_TILE_ORDER, 0) != 0) {
-            auto weight = [&](const int2& t) {
-                const int64_t A = t.x, B = t.y;
-                const double rows = (double)(std::min(r1, (A + 1) * SB) - std::max(r0, A * SB));
-                const double cols = (double)(std::min(c1, (B + 1) * SB) - std::max(c0, B * SB));
-                const bool diag = A == B && rows == (double)std::min<int64_t>(SB, s->nsets - A * SB);
-                return rows * cols * (diag ? 0.45 : 1.0);
-            };
-            std::stable_sort(tiles.begin(), tiles.end(),
-                             [&](const int2& a, const int2& b) { return weight(a) > weight(b); });
-        }
         sc.ntiles = (int64_t)tiles.size();
         // enough workgroups to fill the chip, each over >= 512 sparse words
         const int64_t target = (int64_t)ctx->cus * std::max<int64_t>(1, ctx->option(OPT_SPARSE_WG_PER_CU, 4));
         const int64_t budget = ctx->option(OPT_SPARSE_PART_BUDGET, int64_t(1) << 30);
         const int64_t tile_bytes = SB * SB * 2;
-        // Chunk bounds: equal word counts, or (option sparse_balance) equal
-        // modelled cost (sp_cost: each word's products over all tiles +
-        // visits), so that a run of heavy words (C2 with sparse_absorb: the
-        // ~50 words half the sets lack, at the end of the locus order) gets
-        // narrow chunks instead of one chunk many times the others' work; at
-        // most `cap` words per chunk. On C2 as built (no absorb) the equal
-        // split is faster: the cost split makes 110 smaller chunks (kernel
-        // 0.145 vs 0.136 ms, reduce 0.029 vs 0.034; profiles/r02/sparse6/).
-        const bool balance = ctx->option(OPT_SPARSE_BALANCE, 0) != 0;
         // chunks that fold a dense-word slab (the first sp_fold_slabs) hold
         // at most kChunkWords - kFoldSlabWords words: every chunk does
         const int64_t cap = s->sp_fold_slabs ? kChunkWords - kFoldSlabWords : kChunkWords;
-        auto make_bounds = [&](int64_t n, int64_t wcap) {
-            const int64_t Ws = s->Ws;
-            const bool costed = balance && (int64_t)s->sp_cost.size() == Ws + 1 && s->sp_cost[Ws] > 0.0;
-            auto cum = [&](int64_t m) { return costed ? s->sp_cost[m] : (double)m; };
-            const double step = cum(Ws) / (double)n;
-            std::vector<int32_t> b{0};
-            double next = step;
-            for (int64_t m = 0; m + 1 < Ws; m++) {            // close after word m at the quantile or the cap
-                const double end = cum(m + 1);
-                if (end >= next || m + 1 - b.back() >= wcap) {
-                    b.push_back((int32_t)(m + 1));
-                    while (next <= end) next += step;
-                }
-            }
-            b.push_back((int32_t)Ws);
+        // chunk bounds at equal word counts (n chunks)
+        auto make_bounds = [&](int64_t n) {
+            std::vector<int32_t> b;
+            for (int64_t c = 0; c <= n; c++) b.push_back((int32_t)(s->Ws * c / n));
             return b;
         };
         // A chunk is exact when it holds <= kChunkWords words (64 x 1023 <
@@ -1726,27 +916,20 @@ void sparse_plan(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, in
         if (sc.ntiles) {
             int64_t n0 = std::max<int64_t>(std::max<int64_t>(ceil_div(s->Ws, cap), s->sp_fold_slabs),
                                            std::min<int64_t>(ceil_div(s->Ws, 512), ceil_div(target, sc.ntiles)));
-            // whole groups of 8 chunks for the XCD-mapped v5 / v6 launch
-            const int sk = (int)ctx->option(OPT_SPARSE_KERNEL, 6);
-            if ((sk == 5 || sk == 6) && ctx->option(OPT_SPARSE_XCD, 0) != 0 && n0 > 8)
-                n0 = ceil_div(n0, 8) * 8;                // (empty chunks are allowed)
-            if (balance) bnd = make_bounds(n0, cap);
-            else
-                for (int64_t c = 0; c <= n0; c++) bnd.push_back((int32_t)(s->Ws * c / n0));
+            bnd = make_bounds(n0);
             // Past the partial budget (many tiles: N >> 1000), fewer and
             // longer chunks where the complement bits allow it (bounds_ok), so
             // that the partials fit; otherwise the chunks flush with atomics.
             const int64_t nb0 = (int64_t)bnd.size() - 1;
             if (sc.ntiles * nb0 * tile_bytes > budget) {
                 for (int64_t fewer = std::max<int64_t>(1, budget / (sc.ntiles * tile_bytes)); fewer < nb0; fewer *= 2) {
-                    auto b = make_bounds(fewer, INT64_MAX);
+                    auto b = make_bounds(fewer);
                     if (bounds_ok(b)) { bnd = b; break; }
                 }
             }
             if (ctx->has_option(OPT_SPARSE_CHUNKS))   // tests: a given chunk count (exactness still checked)
                 bnd = make_bounds(std::max<int64_t>(s->sp_fold_slabs,
-                                                    std::max<int64_t>(1, std::min<int64_t>(s->Ws, ctx->option(OPT_SPARSE_CHUNKS, 1)))),
-                                  INT64_MAX);
+                                                    std::max<int64_t>(1, std::min<int64_t>(s->Ws, ctx->option(OPT_SPARSE_CHUNKS, 1)))));
             GD_REQUIRE(bounds_ok(bnd), "sparse chunks exceed the 16-bit counter bound");
         }
         const int64_t nch = sc.ntiles ? (int64_t)bnd.size() - 1 : 0;
@@ -1763,21 +946,11 @@ void sparse_plan(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, in
         const int64_t part_bytes = sc.ntiles * sc.nchunks * tile_bytes;
         sc.use_part = sc.nchunks > 1 && part_bytes <= budget;
         if (sc.use_part) sc.part.alloc((size_t)part_bytes, st);
-        if (ctx->trace() && sc.ntiles) {
-            double cmax = 0.0, csum = 0.0;
-            for (size_t c = 0; c + 1 < bnd.size(); c++) {
-                const double cc = s->sp_cost.empty() ? 0.0 : s->sp_cost[bnd[c + 1]] - s->sp_cost[bnd[c]];
-                cmax = std::max(cmax, cc);
-                csum += cc;
-            }
-            fprintf(stderr, "gdist: sparse chunks: %lld, modelled cost max / mean %.2f\n", (long long)nch,
-                    csum > 0 ? cmax / (csum / (double)nch) : 0.0);
-        }
         if (ctx->trace())
-            fprintf(stderr, "gdist: sparse plan rows [%lld,%lld) cols [%lld,%lld): %lld tiles x %d chunks, %s, win %d, "
+            fprintf(stderr, "gdist: sparse plan rows [%lld,%lld) cols [%lld,%lld): %lld tiles x %d chunks, %s, "
                             "%lld of %lld sparse words positive\n",
                     (long long)r0, (long long)r1, (long long)c0, (long long)c1, (long long)sc.ntiles, sc.nchunks,
-                    sc.use_part ? "partials" : "atomic flush", s->sp_win, (long long)s->sp_pos_words,
+                    sc.use_part ? "partials" : "atomic flush", (long long)s->sp_pos_words,
                     (long long)s->Ws);
         GD_REQUIRE(sc.ntiles * sc.nchunks < (int64_t(1) << 31), "sparse grid too large");
         if (sc.use_part) rare_pair_table(ctx, s, r0, r1, c0, c1, upper, tiles, st, sc);
@@ -1793,74 +966,21 @@ bool sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     if (sc.ntiles == 0) return false;
     const int nchunks = sc.nchunks;
     const int64_t nt = sc.ntiles;
-    // Kernel 6 (default): v5's walk over 1 x 2 micro-tiles, 3 slots (6
-    // products) per lane in flight (C2 A/B, profiles/r02/sparse6/). v1: 6
-    // products per lane in flight (profiles/r01/sparse/sweep_unroll_c2.txt).
+    // 3 slots (6 products) per lane in flight (C2 A/B, profiles/r02/sparse6/).
     // __launch_bounds__'s second argument is the minimum waves per SIMD: 8
     // holds the registers under the 8-wave budget (4 workgroups per CU,
-    // LDS-limited) where 3 let the SGPRs reach 112 (3 per CU): v1 0.310 ->
-    // 0.298 ms (profiles/r01/sparse/occ_{3,8}.json; option sparse_occ = 3).
-    int version = (int)ctx->option(OPT_SPARSE_KERNEL, 6);
-    const int sun = (int)ctx->option(OPT_SPARSE_SUN, version == 6 ? 3 : version == 5 ? 4 : 6);
-    const unsigned long long* fold =
-        s->sp_fold_dense && s->sp_fold_slabs == 0 ? s->sp_dT.as<unsigned long long>() : nullptr;
-    GD_REQUIRE(s->sp_fold_slabs == 0 || version == 5 || version == 6,
-               "dense words folded into the v5 / v6 tile kernel (option sparse_fold): build with that kernel");
-    if ((version == 2 || version == 4) && s->sp_win == 0) version = 1;
-    auto kern = ctx->option(OPT_SPARSE_OCC, 8) == 3 ? sparse_tile_kernel<6, 3>
-                : sun == 4            ? sparse_tile_kernel<4, 8>
-                : sun == 8            ? sparse_tile_kernel<8, 8>
-                                      : sparse_tile_kernel<6, 8>;
-    if (version == 3)                  // v1 over 16-byte records
-        kern = sun == 4 ? sparse_tile_kernel<4, 8, true>
-               : sun == 8 ? sparse_tile_kernel<8, 8, true>
-                          : sparse_tile_kernel<6, 8, true>;
-    const int abl = (int)ctx->option(OPT_SPARSE_ABL, 0);
+    // LDS-limited; profiles/r01/sparse/occ_{3,8}.json)
+    const int sun = (int)ctx->option(OPT_SPARSE_SUN, 3);
+    GD_REQUIRE(sun >= 2 && sun <= 4, "sparse_sun: 2, 3 or 4");
+    auto kern = sun == 2 ? sparse_tile_kernel<2> : sun == 4 ? sparse_tile_kernel<4> : sparse_tile_kernel<3>;
     const bool timed = ctx->option(OPT_TIME_SPARSE, 0) != 0 && !ctx->capturing;
     if (timed) GD_HIP(hipEventRecord(ctx->ev_sp0, st));
-    if (version == 4 && s->sp_win > 0)
-        (sun == 4 ? sparse_tile_kernel4<4, 6> : sun == 1 ? sparse_tile_kernel4<1, 6> : sparse_tile_kernel4<2, 6>)<<<
-            (unsigned)(nt * nchunks), S2T, 0, st>>>(
-            s->sp_off.as<int64_t>(), s->sp_word.as<unsigned long long>(), s->sp_set.as<uint8_t>(),
-            s->sp_nc.as<int32_t>(), s->sp_U, s->Ws, s->sp_win, sc.tiles.as<int2>(), sc.bounds.as<int32_t>(), nchunks, r0, r1, c0, c1,
-            upper ? 1 : 0, d_I, ldI, sc.use_part ? sc.part.as<int32_t>() : nullptr, fold, s->Wd, s->nsets);
-    else if (version == 5 || version == 6) {
-        const int shape = (int)ctx->option(OPT_SPARSE_SHAPE, 12);
-        GD_REQUIRE(version == 5 || shape == 12 || shape == 14 || shape == 22 || shape == 112,
-                   "sparse_shape: 12, 14, 22 or 112");
-        GD_REQUIRE(version == 6 ? sun >= 2 && sun <= (shape == 12 || shape == 112 ? 4 : 3) : sun == 4 || sun == 6,
-                   "sparse_sun out of range for the kernel");
-        auto k5 = version == 5 ? (sun == 4 ? sparse_tile_kernel5<4, 8> : sparse_tile_kernel5<6, 8>)
-                  : shape == 14 ? (sun == 2 ? sparse_tile_kernel5<2, 8, 1, 4> : sparse_tile_kernel5<3, 8, 1, 4>)
-                  : shape == 22 ? (sun == 2 ? sparse_tile_kernel5<2, 8, 2, 2> : sparse_tile_kernel5<3, 8, 2, 2>)
-                  : shape == 112 ? (sun == 2 ? sparse_tile_kernel5<2, 8, 1, 2, true>
-                                   : sun == 4 ? sparse_tile_kernel5<4, 8, 1, 2, true>
-                                              : sparse_tile_kernel5<3, 8, 1, 2, true>)
-                  : sun == 2    ? sparse_tile_kernel5<2, 8, 1, 2>
-                  : sun == 4    ? sparse_tile_kernel5<4, 8, 1, 2>
-                                : sparse_tile_kernel5<3, 8, 1, 2>;
-        const bool xmap = ctx->option(OPT_SPARSE_XCD, 0) != 0;
-        const int64_t grid = xmap ? ceil_div(nchunks, 8) * 8 * nt : nt * nchunks;
-        GD_REQUIRE(grid < (int64_t(1) << 31), "sparse grid too large");
-        k5<<<(unsigned)grid, SNT, 0, st>>>(
-            s->sp_off.as<int64_t>(), s->sp_set.as<uint8_t>(), s->sp_ent.as<ulonglong2>(), s->sp_nc.as<int32_t>(),
-            s->sp_U, s->Ws, sc.tiles.as<int2>(), sc.bounds.as<int32_t>(), nchunks, r0, r1, c0, c1, upper ? 1 : 0, d_I, ldI,
-            sc.use_part ? sc.part.as<int32_t>() : nullptr, fold, s->Wd, s->nsets,
-            ctx->option(OPT_SPARSE_BALANCE, 0) != 0 ? 1 : 0, s->dbits.as<unsigned long long>(), s->sp_fold_slabs,
-            (int)nt, xmap ? 1 : 0);
-    }
-    else if (version == 2)
-        (abl == 1 ? sparse_tile_kernel2<4, 6, 1> : abl == 2 ? sparse_tile_kernel2<4, 6, 2> : sparse_tile_kernel2<4, 6, 0>)<<<(unsigned)(nt * nchunks), S2T, 0, st>>>(
-            s->sp_off.as<int64_t>(), s->sp_word.as<unsigned long long>(), s->sp_set.as<uint8_t>(),
-            s->sp_nc.as<int32_t>(), s->sp_U, s->Ws, s->sp_win, sc.tiles.as<int2>(), sc.bounds.as<int32_t>(), nchunks, r0, r1, c0, c1,
-            upper ? 1 : 0,
-            d_I, ldI, sc.use_part ? sc.part.as<int32_t>() : nullptr, fold, s->Wd, s->nsets);
-    else
-    kern<<<(unsigned)(nt * nchunks), SNT, 0, st>>>(
-        s->sp_off.as<int64_t>(), s->sp_word.as<unsigned long long>(), s->sp_set.as<uint8_t>(),
-        s->sp_ent.as<ulonglong2>(), s->sp_nc.as<int32_t>(),
-        s->sp_U, s->Ws, sc.tiles.as<int2>(), sc.bounds.as<int32_t>(), nchunks, r0, r1, c0, c1, upper ? 1 : 0, d_I, ldI,
-        sc.use_part ? sc.part.as<int32_t>() : nullptr, fold, s->Wd, s->nsets);
+    const int64_t grid = nt * nchunks;
+    GD_REQUIRE(grid < (int64_t(1) << 31), "sparse grid too large");
+    kern<<<(unsigned)grid, SNT, 0, st>>>(s->sp_off.as<int64_t>(), s->sp_ent.as<ulonglong2>(), s->sp_nc.as<int32_t>(),
+                                         s->sp_U, s->Ws, sc.tiles.as<int2>(), sc.bounds.as<int32_t>(), nchunks, r0, r1,
+                                         c0, c1, upper ? 1 : 0, d_I, ldI, sc.use_part ? sc.part.as<int32_t>() : nullptr,
+                                         s->Wd, s->nsets, s->dbits.as<unsigned long long>(), s->sp_fold_slabs);
     GD_HIP(hipGetLastError());
     if (timed) {
         GD_HIP(hipEventRecord(ctx->ev_sp1, st));
@@ -1869,7 +989,7 @@ bool sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     if (sc.use_part) {
         sparse_reduce_kernel<<<(unsigned)(nt * (SB * SB / kReduceCnt / kReduceGroups)), 256, 0, st>>>(
             sc.part.as<int32_t>(), nchunks, sc.tiles.as<int2>(), s->sp_nc.as<int32_t>(), s->sp_U, r0, r1, c0, c1,
-            upper ? 1 : 0, d_I, ldI, fold, s->Wd, s->nsets,
+            upper ? 1 : 0, d_I, ldI,
             sc.rare_in ? sc.rp_key.as<uint32_t>() : nullptr, sc.rare_in ? sc.rp_w.as<uint32_t>() : nullptr,
             sc.rare_in ? sc.rp_off.as<int64_t>() : nullptr, ep ? ep->D : nullptr, ep ? ep->ldD : 0,
             ep ? ep->off : nullptr, ep ? ep->empty_nan : 0);

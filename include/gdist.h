@@ -121,7 +121,10 @@ int  gdist_ctx_create(int device, gdist_ctx** out);
 int  gdist_ctx_destroy(gdist_ctx* ctx);
 int  gdist_ctx_synchronize(gdist_ctx* ctx);
 /* HIP-event time of the last intersect/sketch matrix call's main kernel(s)
- * and of the whole call, in ms (recorded on the stream they run on). */
+ * and of the whole call, in ms (recorded on the stream they run on); NaN when
+ * the call recorded none (a graph-replayed step into device outputs records
+ * no events unless option "step_timing" = 1; a call without a kernel of its
+ * own has no kernel time). */
 int  gdist_ctx_last_timing(gdist_ctx* ctx, double* kernel_ms, double* call_ms, int64_t* launches);
 /* Kernel times (ms, HIP events on the stream they ran on) of the last
  * min(max, 256) matrix calls, oldest first, *count of them; waits for them. */
@@ -131,9 +134,12 @@ int  gdist_ctx_recent_timings(gdist_ctx* ctx, int max, double* kernel_ms, int* c
  * -1 when none was timed. Waits for it. */
 int  gdist_ctx_sparse_kernel_ms(gdist_ctx* ctx, double* ms);
 /* Tuning options of a context: the A/B switches of DESIGN.md §5 by name
- * ("rare_t", "bitset_kernel", "sparse", "sparse_zmax", "sketch_k", ...;
+ * ("rare_t", "bitset_diag", "sparse", "sparse_zmax", "sketch_k", ...;
  * gdist_ctx_option_name enumerates them, EINVAL past the last). Every option
- * defaults to the measured best; GDIST_OPTION_DEFAULT restores it. The
+ * defaults to the measured best; GDIST_OPTION_DEFAULT restores it. No option
+ * changes a result: each picks among exact kernels, tilings, thresholds or
+ * setup paths, and the parity tests run every non-default value against the
+ * oracle; an unknown name is EINVAL. The
  * library never reads the environment, so every host (JNI, ctypes) sharing a
  * context gets the same kernels (concurrent getDistance callers,
  * MethodTableProcessor.java:275). Options read at build time (rare_t,
@@ -178,7 +184,7 @@ int  gdist_sets_build_bitsets(gdist_sets* sets, unsigned flags);
 int  gdist_sets_build_bitsets_ex(gdist_sets* sets, unsigned flags, int64_t rare_threshold);
 /* Rare tier: threshold T, distinct posting lists and their member records.
  * Kmers with identical posting lists (e.g. every kmer covering one shared
- * variant) are one list weighted by their number (GDIST_RARE_DEDUP=0: one
+ * variant) are one list weighted by their number (option "rare_dedup" = 0: one
  * list per kmer); gdist_sets_rare_kmers gives the kmers before merging. */
 int  gdist_sets_rare_info(const gdist_sets* sets, int64_t* threshold, int64_t* lists, int64_t* records);
 int  gdist_sets_rare_kmers(const gdist_sets* sets, int64_t* kmers);
@@ -192,7 +198,7 @@ int  gdist_sets_bitset_info(const gdist_sets* sets, int64_t* dict_size, int64_t*
  * counted from the sets' complement words instead of the AND+popcount tiles.
  * Reports the sparse words, the dense words left to the tiles (padded) and
  * the complement entries (0s when the split was not worth building).
- * GDIST_SPARSE=0 / GDIST_LOCUS_ORDER=0 switch it off (A/B). */
+ * Options "sparse" = 0 / "locus_order" = 0 switch it off (A/B). */
 int  gdist_sets_sparse_info(const gdist_sets* sets, int64_t* sparse_words, int64_t* dense_words, int64_t* entries);
 /* The sparse words by side: counted from the sets' complement words (sets
  * lacking a commonly held kmer) or from their words (sets holding a rarely

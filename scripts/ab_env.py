@@ -14,6 +14,7 @@ n = int(os.environ.get("AB_N", "1000"))
 settings = [s for s in os.environ.get("AB_ENVS", "").split(";")]
 rounds = int(os.environ.get("AB_ROUNDS", "5"))
 ctx = gdist.Context(0)
+ctx.set_option("step_timing", 1)     # graph-replayed steps record their kernel times too
 g = synth.genomes(n, 2_000_000, 0.002, 2)
 blob, off = synth.to_blob(g); del g
 sets = gdist.KmerSets.from_sequences([blob[off[i]:off[i + 1]] for i in range(n)], 21, gdist.KmerType.DNA, 0, ctx)

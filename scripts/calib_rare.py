@@ -24,6 +24,7 @@ case = os.environ.get("CAL_CASE", "c2")
 c = CASES[case]
 N = c["n"]
 ctx = gdist.Context(0)
+ctx.set_option("step_timing", 1)     # graph-replayed steps record their kernel times too
 t = time.time()
 g = synth.genomes(N, c["length"], c["p_max"], c["cfg"], protein=c["protein"])
 blob, off = synth.to_blob(g); del g

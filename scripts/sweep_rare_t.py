@@ -9,6 +9,7 @@ from gdist import synth
 n = int(os.environ.get("SW_N", "1000")); L = int(os.environ.get("SW_LEN", "2000000"))
 Ts = [int(x) for x in os.environ.get("SW_T", "0,3,6,12,25,50,100,250").split(",")]
 ctx = gdist.Context(0)
+ctx.set_option("step_timing", 1)     # graph-replayed steps record their kernel times too
 g = synth.genomes(n, L, 0.002, 2)
 blob, off = synth.to_blob(g); del g
 seqs = [blob[off[i]:off[i + 1]] for i in range(n)]

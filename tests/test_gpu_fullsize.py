@@ -6,6 +6,15 @@
   0, 499 and 998 in full, bit-exact counts and fp64 distances. The oracle
   packs every genome (threads: the C restatement releases the GIL) and
   merges each row set against every column set.
+* C3 at its bench size (10,000 x 33,333 aa proteomes, protein k=8, p <= 0.10)
+  through METHOD_AUTO, which must pick the two-tier bitsets with a rare tier:
+  the bench's whole upper triangle into device outputs (the replayed step),
+  rows 0, 4,999 and 9,998 in full against the oracle
+  (FastaDistanceProcessor.java:157-186 shape).
+* C5 at its bench size (50,000 bottom-1000 sketches of 100 kbp genomes, DNA
+  k=21; WidthProcessor.java:178-185): the device sketches of a sample of
+  genomes against oracle.sketch, and full rows of the bench's whole-triangle
+  sketch matrix against oracle.sketch_distance over every column.
 * The round-1 fault sequence (a sorted and a bitset workload, then a pack, in
   one process) with its codes checked against the oracle.
 """
@@ -76,6 +85,104 @@ def test_c2_full_size_rows_vs_oracle(ctx, opts):
     assert (s0.build_bitsets(), s0.sparse_info()) == info
     I0, _ = s0.matrix((0, 200), (0, n), upper=False, method=gdist.METHOD_BITSET)
     assert np.array_equal(I0, I[:200])
+
+
+def _full_row(M, i):
+    """Row i of a square upper-triangle output: (j, i) for j < i, (i, j) for j > i."""
+    r = M[i].copy()
+    r[:i] = M[:i, i]
+    return r
+
+
+@pytest.mark.timeout(900)
+def test_c3_full_size_auto_vs_oracle(ctx):
+    import gdist
+    from gdist import synth
+    n, L = 10000, 33_333
+    g = synth.genomes(n, L, 0.10, 3, protein=True)           # bench.py's C3 workload (cfg seed 3)
+    blob, off = synth.to_blob(g)
+    del g
+    sets = gdist.KmerSets.from_blob(blob, off, 8, gdist.KmerType.PROT, 0, ctx)
+    chosen, cb, cs = sets.prepare(gdist.METHOD_AUTO)
+    assert chosen == gdist.METHOD_BITSET and 0 < cb < cs, (chosen, cb, cs)
+    thr, lists, recs = sets.rare_info()
+    assert thr > 2 and lists > 0 and recs > lists, "C3 must run the two-tier dictionary with a rare tier"
+    dI, dD = ctx.alloc(n * n * 4), ctx.alloc(n * n * 8)
+    for _ in range(3):                                       # plan + capture + replay, as the bench steps
+        sets.matrix_device(dI.ptr, dD.ptr, n, (0, n), (0, n), upper=True, method=gdist.METHOD_AUTO)
+    I = dI.to_host(np.int32).reshape(n, n)
+    D = dD.to_host(np.float64).reshape(n, n)
+    dI.free(); dD.free()
+    seqs = [bytes(blob[off[i]:off[i + 1]]) for i in range(n)]
+    del blob
+    rows = (0, 4999, 9998)
+    with cf.ThreadPoolExecutor(_threads()) as ex:
+        row_codes = list(ex.map(lambda i: oracle.kmer_codes(seqs[i], 8, 1, 0), rows))
+
+        def column(j):
+            cj = oracle.kmer_codes(seqs[j], 8, 1, 0)
+            return [(oracle.intersect(rc, cj), len(cj)) for rc in row_codes]
+        cols = list(ex.map(column, range(n)))
+    for r, (i, rc) in enumerate(zip(rows, row_codes)):
+        eI = np.array([cols[j][r][0] for j in range(n)], np.int64)
+        eD = np.array([oracle.distance(int(eI[j]), len(rc), int(cols[j][r][1])) for j in range(n)])
+        m = np.arange(n) != i
+        gi, gd = _full_row(I, i).astype(np.int64), _full_row(D, i)
+        assert np.array_equal(gi[m], eI[m]), (i, np.flatnonzero((gi != eI) & m)[:8])
+        assert bits_equal(gd[m], eD[m]), i
+
+
+@pytest.mark.timeout(900)
+def test_c5_full_size_vs_oracle(ctx):
+    import gdist
+    from gdist import synth
+    n, L, w = 50000, 100_000, 1000
+    g = synth.genomes(n, L, 0.05, 5)                          # bench.py's C5 workload (cfg seed 5)
+    blob, off = synth.to_blob(g)
+    del g
+    sets = gdist.KmerSets.from_blob(blob, off, 21, gdist.KmerType.DNA, 0, ctx)
+    sk = sets.sketches(w)
+    del sets
+    soff, sigs = sk.download()
+    assert len(soff) == n + 1 and np.all(np.diff(soff) == w), "100 kbp genomes hold more than 1000 kmers"
+    sig = [sigs[soff[i]:soff[i + 1]] for i in range(n)]
+    # the sketches themselves: a sample of genomes against the oracle
+    rng = np.random.default_rng(55)
+    sample = sorted({0, 24999, 49998, n - 1} | set(rng.choice(n, 300, replace=False).tolist()))
+
+    def oracle_sketch(i):
+        return oracle.sketch(oracle.kmer_codes(bytes(blob[off[i]:off[i + 1]]), 21, 0, 0), 21, 0, w)
+    with cf.ThreadPoolExecutor(_threads()) as ex:
+        osk = list(ex.map(oracle_sketch, sample))
+    del blob
+    for i, e in zip(sample, osk):
+        assert np.array_equal(sig[i], e), i
+    # the bench's whole upper triangle into device outputs (plan, replay)
+    dC, dD = ctx.alloc(n * n * 4), ctx.alloc(n * n * 8)
+    for _ in range(2):
+        sk.matrix_device(dC.ptr, dD.ptr, n, (0, n), (0, n), upper=True)
+    ctx.synchronize()
+
+    def expect(i):
+        e = [oracle.sketch_distance(sig[i], sig[j], w) for j in range(n)]
+        return np.array([c for _, c in e], np.int64), np.array([d for d, _ in e])
+    for i in (0, 24999):
+        eC, eD = expect(i)
+        gc = dC.to_host(np.int32, n - i - 1, i * n + i + 1).astype(np.int64)
+        gd = dD.to_host(np.float64, n - i - 1, i * n + i + 1)
+        assert np.array_equal(gc, eC[i + 1:]), (i, np.flatnonzero(gc != eC[i + 1:])[:8])
+        assert bits_equal(gd, eD[i + 1:]), i
+        # and 2,000 random pairs of the triangle
+    pairs = [(int(a), int(b)) for a, b in rng.integers(0, n, (4000, 2)) if a < b][:2000]
+    for a, b in pairs:
+        d, c = oracle.sketch_distance(sig[a], sig[b], w)
+        assert int(dC.to_host(np.int32, 1, a * n + b)[0]) == c and bits_equal(dD.to_host(np.float64, 1, a * n + b), [d])
+    dC.free(); dD.free()
+    # full rows (both sides of the diagonal) through a row-block call
+    for i in (24999, 49998):
+        C, Dr = sk.matrix((i, i + 1), (0, n))
+        eC, eD = expect(i)
+        assert np.array_equal(C[0].astype(np.int64), eC) and bits_equal(Dr[0], eD), i
 
 
 def test_pack_after_bitset_workload_regression(ctx):

@@ -17,9 +17,13 @@ def test_gpu_box_library_matches_tree():
 def test_option_roundtrip_and_errors(ctx):
     import gdist
     names = gdist.option_names()
-    for n in ("rare_t", "rare_kernel", "bitset_kernel", "sparse", "sparse_zmax", "sketch_k", "reps_block",
+    for n in ("rare_t", "rare_kernel", "bitset_diag", "sparse", "sparse_zmax", "sketch_k", "reps_block",
               "locus_order", "guides", "sparse_part_budget"):
         assert n in names
+    # round 3: superseded kernel variants and the result-changing ablation
+    # switch are gone; every remaining option preserves results
+    for n in ("sparse_abl", "sparse_kernel", "bitset_kernel", "sparse_shape", "sparse_occ", "fold_dense_words"):
+        assert n not in names
     c = gdist.Context(0)
     try:
         assert c.option("sparse") is None
@@ -70,3 +74,27 @@ def test_environment_does_not_change_kernels(monkeypatch):
         assert np.array_equal(I1[iu], I2[iu])
     finally:
         c.close()            # frees a, b, d first (a collection must not outlive its context)
+
+
+def test_plan_follows_options(ctx, opts):
+    """A region's cached launch plan is keyed by the options it reads: turning
+    option sparse_rare off on the same collection and region rebuilds the plan
+    (the rare tier then runs as its own kernel: 2 launches instead of the fused
+    step's 1), and every call stays oracle-exact."""
+    import gdist
+    import oracle
+    from gdist import synth
+    seqs = [bytes(r) for r in synth.genomes(300, 20000, 0.003, 11)]
+    sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
+    sets.build_bitsets()
+    assert sets.sparse_info()[0] > 0 and sets.rare_info()[1] > 0
+    off, codes = oracle.pack(seqs, 21, 0, 0)
+    eI, eD = oracle.matrix(off, codes, 0, 300, 0, 300, flags=0x100)
+    iu = np.triu_indices(300, 1)
+    launches = []
+    for rare in (None, 0, None):
+        opts(sparse_rare=rare)
+        I, D = sets.matrix(upper=True, method=gdist.METHOD_BITSET)
+        assert np.array_equal(I[iu], eI[iu]) and np.array_equal(D[iu].view(np.uint64), eD[iu].view(np.uint64))
+        launches.append(ctx.last_timing()[2])
+    assert launches == [1, 2, 1], launches

@@ -642,14 +642,43 @@ def test_rare_tier_thresholds_exact(ctx, T, kernel, dedup, opts):
     assert bits_equal(d, eD[0, cols])
 
 
-@pytest.mark.parametrize("mode", ["auto", "all_sparse", "mixed", "no_locus", "off", "atomic_flush", "kernel_v1",
-                                  "kernel_v2", "many_chunks", "two_sided", "mixed_fold", "mixed_fold_1chunk",
-                                  "kernel_v4", "kernel_v4_rows", "kernel_v5", "kernel_v5_rows", "kernel_v5_sun6",
-                                  "kernel_v5_atomic", "kernel_v6_rows", "kernel_v6_sun4", "kernel_v6_quads",
-                                  "kernel_v6_2x2", "kernel_v6_2x2_rows", "kernel_v6_atomic", "absorb",
-                                  "mixed_slabs", "mixed_slabs_atomic", "mixed_tiles", "unfused", "rare_kernel",
-                                  "unfused_rare_kernel", "fill_sort", "fill_direct", "pack_pairs", "pack_nosummary", "kernel_v6_consec", "kernel_v6_consec_rows",
-                                  "kernel_v6_consec_sun4"])
+SPARSE_MODES = {
+    "auto": {},
+    "all_sparse": {"sparse_zmax": 100000}, "mixed": {"sparse_zmax": 12},
+    "no_locus": {"locus_order": 0, "sparse_zmax": 40}, "off": {"sparse": 0},
+    # chunks flush with atomics (no partials within a zero budget)
+    "atomic_flush": {"sparse_zmax": 100000, "sparse_part_budget": 0, "sparse_chunks": 5},
+    # 1 x 2 micro-tiles with 2 / 3 (default) / 4 slots per lane in flight
+    "rows_sun2": {"sparse_zmax": 40, "sparse_sun": 2},
+    "sun4": {"sparse_zmax": 100000, "sparse_sun": 4, "sparse_chunks": 7},
+    "sun2_atomic": {"sparse_zmax": 100000, "sparse_sun": 2, "sparse_part_budget": 0, "sparse_chunks": 3},
+    # the dense words counted inside the tile kernel, 8 per chunk (partials / atomic flush),
+    # or by their own tile launch
+    "mixed_slabs": {"sparse_zmax": 12, "sparse_fold": 100000},
+    "mixed_slabs_atomic": {"sparse_zmax": 12, "sparse_fold": 100000, "sparse_part_budget": 0},
+    "mixed_tiles": {"sparse_zmax": 12, "sparse_fold": 0},
+    # the default step is fused (tiles + a reduce that adds the rare pairs and
+    # stores I and D); the same counts with zeroing + rare kernel + epilogue apart
+    "unfused": {"sparse_fused": 0},
+    "rare_kernel": {"sparse_rare": 0},
+    "unfused_rare_kernel": {"sparse_fused": 0, "sparse_rare": 0},
+    # the bitset fill by the (code, set) sort + run ranks, or by the one-pass
+    # windowed searches with global atomics, instead of merged positions + LDS slices
+    "fill_sort": {"fill_sort": 1},
+    "fill_direct": {"fill_sort": 2},
+    # the pack's two (code, set) pair sorts instead of one sort of set|code keys
+    "pack_pairs": {"pack_sort": 1},
+    # the pack without chunk summaries: the bitset build sorts every code for its dictionary
+    "pack_nosummary": {"pack_summary": 0},
+    "many_chunks": {"sparse_zmax": 100000, "sparse_chunks": 37},
+    # a dense-only dictionary: the substitution kmers two or more sets share
+    # are dense too, and their words are counted from the set bits
+    # (positive-sparse) beside the complement words
+    "two_sided": {"rare_t": 2, "guides": 4},
+}
+
+
+@pytest.mark.parametrize("mode", list(SPARSE_MODES))
 def test_sparse_complement_words_exact(ctx, mode, opts):
     """The dense tier in locus order with complement-sparse words: counts and
     distances are bit-exact against the oracle over upper triangles,
@@ -657,70 +686,16 @@ def test_sparse_complement_words_exact(ctx, mode, opts):
     whether every word is sparse, words are split between the sparse kernel
     and the tiles, the locus order is off (code order), or the split is off."""
     import gdist
-    settings = {"all_sparse": {"sparse_zmax": 100000}, "mixed": {"sparse_zmax": 12},
-                "no_locus": {"locus_order": 0, "sparse_zmax": 40}, "off": {"sparse": 0},
-                # chunks flush with atomics (no partials within a zero budget)
-                "atomic_flush": {"sparse_zmax": 100000, "sparse_part_budget": 0, "sparse_chunks": 5},
-                "kernel_v1": {"sparse_zmax": 100000, "sparse_kernel": 1},
-                "kernel_v2": {"sparse_zmax": 100000, "sparse_kernel": 2},
-                "kernel_v4": {"sparse_zmax": 100000, "sparse_kernel": 4},
-                "kernel_v4_rows": {"sparse_zmax": 40, "sparse_kernel": 4, "sparse_sun": 4},
-                "kernel_v5": {"sparse_zmax": 100000, "sparse_kernel": 5},
-                "kernel_v5_rows": {"sparse_zmax": 40, "sparse_kernel": 5},
-                "kernel_v5_sun6": {"sparse_zmax": 100000, "sparse_kernel": 5, "sparse_sun": 6, "sparse_chunks": 7},
-                "kernel_v5_atomic": {"sparse_zmax": 100000, "sparse_kernel": 5, "sparse_part_budget": 0,
-                                     "sparse_chunks": 3},
-                # kernel 6 (the default): micro-tiles of 1 x 2 / 1 x 4 / 2 x 2 entries per slot
-                "kernel_v6_rows": {"sparse_zmax": 40, "sparse_sun": 2},
-                "kernel_v6_sun4": {"sparse_zmax": 100000, "sparse_sun": 4, "sparse_chunks": 7},
-                "kernel_v6_quads": {"sparse_zmax": 100000, "sparse_shape": 14},
-                "kernel_v6_2x2": {"sparse_zmax": 100000, "sparse_shape": 22},
-                "kernel_v6_2x2_rows": {"sparse_zmax": 40, "sparse_shape": 22, "sparse_sun": 2},
-                "kernel_v6_atomic": {"sparse_zmax": 100000, "sparse_part_budget": 0, "sparse_chunks": 3},
-                # consecutive slots per lane (one search + quotient per lane and group)
-                "kernel_v6_consec": {"sparse_zmax": 100000, "sparse_shape": 112},
-                "kernel_v6_consec_rows": {"sparse_zmax": 40, "sparse_shape": 112, "sparse_sun": 2},
-                "kernel_v6_consec_sun4": {"sparse_zmax": 100000, "sparse_shape": 112, "sparse_sun": 4},
-                # the dense words absorbed into the sparse tier (no dense-word launch)
-                "absorb": {"sparse_zmax": 12, "sparse_absorb": 1},
-                # the dense words counted inside the tile kernel, 8 per chunk (partials / atomic flush),
-                # or by their own tile launch
-                "mixed_slabs": {"sparse_zmax": 12, "sparse_fold": 100000},
-                "mixed_slabs_atomic": {"sparse_zmax": 12, "sparse_fold": 100000, "sparse_part_budget": 0},
-                "mixed_tiles": {"sparse_zmax": 12, "sparse_fold": 0},
-                # the default step is fused (tiles + a reduce that adds the rare pairs and
-                # stores I and D); the same counts with zeroing + rare kernel + epilogue apart
-                "unfused": {"sparse_fused": 0},
-                "rare_kernel": {"sparse_rare": 0},
-                "unfused_rare_kernel": {"sparse_fused": 0, "sparse_rare": 0},
-                # the bitset fill by the (code, set) sort + run ranks, or by the one-pass
-                # windowed searches with global atomics, instead of merged positions + LDS slices
-                "fill_sort": {"fill_sort": 1},
-                "fill_direct": {"fill_sort": 2},
-                # the pack's two (code, set) pair sorts instead of one sort of set|code keys
-                "pack_pairs": {"pack_sort": 1},
-                # the pack without chunk summaries: the bitset build sorts every code for its dictionary
-                "pack_nosummary": {"pack_summary": 0},
-                "many_chunks": {"sparse_zmax": 100000, "sparse_chunks": 37},
-                # words counted from either side (complement / positive), model's choice
-                # a dense-only dictionary: the substitution kmers two or more
-                # sets share are dense too, and their words are counted from
-                # the set bits (positive-sparse) beside the complement words
-                "two_sided": {"rare_t": 2, "guides": 4},
-                # the dense words counted in the sparse flush (reduce kernel / one chunk's atomics)
-                "mixed_fold": {"sparse_zmax": 12, "fold_dense_words": 100000, "sparse_chunks": 3},
-                "mixed_fold_1chunk": {"sparse_zmax": 12, "fold_dense_words": 100000, "sparse_chunks": 1}}
+    settings = SPARSE_MODES
     opts(**settings.get(mode, {}))
     n = 300
     seqs = synth_sets(n, 20000, 0.003, 105)
     sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
     _, W = sets.build_bitsets()
     ws, wd, ent = sets.sparse_info()
-    if mode in ("all_sparse", "atomic_flush", "kernel_v1", "kernel_v2", "many_chunks", "kernel_v4", "kernel_v5",
-                "kernel_v5_sun6", "kernel_v5_atomic", "kernel_v6_sun4", "kernel_v6_quads", "kernel_v6_2x2",
-                "kernel_v6_atomic", "absorb", "kernel_v6_consec", "kernel_v6_consec_sun4"):
+    if mode in ("all_sparse", "atomic_flush", "many_chunks", "sun4", "sun2_atomic"):
         assert ws > 0 and wd == 0 and ent > 0
-    elif mode in ("mixed", "mixed_fold", "mixed_fold_1chunk", "mixed_slabs", "mixed_slabs_atomic", "mixed_tiles"):
+    elif mode in ("mixed", "mixed_slabs", "mixed_slabs_atomic", "mixed_tiles"):
         assert ws > 0 and wd > 0
     elif mode == "off":
         assert ws == 0 and wd == W
