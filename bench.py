@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Benchmark of the MI355X pairwise kmer-distance hot path (driver contract).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c2r|c3|c4|c5]
+                    [--rows A:B] [--force-exchange]
 
 Metric (BASELINE.json): genome-pair distances/sec over the N×N upper
 triangle (unordered pairs i<j). Default workload = configs[1] (C2):
@@ -14,10 +15,18 @@ dictionary -> bitsets) happens once before timing and is reported as
 
 N>1 (torch.distributed.run, one process per GPU): weak scaling — the
 genome count grows as 1000·sqrt(N) so every rank keeps ~C2's pair count;
-each rank packs its own shard, the ranks exchange dictionary summaries and
-bitsets with RCCL all-gathers (setup), then every rank computes its
-equal-area row block of the upper triangle; no collective in the timed
-region. `value` = all ranks' pairs / max-over-ranks time.
+each rank packs its own shard; the exchange is chosen by
+gdist_sets_exchange_plan from its per-rank memory estimate: the dictionary
+exchange (summaries, locus keys, bitsets, rare records; RCCL all-gathers)
+when it fits, else ONE in-place all-gather of the packed codes for the
+sorted join (C4: 100,000 x 100 kbp on 8 GPUs). Then every rank computes its
+row block of the upper triangle; no collective in the timed region.
+`value` = all ranks' pairs / max-over-ranks time.
+
+--rows A:B (one GPU) times the rows [A, B) of the triangle only (a slice of
+one rank's block, e.g. C4's per-rank workload); `value` is then the slice's
+pairs / time and the line says so. --force-exchange runs the exchange on a
+one-rank RCCL communicator (ncclAllGather on one GPU).
 
 rank 0 prints one JSON line.
 """
@@ -93,6 +102,10 @@ def main():
                     help="CPU baseline threads (default: this process's CPU share, see host_cpus())")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="context tuning option (gdist_ctx_set_option); GDIST_<NAME> variables are mapped too")
+    ap.add_argument("--rows", default="", metavar="A:B",
+                    help="one GPU: time rows [A, B) of the upper triangle only (a slice; the line reports it)")
+    ap.add_argument("--force-exchange", action="store_true",
+                    help="one GPU: run the multi-rank exchange on a one-rank RCCL communicator")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_c2.json"),
                     help="per-launch HBM traffic measured by rocprofv3 PMC passes (optional)")
     args = ap.parse_args()
@@ -163,8 +176,12 @@ def main():
     rare = None
     sparse_words = None
     auto = None
-    if world > 1:
-        if args.transport == "host":
+    exchange = world > 1 or args.force_exchange
+    if exchange:
+        if args.force_exchange and world == 1:
+            ctx.comm_init(gdist.Context.unique_id(), 1, 0)
+            ctx.set_option("force_exchange", 1)
+        elif args.transport == "host":
             import torch
 
             def gloo_allgather(a):
@@ -178,19 +195,25 @@ def main():
             obj = [uid]
             dist.broadcast_object_list(obj, src=0)
             ctx.comm_init(obj[0], world, rank)
-    if method == "auto":
-        # METHOD_AUTO's own decision (gdist_sets_prepare); multi-GPU runs take the
-        # dictionary path (its cost needs the global dictionary, built by the all-gather)
-        if world == 1:
-            chosen, cb, cs = local.prepare(gdist.METHOD_AUTO)
-            auto = {"chosen": {gdist.METHOD_BITSET: "bitset", gdist.METHOD_SORTED: "sorted"}[chosen],
-                    "est_bitset_s": round(cb, 4), "est_sorted_s": round(cs, 4)}
-            method = auto["chosen"]
-        else:
-            method = "bitset"
+    xplan = None
+    if exchange and method in ("auto", "bitset", "sorted"):
+        # the exchange every rank takes (collective): the dictionary exchange
+        # when its per-rank memory estimate fits, else the code all-gather
+        # for the sorted join (gdist_sets_exchange_plan)
+        want = {"auto": gdist.METHOD_AUTO, "bitset": gdist.METHOD_BITSET, "sorted": gdist.METHOD_SORTED}[method]
+        m, bb, bc = local.exchange_plan(want)
+        xplan = {"exchange": "bitsets" if m == gdist.METHOD_BITSET else "codes",
+                 "est_bytes_per_rank": {"bitsets": bb if math.isfinite(bb) else None, "codes": bc}}
+        method = "bitset" if m == gdist.METHOD_BITSET else "sorted"
+    elif method == "auto":
+        # METHOD_AUTO's own decision on one GPU (gdist_sets_prepare)
+        chosen, cb, cs = local.prepare(gdist.METHOD_AUTO)
+        auto = {"chosen": {gdist.METHOD_BITSET: "bitset", gdist.METHOD_SORTED: "sorted"}[chosen],
+                "est_bitset_s": round(cb, 4), "est_sorted_s": round(cs, 4)}
+        method = auto["chosen"]
     if method == "bitset":
-        sets = local.allgather_bitsets() if world > 1 else local
-        if world == 1 and auto is None:
+        sets = local.allgather_bitsets() if exchange else local
+        if not exchange and auto is None:
             sets.build_bitsets()
         dict_size, width_words = sets.bitset_info()
         rare = dict(zip(("threshold", "lists", "records"), sets.rare_info()))
@@ -198,11 +221,12 @@ def main():
         sparse_words = dict(zip(("sparse_words", "dense_words", "entries"), sets.sparse_info()))
         mflag = gdist.METHOD_BITSET
     elif method == "sorted":
-        sets = local.allgather() if world > 1 else local
+        # the code all-gather consumes the local shard: peak (ranks + 1) x shard
+        sets = local.allgather(consume=True) if exchange else local
         mflag = gdist.METHOD_SORTED
     else:
         sk_local = local.sketches(cfg["width"])
-        sets = sk_local.allgather() if world > 1 else sk_local
+        sets = sk_local.allgather() if exchange else sk_local
         mflag = None
     represent_s = time.time() - t
     barrier()
@@ -218,6 +242,13 @@ def main():
         dist.broadcast_object_list(obj, src=0)
         bounds = obj[0]
     r0, r1 = bounds[rank], bounds[rank + 1]
+    slice_rows = None
+    if args.rows:
+        assert world == 1, "--rows is a one-GPU slice"
+        a, b = (int(x) for x in args.rows.split(":"))
+        assert 0 <= a < b <= N, "--rows outside the collection"
+        r0, r1 = a, b
+        slice_rows = [a, b]
     rows = r1 - r0
     pairs_rank = shard.pairs_in_rows(N, r0, r1)
     dI = ctx.alloc(max(rows, 1) * N * 4)
@@ -265,7 +296,8 @@ def main():
         ts = [t for t in ts[1:] if t > 0]                 # the first call builds nothing new, but warms
         sparse_k_ms = float(np.mean(ts)) if ts else None
     pairs_all = N * (N - 1) // 2
-    value = pairs_all * args.steps / elapsed_max
+    pairs_job = pairs_rank if slice_rows else pairs_all      # a slice's pairs are all this job computes
+    value = pairs_job * args.steps / elapsed_max
     k_avg_ms = float(np.mean(kernel_ms)) if kernel_ms else 0.0
     # end to end: the whole job for one pass over the collection = pack +
     # represent (dictionary, bitsets / sketches) + one step, max over ranks
@@ -278,8 +310,7 @@ def main():
         if method == "bitset":
             bytes_per_pair = 16.0 * width_words                  # 16·W per pair
         elif method == "sorted":
-            sizes = local.sizes() if world == 1 else None
-            bytes_per_pair = 16.0 * float(np.mean(sizes)) if sizes is not None else 0.0   # 8(n_i+n_j)
+            bytes_per_pair = 16.0 * float(np.mean(sets.sizes()))    # 8(n_i+n_j)
         else:
             # the sketch tile kernel keeps the tile's sketches in LDS; each merge
             # step reads 2 dwords and a pair of full sketches takes exactly
@@ -372,7 +403,7 @@ def main():
             "metric": "genome-pair distances/sec (N×N)",
             "value": round(value, 1),
             "unit": "pairs/s",
-            "end_to_end_pairs_per_s": round(pairs_all / e2e_s, 1),
+            "end_to_end_pairs_per_s": round(pairs_job / e2e_s, 1),
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -383,7 +414,8 @@ def main():
             "dtype": "u64" if method != "sketch" else "i32",
             "data": "synthetic (splitmix64 genomes, SURVEY 8d)",
             "config": {"workload": f"{args.config}: {cfg['desc']}", "genomes": N, "genome_length": cfg["length"],
-                       "k": cfg["k"], "pairs_per_step": pairs_all, "parallelism": f"rows{world}",
+                       "k": cfg["k"], "pairs_per_step": pairs_job, "parallelism": f"rows{world}",
+                       "slice_rows": slice_rows, "exchange": xplan,
                        "bitset_words_per_set": width_words or None,
                        "dictionary_size": (dict_size if method == "bitset" else None),
                        "method": method, "auto": auto, "rare_tier": rare, "complement_sparse": sparse_words,
@@ -394,7 +426,7 @@ def main():
             "cpu_optimized": cpu_opt,
             "setup_s": {"generate": round(gen_s, 2), "host_free": round(free_s, 3), "pack": round(pack_s, 2), "represent": round(represent_s, 2),
                         "total": round(setup_s, 2)},
-            "end_to_end": {"pairs_per_s": round(pairs_all / e2e_s, 1), "seconds": round(e2e_s, 3),
+            "end_to_end": {"pairs_per_s": round(pairs_job / e2e_s, 1), "seconds": round(e2e_s, 3),
                            "note": "one pass over the collection from FASTA bytes in host memory: pack (H2D + "
                                    "kmer extraction + sort) + represent (dictionary, bitsets, sparse words) + one "
                                    "step; synthetic-genome generation and the release of the caller's host buffer "
@@ -408,6 +440,8 @@ def main():
         dist.barrier()
         ctx.comm_destroy()
         dist.destroy_process_group()
+    elif exchange:
+        ctx.comm_destroy()
 
 
 def _kmer_codes(seq: bytes, k: int, protein: bool) -> np.ndarray:

@@ -64,11 +64,16 @@ void* cache_alloc(int device, size_t bytes, size_t* cls_out) {
     *cls_out = cls;
     auto& c = block_cache();
     {
+        // best fit: the smallest cached block of at least this class, if it
+        // is at most 25 % larger (chunked setup paths ask for slightly
+        // different sizes every chunk; exact-class reuse left them all cached)
         std::lock_guard<std::mutex> lk(c.mu);
-        auto it = c.free_blocks[device].find(cls);
-        if (it != c.free_blocks[device].end()) {
+        auto& fb = c.free_blocks[device];
+        auto it = fb.lower_bound(cls);
+        if (it != fb.end() && it->first <= cls + cls / 4) {
             void* p = it->second;
-            c.free_blocks[device].erase(it);
+            *cls_out = it->first;
+            fb.erase(it);
             return p;
         }
     }
@@ -154,7 +159,29 @@ static void allgather(gdist_ctx* ctx, const void* d_send, void* d_recv, size_t b
     if (bytes) h2d(d_recv, hr.data(), (size_t)ctx->nranks * bytes, st);
 }
 
+// In place: this rank's `bytes` already sit at d_buf + rank * bytes.
+static void allgather_inplace(gdist_ctx* ctx, void* d_buf, size_t bytes) {
+    hipStream_t st = ctx->stream;
+    char* mine = static_cast<char*>(d_buf) + bytes * ctx->rank;
+    if (ctx->comm) {
+        GD_NCCL(ncclAllGather(mine, d_buf, bytes, ncclUint8, ctx->comm, st));
+        return;
+    }
+    if (!ctx->host_ag) throw ::gdist::Error(GDIST_ECOMM, "communicator not initialised (gdist_comm_init)");
+    std::vector<char> hs(bytes + 1), hr((size_t)ctx->nranks * bytes + 1);
+    if (bytes) d2h(hs.data(), mine, bytes, st);
+    if (ctx->host_ag(hs.data(), hr.data(), (int64_t)bytes, ctx->host_user) != 0)
+        throw ::gdist::Error(GDIST_ECOMM, "host all-gather callback failed");
+    if (bytes) h2d(d_buf, hr.data(), (size_t)ctx->nranks * bytes, st);
+}
+
+
 static void check_sets(const gdist_sets* s) { GD_REQUIRE(s != nullptr && s->ctx != nullptr, "null sets handle"); }
+// entry points that read the codes (or signatures) themselves
+static void check_codes(const gdist_sets* s) {
+    check_sets(s);
+    GD_REQUIRE(s->has_codes, "the collection holds no codes (bitset-only, or consumed by an all-gather)");
+}
 
 // The call's kernel-time events: the next pair of the ring.
 static void begin_timing(gdist_ctx* ctx) {
@@ -504,7 +531,7 @@ int gdist_sets_sizes(const gdist_sets* s, int64_t* sizes) {
 
 int gdist_sets_download(const gdist_sets* s, int64_t* offsets, uint64_t* codes) {
     return guard([&] {
-        check_sets(s);
+        check_codes(s);
         GD_REQUIRE(s->kind != GDIST_SKETCH, "use gdist_sketch_download for sketches");
         use_device(s->ctx);
         std::lock_guard<std::recursive_mutex> lk_(s->ctx->mu);
@@ -590,8 +617,8 @@ int gdist_sets_bitset_download(const gdist_sets* s, uint64_t* bits) {
 
 int gdist_sets_concat(const gdist_sets* a, const gdist_sets* b, gdist_sets** out) {
     return guard([&] {
-        check_sets(a);
-        check_sets(b);
+        check_codes(a);
+        check_codes(b);
         GD_REQUIRE(out, "null output");
         GD_REQUIRE(a->ctx == b->ctx, "sets belong to different contexts");
         GD_REQUIRE(a->kind == b->kind && a->k == b->k && a->width == b->width &&
@@ -945,7 +972,7 @@ int gdist_sketch_build(gdist_ctx* ctx, const gdist_sets* sets, int width, gdist_
     return guard([&] {
         use_device(ctx);
         std::lock_guard<std::recursive_mutex> lk_(ctx->mu);
-        check_sets(sets);
+        check_codes(sets);
         GD_REQUIRE(out, "null output");
         *out = nullptr;
         std::lock_guard<std::recursive_mutex> lk(ctx->mu);
@@ -991,7 +1018,7 @@ int gdist_sketch_upload(gdist_ctx* ctx, int width, int64_t nsets, const int64_t*
 
 int gdist_sketch_download(const gdist_sets* sk, int64_t* offsets, int32_t* sigs) {
     return guard([&] {
-        check_sets(sk);
+        check_codes(sk);
         GD_REQUIRE(sk->kind == GDIST_SKETCH, "not a sketch collection");
         use_device(sk->ctx);
         std::lock_guard<std::recursive_mutex> lk_(sk->ctx->mu);
@@ -1007,7 +1034,7 @@ int gdist_sketch_matrix(gdist_ctx* ctx, const gdist_sets* sk, int64_t r0, int64_
     return guard([&] {
         use_device(ctx);
         std::lock_guard<std::recursive_mutex> lk_(ctx->mu);
-        check_sets(sk);
+        check_codes(sk);
         GD_REQUIRE(sk->ctx == ctx, "sketches belong to another context");
         GD_REQUIRE(sk->kind == GDIST_SKETCH, "not a sketch collection");
         GD_REQUIRE(0 <= r0 && r0 <= r1 && r1 <= sk->nsets && 0 <= c0 && c0 <= c1 && c1 <= sk->nsets,
@@ -1052,7 +1079,7 @@ int gdist_lsh_build(gdist_ctx* ctx, const gdist_sets* sketches, int stages, int 
     return guard([&] {
         use_device(ctx);
         std::lock_guard<std::recursive_mutex> lk_(ctx->mu);
-        check_sets(sketches);
+        check_codes(sketches);
         GD_REQUIRE(out, "null output");
         *out = nullptr;
         auto* L = new gdist_lsh();
@@ -1080,7 +1107,7 @@ int gdist_lsh_closest(gdist_ctx* ctx, const gdist_lsh* lsh, const gdist_sets* qu
         use_device(ctx);
         std::lock_guard<std::recursive_mutex> lk_(ctx->mu);
         GD_REQUIRE(lsh && lsh->ctx == ctx, "index of another context");
-        check_sets(queries);
+        check_codes(queries);
         GD_REQUIRE(count_out && (n == 0 || (idx_out && d_out)), "null output");
         gdist::lsh_closest(ctx, lsh, queries, n, max_dist, idx_out, d_out, count_out);
     });
@@ -1138,16 +1165,25 @@ int gdist_comm_destroy(gdist_ctx* ctx) {
     });
 }
 
-int gdist_sets_allgather(gdist_ctx* ctx, const gdist_sets* local, gdist_sets** out) {
+// The code all-gather (one all-gather of the packed sets). Each
+// rank places its codes in its slot of one padded receive buffer and the
+// gather runs in place (RCCL: sendbuff = recvbuff + rank * count), so no send
+// copy exists; with GDIST_ALLGATHER_CONSUME the local codes are released as
+// soon as they sit in that slot. The padded slots are then compacted in rank
+// order through one staging buffer of the largest shard. Peak device bytes
+// per rank: R x the largest shard (the gather) + one shard (staging or the
+// local codes), e.g. C4 on 8 GPUs: 160 + 20 GB.
+int gdist_sets_allgather_ex(gdist_ctx* ctx, gdist_sets* local, unsigned flags, gdist_sets** out) {
     return guard([&] {
         use_device(ctx);
         std::lock_guard<std::recursive_mutex> lk_(ctx->mu);
         check_sets(local);
         GD_REQUIRE(out, "null output");
+        GD_REQUIRE(local->has_codes, "the local collection holds no codes (bitset-only, or consumed by an all-gather)");
+        GD_REQUIRE((flags & ~GDIST_ALLGATHER_CONSUME) == 0, "unknown all-gather flags");
         if (!has_comm(ctx)) throw ::gdist::Error(GDIST_ECOMM, "communicator not initialised (gdist_comm_init)");
-        std::lock_guard<std::recursive_mutex> lk(ctx->mu);
         hipStream_t st = ctx->stream;
-        const int R = ctx->nranks;
+        const int R = ctx->nranks, me = ctx->rank;
         const size_t es = local->kind == GDIST_SKETCH ? 4 : 8;
         // 1. (nsets, total) of every rank
         DevBuf mine(16, st), all(16 * R, st);
@@ -1156,39 +1192,128 @@ int gdist_sets_allgather(gdist_ctx* ctx, const gdist_sets* local, gdist_sets** o
         allgather(ctx, mine.p, all.p, 16);
         std::vector<int64_t> hall(2 * R);
         d2h(hall.data(), all.p, 16 * R, st);
-        GD_HIP(hipStreamSynchronize(st));
         int64_t mxs = 0, mxt = 0, ns = 0, nt = 0;
         for (int r = 0; r < R; r++) {
             mxs = std::max(mxs, hall[2 * r]); mxt = std::max(mxt, hall[2 * r + 1]);
             ns += hall[2 * r]; nt += hall[2 * r + 1];
         }
-        // 2. offsets and codes, padded to the largest shard (one all-gather each)
-        DevBuf so((mxs + 1) * 8, st), ao((mxs + 1) * 8 * R, st), sc(mxt * es + 8, st), ac((mxt * es + 8) * R, st);
-        GD_HIP(hipMemcpyAsync(so.p, local->off.p, (local->nsets + 1) * 8, hipMemcpyDeviceToDevice, st));
-        if (local->total) GD_HIP(hipMemcpyAsync(sc.p, local->codes.p, local->total * es, hipMemcpyDeviceToDevice, st));
-        allgather(ctx, so.p, ao.p, (mxs + 1) * 8);
-        allgather(ctx, sc.p, ac.p, mxt * es + 8);
+        // 2. offsets (small: a send copy) and codes (in place), padded to the largest shard
+        const size_t ob = (size_t)(mxs + 1) * 8, cb = (size_t)mxt * es + 8;
         std::vector<int64_t> hoff((mxs + 1) * R);
-        d2h(hoff.data(), ao.p, (mxs + 1) * 8 * R, st);
-        GD_HIP(hipStreamSynchronize(st));
+        {
+            DevBuf so(ob, st), ao(ob * R, st);
+            GD_HIP(hipMemcpyAsync(so.p, local->off.p, (local->nsets + 1) * 8, hipMemcpyDeviceToDevice, st));
+            allgather(ctx, so.p, ao.p, ob);
+            d2h(hoff.data(), ao.p, ob * R, st);
+        }
+        const bool consume = (flags & GDIST_ALLGATHER_CONSUME) != 0;
+        DevBuf ac;
+        if (consume && R == 1 && local->codes.bytes >= cb) {
+            ac = std::move(local->codes);            // one rank: the gather buffer is the shard itself
+        } else {
+            ac.alloc(cb * R, st);
+            char* slot = static_cast<char*>(ac.p) + cb * me;
+            if (local->total)
+                GD_HIP(hipMemcpyAsync(slot, local->codes.p, local->total * es, hipMemcpyDeviceToDevice, st));
+        }
+        if (consume) {
+            // the local collection keeps its sizes (h_off) but no device data
+            GD_HIP(hipStreamSynchronize(st));
+            free_bitsets(local);
+            local->codes.release();
+            local->segoff.release();
+            local->guide_codes.release();
+            local->guide_keys.release();
+            local->pack_sum.clear();
+            local->has_codes = false;
+            gdist::cache_trim(ctx->device);           // the gather buffer may need that memory back
+        }
+        allgather_inplace(ctx, ac.p, cb);
+        // 3. compact the slots in rank order: slot r's codes move down to the
+        // sum of the earlier ranks' totals (staged: source and destination overlap)
         auto* s = new gdist_sets();
+        std::unique_ptr<gdist_sets> guard_s(s);
         s->ctx = ctx; s->kind = local->kind; s->k = local->k; s->flags = local->flags; s->width = local->width;
         s->nsets = ns; s->total = nt;
         s->h_off.assign(1, 0);
-        s->codes.alloc(nt * es + 8, st);
         int64_t at = 0;
-        for (int r = 0; r < R; r++) {
-            const int64_t rn = hall[2 * r], rt = hall[2 * r + 1];
-            for (int64_t i = 1; i <= rn; i++) s->h_off.push_back(at + hoff[(mxs + 1) * r + i]);
-            if (rt)
-                GD_HIP(hipMemcpyAsync((char*)s->codes.p + at * es, (char*)ac.p + (mxt * es + 8) * r, rt * es,
-                                      hipMemcpyDeviceToDevice, st));
-            at += rt;
+        {
+            DevBuf stage(R > 1 ? mxt * es + 8 : 8, st);
+            for (int r = 0; r < R; r++) {
+                const int64_t rn = hall[2 * r], rt = hall[2 * r + 1];
+                for (int64_t i = 1; i <= rn; i++) s->h_off.push_back(at + hoff[(mxs + 1) * r + i]);
+                char* src = static_cast<char*>(ac.p) + cb * r;
+                char* dst = static_cast<char*>(ac.p) + at * es;
+                if (rt && src != dst) {
+                    GD_HIP(hipMemcpyAsync(stage.p, src, rt * es, hipMemcpyDeviceToDevice, st));
+                    GD_HIP(hipMemcpyAsync(dst, stage.p, rt * es, hipMemcpyDeviceToDevice, st));
+                }
+                at += rt;
+            }
+            GD_HIP(hipStreamSynchronize(st));
         }
+        s->codes = std::move(ac);                     // R x cb bytes; the compacted codes first
         s->off.alloc((ns + 1) * 8, st);
         h2d(s->off.p, s->h_off.data(), (ns + 1) * 8, st);
         GD_HIP(hipStreamSynchronize(st));
-        *out = s;
+        *out = guard_s.release();
+    });
+}
+
+int gdist_sets_allgather(gdist_ctx* ctx, const gdist_sets* local, gdist_sets** out) {
+    return gdist_sets_allgather_ex(ctx, const_cast<gdist_sets*>(local), 0, out);
+}
+
+// Per-rank peak device bytes of the two exchanges (estimates) and the choice.
+// Collective: one all-gather of (nsets, codes, summary bound) per rank, then
+// the same arithmetic on every rank.
+int gdist_sets_exchange_plan(gdist_ctx* ctx, const gdist_sets* local, int method, int* chosen, double* bytes_bitsets,
+                             double* bytes_codes) {
+    return guard([&] {
+        use_device(ctx);
+        std::lock_guard<std::recursive_mutex> lk_(ctx->mu);
+        check_sets(local);
+        GD_REQUIRE(chosen, "null output");
+        GD_REQUIRE(method >= GDIST_METHOD_AUTO && method <= GDIST_METHOD_BITSET, "unknown method");
+        GD_REQUIRE(local->has_codes, "the local collection holds no codes");
+        hipStream_t st = ctx->stream;
+        const int R = has_comm(ctx) ? ctx->nranks : 1;
+        // the dictionary summary's length is at most the sum of the pack
+        // chunks' summaries when the pack kept them, else the codes themselves
+        int64_t sum_n = 0;
+        for (const auto& p : local->pack_sum) sum_n += p.n;
+        if (local->pack_sum.empty()) sum_n = local->total;
+        std::vector<int64_t> h(3 * R);
+        h[0] = local->nsets; h[1] = local->total; h[2] = sum_n;
+        if (R > 1) {
+            DevBuf mine(24, st), all(24 * R, st);
+            h2d(mine.p, h.data(), 24, st);
+            allgather(ctx, mine.p, all.p, 24);
+            d2h(h.data(), all.p, 24 * R, st);
+        }
+        double mxt = 0, mxn = 0;
+        for (int r = 0; r < R; r++) { mxt = std::max(mxt, (double)h[3 * r + 1]); mxn = std::max(mxn, (double)h[3 * r + 2]); }
+        const double es = local->kind == GDIST_SKETCH ? 4.0 : 8.0;
+        // codes: the padded gather + staging (the local codes consumed)
+        const double b_codes = ((double)R + 1.0) * mxt * es;
+        // bitsets: the local codes + the gathered summaries (12 B per
+        // distinct code) + the merge's workspace (~2x them)
+        const double b_bits = local->kind == GDIST_SKETCH ? INFINITY : mxt * 8.0 + 3.0 * (double)R * mxn * 12.0;
+        hipDeviceProp_t prop;
+        GD_HIP(hipGetDeviceProperties(&prop, ctx->device));
+        const double budget = ctx->has_option(OPT_EXCHANGE_BUDGET) ? (double)ctx->option(OPT_EXCHANGE_BUDGET, 0)
+                                                                    : 0.8 * (double)prop.totalGlobalMem;
+        int m = method;
+        if (m == GDIST_METHOD_AUTO) m = b_bits <= budget ? GDIST_METHOD_BITSET : GDIST_METHOD_SORTED;
+        if (local->kind == GDIST_SKETCH) m = GDIST_METHOD_SORTED;
+        if (ctx->trace())
+            fprintf(stderr, "gdist: exchange plan: bitsets ~%.1f GB, codes ~%.1f GB per rank, budget %.1f GB -> %s\n",
+                    b_bits / 1e9, b_codes / 1e9, budget / 1e9, m == GDIST_METHOD_BITSET ? "bitsets" : "codes");
+        if (m == GDIST_METHOD_SORTED && b_codes > budget)
+            throw Error(GDIST_ENOMEM, "neither exchange fits the device memory budget (option exchange_budget)");
+        *chosen = m;
+        if (bytes_bitsets) *bytes_bitsets = b_bits;
+        if (bytes_codes) *bytes_codes = b_codes;
     });
 }
 

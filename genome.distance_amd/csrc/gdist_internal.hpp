@@ -200,7 +200,8 @@ struct Timing {
     X(PACK_SORT, "pack_sort")                 /* 1: two (code, set) pair sorts instead of packed keys */       \
     X(PACK_SUMMARY, "pack_summary")           /* 0: set|code pack keys, the bitset build re-sorts codes */     \
     X(PACK_OVERLAP, "pack_overlap")           /* 0: upload first / 1: overlapped host thread / 2: registered */\
-    X(PACK_CHUNK, "pack_chunk")               /* kmer windows per pack chunk (default 2^28) */
+    X(PACK_CHUNK, "pack_chunk")               /* kmer windows per pack chunk (default 2^28) */                 \
+    X(EXCHANGE_BUDGET, "exchange_budget")     /* device bytes an exchange may use (default 0.8 x HBM) */
 
 enum Opt : int {
 #define GDIST_OPT_ENUM(id, name) OPT_##id,

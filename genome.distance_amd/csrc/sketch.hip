@@ -299,13 +299,24 @@ void sketch_build(gdist_ctx* ctx, const gdist_sets* s, int width, gdist_sets* ou
     std::vector<int64_t> part_n;
     DevBuf d_out_off((nsets + 1) * 8, st);
     const int64_t kChunk = int64_t(1) << 29;
-    int64_t s0 = 0;
-    while (s0 < nsets) {
-        int64_t s1 = s0 + 1;
-        while (s1 < nsets && s->h_off[s1 + 1] - s->h_off[s0] <= kChunk) s1++;
+    // chunks of whole sets of at most kChunk codes (or one larger set); the
+    // work buffers are sized once for the largest chunk and reused
+    std::vector<std::pair<int64_t, int64_t>> chunks;
+    int64_t nmax = 0, nsmax = 0;
+    for (int64_t a = 0; a < nsets;) {
+        int64_t b = a + 1;
+        while (b < nsets && s->h_off[b + 1] - s->h_off[a] <= kChunk) b++;
+        chunks.push_back({a, b});
+        nmax = std::max(nmax, s->h_off[b] - s->h_off[a]);
+        nsmax = std::max(nsmax, b - a);
+        a = b;
+    }
+    DevBuf kA(nmax * 8 + 8, st), kB(nmax * 8 + 8, st), flag(nmax * 4 + 4, st), pos(nmax * 8 + 8, st),
+        us((nsmax + 1) * 8, st);
+    for (const auto& ch : chunks) {
+        const int64_t s0 = ch.first, s1 = ch.second;
         const int64_t ns = s1 - s0;
         const int64_t n = s->h_off[s1] - s->h_off[s0];
-        DevBuf kA(n * 8 + 8, st), kB(n * 8 + 8, st), flag(n * 4 + 4, st), pos(n * 8 + 8, st), us((ns + 1) * 8, st);
         if (n) {
             hash_keys_kernel<<<grid_for(n), 256, 0, st>>>(s->codes.as<uint64_t>(), s->off.as<int64_t>(), s0, ns, k,
                                                          bits, dna_mode, kA.as<uint64_t>());
@@ -341,7 +352,6 @@ void sketch_build(gdist_ctx* ctx, const gdist_sets* s, int width, gdist_sets* ou
         }
         parts.push_back(std::move(sig));
         part_n.push_back(loc[ns]);
-        s0 = s1;
     }
     out->kind = GDIST_SKETCH;
     out->k = s->k;

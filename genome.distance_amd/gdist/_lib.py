@@ -21,6 +21,7 @@ NO_CASE_FOLD = 0x10
 UPPER_TRIANGLE, OUT_DEVICE, EMPTY_NAN, SKETCH_JACCARD = 0x100, 0x200, 0x400, 0x800
 METHOD_AUTO, METHOD_SORTED, METHOD_BITSET = 0, 1, 2
 BITSET_KEEP_SINGLETONS = 0x1
+ALLGATHER_CONSUME = 0x1
 QUERY_ALL, QUERY_ANY_LE, QUERY_ARGMIN = 0, 1, 2
 UNIQUE_ID_BYTES = 128
 OPTION_DEFAULT = -(1 << 63)   # GDIST_OPTION_DEFAULT
@@ -127,6 +128,8 @@ _SIGS = {
     "gdist_comm_init_host": (C.c_int, [_ctxp, C.c_int, C.c_int, C.c_void_p, _vp]),
     "gdist_comm_destroy": (C.c_int, [_ctxp]),
     "gdist_sets_allgather": (C.c_int, [_ctxp, _setp, C.POINTER(_setp)]),
+    "gdist_sets_allgather_ex": (C.c_int, [_ctxp, _setp, _u32, C.POINTER(_setp)]),
+    "gdist_sets_exchange_plan": (C.c_int, [_ctxp, _setp, C.c_int, C.POINTER(C.c_int), _dblp, _dblp]),
     "gdist_sets_allgather_bitsets": (C.c_int, [_ctxp, _setp, _u32, C.POINTER(_setp)]),
     "gdist_comm_allreduce_max": (C.c_int, [_ctxp, _dblp]),
     "gdist_sets_block_cost": (C.c_int, [_setp, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_int,

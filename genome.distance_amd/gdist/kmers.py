@@ -248,12 +248,26 @@ class _Handle:
     def __len__(self) -> int:
         return self.info()[2]
 
-    def allgather(self):
+    def allgather(self, consume: bool = False):
         """Concatenation of every rank's local collection, in rank order
-        (one RCCL all-gather of offsets, one of codes / signatures)."""
+        (one RCCL all-gather of offsets, one in place of codes / signatures).
+        consume=True releases this collection's device data once its codes
+        are in the gather buffer (GDIST_ALLGATHER_CONSUME): peak memory is
+        then (ranks + 1) x the largest shard instead of + 2 shards."""
         h = C.c_void_p()
-        L.check(L.lib.gdist_sets_allgather(self.ctx.h, self.h, C.byref(h)))
+        L.check(L.lib.gdist_sets_allgather_ex(self.ctx.h, self.h, L.ALLGATHER_CONSUME if consume else 0,
+                                              C.byref(h)))
         return type(self)(self.ctx, h)
+
+    def exchange_plan(self, method: int = L.METHOD_AUTO) -> tuple[int, float, float]:
+        """(method, bytes_bitsets, bytes_codes): the exchange every rank of the
+        communicator takes for a row-sharded N x N (collective call):
+        METHOD_BITSET = the dictionary exchange (allgather_bitsets),
+        METHOD_SORTED = the code all-gather (allgather) for the sorted join."""
+        m = C.c_int()
+        bb, bc = C.c_double(), C.c_double()
+        L.check(L.lib.gdist_sets_exchange_plan(self.ctx.h, self.h, method, C.byref(m), C.byref(bb), C.byref(bc)))
+        return m.value, bb.value, bc.value
 
 
 class KmerSets(_Handle):

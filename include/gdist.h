@@ -292,8 +292,25 @@ typedef int (*gdist_allgather_fn)(const void* send, void* recv, int64_t bytes, v
 int  gdist_comm_init_host(gdist_ctx* ctx, int nranks, int rank, gdist_allgather_fn fn, void* user);
 int  gdist_comm_destroy(gdist_ctx* ctx);
 /* Every rank passes its local shard; every rank receives the concatenation
- * in rank order (one all-gather of offsets and one of codes). */
+ * in rank order (one all-gather of offsets and one, in place, of codes). */
 int  gdist_sets_allgather(gdist_ctx* ctx, const gdist_sets* local, gdist_sets** out);
+/* The same; with GDIST_ALLGATHER_CONSUME the library releases `local`'s
+ * device data once its codes are in the gather buffer (local keeps its sizes
+ * and can still be freed; it can no longer be used for distances). Peak
+ * device bytes per rank: (ranks + 1) x the largest shard's codes. */
+#define GDIST_ALLGATHER_CONSUME 0x1u
+int  gdist_sets_allgather_ex(gdist_ctx* ctx, gdist_sets* local, unsigned flags, gdist_sets** out);
+/* Which exchange a row-sharded N×N over this communicator should use
+ * (collective: every rank calls it with its local shard and gets the same
+ * answer). *chosen = GDIST_METHOD_BITSET: the dictionary exchange
+ * (gdist_sets_allgather_bitsets); GDIST_METHOD_SORTED: the code all-gather
+ * (gdist_sets_allgather_ex) for the sorted join. METHOD_AUTO takes the
+ * dictionary exchange when its per-rank estimate fits the budget (option
+ * "exchange_budget", default 0.8 x the device memory), else the codes; the
+ * estimates (bytes per rank) are returned. ENOMEM when neither fits.
+ * (C4 = 100,000 x 100 kbp on 8 GPUs takes the codes.) */
+int  gdist_sets_exchange_plan(gdist_ctx* ctx, const gdist_sets* local, int method, int* chosen,
+                              double* bytes_bitsets, double* bytes_codes);
 /* Dictionary-rank bitsets of the concatenation (in rank order) of every
  * rank's local sets: one all-gather of the local dictionary summaries
  * (distinct codes + counts), one of the local bitsets. The result holds the

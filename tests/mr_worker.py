@@ -10,7 +10,10 @@ Cases:
   sparse  C2-shaped (shared core, p <= 0.002): the complement-sparse words
           must be active on every rank, so the rank-tagged locus keys are
           all-gathered and min-reduced (gdist_sets_allgather_bitsets)
-  c4      C4-shaped (100 kbp, p <= 0.05, DNA k=21) at small N, METHOD_AUTO
+  c4      C4-shaped (100 kbp, p <= 0.05, DNA k=21) at small N, METHOD_AUTO,
+          and the exchange plan under a memory budget too small for the
+          dictionary exchange: the in-place code all-gather that consumes the
+          local shard (what C4 at 100,000 genomes on 8 GPUs runs)
 """
 import os
 import sys
@@ -29,7 +32,7 @@ from gdist import shard, synth  # noqa: E402
 CASES = {
     "base": dict(n=301, L=6000, p=0.01, cfg=11, legs=("bitset", "sorted", "sketch")),
     "sparse": dict(n=300, L=150_000, p=0.002, cfg=12, legs=("bitset",), sparse=True),
-    "c4": dict(n=200, L=100_000, p=0.05, cfg=4, legs=("auto", "sorted")),
+    "c4": dict(n=200, L=100_000, p=0.05, cfg=4, legs=("auto", "sorted", "codes_plan")),
 }
 SKETCH_W = 200
 
@@ -55,6 +58,24 @@ def run_case(name, c, ctx, rank, world):
         elif leg == "sorted":
             gs = local.allgather()
             assert len(gs) == n
+            results[leg] = gs.matrix((r0, r1), (0, n), upper=True, method=gdist.METHOD_SORTED)
+        elif leg == "codes_plan":
+            m, bb, bc = local.exchange_plan()
+            assert m == gdist.METHOD_BITSET, (m, bb, bc)            # small: the dictionary exchange fits
+            budget = 1 << 30
+            assert bc <= budget < bb, (bb, bc)
+            ctx.set_option("exchange_budget", budget)
+            own = gdist.KmerSets.from_sequences(seqs[s0:s1], 21, gdist.KmerType.DNA, 0, ctx)
+            m, _, _ = own.exchange_plan()
+            assert m == gdist.METHOD_SORTED, m
+            gs = own.allgather(consume=True)
+            ctx.set_option("exchange_budget", None)
+            assert len(gs) == n and len(own) == s1 - s0
+            try:
+                own.matrix(method=gdist.METHOD_SORTED)
+                raise AssertionError("a consumed shard must refuse distance calls")
+            except ValueError:
+                pass
             results[leg] = gs.matrix((r0, r1), (0, n), upper=True, method=gdist.METHOD_SORTED)
         elif leg == "sketch":
             sk = local.sketches(SKETCH_W).allgather()

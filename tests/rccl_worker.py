@@ -35,6 +35,13 @@ def main():
     gs = local.allgather()
     I, D = gs.matrix(upper=True, method=gdist.METHOD_SORTED)
     assert np.array_equal(I[iu], eI[iu]) and np.array_equal(D[iu].view(np.uint64), eD[iu].view(np.uint64))
+    # the in-place code all-gather that consumes its shard (C4's exchange)
+    own = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
+    gc = own.allgather(consume=True)
+    del own
+    I, D = gc.matrix(upper=True, method=gdist.METHOD_SORTED)
+    assert np.array_equal(I[iu], eI[iu]) and np.array_equal(D[iu].view(np.uint64), eD[iu].view(np.uint64))
+    assert [a.tolist() for a in gc.download()] == [off.tolist(), codes.tolist()]
     sk = local.sketches(100)
     ska = sk.allgather()
     assert [a.tolist() for a in ska.download()] == [a.tolist() for a in sk.download()]
