@@ -260,8 +260,19 @@ def main():
         else:
             sets.matrix_device(dI.ptr, dD.ptr, N, (r0, r1), (0, N), upper=True, method=mflag)
 
-    for _ in range(args.warmup):
-        step()
+    # the first call builds the region's launch plans (tile lists, sparse
+    # chunks, the rare pairs' table) before it runs: timed on its own, it is
+    # part of the one-pass end-to-end figure; the second call is captured
+    first_call_s = None
+    for w in range(args.warmup):
+        if w == 0:
+            barrier()
+            t = time.perf_counter()
+            step()
+            barrier()
+            first_call_s = time.perf_counter() - t
+        else:
+            step()
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -301,7 +312,9 @@ def main():
     k_avg_ms = float(np.mean(kernel_ms)) if kernel_ms else 0.0
     # end to end: the whole job for one pass over the collection = pack +
     # represent (dictionary, bitsets / sketches) + one step, max over ranks
-    e2e_s = max_over_ranks(pack_s + represent_s + elapsed / max(args.steps, 1))
+    one_pass_s = first_call_s if first_call_s is not None else elapsed / max(args.steps, 1)
+    e2e_s = max_over_ranks(pack_s + represent_s + one_pass_s)
+    first_call_s = max_over_ranks(first_call_s) if first_call_s is not None else None
 
     verified = verify_sample(cfg, method, N, r0, r1, dI, dD, max_over_ranks)
     out = None
@@ -330,10 +343,10 @@ def main():
             except Exception:
                 traffic = None
         sparse = sparse_words if (method == "bitset" and sparse_words and sparse_words["sparse_words"] > 0) else None
-        kname = {"bitset": "bitset_tile_kernel2<1> (+ rare_pairs_kernel)", "sorted": "sorted_join_kernel",
+        kname = {"bitset": "bitset_tile_kernel2 (+ rare_pairs_kernel)", "sorted": "sorted_join_kernel",
                  "sketch": "sketch_tile_kernel<16,24,LDS,K=2>"}[method]
         if sparse:
-            kname = "sparse_tile_kernel5<3, 8, 1, 2, false> (v6: 1x2 micro-tiles, the dense words folded in)"
+            kname = "sparse_tile_kernel<3> (1x2 micro-tiles, the dense words folded in)"
         if traffic is not None and not pmc.get("kernel", "").startswith(kname.split(" (")[0]):
             traffic = None                    # the PMC summary was taken on another kernel
         valu_peak = VALU_WORDPAIR_PEAK * 4 / 1e12
@@ -427,10 +440,15 @@ def main():
             "setup_s": {"generate": round(gen_s, 2), "host_free": round(free_s, 3), "pack": round(pack_s, 2), "represent": round(represent_s, 2),
                         "total": round(setup_s, 2)},
             "end_to_end": {"pairs_per_s": round(pairs_job / e2e_s, 1), "seconds": round(e2e_s, 3),
+                           "first_call_s": round(first_call_s, 4) if first_call_s is not None else None,
+                           "plan_s": (round(first_call_s - elapsed_max / args.steps, 4)
+                                      if first_call_s is not None else None),
                            "note": "one pass over the collection from FASTA bytes in host memory: pack (H2D + "
-                                   "kmer extraction + sort) + represent (dictionary, bitsets, sparse words) + one "
-                                   "step; synthetic-genome generation and the release of the caller's host buffer "
-                                   "(setup_s.host_free) excluded; max over ranks"},
+                                   "kmer extraction + sort) + represent (dictionary, bitsets, sparse words) + the "
+                                   "FIRST matrix call (it builds the region's launch plans and the rare pairs' "
+                                   "table, then runs; plan_s = that call minus a steady step); synthetic-genome "
+                                   "generation and the release of the caller's host buffer (setup_s.host_free) "
+                                   "excluded; max over ranks"},
         }
         print(json.dumps(out), flush=True)
     if verified is not None and not verified["ok"]:

@@ -790,74 +790,161 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
     tr.mark("sparse: entries + dense words");
 }
 
-// Adds the sparse words' share of |A ∩ B| to I over the region (atomics;
-// the caller zeroed I, the dense tiles add theirs). Launched on `st`; `sc`
-// (the region's cached plan) holds the tile list and the chunk partials.
-// The rare tier's pairs of a region, for the chunk reduce: every posting
-// list adds its weight to each of its pairs in the region (the semantics of
-// rare_pairs_kernel, bitset.hip), here expanded once per region plan on the
-// host, keyed by (tile, counter slot in the cnt_index layout), merged and
-// bucketed by (tile, 512-slot reduce group). Lists are few and short when the
-// sparse tier runs (C2: 0.2 M lists, ~0.3 M pairs); past kRarePairsMax pairs
-// the rare kernel keeps them.
+// The rare tier's pairs of a region, for the chunk reduce (sparse_plan): every
+// posting list adds its weight to each of its pairs in the region (the
+// semantics of rare_pairs_kernel, bitset.hip). Expanded once per region plan
+// on the device: one thread per pair of every list (list found by binary
+// search over the lists' pair offsets, the pair by the triangular inverse),
+// keyed (tile << 14 | counter slot in the cnt_index layout) << 32 | weight,
+// radix-sorted by key, equal keys summed, and bucketed by (tile, 512-slot
+// reduce group). Pairs outside the region get the sentinel key and sort last.
+// Past kRarePairsMax pairs over all lists the rare kernel keeps them.
 constexpr int64_t kRarePairsMax = int64_t(1) << 25;
+constexpr uint64_t kNoPair = ~0ull;
+
+__global__ void rare_list_pairs_kernel(const int64_t* __restrict__ poff, int64_t nl, int mirror,
+                                       int64_t* __restrict__ cnt) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; l < nl; l += stride) {
+        const int64_t m = poff[l + 1] - poff[l];
+        cnt[l] = m * (m - 1) / 2 * (mirror ? 2 : 1);
+    }
+}
+
+__global__ void rare_pair_emit_kernel(const int64_t* __restrict__ poff, const uint32_t* __restrict__ psets,
+                                      const uint32_t* __restrict__ pw, int64_t nl, const int64_t* __restrict__ P,
+                                      int64_t total, int mirror, int64_t r0, int64_t r1, int64_t c0, int64_t c1,
+                                      const int32_t* __restrict__ tile_of, int64_t nb, uint64_t* __restrict__ out,
+                                      int* __restrict__ missing) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += stride) {
+        int64_t lo = 0, hi = nl;                           // the list: last l with P[l] <= q
+        while (hi - lo > 1) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (P[mid] <= q) lo = mid; else hi = mid;
+        }
+        const int64_t l = lo;
+        const int64_t m = poff[l + 1] - poff[l];
+        int64_t t = q - P[l];
+        const int64_t half = m * (m - 1) / 2;
+        const bool flip = mirror && t >= half;
+        if (flip) t -= half;
+        // t -> (x, y), x < y, t = y (y - 1) / 2 + x
+        int64_t y = (int64_t)((1.0 + sqrt(1.0 + 8.0 * (double)t)) * 0.5);
+        while (y * (y - 1) / 2 > t) y--;
+        while ((y + 1) * y / 2 <= t) y++;
+        const int64_t x = t - y * (y - 1) / 2;
+        int64_t i = psets[poff[l] + x], j = psets[poff[l] + y];   // i < j (lists ascend)
+        if (flip) { const int64_t tmp = i; i = j; j = tmp; }
+        uint64_t key = kNoPair;
+        if (i >= r0 && i < r1 && j >= c0 && j < c1) {
+            const int32_t tl = tile_of[(i / SB) * nb + (j / SB)];
+            if (tl >= 0)
+                key = ((uint64_t)(((uint32_t)tl << 14) | (uint32_t)cnt_index((int)(i % SB), (int)(j % SB))) << 32) |
+                      (uint64_t)pw[l];
+            else
+                *missing = 1;                              // a pair of the region outside the plan's tiles
+        }
+        out[q] = key;
+    }
+}
+
+// run heads of the sorted keys (high 32 bits), sentinels excluded
+__global__ void rare_pair_heads_kernel(const uint64_t* __restrict__ k, int64_t n, int32_t* __restrict__ flag) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        flag[i] = k[i] != kNoPair && (i == 0 || (k[i] >> 32) != (k[i - 1] >> 32));
+}
+
+__global__ void rare_pair_runs_kernel(const uint64_t* __restrict__ k, int64_t n, const int32_t* __restrict__ flag,
+                                      const int64_t* __restrict__ pos, uint32_t* __restrict__ ukey,
+                                      uint32_t* __restrict__ uw) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        if (!flag[i]) continue;
+        const uint32_t key = (uint32_t)(k[i] >> 32);
+        uint32_t w = 0;
+        for (int64_t e = i; e < n && k[e] != kNoPair && (uint32_t)(k[e] >> 32) == key; e++) w += (uint32_t)k[e];
+        ukey[pos[i]] = key;
+        uw[pos[i]] = w;
+    }
+}
+
+// goff[g] = first unique key of group g (key >> 9 >= g)
+__global__ void rare_group_offsets_kernel(const uint32_t* __restrict__ ukey, int64_t nu, int64_t ngroups,
+                                          int64_t* __restrict__ goff) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g <= ngroups; g += stride) {
+        int64_t lo = 0, hi = nu;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if ((int64_t)(ukey[mid] >> 9) < g) lo = mid + 1; else hi = mid;
+        }
+        goff[g] = lo;
+    }
+}
+
 static void rare_pair_table(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1,
                             bool upper, const std::vector<int2>& tiles, hipStream_t st, SparseScratch& sc) {
     sc.rare_in = false;
     if (s->n_rare == 0) return;
     if (ctx->option(OPT_SPARSE_RARE, 1) == 0 || s->rare_records > kRarePairsMax) return;
-    std::vector<int64_t> poff(s->n_rare + 1);
-    std::vector<uint32_t> psets(s->rare_records), pw(s->n_rare);
-    d2h(poff.data(), s->post_off.p, poff.size() * 8, st);
-    d2h(psets.data(), s->post_sets.p, psets.size() * 4, st);
-    d2h(pw.data(), s->post_w.p, pw.size() * 4, st);
-    double npairs = 0.0;
-    for (int64_t l = 0; l < s->n_rare; l++) {
-        const double m = (double)(poff[l + 1] - poff[l]);
-        npairs += 0.5 * m * (m - 1.0) * (upper ? 1.0 : 2.0);
+    GD_REQUIRE(tiles.size() < (size_t(1) << 18), "too many tiles for the rare pair keys");
+    const int64_t nl = s->n_rare;
+    DevBuf P((nl + 1) * 8, st);
+    {
+        DevBuf cnt((nl + 1) * 8, st);
+        GD_HIP(hipMemsetAsync(cnt.as<int64_t>() + nl, 0, 8, st));
+        rare_list_pairs_kernel<<<grid_for(nl), 256, 0, st>>>(s->post_off.as<int64_t>(), nl, upper ? 0 : 1,
+                                                             cnt.as<int64_t>());
+        GD_HIP(hipGetLastError());
+        exclusive_scan_i64(ctx, cnt.as<int64_t>(), P.as<int64_t>(), (size_t)(nl + 1));
     }
-    if (npairs > (double)kRarePairsMax) return;
+    int64_t total = 0;
+    d2h(&total, P.as<int64_t>() + nl, 8, st);
+    if (total > kRarePairsMax) return;
     const int64_t nb = ceil_div(s->nsets, SB);
     std::vector<int32_t> tile_of((size_t)nb * nb, -1);
     for (size_t t = 0; t < tiles.size(); t++) tile_of[(size_t)tiles[t].x * nb + tiles[t].y] = (int32_t)t;
-    std::vector<std::pair<uint32_t, uint32_t>> kv;
-    kv.reserve((size_t)npairs);
-    bool missing = false;
-    auto emit = [&](int64_t i, int64_t j, uint32_t w) {
-        const int32_t t = tile_of[(size_t)(i / SB) * nb + (j / SB)];
-        if (t < 0) { missing = true; return; }
-        const int a = (int)(i % SB), b = (int)(j % SB);
-        kv.emplace_back(((uint32_t)t << 14) | (uint32_t)cnt_index(a, b), w);
-    };
-    for (int64_t l = 0; l < s->n_rare; l++)
-        for (int64_t x = poff[l]; x < poff[l + 1]; x++) {
-            const int64_t a = psets[x];
-            for (int64_t y = x + 1; y < poff[l + 1]; y++) {
-                const int64_t b = psets[y];          // b > a
-                if (a >= r0 && a < r1 && b >= c0 && b < c1) emit(a, b, pw[l]);
-                if (!upper && b >= r0 && b < r1 && a >= c0 && a < c1) emit(b, a, pw[l]);
-            }
-        }
-    GD_REQUIRE(!missing, "rare pair outside the sparse plan's tiles");
-    GD_REQUIRE(tiles.size() < (size_t(1) << 18), "too many tiles for the rare pair keys");
-    std::sort(kv.begin(), kv.end());
-    std::vector<uint32_t> keys, ws;
-    for (const auto& e : kv) {
-        if (!keys.empty() && keys.back() == e.first) ws.back() += e.second;
-        else { keys.push_back(e.first); ws.push_back(e.second); }
+    DevBuf dto(tile_of.size() * 4, st);
+    h2d(dto.p, tile_of.data(), tile_of.size() * 4, st);
+    DevBuf kA(total * 8 + 8, st), kB(total * 8 + 8, st), miss(4, st);
+    GD_HIP(hipMemsetAsync(miss.p, 0, 4, st));
+    if (total)
+        rare_pair_emit_kernel<<<grid_for(total), 256, 0, st>>>(
+            s->post_off.as<int64_t>(), s->post_sets.as<uint32_t>(), s->post_w.as<uint32_t>(), nl, P.as<int64_t>(),
+            total, upper ? 0 : 1, r0, r1, c0, c1, dto.as<int32_t>(), nb, kA.as<uint64_t>(), miss.as<int>());
+    GD_HIP(hipGetLastError());
+    int hmiss = 0;
+    d2h(&hmiss, miss.p, 4, st);
+    GD_REQUIRE(!hmiss, "rare pair outside the sparse plan's tiles");
+    uint64_t* keys = kA.as<uint64_t>(); uint64_t* alt = kB.as<uint64_t>();
+    sort_keys_u64(ctx, keys, alt, (size_t)total, 32, 64);
+    int64_t nu = 0;
+    DevBuf flag(total * 4 + 4, st), pos(total * 8 + 8, st);
+    if (total) {
+        rare_pair_heads_kernel<<<grid_for(total), 256, 0, st>>>(keys, total, flag.as<int32_t>());
+        GD_HIP(hipGetLastError());
+        exclusive_scan_i32_to_i64(ctx, flag.as<int32_t>(), pos.as<int64_t>(), (size_t)total);
+        int64_t last = 0;
+        int32_t lf = 0;
+        d2h(&last, pos.as<int64_t>() + total - 1, 8, st);
+        d2h(&lf, flag.as<int32_t>() + total - 1, 4, st);
+        nu = last + lf;
+    }
+    sc.rp_key.alloc(nu * 4 + 4, st);
+    sc.rp_w.alloc(nu * 4 + 4, st);
+    if (nu) {
+        rare_pair_runs_kernel<<<grid_for(total), 256, 0, st>>>(keys, total, flag.as<int32_t>(), pos.as<int64_t>(),
+                                                               sc.rp_key.as<uint32_t>(), sc.rp_w.as<uint32_t>());
+        GD_HIP(hipGetLastError());
     }
     const int64_t ngroups = (int64_t)tiles.size() * (SB * SB / 512);
-    std::vector<int64_t> goff(ngroups + 1, 0);
-    for (uint32_t k : keys) goff[(k >> 9) + 1]++;
-    for (int64_t g = 0; g < ngroups; g++) goff[g + 1] += goff[g];
-    sc.rp_key.alloc(keys.size() * 4 + 4, st);
-    sc.rp_w.alloc(ws.size() * 4 + 4, st);
-    sc.rp_off.alloc(goff.size() * 8, st);
-    if (!keys.empty()) {
-        h2d(sc.rp_key.p, keys.data(), keys.size() * 4, st);
-        h2d(sc.rp_w.p, ws.data(), ws.size() * 4, st);
-    }
-    h2d(sc.rp_off.p, goff.data(), goff.size() * 8, st);
+    sc.rp_off.alloc((ngroups + 1) * 8, st);
+    rare_group_offsets_kernel<<<grid_for(ngroups + 1), 256, 0, st>>>(sc.rp_key.as<uint32_t>(), nu, ngroups,
+                                                                      sc.rp_off.as<int64_t>());
+    GD_HIP(hipGetLastError());
+    GD_HIP(hipStreamSynchronize(st));
     sc.rare_in = true;
 }
 
