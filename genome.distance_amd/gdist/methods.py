@@ -12,13 +12,14 @@ plugin API of the un-vendored org.theseed:distance module:
 its previous-results reuse (:186-221, :270-272, :319-332), header, Java
 `Double.toString` rows (:283-289) and correlation statistics (:339-378).
 
-GPU form: a Measurer keeps its genome's kmer set packed in HBM. The pair
-list is grouped by id1 (GenomePairList.prepare, :240), so the driver asks
-each method for the whole group at once (`prefetch`: one pack of the group's
-second genomes and one device row query per method) and the per-pair
-`getDistance` calls — still issued concurrently, one thread per method, as
-:275 does — are answered from that row. `getDistance` on a genome outside a
-prefetched group is a correct single-pair device call.
+GPU form: a Measurer keeps its genome's kmer text. The pair list is grouped
+by id1 (GenomePairList.prepare, :240), so the driver asks each method for the
+whole group at once (`prefetch`: ONE pack of the first genome with the
+group's second genomes and one device row query per method) and the per-pair
+`getDistance` calls — issued concurrently, one thread per method, as :275
+does — are answered from that row without a lock on the method. A
+`getDistance` on a genome outside a prefetched group is one device call of
+its own (pack of the two genomes + a one-column row query).
 
 What the un-vendored module decides and this restatement infers (parity
 unpinned): the kmer methods' type names and parameter syntax
@@ -43,15 +44,16 @@ from .processors import Genome, ParseFailureException
 
 
 class Measurer:
-    """A genome prepared for repeated distance measurements (its kmer set in HBM)."""
+    """A genome prepared for repeated distance measurements: its kmer text,
+    built once (getMeasurer, MethodTableProcessor.java:397-407), and the row
+    of distances of its id1 group once prefetched."""
 
     def __init__(self, method: "DistanceMethod", genome: Genome):
         self.method = method
         self.genome = genome
-        self.sets = KmerSets.from_sequences([method.kmer_text(genome)], method.k, method.kmer_type,
-                                            method.flags, method.ctx)
+        self.text = method.kmer_text(genome)
         self._row: dict[str, float] = {}      # prefetched distances by second genome id
-        self._lock = threading.Lock()
+        self._lock = threading.Lock()         # guards _row only, never a device call
 
 
 class DistanceMethod:
@@ -84,7 +86,6 @@ class DistanceMethod:
 
     def __init__(self, ctx: Context | None = None):
         self.ctx = ctx or Context.default()
-        self._lock = threading.Lock()
 
     def parseParmString(self, parms: str) -> None:
         raise NotImplementedError
@@ -93,7 +94,10 @@ class DistanceMethod:
         return Measurer(self, genome)
 
     def getDistance(self, measurer: Measurer, genome: Genome) -> float:
-        """Thread-safe (the reference calls it from ForkJoin threads, :275)."""
+        """Thread-safe (the reference calls it from ForkJoin threads, :275):
+        a prefetched group's distance is a dictionary read; any other pair is
+        one device call of its own (no lock held across it: the library's
+        context serialises only its own device work)."""
         with measurer._lock:
             d = measurer._row.get(genome.id)
         if d is not None:
@@ -101,23 +105,29 @@ class DistanceMethod:
         return self.getDistances(measurer, [genome])[0]
 
     def getDistances(self, measurer: Measurer, genomes: Sequence[Genome]) -> list[float]:
-        """Batched getDistance: one pack of `genomes` and one device row query."""
+        """Batched getDistance: the measurer's genome and `genomes` packed in
+        ONE call (set 0 = the measurer's) and one device row query of set 0
+        against the rest: no copy of the measurer's set, no method-wide lock."""
         if not genomes:
             return []
-        with self._lock:
-            others = KmerSets.from_sequences([self.kmer_text(g) for g in genomes], self.k, self.kmer_type,
-                                             self.flags, self.ctx)
-            both = measurer.sets.concat(others)
-            d = both.row_query(0, range(1, 1 + len(genomes)), L.QUERY_ALL)
+        sets = KmerSets.from_sequences([measurer.text] + [self.kmer_text(g) for g in genomes], self.k,
+                                       self.kmer_type, self.flags, self.ctx)
+        try:
+            d = sets.row_query(0, range(1, 1 + len(genomes)), L.QUERY_ALL)
+        finally:
+            sets.free()
         return [float(x) for x in d]
 
     def prefetch(self, measurer: Measurer, genomes: Sequence[Genome]) -> None:
-        """Distances of a whole id1 group, kept on the measurer for getDistance."""
-        todo = [g for g in genomes if g.id not in measurer._row]
+        """Distances of a whole id1 group in one batched query, kept on the
+        measurer for getDistance (GenomePairList.prepare groups pairs by id1,
+        MethodTableProcessor.java:240,261-275)."""
+        with measurer._lock:
+            todo = [g for g in genomes if g.id not in measurer._row]
         uniq = list({g.id: g for g in todo}.values())
-        for g, d in zip(uniq, self.getDistances(measurer, uniq)):
-            with measurer._lock:
-                measurer._row[g.id] = d
+        row = dict(zip((g.id for g in uniq), self.getDistances(measurer, uniq)))
+        with measurer._lock:
+            measurer._row.update(row)
 
     def close(self) -> None:
         pass

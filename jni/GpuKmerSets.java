@@ -1,0 +1,66 @@
+package org.theseed.genome.distance.gpu;
+
+/**
+ * Java side of jni/gdist_jni.c: a collection of kmer sets resident on one
+ * MI355X (libgdist.so, include/gdist.h). What it replaces in the reference:
+ * KmerType.createKmers / new GenomeKmers / new ProteinKmers (pack),
+ * SequenceKmers.distance over row blocks (distances: FastaDistanceProcessor
+ * and GenomeProcessor loops), anyMatch / argmin row queries
+ * (DistanceRepsProcessor), hashSet(width) + Sketch.distance (WidthProcessor).
+ * Callers batch: one call per row block, group or matrix, never per pair.
+ */
+public final class GpuKmerSets implements AutoCloseable {
+    static { System.loadLibrary("gdist_jni"); }
+
+    public static final int DNA = 0, PROT = 1;
+    public static final int METHOD_AUTO = 0, METHOD_SORTED = 1, METHOD_BITSET = 2;
+    public static final int UPPER_TRIANGLE = 0x100;
+
+    static native long nCtxCreate(int device);
+    static native void nCtxDestroy(long ctx);
+    static native void nSetOption(long ctx, String name, long value);
+    static native long nPack(long ctx, int kind, int k, int flags, byte[][] seqs);
+    static native void nFree(long sets);
+    static native long nSize(long sets);
+    static native void nSizes(long sets, long[] out);
+    static native void nBuildBitsets(long sets, int flags);
+    static native int nPrepare(long ctx, long sets, int method, double pairs);
+    static native void nMatrix(long ctx, long sets, long r0, long r1, long c0, long c1, int method, int flags,
+                               double[] out, int ld);
+    static native boolean nAnyLe(long ctx, long sets, long q, long[] cols, double t);
+    static native int nArgmin(long ctx, long sets, long q, long[] cols, double[] bestD);
+    static native void nRow(long ctx, long sets, long q, long[] cols, double[] out);
+    static native long nGreedyReps(long ctx, long sets, double t, long[] tieRank, int[] isRep, long[] repOf,
+                                   double[] repDist);
+    static native long nSketch(long ctx, long sets, int width);
+    static native void nSketchMatrix(long ctx, long sk, long r0, long r1, long c0, long c1, int flags,
+                                     double[] out, int ld);
+
+    private final long ctx;
+    private long handle;
+
+    /** kmer sets of `seqs` (KmerType.createKmers(seq, k) for each), packed on the device. */
+    public GpuKmerSets(long ctx, int kind, int k, byte[][] seqs) {
+        this.ctx = ctx;
+        this.handle = nPack(ctx, kind, k, 0, seqs);
+    }
+
+    public long size() { return nSize(handle); }
+
+    /** distances of rows [r0, r1) x columns [c0, c1), row-major with stride ld */
+    public void distances(long r0, long r1, long c0, long c1, boolean upperTriangle, double[] out, int ld) {
+        nMatrix(ctx, handle, r0, r1, c0, c1, METHOD_AUTO, upperTriangle ? UPPER_TRIANGLE : 0, out, ld);
+    }
+
+    public boolean anyWithin(long q, long[] cols, double maxDist) { return nAnyLe(ctx, handle, q, cols, maxDist); }
+
+    public void row(long q, long[] cols, double[] out) { nRow(ctx, handle, q, cols, out); }
+
+    @Override
+    public synchronized void close() {
+        if (handle != 0) {
+            nFree(handle);
+            handle = 0;
+        }
+    }
+}
