@@ -1709,9 +1709,7 @@ double sorted_cost_s(const gdist_sets* s, double pairs) {
 }
 
 void free_bitsets(gdist_sets* s) {
-    s->graphs.clear();
-    s->plans.clear();
-    free_sparse(s);
+    free_sparse(s);                      // (synchronises both streams, clears plans and graphs)
     s->bits.release();
     s->post_off.release();
     s->post_sets.release();
@@ -1753,6 +1751,9 @@ static MatrixPlan& matrix_plan(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, 
     auto it = s->plans.find(key);
     if (it == s->plans.end()) {
         if (s->plans.size() >= 8) {   // row-block loops: keep the cache small
+            // launches on either stream may still read the old plans' buffers
+            GD_HIP(hipStreamSynchronize(ctx->side));
+            GD_HIP(hipStreamSynchronize(ctx->stream));
             s->graphs.clear();        // (captured steps hold the plans' buffers)
             s->plans.clear();
         }

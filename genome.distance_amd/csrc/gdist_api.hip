@@ -64,16 +64,11 @@ void* cache_alloc(int device, size_t bytes, size_t* cls_out) {
     *cls_out = cls;
     auto& c = block_cache();
     {
-        // best fit: the smallest cached block of at least this class, if it
-        // is at most 25 % larger (chunked setup paths ask for slightly
-        // different sizes every chunk; exact-class reuse left them all cached)
         std::lock_guard<std::mutex> lk(c.mu);
-        auto& fb = c.free_blocks[device];
-        auto it = fb.lower_bound(cls);
-        if (it != fb.end() && it->first <= cls + cls / 4) {
+        auto it = c.free_blocks[device].find(cls);
+        if (it != c.free_blocks[device].end()) {
             void* p = it->second;
-            *cls_out = it->first;
-            fb.erase(it);
+            c.free_blocks[device].erase(it);
             return p;
         }
     }
@@ -386,7 +381,14 @@ int gdist_dev_alloc(gdist_ctx* ctx, int64_t bytes, void** dptr) {
         std::lock_guard<std::recursive_mutex> lk_(ctx->mu);
         GD_REQUIRE(dptr && bytes >= 0, "bad allocation request");
         *dptr = nullptr;
-        if (bytes) GD_HIP(hipMalloc(dptr, (size_t)bytes));
+        if (!bytes) return;
+        hipError_t e = hipMalloc(dptr, (size_t)bytes);
+        if (e == hipErrorOutOfMemory) {          // the library's cached blocks may hold the memory
+            (void)hipGetLastError();
+            gdist::cache_trim(ctx->device);
+            e = hipMalloc(dptr, (size_t)bytes);
+        }
+        GD_HIP(e);
     });
 }
 
@@ -1294,8 +1296,10 @@ int gdist_sets_exchange_plan(gdist_ctx* ctx, const gdist_sets* local, int method
         double mxt = 0, mxn = 0;
         for (int r = 0; r < R; r++) { mxt = std::max(mxt, (double)h[3 * r + 1]); mxn = std::max(mxn, (double)h[3 * r + 2]); }
         const double es = local->kind == GDIST_SKETCH ? 4.0 : 8.0;
-        // codes: the padded gather + staging (the local codes consumed)
-        const double b_codes = ((double)R + 1.0) * mxt * es;
+        // codes (the local shard consumed, GDIST_ALLGATHER_CONSUME): the padded
+        // gather + one shard (the local codes while they are copied into their
+        // slot, then the compaction's staging); one rank adopts its own buffer
+        const double b_codes = R == 1 ? mxt * es : ((double)R + 1.0) * mxt * es;
         // bitsets: the local codes + the gathered summaries (12 B per
         // distinct code) + the merge's workspace (~2x them)
         const double b_bits = local->kind == GDIST_SKETCH ? INFINITY : mxt * 8.0 + 3.0 * (double)R * mxn * 12.0;

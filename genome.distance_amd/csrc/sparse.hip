@@ -624,6 +624,10 @@ void locus_perm(gdist_ctx* ctx, DevBuf& key, int64_t U, DevBuf& perm) {
 bool locus_order_enabled(const gdist_ctx* ctx) { return ctx->option(OPT_LOCUS_ORDER, 1) != 0; }
 
 void free_sparse(gdist_sets* s) {
+    if (s->ctx) {                        // launches on the side stream may still read these buffers
+        (void)hipStreamSynchronize(s->ctx->side);
+        (void)hipStreamSynchronize(s->ctx->stream);
+    }
     s->graphs.clear();
     s->plans.clear();
     s->dbits.release();
@@ -885,7 +889,11 @@ __global__ void rare_group_offsets_kernel(const uint32_t* __restrict__ ukey, int
 }
 
 static void rare_pair_table(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1,
-                            bool upper, const std::vector<int2>& tiles, hipStream_t st, SparseScratch& sc) {
+                            bool upper, const std::vector<int2>& tiles, SparseScratch& sc) {
+    // on the context's main stream, whatever stream the plan is built for:
+    // the radix sort and the scans run there; the table is complete (stream
+    // synchronised) before any launch reads it
+    hipStream_t st = ctx->stream;
     sc.rare_in = false;
     if (s->n_rare == 0) return;
     if (ctx->option(OPT_SPARSE_RARE, 1) == 0 || s->rare_records > kRarePairsMax) return;
@@ -1040,7 +1048,7 @@ void sparse_plan(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, in
                     sc.use_part ? "partials" : "atomic flush", (long long)s->sp_pos_words,
                     (long long)s->Ws);
         GD_REQUIRE(sc.ntiles * sc.nchunks < (int64_t(1) << 31), "sparse grid too large");
-        if (sc.use_part) rare_pair_table(ctx, s, r0, r1, c0, c1, upper, tiles, st, sc);
+        if (sc.use_part) rare_pair_table(ctx, s, r0, r1, c0, c1, upper, tiles, sc);
         sc.ready = true;
     }
 }

@@ -307,7 +307,8 @@ int  gdist_sets_allgather_ex(gdist_ctx* ctx, gdist_sets* local, unsigned flags, 
  * (gdist_sets_allgather_ex) for the sorted join. METHOD_AUTO takes the
  * dictionary exchange when its per-rank estimate fits the budget (option
  * "exchange_budget", default 0.8 x the device memory), else the codes; the
- * estimates (bytes per rank) are returned. ENOMEM when neither fits.
+ * estimates (bytes per rank; the codes' assume the shard is consumed) are
+ * returned. ENOMEM when neither fits.
  * (C4 = 100,000 x 100 kbp on 8 GPUs takes the codes.) */
 int  gdist_sets_exchange_plan(gdist_ctx* ctx, const gdist_sets* local, int method, int* chosen,
                               double* bytes_bitsets, double* bytes_codes);
