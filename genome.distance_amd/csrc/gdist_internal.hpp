@@ -201,7 +201,8 @@ struct Timing {
     X(PACK_SUMMARY, "pack_summary")           /* 0: set|code pack keys, the bitset build re-sorts codes */     \
     X(PACK_OVERLAP, "pack_overlap")           /* 0: upload first / 1: overlapped host thread / 2: registered */\
     X(PACK_CHUNK, "pack_chunk")               /* kmer windows per pack chunk (default 2^28) */                 \
-    X(EXCHANGE_BUDGET, "exchange_budget")     /* device bytes an exchange may use (default 0.8 x HBM) */
+    X(EXCHANGE_BUDGET, "exchange_budget")     /* device bytes an exchange may use (default 0.8 x HBM) */    \
+    X(PACK_CODES_BUDGET, "pack_codes_budget") /* bytes of the one-buffer pack (default 1/4 HBM; past it: grown) */
 
 enum Opt : int {
 #define GDIST_OPT_ENUM(id, name) OPT_##id,

@@ -586,14 +586,43 @@ void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_se
     Trace tr(st, ctx->trace());
     tr.mark("pack: validate/fold");
     size_t ci = 0;
-    // every chunk compacts its unique codes straight into one buffer sized
-    // for every window (an upper bound; trimmed below when far too large)
+    // every chunk compacts its unique codes straight into one buffer. When
+    // a buffer for every window (the upper bound `cap`) fits the budget
+    // (option pack_codes_budget, default 1/4 of the device memory) it is
+    // that; otherwise it is sized after the first chunk from its unique /
+    // window ratio and grows (by >= 25 %, re-projected) when a chunk would
+    // overflow it, so repetitive input (small k, near-identical sets) needs
+    // about its unique codes instead of 8 B per window
     int64_t cap = 0;
     for (int64_t s = 0; s < nseq; s++) cap += nwin[s] * mult;
-    DevBuf all_codes(cap * 8 + 8, st);
+    int64_t codes_budget = ctx->option(OPT_PACK_CODES_BUDGET, -1);
+    if (codes_budget < 0) {
+        hipDeviceProp_t prop;
+        GD_HIP(hipGetDeviceProperties(&prop, ctx->device));
+        codes_budget = (int64_t)(prop.totalGlobalMem / 4);
+    }
+    int64_t base = 0;                      // unique codes compacted so far
+    DevBuf all_codes;
+    int64_t all_cap = 0;                   // codes all_codes holds room for
+    if (cap * 8 <= codes_budget) {
+        all_codes.alloc(cap * 8 + 8, st);
+        all_cap = cap;
+    }
+    // room for `need` codes after `done` of the cap's windows were packed
+    auto ensure = [&](int64_t need, int64_t done) {
+        if (need <= all_cap) return;
+        const double proj = (double)need * (double)cap / (double)std::max<int64_t>(done, 1) * 1.125;
+        int64_t want = std::max<int64_t>(need, (int64_t)std::min<double>((double)cap, proj));
+        if (all_cap) want = std::max<int64_t>(want, std::min<int64_t>(cap, all_cap + all_cap / 4));
+        want = std::max(need, std::min(cap, want));
+        DevBuf grown(want * 8 + 8, st);
+        if (base) GD_HIP(hipMemcpyAsync(grown.p, all_codes.p, base * 8, hipMemcpyDeviceToDevice, st));
+        all_codes = std::move(grown);      // releases the old block after the stream drained
+        all_cap = want;
+    };
+    int64_t done = 0;                      // windows (x strands) of the chunks packed so far
     std::vector<int64_t> h_off(nseq + 1, 0);
     DevBuf d_off((nseq + 1) * sizeof(int64_t), st);
-    int64_t base = 0;
     int64_t s0 = 0;
     bool want_sum = ctx->option(OPT_PACK_SUMMARY, 1) != 0, sum_ok = true;
     std::vector<Summary> pack_sum;
@@ -683,6 +712,8 @@ void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_se
                 GD_HIP(hipStreamSynchronize(st));
             }
             tr.mark("pack: unique+summary+by set");
+            done += n;
+            ensure(base + uniq, done);
             if (uniq > 0) {
                 cm_codes_kernel<<<grid_for(uniq), 256, 0, st>>>(keys, uniq, idbits, all_codes.as<uint64_t>() + base);
                 GD_HIP(hipGetLastError());
@@ -747,6 +778,8 @@ void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_se
         d2h(co.data(), d_off.as<int64_t>() + s0, (nc + 1) * sizeof(int64_t), st);
         GD_HIP(hipStreamSynchronize(st));
         const int64_t uniq = co[nc] - base;
+        done += n;
+        ensure(base + uniq, done);
         if (n > 0) {
             compact_kernel<<<grid_for(n), 256, 0, st>>>(keys, flag.as<int32_t>(), pos.as<int64_t>(), n,
                                                          all_codes.as<uint64_t>() + base);
@@ -767,7 +800,11 @@ void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_se
         GD_HIP(hipMemsetAsync(out->off.p, 0, sizeof(int64_t), st));
         out->h_off.assign(1, 0);
     }
-    if (base < cap / 2 && (cap - base) * 8 > (int64_t(64) << 20)) {
+    if (!all_codes.p) {                   // no window at all
+        all_codes.alloc(8, st);
+        all_cap = 0;
+    }
+    if (base < all_cap / 2 && (all_cap - base) * 8 > (int64_t(64) << 20)) {
         // mostly repeated windows: keep an exact-size copy instead of the bound
         out->codes.alloc(base * 8 + 8, st);
         if (base) GD_HIP(hipMemcpyAsync(out->codes.p, all_codes.p, base * 8, hipMemcpyDeviceToDevice, st));

@@ -64,7 +64,11 @@ PACK_MODES = {"default": {}, "set_major": {"pack_summary": 0},
               # chunk c + 1 overlapped with chunk c (or not)
               "chunked": {"pack_chunk": 1000}, "chunked_set_major": {"pack_chunk": 1000, "pack_summary": 0},
               "chunked_no_overlap": {"pack_chunk": 1000, "pack_overlap": 0},
-              "chunked_pinned": {"pack_chunk": 1000, "pack_overlap": 2}}
+              "chunked_pinned": {"pack_chunk": 1000, "pack_overlap": 2},
+              # the codes buffer sized from the first chunk and grown (budget 0:
+              # never the one buffer for every window)
+              "grown": {"pack_chunk": 1000, "pack_codes_budget": 0},
+              "grown_set_major": {"pack_chunk": 1000, "pack_codes_budget": 0, "pack_summary": 0}}
 
 
 @pytest.mark.parametrize("mode", sorted(PACK_MODES))
@@ -100,7 +104,26 @@ def test_pack_random_modes(ctx, opts, seed, mode):
         assert np.array_equal(off, eo) and np.array_equal(codes, ec), (kind, k, flags)
 
 
-@pytest.mark.parametrize("mode", ["chunked", "chunked_set_major", "chunked_no_overlap", "chunked_pinned"])
+def test_pack_repetitive_small_k_grown(ctx, opts):
+    """repetitive input with a small k (protein k=3 over a few
+    residues: every set holds a few hundred distinct kmers of thousands of
+    windows) packed in small chunks into the grown codes buffer: codes,
+    offsets and the matrix equal the oracle."""
+    import gdist
+    rng = np.random.default_rng(5)
+    seqs = [bytes(rng.choice(np.frombuffer(b"ACDEFG", np.uint8), 4000)) for _ in range(60)]
+    opts(pack_chunk=20000, pack_codes_budget=0)
+    sets = gdist.KmerSets.from_sequences(seqs, 3, gdist.KmerType.PROT, 0, ctx)
+    eo, ec = oracle_pack(seqs, 3, 1, 0)
+    off, codes = sets.download()
+    assert np.array_equal(off, eo) and np.array_equal(codes, ec)
+    assert len(ec) < 60 * 4000 / 10                  # far fewer unique codes than windows
+    eI, eD = oracle.matrix(eo, ec, 0, 60, 0, 60)
+    I, D = sets.matrix(method=gdist.METHOD_SORTED)
+    assert np.array_equal(I, eI) and bits_equal(D, eD)
+
+
+@pytest.mark.parametrize("mode", ["chunked", "chunked_set_major", "chunked_no_overlap", "chunked_pinned", "grown"])
 def test_chunked_pack_bitset_matrix(ctx, opts, mode):
     """A collection packed in ~20 chunks (chunk summaries merged for the
     dictionary, uploads overlapped): codes, then the bitset matrix, equal the
