@@ -927,7 +927,13 @@ static void rare_pair_table(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int
     d2h(&hmiss, miss.p, 4, st);
     GD_REQUIRE(!hmiss, "rare pair outside the sparse plan's tiles");
     uint64_t* keys = kA.as<uint64_t>(); uint64_t* alt = kB.as<uint64_t>();
-    sort_keys_u64(ctx, keys, alt, (size_t)total, 32, 64);
+    // sorted over all their bits (the low half, the weight, only orders equal
+    // keys): rocPRIM's radix sort with a non-zero begin_bit left these keys
+    // unsorted on gfx950 (round 3; every sort here starts at bit 0). The
+    // sentinel (all ones) sorts last.
+    int tbits = 1;
+    while ((int64_t(1) << tbits) < (int64_t)tiles.size()) tbits++;
+    sort_keys_u64(ctx, keys, alt, (size_t)total, 0, std::min(64, 32 + 14 + tbits + 1));
     int64_t nu = 0;
     DevBuf flag(total * 4 + 4, st), pos(total * 8 + 8, st);
     if (total) {
