@@ -81,6 +81,22 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+class stdout_to_stderr:
+    """RCCL prints its version banner on stdout when a communicator is
+    created; the driver reads ONE JSON line from stdout, so file descriptor
+    1 points at stderr while the library initialises RCCL."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -179,7 +195,8 @@ def main():
     exchange = world > 1 or args.force_exchange
     if exchange:
         if args.force_exchange and world == 1:
-            ctx.comm_init(gdist.Context.unique_id(), 1, 0)
+            with stdout_to_stderr():
+                ctx.comm_init(gdist.Context.unique_id(), 1, 0)
             ctx.set_option("force_exchange", 1)
         elif args.transport == "host":
             import torch
@@ -194,7 +211,8 @@ def main():
             uid = gdist.Context.unique_id() if rank == 0 else None
             obj = [uid]
             dist.broadcast_object_list(obj, src=0)
-            ctx.comm_init(obj[0], world, rank)
+            with stdout_to_stderr():
+                ctx.comm_init(obj[0], world, rank)
     xplan = None
     if exchange and method in ("auto", "bitset", "sorted"):
         # the exchange every rank takes (collective): the dictionary exchange

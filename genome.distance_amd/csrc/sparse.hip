@@ -369,8 +369,12 @@ __device__ __forceinline__ void sparse_walk_off(const int4* __restrict__ rec, in
 #pragma unroll
         for (int u = 0; u < SUN; u++) {
             const uint32_t rc = a[u].a;
+            // the second column's word is masked, not branched on: a branch
+            // let the compiler sink that load behind it and wait on memory
+            // inside the loop (round 3 ISA)
+            const uint32_t m1 = ncol[u] > 1 ? ~0u : 0u;
             const uint32_t v0 = (uint32_t)(__popc(a[u].b & b0[u].a) + __popc(a[u].c & b0[u].b));
-            const uint32_t v1 = ncol[u] > 1 ? (uint32_t)(__popc(a[u].b & b1[u].a) + __popc(a[u].c & b1[u].b)) : 0u;
+            const uint32_t v1 = (uint32_t)(__popc(a[u].b & b1[u].a & m1) + __popc(a[u].c & b1[u].b & m1));
             cnt_add(cnt, rc, b0[u].c, v0);
             cnt_add(cnt, rc, b1[u].c, v1);
         }
