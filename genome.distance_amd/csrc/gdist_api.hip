@@ -582,6 +582,14 @@ int gdist_sets_sparse_sides(const gdist_sets* s, int64_t* complement_words, int6
     });
 }
 
+int gdist_sets_group_info(const gdist_sets* s, int64_t* groups, int64_t* grouped_words) {
+    return guard([&] {
+        check_sets(s);
+        if (groups) *groups = s->sparse ? s->sp_groups : 0;
+        if (grouped_words) *grouped_words = s->sparse ? s->sp_group_words : 0;
+    });
+}
+
 int gdist_sets_rare_kmers(const gdist_sets* s, int64_t* kmers) {
     return guard([&] {
         check_sets(s);

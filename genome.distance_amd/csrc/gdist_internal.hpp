@@ -202,7 +202,8 @@ struct Timing {
     X(PACK_OVERLAP, "pack_overlap")           /* 0: upload first / 1: overlapped host thread / 2: registered */\
     X(PACK_CHUNK, "pack_chunk")               /* kmer windows per pack chunk (default 2^28) */                 \
     X(EXCHANGE_BUDGET, "exchange_budget")     /* device bytes an exchange may use (default 0.8 x HBM) */    \
-    X(PACK_CODES_BUDGET, "pack_codes_budget") /* bytes of the one-buffer pack (default 1/4 HBM; past it: grown) */
+    X(PACK_CODES_BUDGET, "pack_codes_budget") /* bytes of the one-buffer pack (default 1/4 HBM; past it: grown) */\
+    X(SPARSE_GROUPS, "sparse_groups")         /* 0: no group tier (clade patterns) in the sparse words */
 
 enum Opt : int {
 #define GDIST_OPT_ENUM(id, name) OPT_##id,
@@ -335,6 +336,11 @@ struct gdist_sets {
     int64_t sp_pos_words = 0;             // sparse words counted from their set bits (positive-sparse)
     bool sp_fold_dense = false;           // the dense words are counted by the sparse tile kernel (no tile launch),
     int sp_fold_slabs = 0;                // 8 words per chunk in the first sp_fold_slabs chunks
+    // group tier (sparse.hip): words whose heavy entries are one group's
+    // pattern keep per member only the residual; the group part of every
+    // pair is X[i][j] (int32 [nsets][nsets], symmetric), added by the reduce
+    gdist::DevBuf sp_x;
+    int64_t sp_groups = 0, sp_group_words = 0;
     std::vector<int32_t> sp_bucket_bits;  // [nsets][sp_nbk]: complement bits per set and 1024 sparse words
     int64_t sp_nbk = 0;
     // summaries of the pack chunks (option pack_summary): the code-major pack

@@ -25,6 +25,7 @@
 // C2 (1000 x 2 Mbp): 62.5 K words of which every one is sparse (z_w ~ 51 of
 // 1000), 95 M products per step instead of 31 G word pairs.
 #include <algorithm>
+#include <map>
 #include <cmath>
 #include <cstring>
 
@@ -132,27 +133,45 @@ __device__ __forceinline__ unsigned long long entry_word(unsigned long long b, u
     return pos ? (b & m) : (~b & m);
 }
 
-// entries per (block b, sparse word s): sets of the block whose entry word is non-zero
+// Group tier (below): a factorised word s keeps of each grouped set only
+// the residual, the bits of its entry word outside its group's pattern
+constexpr int kGroupMax = 64;                    // groups (disjoint sets of sets) per collection
+struct GroupWords {
+    const int32_t* grp = nullptr;               // [N] group of each set, -1: none
+    const int32_t* prow = nullptr;              // [Ws] pattern row of sparse word s, -1: not factorised
+    const unsigned long long* pats = nullptr;   // [rows][m] each group's pattern in the word
+    int m = 0;                                  // groups
+    int32_t* V = nullptr;                       // [m][N] group x set part (filled with the entries)
+    int64_t N = 0;
+};
+__device__ __forceinline__ unsigned long long residual(unsigned long long e, const GroupWords& gw, int r, int64_t i) {
+    if (r < 0) return e;
+    const int g = gw.grp[i];
+    return g >= 0 ? (e & ~gw.pats[(int64_t)r * gw.m + g]) : e;
+}
+
+// entries per (block b, sparse word s): sets of the block whose (residual) entry word is non-zero
 __global__ __launch_bounds__(256) void sparse_count_kernel(const unsigned long long* __restrict__ bits, int64_t N,
                                                            int64_t W, int64_t U, const int32_t* __restrict__ sw,
                                                            const uint8_t* __restrict__ spos, int64_t Ws,
-                                                           int32_t* __restrict__ cnt) {
+                                                           GroupWords gw, int32_t* __restrict__ cnt) {
     const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t b = blockIdx.y;
     if (s >= Ws) return;
     const int64_t w = sw[s];
     const bool pos = spos[s] != 0;
     const unsigned long long m = valid_mask(w, U);
+    const int r = gw.prow ? gw.prow[s] : -1;
     const int64_t i1 = (b + 1) * SB < N ? (b + 1) * SB : N;
     int c = 0;
-    for (int64_t i = b * SB; i < i1; i++) c += entry_word(bits[i * W + w], m, pos) != 0;
+    for (int64_t i = b * SB; i < i1; i++) c += residual(entry_word(bits[i * W + w], m, pos), gw, r, i) != 0;
     cnt[b * Ws + s] = c;
 }
 
 __global__ __launch_bounds__(256) void sparse_fill_kernel(const unsigned long long* __restrict__ bits, int64_t N,
                                                           int64_t W, int64_t U, const int32_t* __restrict__ sw,
                                                           const uint8_t* __restrict__ spos,
-                                                          int64_t Ws, const int64_t* __restrict__ off,
+                                                          int64_t Ws, GroupWords gw, const int64_t* __restrict__ off,
                                                           unsigned long long* __restrict__ word,
                                                           uint8_t* __restrict__ set, int32_t* __restrict__ nc,
                                                           int32_t* __restrict__ bucket_bits, int64_t nbk) {
@@ -162,17 +181,200 @@ __global__ __launch_bounds__(256) void sparse_fill_kernel(const unsigned long lo
     const int64_t w = sw[s];
     const bool pos = spos[s] != 0;
     const unsigned long long m = valid_mask(w, U);
+    const int r = gw.prow ? gw.prow[s] : -1;
     const int64_t i1 = (b + 1) * SB < N ? (b + 1) * SB : N;
     int64_t p = off[b * Ws + s];
     for (int64_t i = b * SB; i < i1; i++) {
-        const unsigned long long c = entry_word(bits[i * W + w], m, pos);
+        const unsigned long long e = entry_word(bits[i * W + w], m, pos);
+        // constant part: the complement words' WHOLE complement bits
+        if (!pos && e) atomicAdd(nc + i, (int32_t)__popcll(e));
+        const unsigned long long c = residual(e, gw, r, i);
         if (c) {
             word[p] = c;
             set[p] = (uint8_t)(i - b * SB);
             p++;
-            if (!pos) atomicAdd(nc + i, (int32_t)__popcll(c));     // constant part: complement words only
             atomicAdd(bucket_bits + i * nbk + (s >> kBucketShift), (int32_t)__popcll(c));
+            if (r >= 0)                    // V[G][i] += popc(P_G & a_i) (group tier)
+                for (int g = 0; g < gw.m; g++) {
+                    const int v = __popcll(gw.pats[(int64_t)r * gw.m + g] & c);
+                    if (v) atomicAdd(gw.V + (int64_t)g * gw.N + i, v);
+                }
         }
+    }
+}
+
+// ---- group tier -----------------------------------------------------------
+// Structured collections (clades: C2-realistic) hold words whose entry word
+// carries, in every member of a group of sets, that group's pattern (the
+// clade's variant lacked, or held, by all its members), plus each set's own
+// few bits. The groups partition (part of) the sets. In a factorised word,
+// group G's pattern P_G is the AND of its members' entry words, so a member's
+// e_i = P_G ∪ a_i with P_G ∩ a_i = ∅ (a_i, the residual) and an ungrouped
+// set has P = ∅, a_i = e_i. Per pair the four parts are disjoint:
+//   popc(e_i & e_j) = popc(P_gi & P_gj) + popc(P_gi & a_j) + popc(a_i & P_gj) + popc(a_i & a_j)
+// Summed over the factorised words:
+//   T[G][H] = Σ_w popc(P_G & P_H),  V[G][j] = Σ_w popc(P_G & a_j)  (0 for members of G)
+//   X[i][j] = T[gi][gj] + V[gi][j] + V[gj][i]
+// and the residuals are ordinary sparse entries; the reduce / flush adds
+// X[i][j] (int32, [N][N]). Any choice of groups is exact (the pattern is the
+// AND over the members); the choice only decides how much work leaves the
+// products. Groups are found from the data: per heavy word, the most
+// frequent non-zero entry value v and its members {i : e_i ⊇ v}; member
+// lists recurring over many words (hash of the bitmap) are taken greedily,
+// most words first, keeping them disjoint.
+constexpr int kGroupSample = 4096;               // sets sampled for a word's modal entry value
+constexpr int kGroupMinSize = 16;                // smallest group worth a pattern
+constexpr int kGroupMinWords = 8;                // ... and the fewest words it must recur in
+constexpr int kGroupMinZ = 32;                   // candidate words: at least this many entries
+constexpr int64_t kGroupMaxN = 16384;            // X is N x N int32
+
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// Per candidate word c: the most frequent non-zero entry value v among the
+// first kGroupSample sets (bitonic sort in LDS, longest run), then its
+// members {i : e_i ⊇ v} over all sets as a bitmap, their number and a hash
+// of the bitmap.
+__global__ __launch_bounds__(256) void group_modal_kernel(const unsigned long long* __restrict__ bits, int64_t N,
+                                                          int64_t W, int64_t U, const int32_t* __restrict__ cw,
+                                                          const uint8_t* __restrict__ cpos, int64_t nwb,
+                                                          unsigned long long* __restrict__ mbits,
+                                                          int32_t* __restrict__ msize,
+                                                          unsigned long long* __restrict__ mhash) {
+    __shared__ unsigned long long v[kGroupSample];
+    __shared__ unsigned long long rv[256];
+    __shared__ int rn[256];
+    const int64_t c = blockIdx.x;
+    const int64_t w = cw[c];
+    const bool pos = cpos[c] != 0;
+    const unsigned long long m = valid_mask(w, U);
+    const int n = (int)(N < kGroupSample ? N : kGroupSample);
+    int np = 1;
+    while (np < n) np <<= 1;
+    for (int t = threadIdx.x; t < np; t += 256) v[t] = t < n ? entry_word(bits[(int64_t)t * W + w], m, pos) : ~0ull;
+    __syncthreads();
+    for (int k = 2; k <= np; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int t = threadIdx.x; t < np; t += 256) {
+                const int x = t ^ j;
+                if (x > t) {
+                    const unsigned long long a = v[t], b = v[x];
+                    if ((a > b) == ((t & k) == 0)) { v[t] = b; v[x] = a; }
+                }
+            }
+            __syncthreads();
+        }
+    int bn = 0;
+    unsigned long long bv = 0;
+    for (int p = threadIdx.x; p < n; p += 256) {
+        const unsigned long long x = v[p];
+        if (x == 0 || (p > 0 && v[p - 1] == x)) continue;
+        int e = p + 1;
+        while (e < n && v[e] == x) e++;
+        if (e - p > bn || (e - p == bn && x < bv)) { bn = e - p; bv = x; }
+    }
+    rv[threadIdx.x] = bv;
+    rn[threadIdx.x] = bn;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) {
+            const int a = rn[threadIdx.x], b = rn[threadIdx.x + o];
+            const unsigned long long x = rv[threadIdx.x], y = rv[threadIdx.x + o];
+            if (b > a || (b == a && y < x)) { rn[threadIdx.x] = b; rv[threadIdx.x] = y; }
+        }
+        __syncthreads();
+    }
+    const unsigned long long v0 = rn[0] >= 2 ? rv[0] : 0ull;
+    __syncthreads();
+    int cnt = 0;
+    unsigned long long h = 0;
+    for (int64_t q = threadIdx.x; q < nwb; q += 256) {
+        unsigned long long word = 0;
+        for (int b = 0; b < 64; b++) {
+            const int64_t i = q * 64 + b;
+            if (i >= N) break;
+            const unsigned long long e = entry_word(bits[i * W + w], m, pos);
+            if (v0 && (e & v0) == v0) word |= 1ull << b;
+        }
+        mbits[c * nwb + q] = word;
+        cnt += __popcll(word);
+        h += mix64(word ^ (0x632BE59BD9B4E019ull * (unsigned long long)(q + 1)));
+    }
+    rn[threadIdx.x] = cnt;
+    rv[threadIdx.x] = h;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) { rn[threadIdx.x] += rn[threadIdx.x + o]; rv[threadIdx.x] += rv[threadIdx.x + o]; }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) { msize[c] = v0 ? rn[0] : 0; mhash[c] = rv[0]; }
+}
+
+// Every group's pattern in candidate word c (AND of its members' entry
+// words, LDS atomics) and the word's residual entry count
+__global__ __launch_bounds__(256) void group_pattern_kernel(const unsigned long long* __restrict__ bits, int64_t N,
+                                                            int64_t W, int64_t U, const int32_t* __restrict__ cw,
+                                                            const uint8_t* __restrict__ cpos,
+                                                            const int32_t* __restrict__ grp, int mg,
+                                                            unsigned long long* __restrict__ cpat,
+                                                            int32_t* __restrict__ zres) {
+    __shared__ unsigned long long pat[kGroupMax];
+    __shared__ int rz[256];
+    const int64_t c = blockIdx.x;
+    const int64_t w = cw[c];
+    const bool pos = cpos[c] != 0;
+    const unsigned long long m = valid_mask(w, U);
+    for (int g = threadIdx.x; g < mg; g += 256) pat[g] = ~0ull;
+    __syncthreads();
+    for (int64_t i = threadIdx.x; i < N; i += 256) {
+        const int g = grp[i];
+        if (g >= 0) atomicAnd(&pat[g], entry_word(bits[i * W + w], m, pos));
+    }
+    __syncthreads();
+    int z = 0;
+    for (int64_t i = threadIdx.x; i < N; i += 256) {
+        const int g = grp[i];
+        const unsigned long long e = entry_word(bits[i * W + w], m, pos);
+        z += (g >= 0 ? (e & ~pat[g]) : e) != 0;
+    }
+    rz[threadIdx.x] = z;
+    for (int g = threadIdx.x; g < mg; g += 256) cpat[c * mg + g] = pat[g];
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) rz[threadIdx.x] += rz[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) zres[c] = rz[0];
+}
+
+// T[G][H] += popc(P_G & P_H) per factorised word (pattern row r)
+__global__ void group_t_kernel(const unsigned long long* __restrict__ pats, int64_t rows, int mg,
+                               int32_t* __restrict__ T) {
+    const int64_t r = blockIdx.x;
+    if (r >= rows) return;
+    for (int e = threadIdx.x; e < mg * mg; e += blockDim.x) {
+        const int G = e / mg, H = e - G * mg;
+        const int v = __popcll(pats[r * mg + G] & pats[r * mg + H]);
+        if (v) atomicAdd(T + e, v);
+    }
+}
+
+// X[i][j] = T[gi][gj] + V[gi][j] + V[gj][i]
+__global__ void group_x_kernel(int64_t N, const int32_t* __restrict__ grp, int mg, const int32_t* __restrict__ T,
+                               const int32_t* __restrict__ V, int32_t* __restrict__ X) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < N * N; e += stride) {
+        const int64_t i = e / N, j = e - i * N;
+        const int gi = grp[i], gj = grp[j];
+        int x = 0;
+        if (gi >= 0) x += V[(int64_t)gi * N + j];
+        if (gj >= 0) x += V[(int64_t)gj * N + i];
+        if (gi >= 0 && gj >= 0) x += T[gi * mg + gj];
+        X[e] = x;
     }
 }
 
@@ -403,7 +605,8 @@ __global__ __launch_bounds__(SNT, 8) void sparse_tile_kernel(
     const int64_t* __restrict__ off, const ulonglong2* __restrict__ ent, const int32_t* __restrict__ nc, int64_t Us,
     int64_t Ws, const int2* __restrict__ tiles, const int32_t* __restrict__ cbnd, int nchunks, int64_t r0, int64_t r1,
     int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I, int64_t ldI, int32_t* __restrict__ part, int64_t Wdp,
-    int64_t N, const unsigned long long* __restrict__ slab_bits, int slabs) {
+    int64_t N, const unsigned long long* __restrict__ slab_bits, int slabs, const int32_t* __restrict__ X) {
+    // X: the group tier's part of every pair (or null), added with the constant part
     // slab_bits / slabs: the in-kernel fold's dense words (set-major [N][Wdp])
     __shared__ uint32_t cnt[SB * SB / 2];                  // 32 KiB, 16-bit counters (cnt_index layout)
     __shared__ int4 rec[SNW][64];                          // 8 KiB: the batch's walk records
@@ -502,7 +705,8 @@ __global__ __launch_bounds__(SNT, 8) void sparse_tile_kernel(
         const int64_t i = A * SB + a, j = B * SB + b;
         if (i < r0 || i >= r1 || j < c0 || j >= c1 || (upper && j <= i)) continue;
         // the constant part once per pair: by chunk 0 (chunks flush with atomics)
-        const int v = (int)((cnt[t >> 1] >> ((t & 1) << 4)) & 0xFFFFu) + (ch == 0 ? (int)Us - nc[i] - nc[j] : 0);
+        const int v = (int)((cnt[t >> 1] >> ((t & 1) << 4)) & 0xFFFFu) +
+                      (ch == 0 ? (int)Us - nc[i] - nc[j] + (X ? X[i * N + j] : 0) : 0);
         if (v) atomicAdd(I + (i - r0) * ldI + (j - c0), v);
     }
 }
@@ -525,7 +729,8 @@ __global__ __launch_bounds__(256) void sparse_reduce_kernel(const int32_t* __res
                                                             const uint32_t* __restrict__ rp_w,
                                                             const int64_t* __restrict__ rp_off,
                                                             double* __restrict__ D, int64_t ldD,
-                                                            const int64_t* __restrict__ soff, int empty_nan) {
+                                                            const int64_t* __restrict__ soff, int empty_nan,
+                                                            const int32_t* __restrict__ X, int64_t N) {
 #pragma clang fp contract(off)
     constexpr int per_tile = SB * SB / kReduceCnt / kReduceGroups;       // workgroups per tile
     __shared__ uint32_t sum[4][kReduceCnt][kReduceGroups];               // 8 KiB
@@ -569,7 +774,7 @@ __global__ __launch_bounds__(256) void sparse_reduce_kernel(const int32_t* __res
         cnt_pair(t, a, b);
         const int64_t i = (int64_t)tiles[tile].x * SB + a, j = (int64_t)tiles[tile].y * SB + b;
         if (i < r0 || i >= r1 || j < c0 || j >= c1 || (upper && j <= i)) continue;
-        int v = (int)Us - nc[i] - nc[j] + (int)tot;
+        int v = (int)Us - nc[i] - nc[j] + (int)tot + (X ? X[i * N + j] : 0);
         if (D && i == j) v = (int)(soff[i + 1] - soff[i]);        // a set with itself (self_pairs_kernel)
         if (D) {                             // fused: the only writer of I over the region, then D
             I[(i - r0) * ldI + (j - c0)] = v;
@@ -646,6 +851,8 @@ void free_sparse(gdist_sets* s) {
     s->sp_fold_dense = false;
     s->sp_fold_slabs = 0;
     s->sp_products = s->sp_items = 0.0;
+    s->sp_x.release();
+    s->sp_groups = s->sp_group_words = 0;
 }
 
 // Modelled seconds of the sparse words over a block: products (each pair's
@@ -684,12 +891,119 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
         z[w] = wpos[w] ? zp[w] : zc[w];
     }
     tr.mark("sparse: word classes");
+    // ---- group tier: heavy words whose entries are the groups' patterns
+    const bool zm = ctx->has_option(OPT_SPARSE_ZMAX);
+    const int64_t nwb = ceil_div(N, 64);
+    std::vector<int32_t> wrow(W, -1);                     // factorised word -> pattern row
+    std::vector<unsigned long long> prow_pats;            // rows x mg patterns
+    std::vector<int32_t> grp;                             // set -> group
+    int mg = 0;
+    if (ctx->option(OPT_SPARSE_GROUPS, 1) != 0 && !zm && N >= 2 * kGroupMinSize && N <= kGroupMaxN) {
+        std::vector<int32_t> cw;
+        std::vector<uint8_t> cp;
+        for (int64_t w = 0; w < Wv; w++)
+            if (z[w] >= kGroupMinZ) { cw.push_back((int32_t)w); cp.push_back(wpos[w]); }
+        const int64_t nc = (int64_t)cw.size();
+        if (nc > 0) {
+            DevBuf dcw(nc * 4, st), dcp(nc + 8, st), ms(nc * 4, st), mh(nc * 8, st);
+            h2d(dcw.p, cw.data(), nc * 4, st);
+            h2d(dcp.p, cp.data(), nc, st);
+            std::vector<int32_t> hs(nc);
+            std::vector<unsigned long long> hh(nc);
+            // 1. discovery: each heavy word's modal pattern and its members
+            std::map<std::pair<unsigned long long, int32_t>, std::vector<int64_t>> by;
+            std::vector<std::pair<int64_t, std::vector<unsigned long long>>> cands;   // (words, member bitmap)
+            {
+                DevBuf mb((size_t)nc * nwb * 8, st);
+                group_modal_kernel<<<(unsigned)nc, 256, 0, st>>>(bits, N, W, U, dcw.as<int32_t>(), dcp.as<uint8_t>(),
+                                                                  nwb, mb.as<unsigned long long>(), ms.as<int32_t>(),
+                                                                  mh.as<unsigned long long>());
+                GD_HIP(hipGetLastError());
+                d2h(hs.data(), ms.p, nc * 4, st);
+                d2h(hh.data(), mh.p, nc * 8, st);
+                for (int64_t c = 0; c < nc; c++)
+                    if (hs[c] >= kGroupMinSize && hs[c] < N) by[{hh[c], hs[c]}].push_back(c);
+                std::vector<const std::vector<int64_t>*> order;
+                for (auto& kv : by)
+                    if ((int64_t)kv.second.size() >= kGroupMinWords) order.push_back(&kv.second);
+                std::stable_sort(order.begin(), order.end(), [](const std::vector<int64_t>* a,
+                                                                const std::vector<int64_t>* b) {
+                    return a->size() > b->size();
+                });
+                if (order.size() > 256) order.resize(256);   // the 256 most recurring lists
+                for (auto* o : order) {
+                    std::vector<unsigned long long> bm(nwb);
+                    d2h(bm.data(), mb.as<unsigned long long>() + (*o)[0] * nwb, nwb * 8, st);
+                    cands.push_back({(int64_t)o->size(), std::move(bm)});
+                }
+            }
+            // 2. the groups: the atoms of the recurring member lists (sets in
+            //    exactly the same lists form one group), so that a list which is
+            //    a union of groups (clades sharing a pattern) is expressed by
+            //    its groups, each with that pattern
+            grp.assign(N, -1);
+            {
+                std::vector<unsigned long long> sig(N, 0);
+                for (size_t k = 0; k < cands.size(); k++) {
+                    const unsigned long long key = 0x9E3779B97F4A7C15ull * (unsigned long long)(k + 1);
+                    for (int64_t q = 0; q < nwb; q++)
+                        for (unsigned long long b = cands[k].second[q]; b; b &= b - 1) {
+                            unsigned long long& x = sig[q * 64 + __builtin_ctzll(b)];
+                            x = (x ^ key) * 0xBF58476D1CE4E5B9ull + 1;      // order-dependent: lists in order
+                        }
+                }
+                std::map<unsigned long long, std::vector<int64_t>> atoms;
+                for (int64_t i = 0; i < N; i++)
+                    if (sig[i]) atoms[sig[i]].push_back(i);
+                std::vector<const std::vector<int64_t>*> order;
+                for (auto& kv : atoms)
+                    if ((int64_t)kv.second.size() >= kGroupMinSize) order.push_back(&kv.second);
+                std::stable_sort(order.begin(), order.end(), [](const std::vector<int64_t>* a,
+                                                                const std::vector<int64_t>* b) {
+                    return a->size() > b->size();
+                });
+                for (auto* o : order) {
+                    if (mg >= kGroupMax) break;
+                    for (int64_t i : *o) grp[i] = mg;
+                    mg++;
+                }
+            }
+            // 3. every group's pattern per candidate word; factorise the words
+            //    whose residual entries are fewer
+            if (mg > 0) {
+                DevBuf dgrp(N * 4, st), cpat((size_t)nc * mg * 8, st), zres(nc * 4, st);
+                h2d(dgrp.p, grp.data(), N * 4, st);
+                group_pattern_kernel<<<(unsigned)nc, 256, 0, st>>>(bits, N, W, U, dcw.as<int32_t>(), dcp.as<uint8_t>(),
+                                                                    dgrp.as<int32_t>(), mg,
+                                                                    cpat.as<unsigned long long>(), zres.as<int32_t>());
+                GD_HIP(hipGetLastError());
+                std::vector<unsigned long long> hp((size_t)nc * mg);
+                std::vector<int32_t> hz(nc);
+                d2h(hp.data(), cpat.p, hp.size() * 8, st);
+                d2h(hz.data(), zres.p, nc * 4, st);
+                for (int64_t c = 0; c < nc; c++) {
+                    const int64_t w = cw[c];
+                    if (hz[c] >= z[w]) continue;
+                    wrow[w] = (int32_t)(prow_pats.size() / mg);
+                    prow_pats.insert(prow_pats.end(), hp.begin() + c * mg, hp.begin() + (c + 1) * mg);
+                    z[w] = hz[c];                 // the residual entries decide the word's class
+                }
+            }
+            if (ctx->trace()) {
+                int64_t grouped_sets = 0;
+                for (int32_t g : grp) grouped_sets += g >= 0;
+                fprintf(stderr, "gdist: group tier: %lld candidate words, %zu recurring member lists, %d groups "
+                                "(%lld sets), %zu words factorised\n",
+                        (long long)nc, cands.size(), mg, (long long)grouped_sets, mg ? prow_pats.size() / mg : 0);
+            }
+        }
+        tr.mark("sparse: group tier");
+    }
     // A word is sparse when its products + visits cost less than its column
     // of word pairs in the dense tiles (option sparse_zmax overrides).
     const double n = (double)N, pairs = 0.5 * n * (n - 1.0);
     const double nb = (double)ceil_div(N, SB), tiles = nb * (nb + 1) / 2;
     const double dense_word_s = pairs / kDenseWordPairsPerS;
-    const bool zm = ctx->has_option(OPT_SPARSE_ZMAX);
     const int64_t zmax = ctx->option(OPT_SPARSE_ZMAX, 0);
     std::vector<int32_t> sw, dw;
     double products = 0.0;
@@ -726,8 +1040,36 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
     DevBuf dsw(Ws * 4, st), dsp(Ws + 8, st), cnt(nblk * Ws * 4 + 4, st);
     h2d(dsw.p, sw.data(), Ws * 4, st);
     h2d(dsp.p, spos.data(), Ws, st);
+    // the sparse words' pattern rows (group tier)
+    std::vector<int32_t> sprow(Ws, -1);
+    std::vector<unsigned long long> spats;
+    int64_t grouped = 0;
+    for (int64_t k = 0; k < Ws; k++)
+        if (wrow[sw[k]] >= 0) {
+            sprow[k] = (int32_t)grouped++;
+            spats.insert(spats.end(), prow_pats.begin() + (int64_t)wrow[sw[k]] * mg,
+                         prow_pats.begin() + ((int64_t)wrow[sw[k]] + 1) * mg);
+        }
+    DevBuf dgrp, dprow, dpats, dV;
+    GroupWords gw;
+    if (grouped) {
+        dgrp.alloc(N * 4, st);
+        dprow.alloc(Ws * 4, st);
+        dpats.alloc(spats.size() * 8, st);
+        dV.alloc((size_t)mg * N * 4, st);
+        h2d(dgrp.p, grp.data(), N * 4, st);
+        h2d(dprow.p, sprow.data(), Ws * 4, st);
+        h2d(dpats.p, spats.data(), spats.size() * 8, st);
+        GD_HIP(hipMemsetAsync(dV.p, 0, (size_t)mg * N * 4, st));
+        gw.grp = dgrp.as<int32_t>();
+        gw.prow = dprow.as<int32_t>();
+        gw.pats = dpats.as<unsigned long long>();
+        gw.m = mg;
+        gw.V = dV.as<int32_t>();
+        gw.N = N;
+    }
     dim3 gs((unsigned)ceil_div(Ws, 256), (unsigned)nblk);
-    sparse_count_kernel<<<gs, 256, 0, st>>>(bits, N, W, U, dsw.as<int32_t>(), dsp.as<uint8_t>(), Ws,
+    sparse_count_kernel<<<gs, 256, 0, st>>>(bits, N, W, U, dsw.as<int32_t>(), dsp.as<uint8_t>(), Ws, gw,
                                             cnt.as<int32_t>());
     GD_HIP(hipGetLastError());
     GD_HIP(hipMemsetAsync(cnt.as<int32_t>() + nblk * Ws, 0, 4, st));
@@ -743,7 +1085,7 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
     const int64_t nbk = ceil_div(Ws, int64_t(1) << kBucketShift);
     DevBuf dbb((size_t)N * nbk * 4, st);
     GD_HIP(hipMemsetAsync(dbb.p, 0, (size_t)N * nbk * 4, st));
-    sparse_fill_kernel<<<gs, 256, 0, st>>>(bits, N, W, U, dsw.as<int32_t>(), dsp.as<uint8_t>(), Ws,
+    sparse_fill_kernel<<<gs, 256, 0, st>>>(bits, N, W, U, dsw.as<int32_t>(), dsp.as<uint8_t>(), Ws, gw,
                                            s->sp_off.as<int64_t>(),
                                            sp_word.as<unsigned long long>(), sp_set.as<uint8_t>(),
                                            s->sp_nc.as<int32_t>(), dbb.as<int32_t>(), nbk);
@@ -762,6 +1104,22 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
                                                                 sp_set.as<uint8_t>(), total,
                                                                 s->sp_ent.as<ulonglong2>());
     GD_HIP(hipGetLastError());
+    if (grouped) {
+        // the group part of every pair: T from the pattern rows, V came with
+        // the entries (sparse_fill_kernel), then X
+        DevBuf T((size_t)mg * mg * 4, st);
+        GD_HIP(hipMemsetAsync(T.p, 0, (size_t)mg * mg * 4, st));
+        group_t_kernel<<<(unsigned)grouped, 256, 0, st>>>(dpats.as<unsigned long long>(), grouped, mg,
+                                                           T.as<int32_t>());
+        GD_HIP(hipGetLastError());
+        s->sp_x.alloc((size_t)N * N * 4, st);
+        group_x_kernel<<<grid_for(N * N), 256, 0, st>>>(N, dgrp.as<int32_t>(), mg, T.as<int32_t>(), dV.as<int32_t>(),
+                                                         s->sp_x.as<int32_t>());
+        GD_HIP(hipGetLastError());
+        GD_HIP(hipStreamSynchronize(st));
+        s->sp_groups = mg;
+        s->sp_group_words = grouped;
+    }
     if (Wdp) {
         DevBuf ddw(Wd * 4, st);
         h2d(ddw.p, dw.data(), Wd * 4, st);
@@ -1085,7 +1443,8 @@ bool sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     kern<<<(unsigned)grid, SNT, 0, st>>>(s->sp_off.as<int64_t>(), s->sp_ent.as<ulonglong2>(), s->sp_nc.as<int32_t>(),
                                          s->sp_U, s->Ws, sc.tiles.as<int2>(), sc.bounds.as<int32_t>(), nchunks, r0, r1,
                                          c0, c1, upper ? 1 : 0, d_I, ldI, sc.use_part ? sc.part.as<int32_t>() : nullptr,
-                                         s->Wd, s->nsets, s->dbits.as<unsigned long long>(), s->sp_fold_slabs);
+                                         s->Wd, s->nsets, s->dbits.as<unsigned long long>(), s->sp_fold_slabs,
+                                         s->sp_x.as<int32_t>());
     GD_HIP(hipGetLastError());
     if (timed) {
         GD_HIP(hipEventRecord(ctx->ev_sp1, st));
@@ -1097,7 +1456,7 @@ bool sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
             upper ? 1 : 0, d_I, ldI,
             sc.rare_in ? sc.rp_key.as<uint32_t>() : nullptr, sc.rare_in ? sc.rp_w.as<uint32_t>() : nullptr,
             sc.rare_in ? sc.rp_off.as<int64_t>() : nullptr, ep ? ep->D : nullptr, ep ? ep->ldD : 0,
-            ep ? ep->off : nullptr, ep ? ep->empty_nan : 0);
+            ep ? ep->off : nullptr, ep ? ep->empty_nan : 0, s->sp_x.as<int32_t>(), s->nsets);
         GD_HIP(hipGetLastError());
     }
     return sc.use_part && sc.rare_in;

@@ -395,6 +395,12 @@ class KmerSets(_Handle):
         L.check(L.lib.gdist_sets_sparse_info(self.h, C.byref(a), C.byref(b), C.byref(c)))
         return a.value, b.value, c.value
 
+    def group_info(self) -> tuple[int, int]:
+        """(groups, grouped sparse words) of the group tier (gdist_sets_group_info)."""
+        g, w = C.c_int64(), C.c_int64()
+        L.check(L.lib.gdist_sets_group_info(self.h, C.byref(g), C.byref(w)))
+        return g.value, w.value
+
     def sparse_sides(self) -> tuple[int, int]:
         """(complement-sparse words, positive-sparse words)."""
         a, b = C.c_int64(), C.c_int64()

@@ -204,6 +204,13 @@ int  gdist_sets_sparse_info(const gdist_sets* sets, int64_t* sparse_words, int64
  * lacking a commonly held kmer) or from their words (sets holding a rarely
  * held one: positive-sparse). */
 int  gdist_sets_sparse_sides(const gdist_sets* sets, int64_t* complement_words, int64_t* positive_words);
+/* The group tier of the sparse words: groups of sets (e.g.
+ * the clades of a structured collection) whose members all carry the same
+ * pattern in a word; those words keep per member only the residual entries
+ * and the group part of every pair is precomputed. Reports the groups used
+ * and the sparse words factorised by one (0s without the tier; option
+ * "sparse_groups" = 0 switches it off). */
+int  gdist_sets_group_info(const gdist_sets* sets, int64_t* groups, int64_t* grouped_words);
 /* Copy the bitsets (nsets x words_per_set uint64, row-major) to the host. */
 int  gdist_sets_bitset_download(const gdist_sets* sets, uint64_t* bits);
 /* Concatenate two collections (e.g. base genomes + comparison genomes). */
