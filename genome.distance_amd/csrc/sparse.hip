@@ -138,16 +138,19 @@ __device__ __forceinline__ unsigned long long entry_word(unsigned long long b, u
 constexpr int kGroupMax = 64;                    // groups (disjoint sets of sets) per collection
 struct GroupWords {
     const int32_t* grp = nullptr;               // [N] group of each set, -1: none
-    const int32_t* prow = nullptr;              // [Ws] pattern row of sparse word s, -1: not factorised
+    const int32_t* prow = nullptr;              // [Ws] pattern row of sparse word s (| kRowLack), -1: not factorised
     const unsigned long long* pats = nullptr;   // [rows][m] each group's pattern in the word
     int m = 0;                                  // groups
     int32_t* V = nullptr;                       // [m][N] group x set part (filled with the entries)
     int64_t N = 0;
 };
+constexpr int32_t kRowLack = 1 << 30;           // pattern row flag: the word's residuals are the lacked bits
 __device__ __forceinline__ unsigned long long residual(unsigned long long e, const GroupWords& gw, int r, int64_t i) {
     if (r < 0) return e;
     const int g = gw.grp[i];
-    return g >= 0 ? (e & ~gw.pats[(int64_t)r * gw.m + g]) : e;
+    if (g < 0) return e;                        // (0 in a lacked-mode word)
+    const unsigned long long P = gw.pats[(int64_t)(r & ~kRowLack) * gw.m + g];
+    return (r & kRowLack) ? (P & ~e) : (e & ~P);
 }
 
 // entries per (block b, sparse word s): sets of the block whose (residual) entry word is non-zero
@@ -194,11 +197,14 @@ __global__ __launch_bounds__(256) void sparse_fill_kernel(const unsigned long lo
             set[p] = (uint8_t)(i - b * SB);
             p++;
             atomicAdd(bucket_bits + i * nbk + (s >> kBucketShift), (int32_t)__popcll(c));
-            if (r >= 0)                    // V[G][i] += popc(P_G & a_i) (group tier)
+            if (r >= 0) {                  // V[G][i] += popc(P_G & a_i), -= popc(P_G & b_i) (group tier)
+                const unsigned long long* P = gw.pats + (int64_t)(r & ~kRowLack) * gw.m;
+                const int sg = (r & kRowLack) ? -1 : 1;
                 for (int g = 0; g < gw.m; g++) {
-                    const int v = __popcll(gw.pats[(int64_t)r * gw.m + g] & c);
-                    if (v) atomicAdd(gw.V + (int64_t)g * gw.N + i, v);
+                    const int v = __popcll(P[g] & c);
+                    if (v) atomicAdd(gw.V + (int64_t)g * gw.N + i, sg * v);
                 }
+            }
         }
     }
 }
@@ -216,9 +222,14 @@ __global__ __launch_bounds__(256) void sparse_fill_kernel(const unsigned long lo
 //   T[G][H] = Σ_w popc(P_G & P_H),  V[G][j] = Σ_w popc(P_G & a_j)  (0 for members of G)
 //   X[i][j] = T[gi][gj] + V[gi][j] + V[gj][i]
 // and the residuals are ordinary sparse entries; the reduce / flush adds
-// X[i][j] (int32, [N][N]). Any choice of groups is exact (the pattern is the
-// AND over the members); the choice only decides how much work leaves the
-// products. Groups are found from the data: per heavy word, the most
+// X[i][j] (int32, [N][N]). Lacked mode, for words whose members mostly
+// hold the group's bits (a clade's variant kmers on the positive side, where
+// one member's own substitution would drop a bit from the AND): P_G is the OR
+// of the members' entry words and the residual is b_i = P_G \ e_i, so
+//   popc(e_i & e_j) = popc(P_gi & P_gj) - popc(P_gi & b_j) - popc(b_i & P_gj) + popc(b_i & b_j)
+// (the V terms enter with a minus; allowed only when no ungrouped set has an
+// entry in the word). Any choice of groups is exact; the choice only decides
+// how much work leaves the products. Groups are found from the data: per heavy word, the most
 // frequent non-zero entry value v and its members {i : e_i ⊇ v}; member
 // lists recurring over many words (hash of the bitmap) are taken greedily,
 // most words first, keeping them disjoint.
@@ -314,41 +325,50 @@ __global__ __launch_bounds__(256) void group_modal_kernel(const unsigned long lo
     if (threadIdx.x == 0) { msize[c] = v0 ? rn[0] : 0; mhash[c] = rv[0]; }
 }
 
-// Every group's pattern in candidate word c (AND of its members' entry
-// words, LDS atomics) and the word's residual entry count
+// Every group's patterns in candidate word c (AND and OR of its members'
+// entry words, LDS atomics) and the word's residual entry count in either mode
 __global__ __launch_bounds__(256) void group_pattern_kernel(const unsigned long long* __restrict__ bits, int64_t N,
                                                             int64_t W, int64_t U, const int32_t* __restrict__ cw,
                                                             const uint8_t* __restrict__ cpos,
                                                             const int32_t* __restrict__ grp, int mg,
                                                             unsigned long long* __restrict__ cpat,
                                                             int32_t* __restrict__ zres) {
-    __shared__ unsigned long long pat[kGroupMax];
-    __shared__ int rz[256];
+    __shared__ unsigned long long pat[kGroupMax], por[kGroupMax];
+    __shared__ int rz[256], ro[256];
     const int64_t c = blockIdx.x;
     const int64_t w = cw[c];
     const bool pos = cpos[c] != 0;
     const unsigned long long m = valid_mask(w, U);
-    for (int g = threadIdx.x; g < mg; g += 256) pat[g] = ~0ull;
+    for (int g = threadIdx.x; g < mg; g += 256) { pat[g] = ~0ull; por[g] = 0ull; }
     __syncthreads();
     for (int64_t i = threadIdx.x; i < N; i += 256) {
         const int g = grp[i];
-        if (g >= 0) atomicAnd(&pat[g], entry_word(bits[i * W + w], m, pos));
+        const unsigned long long e = entry_word(bits[i * W + w], m, pos);
+        if (g >= 0) { atomicAnd(&pat[g], e); if (e) atomicOr(&por[g], e); }
     }
     __syncthreads();
-    int z = 0;
+    int z = 0, zo = 0;
     for (int64_t i = threadIdx.x; i < N; i += 256) {
         const int g = grp[i];
         const unsigned long long e = entry_word(bits[i * W + w], m, pos);
         z += (g >= 0 ? (e & ~pat[g]) : e) != 0;
+        zo += g >= 0 ? ((por[g] & ~e) != 0) : (e ? 1 << 20 : 0);     // an ungrouped entry rules lacked mode out
     }
     rz[threadIdx.x] = z;
-    for (int g = threadIdx.x; g < mg; g += 256) cpat[c * mg + g] = pat[g];
+    ro[threadIdx.x] = zo;
+    for (int g = threadIdx.x; g < mg; g += 256) {
+        cpat[(2 * c) * mg + g] = pat[g];
+        cpat[(2 * c + 1) * mg + g] = por[g];
+    }
     __syncthreads();
     for (int o = 128; o > 0; o >>= 1) {
-        if (threadIdx.x < o) rz[threadIdx.x] += rz[threadIdx.x + o];
+        if (threadIdx.x < o) {
+            rz[threadIdx.x] += rz[threadIdx.x + o];
+            ro[threadIdx.x] = min(ro[threadIdx.x] + ro[threadIdx.x + o], 1 << 20);
+        }
         __syncthreads();
     }
-    if (threadIdx.x == 0) zres[c] = rz[0];
+    if (threadIdx.x == 0) { zres[2 * c] = rz[0]; zres[2 * c + 1] = ro[0]; }
 }
 
 // T[G][H] += popc(P_G & P_H) per factorised word (pattern row r)
@@ -898,6 +918,7 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
     std::vector<unsigned long long> prow_pats;            // rows x mg patterns
     std::vector<int32_t> grp;                             // set -> group
     int mg = 0;
+    int64_t lacked_words = 0;
     if (ctx->option(OPT_SPARSE_GROUPS, 1) != 0 && !zm && N >= 2 * kGroupMinSize && N <= kGroupMaxN) {
         std::vector<int32_t> cw;
         std::vector<uint8_t> cp;
@@ -940,17 +961,25 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
             // 2. the groups: the atoms of the recurring member lists (sets in
             //    exactly the same lists form one group), so that a list which is
             //    a union of groups (clades sharing a pattern) is expressed by
-            //    its groups, each with that pattern
+            //    its groups, each with that pattern. Lists refine the partition
+            //    most recurring first, and a list that would split off a part
+            //    smaller than a group (a clade less a member) is passed over.
             grp.assign(N, -1);
             {
                 std::vector<unsigned long long> sig(N, 0);
+                std::vector<unsigned char> in(N);
                 for (size_t k = 0; k < cands.size(); k++) {
+                    for (int64_t i = 0; i < N; i++) in[i] = (cands[k].second[i >> 6] >> (i & 63)) & 1;
+                    std::map<unsigned long long, std::pair<int64_t, int64_t>> split;   // atom -> (in, out)
+                    for (int64_t i = 0; i < N; i++) (in[i] ? split[sig[i]].first : split[sig[i]].second)++;
+                    bool ok = true;
+                    for (auto& kv : split)
+                        if ((kv.second.first && kv.second.first < kGroupMinSize) ||
+                            (kv.second.second && kv.second.second < kGroupMinSize && kv.first != 0)) ok = false;
+                    if (!ok) continue;
                     const unsigned long long key = 0x9E3779B97F4A7C15ull * (unsigned long long)(k + 1);
-                    for (int64_t q = 0; q < nwb; q++)
-                        for (unsigned long long b = cands[k].second[q]; b; b &= b - 1) {
-                            unsigned long long& x = sig[q * 64 + __builtin_ctzll(b)];
-                            x = (x ^ key) * 0xBF58476D1CE4E5B9ull + 1;      // order-dependent: lists in order
-                        }
+                    for (int64_t i = 0; i < N; i++)
+                        if (in[i]) sig[i] = (sig[i] ^ key) * 0xBF58476D1CE4E5B9ull + 1;
                 }
                 std::map<unsigned long long, std::vector<int64_t>> atoms;
                 for (int64_t i = 0; i < N; i++)
@@ -971,30 +1000,33 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
             // 3. every group's pattern per candidate word; factorise the words
             //    whose residual entries are fewer
             if (mg > 0) {
-                DevBuf dgrp(N * 4, st), cpat((size_t)nc * mg * 8, st), zres(nc * 4, st);
+                DevBuf dgrp(N * 4, st), cpat((size_t)nc * 2 * mg * 8, st), zres(nc * 2 * 4, st);
                 h2d(dgrp.p, grp.data(), N * 4, st);
                 group_pattern_kernel<<<(unsigned)nc, 256, 0, st>>>(bits, N, W, U, dcw.as<int32_t>(), dcp.as<uint8_t>(),
                                                                     dgrp.as<int32_t>(), mg,
                                                                     cpat.as<unsigned long long>(), zres.as<int32_t>());
                 GD_HIP(hipGetLastError());
-                std::vector<unsigned long long> hp((size_t)nc * mg);
-                std::vector<int32_t> hz(nc);
+                std::vector<unsigned long long> hp((size_t)nc * 2 * mg);
+                std::vector<int32_t> hz(nc * 2);
                 d2h(hp.data(), cpat.p, hp.size() * 8, st);
-                d2h(hz.data(), zres.p, nc * 4, st);
+                d2h(hz.data(), zres.p, nc * 2 * 4, st);
                 for (int64_t c = 0; c < nc; c++) {
                     const int64_t w = cw[c];
-                    if (hz[c] >= z[w]) continue;
-                    wrow[w] = (int32_t)(prow_pats.size() / mg);
-                    prow_pats.insert(prow_pats.end(), hp.begin() + c * mg, hp.begin() + (c + 1) * mg);
-                    z[w] = hz[c];                 // the residual entries decide the word's class
+                    const int lack = hz[2 * c + 1] < hz[2 * c] ? 1 : 0;
+                    if (hz[2 * c + lack] >= z[w]) continue;
+                    wrow[w] = (int32_t)(prow_pats.size() / mg) | (lack ? kRowLack : 0);
+                    prow_pats.insert(prow_pats.end(), hp.begin() + (2 * c + lack) * mg, hp.begin() + (2 * c + lack + 1) * mg);
+                    z[w] = hz[2 * c + lack];      // the residual entries decide the word's class
+                    lacked_words += lack;
                 }
             }
             if (ctx->trace()) {
                 int64_t grouped_sets = 0;
                 for (int32_t g : grp) grouped_sets += g >= 0;
                 fprintf(stderr, "gdist: group tier: %lld candidate words, %zu recurring member lists, %d groups "
-                                "(%lld sets), %zu words factorised\n",
-                        (long long)nc, cands.size(), mg, (long long)grouped_sets, mg ? prow_pats.size() / mg : 0);
+                                "(%lld sets), %zu words factorised (%lld in lacked mode)\n",
+                        (long long)nc, cands.size(), mg, (long long)grouped_sets, mg ? prow_pats.size() / mg : 0,
+                        (long long)lacked_words);
             }
         }
         tr.mark("sparse: group tier");
@@ -1046,9 +1078,9 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
     int64_t grouped = 0;
     for (int64_t k = 0; k < Ws; k++)
         if (wrow[sw[k]] >= 0) {
-            sprow[k] = (int32_t)grouped++;
-            spats.insert(spats.end(), prow_pats.begin() + (int64_t)wrow[sw[k]] * mg,
-                         prow_pats.begin() + ((int64_t)wrow[sw[k]] + 1) * mg);
+            const int64_t row = wrow[sw[k]] & ~kRowLack;
+            sprow[k] = (int32_t)grouped++ | (wrow[sw[k]] & kRowLack);
+            spats.insert(spats.end(), prow_pats.begin() + row * mg, prow_pats.begin() + (row + 1) * mg);
         }
     DevBuf dgrp, dprow, dpats, dV;
     GroupWords gw;
