@@ -122,9 +122,12 @@ def main():
                     help="one GPU: time rows [A, B) of the upper triangle only (a slice; the line reports it)")
     ap.add_argument("--force-exchange", action="store_true",
                     help="one GPU: run the multi-rank exchange on a one-rank RCCL communicator")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_c2.json"),
-                    help="per-launch HBM traffic measured by rocprofv3 PMC passes (optional)")
+    ap.add_argument("--pmc-json", default=None,
+                    help="per-launch HBM traffic measured by rocprofv3 PMC passes "
+                         "(default profiles/pmc_<config>.json, if present)")
     args = ap.parse_args()
+    if args.pmc_json is None:
+        args.pmc_json = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -148,7 +148,16 @@ inline int sketch_stride(int width) { return width | 1; }
 //             common = ia + ib - steps (a common element advances both).
 //   phase 2 - closed form: the rest of the non-exhausted side are distinct
 //             union elements with no common ones.
-template <int R, int C, bool LDS, int KW>
+//
+// V2 (round 3): lanes of a 32-lane LDS group cover a 4 x 8 block of pairs
+// (4 row sketches, 8 column sketches) instead of one and a third rows of 24
+// columns, so a group's reads fall on 4 (rows) or 8 (columns) sketches at
+// similar positions, not 24 scattered ones; each LDS row carries two INT_MAX
+// sentinels past its last hash, so while fewer than max(ina, inb) steps are
+// taken (one side still has elements) the two-step rounds run without bounds
+// checks. A pair whose sketch ends in INT_MAX (a real hash the sentinel
+// would equal) takes the checked loop.
+template <int R, int C, bool LDS, int KW, bool V2 = false>
 __global__ __launch_bounds__(R * C) void sketch_tile_kernel(const int32_t* __restrict__ sig,
                                                             const int64_t* __restrict__ off, int width, int sw,
                                                             int64_t r0, int64_t r1, int64_t c0, int64_t c1,
@@ -160,9 +169,18 @@ __global__ __launch_bounds__(R * C) void sketch_tile_kernel(const int32_t* __res
     extern __shared__ int32_t sm[];   // [R+C][sketch_stride(width)] (+ slack)
     __shared__ int64_t s_base[NS];
     __shared__ int32_t s_n[NS];
+    static_assert(!V2 || (R % 4 == 0 && C % 8 == 0 && LDS && (KW == 2 || KW == 4)), "V2: 4 x 8 lane groups, LDS, K = 2, 4");
     const int tr = blockIdx.x / tiles_c, tcb = blockIdx.x % tiles_c;
     const int64_t row0 = r0 + (int64_t)tr * R, col0 = c0 + (int64_t)tcb * C;
-    const int ty = threadIdx.x / C, tx = threadIdx.x - ty * C;
+    int ty, tx;
+    if (V2) {
+        const int g = threadIdx.x >> 5, l = threadIdx.x & 31;
+        ty = (g / (C / 8)) * 4 + (l >> 3);
+        tx = (g % (C / 8)) * 8 + (l & 7);
+    } else {
+        ty = threadIdx.x / C;
+        tx = threadIdx.x - ty * C;
+    }
     if (upper && col0 + C - 1 <= row0) return;
     if (LDS) {
         if (threadIdx.x < NS) {
@@ -177,13 +195,14 @@ __global__ __launch_bounds__(R * C) void sketch_tile_kernel(const int32_t* __res
         for (int s = wave; s < NS; s += NW) {
             const int n = __builtin_amdgcn_readfirstlane(s_n[s]);
             const int32_t* src = sig + s_base[s];
+            if (V2 && lane < KW) sm[s * sw + n + lane] = 0x7FFFFFFF;     // sentinels past the hashes
             for (int t = 0; t < n; t += 64) {
                 if (t + lane < n)
                     __builtin_amdgcn_global_load_lds((gbl_void_t*)(src + t + lane),
                                                      (lds_void_t*)(sm + s * sw + t), 4, 0, 0);
             }
         }
-        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
     const int64_t i = row0 + ty, j = col0 + tx;
     if (i >= r1 || j >= c1 || (upper && j <= i)) return;
@@ -193,6 +212,28 @@ __global__ __launch_bounds__(R * C) void sketch_tile_kernel(const int32_t* __res
     const int32_t* B = LDS ? sm + (R + tx) * sw : sig + off[j];
     const int lim = jaccard ? ina + inb : width;
     int ia = 0, ib = 0, steps = 0;
+    if (V2) {
+        // unchecked KW-step rounds while steps < max(ina, inb) (and < lim):
+        // one side still has hashes, the other reads its sentinels
+        int ns = min(lim, max(ina, inb)) & ~(KW - 1);
+        if ((ina > 0 && A[ina - 1] == 0x7FFFFFFF) || (inb > 0 && B[inb - 1] == 0x7FFFFFFF)) ns = 0;
+        for (; steps < ns; steps += KW) {
+            int32_t a[KW], b[KW];
+#pragma unroll
+            for (int u = 0; u < KW; u++) { a[u] = A[ia + u]; b[u] = B[ib + u]; }
+#pragma unroll
+            for (int t = 0; t < KW; t++) {
+                const bool le = a[0] <= b[0], ge = b[0] <= a[0];
+                ia += le;
+                ib += ge;
+#pragma unroll
+                for (int u = 0; u + 1 < KW - t; u++) {
+                    a[u] = le ? a[u + 1] : a[u];
+                    b[u] = ge ? b[u + 1] : b[u];
+                }
+            }
+        }
+    }
     if (KW > 1) {
         // steady state: both sides have >= KW elements left and >= KW steps
         // remain, so KW steps run unchecked on a KW-element window per side
@@ -244,16 +285,18 @@ constexpr size_t sketch_meta_bytes() { return (size_t)(R + C) * (sizeof(int64_t)
 template <int R, int C>
 bool launch_sketch_tiles(hipStream_t st, const gdist_sets* sk, int width, int64_t r0, int64_t r1, int64_t c0,
                          int64_t c1, bool upper, int jac, int en, int32_t* d_common, double* d_D, int64_t ld,
-                         bool force_global, int64_t kw_opt) {
-    const int sw = sketch_stride(width);
+                         bool force_global, int64_t kw_opt, bool v2_opt) {
+    // option sketch_k selects the merge window (1, 2, 4, 6; A/B measurements)
+    const int kw = (int)kw_opt;
+    const bool v2 = (kw == 2 || kw == 4) && v2_opt;
+    const int sw = v2 ? ((width + kw) | 1) : sketch_stride(width);
     const size_t lds = (size_t)(R + C) * sw * 4 + LDS_SK_SLACK;
     const bool use_lds = !force_global && lds + sketch_meta_bytes<R, C>() <= (size_t)LDS_SK_MAX;
     if (!use_lds && !force_global) return false;
     const int tr = (int)ceil_div(r1 - r0, R), tc = (int)ceil_div(c1 - c0, C);
     const int64_t grid = (int64_t)tr * tc;
     GD_REQUIRE(grid < (int64_t(1) << 31), "sketch grid too large");
-    // option sketch_k selects the merge window (1, 2, 4, 6; A/B measurements)
-    const int kw = (int)kw_opt;
+
     const int32_t* sig = sk->codes.as<int32_t>();
     const int64_t* off = sk->off.as<int64_t>();
     if (!use_lds) {
@@ -268,9 +311,15 @@ bool launch_sketch_tiles(hipStream_t st, const gdist_sets* sk, int width, int64_
         };
         switch (kw) {
             case 1: go(&sketch_tile_kernel<R, C, true, 1>); break;
-            case 4: go(&sketch_tile_kernel<R, C, true, 4>); break;
+            case 4:
+                if (v2) go(&sketch_tile_kernel<R, C, true, 4, true>);
+                else go(&sketch_tile_kernel<R, C, true, 4>);
+                break;
             case 6: go(&sketch_tile_kernel<R, C, true, 6>); break;
-            default: go(&sketch_tile_kernel<R, C, true, 2>); break;
+            default:
+                if (v2) go(&sketch_tile_kernel<R, C, true, 2, true>);
+                else go(&sketch_tile_kernel<R, C, true, 2>);
+                break;
         }
     }
     GD_HIP(hipGetLastError());
@@ -383,11 +432,12 @@ void sketch_matrix(gdist_ctx* ctx, const gdist_sets* sk, int64_t r0, int64_t r1,
     // option sketch_tile = 16 forces the 16x16 tile (A/B measurements)
     const bool only16 = ctx->option(OPT_SKETCH_TILE, 0) == 16;
     const int64_t kw = ctx->option(OPT_SKETCH_K, 2);
+    const bool v2 = ctx->option(OPT_SKETCH_V2, 1) != 0;
     GD_HIP(hipEventRecord(ctx->ev_k0, st));
     if (only16 || !launch_sketch_tiles<16, 24>(st, sk, width, r0, r1, c0, c1, upper, jac, en, d_common, d_D, ld,
-                                               false, kw))
-        if (!launch_sketch_tiles<16, 16>(st, sk, width, r0, r1, c0, c1, upper, jac, en, d_common, d_D, ld, false, kw))
-            launch_sketch_tiles<16, 16>(st, sk, width, r0, r1, c0, c1, upper, jac, en, d_common, d_D, ld, true, kw);
+                                               false, kw, v2))
+        if (!launch_sketch_tiles<16, 16>(st, sk, width, r0, r1, c0, c1, upper, jac, en, d_common, d_D, ld, false, kw, v2))
+            launch_sketch_tiles<16, 16>(st, sk, width, r0, r1, c0, c1, upper, jac, en, d_common, d_D, ld, true, kw, v2);
     GD_HIP(hipEventRecord(ctx->ev_k1, st));
     ctx->last.launches = 1;
 }

@@ -427,6 +427,41 @@ def test_sketch_matrix_vs_oracle(ctx):
     assert C[0, 1] == 2 and D[0, 1] == pyref.sketch_distance([1, 5, 9], [5, 9, 11], 4)[0]
 
 
+@pytest.mark.parametrize("v2,k", [(1, 2), (1, 4), (0, 2), (0, 1)])
+def test_sketch_merge_edges_vs_oracle(ctx, opts, v2, k):
+    """Uploaded sketches with the merge's edge cases, every pair against the
+    oracle, both merge loops (option sketch_v2): empty and short sketches,
+    identical ones, disjoint ones, INT_MIN / INT_MAX hashes (INT_MAX is the
+    V2 loop's LDS sentinel: such pairs take the checked loop)."""
+    import gdist
+    opts(sketch_v2=v2, sketch_k=k)
+    rng = np.random.default_rng(1234)
+    for w in (64, 1000):
+        sk = []
+        for t in range(96):
+            n = [0, 1, 2, w // 2, w - 1, w, w, w][t % 8]
+            lo, hi = (-2**31, 2**31 - 1) if t % 3 else (-2**31, -2**31 + 40 * w)
+            v = np.unique(rng.integers(lo, hi, size=3 * n + 8, endpoint=True, dtype=np.int64))
+            v = np.sort(rng.choice(v, size=min(n, len(v)), replace=False)).astype(np.int32)
+            if t % 11 == 0 and n:
+                v[-1] = 2**31 - 1
+                v = np.unique(v)
+            if t % 13 == 0 and n:
+                v[0] = -2**31
+                v = np.unique(v)
+            sk.append(v)
+        sk[10] = sk[9].copy()                                     # identical pair
+        sk[20] = np.arange(w, dtype=np.int32) * 2                 # disjoint interleaved pair
+        sk[21] = np.arange(w, dtype=np.int32) * 2 + 1
+        S = gdist.SketchSets.from_signatures(sk, w, ctx)
+        for fl in (0, gdist.SKETCH_JACCARD):
+            C, D = S.matrix(flags=fl)
+            for i in range(len(sk)):
+                for j in range(len(sk)):
+                    d, c = oracle.sketch_distance(sk[i], sk[j], w, fl)
+                    assert C[i, j] == c and bits_equal(np.array([D[i, j]]), np.array([d])), (w, fl, i, j)
+
+
 # ---------------------------------------------------------------- processors
 def test_fasta_distance_processor_output(ctx):
     import gdist
