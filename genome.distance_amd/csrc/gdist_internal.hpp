@@ -338,9 +338,11 @@ struct gdist_sets {
     bool sp_fold_dense = false;           // the dense words are counted by the sparse tile kernel (no tile launch),
     int sp_fold_slabs = 0;                // 8 words per chunk in the first sp_fold_slabs chunks
     // group tier (sparse.hip): words whose heavy entries are one group's
-    // pattern keep per member only the residual; the group part of every
-    // pair is X[i][j] (int32 [nsets][nsets], symmetric), added by the reduce
-    gdist::DevBuf sp_x;
+    // pattern keep per member only the residual; the group part of pair
+    // (i, j) is T[gi][gj] + V[gi][j] + V[gj][i], evaluated by the flush /
+    // reduce from the set -> group map, V (int32 [groups][nsets]) and T
+    // (int32 [groups][groups])
+    gdist::DevBuf sp_grp, sp_V, sp_T;
     int64_t sp_groups = 0, sp_group_words = 0;
     std::vector<int32_t> sp_bucket_bits;  // [nsets][sp_nbk]: complement bits per set and 1024 sparse words
     int64_t sp_nbk = 0;

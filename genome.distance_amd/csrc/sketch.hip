@@ -169,14 +169,15 @@ __global__ __launch_bounds__(R * C) void sketch_tile_kernel(const int32_t* __res
     extern __shared__ int32_t sm[];   // [R+C][sketch_stride(width)] (+ slack)
     __shared__ int64_t s_base[NS];
     __shared__ int32_t s_n[NS];
-    static_assert(!V2 || (R % 4 == 0 && C % 8 == 0 && LDS && (KW == 2 || KW == 4)), "V2: 4 x 8 lane groups, LDS, K = 2, 4");
+    constexpr int GR = 4, GC = 8;
+    static_assert(!V2 || (R % GR == 0 && C % GC == 0 && LDS && KW == 2), "V2: GR x GC lane groups, LDS, K = 2");
     const int tr = blockIdx.x / tiles_c, tcb = blockIdx.x % tiles_c;
     const int64_t row0 = r0 + (int64_t)tr * R, col0 = c0 + (int64_t)tcb * C;
     int ty, tx;
     if (V2) {
         const int g = threadIdx.x >> 5, l = threadIdx.x & 31;
-        ty = (g / (C / 8)) * 4 + (l >> 3);
-        tx = (g % (C / 8)) * 8 + (l & 7);
+        ty = (g / (C / GC)) * GR + l / GC;
+        tx = (g % (C / GC)) * GC + l % GC;
     } else {
         ty = threadIdx.x / C;
         tx = threadIdx.x - ty * C;
@@ -195,7 +196,7 @@ __global__ __launch_bounds__(R * C) void sketch_tile_kernel(const int32_t* __res
         for (int s = wave; s < NS; s += NW) {
             const int n = __builtin_amdgcn_readfirstlane(s_n[s]);
             const int32_t* src = sig + s_base[s];
-            if (V2 && lane < KW) sm[s * sw + n + lane] = 0x7FFFFFFF;     // sentinels past the hashes
+            if (V2 && lane < 2) sm[s * sw + n + lane] = 0x7FFFFFFF;      // sentinels past the hashes
             for (int t = 0; t < n; t += 64) {
                 if (t + lane < n)
                     __builtin_amdgcn_global_load_lds((gbl_void_t*)(src + t + lane),
@@ -213,26 +214,24 @@ __global__ __launch_bounds__(R * C) void sketch_tile_kernel(const int32_t* __res
     const int lim = jaccard ? ina + inb : width;
     int ia = 0, ib = 0, steps = 0;
     if (V2) {
-        // unchecked KW-step rounds while steps < max(ina, inb) (and < lim):
-        // one side still has hashes, the other reads its sentinels
-        int ns = min(lim, max(ina, inb)) & ~(KW - 1);
-        if ((ina > 0 && A[ina - 1] == 0x7FFFFFFF) || (inb > 0 && B[inb - 1] == 0x7FFFFFFF)) ns = 0;
-        for (; steps < ns; steps += KW) {
-            int32_t a[KW], b[KW];
-#pragma unroll
-            for (int u = 0; u < KW; u++) { a[u] = A[ia + u]; b[u] = B[ib + u]; }
-#pragma unroll
-            for (int t = 0; t < KW; t++) {
-                const bool le = a[0] <= b[0], ge = b[0] <= a[0];
-                ia += le;
-                ib += ge;
-#pragma unroll
-                for (int u = 0; u + 1 < KW - t; u++) {
-                    a[u] = le ? a[u + 1] : a[u];
-                    b[u] = ge ? b[u + 1] : b[u];
-                }
-            }
-        }
+        const bool imax = (ina > 0 && A[ina - 1] == 0x7FFFFFFF) || (inb > 0 && B[inb - 1] == 0x7FFFFFFF);
+        // one unchecked two-step round of a merge at (pa, pb): the rows'
+        // sentinels stand in for an exhausted side
+        auto round2 = [&](int& pa, int& pb) {
+            const int32_t a0 = A[pa], a1 = A[pa + 1], b0 = B[pb], b1 = B[pb + 1];
+            const bool le = a0 <= b0, ge = b0 <= a0;
+            const int32_t x = le ? a1 : a0, y = ge ? b1 : b0;
+            pa += le;
+            pb += ge;
+            pa += x <= y;
+            pb += y <= x;
+        };
+        // unchecked rounds while steps < max(ina, inb) (and < lim): one side
+        // still has hashes, the other reads its sentinels
+        const int ns = imax ? 0 : min(lim, max(ina, inb));
+        const int nr = ns > steps ? (ns - steps) >> 1 : 0;
+        for (int r = 0; r < nr; r++) round2(ia, ib);
+        steps += 2 * nr;
     }
     if (KW > 1) {
         // steady state: both sides have >= KW elements left and >= KW steps
@@ -288,8 +287,8 @@ bool launch_sketch_tiles(hipStream_t st, const gdist_sets* sk, int width, int64_
                          bool force_global, int64_t kw_opt, bool v2_opt) {
     // option sketch_k selects the merge window (1, 2, 4, 6; A/B measurements)
     const int kw = (int)kw_opt;
-    const bool v2 = (kw == 2 || kw == 4) && v2_opt;
-    const int sw = v2 ? ((width + kw) | 1) : sketch_stride(width);
+    const bool v2 = kw == 2 && v2_opt;
+    const int sw = v2 ? ((width + 2) | 1) : sketch_stride(width);
     const size_t lds = (size_t)(R + C) * sw * 4 + LDS_SK_SLACK;
     const bool use_lds = !force_global && lds + sketch_meta_bytes<R, C>() <= (size_t)LDS_SK_MAX;
     if (!use_lds && !force_global) return false;
@@ -312,8 +311,7 @@ bool launch_sketch_tiles(hipStream_t st, const gdist_sets* sk, int width, int64_
         switch (kw) {
             case 1: go(&sketch_tile_kernel<R, C, true, 1>); break;
             case 4:
-                if (v2) go(&sketch_tile_kernel<R, C, true, 4, true>);
-                else go(&sketch_tile_kernel<R, C, true, 4>);
+                go(&sketch_tile_kernel<R, C, true, 4>);
                 break;
             case 6: go(&sketch_tile_kernel<R, C, true, 6>); break;
             default:

@@ -237,7 +237,7 @@ constexpr int kGroupSample = 4096;               // sets sampled for a word's mo
 constexpr int kGroupMinSize = 16;                // smallest group worth a pattern
 constexpr int kGroupMinWords = 8;                // ... and the fewest words it must recur in
 constexpr int kGroupMinZ = 32;                   // candidate words: at least this many entries
-constexpr int64_t kGroupMaxN = 16384;            // X is N x N int32
+constexpr int64_t kGroupMaxN = 16384;            // discovery keeps an N-bit member bitmap per heavy word
 
 __device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
     z += 0x9E3779B97F4A7C15ull;
@@ -383,20 +383,25 @@ __global__ void group_t_kernel(const unsigned long long* __restrict__ pats, int6
     }
 }
 
-// X[i][j] = T[gi][gj] + V[gi][j] + V[gj][i]
-__global__ void group_x_kernel(int64_t N, const int32_t* __restrict__ grp, int mg, const int32_t* __restrict__ T,
-                               const int32_t* __restrict__ V, int32_t* __restrict__ X) {
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < N * N; e += stride) {
-        const int64_t i = e / N, j = e - i * N;
+// The group part of pair (i, j): T[gi][gj] + V[gi][j] + V[gj][i] (0 without
+// groups), evaluated per pair by the tile kernel's flush and the chunk
+// reduce from the small tables
+struct GroupPart {
+    const int32_t* grp = nullptr;               // [N] group of each set, -1: none (null: no group tier)
+    const int32_t* V = nullptr;                 // [m][N]
+    const int32_t* T = nullptr;                 // [m][m]
+    int m = 0;
+    int64_t N = 0;
+    __device__ __forceinline__ int at(int64_t i, int64_t j) const {
+        if (!grp) return 0;
         const int gi = grp[i], gj = grp[j];
         int x = 0;
         if (gi >= 0) x += V[(int64_t)gi * N + j];
         if (gj >= 0) x += V[(int64_t)gj * N + i];
-        if (gi >= 0 && gj >= 0) x += T[gi * mg + gj];
-        X[e] = x;
+        if (gi >= 0 && gj >= 0) x += T[gi * m + gj];
+        return x;
     }
-}
+};
 
 // LDS counter of local pair (row a, column b), as a 16-bit slot t (dword
 // t >> 1, half t & 1): row a owns dwords [64 a, 64 a + 64); column b sits in
@@ -625,8 +630,8 @@ __global__ __launch_bounds__(SNT, 8) void sparse_tile_kernel(
     const int64_t* __restrict__ off, const ulonglong2* __restrict__ ent, const int32_t* __restrict__ nc, int64_t Us,
     int64_t Ws, const int2* __restrict__ tiles, const int32_t* __restrict__ cbnd, int nchunks, int64_t r0, int64_t r1,
     int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I, int64_t ldI, int32_t* __restrict__ part, int64_t Wdp,
-    int64_t N, const unsigned long long* __restrict__ slab_bits, int slabs, const int32_t* __restrict__ X) {
-    // X: the group tier's part of every pair (or null), added with the constant part
+    int64_t N, const unsigned long long* __restrict__ slab_bits, int slabs, GroupPart gp) {
+    // gp: the group tier's part of every pair, added with the constant part
     // slab_bits / slabs: the in-kernel fold's dense words (set-major [N][Wdp])
     __shared__ uint32_t cnt[SB * SB / 2];                  // 32 KiB, 16-bit counters (cnt_index layout)
     __shared__ int4 rec[SNW][64];                          // 8 KiB: the batch's walk records
@@ -726,7 +731,7 @@ __global__ __launch_bounds__(SNT, 8) void sparse_tile_kernel(
         if (i < r0 || i >= r1 || j < c0 || j >= c1 || (upper && j <= i)) continue;
         // the constant part once per pair: by chunk 0 (chunks flush with atomics)
         const int v = (int)((cnt[t >> 1] >> ((t & 1) << 4)) & 0xFFFFu) +
-                      (ch == 0 ? (int)Us - nc[i] - nc[j] + (X ? X[i * N + j] : 0) : 0);
+                      (ch == 0 ? (int)Us - nc[i] - nc[j] + gp.at(i, j) : 0);
         if (v) atomicAdd(I + (i - r0) * ldI + (j - c0), v);
     }
 }
@@ -750,7 +755,7 @@ __global__ __launch_bounds__(256) void sparse_reduce_kernel(const int32_t* __res
                                                             const int64_t* __restrict__ rp_off,
                                                             double* __restrict__ D, int64_t ldD,
                                                             const int64_t* __restrict__ soff, int empty_nan,
-                                                            const int32_t* __restrict__ X, int64_t N) {
+                                                            GroupPart gp) {
 #pragma clang fp contract(off)
     constexpr int per_tile = SB * SB / kReduceCnt / kReduceGroups;       // workgroups per tile
     __shared__ uint32_t sum[4][kReduceCnt][kReduceGroups];               // 8 KiB
@@ -794,7 +799,7 @@ __global__ __launch_bounds__(256) void sparse_reduce_kernel(const int32_t* __res
         cnt_pair(t, a, b);
         const int64_t i = (int64_t)tiles[tile].x * SB + a, j = (int64_t)tiles[tile].y * SB + b;
         if (i < r0 || i >= r1 || j < c0 || j >= c1 || (upper && j <= i)) continue;
-        int v = (int)Us - nc[i] - nc[j] + (int)tot + (X ? X[i * N + j] : 0);
+        int v = (int)Us - nc[i] - nc[j] + (int)tot + gp.at(i, j);
         if (D && i == j) v = (int)(soff[i + 1] - soff[i]);        // a set with itself (self_pairs_kernel)
         if (D) {                             // fused: the only writer of I over the region, then D
             I[(i - r0) * ldI + (j - c0)] = v;
@@ -871,7 +876,9 @@ void free_sparse(gdist_sets* s) {
     s->sp_fold_dense = false;
     s->sp_fold_slabs = 0;
     s->sp_products = s->sp_items = 0.0;
-    s->sp_x.release();
+    s->sp_grp.release();
+    s->sp_V.release();
+    s->sp_T.release();
     s->sp_groups = s->sp_group_words = 0;
 }
 
@@ -1138,17 +1145,16 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
     GD_HIP(hipGetLastError());
     if (grouped) {
         // the group part of every pair: T from the pattern rows, V came with
-        // the entries (sparse_fill_kernel), then X
+        // the entries (sparse_fill_kernel); the set -> group map stays
         DevBuf T((size_t)mg * mg * 4, st);
         GD_HIP(hipMemsetAsync(T.p, 0, (size_t)mg * mg * 4, st));
         group_t_kernel<<<(unsigned)grouped, 256, 0, st>>>(dpats.as<unsigned long long>(), grouped, mg,
                                                            T.as<int32_t>());
         GD_HIP(hipGetLastError());
-        s->sp_x.alloc((size_t)N * N * 4, st);
-        group_x_kernel<<<grid_for(N * N), 256, 0, st>>>(N, dgrp.as<int32_t>(), mg, T.as<int32_t>(), dV.as<int32_t>(),
-                                                         s->sp_x.as<int32_t>());
-        GD_HIP(hipGetLastError());
         GD_HIP(hipStreamSynchronize(st));
+        s->sp_grp = std::move(dgrp);
+        s->sp_V = std::move(dV);
+        s->sp_T = std::move(T);
         s->sp_groups = mg;
         s->sp_group_words = grouped;
     }
@@ -1453,6 +1459,18 @@ void sparse_plan(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, in
     }
 }
 
+GroupPart group_part(const gdist_sets* s) {
+    GroupPart g;
+    if (s->sp_groups > 0) {
+        g.grp = s->sp_grp.as<int32_t>();
+        g.V = s->sp_V.as<int32_t>();
+        g.T = s->sp_T.as<int32_t>();
+        g.m = (int)s->sp_groups;
+        g.N = s->nsets;
+    }
+    return g;
+}
+
 bool sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1, bool upper,
                    int32_t* d_I, int64_t ldI, hipStream_t st, SparseScratch& sc, const SparseEpilogue* ep) {
     if (!s->sparse || r1 <= r0 || c1 <= c0) return false;
@@ -1476,7 +1494,7 @@ bool sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
                                          s->sp_U, s->Ws, sc.tiles.as<int2>(), sc.bounds.as<int32_t>(), nchunks, r0, r1,
                                          c0, c1, upper ? 1 : 0, d_I, ldI, sc.use_part ? sc.part.as<int32_t>() : nullptr,
                                          s->Wd, s->nsets, s->dbits.as<unsigned long long>(), s->sp_fold_slabs,
-                                         s->sp_x.as<int32_t>());
+                                         group_part(s));
     GD_HIP(hipGetLastError());
     if (timed) {
         GD_HIP(hipEventRecord(ctx->ev_sp1, st));
@@ -1488,7 +1506,7 @@ bool sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
             upper ? 1 : 0, d_I, ldI,
             sc.rare_in ? sc.rp_key.as<uint32_t>() : nullptr, sc.rare_in ? sc.rp_w.as<uint32_t>() : nullptr,
             sc.rare_in ? sc.rp_off.as<int64_t>() : nullptr, ep ? ep->D : nullptr, ep ? ep->ldD : 0,
-            ep ? ep->off : nullptr, ep ? ep->empty_nan : 0, s->sp_x.as<int32_t>(), s->nsets);
+            ep ? ep->off : nullptr, ep ? ep->empty_nan : 0, group_part(s));
         GD_HIP(hipGetLastError());
     }
     return sc.use_part && sc.rare_in;

@@ -427,10 +427,11 @@ def test_sketch_matrix_vs_oracle(ctx):
     assert C[0, 1] == 2 and D[0, 1] == pyref.sketch_distance([1, 5, 9], [5, 9, 11], 4)[0]
 
 
-@pytest.mark.parametrize("v2,k", [(1, 2), (1, 4), (0, 2), (0, 1)])
+@pytest.mark.parametrize("v2,k", [(1, 2), (0, 2), (0, 4), (0, 1)])
 def test_sketch_merge_edges_vs_oracle(ctx, opts, v2, k):
     """Uploaded sketches with the merge's edge cases, every pair against the
-    oracle, both merge loops (option sketch_v2): empty and short sketches,
+    oracle, every merge loop (options sketch_v2, sketch_k):
+    empty and short sketches,
     identical ones, disjoint ones, INT_MIN / INT_MAX hashes (INT_MAX is the
     V2 loop's LDS sentinel: such pairs take the checked loop)."""
     import gdist
