@@ -218,6 +218,7 @@ constexpr int RCH = 16384;   // max columns per LDS chunk (64 KiB of counters)
 __global__ __launch_bounds__(256) void rare_rows_kernel(const int64_t* __restrict__ soff,
                                                         const uint64_t* __restrict__ sent,
                                                         const uint32_t* __restrict__ sw,
+                                                        const uint16_t* __restrict__ sskip,
                                                         const uint32_t* __restrict__ psets, int64_t r0, int64_t r1,
                                                         int64_t c0, int64_t c1, int nch, int nsplit, int upper,
                                                         int32_t* __restrict__ I, int64_t ldI) {
@@ -242,7 +243,9 @@ __global__ __launch_bounds__(256) void rare_rows_kernel(const int64_t* __restric
         const int64_t x = xbase + threadIdx.x;
         const uint64_t ent = x < xe ? sent[x] : 0ull;  // coalesced: no random bounds lookup
         const int32_t w = x < xe ? (int32_t)sw[x] : 0;
-        const int64_t b = (int64_t)(ent >> 24), e = b + (int64_t)(ent & 0xFFFFFFu);
+        const int64_t b0 = (int64_t)(ent >> 24), e = b0 + (int64_t)(ent & 0xFFFFFFu);
+        // upper triangle: only the members after the row's own set (ascending lists)
+        const int64_t b = upper && x < xe ? b0 + sskip[x] : b0;
         const bool lng = e - b >= kLongList;
         for (unsigned long long m = __ballot(lng); m; m &= m - 1) {   // long lists: the wave walks them
             const int l = __ffsll((long long)m) - 1;
@@ -254,10 +257,18 @@ __global__ __launch_bounds__(256) void rare_rows_kernel(const int64_t* __restric
             }
         }
         if (lng) continue;
-#pragma unroll 4
-        for (int64_t y = b; y < e; y++) {
-            const int64_t t = psets[y];
-            if (t >= lo && t < ce && t != i) atomicAdd(&cnt[t - cb], w);
+        // four members per 16-byte load (dword-aligned: global_load_dwordx4;
+        // post_sets is padded past its last list)
+#pragma unroll 2
+        for (int64_t y = b; y < e; y += 4) {
+            uint4 v;
+            __builtin_memcpy(&v, psets + y, 16);
+            const uint32_t mem[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int64_t t = mem[u];
+                if (y + u < e && t >= lo && t < ce && t != i) atomicAdd(&cnt[t - cb], w);
+            }
         }
     }
     __syncthreads();
@@ -319,6 +330,25 @@ __global__ void rare_entries_kernel(const uint64_t* __restrict__ keys, int64_t n
         const uint32_t r = (uint32_t)keys[i];
         const int64_t b = poff[r];
         ent[i] = ((uint64_t)b << 24) | (uint64_t)(poff[r + 1] - b);
+    }
+}
+
+// per (set, list) record: one past the set's position in its list (the
+// members an upper-triangle row walk starts at; lists are ascending), 0
+// past 65534 members (the walk then starts at the list's first member)
+__global__ void rare_skip_kernel(const uint64_t* __restrict__ keys, int64_t n, const int64_t* __restrict__ poff,
+                                 const uint32_t* __restrict__ psets, uint16_t* __restrict__ skip) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint32_t set = (uint32_t)(keys[i] >> 32), r = (uint32_t)keys[i];
+        int64_t lo = poff[r], hi = poff[r + 1];
+        const int64_t b = lo;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (psets[mid] < set) lo = mid + 1; else hi = mid;
+        }
+        const int64_t k = lo - b + 1;
+        skip[i] = k < 65535 ? (uint16_t)k : (uint16_t)0;
     }
 }
 
@@ -1466,7 +1496,7 @@ void build_postings(gdist_ctx* ctx, gdist_sets* s, unsigned long long* recs, int
     s->rare_kmers = Ur;
     s->rare_records = n;
     s->post_off.alloc((Ur + 1) * 8, st);
-    s->post_sets.alloc(n * 4 + 4, st);
+    s->post_sets.alloc(n * 4 + 16, st);          // padded: the row walk reads 16 bytes at a time
     s->rare_incs = s->rare_max_list = s->rare_incs_long = 0;
     if (Ur == 0 || n == 0) {
         GD_HIP(hipMemsetAsync(s->post_off.p, 0, (Ur + 1) * 8, st));
@@ -1475,6 +1505,7 @@ void build_postings(gdist_ctx* ctx, gdist_sets* s, unsigned long long* recs, int
         GD_HIP(hipMemsetAsync(s->srare_off.p, 0, (s->nsets + 1) * 8, st));
         s->srare_ent.alloc(8, st);
         s->srare_w.alloc(4, st);
+        s->srare_skip.alloc(8, st);
         s->n_rare = 0;
         s->rare_records = 0;
         GD_HIP(hipStreamSynchronize(st));
@@ -1522,7 +1553,7 @@ void build_postings(gdist_ctx* ctx, gdist_sets* s, unsigned long long* recs, int
         d2h(&hf[1], rk.as<int32_t>() + n - 1, 4, st);
         nl = h[0] + hf[0];
         nrec = h[1] + hf[1];
-        DevBuf noff((nl + 1) * 8, st), nsets(nrec * 4 + 4, st);
+        DevBuf noff((nl + 1) * 8, st), nsets(nrec * 4 + 16, st);
         s->post_w.alloc(nl * 4 + 4, st);
         list_offsets_kernel<<<grid_for(Ur), 256, 0, st>>>(s->post_off.as<int64_t>(), Ur, keep.as<int32_t>(),
                                                           newid.as<int64_t>(), rpos.as<int64_t>(),
@@ -1559,6 +1590,9 @@ void build_postings(gdist_ctx* ctx, gdist_sets* s, unsigned long long* recs, int
                                                         s->srare_ent.as<uint64_t>());
     entry_weights_kernel<<<grid_for(nrec), 256, 0, st>>>(kalt, nrec, s->post_w.as<uint32_t>(),
                                                          s->srare_w.as<uint32_t>());
+    s->srare_skip.alloc(nrec * 2 + 8, st);
+    rare_skip_kernel<<<grid_for(nrec), 256, 0, st>>>(kalt, nrec, s->post_off.as<int64_t>(), s->post_sets.as<uint32_t>(),
+                                                     s->srare_skip.as<uint16_t>());
     GD_HIP(hipGetLastError());
     // pair increments of the tier (cost model, kernel choice)
     DevBuf d_incs(24, st);
@@ -1717,6 +1751,7 @@ void free_bitsets(gdist_sets* s) {
     s->srare_off.release();
     s->srare_ent.release();
     s->srare_w.release();
+    s->srare_skip.release();
     s->W = s->dict_size = 0;
     s->n_rare = s->rare_T = s->rare_records = s->rare_incs = s->rare_max_list = s->rare_incs_long = 0;
     s->rare_kmers = 0;
@@ -1893,7 +1928,7 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
             GD_REQUIRE(rgrid < (int64_t(1) << 31), "rare-tier grid too large");
             const size_t lds = (size_t)std::min<int64_t>(nc, RCH) * 4;
             rare_rows_kernel<<<(unsigned)rgrid, 256, lds, st>>>(s->srare_off.as<int64_t>(), s->srare_ent.as<uint64_t>(),
-                                                                s->srare_w.as<uint32_t>(),
+                                                                s->srare_w.as<uint32_t>(), s->srare_skip.as<uint16_t>(),
                                                                 s->post_sets.as<uint32_t>(), r0, r1, c0, c1, nch,
                                                                 nsplit, upper ? 1 : 0, d_I, ldI);
         }

@@ -318,6 +318,7 @@ struct gdist_sets {
     // post_w[list], and srare_w[] aligned with srare_ent.
     gdist::DevBuf post_w;                 // uint32 [n_rare]
     gdist::DevBuf srare_w;                // uint32 [rare_records]
+    gdist::DevBuf srare_skip;             // uint16 [rare_records]: 1 + the set's position in the list (0: none)
     int64_t rare_kmers = 0;               // rare dictionary entries before identical lists merge
     // locus guides (pack time, sparse.hip): the kmers of the first kGuides
     // sequences with the position of their first window (window * strands +
