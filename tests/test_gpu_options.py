@@ -18,11 +18,12 @@ def test_option_roundtrip_and_errors(ctx):
     import gdist
     names = gdist.option_names()
     for n in ("rare_t", "rare_kernel", "bitset_diag", "sparse", "sparse_zmax", "sketch_k", "reps_block",
-              "locus_order", "guides", "sparse_part_budget"):
+              "locus_order", "guides", "sparse_part_budget", "sparse_groups", "sketch_v2"):
         assert n in names
     # round 3: superseded kernel variants and the result-changing ablation
     # switch are gone; every remaining option preserves results
-    for n in ("sparse_abl", "sparse_kernel", "bitset_kernel", "sparse_shape", "sparse_occ", "fold_dense_words"):
+    for n in ("sparse_abl", "sparse_kernel", "bitset_kernel", "sparse_shape", "sparse_occ", "fold_dense_words",
+              "sketch_sw", "sketch_map", "sketch_split"):
         assert n not in names
     c = gdist.Context(0)
     try:
