@@ -79,6 +79,16 @@ def test_c1_method_table_bit_exact(ctx, tmp_path):
     st = stats.getvalue().splitlines()
     assert st[0] == "method1\tmethod2\tPearson\tKendall\tSpearman\tvariation\tIQR"
     assert [l.split("\t")[:2] for l in st[1:]] == [["KMER_K21", "PROT_K8"], ["PROT_K8", "KMER_K21"]]
+    # the statistics' values against scipy's (commons-math Pearson, Kendall
+    # tau-b, Spearman on average ranks; MethodTableProcessor.java:364-366),
+    # over the table's distance columns in pair order; %8.4f fields
+    from scipy import stats as sst
+    d1 = np.array([float(l.split("\t")[5]) for l in lines[1:]])
+    d2 = np.array([float(l.split("\t")[6]) for l in lines[1:]])
+    exp = (sst.pearsonr(d1, d2)[0], sst.kendalltau(d1, d2, variant="b")[0], sst.spearmanr(d1, d2)[0])
+    for row in st[1:]:
+        got = [float(x) for x in row.split("\t")[2:5]]
+        assert np.allclose(got, exp, atol=5.1e-5, rtol=0), (row, exp)
 
     # --previous: every pair reused (getDistance must not run), same rows
     prev = tmp_path / "prev.tbl"

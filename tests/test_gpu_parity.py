@@ -314,9 +314,10 @@ def test_device_outputs_and_leading_dimension(ctx):
     sets.matrix_device(dI.ptr, dD.ptr, ld, (0, 130), (0, 130), method=gdist.METHOD_BITSET)
     I = dI.to_host(np.int32).reshape(130, ld)[:, :130]
     D = dD.to_host(np.float64).reshape(130, ld)[:, :130]
-    eI, eD = sets.matrix(method=gdist.METHOD_SORTED)
-    assert np.array_equal(I, eI) and bits_equal(D, eD)
     k_ms, call_ms, launches = ctx.last_timing()
+    off, codes = oracle_pack(seqs, 12, 0, 0)
+    eI, eD = oracle.matrix(off, codes, 0, 130, 0, 130)
+    assert np.array_equal(I, eI) and bits_equal(D, eD)
     assert launches == 1 and 0 < k_ms <= call_ms
 
 
@@ -333,16 +334,22 @@ def test_device_upper_leaves_lower_untouched(ctx, method):
     dI, dD = ctx.alloc(nr * ld * 4), ctx.alloc(nr * ld * 8)
     dI.from_host(np.full(nr * ld, -7, np.int32))
     dD.from_host(np.full(nr * ld, 42.5))
+    off, codes = oracle_pack(seqs, 15, 0, 0)
     if method == "sketch":
         sk = sets.sketches(64)
         sk.matrix_device(dI.ptr, dD.ptr, ld, (r0, r1), (c0, c1), upper=True)
-        eI, eD = sk.matrix((r0, r1), (c0, c1))
+        ref = [oracle.sketch(codes[off[i]:off[i + 1]], 15, 0, 64) for i in range(n)]
+        eI = np.zeros((nr, c1 - c0), np.int32)
+        eD = np.zeros((nr, c1 - c0))
+        for a in range(nr):
+            for b in range(c1 - c0):
+                eD[a, b], eI[a, b] = oracle.sketch_distance(ref[r0 + a], ref[c0 + b], 64, 0)
     else:
         m = gdist.METHOD_SORTED if method == "sorted" else gdist.METHOD_BITSET
         if method == "bitset":
             sets.build_bitsets()
         sets.matrix_device(dI.ptr, dD.ptr, ld, (r0, r1), (c0, c1), upper=True, method=m)
-        eI, eD = sets.matrix((r0, r1), (c0, c1), method=gdist.METHOD_SORTED)
+        eI, eD = oracle.matrix(off, codes, r0, r1, c0, c1)
     I = dI.to_host(np.int32).reshape(nr, ld)[:, :c1 - c0]
     D = dD.to_host(np.float64).reshape(nr, ld)[:, :c1 - c0]
     up = np.fromfunction(lambda a, b: (c0 + b) > (r0 + a), (nr, c1 - c0))
@@ -780,7 +787,7 @@ def test_sparse_complement_words_exact(ctx, mode, opts):
 def test_sparse_equals_dense_at_size(ctx, opts):
     """C2-shaped collection (shared core, sparse substitutions): the whole
     triangle through the complement-sparse words equals the plain AND+popcount
-    tiles pair for pair, and the oracle on a corner block; row-sharded blocks
+    tiles pair for pair, and the oracle over the whole triangle; row-sharded blocks
     (unaligned, as ranks get them) agree too."""
     import gdist
     n = 420
@@ -802,10 +809,9 @@ def test_sparse_equals_dense_at_size(ctx, opts):
         Ib, _ = sp.matrix((r0, r1), (0, n), upper=True, method=gdist.METHOD_BITSET)
         mask = np.fromfunction(lambda a, b: b > (r0 + a), (r1 - r0, n))
         assert np.array_equal(Ib[mask], eI[r0:r1][mask]), (r0, r1)
-    off, codes = oracle_pack(seqs[:12], 21, 0, 0)
-    oI, oD = oracle.matrix(off, codes, 0, 12, 0, 12, flags=0x100)
-    iu12 = np.triu_indices(12, 1)
-    assert np.array_equal(I[:12, :12][iu12], oI[iu12]) and bits_equal(D[:12, :12][iu12], oD[iu12])
+    off, codes = oracle_pack(seqs, 21, 0, 0)
+    oI, oD = oracle.matrix(off, codes, 0, n, 0, n, flags=0x100, nthreads=8)
+    assert np.array_equal(I[iu], oI[iu]) and bits_equal(D[iu], oD[iu])
 
 
 def test_auto_method_prepare(ctx):
