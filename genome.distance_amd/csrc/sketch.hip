@@ -161,7 +161,8 @@ template <int R, int C, bool LDS, int KW, bool V2 = false>
 __global__ __launch_bounds__(R * C) void sketch_tile_kernel(const int32_t* __restrict__ sig,
                                                             const int64_t* __restrict__ off, int width, int sw,
                                                             int64_t r0, int64_t r1, int64_t c0, int64_t c1,
-                                                            int tiles_c, int upper, int jaccard, int empty_nan,
+                                                            int64_t tile0, int tiles_c, int upper, int jaccard,
+                                                            int empty_nan,
                                                             int32_t* __restrict__ common_out,
                                                             double* __restrict__ D, int64_t ld) {
 #pragma clang fp contract(off)
@@ -171,7 +172,8 @@ __global__ __launch_bounds__(R * C) void sketch_tile_kernel(const int32_t* __res
     __shared__ int32_t s_n[NS];
     constexpr int GR = 4, GC = 8;
     static_assert(!V2 || (R % GR == 0 && C % GC == 0 && LDS && KW == 2), "V2: GR x GC lane groups, LDS, K = 2");
-    const int tr = blockIdx.x / tiles_c, tcb = blockIdx.x % tiles_c;
+    const int64_t bt = tile0 + blockIdx.x;
+    const int tr = (int)(bt / tiles_c), tcb = (int)(bt % tiles_c);
     const int64_t row0 = r0 + (int64_t)tr * R, col0 = c0 + (int64_t)tcb * C;
     int ty, tx;
     if (V2) {
@@ -294,19 +296,23 @@ bool launch_sketch_tiles(hipStream_t st, const gdist_sets* sk, int width, int64_
     if (!use_lds && !force_global) return false;
     const int tr = (int)ceil_div(r1 - r0, R), tc = (int)ceil_div(c1 - c0, C);
     const int64_t grid = (int64_t)tr * tc;
-    GD_REQUIRE(grid < (int64_t(1) << 31), "sketch grid too large");
+    // a dispatch holds < 2^32 work-items: launches of at most 2^31 threads
+    const int threads = R * C;
+    const int64_t per = (int64_t(1) << 31) / threads;
 
     const int32_t* sig = sk->codes.as<int32_t>();
     const int64_t* off = sk->off.as<int64_t>();
     if (!use_lds) {
-        sketch_tile_kernel<R, C, false, 1><<<(unsigned)grid, R * C, 0, st>>>(
-            sig, off, width, sw, r0, r1, c0, c1, tc, upper, jac, en, d_common, d_D, ld);
+        for (int64_t t0 = 0; t0 < grid; t0 += per)
+            sketch_tile_kernel<R, C, false, 1><<<(unsigned)std::min(per, grid - t0), R * C, 0, st>>>(
+                sig, off, width, sw, r0, r1, c0, c1, t0, tc, upper, jac, en, d_common, d_D, ld);
     } else {
         auto go = [&](auto kern) {
             GD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        LDS_SK_MAX - (int)sketch_meta_bytes<R, C>()));
-            kern<<<(unsigned)grid, R * C, lds, st>>>(sig, off, width, sw, r0, r1, c0, c1, tc, upper, jac, en, d_common,
-                                                      d_D, ld);
+            for (int64_t t0 = 0; t0 < grid; t0 += per)
+                kern<<<(unsigned)std::min(per, grid - t0), threads, lds, st>>>(sig, off, width, sw, r0, r1, c0, c1, t0, tc,
+                                                                            upper, jac, en, d_common, d_D, ld);
         };
         switch (kw) {
             case 1: go(&sketch_tile_kernel<R, C, true, 1>); break;
