@@ -80,18 +80,19 @@ __device__ __forceinline__ int wave_sum(int v) {
 
 __global__ __launch_bounds__(NTJ, 1) void sorted_join_kernel(
     const uint64_t* __restrict__ codes, const int64_t* __restrict__ segoff, int nseg,
-    const int64_t* __restrict__ cb_prefix, int ncb, int64_t nunits, int64_t r0, int64_t r1, int64_t c0,
+    const int64_t* __restrict__ cb_prefix, int ncb, int64_t u0, int64_t nunits, int64_t r0, int64_t r1, int64_t c0,
     int64_t c1, const int64_t* __restrict__ colidx, int upper, int32_t* __restrict__ I, int64_t ldI) {
     __shared__ unsigned long long table[TBL];
     __shared__ int32_t cnt[CBW];
     __shared__ int has_empty_key;
 
-    // XCD-aware bijective remap: XCD x gets a contiguous range of units
+    // XCD-aware bijective remap of this launch's units [u0, u0 + G): XCD x
+    // gets a contiguous range of them
     const int64_t G = gridDim.x;
     const int64_t b = blockIdx.x;
     const int64_t x = b & 7, kq = b >> 3;
     const int64_t q = G >> 3, rem = G & 7;
-    const int64_t u = x * q + (x < rem ? x : rem) + kq;
+    const int64_t u = u0 + x * q + (x < rem ? x : rem) + kq;
     if (u >= nunits) return;
 
     // unit -> (column block, row)
@@ -225,16 +226,20 @@ static void launch_join(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t
     }
     const int64_t nunits = prefix[ncb];
     if (nunits == 0) return;
-    GD_REQUIRE(nunits < (int64_t(1) << 31), "sorted matrix grid too large");
     DevBuf dp((ncb + 1) * 8, st);
     h2d(dp.p, prefix.data(), (ncb + 1) * 8, st);
     GD_HIP(hipEventRecord(ctx->ev_k0, st));
-    sorted_join_kernel<<<(unsigned)nunits, NTJ, 0, st>>>(s->codes.as<uint64_t>(), s->segoff.as<int64_t>(), s->nseg,
-                                                         dp.as<int64_t>(), ncb, nunits, r0, r1, c0, c1, d_colidx,
-                                                         upper ? 1 : 0, d_I, ldI);
+    // a dispatch holds < 2^32 work-items: launches of at most 2^31 threads
+    // (C4's largest row block is ~55 M units)
+    const int64_t per = (int64_t(1) << 31) / NTJ;
+    int launches = 0;
+    for (int64_t u0 = 0; u0 < nunits; u0 += per, launches++)
+        sorted_join_kernel<<<(unsigned)std::min(per, nunits - u0), NTJ, 0, st>>>(
+            s->codes.as<uint64_t>(), s->segoff.as<int64_t>(), s->nseg, dp.as<int64_t>(), ncb, u0, nunits, r0, r1, c0,
+            c1, d_colidx, upper ? 1 : 0, d_I, ldI);
     GD_HIP(hipGetLastError());
     GD_HIP(hipEventRecord(ctx->ev_k1, st));
-    ctx->last.launches = 1;
+    ctx->last.launches = launches;
 }
 
 void sorted_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1,
