@@ -221,7 +221,7 @@ __global__ __launch_bounds__(256) void rare_rows_kernel(const int64_t* __restric
                                                         const uint16_t* __restrict__ sskip,
                                                         const uint32_t* __restrict__ psets, int64_t r0, int64_t r1,
                                                         int64_t c0, int64_t c1, int nch, int nsplit, int upper,
-                                                        int32_t* __restrict__ I, int64_t ldI) {
+                                                        int atomic_flush, int32_t* __restrict__ I, int64_t ldI) {
     extern __shared__ int32_t cnt[];
     const int64_t unit = blockIdx.x / nsplit;
     const int split = blockIdx.x % nsplit;
@@ -276,7 +276,7 @@ __global__ __launch_bounds__(256) void rare_rows_kernel(const int64_t* __restric
     for (int t = threadIdx.x; t < n; t += blockDim.x) {
         const int v = cnt[t];
         if (v && cb + t >= lo) {
-            if (nsplit > 1) atomicAdd(row + t, v);
+            if (nsplit > 1 || atomic_flush) atomicAdd(row + t, v);
             else row[t] += v;
         }
     }
@@ -1845,10 +1845,26 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     if (s->n_rare > 0) (void)bitset_block_cost_s(s, r0, r1, c0, c1, upper, &row_major);
     const bool list_major = ctx->has_option(OPT_RARE_KERNEL) ? ctx->option(OPT_RARE_KERNEL, 0) == 0 : !row_major;
     const bool overlap = s->n_rare > 0 && list_major && ctx->option(OPT_RARE_OVERLAP, 1) != 0;
+    // The row-major rare kernel too, when it flushes its rows with atomics
+    // (round 3, C3: its scattered list reads overlap the VALU-bound tiles)
+    const bool rows_side = s->n_rare > 0 && !list_major && !s->sparse && ctx->option(OPT_RARE_OVERLAP, 1) != 0;
     // The sparse words and the list-major rare kernel add atomically, like
     // the dense tiles, so they run on the side stream beside them.
-    const bool side = overlap || s->sparse;
+    const bool side = overlap || s->sparse || rows_side;
     bool rare_done = false;               // the sparse chunk reduce added the rare pairs
+    auto launch_rare_rows = [&](hipStream_t rs, bool atomic_flush) {
+        const int nch = (int)ceil_div(nc, RCH);
+        const int64_t units = nr * nch;
+        // few rows (C2: 1000): slice each row's rare kmers over several workgroups
+        const int nsplit = (int)std::max<int64_t>(1, std::min<int64_t>(16, ceil_div((int64_t)ctx->cus * 8, units)));
+        const int64_t rgrid = units * nsplit;
+        GD_REQUIRE(rgrid < (int64_t(1) << 31), "rare-tier grid too large");
+        const size_t lds = (size_t)std::min<int64_t>(nc, RCH) * 4;
+        rare_rows_kernel<<<(unsigned)rgrid, 256, lds, rs>>>(s->srare_off.as<int64_t>(), s->srare_ent.as<uint64_t>(),
+                                                           s->srare_w.as<uint32_t>(), s->srare_skip.as<uint16_t>(),
+                                                           s->post_sets.as<uint32_t>(), r0, r1, c0, c1, nch, nsplit,
+                                                           upper ? 1 : 0, atomic_flush ? 1 : 0, d_I, ldI);
+    };
     if (!ctx->capturing) GD_HIP(hipEventRecord(ctx->ev_k0, st));
     if (side) {
         GD_HIP(hipEventRecord(ctx->ev_fork, st));
@@ -1861,6 +1877,7 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
             rare_pairs_kernel<<<grid_for(s->n_rare, 256, 256 * 64), 256, 0, ctx->side>>>(
                 s->post_off.as<int64_t>(), s->post_sets.as<uint32_t>(), s->post_w.as<uint32_t>(), s->n_rare, r0, r1,
                 c0, c1, upper ? 1 : 0, d_I, ldI);
+        if (rows_side) launch_rare_rows(ctx->side, true);
         GD_HIP(hipGetLastError());
         GD_HIP(hipEventRecord(ctx->ev_join, ctx->side));
     }
@@ -1919,18 +1936,8 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
             rare_pairs_kernel<<<grid_for(s->n_rare, 256, 256 * 64), 256, 0, st>>>(
                 s->post_off.as<int64_t>(), s->post_sets.as<uint32_t>(), s->post_w.as<uint32_t>(), s->n_rare, r0, r1,
                 c0, c1, upper ? 1 : 0, d_I, ldI);
-        } else {
-            const int nch = (int)ceil_div(nc, RCH);
-            const int64_t units = nr * nch;
-            // few rows (C2: 1000): slice each row's rare kmers over several workgroups
-            const int nsplit = (int)std::max<int64_t>(1, std::min<int64_t>(16, ceil_div((int64_t)ctx->cus * 8, units)));
-            const int64_t rgrid = units * nsplit;
-            GD_REQUIRE(rgrid < (int64_t(1) << 31), "rare-tier grid too large");
-            const size_t lds = (size_t)std::min<int64_t>(nc, RCH) * 4;
-            rare_rows_kernel<<<(unsigned)rgrid, 256, lds, st>>>(s->srare_off.as<int64_t>(), s->srare_ent.as<uint64_t>(),
-                                                                s->srare_w.as<uint32_t>(), s->srare_skip.as<uint16_t>(),
-                                                                s->post_sets.as<uint32_t>(), r0, r1, c0, c1, nch,
-                                                                nsplit, upper ? 1 : 0, d_I, ldI);
+        } else if (!rows_side) {
+            launch_rare_rows(st, false);
         }
         GD_HIP(hipGetLastError());
         ctx->last.launches = 2;

@@ -207,7 +207,8 @@ int  gdist_sets_sparse_sides(const gdist_sets* sets, int64_t* complement_words, 
 /* The group tier of the sparse words: groups of sets (e.g.
  * the clades of a structured collection) whose members all carry the same
  * pattern in a word; those words keep per member only the residual entries
- * and the group part of every pair is precomputed. Reports the groups used
+ * and the group part of a pair is evaluated from per-group tables (T, V)
+ * with the pair's constant part. Reports the groups used
  * and the sparse words factorised by one (0s without the tier; option
  * "sparse_groups" = 0 switches it off). */
 int  gdist_sets_group_info(const gdist_sets* sets, int64_t* groups, int64_t* grouped_words);
