@@ -187,6 +187,8 @@ struct Timing {
     X(SKETCH_K, "sketch_k")                   /* sketch merge window (1 / 2 / 4 / 6, default 2) */             \
     X(SKETCH_TILE, "sketch_tile")             /* 16: force the 16x16 sketch tile */                            \
     X(SKETCH_V2, "sketch_v2")                 /* 0: the round-2 lane map and checked merge loop */             \
+    X(SKETCH_PHASE, "sketch_phase")           /* 0: whole sketches in LDS (V2), not value-range windows */     \
+    X(SKETCH_CAP, "sketch_cap")               /* hashes per sketch window of the phased kernel */              \
     X(SPARSE_PART_BUDGET, "sparse_part_budget") /* bytes of sparse chunk partials one region may hold */       \
     X(GUIDES, "guides")                       /* guide sequences keyed at pack time (default kGuides) */       \
     X(FORCE_EXCHANGE, "force_exchange")       /* 1: a one-rank communicator runs every collective (tests) */   \

@@ -1,5 +1,6 @@
-"""A/B of sketch merge windows (GDIST_SKETCH_K: kN), tile shapes
-(GDIST_SKETCH_TILE: tN) in ONE process on the C5 workload: every variant's common
+"""A/B of sketch kernels in ONE process: variants are '+'-joined parts, kN
+(option sketch_k), tN (sketch_tile) or name=value (any option, e.g.
+sketch_phase=0, sketch_cap=200; "default" = no options), on the C5 workload: every variant's common
 counts on a row block are checked identical to the first variant's, then the
 full upper triangle is timed in interleaved rounds."""
 import os, sys, time
@@ -11,16 +12,24 @@ from gdist import synth
 
 n = int(os.environ.get("AB_N", "50000")); L = int(os.environ.get("AB_LEN", "100000"))
 width = int(os.environ.get("AB_WIDTH", "1000"))
-variants = os.environ.get("AB_VARIANTS", "k1,k2,k4,k6").split(",")
+variants = os.environ.get("AB_VARIANTS", "default,sketch_phase=0").split(",")
 rounds = int(os.environ.get("AB_ROUNDS", "3"))
 check_rows = min(n, 2048)
 
 
+KNOBS = ("sketch_tile", "sketch_k", "sketch_phase", "sketch_cap", "sketch_v2")
+
+
 def apply(v):
-    ctx.set_option("sketch_tile", None)
-    ctx.set_option("sketch_k", None)
+    for k in KNOBS:
+        ctx.set_option(k, None)
     for part in v.split("+"):
-        if part.startswith("k"):
+        if "=" in part:
+            name, val = part.split("=")
+            ctx.set_option(name, int(val))
+        elif part == "default":
+            pass
+        elif part.startswith("k"):
             ctx.set_option("sketch_k", int(part[1:]))
         elif part.startswith("t"):
             ctx.set_option("sketch_tile", int(part[1:]))

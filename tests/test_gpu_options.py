@@ -18,7 +18,8 @@ def test_option_roundtrip_and_errors(ctx):
     import gdist
     names = gdist.option_names()
     for n in ("rare_t", "rare_kernel", "bitset_diag", "sparse", "sparse_zmax", "sketch_k", "reps_block",
-              "locus_order", "guides", "sparse_part_budget", "sparse_groups", "sketch_v2"):
+              "locus_order", "guides", "sparse_part_budget", "sparse_groups", "sketch_v2", "sketch_phase",
+              "sketch_cap"):
         assert n in names
     # round 3: superseded kernel variants and the result-changing ablation
     # switch are gone; every remaining option preserves results

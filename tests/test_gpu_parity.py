@@ -434,15 +434,18 @@ def test_sketch_matrix_vs_oracle(ctx):
     assert C[0, 1] == 2 and D[0, 1] == pyref.sketch_distance([1, 5, 9], [5, 9, 11], 4)[0]
 
 
-@pytest.mark.parametrize("v2,k", [(1, 2), (0, 2), (0, 4), (0, 1)])
-def test_sketch_merge_edges_vs_oracle(ctx, opts, v2, k):
+@pytest.mark.parametrize("phase,cap,v2,k", [(1, 300, 1, 2), (1, 1, 1, 2), (1, 7, 1, 2), (1, 64, 1, 2),
+                                             (1, 600, 1, 2), (0, 300, 1, 2), (0, 300, 0, 2), (0, 300, 0, 4),
+                                             (0, 300, 0, 1)])
+def test_sketch_merge_edges_vs_oracle(ctx, opts, phase, cap, v2, k):
     """Uploaded sketches with the merge's edge cases, every pair against the
-    oracle, every merge loop (options sketch_v2, sketch_k):
-    empty and short sketches,
+    oracle, every merge loop (options sketch_phase + sketch_cap: value-range
+    windows of 1..600 hashes, i.e. up to ~1000 phases per tile; sketch_v2,
+    sketch_k: whole sketches in LDS): empty and short sketches,
     identical ones, disjoint ones, INT_MIN / INT_MAX hashes (INT_MAX is the
-    V2 loop's LDS sentinel: such pairs take the checked loop)."""
+    LDS sentinel: such pairs take the checked loop)."""
     import gdist
-    opts(sketch_v2=v2, sketch_k=k)
+    opts(sketch_phase=phase, sketch_cap=cap, sketch_v2=v2, sketch_k=k)
     rng = np.random.default_rng(1234)
     for w in (64, 1000):
         sk = []
