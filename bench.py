@@ -346,10 +346,10 @@ def main():
         elif method == "sorted":
             bytes_per_pair = 16.0 * float(np.mean(sets.sizes()))    # 8(n_i+n_j)
         else:
-            # the sketch tile kernel keeps the tile's sketches in LDS; each merge
-            # step reads 2 dwords and a pair of full sketches takes exactly
-            # `width` steps (phase 1 ends at taken == width), so 8*width B of
-            # LDS reads per pair; HBM/L2 traffic is the tile fill, ~1/10 of that
+            # the sketch kernels merge from LDS; each merge step reads 2 dwords
+            # and a pair of full sketches takes exactly `width` steps (the merge
+            # ends at taken == width), so 8*width B of LDS reads per pair;
+            # HBM/L2 traffic is the windows' fill, ~1/10 of that
             bytes_per_pair = 8.0 * cfg["width"]
         algo_bytes = pairs_rank * bytes_per_pair
         achieved = algo_bytes / (k_avg_ms * 1e-3) / 1e9 if k_avg_ms > 0 else 0.0
@@ -364,8 +364,10 @@ def main():
             except Exception:
                 traffic = None
         sparse = sparse_words if (method == "bitset" and sparse_words and sparse_words["sparse_words"] > 0) else None
+        sk_whole = options.get("sketch_phase", 1) == 0
         kname = {"bitset": "bitset_tile_kernel2 (+ rare_pairs_kernel)", "sorted": "sorted_join_kernel",
-                 "sketch": "sketch_tile_kernel<16,24,LDS,K=2>"}[method]
+                 "sketch": ("sketch_tile_kernel<16,24,LDS,K=2>" if sk_whole else
+                            "sketch_phase_kernel (32x32, interleaved value-range LDS windows)")}[method]
         if sparse:
             kname = "sparse_tile_kernel<3> (1x2 micro-tiles, the dense words folded in)"
         if traffic is not None and not pmc.get("kernel", "").startswith(kname.split(" (")[0]):

@@ -476,6 +476,195 @@ __global__ __launch_bounds__(kSkTile * kSkTile) void sketch_phase_kernel(
     if (D) D[o] = d;
 }
 
+// Ring variant (option sketch_phase = 2, default). The value-range phases
+// above make every pair of a wave wait for the wave's longest window merge,
+// and a pair's merge per phase is the union of its two windows — twice as
+// many steps for a dissimilar pair as for a near-identical one, so C5's waves
+// run ~1.45x their lanes' mean steps. Here phases are
+// step-synchronised instead: every open pair takes (up to) the same budget
+// K of merge steps per phase, from a per-sketch LDS ring of RS slots in the
+// same interleaved layout (slot q of sketch s at dword 64 q + s; RS a power
+// of two, slot = position & (RS - 1)) plus one mirror row (row RS = row 0),
+// so the head pair (q, q + 1) is one ds_read2st64 at any slot. (Unmasked
+// slot indexes with kmax + 1 mirror rows cut 2 VALU per round but the larger
+// LDS leaves one workgroup per CU: C5 389 vs 336 ms.)
+// Each phase: s_min[s] = the least position of the open pairs reading s;
+// the ring is topped up to top_s = min(n_s + 2, s_min[s] + RS) (positions
+// n_s, n_s + 1 are INT_MAX sentinels; positions below s_min are never read
+// again and not loaded; every slot a load overwrites held a position <
+// s_min[s]); a pair at (pa, pb) may take K = min(kmax, lim - steps,
+// top_a - pa, top_b - pb) steps, since a round starting after j <= K - 2
+// steps reads positions <= p + K - 1. Within K the unchecked rounds run in
+// batches bounded by the remaining real union (>= the longer remainder, as
+// above), then at most one checked step. A pair with no room (it leads a
+// sketch by a whole ring over that sketch's slowest pair) takes up to kmax
+// checked steps straight from global memory, so every phase advances
+// (option sketch_wait = 1: such a pair waits for the slower ones instead,
+// and reads global memory only after a phase in which no pair advanced —
+// C5: 430 vs 336 ms with a 448-slot ring, the waiting pairs add phases). Positions, steps and the
+// closed form are the merge's: results are identical
+// (test_sketch_merge_edges_vs_oracle runs rings of 16..448 slots).
+__global__ __launch_bounds__(kSkTile * kSkTile) void sketch_ring_kernel(
+    const int32_t* __restrict__ sig, const int64_t* __restrict__ off, int width, int RS, int kmax, int64_t r0,
+    int64_t r1, int64_t c0, int64_t c1, int64_t tile0, int tiles_c, int upper, int jaccard, int empty_nan,
+    int32_t* __restrict__ common_out, double* __restrict__ D, int64_t ld, int fallback) {
+#pragma clang fp contract(off)
+    constexpr int R = kSkTile, C = kSkTile, NT = R * C, NW = NT / 64, NS = kSkLanes;
+    extern __shared__ int32_t sm[];   // [RS + 1][64]: ring slot q of sketch s at 64 q + s, row RS = row 0
+    __shared__ int64_t s_base[NS];
+    __shared__ int32_t s_n[NS], s_top[NS], s_min[NS], s_imax[NS];
+    const int64_t bt = tile0 + blockIdx.x;
+    const int tr = (int)(bt / tiles_c), tcb = (int)(bt % tiles_c);
+    const int64_t row0 = r0 + (int64_t)tr * R, col0 = c0 + (int64_t)tcb * C;
+    const int g = threadIdx.x >> 5, l = threadIdx.x & 31;
+    const int ty = l, tx = (l + g) & (C - 1);
+    if (upper && col0 + C - 1 <= row0) return;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (threadIdx.x < NS) {
+        const int s = threadIdx.x;
+        const int64_t gi = s < R ? row0 + s : col0 + (s - R);
+        const bool ok = s < R ? gi < r1 : gi < c1;
+        const int64_t b = ok ? off[gi] : 0;
+        const int n = ok ? (int)(off[gi + 1] - b) : 0;
+        s_base[s] = b;
+        s_n[s] = n;
+        s_top[s] = 0;
+        s_imax[s] = n > 0 && sig[b + n - 1] == 0x7FFFFFFF;
+    }
+    __syncthreads();
+    const int64_t i = row0 + ty, j = col0 + tx;
+    const bool valid = i < r1 && j < c1 && !(upper && j <= i);
+    const int ina = s_n[ty], inb = s_n[R + tx];
+    const bool imax = s_imax[ty] || s_imax[R + tx];
+    const int lim = jaccard ? ina + inb : width;
+    int ia = 0, ib = 0, steps = 0, extra = 0;
+    bool open = valid;
+    if (open && (ina == 0 || inb == 0 || lim == 0)) {
+        extra = min(ina + inb, lim);
+        open = false;
+    }
+    const int32_t* Arow = sm + ty;
+    const int32_t* Brow = sm + R + tx;
+    const int32_t* gA = sig + s_base[ty];
+    const int32_t* gB = sig + s_base[R + tx];
+    bool stalled = false;
+    for (;;) {
+        // 1. the least position of the open pairs on every sketch
+        if (threadIdx.x < NS) s_min[threadIdx.x] = 0x7FFFFFFF;
+        __syncthreads();
+        if (open) {
+            atomicMin(&s_min[ty], ia);
+            atomicMin(&s_min[R + tx], ib);
+        }
+        __syncthreads();
+        // 2. top the rings up: positions [max(top, least), min(n + 2, least +
+        // RS)), the sentinels past n; thread (s = lane, q = wave) moves 4
+        // positions per step, the 32 lanes of a group store to 32 distinct banks
+        {
+            const int s = lane;
+            const int n = s_n[s], least = s_min[s];
+            const int lo = least == 0x7FFFFFFF ? 0 : max(s_top[s], least);
+            const int hi = least == 0x7FFFFFFF ? 0 : min(n + 2, least + RS);
+            const int32_t* src = sig + s_base[s];
+            const int M = RS - 1;                   // RS: a power of two
+            int q = (lo + wave * 4) & M;
+            for (int t = lo + wave * 4; t < hi; t += NW * 4) {
+                i32x4_a4 v;
+                if (t + 4 <= n) {
+                    v = *reinterpret_cast<const i32x4_a4*>(src + t);
+                } else {
+                    v.x = t < n ? src[t] : 0x7FFFFFFF;
+                    v.y = t + 1 < n ? src[t + 1] : 0x7FFFFFFF;
+                    v.z = t + 2 < n ? src[t + 2] : 0x7FFFFFFF;
+                    v.w = 0x7FFFFFFF;
+                }
+                const int32_t vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    if (t + u < hi) {
+                        const int qu = (q + u) & M;
+                        sm[qu * NS + s] = vv[u];
+                        if (qu == 0) sm[RS * NS + s] = vv[u];
+                    }
+                }
+                q = (q + NW * 4) & M;
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < NS && s_min[threadIdx.x] != 0x7FFFFFFF)
+            s_top[threadIdx.x] = min(s_n[threadIdx.x] + 2, s_min[threadIdx.x] + RS);
+        // 3. K steps per open pair
+        int done = 0;
+        if (open) {
+            const int roomA = min(s_n[ty] + 2, s_min[ty] + RS) - ia;
+            const int roomB = min(s_n[R + tx] + 2, s_min[R + tx] + RS) - ib;
+            const int K = min(min(kmax, lim - steps), min(roomA, roomB));
+            if (K > 0) {
+                const int mask = RS - 1;
+                int pa = ia, pb = ib;
+                while (!imax) {
+                    const int ns = min(K - done, max(ina - pa, inb - pb));
+                    if (ns < 2) break;
+                    const int nr = ns >> 1;
+                    for (int r = 0; r < nr; r++) {
+                        const int32_t* pA = Arow + (pa & mask) * NS;      // slot RS - 1: pA[NS] is the mirror row
+                        const int32_t* pB = Brow + (pb & mask) * NS;
+                        const int32_t a0 = pA[0], a1 = pA[NS], b0 = pB[0], b1 = pB[NS];
+                        const bool le = a0 <= b0, ge = b0 <= a0;
+                        const int32_t x = le ? a1 : a0, y = ge ? b1 : b0;
+                        pa += le;
+                        pb += ge;
+                        pa += x <= y;
+                        pb += y <= x;
+                    }
+                    done += 2 * nr;
+                }
+                while (done < K && pa < ina && pb < inb) {            // checked steps inside the rings
+                    const int32_t va = Arow[(pa & mask) * NS], vb = Brow[(pb & mask) * NS];
+                    pa += va <= vb;
+                    pb += vb <= va;
+                    done++;
+                }
+                ia = pa;
+                ib = pb;
+            } else if (stalled || fallback) {
+                // no room in a ring: checked steps from global memory (option
+                // sketch_wait = 1: only after a phase with no progress anywhere)
+                const int Kg = min(kmax, lim - steps);
+                while (done < Kg && ia < ina && ib < inb) {
+                    const int32_t va = gA[ia], vb = gB[ib];
+                    ia += va <= vb;
+                    ib += vb <= va;
+                    done++;
+                }
+            }
+            steps += done;
+            if (steps >= lim) open = false;
+            else if (ia == ina || ib == inb) {     // a side ended: the rest are union-only
+                extra = min((ina - ia) + (inb - ib), lim - steps);
+                open = false;
+            }
+        }
+        stalled = !__syncthreads_or(done > 0 ? 1 : 0);
+        if (!__syncthreads_or(open ? 1 : 0)) break;
+    }
+    if (!valid) return;
+    const int common = ia + ib - steps;
+    const int taken = steps + extra;
+    const int64_t na = ina, nb = inb;
+    double d;
+    if (jaccard) {
+        if (common > 0) d = 1.0 - (double)common / (double)(na + nb - common);
+        else d = (empty_nan && na + nb == 0) ? __builtin_nan("") : 1.0;
+    } else {
+        if (common > 0) d = 1.0 - (double)common / (double)taken;
+        else d = (empty_nan && taken == 0) ? __builtin_nan("") : 1.0;
+    }
+    const int64_t o = (i - r0) * ld + (j - c0);
+    if (common_out) common_out[o] = (int32_t)common;
+    if (D) D[o] = d;
+}
+
 template <int R, int C>
 constexpr size_t sketch_meta_bytes() { return (size_t)(R + C) * (sizeof(int64_t) + sizeof(int32_t)); }
 
@@ -496,6 +685,29 @@ void launch_sketch_phase(hipStream_t st, const gdist_sets* sk, int width, int ca
         sketch_phase_kernel<<<(unsigned)std::min(per, grid - t0), threads, lds, st>>>(
             sk->codes.as<int32_t>(), sk->off.as<int64_t>(), width, cap, r0, r1, c0, c1, t0, tc, upper, jac, en,
             d_common, d_D, ld);
+    GD_HIP(hipGetLastError());
+}
+
+// ring kernel LDS: RS ring rows + the mirror row, 64 dwords each
+inline size_t sketch_ring_lds(int rs) { return (size_t)(rs + 1) * kSkLanes * 4; }
+
+void launch_sketch_ring(hipStream_t st, const gdist_sets* sk, int width, int rs, int kmax, int64_t r0, int64_t r1,
+                        int64_t c0, int64_t c1, bool upper, int jac, int en, int32_t* d_common, double* d_D,
+                        int64_t ld, bool fallback) {
+    const size_t lds = sketch_ring_lds(rs);
+    GD_REQUIRE(rs >= 16 && (rs & (rs - 1)) == 0 && kmax >= 2 && kmax < rs,
+               "sketch ring: a power of two >= 16 slots, 2 <= steps per phase < slots");
+    GD_REQUIRE(lds + (size_t)kSkLanes * 24 + 64 <= (size_t)LDS_SK_MAX, "sketch ring exceeds LDS");
+    const int tr = (int)ceil_div(r1 - r0, kSkTile), tc = (int)ceil_div(c1 - c0, kSkTile);
+    const int64_t grid = (int64_t)tr * tc;
+    const int threads = kSkTile * kSkTile;
+    const int64_t per = (int64_t(1) << 31) / threads;     // a dispatch holds < 2^32 work-items
+    GD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&sketch_ring_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    for (int64_t t0 = 0; t0 < grid; t0 += per)
+        sketch_ring_kernel<<<(unsigned)std::min(per, grid - t0), threads, lds, st>>>(
+            sk->codes.as<int32_t>(), sk->off.as<int64_t>(), width, rs, kmax, r0, r1, c0, c1, t0, tc, upper, jac, en,
+            d_common, d_D, ld, fallback ? 1 : 0);
     GD_HIP(hipGetLastError());
 }
 
@@ -656,10 +868,18 @@ void sketch_matrix(gdist_ctx* ctx, const gdist_sets* sk, int64_t r0, int64_t r1,
     // option sketch_phase = 0 keeps whole sketches in LDS (the V2 / window
     // kernels); sketch_cap sets the phased kernel's window (default: two
     // 32 x 32 workgroups per CU)
-    const bool phase = ctx->option(OPT_SKETCH_PHASE, 1) != 0 && !only16 && kw == 2;
+    const bool phase = ctx->option(OPT_SKETCH_PHASE, 2) != 0 && !only16 && kw == 2;
     const int cap = (int)std::max<int64_t>(1, std::min<int64_t>(ctx->option(OPT_SKETCH_CAP, 300), 600));
     GD_HIP(hipEventRecord(ctx->ev_k0, st));
-    if (phase)
+    const int64_t mode = ctx->option(OPT_SKETCH_PHASE, 2);
+    if (phase && mode == 2) {
+        // options sketch_cap (steps per phase, default 160) and sketch_ring
+        // (ring slots, default 256: 257 rows of 256 B = 66 KB, two workgroups per CU)
+        const int kmax = (int)std::max<int64_t>(2, std::min<int64_t>(ctx->option(OPT_SKETCH_CAP, 160), 1 << 20));
+        const int rs = (int)std::max<int64_t>(16, std::min<int64_t>(ctx->option(OPT_SKETCH_RING, 256), 1 << 20));
+        launch_sketch_ring(st, sk, width, rs, std::min(kmax, rs - 1), r0, r1, c0, c1, upper, jac, en, d_common, d_D,
+                           ld, ctx->option(OPT_SKETCH_WAIT, 0) == 0);
+    } else if (phase)
         launch_sketch_phase(st, sk, width, cap, r0, r1, c0, c1, upper, jac, en, d_common, d_D, ld);
     else if (only16 || !launch_sketch_tiles<16, 24>(st, sk, width, r0, r1, c0, c1, upper, jac, en, d_common, d_D, ld,
                                                false, kw, v2))
