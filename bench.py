@@ -367,7 +367,7 @@ def main():
         sk_whole = options.get("sketch_phase", 1) == 0
         kname = {"bitset": "bitset_tile_kernel2 (+ rare_pairs_kernel)", "sorted": "sorted_join_kernel",
                  "sketch": ("sketch_tile_kernel<16,24,LDS,K=2>" if sk_whole else
-                            "sketch_phase_kernel (32x32, interleaved value-range LDS windows)")}[method]
+                            "sketch_ring_kernel (32x32, interleaved LDS rings, step-synchronised phases)")}[method]
         if sparse:
             kname = "sparse_tile_kernel<3> (1x2 micro-tiles, the dense words folded in)"
         if traffic is not None and not pmc.get("kernel", "").startswith(kname.split(" (")[0]):

@@ -187,8 +187,8 @@ struct Timing {
     X(SKETCH_K, "sketch_k")                   /* sketch merge window (1 / 2 / 4 / 6, default 2) */             \
     X(SKETCH_TILE, "sketch_tile")             /* 16: force the 16x16 sketch tile */                            \
     X(SKETCH_V2, "sketch_v2")                 /* 0: the round-2 lane map and checked merge loop */             \
-    X(SKETCH_PHASE, "sketch_phase")           /* 0 whole sketches (V2) / 1 value-range windows / 2 step rings */ \
-    X(SKETCH_CAP, "sketch_cap")               /* window hashes (phase 1, 300) / steps per phase (2, 160) */    \
+    X(SKETCH_PHASE, "sketch_phase")           /* 0: whole sketches in LDS (V2 / windows), not the ring kernel */ \
+    X(SKETCH_CAP, "sketch_cap")               /* ring kernel: merge steps per phase (default 160) */           \
     X(SKETCH_RING, "sketch_ring")             /* ring kernel slots per sketch (default 256) */                 \
     X(SKETCH_WAIT, "sketch_wait")             /* 1: ring pairs without room wait (global reads only if stuck) */ \
     X(SPARSE_PART_BUDGET, "sparse_part_budget") /* bytes of sparse chunk partials one region may hold */       \

@@ -11,8 +11,10 @@
 //
 // Build: hash every code of a chunk of sets, radix-sort 64-bit keys
 // (set id << 32 | biased hash), keep the first `width` distinct hashes of
-// each set. Matrix: a workgroup owns a 16×16 tile of sketch pairs; the 32
-// sketches are staged in LDS and each thread merges one pair.
+// each set. Matrix: sketch_ring_kernel (default) — a workgroup owns a
+// 32 x 32 tile of sketch pairs, one lane per pair, the 64 sketches streaming
+// through interleaved LDS rings in step-synchronised phases; the
+// whole-sketch kernels (option sketch_phase = 0) stage whole sketches in LDS.
 #include <cstring>
 #include <rocprim/rocprim.hpp>
 
@@ -280,214 +282,32 @@ __global__ __launch_bounds__(R * C) void sketch_tile_kernel(const int32_t* __res
     if (D) D[o] = d;
 }
 
-// Phased merge (round 3, default). The whole-sketch kernel above is bound by
-// LDS bank conflicts: its lanes read their sketches at data-dependent
-// positions, so a 32-lane group's ds_read hits random banks (68 % of LDS
-// cycles are conflict cycles, profiles/r03/sketch/pmc_v2.txt). Here the tile
-// is 32 row x 32 column sketches and LDS is interleaved: hash t of sketch s
-// (rows 0..31, columns 32..63) sits at dword 64 t + s, so its bank is s mod 32
-// whatever t is. Lane l of 32-lane group g merges row l with column
-// (l + g) mod 32: the 32 lanes of a group read 32 distinct rows and 32
-// distinct columns — conflict-free reads at any merge positions. The two
-// heads of a side (t, t + 1) are one ds_read2_b32 (offsets 0 and 64 dwords).
-//
-// 64 whole sketches do not fit LDS interleaved, so they pass through in
-// value-range windows: each phase loads, per sketch, its next `cap` + 1
-// hashes from its current position; T = the smallest of those (cap+1)-th
-// hashes over the tile, and every sketch's window is its hashes < T (at most
-// `cap`; all of them when every sketch has <= cap left: T = +inf, the last
-// phase). A merge consumes hashes in value order, so a pair's merge runs
-// through both windows in full (all hashes < T of both sides) and stops there
-// with ia, ib at the window ends — the next phase starts every open pair
-// exactly at the new window starts. Pair state (ia, ib, steps) stays in
-// registers across phases. Two INT_MAX sentinels after each window let the
-// unchecked two-step rounds run while fewer than max(remaining window hashes)
-// steps are taken (the V2 argument, per window); the checked tail compares
-// positions with the window ends (hashes past a window end are >= T > every
-// window hash of the other side). A side that ends inside its window closes
-// the pair in closed form (the rest of the other side are distinct union
-// elements). A pair with an INT_MAX hash (the sentinel value) takes the
-// checked loop only. The phase logic is restated and checked against the
-// oracle in tests/test_gpu_parity.py::test_sketch_merge_edges_vs_oracle
-// (window capacities 1..600). With cap = 300 a tile's windows take 77 KB:
-// two workgroups, 32 waves per CU.
-//
-// Merge semantics: Sketch.distance (WidthProcessor.java:185), restated in
-// oracle/gdist_oracle.c:or_sketch_distance.
 constexpr int kSkTile = 32;                 // rows = columns = LDS banks of ds_read_b32
 constexpr int kSkLanes = 2 * kSkTile;       // interleave stride (dwords) = sketches per tile
 typedef int32_t i32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 
-__global__ __launch_bounds__(kSkTile * kSkTile) void sketch_phase_kernel(
-    const int32_t* __restrict__ sig, const int64_t* __restrict__ off, int width, int cap, int64_t r0, int64_t r1,
-    int64_t c0, int64_t c1, int64_t tile0, int tiles_c, int upper, int jaccard, int empty_nan,
-    int32_t* __restrict__ common_out, double* __restrict__ D, int64_t ld) {
-#pragma clang fp contract(off)
-    constexpr int R = kSkTile, C = kSkTile, NT = R * C, NW = NT / 64, NS = kSkLanes;
-    extern __shared__ int32_t sm[];   // [cap + 2][64]: window hash t of sketch s at 64 t + s
-    __shared__ int64_t s_base[NS];
-    __shared__ int32_t s_n[NS], s_pos[NS], s_end[NS], s_imax[NS];
-    __shared__ int s_last;
-    const int64_t bt = tile0 + blockIdx.x;
-    const int tr = (int)(bt / tiles_c), tcb = (int)(bt % tiles_c);
-    const int64_t row0 = r0 + (int64_t)tr * R, col0 = c0 + (int64_t)tcb * C;
-    const int g = threadIdx.x >> 5, l = threadIdx.x & 31;
-    const int ty = l, tx = (l + g) & (C - 1);
-    if (upper && col0 + C - 1 <= row0) return;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (threadIdx.x < NS) {
-        const int s = threadIdx.x;
-        const int64_t gi = s < R ? row0 + s : col0 + (s - R);
-        const bool ok = s < R ? gi < r1 : gi < c1;
-        const int64_t b = ok ? off[gi] : 0;
-        const int n = ok ? (int)(off[gi + 1] - b) : 0;
-        s_base[s] = b;
-        s_n[s] = n;
-        s_pos[s] = 0;
-        s_imax[s] = n > 0 && sig[b + n - 1] == 0x7FFFFFFF;
-    }
-    __syncthreads();
-    const int64_t i = row0 + ty, j = col0 + tx;
-    const bool valid = i < r1 && j < c1 && !(upper && j <= i);
-    const int ina = s_n[ty], inb = s_n[R + tx];
-    const bool imax = s_imax[ty] || s_imax[R + tx];
-    const int lim = jaccard ? ina + inb : width;
-    int ia = 0, ib = 0, steps = 0, extra = 0;
-    bool open = valid;
-    if (open && (ina == 0 || inb == 0 || lim == 0)) {
-        extra = min(ina + inb, lim);
-        open = false;
-    }
-    const int32_t* Arow = sm + ty;
-    const int32_t* Brow = sm + R + tx;
-    for (;;) {
-        // 1. windows: the next cap + 1 hashes of every sketch. Thread (s =
-        // lane, q = wave) moves hashes 4q.. of sketch s, 4 per 16-byte load,
-        // q += NW: the 32 lanes of a group store to 32 distinct banks.
-        {
-            const int s = lane;
-            const int n = s_n[s], p = s_pos[s];
-            const int L = min(cap + 1, n - p);
-            const int32_t* src = sig + s_base[s] + p;
-            for (int t = wave * 4; t < L; t += NW * 4) {
-                i32x4_a4 v;
-                if (t + 4 <= L) {
-                    v = *reinterpret_cast<const i32x4_a4*>(src + t);
-                } else {
-                    v.x = src[t];
-                    v.y = t + 1 < L ? src[t + 1] : 0;
-                    v.z = t + 2 < L ? src[t + 2] : 0;
-                    v.w = 0;
-                }
-                sm[(t + 0) * NS + s] = v.x;
-                sm[(t + 1) * NS + s] = v.y;
-                sm[(t + 2) * NS + s] = v.z;
-                sm[(t + 3) * NS + s] = v.w;
-            }
-        }
-        __syncthreads();
-        // 2. the phase bound T and each window's end (wave 0, a lane per sketch)
-        if (wave == 0) {
-            int64_t cand = INT64_MAX;
-            const int n = s_n[lane], p = s_pos[lane];
-            const int L = min(cap + 1, n - p);
-            if (n - p > cap) cand = sm[cap * NS + lane];
-#pragma unroll
-            for (int d = 32; d >= 1; d >>= 1) {
-                const int64_t o = __shfl_xor(cand, d, 64);
-                cand = o < cand ? o : cand;
-            }
-            int e = L;                              // last phase: every remaining hash
-            if (cand != INT64_MAX) {                // hashes < T (at most cap of them)
-                int lo = 0, hi = min(L, cap);
-                while (lo < hi) {
-                    const int mid = (lo + hi) >> 1;
-                    if ((int64_t)sm[mid * NS + lane] < cand) lo = mid + 1; else hi = mid;
-                }
-                e = lo;
-            }
-            sm[e * NS + lane] = 0x7FFFFFFF;
-            sm[(e + 1) * NS + lane] = 0x7FFFFFFF;
-            s_end[lane] = p + e;
-            if (lane == 0) s_last = cand == INT64_MAX;
-        }
-        __syncthreads();
-        // 3. merge through both windows
-        if (open) {
-            const int pa0 = s_pos[ty], pb0 = s_pos[R + tx];
-            const int ea = s_end[ty] - pa0, eb = s_end[R + tx] - pb0;
-            int pa = ia - pa0, pb = ib - pb0;      // 0, 0 for every open pair
-            // unchecked rounds in batches: a batch of ns steps is safe while ns <=
-            // the union of what is left of both windows, which is >= the longer
-            // remainder; re-bounding after each batch leaves ~1 step to the
-            // checked loop instead of the shorter window's share of the union
-            // (one bound per window left ~40 % of C5's steps checked)
-            while (!imax) {
-                const int ns = min(lim - steps, max(ea - pa, eb - pb));
-                if (ns < 2) break;
-                const int nr = ns >> 1;
-                for (int r = 0; r < nr; r++) {
-                    const int32_t a0 = Arow[pa * NS], a1 = Arow[pa * NS + NS];
-                    const int32_t b0 = Brow[pb * NS], b1 = Brow[pb * NS + NS];
-                    const bool le = a0 <= b0, ge = b0 <= a0;
-                    const int32_t x = le ? a1 : a0, y = ge ? b1 : b0;
-                    pa += le;
-                    pb += ge;
-                    pa += x <= y;
-                    pb += y <= x;
-                }
-                steps += 2 * nr;
-            }
-            while (steps < lim && (pa < ea || pb < eb)) {
-                const int32_t va = Arow[pa * NS], vb = Brow[pb * NS];
-                const bool aa = pa < ea && (pb >= eb || va <= vb);
-                const bool bb = pb < eb && (pa >= ea || vb <= va);
-                pa += aa;
-                pb += bb;
-                steps++;
-            }
-            ia = pa0 + pa;
-            ib = pb0 + pb;
-            if (steps >= lim) open = false;
-            else if (ia == ina || ib == inb) {     // a side ended: the rest are union-only
-                extra = min((ina - ia) + (inb - ib), lim - steps);
-                open = false;
-            }
-        }
-        const int more = __syncthreads_or(open ? 1 : 0);
-        if (!more || s_last) break;
-        if (threadIdx.x < NS) s_pos[threadIdx.x] = s_end[threadIdx.x];
-        __syncthreads();
-    }
-    if (!valid) return;
-    const int common = ia + ib - steps;
-    const int taken = steps + extra;
-    const int64_t na = ina, nb = inb;
-    double d;
-    if (jaccard) {
-        if (common > 0) d = 1.0 - (double)common / (double)(na + nb - common);
-        else d = (empty_nan && na + nb == 0) ? __builtin_nan("") : 1.0;
-    } else {
-        if (common > 0) d = 1.0 - (double)common / (double)taken;
-        else d = (empty_nan && taken == 0) ? __builtin_nan("") : 1.0;
-    }
-    const int64_t o = (i - r0) * ld + (j - c0);
-    if (common_out) common_out[o] = (int32_t)common;
-    if (D) D[o] = d;
-}
-
-// Ring variant (option sketch_phase = 2, default). The value-range phases
-// above make every pair of a wave wait for the wave's longest window merge,
-// and a pair's merge per phase is the union of its two windows — twice as
-// many steps for a dissimilar pair as for a near-identical one, so C5's waves
-// run ~1.45x their lanes' mean steps. Here phases are
-// step-synchronised instead: every open pair takes (up to) the same budget
-// K of merge steps per phase, from a per-sketch LDS ring of RS slots in the
-// same interleaved layout (slot q of sketch s at dword 64 q + s; RS a power
-// of two, slot = position & (RS - 1)) plus one mirror row (row RS = row 0),
-// so the head pair (q, q + 1) is one ds_read2st64 at any slot. (Unmasked
-// slot indexes with kmax + 1 mirror rows cut 2 VALU per round but the larger
-// LDS leaves one workgroup per CU: C5 389 vs 336 ms.)
+// Ring kernel (round 3, default; option sketch_phase = 0 keeps the
+// whole-sketch kernels above). Those are bound by LDS bank conflicts: their
+// lanes read their sketches at data-dependent positions, so a 32-lane
+// group's ds_read hits random banks (68 % of LDS cycles are conflict cycles,
+// profiles/r03/sketch/pmc_v2.txt). Here the tile is 32 row x 32 column
+// sketches and LDS is interleaved: slot q of sketch s (rows 0..31, columns
+// 32..63) sits at dword 64 q + s, so its bank is s mod 32 whatever q is. Lane
+// l of 32-lane group g merges row l with column (l + g) mod 32: the 32 lanes
+// of a group read 32 distinct rows and 32 distinct columns — conflict-free at
+// any merge positions (SQ_LDS_BANK_CONFLICT = 0, profiles/r03/sketch2/).
+//
+// 64 whole sketches do not fit LDS interleaved, so each sketch streams
+// through a ring of RS slots (RS a power of two, slot = position & (RS - 1),
+// plus one mirror row RS = row 0 so the head pair (q, q + 1) is one
+// ds_read2st64 at any slot) in step-synchronised phases: every open pair
+// takes (up to) the same budget K of merge steps per phase. (Value-range
+// phases — every sketch's hashes below a common bound per phase — were
+// measured first: a pair's merge per phase is then the union of its two
+// windows, twice as many steps for a dissimilar pair as for a near-identical
+// one, and C5's waves ran ~1.45x their lanes' mean steps: 368 vs 320 ms.
+// Unmasked slot indexes with kmax + 1 mirror rows cut 2 VALU per round, but
+// the larger LDS leaves one workgroup per CU: 389 ms.)
 // Each phase: s_min[s] = the least position of the open pairs reading s;
 // the ring is topped up to top_s = min(n_s + 2, s_min[s] + RS) (positions
 // n_s, n_s + 1 are INT_MAX sentinels; positions below s_min are never read
@@ -507,14 +327,26 @@ __global__ __launch_bounds__(kSkTile * kSkTile) void sketch_phase_kernel(
 __global__ __launch_bounds__(kSkTile * kSkTile) void sketch_ring_kernel(
     const int32_t* __restrict__ sig, const int64_t* __restrict__ off, int width, int RS, int kmax, int64_t r0,
     int64_t r1, int64_t c0, int64_t c1, int64_t tile0, int tiles_c, int upper, int jaccard, int empty_nan,
-    int32_t* __restrict__ common_out, double* __restrict__ D, int64_t ld, int fallback) {
+    int32_t* __restrict__ common_out, double* __restrict__ D, int64_t ld, int fallback, int tri) {
 #pragma clang fp contract(off)
     constexpr int R = kSkTile, C = kSkTile, NT = R * C, NW = NT / 64, NS = kSkLanes;
     extern __shared__ int32_t sm[];   // [RS + 1][64]: ring slot q of sketch s at 64 q + s, row RS = row 0
     __shared__ int64_t s_base[NS];
     __shared__ int32_t s_n[NS], s_top[NS], s_min[NS], s_imax[NS];
     const int64_t bt = tile0 + blockIdx.x;
-    const int tr = (int)(bt / tiles_c), tcb = (int)(bt % tiles_c);
+    int tr, tcb;
+    if (tri) {
+        // a square upper triangle launches only its tiles tr <= tcb:
+        // bt = tcb (tcb + 1) / 2 + tr
+        int64_t a = (int64_t)((__builtin_sqrt(8.0 * (double)bt + 1.0) - 1.0) * 0.5);
+        while (a * (a + 1) / 2 > bt) a--;
+        while ((a + 1) * (a + 2) / 2 <= bt) a++;
+        tcb = (int)a;
+        tr = (int)(bt - a * (a + 1) / 2);
+    } else {
+        tr = (int)(bt / tiles_c);
+        tcb = (int)(bt % tiles_c);
+    }
     const int64_t row0 = r0 + (int64_t)tr * R, col0 = c0 + (int64_t)tcb * C;
     const int g = threadIdx.x >> 5, l = threadIdx.x & 31;
     const int ty = l, tx = (l + g) & (C - 1);
@@ -668,26 +500,6 @@ __global__ __launch_bounds__(kSkTile * kSkTile) void sketch_ring_kernel(
 template <int R, int C>
 constexpr size_t sketch_meta_bytes() { return (size_t)(R + C) * (sizeof(int64_t) + sizeof(int32_t)); }
 
-// the phased kernel's LDS: cap hashes + 2 sentinels per sketch, 64 sketches
-inline size_t sketch_phase_lds(int cap) { return (size_t)(cap + 2) * kSkLanes * 4; }
-
-void launch_sketch_phase(hipStream_t st, const gdist_sets* sk, int width, int cap, int64_t r0, int64_t r1, int64_t c0,
-                         int64_t c1, bool upper, int jac, int en, int32_t* d_common, double* d_D, int64_t ld) {
-    const size_t lds = sketch_phase_lds(cap);
-    GD_REQUIRE(lds + (size_t)kSkLanes * 24 + 64 <= (size_t)LDS_SK_MAX, "sketch window capacity exceeds LDS");
-    const int tr = (int)ceil_div(r1 - r0, kSkTile), tc = (int)ceil_div(c1 - c0, kSkTile);
-    const int64_t grid = (int64_t)tr * tc;
-    const int threads = kSkTile * kSkTile;
-    const int64_t per = (int64_t(1) << 31) / threads;     // a dispatch holds < 2^32 work-items
-    GD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&sketch_phase_kernel),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    for (int64_t t0 = 0; t0 < grid; t0 += per)
-        sketch_phase_kernel<<<(unsigned)std::min(per, grid - t0), threads, lds, st>>>(
-            sk->codes.as<int32_t>(), sk->off.as<int64_t>(), width, cap, r0, r1, c0, c1, t0, tc, upper, jac, en,
-            d_common, d_D, ld);
-    GD_HIP(hipGetLastError());
-}
-
 // ring kernel LDS: RS ring rows + the mirror row, 64 dwords each
 inline size_t sketch_ring_lds(int rs) { return (size_t)(rs + 1) * kSkLanes * 4; }
 
@@ -699,7 +511,10 @@ void launch_sketch_ring(hipStream_t st, const gdist_sets* sk, int width, int rs,
                "sketch ring: a power of two >= 16 slots, 2 <= steps per phase < slots");
     GD_REQUIRE(lds + (size_t)kSkLanes * 24 + 64 <= (size_t)LDS_SK_MAX, "sketch ring exceeds LDS");
     const int tr = (int)ceil_div(r1 - r0, kSkTile), tc = (int)ceil_div(c1 - c0, kSkTile);
-    const int64_t grid = (int64_t)tr * tc;
+    // a square upper triangle (the all-pairs call) launches only tiles on or
+    // above the diagonal instead of exiting the lower half's workgroups
+    const bool tri = upper && r0 == c0 && r1 == c1;
+    const int64_t grid = tri ? (int64_t)tc * (tc + 1) / 2 : (int64_t)tr * tc;
     const int threads = kSkTile * kSkTile;
     const int64_t per = (int64_t(1) << 31) / threads;     // a dispatch holds < 2^32 work-items
     GD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&sketch_ring_kernel),
@@ -707,7 +522,7 @@ void launch_sketch_ring(hipStream_t st, const gdist_sets* sk, int width, int rs,
     for (int64_t t0 = 0; t0 < grid; t0 += per)
         sketch_ring_kernel<<<(unsigned)std::min(per, grid - t0), threads, lds, st>>>(
             sk->codes.as<int32_t>(), sk->off.as<int64_t>(), width, rs, kmax, r0, r1, c0, c1, t0, tc, upper, jac, en,
-            d_common, d_D, ld, fallback ? 1 : 0);
+            d_common, d_D, ld, fallback ? 1 : 0, tri ? 1 : 0);
     GD_HIP(hipGetLastError());
 }
 
@@ -866,22 +681,18 @@ void sketch_matrix(gdist_ctx* ctx, const gdist_sets* sk, int64_t r0, int64_t r1,
     const int64_t kw = ctx->option(OPT_SKETCH_K, 2);
     const bool v2 = ctx->option(OPT_SKETCH_V2, 1) != 0;
     // option sketch_phase = 0 keeps whole sketches in LDS (the V2 / window
-    // kernels); sketch_cap sets the phased kernel's window (default: two
-    // 32 x 32 workgroups per CU)
-    const bool phase = ctx->option(OPT_SKETCH_PHASE, 2) != 0 && !only16 && kw == 2;
-    const int cap = (int)std::max<int64_t>(1, std::min<int64_t>(ctx->option(OPT_SKETCH_CAP, 300), 600));
+    // kernels); sketch_cap sets the ring kernel's steps per phase and
+    // sketch_ring its slots per sketch
+    const bool ring = ctx->option(OPT_SKETCH_PHASE, 1) != 0 && !only16 && kw == 2;
     GD_HIP(hipEventRecord(ctx->ev_k0, st));
-    const int64_t mode = ctx->option(OPT_SKETCH_PHASE, 2);
-    if (phase && mode == 2) {
-        // options sketch_cap (steps per phase, default 160) and sketch_ring
-        // (ring slots, default 256: 257 rows of 256 B = 66 KB, two workgroups per CU)
+    if (ring) {
+        // default 160 steps per phase, 256 slots: 257 rows of 256 B = 66 KB,
+        // two workgroups per CU
         const int kmax = (int)std::max<int64_t>(2, std::min<int64_t>(ctx->option(OPT_SKETCH_CAP, 160), 1 << 20));
         const int rs = (int)std::max<int64_t>(16, std::min<int64_t>(ctx->option(OPT_SKETCH_RING, 256), 1 << 20));
         launch_sketch_ring(st, sk, width, rs, std::min(kmax, rs - 1), r0, r1, c0, c1, upper, jac, en, d_common, d_D,
                            ld, ctx->option(OPT_SKETCH_WAIT, 0) == 0);
-    } else if (phase)
-        launch_sketch_phase(st, sk, width, cap, r0, r1, c0, c1, upper, jac, en, d_common, d_D, ld);
-    else if (only16 || !launch_sketch_tiles<16, 24>(st, sk, width, r0, r1, c0, c1, upper, jac, en, d_common, d_D, ld,
+    } else if (only16 || !launch_sketch_tiles<16, 24>(st, sk, width, r0, r1, c0, c1, upper, jac, en, d_common, d_D, ld,
                                                false, kw, v2))
         if (!launch_sketch_tiles<16, 16>(st, sk, width, r0, r1, c0, c1, upper, jac, en, d_common, d_D, ld, false, kw, v2))
             launch_sketch_tiles<16, 16>(st, sk, width, r0, r1, c0, c1, upper, jac, en, d_common, d_D, ld, true, kw, v2);

@@ -435,25 +435,23 @@ def test_sketch_matrix_vs_oracle(ctx):
 
 
 @pytest.mark.parametrize("phase,cap,ring,v2,k", [
-    (1, 300, None, 1, 2), (1, 1, None, 1, 2), (1, 7, None, 1, 2), (1, 64, None, 1, 2), (1, 600, None, 1, 2),
-    (2, None, None, 1, 2), (2, 2, 512, 1, 2), (2, 7, 512, 1, 2), (2, 64, 256, 1, 2), (2, 255, 256, 1, 2),
-    (2, 5000, 128, 1, 2), (2, 15, 16, 1, 2), (2, 8, 32, 1, 2), (2, 120, 512, 1, 2), ("w", 15, 16, 1, 2),
+    (1, None, None, 1, 2), (1, 2, 512, 1, 2), (1, 7, 512, 1, 2), (1, 64, 256, 1, 2), (1, 255, 256, 1, 2),
+    (1, 5000, 128, 1, 2), (1, 15, 16, 1, 2), (1, 8, 32, 1, 2), (1, 120, 512, 1, 2), ("w", 15, 16, 1, 2),
     ("w", 8, 32, 1, 2), ("w", 64, 256, 1, 2),
     (0, 300, None, 1, 2), (0, 300, None, 0, 2), (0, 300, None, 0, 4), (0, 300, None, 0, 1)])
 def test_sketch_merge_edges_vs_oracle(ctx, opts, phase, cap, ring, v2, k):
     """Uploaded sketches with the merge's edge cases, every pair against the
-    oracle, every merge loop (options sketch_phase + sketch_cap: value-range
-    windows of 1..600 hashes, i.e. up to ~1000 phases per tile; sketch_phase
-    2, the default: step rings of 16..600 slots with 2..255 steps per phase —
-    pairs without room in a small ring take global-memory steps, or with
-    sketch_wait wait for the slower pairs until a phase makes no progress;
-    sketch_v2, sketch_k: whole sketches
-    in LDS): empty and short sketches,
+    oracle, every merge loop (the ring kernel, the default: options
+    sketch_ring + sketch_cap, rings of 16..512 slots with 2..5000 steps per
+    phase; pairs without room in a small ring take global-memory steps, or
+    with sketch_wait wait for the slower pairs until a phase makes no
+    progress; sketch_phase = 0 with sketch_v2 / sketch_k: whole sketches in
+    LDS): empty and short sketches,
     identical ones, disjoint ones, INT_MIN / INT_MAX hashes (INT_MAX is the
     LDS sentinel: such pairs take the checked loop)."""
     import gdist
     wait = phase == "w"                       # ring pairs without room wait (option sketch_wait)
-    opts(sketch_phase=2 if wait else phase, sketch_wait=1 if wait else None, sketch_cap=cap, sketch_ring=ring,
+    opts(sketch_phase=1 if wait else phase, sketch_wait=1 if wait else None, sketch_cap=cap, sketch_ring=ring,
          sketch_v2=v2, sketch_k=k)
     rng = np.random.default_rng(1234)
     for w in (64, 1000):
