@@ -770,7 +770,17 @@ __global__ __launch_bounds__(256) void sparse_reduce_kernel(const int32_t* __res
         acc[4] += v.z & 0xFFFFu; acc[5] += v.z >> 16;
         acc[6] += v.w & 0xFFFFu; acc[7] += v.w >> 16;
     };
+    // 8 independent 16-byte loads in flight per lane (4 in round 2/3: the
+    // partials sit in L2 / the Infinity Cache right after the tile kernel,
+    // and the read is latency-bound at 4 per lane)
     int c = wv;
+    for (; c + 28 < nchunks; c += 32) {
+        uint4 v[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) v[k] = p[(int64_t)(c + 4 * k) * (SB * SB / 8)];
+#pragma unroll
+        for (int k = 0; k < 8; k++) add(v[k]);
+    }
     for (; c + 12 < nchunks; c += 16) {
         uint4 v[4];
 #pragma unroll
