@@ -1782,7 +1782,8 @@ static MatrixPlan& matrix_plan(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, 
     // so that changing one builds a new plan instead of reusing a stale one
     const std::vector<int64_t> key{r0, r1, c0, c1, upper ? 1 : 0, split_diag ? 1 : 0, max_rr, tW,
                                    ctx->option(OPT_SPARSE_RARE, 1), ctx->option(OPT_SPARSE_CHUNKS, -1),
-                                   ctx->option(OPT_SPARSE_PART_BUDGET, -1), ctx->option(OPT_SPARSE_WG_PER_CU, -1)};
+                                   ctx->option(OPT_SPARSE_PART_BUDGET, -1), ctx->option(OPT_SPARSE_WG_PER_CU, -1),
+                                   ctx->option(OPT_SPARSE_XCD, 0)};
     auto it = s->plans.find(key);
     if (it == s->plans.end()) {
         if (s->plans.size() >= 8) {   // row-block loops: keep the cache small

@@ -630,12 +630,26 @@ __global__ __launch_bounds__(SNT, 8) void sparse_tile_kernel(
     const int64_t* __restrict__ off, const ulonglong2* __restrict__ ent, const int32_t* __restrict__ nc, int64_t Us,
     int64_t Ws, const int2* __restrict__ tiles, const int32_t* __restrict__ cbnd, int nchunks, int64_t r0, int64_t r1,
     int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I, int64_t ldI, int32_t* __restrict__ part, int64_t Wdp,
-    int64_t N, const unsigned long long* __restrict__ slab_bits, int slabs, GroupPart gp) {
+    int64_t N, const unsigned long long* __restrict__ slab_bits, int slabs, GroupPart gp, int xmap, int ntiles) {
     // gp: the group tier's part of every pair, added with the constant part
     // slab_bits / slabs: the in-kernel fold's dense words (set-major [N][Wdp])
     __shared__ uint32_t cnt[SB * SB / 2];                  // 32 KiB, 16-bit counters (cnt_index layout)
     __shared__ int4 rec[SNW][64];                          // 8 KiB: the batch's walk records
-    const int tile = blockIdx.x / nchunks, ch = blockIdx.x % nchunks;
+    int tile, ch;
+    if (xmap) {
+        // option sparse_xcd: workgroup b = 8 (t + ntiles g) + x runs chunk
+        // 8 g + x of tile t. Workgroups are dealt to the 8 XCDs round-robin,
+        // so chunk c of every tile runs on XCD c mod 8, the tiles of one
+        // chunk back to back: that XCD's L2 serves the chunk's records
+        // (~0.85 MB on C2) to all the tiles reading them
+        const int x = (int)(blockIdx.x & 7), k = (int)(blockIdx.x >> 3);
+        tile = k % ntiles;
+        ch = 8 * (k / ntiles) + x;
+        if (ch >= nchunks) return;
+    } else {
+        tile = blockIdx.x / nchunks;
+        ch = blockIdx.x % nchunks;
+    }
     const int64_t A = tiles[tile].x, B = tiles[tile].y;
     const int rlo = (int)(r0 - A * SB > 0 ? r0 - A * SB : 0);
     const int rhi = (int)(r1 - A * SB < SB ? r1 - A * SB : SB);
@@ -1438,6 +1452,13 @@ void sparse_plan(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, in
                     if (bounds_ok(b)) { bnd = b; break; }
                 }
             }
+            // XCD-mapped order (option sparse_xcd): whole groups of 8 chunks, so
+            // every XCD gets the same number of chunks of every tile
+            const int64_t nb1 = (int64_t)bnd.size() - 1;
+            if (ctx->option(OPT_SPARSE_XCD, 0) != 0 && nb1 > 8 && nb1 % 8) {
+                auto b = make_bounds(ceil_div(nb1, 8) * 8);
+                if (bounds_ok(b)) bnd = b;
+            }
             if (ctx->has_option(OPT_SPARSE_CHUNKS))   // tests: a given chunk count (exactness still checked)
                 bnd = make_bounds(std::max<int64_t>(s->sp_fold_slabs,
                                                     std::max<int64_t>(1, std::min<int64_t>(s->Ws, ctx->option(OPT_SPARSE_CHUNKS, 1)))));
@@ -1498,13 +1519,14 @@ bool sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     auto kern = sun == 2 ? sparse_tile_kernel<2> : sun == 4 ? sparse_tile_kernel<4> : sparse_tile_kernel<3>;
     const bool timed = ctx->option(OPT_TIME_SPARSE, 0) != 0 && !ctx->capturing;
     if (timed) GD_HIP(hipEventRecord(ctx->ev_sp0, st));
-    const int64_t grid = nt * nchunks;
+    const bool xmap = ctx->option(OPT_SPARSE_XCD, 0) != 0;
+    const int64_t grid = xmap ? ceil_div(nchunks, 8) * 8 * nt : nt * nchunks;
     GD_REQUIRE(grid < (int64_t(1) << 31), "sparse grid too large");
     kern<<<(unsigned)grid, SNT, 0, st>>>(s->sp_off.as<int64_t>(), s->sp_ent.as<ulonglong2>(), s->sp_nc.as<int32_t>(),
                                          s->sp_U, s->Ws, sc.tiles.as<int2>(), sc.bounds.as<int32_t>(), nchunks, r0, r1,
                                          c0, c1, upper ? 1 : 0, d_I, ldI, sc.use_part ? sc.part.as<int32_t>() : nullptr,
                                          s->Wd, s->nsets, s->dbits.as<unsigned long long>(), s->sp_fold_slabs,
-                                         group_part(s));
+                                         group_part(s), xmap ? 1 : 0, (int)nt);
     GD_HIP(hipGetLastError());
     if (timed) {
         GD_HIP(hipEventRecord(ctx->ev_sp1, st));

@@ -2,11 +2,11 @@
 # rocprofv3 evidence for one bench line: kernel trace + stats of the bench
 # command, then FETCH_SIZE and WRITE_SIZE in separate PMC passes (kernel
 # trace only), then the per-launch HBM bytes of the dominant kernel
-# (scripts/pmc_json.py). Usage: profile.sh CONFIG N KERNEL OUTDIR
+# (scripts/pmc_json.py). Usage: profile.sh CONFIG N KERNEL OUTDIR [EXTRA BENCH ARGS]
 set -o pipefail
 export TMPDIR=/tmp
-CFG=$1; N=$2; KERN=$3; OUT=$4
-ARGS="--config $CFG --steps 20 --warmup 3 --no-cpu-baseline"
+CFG=$1; N=$2; KERN=$3; OUT=$4; EXTRA=${5:-}
+ARGS="--config $CFG --steps 20 --warmup 3 --no-cpu-baseline $EXTRA"
 mkdir -p $OUT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_trace -o run -- \
     python3 bench.py $ARGS > $OUT/prof_trace.json 2> $OUT/prof_trace.err &&

@@ -747,6 +747,11 @@ SPARSE_MODES = {
     # the pack without chunk summaries: the bitset build sorts every code for its dictionary
     "pack_nosummary": {"pack_summary": 0},
     "many_chunks": {"sparse_zmax": 100000, "sparse_chunks": 37},
+    # chunk c of every tile on XCD c mod 8 (option sparse_xcd), with a chunk
+    # count that leaves empty workgroups in the last group of 8, and atomics
+    "xcd": {"sparse_zmax": 100000, "sparse_xcd": 1, "sparse_chunks": 13},
+    "xcd_default": {"sparse_xcd": 1},
+    "xcd_atomic": {"sparse_zmax": 100000, "sparse_xcd": 1, "sparse_part_budget": 0, "sparse_chunks": 6},
     # a dense-only dictionary: the substitution kmers two or more sets share
     # are dense too, and their words are counted from the set bits
     # (positive-sparse) beside the complement words
