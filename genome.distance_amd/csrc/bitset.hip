@@ -1719,11 +1719,13 @@ double bitset_block_cost_s(const gdist_sets* s, int64_t r0, int64_t r1, int64_t 
                 const int64_t cmax = std::min(c1, (B + 1) * BT) - 1;
                 if (!(upper && cmax <= rmin)) sp_tiles += 1.0;
             }
-    // the rare tier's pairs ride in the sparse chunk reduce (sparse.hip,
-    // rare_pair_table) when the lists are few: no rare kernel then
-    const bool rare_in_reduce = s->sparse && s->n_rare > 0 && s->rare_records <= (int64_t(1) << 25);
+    // the rare tier's pairs are recounted by the sparse tile launch's rare
+    // rows (sparse.hip rare_slab_plan) when the tier is small and its lists
+    // short; priced as the list-major kernel beside the tiles
+    const bool rare_in_reduce = s->sparse && s->n_rare > 0 && s->rare_max_list <= kLongList &&
+                                (double)s->rare_records + (double)s->rare_incs <= double(int64_t(1) << 26);
     return (off + kDiagTileShare * diag) * (double)(BT * BT) * tW / kDenseWordPairsPerS +
-           (rare_in_reduce ? 0.0 : rc.cost()) +
+           (rare_in_reduce ? rc.list_s * kRareOverlapExposed : rc.cost()) +
            sparse_block_cost_s(s, tot > 0 ? std::min(1.0, pairs / tot) : 1.0, sp_tiles);
 }
 

@@ -695,6 +695,8 @@ static int resolve_method(gdist_ctx* ctx, gdist_sets* s, int method, double pair
         m = s->bits.p ? GDIST_METHOD_BITSET : GDIST_METHOD_SORTED;
     }
     GD_REQUIRE(m == GDIST_METHOD_BITSET || s->has_codes, "this collection holds bitsets only");
+    // a shard consumed by the code all-gather holds neither codes nor bitsets
+    GD_REQUIRE(s->has_codes || s->bits.p, "the collection holds no codes (consumed by an all-gather)");
     if (m == GDIST_METHOD_BITSET && !s->bits.p) build_bitsets(ctx, s, 0);
     if (m == GDIST_METHOD_SORTED && !s->segoff.p) build_segments(ctx, s);
     return m;
@@ -1309,8 +1311,21 @@ int gdist_sets_exchange_plan(gdist_ctx* ctx, const gdist_sets* local, int method
         // slot, then the compaction's staging); one rank adopts its own buffer
         const double b_codes = R == 1 ? mxt * es : ((double)R + 1.0) * mxt * es;
         // bitsets: the local codes + the gathered summaries (12 B per
-        // distinct code) + the merge's workspace (~2x them)
-        const double b_bits = local->kind == GDIST_SKETCH ? INFINITY : mxt * 8.0 + 3.0 * (double)R * mxn * 12.0;
+        // distinct code) + the merge's workspace (~2x them) + the bitsets the
+        // exchange allocates: every set's words (N_total x W) and the R x
+        // (largest shard) x W gather buffer, W bounded by the distinct codes
+        // (min(R x largest summary, sum of summaries) / 64)
+        double n_total = 0, mxs = 0, sum_all = 0;
+        for (int r = 0; r < R; r++) {
+            n_total += (double)h[3 * r];
+            mxs = std::max(mxs, (double)h[3 * r]);
+            sum_all += (double)h[3 * r + 2];
+        }
+        const double w_bound = std::ceil(std::min((double)R * mxn, sum_all) / 64.0);
+        const double b_bits = local->kind == GDIST_SKETCH
+                                  ? INFINITY
+                                  : mxt * 8.0 + 3.0 * (double)R * mxn * 12.0 +
+                                        (n_total + (double)R * mxs) * w_bound * 8.0;
         hipDeviceProp_t prop;
         GD_HIP(hipGetDeviceProperties(&prop, ctx->device));
         const double budget = ctx->has_option(OPT_EXCHANGE_BUDGET) ? (double)ctx->option(OPT_EXCHANGE_BUDGET, 0)

@@ -127,9 +127,12 @@ struct SparseScratch {
     bool ready = false;
     DevBuf tiles, part;   // tile list, per-chunk counters
     DevBuf bounds;        // int32 [nchunks + 1]: first sparse word of each chunk (cost-balanced)
-    // the rare tier's pairs of the region, added by the chunk reduce (no rare
-    // kernel): keys tile << 14 | counter slot, weights, CSR over (tile, 512-slot group)
-    DevBuf rp_key, rp_w, rp_off;
+    // the rare tier's pairs are recounted every step by the sparse tile
+    // launch's leading workgroups into a per-tile slab the chunk reduce adds
+    // (sparse.hip rare_slab_row): the region's (row block, column block) ->
+    // tile map and the slab (uint32 [ntiles][128 x 128], written each step)
+    DevBuf rare_tile, rare_slab;
+    int64_t rare_ab0 = 0, rare_nbc = 0;
     bool rare_in = false;
     int nchunks = 0;
     bool use_part = false;   // chunks store partials (else flush with atomics)

@@ -503,7 +503,7 @@ constexpr size_t sketch_meta_bytes() { return (size_t)(R + C) * (sizeof(int64_t)
 // ring kernel LDS: RS ring rows + the mirror row, 64 dwords each
 inline size_t sketch_ring_lds(int rs) { return (size_t)(rs + 1) * kSkLanes * 4; }
 
-void launch_sketch_ring(hipStream_t st, const gdist_sets* sk, int width, int rs, int kmax, int64_t r0, int64_t r1,
+int launch_sketch_ring(hipStream_t st, const gdist_sets* sk, int width, int rs, int kmax, int64_t r0, int64_t r1,
                         int64_t c0, int64_t c1, bool upper, int jac, int en, int32_t* d_common, double* d_D,
                         int64_t ld, bool fallback) {
     const size_t lds = sketch_ring_lds(rs);
@@ -519,15 +519,18 @@ void launch_sketch_ring(hipStream_t st, const gdist_sets* sk, int width, int rs,
     const int64_t per = (int64_t(1) << 31) / threads;     // a dispatch holds < 2^32 work-items
     GD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&sketch_ring_kernel),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    for (int64_t t0 = 0; t0 < grid; t0 += per)
+    int launches = 0;
+    for (int64_t t0 = 0; t0 < grid; t0 += per, launches++)
         sketch_ring_kernel<<<(unsigned)std::min(per, grid - t0), threads, lds, st>>>(
             sk->codes.as<int32_t>(), sk->off.as<int64_t>(), width, rs, kmax, r0, r1, c0, c1, t0, tc, upper, jac, en,
             d_common, d_D, ld, fallback ? 1 : 0, tri ? 1 : 0);
     GD_HIP(hipGetLastError());
+    return launches;
 }
 
+// launches made (0: the tile does not fit LDS and no global fallback was asked)
 template <int R, int C>
-bool launch_sketch_tiles(hipStream_t st, const gdist_sets* sk, int width, int64_t r0, int64_t r1, int64_t c0,
+int launch_sketch_tiles(hipStream_t st, const gdist_sets* sk, int width, int64_t r0, int64_t r1, int64_t c0,
                          int64_t c1, bool upper, int jac, int en, int32_t* d_common, double* d_D, int64_t ld,
                          bool force_global, int64_t kw_opt, bool v2_opt) {
     // option sketch_k selects the merge window (1, 2, 4, 6; A/B measurements)
@@ -536,9 +539,10 @@ bool launch_sketch_tiles(hipStream_t st, const gdist_sets* sk, int width, int64_
     const int sw = v2 ? ((width + 2) | 1) : sketch_stride(width);
     const size_t lds = (size_t)(R + C) * sw * 4 + LDS_SK_SLACK;
     const bool use_lds = !force_global && lds + sketch_meta_bytes<R, C>() <= (size_t)LDS_SK_MAX;
-    if (!use_lds && !force_global) return false;
+    if (!use_lds && !force_global) return 0;
     const int tr = (int)ceil_div(r1 - r0, R), tc = (int)ceil_div(c1 - c0, C);
     const int64_t grid = (int64_t)tr * tc;
+    const int launches = (int)ceil_div(grid, (int64_t(1) << 31) / (R * C));
     // a dispatch holds < 2^32 work-items: launches of at most 2^31 threads
     const int threads = R * C;
     const int64_t per = (int64_t(1) << 31) / threads;
@@ -570,7 +574,7 @@ bool launch_sketch_tiles(hipStream_t st, const gdist_sets* sk, int width, int64_
         }
     }
     GD_HIP(hipGetLastError());
-    return true;
+    return launches;
 }
 
 }  // namespace
@@ -685,19 +689,27 @@ void sketch_matrix(gdist_ctx* ctx, const gdist_sets* sk, int64_t r0, int64_t r1,
     // sketch_ring its slots per sketch
     const bool ring = ctx->option(OPT_SKETCH_PHASE, 1) != 0 && !only16 && kw == 2;
     GD_HIP(hipEventRecord(ctx->ev_k0, st));
+    int launches = 0;
     if (ring) {
         // default 160 steps per phase, 256 slots: 257 rows of 256 B = 66 KB,
         // two workgroups per CU
         const int kmax = (int)std::max<int64_t>(2, std::min<int64_t>(ctx->option(OPT_SKETCH_CAP, 160), 1 << 20));
         const int rs = (int)std::max<int64_t>(16, std::min<int64_t>(ctx->option(OPT_SKETCH_RING, 256), 1 << 20));
-        launch_sketch_ring(st, sk, width, rs, std::min(kmax, rs - 1), r0, r1, c0, c1, upper, jac, en, d_common, d_D,
-                           ld, ctx->option(OPT_SKETCH_WAIT, 0) == 0);
-    } else if (only16 || !launch_sketch_tiles<16, 24>(st, sk, width, r0, r1, c0, c1, upper, jac, en, d_common, d_D, ld,
-                                               false, kw, v2))
-        if (!launch_sketch_tiles<16, 16>(st, sk, width, r0, r1, c0, c1, upper, jac, en, d_common, d_D, ld, false, kw, v2))
-            launch_sketch_tiles<16, 16>(st, sk, width, r0, r1, c0, c1, upper, jac, en, d_common, d_D, ld, true, kw, v2);
+        launches = launch_sketch_ring(st, sk, width, rs, std::min(kmax, rs - 1), r0, r1, c0, c1, upper, jac, en,
+                                      d_common, d_D, ld, ctx->option(OPT_SKETCH_WAIT, 0) == 0);
+    } else {
+        if (!only16)
+            launches = launch_sketch_tiles<16, 24>(st, sk, width, r0, r1, c0, c1, upper, jac, en, d_common, d_D, ld,
+                                                   false, kw, v2);
+        if (!launches)
+            launches = launch_sketch_tiles<16, 16>(st, sk, width, r0, r1, c0, c1, upper, jac, en, d_common, d_D, ld,
+                                                   false, kw, v2);
+        if (!launches)
+            launches = launch_sketch_tiles<16, 16>(st, sk, width, r0, r1, c0, c1, upper, jac, en, d_common, d_D, ld,
+                                                   true, kw, v2);
+    }
     GD_HIP(hipEventRecord(ctx->ev_k1, st));
-    ctx->last.launches = 1;
+    ctx->last.launches = launches;
 }
 
 }  // namespace gdist

@@ -40,6 +40,7 @@ inline int grid_for(int64_t n, int block = 256, int64_t cap = 256 * 32) {
 }
 
 constexpr int SB = 128;                  // sets per block of the sparse entry index (tile edge)
+constexpr int SNT = 512;                 // threads per workgroup (4 per CU, LDS-limited: 8 waves per SIMD)
 constexpr int kBucketShift = 10;         // sparse words per complement-bit bucket: 1024
 
 // ---- locus order -------------------------------------------------------
@@ -451,6 +452,76 @@ __global__ void sparse_records_kernel(const unsigned long long* __restrict__ wor
     }
 }
 
+// the rare tier's set -> list CSR (bitset.hip build_postings), walked in every step
+struct RareRows {
+    const int64_t* soff = nullptr;        // [N + 1] (null: no walk)
+    const uint64_t* sent = nullptr;       // (list start << 24 | list length) per (set, list) record
+    const uint32_t* sw = nullptr;         // the list's weight
+    const uint16_t* sskip = nullptr;      // 1 + the set's position in its list (0: none)
+    const uint32_t* psets = nullptr;      // list members, ascending
+};
+inline RareRows rare_rows_of(const gdist_sets* s) {
+    return RareRows{s->srare_off.as<int64_t>(), s->srare_ent.as<uint64_t>(), s->srare_w.as<uint32_t>(),
+                    s->srare_skip.as<uint16_t>(), s->post_sets.as<uint32_t>()};
+}
+
+// The rare tier's pairs, recounted in every step by workgroups of the tile
+// launch itself (the first nrare workgroups; no per-pair state survives
+// between steps, no extra launch, no second stream): one workgroup per (row
+// i, chunk of 8192 columns) walks the row's (set, list) records, adds each
+// list member in the chunk (upper triangle: from the row's own position on,
+// members after i) into LDS counters, and STORES the row into every tile
+// slab of the region's tiles it meets (kRareSlab layout = cnt_index, 0 where
+// no rare kmer is shared), so the chunk reduce adds them coalesced. These
+// latency-bound walks run beside the tile workgroups of the same launch.
+constexpr int kRareChunkCols = SB * SB / 2;       // the tile kernel's 32 KiB of LDS counters, one per column
+struct RareSlab {
+    RareRows rr;
+    int nrare = 0;                        // leading workgroups doing rare rows (0: none)
+    int nch = 1;                          // column chunks per row
+    uint32_t* slab = nullptr;             // uint32 [ntiles][128 x 128]
+    const int32_t* tile_of = nullptr;     // [row blocks of the region][column blocks]: tile index or -1
+    int64_t ab0 = 0, nbc = 0;             // first row block of the region, column blocks
+};
+__device__ __forceinline__ void rare_slab_row(const RareSlab& rs, int unit, int64_t r0, int64_t c0, int64_t c1,
+                                              int upper, uint32_t* __restrict__ cnt) {
+    const int64_t i = r0 + unit / rs.nch;
+    const int64_t cb = c0 + (int64_t)(unit % rs.nch) * kRareChunkCols;
+    const int64_t ce = cb + kRareChunkCols < c1 ? cb + kRareChunkCols : c1;
+    const int n = (int)(ce - cb);
+    for (int t = threadIdx.x; t < n; t += SNT) cnt[t] = 0;
+    __syncthreads();
+    const int64_t xb = rs.rr.soff[i], xe = rs.rr.soff[i + 1];
+    for (int64_t x = xb + threadIdx.x; x < xe; x += SNT) {
+        const uint64_t ent = rs.rr.sent[x];
+        const uint32_t w = rs.rr.sw[x];
+        const int64_t b0 = (int64_t)(ent >> 24), e = b0 + (int64_t)(ent & 0xFFFFFFu);
+        const int sk = upper ? (int)rs.rr.sskip[x] : 0;
+        for (int64_t y = b0 + sk; y < e; y++) {
+            const int64_t t = rs.rr.psets[y];
+            if (t >= ce) break;                                     // members ascend
+            if (t < cb || t == i || (upper && t < i)) continue;     // (skip 0: from the list's start)
+            atomicAdd(&cnt[t - cb], w);
+        }
+    }
+    __syncthreads();
+    // the row's slots of every tile it meets: 128 columns per column block
+    const int64_t A = i / SB;
+    const int a = (int)(i - A * SB);
+    const int64_t B0 = cb / SB, B1 = (ce - 1) / SB;
+    for (int64_t e = threadIdx.x; e < (B1 - B0 + 1) * SB; e += SNT) {
+        const int64_t B = B0 + e / SB;
+        const int b = (int)(e % SB);
+        const int32_t tl = rs.tile_of[(A - rs.ab0) * rs.nbc + B];
+        if (tl < 0) continue;
+        const int64_t j = B * SB + b;
+        // a block straddling two chunks gets each column from its own chunk;
+        // slots outside the region are never read by the reduce
+        if (j < cb || j >= ce) continue;
+        rs.slab[(int64_t)tl * (SB * SB) + cnt_index(a, b)] = cnt[j - cb];
+    }
+}
+
 // ---- the sparse tile kernel ---------------------------------------------
 // One workgroup per (128 x 128 tile of absolute set blocks (A, B), chunk of
 // the sparse words). Each wave takes 64 sparse words at a time: lane l loads
@@ -478,7 +549,6 @@ __global__ void sparse_records_kernel(const unsigned long long* __restrict__ wor
 //   * the counter add is unconditional (a zero product adds 0), so no slot
 //     waits on another's branch; idle slots read the zero sentinel record
 //     past the last entry instead of being masked.
-constexpr int SNT = 512;                 // threads per workgroup (4 per CU, LDS-limited: 8 waves per SIMD)
 // Counters are 16-bit, two to an LDS dword: a chunk holds at most kChunkWords
 // sparse words, so a pair's count in one chunk is at most 64 x 1023 < 2^16
 // and a packed ds_add_u32 never carries into the neighbour (32 KiB per tile)
@@ -630,11 +700,17 @@ __global__ __launch_bounds__(SNT, 8) void sparse_tile_kernel(
     const int64_t* __restrict__ off, const ulonglong2* __restrict__ ent, const int32_t* __restrict__ nc, int64_t Us,
     int64_t Ws, const int2* __restrict__ tiles, const int32_t* __restrict__ cbnd, int nchunks, int64_t r0, int64_t r1,
     int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I, int64_t ldI, int32_t* __restrict__ part, int64_t Wdp,
-    int64_t N, const unsigned long long* __restrict__ slab_bits, int slabs, GroupPart gp, int xmap, int ntiles) {
+    int64_t N, const unsigned long long* __restrict__ slab_bits, int slabs, GroupPart gp, int xmap, int ntiles,
+    RareSlab rs) {
     // gp: the group tier's part of every pair, added with the constant part
     // slab_bits / slabs: the in-kernel fold's dense words (set-major [N][Wdp])
     __shared__ uint32_t cnt[SB * SB / 2];                  // 32 KiB, 16-bit counters (cnt_index layout)
     __shared__ int4 rec[SNW][64];                          // 8 KiB: the batch's walk records
+    if ((int)blockIdx.x < rs.nrare) {                      // a rare row of this step (above)
+        rare_slab_row(rs, (int)blockIdx.x, r0, c0, c1, upper, cnt);
+        return;
+    }
+    const unsigned bid = blockIdx.x - (unsigned)rs.nrare;
     int tile, ch;
     if (xmap) {
         // option sparse_xcd: workgroup b = 8 (t + ntiles g) + x runs chunk
@@ -642,13 +718,13 @@ __global__ __launch_bounds__(SNT, 8) void sparse_tile_kernel(
         // so chunk c of every tile runs on XCD c mod 8, the tiles of one
         // chunk back to back: that XCD's L2 serves the chunk's records
         // (~0.85 MB on C2) to all the tiles reading them
-        const int x = (int)(blockIdx.x & 7), k = (int)(blockIdx.x >> 3);
+        const int x = (int)(bid & 7), k = (int)(bid >> 3);
         tile = k % ntiles;
         ch = 8 * (k / ntiles) + x;
         if (ch >= nchunks) return;
     } else {
-        tile = blockIdx.x / nchunks;
-        ch = blockIdx.x % nchunks;
+        tile = (int)(bid / (unsigned)nchunks);
+        ch = (int)(bid % (unsigned)nchunks);
     }
     const int64_t A = tiles[tile].x, B = tiles[tile].y;
     const int rlo = (int)(r0 - A * SB > 0 ? r0 - A * SB : 0);
@@ -764,9 +840,7 @@ __global__ __launch_bounds__(256) void sparse_reduce_kernel(const int32_t* __res
                                                             const int32_t* __restrict__ nc, int64_t Us, int64_t r0,
                                                             int64_t r1, int64_t c0, int64_t c1, int upper,
                                                             int32_t* __restrict__ I, int64_t ldI,
-                                                            const uint32_t* __restrict__ rp_key,
-                                                            const uint32_t* __restrict__ rp_w,
-                                                            const int64_t* __restrict__ rp_off,
+                                                            const uint32_t* __restrict__ rslab,
                                                             double* __restrict__ D, int64_t ldD,
                                                             const int64_t* __restrict__ soff, int empty_nan,
                                                             GroupPart gp) {
@@ -806,19 +880,14 @@ __global__ __launch_bounds__(256) void sparse_reduce_kernel(const int32_t* __res
 #pragma unroll
     for (int k = 0; k < kReduceCnt; k++) sum[wv][k][lane] = acc[k];
     __syncthreads();
-    if (rp_off) {                            // the rare tier's pairs of this group's 512 slots
-        const int64_t grp = (int64_t)tile * per_tile + (blockIdx.x % per_tile);
-        for (int64_t p = rp_off[grp] + threadIdx.x; p < rp_off[grp + 1]; p += 256) {
-            const int c = (int)(rp_key[p] & 511);
-            atomicAdd(&sum[0][c % kReduceCnt][c / kReduceCnt], rp_w[p]);
-        }
-        __syncthreads();
-    }
     // 512 counters per workgroup: each thread finalizes two
     for (int e = threadIdx.x; e < kReduceCnt * kReduceGroups; e += 256) {
         const int gl = e / kReduceCnt, k = e % kReduceCnt;               // consecutive threads: consecutive counters
-        const uint32_t tot = sum[0][k][gl] + sum[1][k][gl] + sum[2][k][gl] + sum[3][k][gl];
         const int t = ((blockIdx.x % per_tile) * kReduceGroups + gl) * kReduceCnt + k;   // cnt_index layout
+        // + the rare tier's pairs of this step (the tile launch's rare rows
+        // wrote every slot of the region's rows: same layout, coalesced)
+        const uint32_t tot = sum[0][k][gl] + sum[1][k][gl] + sum[2][k][gl] + sum[3][k][gl] +
+                             (rslab ? rslab[(int64_t)tile * (SB * SB) + t] : 0u);
         int a, b;
         cnt_pair(t, a, b);
         const int64_t i = (int64_t)tiles[tile].x * SB + a, j = (int64_t)tiles[tile].y * SB + b;
@@ -1218,171 +1287,29 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
     tr.mark("sparse: entries + dense words");
 }
 
-// The rare tier's pairs of a region, for the chunk reduce (sparse_plan): every
-// posting list adds its weight to each of its pairs in the region (the
-// semantics of rare_pairs_kernel, bitset.hip). Expanded once per region plan
-// on the device: one thread per pair of every list (list found by binary
-// search over the lists' pair offsets, the pair by the triangular inverse),
-// keyed (tile << 14 | counter slot in the cnt_index layout) << 32 | weight,
-// radix-sorted by key, equal keys summed, and bucketed by (tile, 512-slot
-// reduce group). Pairs outside the region get the sentinel key and sort last.
-// Past kRarePairsMax pairs over all lists the rare kernel keeps them.
-constexpr int64_t kRarePairsMax = int64_t(1) << 25;
-constexpr uint64_t kNoPair = ~0ull;
+// The rare tier's pairs of a region are recounted in every step by the
+// leading workgroups of the sparse tile launch (rare_slab_row above) into a
+// per-tile slab the chunk reduce adds. The plan keeps only geometry: the
+// region's (row block, column block) -> tile map and the slab's allocation.
+// Taken when the tier is small and its lists short (a row's thread walks a
+// list serially); otherwise the rare kernels of bitset_matrix count them.
+constexpr double kRareSlabWorkMax = double(int64_t(1) << 26);
 
-__global__ void rare_list_pairs_kernel(const int64_t* __restrict__ poff, int64_t nl, int mirror,
-                                       int64_t* __restrict__ cnt) {
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; l < nl; l += stride) {
-        const int64_t m = poff[l + 1] - poff[l];
-        cnt[l] = m * (m - 1) / 2 * (mirror ? 2 : 1);
-    }
-}
-
-__global__ void rare_pair_emit_kernel(const int64_t* __restrict__ poff, const uint32_t* __restrict__ psets,
-                                      const uint32_t* __restrict__ pw, int64_t nl, const int64_t* __restrict__ P,
-                                      int64_t total, int mirror, int64_t r0, int64_t r1, int64_t c0, int64_t c1,
-                                      const int32_t* __restrict__ tile_of, int64_t nb, uint64_t* __restrict__ out,
-                                      int* __restrict__ missing) {
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += stride) {
-        int64_t lo = 0, hi = nl;                           // the list: last l with P[l] <= q
-        while (hi - lo > 1) {
-            const int64_t mid = (lo + hi) >> 1;
-            if (P[mid] <= q) lo = mid; else hi = mid;
-        }
-        const int64_t l = lo;
-        const int64_t m = poff[l + 1] - poff[l];
-        int64_t t = q - P[l];
-        const int64_t half = m * (m - 1) / 2;
-        const bool flip = mirror && t >= half;
-        if (flip) t -= half;
-        // t -> (x, y), x < y, t = y (y - 1) / 2 + x
-        int64_t y = (int64_t)((1.0 + sqrt(1.0 + 8.0 * (double)t)) * 0.5);
-        while (y * (y - 1) / 2 > t) y--;
-        while ((y + 1) * y / 2 <= t) y++;
-        const int64_t x = t - y * (y - 1) / 2;
-        int64_t i = psets[poff[l] + x], j = psets[poff[l] + y];   // i < j (lists ascend)
-        if (flip) { const int64_t tmp = i; i = j; j = tmp; }
-        uint64_t key = kNoPair;
-        if (i >= r0 && i < r1 && j >= c0 && j < c1) {
-            const int32_t tl = tile_of[(i / SB) * nb + (j / SB)];
-            if (tl >= 0)
-                key = ((uint64_t)(((uint32_t)tl << 14) | (uint32_t)cnt_index((int)(i % SB), (int)(j % SB))) << 32) |
-                      (uint64_t)pw[l];
-            else
-                *missing = 1;                              // a pair of the region outside the plan's tiles
-        }
-        out[q] = key;
-    }
-}
-
-// run heads of the sorted keys (high 32 bits), sentinels excluded
-__global__ void rare_pair_heads_kernel(const uint64_t* __restrict__ k, int64_t n, int32_t* __restrict__ flag) {
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-        flag[i] = k[i] != kNoPair && (i == 0 || (k[i] >> 32) != (k[i - 1] >> 32));
-}
-
-__global__ void rare_pair_runs_kernel(const uint64_t* __restrict__ k, int64_t n, const int32_t* __restrict__ flag,
-                                      const int64_t* __restrict__ pos, uint32_t* __restrict__ ukey,
-                                      uint32_t* __restrict__ uw) {
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        if (!flag[i]) continue;
-        const uint32_t key = (uint32_t)(k[i] >> 32);
-        uint32_t w = 0;
-        for (int64_t e = i; e < n && k[e] != kNoPair && (uint32_t)(k[e] >> 32) == key; e++) w += (uint32_t)k[e];
-        ukey[pos[i]] = key;
-        uw[pos[i]] = w;
-    }
-}
-
-// goff[g] = first unique key of group g (key >> 9 >= g)
-__global__ void rare_group_offsets_kernel(const uint32_t* __restrict__ ukey, int64_t nu, int64_t ngroups,
-                                          int64_t* __restrict__ goff) {
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g <= ngroups; g += stride) {
-        int64_t lo = 0, hi = nu;
-        while (lo < hi) {
-            const int64_t mid = (lo + hi) >> 1;
-            if ((int64_t)(ukey[mid] >> 9) < g) lo = mid + 1; else hi = mid;
-        }
-        goff[g] = lo;
-    }
-}
-
-static void rare_pair_table(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1,
-                            bool upper, const std::vector<int2>& tiles, SparseScratch& sc) {
-    // on the context's main stream, whatever stream the plan is built for:
-    // the radix sort and the scans run there; the table is complete (stream
-    // synchronised) before any launch reads it
+static void rare_slab_plan(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1,
+                           const std::vector<int2>& tiles, SparseScratch& sc) {
     hipStream_t st = ctx->stream;
     sc.rare_in = false;
     if (s->n_rare == 0) return;
-    if (ctx->option(OPT_SPARSE_RARE, 1) == 0 || s->rare_records > kRarePairsMax) return;
-    GD_REQUIRE(tiles.size() < (size_t(1) << 18), "too many tiles for the rare pair keys");
-    const int64_t nl = s->n_rare;
-    DevBuf P((nl + 1) * 8, st);
-    {
-        DevBuf cnt((nl + 1) * 8, st);
-        GD_HIP(hipMemsetAsync(cnt.as<int64_t>() + nl, 0, 8, st));
-        rare_list_pairs_kernel<<<grid_for(nl), 256, 0, st>>>(s->post_off.as<int64_t>(), nl, upper ? 0 : 1,
-                                                             cnt.as<int64_t>());
-        GD_HIP(hipGetLastError());
-        exclusive_scan_i64(ctx, cnt.as<int64_t>(), P.as<int64_t>(), (size_t)(nl + 1));
-    }
-    int64_t total = 0;
-    d2h(&total, P.as<int64_t>() + nl, 8, st);
-    if (total > kRarePairsMax) return;
-    const int64_t nb = ceil_div(s->nsets, SB);
-    std::vector<int32_t> tile_of((size_t)nb * nb, -1);
-    for (size_t t = 0; t < tiles.size(); t++) tile_of[(size_t)tiles[t].x * nb + tiles[t].y] = (int32_t)t;
-    DevBuf dto(tile_of.size() * 4, st);
-    h2d(dto.p, tile_of.data(), tile_of.size() * 4, st);
-    DevBuf kA(total * 8 + 8, st), kB(total * 8 + 8, st), miss(4, st);
-    GD_HIP(hipMemsetAsync(miss.p, 0, 4, st));
-    if (total)
-        rare_pair_emit_kernel<<<grid_for(total), 256, 0, st>>>(
-            s->post_off.as<int64_t>(), s->post_sets.as<uint32_t>(), s->post_w.as<uint32_t>(), nl, P.as<int64_t>(),
-            total, upper ? 0 : 1, r0, r1, c0, c1, dto.as<int32_t>(), nb, kA.as<uint64_t>(), miss.as<int>());
-    GD_HIP(hipGetLastError());
-    int hmiss = 0;
-    d2h(&hmiss, miss.p, 4, st);
-    GD_REQUIRE(!hmiss, "rare pair outside the sparse plan's tiles");
-    uint64_t* keys = kA.as<uint64_t>(); uint64_t* alt = kB.as<uint64_t>();
-    // sorted over all their bits (the low half, the weight, only orders equal
-    // keys): rocPRIM's radix sort with a non-zero begin_bit left these keys
-    // unsorted on gfx950 (round 3; every sort here starts at bit 0). The
-    // sentinel (all ones) sorts last.
-    int tbits = 1;
-    while ((int64_t(1) << tbits) < (int64_t)tiles.size()) tbits++;
-    sort_keys_u64(ctx, keys, alt, (size_t)total, 0, std::min(64, 32 + 14 + tbits + 1));
-    int64_t nu = 0;
-    DevBuf flag(total * 4 + 4, st), pos(total * 8 + 8, st);
-    if (total) {
-        rare_pair_heads_kernel<<<grid_for(total), 256, 0, st>>>(keys, total, flag.as<int32_t>());
-        GD_HIP(hipGetLastError());
-        exclusive_scan_i32_to_i64(ctx, flag.as<int32_t>(), pos.as<int64_t>(), (size_t)total);
-        int64_t last = 0;
-        int32_t lf = 0;
-        d2h(&last, pos.as<int64_t>() + total - 1, 8, st);
-        d2h(&lf, flag.as<int32_t>() + total - 1, 4, st);
-        nu = last + lf;
-    }
-    sc.rp_key.alloc(nu * 4 + 4, st);
-    sc.rp_w.alloc(nu * 4 + 4, st);
-    if (nu) {
-        rare_pair_runs_kernel<<<grid_for(total), 256, 0, st>>>(keys, total, flag.as<int32_t>(), pos.as<int64_t>(),
-                                                               sc.rp_key.as<uint32_t>(), sc.rp_w.as<uint32_t>());
-        GD_HIP(hipGetLastError());
-    }
-    const int64_t ngroups = (int64_t)tiles.size() * (SB * SB / 512);
-    sc.rp_off.alloc((ngroups + 1) * 8, st);
-    rare_group_offsets_kernel<<<grid_for(ngroups + 1), 256, 0, st>>>(sc.rp_key.as<uint32_t>(), nu, ngroups,
-                                                                      sc.rp_off.as<int64_t>());
-    GD_HIP(hipGetLastError());
-    GD_HIP(hipStreamSynchronize(st));
+    if (ctx->option(OPT_SPARSE_RARE, 1) == 0 || tiles.empty()) return;
+    if ((double)s->rare_records + (double)s->rare_incs > kRareSlabWorkMax || s->rare_max_list > kLongList) return;
+    const int64_t nbc = ceil_div(s->nsets, SB), ab0 = r0 / SB, nrb = (r1 - 1) / SB - ab0 + 1;
+    std::vector<int32_t> tile_of((size_t)(nrb * nbc), -1);
+    for (size_t t = 0; t < tiles.size(); t++) tile_of[(size_t)((tiles[t].x - ab0) * nbc + tiles[t].y)] = (int32_t)t;
+    sc.rare_tile.alloc(tile_of.size() * 4, st);
+    h2d(sc.rare_tile.p, tile_of.data(), tile_of.size() * 4, st);
+    sc.rare_slab.alloc(tiles.size() * (size_t)(SB * SB) * 4, st);
+    sc.rare_ab0 = ab0;
+    sc.rare_nbc = nbc;
     sc.rare_in = true;
 }
 
@@ -1485,7 +1412,7 @@ void sparse_plan(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, in
                     sc.use_part ? "partials" : "atomic flush", (long long)s->sp_pos_words,
                     (long long)s->Ws);
         GD_REQUIRE(sc.ntiles * sc.nchunks < (int64_t(1) << 31), "sparse grid too large");
-        if (sc.use_part) rare_pair_table(ctx, s, r0, r1, c0, c1, upper, tiles, sc);
+        if (sc.use_part) rare_slab_plan(ctx, s, r0, r1, tiles, sc);
         sc.ready = true;
     }
 }
@@ -1517,16 +1444,30 @@ bool sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     const int sun = (int)ctx->option(OPT_SPARSE_SUN, 3);
     GD_REQUIRE(sun >= 2 && sun <= 4, "sparse_sun: 2, 3 or 4");
     auto kern = sun == 2 ? sparse_tile_kernel<2> : sun == 4 ? sparse_tile_kernel<4> : sparse_tile_kernel<3>;
+    // the rare tier's pairs of this step: the launch's leading workgroups
+    const bool rare = sc.use_part && sc.rare_in;
     const bool timed = ctx->option(OPT_TIME_SPARSE, 0) != 0 && !ctx->capturing;
     if (timed) GD_HIP(hipEventRecord(ctx->ev_sp0, st));
     const bool xmap = ctx->option(OPT_SPARSE_XCD, 0) != 0;
-    const int64_t grid = xmap ? ceil_div(nchunks, 8) * 8 * nt : nt * nchunks;
+    RareSlab rs;
+    if (rare) {
+        rs.rr = rare_rows_of(s);
+        rs.nch = (int)ceil_div(c1 - c0, kRareChunkCols);
+        const int64_t nrare = (r1 - r0) * rs.nch;
+        GD_REQUIRE(nrare < (int64_t(1) << 30), "too many rare rows");
+        rs.nrare = (int)nrare;
+        rs.slab = sc.rare_slab.as<uint32_t>();
+        rs.tile_of = sc.rare_tile.as<int32_t>();
+        rs.ab0 = sc.rare_ab0;
+        rs.nbc = sc.rare_nbc;
+    }
+    const int64_t grid = (xmap ? ceil_div(nchunks, 8) * 8 * nt : nt * nchunks) + rs.nrare;
     GD_REQUIRE(grid < (int64_t(1) << 31), "sparse grid too large");
     kern<<<(unsigned)grid, SNT, 0, st>>>(s->sp_off.as<int64_t>(), s->sp_ent.as<ulonglong2>(), s->sp_nc.as<int32_t>(),
                                          s->sp_U, s->Ws, sc.tiles.as<int2>(), sc.bounds.as<int32_t>(), nchunks, r0, r1,
                                          c0, c1, upper ? 1 : 0, d_I, ldI, sc.use_part ? sc.part.as<int32_t>() : nullptr,
                                          s->Wd, s->nsets, s->dbits.as<unsigned long long>(), s->sp_fold_slabs,
-                                         group_part(s), xmap ? 1 : 0, (int)nt);
+                                         group_part(s), xmap ? 1 : 0, (int)nt, rs);
     GD_HIP(hipGetLastError());
     if (timed) {
         GD_HIP(hipEventRecord(ctx->ev_sp1, st));
@@ -1536,8 +1477,7 @@ bool sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
         sparse_reduce_kernel<<<(unsigned)(nt * (SB * SB / kReduceCnt / kReduceGroups)), 256, 0, st>>>(
             sc.part.as<int32_t>(), nchunks, sc.tiles.as<int2>(), s->sp_nc.as<int32_t>(), s->sp_U, r0, r1, c0, c1,
             upper ? 1 : 0, d_I, ldI,
-            sc.rare_in ? sc.rp_key.as<uint32_t>() : nullptr, sc.rare_in ? sc.rp_w.as<uint32_t>() : nullptr,
-            sc.rare_in ? sc.rp_off.as<int64_t>() : nullptr, ep ? ep->D : nullptr, ep ? ep->ldD : 0,
+            rare ? sc.rare_slab.as<uint32_t>() : nullptr, ep ? ep->D : nullptr, ep ? ep->ldD : 0,
             ep ? ep->off : nullptr, ep ? ep->empty_nan : 0, group_part(s));
         GD_HIP(hipGetLastError());
     }

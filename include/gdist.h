@@ -305,7 +305,10 @@ int  gdist_sets_allgather(gdist_ctx* ctx, const gdist_sets* local, gdist_sets** 
 /* The same; with GDIST_ALLGATHER_CONSUME the library releases `local`'s
  * device data once its codes are in the gather buffer (local keeps its sizes
  * and can still be freed; it can no longer be used for distances). Peak
- * device bytes per rank: (ranks + 1) x the largest shard's codes. */
+ * device bytes per rank: (ranks + 1) x the largest shard's codes. The local
+ * data is released BEFORE the collective runs: if the all-gather itself
+ * fails (GDIST_ECOMM, or the host transport's callback), `local` stays
+ * unusable and no result is returned; the caller re-packs its shard. */
 #define GDIST_ALLGATHER_CONSUME 0x1u
 int  gdist_sets_allgather_ex(gdist_ctx* ctx, gdist_sets* local, unsigned flags, gdist_sets** out);
 /* Which exchange a row-sharded N×N over this communicator should use

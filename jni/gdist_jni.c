@@ -39,6 +39,28 @@ static void throw_oom(JNIEnv* env) {
     if (c) (*env)->ThrowNew(env, c, "native buffer");
 }
 
+static void throw_arg(JNIEnv* env, const char* msg) {
+    jclass c = (*env)->FindClass(env, "java/lang/IllegalArgumentException");
+    if (c) (*env)->ThrowNew(env, c, msg);
+}
+
+/* the number of sets of a collection (-1 with the exception thrown) */
+static int64_t nsets_of(JNIEnv* env, const gdist_sets* s) {
+    int kind = 0, k = 0;
+    int64_t n = 0, total = 0;
+    int rc = gdist_sets_info(s, &kind, &k, &n, &total);
+    if (rc) { throw_for(env, rc); return -1; }
+    return n;
+}
+
+/* an array argument shorter than the collection it describes: the library
+ * writes (or reads) one element per set, so it is refused up front */
+static int too_short(JNIEnv* env, jarray a, int64_t n, const char* what) {
+    if (a && (int64_t)(*env)->GetArrayLength(env, a) >= n) return 0;
+    throw_arg(env, what);
+    return 1;
+}
+
 #define CTX(h) ((gdist_ctx*)(intptr_t)(h))
 #define SETS(h) ((gdist_sets*)(intptr_t)(h))
 
@@ -82,6 +104,7 @@ JNIEXPORT jlong JNICALL JFN(nPack)(JNIEnv* env, jclass c, jlong ctx, jint kind, 
         if (a) {
             (*env)->GetByteArrayRegion(env, a, 0, (jsize)(off[i + 1] - off[i]), (jbyte*)blob + off[i]);
             (*env)->DeleteLocalRef(env, a);
+            if ((*env)->ExceptionCheck(env)) { free(blob); free(off); return 0; }
         }
     }
     gdist_sets* s = NULL;
@@ -107,11 +130,12 @@ JNIEXPORT jlong JNICALL JFN(nSize)(JNIEnv* env, jclass c, jlong sets) {
 
 /* SequenceKmers.size() of every set */
 JNIEXPORT void JNICALL JFN(nSizes)(JNIEnv* env, jclass c, jlong sets, jlongArray out) {
-    const jsize n = (*env)->GetArrayLength(env, out);
+    const int64_t n = nsets_of(env, SETS(sets));
+    if (n < 0 || too_short(env, out, n, "out shorter than the number of sets")) return;
     int64_t* v = malloc(((size_t)n + 1) * sizeof(int64_t));
     if (!v) { throw_oom(env); return; }
     int rc = gdist_sets_sizes(SETS(sets), v);
-    if (!rc) (*env)->SetLongArrayRegion(env, out, 0, n, (const jlong*)v);
+    if (!rc) (*env)->SetLongArrayRegion(env, out, 0, (jsize)n, (const jlong*)v);
     free(v);
     if (rc) throw_for(env, rc);
 }
@@ -142,16 +166,20 @@ JNIEXPORT void JNICALL JFN(nMatrix)(JNIEnv* env, jclass c, jlong ctx, jlong sets
     if (!d) { throw_oom(env); return; }
     /* untouched entries (j <= i with GDIST_UPPER_TRIANGLE) keep the array's values */
     (*env)->GetDoubleArrayRegion(env, out, 0, (jsize)cells, d);
+    if ((*env)->ExceptionCheck(env)) { free(d); return; }
     int rc = gdist_intersect_matrix(CTX(ctx), SETS(sets), r0, r1, c0, c1, method, (unsigned)flags, NULL, d, ld);
     if (!rc) (*env)->SetDoubleArrayRegion(env, out, 0, (jsize)cells, d);
     free(d);
     if (rc) throw_for(env, rc);
 }
 
+/* NULL with an exception pending (out of memory, or the copy failed) */
 static int64_t* copy_cols(JNIEnv* env, jlongArray cols, jsize* n) {
     *n = (*env)->GetArrayLength(env, cols);
     int64_t* cl = malloc(((size_t)*n + 1) * sizeof(int64_t));
-    if (cl) (*env)->GetLongArrayRegion(env, cols, 0, *n, (jlong*)cl);
+    if (!cl) { throw_oom(env); return NULL; }
+    (*env)->GetLongArrayRegion(env, cols, 0, *n, (jlong*)cl);
+    if ((*env)->ExceptionCheck(env)) { free(cl); return NULL; }
     return cl;
 }
 
@@ -160,7 +188,7 @@ JNIEXPORT jboolean JNICALL JFN(nAnyLe)(JNIEnv* env, jclass c, jlong ctx, jlong s
                                        jdouble t) {
     jsize n = 0;
     int64_t* cl = copy_cols(env, cols, &n);
-    if (!cl) { throw_oom(env); return JNI_FALSE; }
+    if (!cl) return JNI_FALSE;
     int32_t hit = 0;
     int rc = gdist_row_query(CTX(ctx), SETS(sets), q, cl, n, GDIST_QUERY_ANY_LE, t, NULL, &hit, NULL, NULL);
     free(cl);
@@ -174,7 +202,7 @@ JNIEXPORT jint JNICALL JFN(nArgmin)(JNIEnv* env, jclass c, jlong ctx, jlong sets
                                     jdoubleArray bestD) {
     jsize n = 0;
     int64_t* cl = copy_cols(env, cols, &n);
-    if (!cl) { throw_oom(env); return -1; }
+    if (!cl) return -1;
     int64_t idx = -1;
     double d = 1.0;
     int rc = gdist_row_query(CTX(ctx), SETS(sets), q, cl, n, GDIST_QUERY_ARGMIN, 1.0, NULL, NULL, &idx, &d);
@@ -189,8 +217,10 @@ JNIEXPORT void JNICALL JFN(nRow)(JNIEnv* env, jclass c, jlong ctx, jlong sets, j
                                  jdoubleArray out) {
     jsize n = 0;
     int64_t* cl = copy_cols(env, cols, &n);
+    if (!cl) return;
+    if (too_short(env, out, n, "out shorter than cols")) { free(cl); return; }
     double* d = malloc(((size_t)n + 1) * sizeof(double));
-    if (!cl || !d) { free(cl); free(d); throw_oom(env); return; }
+    if (!d) { free(cl); throw_oom(env); return; }
     int rc = gdist_row_query(CTX(ctx), SETS(sets), q, cl, n, GDIST_QUERY_ALL, 1.0, d, NULL, NULL, NULL);
     if (!rc) (*env)->SetDoubleArrayRegion(env, out, 0, n, d);
     free(cl);
@@ -202,7 +232,12 @@ JNIEXPORT void JNICALL JFN(nRow)(JNIEnv* env, jclass c, jlong ctx, jlong sets, j
 JNIEXPORT jlong JNICALL JFN(nGreedyReps)(JNIEnv* env, jclass c, jlong ctx, jlong sets, jdouble t,
                                          jlongArray tieRank, jintArray isRep, jlongArray repOf,
                                          jdoubleArray repDist) {
-    const jsize n = (*env)->GetArrayLength(env, isRep);
+    const int64_t n = nsets_of(env, SETS(sets));
+    if (n < 0 || too_short(env, isRep, n, "isRep shorter than the number of sets") ||
+        (tieRank && too_short(env, tieRank, n, "tieRank shorter than the number of sets")) ||
+        (repOf && too_short(env, repOf, n, "repOf shorter than the number of sets")) ||
+        (repDist && too_short(env, repDist, n, "repDist shorter than the number of sets")))
+        return 0;
     int64_t* tr = tieRank ? malloc(((size_t)n + 1) * sizeof(int64_t)) : NULL;
     int32_t* ir = malloc(((size_t)n + 1) * sizeof(int32_t));
     int64_t* ro = repOf ? malloc(((size_t)n + 1) * sizeof(int64_t)) : NULL;
@@ -212,13 +247,16 @@ JNIEXPORT jlong JNICALL JFN(nGreedyReps)(JNIEnv* env, jclass c, jlong ctx, jlong
         throw_oom(env);
         return 0;
     }
-    if (tr) (*env)->GetLongArrayRegion(env, tieRank, 0, n, (jlong*)tr);
+    if (tr) {
+        (*env)->GetLongArrayRegion(env, tieRank, 0, (jsize)n, (jlong*)tr);
+        if ((*env)->ExceptionCheck(env)) { free(tr); free(ir); free(ro); free(rd); return 0; }
+    }
     int64_t nreps = 0;
     int rc = gdist_greedy_reps(CTX(ctx), SETS(sets), GDIST_METHOD_AUTO, t, tr, ir, ro, rd, &nreps);
     if (!rc) {
-        (*env)->SetIntArrayRegion(env, isRep, 0, n, (const jint*)ir);
-        if (ro) (*env)->SetLongArrayRegion(env, repOf, 0, n, (const jlong*)ro);
-        if (rd) (*env)->SetDoubleArrayRegion(env, repDist, 0, n, rd);
+        (*env)->SetIntArrayRegion(env, isRep, 0, (jsize)n, (const jint*)ir);
+        if (ro) (*env)->SetLongArrayRegion(env, repOf, 0, (jsize)n, (const jlong*)ro);
+        if (rd) (*env)->SetDoubleArrayRegion(env, repDist, 0, (jsize)n, rd);
     }
     free(tr); free(ir); free(ro); free(rd);
     if (rc) { throw_for(env, rc); return 0; }
@@ -244,6 +282,7 @@ JNIEXPORT void JNICALL JFN(nSketchMatrix)(JNIEnv* env, jclass c, jlong ctx, jlon
     double* d = malloc((size_t)(cells ? cells : 1) * sizeof(double));
     if (!d) { throw_oom(env); return; }
     (*env)->GetDoubleArrayRegion(env, out, 0, (jsize)cells, d);
+    if ((*env)->ExceptionCheck(env)) { free(d); return; }
     int rc = gdist_sketch_matrix(CTX(ctx), SETS(sk), r0, r1, c0, c1, (unsigned)flags, NULL, d, ld);
     if (!rc) (*env)->SetDoubleArrayRegion(env, out, 0, (jsize)cells, d);
     free(d);

@@ -64,6 +64,9 @@ def run_case(name, c, ctx, rank, world):
             assert m == gdist.METHOD_BITSET, (m, bb, bc)            # small: the dictionary exchange fits
             budget = 1 << 30
             assert bc <= budget < bb, (bb, bc)
+            # the bitsets estimate counts the bitsets the exchange allocates: at
+            # least every set's ancestral words (~200 K kmers both strands)
+            assert bb >= n * (200_000 // 64) * 8, bb
             ctx.set_option("exchange_budget", budget)
             own = gdist.KmerSets.from_sequences(seqs[s0:s1], 21, gdist.KmerType.DNA, 0, ctx)
             m, _, _ = own.exchange_plan()
@@ -71,11 +74,17 @@ def run_case(name, c, ctx, rank, world):
             gs = own.allgather(consume=True)
             ctx.set_option("exchange_budget", None)
             assert len(gs) == n and len(own) == s1 - s0
-            try:
-                own.matrix(method=gdist.METHOD_SORTED)
-                raise AssertionError("a consumed shard must refuse distance calls")
-            except ValueError:
-                pass
+            # a consumed shard holds neither codes nor bitsets: every method and
+            # the greedy reps refuse it (EINVAL) instead of reading released memory
+            for call in (lambda: own.matrix(method=gdist.METHOD_SORTED),
+                         lambda: own.matrix(method=gdist.METHOD_BITSET),
+                         lambda: own.matrix(method=gdist.METHOD_AUTO),
+                         lambda: own.greedy_reps(0.5)):
+                try:
+                    call()
+                    raise AssertionError("a consumed shard must refuse distance calls")
+                except ValueError:
+                    pass
             results[leg] = gs.matrix((r0, r1), (0, n), upper=True, method=gdist.METHOD_SORTED)
         elif leg == "sketch":
             sk = local.sketches(SKETCH_W).allgather()

@@ -945,6 +945,9 @@ def test_graph_replay_of_repeated_steps(ctx, opts, sparse):
     sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
     sets.build_bitsets()
     assert (sets.sparse_info()[0] > 0) == sparse
+    # a rare tier: the replayed sparse step recounts its pairs every call (the
+    # per-step slab is zeroed inside the graph; a stale slab would add them twice)
+    assert sets.rare_info()[1] > 0
     off, codes = oracle_pack(seqs, 21, 0, 0)
     for (r0, r1) in [(0, n), (37, 211)]:
         eI, eD = oracle.matrix(off, codes, r0, r1, 0, n, flags=0x100)
