@@ -124,10 +124,8 @@ def main():
                     help="one GPU: run the multi-rank exchange on a one-rank RCCL communicator")
     ap.add_argument("--pmc-json", default=None,
                     help="per-launch HBM traffic measured by rocprofv3 PMC passes "
-                         "(default profiles/pmc_<config>.json, if present)")
+                         "(default: the profiles/pmc_<config>*.json taken on the line's kernel, if any)")
     args = ap.parse_args()
-    if args.pmc_json is None:
-        args.pmc_json = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -282,7 +280,8 @@ def main():
             sets.matrix_device(dI.ptr, dD.ptr, N, (r0, r1), (0, N), upper=True, method=mflag)
 
     # the first call builds the region's launch plans (tile lists, sparse
-    # chunks, the rare pairs' table) before it runs: timed on its own, it is
+    # chunks, the tile map of the rare rows: geometry only) before it runs;
+    # every step recounts every pair, the rare tier included. Timed on its own, it is
     # part of the one-pass end-to-end figure; the second call is captured
     first_call_s = None
     for w in range(args.warmup):
@@ -313,20 +312,24 @@ def main():
         step()
     kernel_ms = ctx.recent_timings(kt)
     ctx.set_option("step_timing", prev_st)
-    # The sparse tile kernel alone, after the timed region (roofline): HIP
-    # events around its launch on the stream it runs on (option time_sparse;
-    # such calls run unreplayed, one event pair per call)
-    sparse_k_ms = None
-    if method == "bitset" and sparse_words and sparse_words["sparse_words"] > 0:
-        prev = ctx.option("time_sparse")
-        ctx.set_option("time_sparse", 1)
-        ts = []
-        for _ in range(max(3, min(args.steps, 20))):
+    # Each kernel family alone, after the timed region (roofline): HIP events
+    # around its launches on the stream they run on (option time_kernels; such
+    # calls run unreplayed, one event pair per family and call): the sparse
+    # tile launch, the rare-tier kernel, the dense tiles, the sorted join
+    fam_ms = {}
+    if method in ("bitset", "sorted"):
+        prev = ctx.option("time_kernels")
+        ctx.set_option("time_kernels", 1)
+        acc = {f: [] for f in ctx.KERNEL_FAMILIES}
+        for it in range(max(3, min(args.steps, 20))):
             step()
-            ts.append(ctx.sparse_kernel_ms())
-        ctx.set_option("time_sparse", prev)
-        ts = [t for t in ts[1:] if t > 0]                 # the first call builds nothing new, but warms
-        sparse_k_ms = float(np.mean(ts)) if ts else None
+            for f in acc:
+                v = ctx.kernel_ms(f)
+                if it > 0 and v > 0:                       # the first call builds nothing new, but warms
+                    acc[f].append(v)
+        ctx.set_option("time_kernels", prev)
+        fam_ms = {f: float(np.mean(v)) for f, v in acc.items() if v}
+    sparse_k_ms = fam_ms.get("sparse")
     pairs_all = N * (N - 1) // 2
     pairs_job = pairs_rank if slice_rows else pairs_all      # a slice's pairs are all this job computes
     value = pairs_job * args.steps / elapsed_max
@@ -352,26 +355,27 @@ def main():
             # HBM/L2 traffic is the windows' fill, ~1/10 of that
             bytes_per_pair = 8.0 * cfg["width"]
         algo_bytes = pairs_rank * bytes_per_pair
-        achieved = algo_bytes / (k_avg_ms * 1e-3) / 1e9 if k_avg_ms > 0 else 0.0
-        traffic = None
-        pmc = {}
-        if os.path.exists(args.pmc_json):
-            try:
-                with open(args.pmc_json) as f:
-                    pmc = json.load(f)
-                if pmc.get("config") == args.config and pmc.get("n") == N:
-                    traffic = pmc.get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
+
+        def pmc_traffic(kern):
+            """HBM bytes per launch of `kern` from the committed PMC passes
+            (profiles/pmc_<config>*.json: FETCH_SIZE x 2 + WRITE_SIZE), only a
+            summary taken on this kernel at this collection size."""
+            import glob
+            files = [args.pmc_json] if args.pmc_json else \
+                sorted(glob.glob(os.path.join(ROOT, "profiles", f"pmc_{args.config}*.json")))
+            for fn in files:
+                try:
+                    with open(fn) as f:
+                        pmc = json.load(f)
+                except Exception:
+                    continue
+                if pmc.get("config") == args.config and pmc.get("n") == N and \
+                        pmc.get("kernel", "").startswith(kern):
+                    return pmc.get("hbm_bytes_per_launch")
+            return None
+
         sparse = sparse_words if (method == "bitset" and sparse_words and sparse_words["sparse_words"] > 0) else None
         sk_whole = options.get("sketch_phase", 1) == 0
-        kname = {"bitset": "bitset_tile_kernel2 (+ rare_pairs_kernel)", "sorted": "sorted_join_kernel",
-                 "sketch": ("sketch_tile_kernel<16,24,LDS,K=2>" if sk_whole else
-                            "sketch_ring_kernel (32x32, interleaved LDS rings, step-synchronised phases)")}[method]
-        if sparse:
-            kname = "sparse_tile_kernel<3> (1x2 micro-tiles, the dense words folded in)"
-        if traffic is not None and not pmc.get("kernel", "").startswith(kname.split(" (")[0]):
-            traffic = None                    # the PMC summary was taken on another kernel
         valu_peak = VALU_WORDPAIR_PEAK * 4 / 1e12
         if sparse:
             # Complement-sparse dense tier (DESIGN.md §3-4): the step's work is
@@ -380,6 +384,7 @@ def main():
             # once: its row block's and column block's entries (8 B complement
             # word + 1 B set) and their (block, word) offsets (2 x 8 B), one side
             # for a whole diagonal tile.
+            kname = "sparse_tile_kernel<3> (1x2 micro-tiles, the dense words folded in, the rare rows trailing)"
             nb = -(-N // 128)
             side = sparse["entries"] / nb * 9.0 + sparse["sparse_words"] * 16.0
             algo_sparse = 0.0
@@ -394,41 +399,75 @@ def main():
             ach = algo_sparse / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
             dense_ops = pairs_rank * width_words * 4 / (k_avg_ms * 1e-3) / 1e12 if k_avg_ms > 0 else 0.0
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kname,
-                    "kernel_avg_ms": round(kms, 4), "step_kernel_span_ms": round(k_avg_ms, 4),
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("sparse_tile_kernel"),
+                    "kernel": kname, "kernel_avg_ms": round(kms, 4), "step_kernel_span_ms": round(k_avg_ms, 4),
                     "algo_bytes_per_launch": round(algo_sparse),
                     "limiter": SPARSE_LIMITER,
                     "note": "algorithmic bytes = the sparse entries (8 B word + 1 B set) + offsets each sparse "
-                            "tile streams once; kernel_avg_ms = HIP events around the sparse tile kernel alone "
-                            "(option time_sparse, after the timed region); step_kernel_span_ms = HIP-event span "
-                            "of the timed steps' launches (zeroing, sparse tiles, chunk reduce, rare tier "
-                            "beside them, epilogue)",
+                            "tile streams once; kernel_avg_ms = HIP events around the sparse tile launch alone "
+                            "(option time_kernels, after the timed region; its trailing workgroups recount the "
+                            "rare tier's pairs of the step); step_kernel_span_ms = HIP-event span of the timed "
+                            "steps' launches (sparse tiles + rare rows, then the chunk reduce that stores I and D)",
                     "dense_equivalent": {"lane_ops_per_s_T": round(dense_ops, 2),
                                          "x_dense_valu_ceiling": round(dense_ops / valu_peak, 2),
                                          "note": "the same pairs as AND+popcount over all W bitset words "
                                                  "(4 lane-ops per word pair) in the step's kernel time, against the "
                                                  "measured and+bcnt ceiling the dense tiles are bound by"}}
         elif method == "bitset":
-            # The tiles reuse each bitset from LDS across 128 partners, so the 16*W
-            # B/pair streaming figure runs far past the HBM peak: the binding
-            # resource is VALU issue. One 64-bit word pair = 4 lane-ops
-            # (2 v_and_b32 + 2 v_bcnt_u32_b32); peak = the measured and+bcnt ceiling.
-            wp = pairs_rank * width_words / (k_avg_ms * 1e-3) if k_avg_ms > 0 else 0.0
-            tops, tops_peak = wp * 4 / 1e12, valu_peak
-            roof = {"bound": "valu", "achieved": round(tops, 3), "peak": round(tops_peak, 3), "unit": "TOP/s",
-                    "frac": round(tops / tops_peak, 4), "traffic": traffic, "kernel": kname,
-                    "kernel_avg_ms": round(k_avg_ms, 4), "ops_per_pair": 4 * width_words,
-                    "note": "lane-ops of the dense tier (pairs x W word pairs x 4); kernel time includes the "
-                            "rare tier; peak = measured and+bcnt issue ceiling (profiles/r01/valu_microbench.txt)",
-                    "hbm": {"achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                            "frac": round(achieved / HBM_PEAK_GBS, 4), "bytes_per_pair": bytes_per_pair,
-                            "note": "16*W B/pair streaming model (SURVEY 8d); traffic = measured HBM bytes/launch"}}
+            # Two tiers in one step (C3): the dense tiles (VALU-bound: they reuse
+            # each bitset from LDS across 128 partners, so the 16*W B/pair
+            # streaming figure runs far past the HBM peak) and, beside them on
+            # the side stream, the rare-tier kernel. The line's roofline is the
+            # LONGER of the two, each timed alone by HIP events on its stream.
+            d_ms, r_ms = fam_ms.get("dense", 0.0), fam_ms.get("rare", 0.0)
+            wp = pairs_rank * width_words / (d_ms * 1e-3) if d_ms > 0 else 0.0
+            tops = wp * 4 / 1e12
+            dense_roof = {"bound": "valu", "achieved": round(tops, 3), "peak": round(valu_peak, 3), "unit": "TOP/s",
+                          "frac": round(tops / valu_peak, 4), "traffic": pmc_traffic("bitset_tile_kernel2"),
+                          "kernel": "bitset_tile_kernel2 (dense tier tiles)", "kernel_avg_ms": round(d_ms, 4),
+                          "ops_per_pair": 4 * width_words,
+                          "note": "lane-ops of the dense tier (pairs x W word pairs x 4) / the dense tile launches' "
+                                  "own time; peak = measured and+bcnt issue ceiling "
+                                  "(profiles/r01/valu_microbench.txt)",
+                          "hbm_streaming_model": {"achieved": round(algo_bytes / (d_ms * 1e-3) / 1e9, 1) if d_ms else 0,
+                                                  "bytes_per_pair": bytes_per_pair,
+                                                  "note": "16*W B/pair (SURVEY 8d), operands reused from LDS"}}
+            roof = dense_roof
+            if r_ms > 0 and rare:
+                # rare tier, row-major walk (rare_rows_kernel) or list-major
+                # (rare_pairs_kernel): its useful bytes = the rows' (set, list)
+                # records (8 B list + 4 B weight + 2 B skip) + one 4-byte member
+                # read per pair increment + the I updates (4 B read + 4 B write
+                # per pair of the block)
+                rec, incs = sets.rare_info()[2], sets.rare_stats()[0]
+                f_rows = (r1 - r0) / N
+                f_pairs = pairs_rank / max(1, N * (N - 1) // 2)
+                rare_bytes = 14.0 * rec * f_rows + 4.0 * incs * f_pairs + 8.0 * pairs_rank
+                rk = "rare_rows_kernel" if sets.block_cost((r0, r1))[1] == 1 else "rare_pairs_kernel"
+                ach = rare_bytes / (r_ms * 1e-3) / 1e9
+                rare_roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(rk),
+                             "kernel": f"{rk} (rare tier, beside the dense tiles)", "kernel_avg_ms": round(r_ms, 4),
+                             "algo_bytes_per_launch": round(rare_bytes),
+                             "note": "algorithmic bytes = 14 B per (set, list) record of the rows + 4 B per member "
+                                     "read (pair increments) + 8 B per pair of I updated; scattered 4-byte member "
+                                     "reads from lists of ~18 sets: each read brings a whole line"}
+                if r_ms > d_ms:
+                    roof = dict(rare_roof, other=dense_roof)
+                else:
+                    roof = dict(dense_roof, other=rare_roof)
+            roof["step_kernel_span_ms"] = round(k_avg_ms, 4)
         else:
+            kname = {"sorted": "sorted_join_kernel",
+                     "sketch": ("sketch_tile_kernel<16,24,LDS,K=2>" if sk_whole else
+                                "sketch_ring_kernel (32x32, interleaved LDS rings, step-synchronised phases)")}[method]
+            kms = fam_ms.get("sorted", k_avg_ms) if method == "sorted" else k_avg_ms
+            achieved = algo_bytes / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
             peak = LDS_B32_PEAK_GBS if method == "sketch" else HBM_PEAK_GBS
             roof = {"bound": "lds" if method == "sketch" else "hbm", "achieved": round(achieved, 1), "peak": peak,
-                    "unit": "GB/s", "frac": round(achieved / peak, 4), "traffic": traffic, "kernel": kname,
-                    "kernel_avg_ms": round(k_avg_ms, 4), "algo_bytes_per_launch": algo_bytes,
-                    "bytes_per_pair": bytes_per_pair}
+                    "unit": "GB/s", "frac": round(achieved / peak, 4), "traffic": pmc_traffic(kname.split(" ")[0]),
+                    "kernel": kname, "kernel_avg_ms": round(kms, 4), "step_kernel_span_ms": round(k_avg_ms, 4),
+                    "algo_bytes_per_launch": algo_bytes, "bytes_per_pair": bytes_per_pair}
         # ---------------------------------------------------------------- CPU baseline
         cpu = None
         cpu_opt = None
@@ -468,8 +507,8 @@ def main():
                                       if first_call_s is not None else None),
                            "note": "one pass over the collection from FASTA bytes in host memory: pack (H2D + "
                                    "kmer extraction + sort) + represent (dictionary, bitsets, sparse words) + the "
-                                   "FIRST matrix call (it builds the region's launch plans and the rare pairs' "
-                                   "table, then runs; plan_s = that call minus a steady step); synthetic-genome "
+                                   "FIRST matrix call (it builds the region's launch plans, geometry only, then "
+                                   "runs; plan_s = that call minus a steady step); synthetic-genome "
                                    "generation and the release of the caller's host buffer (setup_s.host_free) "
                                    "excluded; max over ranks"},
         }

@@ -215,13 +215,19 @@ constexpr int RCH = 16384;   // max columns per LDS chunk (64 KiB of counters)
 // grid = nr rows x nch column chunks x nsplit slices of the row's rare kmers;
 // counters live in dynamic LDS sized to the chunk. With nsplit > 1 several
 // workgroups share a row chunk and flush with global atomics.
+// Member = uint32 (post_sets) or uint16 (post_sets16, collections of at most
+// 65,536 sets): the walk's scattered list reads are whole lines from HBM or
+// the Infinity Cache, and 2-byte members halve the lines a list spans and
+// let C3's lists (72 M members: 287 MB as uint32) sit in the 256 MiB cache.
+template <typename M>
 __global__ __launch_bounds__(256) void rare_rows_kernel(const int64_t* __restrict__ soff,
                                                         const uint64_t* __restrict__ sent,
                                                         const uint32_t* __restrict__ sw,
                                                         const uint16_t* __restrict__ sskip,
-                                                        const uint32_t* __restrict__ psets, int64_t r0, int64_t r1,
+                                                        const M* __restrict__ psets, int64_t r0, int64_t r1,
                                                         int64_t c0, int64_t c1, int nch, int nsplit, int upper,
                                                         int atomic_flush, int32_t* __restrict__ I, int64_t ldI) {
+    constexpr int PER = 16 / (int)sizeof(M);     // members per 16-byte load
     extern __shared__ int32_t cnt[];
     const int64_t unit = blockIdx.x / nsplit;
     const int split = blockIdx.x % nsplit;
@@ -257,15 +263,15 @@ __global__ __launch_bounds__(256) void rare_rows_kernel(const int64_t* __restric
             }
         }
         if (lng) continue;
-        // four members per 16-byte load (dword-aligned: global_load_dwordx4;
-        // post_sets is padded past its last list)
+        // PER members per 16-byte load (global_load_dwordx4 when the list
+        // start is dword-aligned; post_sets / post_sets16 are padded past the
+        // last list)
 #pragma unroll 2
-        for (int64_t y = b; y < e; y += 4) {
-            uint4 v;
-            __builtin_memcpy(&v, psets + y, 16);
-            const uint32_t mem[4] = {v.x, v.y, v.z, v.w};
+        for (int64_t y = b; y < e; y += PER) {
+            M mem[PER];
+            __builtin_memcpy(mem, psets + y, 16);
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
+            for (int u = 0; u < PER; u++) {
                 const int64_t t = mem[u];
                 if (y + u < e && t >= lo && t < ce && t != i) atomicAdd(&cnt[t - cb], w);
             }
@@ -1473,6 +1479,11 @@ __global__ void list_offsets_kernel(const int64_t* __restrict__ poff, int64_t nl
         if (keep[l]) { out_off[newid[l]] = rpos[poff[l]]; out_w[newid[l]] = weight[l]; }
 }
 
+__global__ void narrow_u16_kernel(const uint32_t* __restrict__ in, int64_t n, uint16_t* __restrict__ out) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) out[i] = (uint16_t)in[i];
+}
+
 __global__ void fill_u32_kernel(uint32_t* __restrict__ p, int64_t n, uint32_t v) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = v;
@@ -1594,6 +1605,16 @@ void build_postings(gdist_ctx* ctx, gdist_sets* s, unsigned long long* recs, int
     rare_skip_kernel<<<grid_for(nrec), 256, 0, st>>>(kalt, nrec, s->post_off.as<int64_t>(), s->post_sets.as<uint32_t>(),
                                                      s->srare_skip.as<uint16_t>());
     GD_HIP(hipGetLastError());
+    // 2-byte members for the row-major walk (collections of <= 65,536 sets;
+    // option rare_u16 = 0 keeps the 4-byte ones)
+    s->post_sets16.release();
+    if (s->nsets <= 65536 && ctx->option(OPT_RARE_U16, 1) != 0) {
+        s->post_sets16.alloc(nrec * 2 + 16, st);
+        GD_HIP(hipMemsetAsync(s->post_sets16.as<uint16_t>() + nrec, 0, 16, st));
+        narrow_u16_kernel<<<grid_for(nrec), 256, 0, st>>>(s->post_sets.as<uint32_t>(), nrec,
+                                                          s->post_sets16.as<uint16_t>());
+        GD_HIP(hipGetLastError());
+    }
     // pair increments of the tier (cost model, kernel choice)
     DevBuf d_incs(24, st);
     GD_HIP(hipMemsetAsync(d_incs.p, 0, 24, st));
@@ -1749,6 +1770,7 @@ void free_bitsets(gdist_sets* s) {
     s->bits.release();
     s->post_off.release();
     s->post_sets.release();
+    s->post_sets16.release();
     s->post_w.release();
     s->srare_off.release();
     s->srare_ent.release();
@@ -1863,10 +1885,25 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
         const int64_t rgrid = units * nsplit;
         GD_REQUIRE(rgrid < (int64_t(1) << 31), "rare-tier grid too large");
         const size_t lds = (size_t)std::min<int64_t>(nc, RCH) * 4;
-        rare_rows_kernel<<<(unsigned)rgrid, 256, lds, rs>>>(s->srare_off.as<int64_t>(), s->srare_ent.as<uint64_t>(),
-                                                           s->srare_w.as<uint32_t>(), s->srare_skip.as<uint16_t>(),
-                                                           s->post_sets.as<uint32_t>(), r0, r1, c0, c1, nch, nsplit,
-                                                           upper ? 1 : 0, atomic_flush ? 1 : 0, d_I, ldI);
+        FamilyTimer ft(ctx, GDIST_KERNEL_RARE, rs);
+        if (s->post_sets16.p)
+            rare_rows_kernel<uint16_t><<<(unsigned)rgrid, 256, lds, rs>>>(
+                s->srare_off.as<int64_t>(), s->srare_ent.as<uint64_t>(), s->srare_w.as<uint32_t>(),
+                s->srare_skip.as<uint16_t>(), s->post_sets16.as<uint16_t>(), r0, r1, c0, c1, nch, nsplit,
+                upper ? 1 : 0, atomic_flush ? 1 : 0, d_I, ldI);
+        else
+            rare_rows_kernel<uint32_t><<<(unsigned)rgrid, 256, lds, rs>>>(
+                s->srare_off.as<int64_t>(), s->srare_ent.as<uint64_t>(), s->srare_w.as<uint32_t>(),
+                s->srare_skip.as<uint16_t>(), s->post_sets.as<uint32_t>(), r0, r1, c0, c1, nch, nsplit,
+                upper ? 1 : 0, atomic_flush ? 1 : 0, d_I, ldI);
+        ft.end();
+    };
+    auto launch_rare_pairs = [&](hipStream_t rs) {
+        FamilyTimer ft(ctx, GDIST_KERNEL_RARE, rs);
+        rare_pairs_kernel<<<grid_for(s->n_rare, 256, 256 * 64), 256, 0, rs>>>(
+            s->post_off.as<int64_t>(), s->post_sets.as<uint32_t>(), s->post_w.as<uint32_t>(), s->n_rare, r0, r1, c0,
+            c1, upper ? 1 : 0, d_I, ldI);
+        ft.end();
     };
     if (!ctx->capturing) GD_HIP(hipEventRecord(ctx->ev_k0, st));
     if (side) {
@@ -1876,10 +1913,7 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
         // beside the sparse kernel the list-major rare kernel goes to the main
         // stream after the dense tiles (the side stream is busy until the
         // sparse tiles and their reduce end: C2 0.0185 ms in line there)
-        if (overlap && !s->sparse)
-            rare_pairs_kernel<<<grid_for(s->n_rare, 256, 256 * 64), 256, 0, ctx->side>>>(
-                s->post_off.as<int64_t>(), s->post_sets.as<uint32_t>(), s->post_w.as<uint32_t>(), s->n_rare, r0, r1,
-                c0, c1, upper ? 1 : 0, d_I, ldI);
+        if (overlap && !s->sparse) launch_rare_pairs(ctx->side);
         if (rows_side) launch_rare_rows(ctx->side, true);
         GD_HIP(hipGetLastError());
         GD_HIP(hipEventRecord(ctx->ev_join, ctx->side));
@@ -1907,6 +1941,7 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
         };
         const int2* dg = p.tiles.as<int2>();
         const size_t* at = p.at;
+        FamilyTimer ft(ctx, GDIST_KERNEL_DENSE, st);
         {
             launch(bitset_tile_kernel2<false>, dg, at[1]);
             launch(bitset_tile_kernel2<true>, dg + at[1], at[2] - at[1]);
@@ -1925,20 +1960,16 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
                 default: break;   // no partial row tile
             }
         }
+        ft.end();
     }
-    if (overlap && s->sparse && !rare_done)
-        rare_pairs_kernel<<<grid_for(s->n_rare, 256, 256 * 64), 256, 0, st>>>(
-            s->post_off.as<int64_t>(), s->post_sets.as<uint32_t>(), s->post_w.as<uint32_t>(), s->n_rare, r0, r1, c0,
-            c1, upper ? 1 : 0, d_I, ldI);
+    if (overlap && s->sparse && !rare_done) launch_rare_pairs(st);
     GD_HIP(hipGetLastError());
     ctx->last.launches = 1;
     if (side) GD_HIP(hipStreamWaitEvent(st, ctx->ev_join, 0));
     if (s->n_rare > 0 && !rare_done) {
         if (overlap) {
         } else if (list_major) {
-            rare_pairs_kernel<<<grid_for(s->n_rare, 256, 256 * 64), 256, 0, st>>>(
-                s->post_off.as<int64_t>(), s->post_sets.as<uint32_t>(), s->post_w.as<uint32_t>(), s->n_rare, r0, r1,
-                c0, c1, upper ? 1 : 0, d_I, ldI);
+            launch_rare_pairs(st);
         } else if (!rows_side) {
             launch_rare_rows(st, false);
         }

@@ -256,8 +256,10 @@ int gdist_ctx_create(int device, gdist_ctx** out) {
         GD_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
         GD_HIP(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
         GD_HIP(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
-        GD_HIP(hipEventCreateWithFlags(&c->ev_sp0, kTimingEventFlags));
-        GD_HIP(hipEventCreateWithFlags(&c->ev_sp1, kTimingEventFlags));
+        for (int f = 0; f < gdist_ctx::kFamilies; f++) {
+            GD_HIP(hipEventCreateWithFlags(&c->ev_kf0[f], kTimingEventFlags));
+            GD_HIP(hipEventCreateWithFlags(&c->ev_kf1[f], kTimingEventFlags));
+        }
         GD_HIP(hipEventCreateWithFlags(&c->ev_stage[0], hipEventDisableTiming));
         GD_HIP(hipEventCreateWithFlags(&c->ev_stage[1], hipEventDisableTiming));
         GD_HIP(hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device));
@@ -280,8 +282,10 @@ int gdist_ctx_destroy(gdist_ctx* ctx) {
         (void)hipStreamSynchronize(ctx->side);
         (void)hipEventDestroy(ctx->ev_fork);
         (void)hipEventDestroy(ctx->ev_join);
-        (void)hipEventDestroy(ctx->ev_sp0);
-        (void)hipEventDestroy(ctx->ev_sp1);
+        for (int f = 0; f < gdist_ctx::kFamilies; f++) {
+            (void)hipEventDestroy(ctx->ev_kf0[f]);
+            (void)hipEventDestroy(ctx->ev_kf1[f]);
+        }
         (void)hipStreamDestroy(ctx->side);
         (void)hipEventDestroy(ctx->ev_stage[0]);
         (void)hipEventDestroy(ctx->ev_stage[1]);
@@ -347,16 +351,17 @@ int gdist_ctx_recent_timings(gdist_ctx* ctx, int max, double* kernel_ms, int* co
     });
 }
 
-int gdist_ctx_sparse_kernel_ms(gdist_ctx* ctx, double* ms) {
+int gdist_ctx_kernel_ms(gdist_ctx* ctx, int family, double* ms) {
     return guard([&] {
         GD_REQUIRE(ctx && ms, "null argument");
+        GD_REQUIRE(family >= 0 && family < gdist_ctx::kFamilies, "unknown kernel family");
         use_device(ctx);
         std::lock_guard<std::recursive_mutex> lk_(ctx->mu);
         *ms = -1.0;
-        if (!ctx->sp_timed) return;
-        GD_HIP(hipEventSynchronize(ctx->ev_sp1));
+        if (!ctx->kf_timed[family]) return;
+        GD_HIP(hipEventSynchronize(ctx->ev_kf1[family]));
         float t = 0.f;
-        GD_HIP(hipEventElapsedTime(&t, ctx->ev_sp0, ctx->ev_sp1));
+        GD_HIP(hipEventElapsedTime(&t, ctx->ev_kf0[family], ctx->ev_kf1[family]));
         *ms = t;
     });
 }
@@ -802,13 +807,14 @@ int gdist_intersect_matrix(gdist_ctx* ctx, const gdist_sets* sets, int64_t r0, i
         hipStream_t st = ctx->stream;
         ctx->pending = false;          // an unread previous call's times are dropped, not waited for
         ctx->last = Timing{};
+        for (bool& f : ctx->kf_timed) f = false;
         // Graph-replayed steps record no timing events unless option
         // step_timing = 1: four event records (call and kernel span) cost
         // 13 us between two C2 steps even without the system fence (0.161
         // vs 0.148 ms, profiles/r02/sparse6/events.txt). Such calls leave
         // last_timing empty and are not in recent_timings.
         const bool quiet = dev && I_out && m == GDIST_METHOD_BITSET && ctx->option(OPT_GRAPH, 1) != 0 &&
-                           ctx->option(OPT_STEP_TIMING, 0) == 0 && ctx->option(OPT_TIME_SPARSE, 0) == 0;
+                           ctx->option(OPT_STEP_TIMING, 0) == 0 && ctx->option(OPT_TIME_KERNELS, 0) == 0;
         bool timing_started = false;
         auto start_timing = [&] {
             if (timing_started) return;
@@ -839,7 +845,7 @@ int gdist_intersect_matrix(gdist_ctx* ctx, const gdist_sets* sets, int64_t r0, i
         // runs uncaptured (it builds the launch plans), the second is
         // captured; a refused capture leaves the key uncaptured.
         if (dev && I_out && m == GDIST_METHOD_BITSET && ctx->option(OPT_GRAPH, 1) != 0 &&
-            ctx->option(OPT_TIME_SPARSE, 0) == 0) {
+            ctx->option(OPT_TIME_KERNELS, 0) == 0) {
             std::vector<int64_t> key{r0, r1, c0, c1, (int64_t)flags, (int64_t)(intptr_t)I_out,
                                      (int64_t)(intptr_t)D_out, ld};
             key.insert(key.end(), ctx->opt, ctx->opt + OPT_COUNT);

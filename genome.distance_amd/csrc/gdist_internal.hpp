@@ -199,7 +199,7 @@ struct Timing {
     X(FORCE_EXCHANGE, "force_exchange")       /* 1: a one-rank communicator runs every collective (tests) */   \
     X(SPARSE_CHUNKS, "sparse_chunks")         /* chunks of the sparse words per tile (tests) */                \
     X(GRAPH, "graph")                         /* 0: no hipGraph replay of repeated matrix calls */             \
-    X(TIME_SPARSE, "time_sparse")             /* 1: HIP events around the sparse tile kernel (no replay) */    \
+    X(TIME_KERNELS, "time_kernels")           /* 1: HIP events around each kernel family's launches (no replay) */ \
     X(STEP_TIMING, "step_timing")             /* 1: graph-replayed steps record timing events too */           \
     X(SPARSE_RARE, "sparse_rare")             /* 0: the rare pairs by the rare kernel, not the chunk reduce */ \
     X(SPARSE_FUSED, "sparse_fused")           /* 0: zeroing, rare kernel and epilogue as their own launches */ \
@@ -212,7 +212,8 @@ struct Timing {
     X(EXCHANGE_BUDGET, "exchange_budget")     /* device bytes an exchange may use (default 0.8 x HBM) */    \
     X(PACK_CODES_BUDGET, "pack_codes_budget") /* bytes of the one-buffer pack (default 1/4 HBM; past it: grown) */\
     X(SPARSE_GROUPS, "sparse_groups")         /* 0: no group tier (clade patterns) in the sparse words */       \
-    X(SPARSE_XCD, "sparse_xcd")               /* 1: chunk c of every sparse tile on XCD c mod 8 */
+    X(SPARSE_XCD, "sparse_xcd")               /* 1: chunk c of every sparse tile on XCD c mod 8 */           \
+    X(RARE_U16, "rare_u16")                   /* 0: 4-byte list members in the row-major rare walk */
 
 enum Opt : int {
 #define GDIST_OPT_ENUM(id, name) OPT_##id,
@@ -259,9 +260,11 @@ struct gdist_ctx {
     size_t pinned_bytes = 0;
     hipEvent_t ev_stage[2] = {nullptr, nullptr};
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    // option time_sparse: the sparse tile kernel alone (uncaptured calls)
-    hipEvent_t ev_sp0 = nullptr, ev_sp1 = nullptr;
-    bool sp_timed = false;
+    // option time_kernels: each kernel family's launches alone (uncaptured
+    // calls), by family (GDIST_KERNEL_SPARSE / RARE / DENSE / SORTED)
+    static constexpr int kFamilies = 4;
+    hipEvent_t ev_kf0[kFamilies] = {}, ev_kf1[kFamilies] = {};
+    bool kf_timed[kFamilies] = {};
     gdist::Timing last;
     int cus = 256;
     // RCCL communicator (multi-GPU row sharding)
@@ -314,6 +317,7 @@ struct gdist_sets {
     // rare tier of the dictionary: kmers held by 2..rare_T-1 sets as posting lists
     gdist::DevBuf post_off;               // int64 [n_rare+1]
     gdist::DevBuf post_sets;              // uint32 [rare_records], ascending within a list
+    gdist::DevBuf post_sets16;            // uint16 copy for the row-major walk (nsets <= 65,536; else empty)
     int64_t n_rare = 0, rare_T = 0, rare_records = 0;
     int64_t rare_incs = 0;                // sum over rare lists of m(m-1)/2 pair increments
     int64_t rare_max_list = 0;            // longest rare posting list
@@ -540,5 +544,24 @@ void sketch_matrix(gdist_ctx* ctx, const gdist_sets* sk, int64_t r0, int64_t r1,
                    int64_t c1, unsigned flags, int32_t* d_common, double* d_D, int64_t ld);
 
 __host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// HIP events around one kernel family's launches on stream st (option
+// time_kernels, calls not captured): gdist_ctx_kernel_ms reads them
+struct FamilyTimer {
+    gdist_ctx* ctx;
+    int fam;
+    hipStream_t st;
+    bool on;
+    FamilyTimer(gdist_ctx* c, int f, hipStream_t s)
+        : ctx(c), fam(f), st(s), on(c->option(OPT_TIME_KERNELS, 0) != 0 && !c->capturing) {
+        if (on) GD_HIP(hipEventRecord(ctx->ev_kf0[fam], st));
+    }
+    void end() {
+        if (!on) return;
+        GD_HIP(hipEventRecord(ctx->ev_kf1[fam], st));
+        ctx->kf_timed[fam] = true;
+        on = false;
+    }
+};
 
 }  // namespace gdist

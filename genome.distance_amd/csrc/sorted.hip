@@ -233,11 +233,13 @@ static void launch_join(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t
     // (C4's largest row block is ~55 M units)
     const int64_t per = (int64_t(1) << 31) / NTJ;
     int launches = 0;
+    FamilyTimer ft(ctx, GDIST_KERNEL_SORTED, st);
     for (int64_t u0 = 0; u0 < nunits; u0 += per, launches++)
         sorted_join_kernel<<<(unsigned)std::min(per, nunits - u0), NTJ, 0, st>>>(
             s->codes.as<uint64_t>(), s->segoff.as<int64_t>(), s->nseg, dp.as<int64_t>(), ncb, u0, nunits, r0, r1, c0,
             c1, d_colidx, upper ? 1 : 0, d_I, ldI);
     GD_HIP(hipGetLastError());
+    ft.end();
     GD_HIP(hipEventRecord(ctx->ev_k1, st));
     ctx->last.launches = launches;
 }

@@ -466,7 +466,7 @@ inline RareRows rare_rows_of(const gdist_sets* s) {
 }
 
 // The rare tier's pairs, recounted in every step by workgroups of the tile
-// launch itself (the first nrare workgroups; no per-pair state survives
+// launch itself (its last nrare workgroups; no per-pair state survives
 // between steps, no extra launch, no second stream): one workgroup per (row
 // i, chunk of 8192 columns) walks the row's (set, list) records, adds each
 // list member in the chunk (upper triangle: from the row's own position on,
@@ -477,7 +477,7 @@ inline RareRows rare_rows_of(const gdist_sets* s) {
 constexpr int kRareChunkCols = SB * SB / 2;       // the tile kernel's 32 KiB of LDS counters, one per column
 struct RareSlab {
     RareRows rr;
-    int nrare = 0;                        // leading workgroups doing rare rows (0: none)
+    int nrare = 0;                        // trailing workgroups doing rare rows (0: none)
     int nch = 1;                          // column chunks per row
     uint32_t* slab = nullptr;             // uint32 [ntiles][128 x 128]
     const int32_t* tile_of = nullptr;     // [row blocks of the region][column blocks]: tile index or -1
@@ -706,11 +706,14 @@ __global__ __launch_bounds__(SNT, 8) void sparse_tile_kernel(
     // slab_bits / slabs: the in-kernel fold's dense words (set-major [N][Wdp])
     __shared__ uint32_t cnt[SB * SB / 2];                  // 32 KiB, 16-bit counters (cnt_index layout)
     __shared__ int4 rec[SNW][64];                          // 8 KiB: the batch's walk records
-    if ((int)blockIdx.x < rs.nrare) {                      // a rare row of this step (above)
-        rare_slab_row(rs, (int)blockIdx.x, r0, c0, c1, upper, cnt);
+    // the rare rows of this step (above) are the launch's LAST workgroups:
+    // they fill the CUs the tile workgroups' last round leaves idle
+    const unsigned ntw = gridDim.x - (unsigned)rs.nrare;
+    if (blockIdx.x >= ntw) {
+        rare_slab_row(rs, (int)(blockIdx.x - ntw), r0, c0, c1, upper, cnt);
         return;
     }
-    const unsigned bid = blockIdx.x - (unsigned)rs.nrare;
+    const unsigned bid = blockIdx.x;
     int tile, ch;
     if (xmap) {
         // option sparse_xcd: workgroup b = 8 (t + ntiles g) + x runs chunk
@@ -1288,7 +1291,7 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
 }
 
 // The rare tier's pairs of a region are recounted in every step by the
-// leading workgroups of the sparse tile launch (rare_slab_row above) into a
+// trailing workgroups of the sparse tile launch (rare_slab_row above) into a
 // per-tile slab the chunk reduce adds. The plan keeps only geometry: the
 // region's (row block, column block) -> tile map and the slab's allocation.
 // Taken when the tier is small and its lists short (a row's thread walks a
@@ -1444,10 +1447,9 @@ bool sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     const int sun = (int)ctx->option(OPT_SPARSE_SUN, 3);
     GD_REQUIRE(sun >= 2 && sun <= 4, "sparse_sun: 2, 3 or 4");
     auto kern = sun == 2 ? sparse_tile_kernel<2> : sun == 4 ? sparse_tile_kernel<4> : sparse_tile_kernel<3>;
-    // the rare tier's pairs of this step: the launch's leading workgroups
+    // the rare tier's pairs of this step: the launch's trailing workgroups
     const bool rare = sc.use_part && sc.rare_in;
-    const bool timed = ctx->option(OPT_TIME_SPARSE, 0) != 0 && !ctx->capturing;
-    if (timed) GD_HIP(hipEventRecord(ctx->ev_sp0, st));
+    FamilyTimer ft(ctx, GDIST_KERNEL_SPARSE, st);
     const bool xmap = ctx->option(OPT_SPARSE_XCD, 0) != 0;
     RareSlab rs;
     if (rare) {
@@ -1469,10 +1471,7 @@ bool sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
                                          s->Wd, s->nsets, s->dbits.as<unsigned long long>(), s->sp_fold_slabs,
                                          group_part(s), xmap ? 1 : 0, (int)nt, rs);
     GD_HIP(hipGetLastError());
-    if (timed) {
-        GD_HIP(hipEventRecord(ctx->ev_sp1, st));
-        ctx->sp_timed = true;
-    }
+    ft.end();
     if (sc.use_part) {
         sparse_reduce_kernel<<<(unsigned)(nt * (SB * SB / kReduceCnt / kReduceGroups)), 256, 0, st>>>(
             sc.part.as<int32_t>(), nchunks, sc.tiles.as<int2>(), s->sp_nc.as<int32_t>(), s->sp_U, r0, r1, c0, c1,

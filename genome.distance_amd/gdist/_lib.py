@@ -86,7 +86,7 @@ _SIGS = {
     "gdist_ctx_synchronize": (C.c_int, [_ctxp]),
     "gdist_ctx_last_timing": (C.c_int, [_ctxp, _dblp, _dblp, _i64p]),
     "gdist_ctx_recent_timings": (C.c_int, [_ctxp, C.c_int, _dblp, C.POINTER(C.c_int)]),
-    "gdist_ctx_sparse_kernel_ms": (C.c_int, [_ctxp, _dblp]),
+    "gdist_ctx_kernel_ms": (C.c_int, [_ctxp, C.c_int, _dblp]),
     "gdist_ctx_set_option": (C.c_int, [_ctxp, C.c_char_p, _i64]),
     "gdist_ctx_get_option": (C.c_int, [_ctxp, C.c_char_p, _i64p, C.POINTER(C.c_int)]),
     "gdist_ctx_option_name": (C.c_int, [C.c_int, C.POINTER(C.c_char_p)]),

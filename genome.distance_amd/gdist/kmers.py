@@ -109,11 +109,14 @@ class Context:
         L.check(L.lib.gdist_ctx_last_timing(self.h, C.byref(k), C.byref(c), C.byref(n)))
         return k.value, c.value, n.value
 
-    def sparse_kernel_ms(self) -> float:
-        """HIP-event ms of the sparse tile kernel in the last call made with
-        option time_sparse = 1 (-1: none timed)."""
+    KERNEL_FAMILIES = {"sparse": 0, "rare": 1, "dense": 2, "sorted": 3}
+
+    def kernel_ms(self, family: str) -> float:
+        """HIP-event ms of one kernel family's launches (sparse / rare / dense /
+        sorted) in the last call made with option time_kernels = 1 (-1: that
+        family was not timed)."""
         v = C.c_double()
-        L.check(L.lib.gdist_ctx_sparse_kernel_ms(self.h, C.byref(v)))
+        L.check(L.lib.gdist_ctx_kernel_ms(self.h, self.KERNEL_FAMILIES[family], C.byref(v)))
         return v.value
 
     def recent_timings(self, n: int) -> list[float]:

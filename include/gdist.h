@@ -129,10 +129,17 @@ int  gdist_ctx_last_timing(gdist_ctx* ctx, double* kernel_ms, double* call_ms, i
 /* Kernel times (ms, HIP events on the stream they ran on) of the last
  * min(max, 256) matrix calls, oldest first, *count of them; waits for them. */
 int  gdist_ctx_recent_timings(gdist_ctx* ctx, int max, double* kernel_ms, int* count);
-/* HIP-event time (ms) of the sparse tile kernel alone in the last matrix call
- * made with option "time_sparse" = 1 (such calls are not graph-replayed);
- * -1 when none was timed. Waits for it. */
-int  gdist_ctx_sparse_kernel_ms(gdist_ctx* ctx, double* ms);
+/* HIP-event time (ms) of one kernel family's launches alone, on the stream
+ * they ran on, in the last matrix call made with option "time_kernels" = 1
+ * (such calls are not graph-replayed); -1 when that family was not timed.
+ * Waits for it. Families: the sparse tile launch (with the rare rows it
+ * carries), the rare-tier kernel (list- or row-major), the dense tile
+ * launches, the sorted join. */
+#define GDIST_KERNEL_SPARSE 0
+#define GDIST_KERNEL_RARE   1
+#define GDIST_KERNEL_DENSE  2
+#define GDIST_KERNEL_SORTED 3
+int  gdist_ctx_kernel_ms(gdist_ctx* ctx, int family, double* ms);
 /* Tuning options of a context: the A/B switches of DESIGN.md §5 by name
  * ("rare_t", "bitset_diag", "sparse", "sparse_zmax", "sketch_k", ...;
  * gdist_ctx_option_name enumerates them, EINVAL past the last). Every option
