@@ -36,6 +36,15 @@ public final class GpuKmerSets implements AutoCloseable {
     static native void nSketchMatrix(long ctx, long sk, long r0, long r1, long c0, long c1, int flags,
                                      double[] out, int ld);
 
+    /** One device context (gdist_ctx): serialises its calls, shared by threads. */
+    public static final class Context implements AutoCloseable {
+        final long h;
+        public Context(int device) { this.h = nCtxCreate(device); }
+        /** a tuning option (gdist_ctx_set_option); results never change */
+        public void setOption(String name, long value) { nSetOption(h, name, value); }
+        @Override public void close() { nCtxDestroy(h); }
+    }
+
     private final long ctx;
     private long handle;
 
@@ -45,16 +54,61 @@ public final class GpuKmerSets implements AutoCloseable {
         this.handle = nPack(ctx, kind, k, 0, seqs);
     }
 
+    public GpuKmerSets(Context ctx, int kind, int k, byte[][] seqs) { this(ctx.h, kind, k, seqs); }
+
+    private GpuKmerSets(long ctx, long handle) {
+        this.ctx = ctx;
+        this.handle = handle;
+    }
+
+    /** the number of sets */
     public long size() { return nSize(handle); }
+
+    /** SequenceKmers.size() of every set */
+    public long[] sizes() {
+        long[] out = new long[(int) size()];
+        nSizes(handle, out);
+        return out;
+    }
+
+    /** the two-tier bitsets now (otherwise the first distance call decides, METHOD_AUTO) */
+    public void buildBitsets() { nBuildBitsets(handle, 0); }
+
+    /** the representation METHOD_AUTO picks for `pairs` pairs (METHOD_BITSET / METHOD_SORTED) */
+    public int prepare(double pairs) { return nPrepare(ctx, handle, METHOD_AUTO, pairs); }
 
     /** distances of rows [r0, r1) x columns [c0, c1), row-major with stride ld */
     public void distances(long r0, long r1, long c0, long c1, boolean upperTriangle, double[] out, int ld) {
         nMatrix(ctx, handle, r0, r1, c0, c1, METHOD_AUTO, upperTriangle ? UPPER_TRIANGLE : 0, out, ld);
     }
 
+    /** anyMatch(d <= maxDist) of set q against cols (DistanceRepsProcessor.java:190) */
     public boolean anyWithin(long q, long[] cols, double maxDist) { return nAnyLe(ctx, handle, q, cols, maxDist); }
 
+    /** the distances of set q to cols */
     public void row(long q, long[] cols, double[] out) { nRow(ctx, handle, q, cols, out); }
+
+    /** argmin over cols (DistanceRepsProcessor.java:238-239): the position in cols,
+     *  -1 when none is below 1.0; bestD[0] = its distance */
+    public int closest(long q, long[] cols, double[] bestD) { return nArgmin(ctx, handle, q, cols, bestD); }
+
+    /** Both passes of DistanceRepsProcessor.java:185-262 in one call: isRep[i] = 1
+     *  for representatives (in set order, greedy); repOf / repDist = each set's
+     *  closest representative. tieRank (optional) = repMap's iteration order of
+     *  the representatives, which breaks argmin ties as the reference's reduce does.
+     *  Every array holds one element per set. Returns the number of representatives. */
+    public long greedyReps(double maxDist, long[] tieRank, int[] isRep, long[] repOf, double[] repDist) {
+        return nGreedyReps(ctx, handle, maxDist, tieRank, isRep, repOf, repDist);
+    }
+
+    /** hashSet(width) of every set, as a sketch collection (WidthProcessor.java:178) */
+    public GpuKmerSets sketches(int width) { return new GpuKmerSets(ctx, nSketch(ctx, handle, width)); }
+
+    /** Sketch.distance of rows [r0, r1) x columns [c0, c1) of a sketch collection
+     *  (WidthProcessor.java:183-185), row-major with stride ld */
+    public void sketchDistances(long r0, long r1, long c0, long c1, boolean upperTriangle, double[] out, int ld) {
+        nSketchMatrix(ctx, handle, r0, r1, c0, c1, upperTriangle ? UPPER_TRIANGLE : 0, out, ld);
+    }
 
     @Override
     public synchronized void close() {

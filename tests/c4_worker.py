@@ -1,0 +1,118 @@
+"""Worker of tests/test_gpu_fullsize.py::test_c4_full_size_slices_vs_oracle:
+C4 at its bench size on one GPU, in its own process (RCCL communicator, the
+160 GB of gathered codes released at exit).
+
+C4 = 100,000 synthetic 100 kbp genomes, DNA k=21 both strands, p <= 0.05,
+cfg seed 4 (bench.py CONFIGS["c4"]). On the 8-GPU node every rank packs its
+shard and ONE in-place code all-gather gives every rank all 100,000 sets
+(DESIGN.md §6); here one GPU holds the whole collection, packed from one host
+buffer, and the same consuming all-gather runs through ncclAllGather on a
+one-rank communicator (the path `bench.py --config c4 --rows A:B
+--force-exchange` takes). Then the per-rank slices the bench times: rank 0's
+rows 0-63 and the first rows of the last rank's block
+(gdist.shard.triangle_bounds(100000, 8)), each against every column
+(FastaDistanceProcessor.java:157-186: the pair loop of a row block).
+
+Checked against the CPU oracle (the checker): rows 0, 63 and the last
+block's first row in full — oracle.kmer_codes of every genome, threaded,
+intersected with the three row sets — bit-exact counts and fp64 distances.
+Progress lines go to stdout and to gpurun_out/c4_worker.log (a long run that
+keeps writing is not taken for a hung one).
+"""
+import concurrent.futures as cf
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "genome.distance_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import gdist  # noqa: E402
+import oracle  # noqa: E402  (test infrastructure: the checker)
+from gdist import shard, synth  # noqa: E402
+
+N, L, P, CFG, K = 100_000, 100_000, 0.05, 4, 21
+T0 = time.time()
+LOG = os.path.join(ROOT, "gpurun_out", "c4_worker.log")
+
+
+def log(msg):
+    line = f"[c4 {time.time() - T0:7.1f}s] {msg}"
+    print(line, flush=True)
+    try:
+        os.makedirs(os.path.dirname(LOG), exist_ok=True)
+        with open(LOG, "a") as f:
+            f.write(line + "\n")
+    except OSError:
+        pass
+
+
+def threads():
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    return max(1, min(aff, int(omp))) if omp.isdigit() and int(omp) > 0 else max(1, min(aff, 16))
+
+
+def main():
+    ctx = gdist.Context(0)
+    ctx.comm_init(gdist.Context.unique_id(), 1, 0)
+    g = synth.genomes(N, L, P, CFG)
+    blob, off = synth.to_blob(g)
+    del g
+    log(f"generated {N} x {L} bp")
+    local = gdist.KmerSets.from_blob(blob, off, K, gdist.KmerType.DNA, 0, ctx)
+    sizes = local.sizes()
+    log(f"packed: {int(sizes.sum())} codes")
+    m, bb, bc = local.exchange_plan()
+    assert m == gdist.METHOD_SORTED, ("C4 must take the code all-gather", m, bb, bc)
+    gs = local.allgather(consume=True)
+    assert len(gs) == N and np.array_equal(gs.sizes(), sizes)
+    log(f"consuming code all-gather done (estimates: bitsets {bb:.3g} B, codes {bc:.3g} B per rank)")
+    bounds = shard.triangle_bounds(N, 8, 1)
+    last = bounds[7]
+    slices = [(0, 64), (last, last + 16)]
+    rows = {0: None, 63: None, last: None}
+    for (a, b) in slices:
+        t = time.time()
+        I, D = gs.matrix((a, b), (0, N), upper=True, method=gdist.METHOD_SORTED)
+        log(f"slice rows [{a}, {b}) x {N} columns: {time.time() - t:.2f} s")
+        for i in rows:
+            if a <= i < b:
+                rows[i] = (I[i - a].copy(), D[i - a].copy())
+        del I, D
+    # the oracle: every genome's codes, intersected with the three row sets
+    row_ids = sorted(rows)
+    row_codes = [oracle.kmer_codes(bytes(blob[off[i]:off[i + 1]]), K, 0, 0) for i in row_ids]
+    assert [len(c) for c in row_codes] == [int(sizes[i]) for i in row_ids]
+
+    def column(j):
+        cj = oracle.kmer_codes(bytes(blob[off[j]:off[j + 1]]), K, 0, 0)
+        return len(cj), [oracle.intersect(rc, cj) for rc in row_codes]
+
+    eI = np.zeros((len(row_ids), N), np.int64)
+    nb = np.zeros(N, np.int64)
+    with cf.ThreadPoolExecutor(threads()) as ex:
+        for j0 in range(0, N, 10_000):
+            for j, (n_j, inter) in zip(range(j0, min(N, j0 + 10_000)), ex.map(column, range(j0, min(N, j0 + 10_000)))):
+                nb[j] = n_j
+                eI[:, j] = inter
+            log(f"oracle columns {min(N, j0 + 10_000)} / {N}")
+    assert np.array_equal(nb, sizes)
+    for r, i in enumerate(row_ids):
+        I, D = rows[i]
+        js = np.arange(i + 1, N)
+        assert np.array_equal(I[js].astype(np.int64), eI[r, js]), (i, js[I[js] != eI[r, js]][:8])
+        eD = np.array([oracle.distance(int(eI[r, j]), len(row_codes[r]), int(nb[j])) for j in js])
+        assert np.array_equal(D[js].view(np.uint64), eD.view(np.uint64)), i
+        log(f"row {i}: {len(js)} pairs bit-exact")
+    ctx.comm_destroy()
+    print("C4_OK", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -15,11 +15,18 @@
   k=21; WidthProcessor.java:178-185): the device sketches of a sample of
   genomes against oracle.sketch, and full rows of the bench's whole-triangle
   sketch matrix against oracle.sketch_distance over every column.
+* C4 at its bench size (100,000 x 100 kbp, DNA k=21, p <= 0.05) on one GPU,
+  in a subprocess (tests/c4_worker.py): the consuming code all-gather on a
+  one-rank RCCL communicator, then rank 0's rows 0-63 and the last rank's
+  first rows of the 8-GPU partition against every column; three rows in full
+  against the oracle.
 * The round-1 fault sequence (a sorted and a bitset workload, then a pack, in
   one process) with its codes checked against the oracle.
 """
 import concurrent.futures as cf
 import os
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -210,3 +217,13 @@ def test_pack_after_bitset_workload_regression(ctx):
         Ia, _ = a.matrix(method=gdist.METHOD_BITSET)
         assert np.array_equal(Ia, eI), trial
         del a
+
+
+@pytest.mark.timeout(1150)
+def test_c4_full_size_slices_vs_oracle():
+    """C4 (BASELINE configs[3]) at its size: see tests/c4_worker.py."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, "-u", os.path.join(here, "c4_worker.py")], capture_output=True, text=True,
+                       timeout=1100)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
+    assert "C4_OK" in r.stdout
