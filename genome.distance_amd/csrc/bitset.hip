@@ -613,12 +613,14 @@ void bitset_row(gdist_ctx* ctx, const gdist_sets* s, int64_t q, const int64_t* d
     bitset_row_kernel<<<(unsigned)ceil_div(ncols, 4), 256, 0, ctx->stream>>>(s->bits.as<unsigned long long>(), s->W,
                                                                              q, d_cols, ncols, d_I);
     GD_HIP(hipGetLastError());
-    if (s->n_rare > 0) {
+    if (s->n_rare > 0 || s->variant) {
         DevBuf cnt(s->nsets * 4 + 4, ctx->stream);
         GD_HIP(hipMemsetAsync(cnt.p, 0, s->nsets * 4, ctx->stream));
-        rare_query_kernel<<<256, 256, 0, ctx->stream>>>(s->srare_off.as<int64_t>(), s->srare_ent.as<uint64_t>(),
-                                                        s->srare_w.as<uint32_t>(), s->post_sets.as<uint32_t>(), q,
-                                                        cnt.as<int32_t>());
+        if (s->n_rare > 0)
+            rare_query_kernel<<<256, 256, 0, ctx->stream>>>(s->srare_off.as<int64_t>(), s->srare_ent.as<uint64_t>(),
+                                                            s->srare_w.as<uint32_t>(), s->post_sets.as<uint32_t>(), q,
+                                                            cnt.as<int32_t>());
+        variant_query(ctx, s, q, cnt.as<int32_t>());
         gather_add_kernel<<<(unsigned)ceil_div(ncols, 256), 256, 0, ctx->stream>>>(d_cols, ncols, cnt.as<int32_t>(),
                                                                                    d_I);
         GD_HIP(hipGetLastError());
@@ -1285,14 +1287,15 @@ __global__ __launch_bounds__(1024) void pos_bits_kernel(const uint32_t* __restri
 // rare-tier records appended to rare_out (capacity cap)
 void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_t U, int64_t W,
                unsigned long long* bits, const uint64_t* rare, int64_t Ur, int64_t id_base,
-               unsigned long long* rare_out, int64_t rare_cap, int64_t* rare_written, const uint32_t* perm) {
+               unsigned long long* rare_out, int64_t rare_cap, int64_t* rare_written, const uint32_t* perm,
+               const FillHook& hook) {
     hipStream_t st = ctx->stream;
     const int cbits = std::min(64, code_bits(s->kind, s->k, s->flags));
     Trace tr(st, ctx->trace());
     GD_HIP(hipMemsetAsync(bits, 0, (size_t)s->nsets * W * 8, st));
     DevBuf rcnt(8, st);
     GD_HIP(hipMemsetAsync(rcnt.p, 0, 8, st));
-    const int64_t mode = ctx->option(OPT_FILL_SORT, 0);
+    const int64_t mode = hook ? 0 : ctx->option(OPT_FILL_SORT, 0);   // the hook needs the position arrays
     if (U + Ur > 0 && mode == 0) {
         GD_REQUIRE(s->nsets < (int64_t(1) << 23) && s->h_off[s->nsets] < (int64_t(1) << 40),
                    "collection too large for packed fill segments");
@@ -1333,6 +1336,7 @@ void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_
                 GD_HIP(hipGetLastError());
             }
             tr.mark("fill: merged positions");
+            if (hook) hook(pos.as<uint32_t>(), s0, s1, base);
             for (int64_t c0 = s0; c0 < s1; c0 += 65535) {
                 const unsigned ny = (unsigned)std::min<int64_t>(65535, s1 - c0);
                 pos_bits_kernel<<<dim3(nslice, ny), 1024, 0, st>>>(pos.as<uint32_t>(), s->off.as<int64_t>(), c0, base,
@@ -1635,13 +1639,38 @@ void build_bitsets(gdist_ctx* ctx, gdist_sets* s, unsigned flags, int64_t rare_t
     int64_t T = keep ? 0 : rare_threshold;     // < 0: cost-optimal from the count histogram
     Trace tr(ctx->stream, ctx->trace());
     Summary sum;
-    local_summary(ctx, s, sum);
+    // a collection without pack summaries and too many codes for one sort
+    // (a gathered 8-GPU collection: C4's 2e10 codes) is counted by code
+    // ranges, singletons dropped as they are counted (option range_summary)
+    const int64_t rs_opt = ctx->option(OPT_RANGE_SUMMARY, -1);
+    const bool by_range = rs_opt > 0 || (rs_opt < 0 && s->pack_sum.empty() && s->total > kRangeSummaryMin);
+    if (by_range) range_summary(ctx, s, keep ? 1 : 2, sum);
+    else local_summary(ctx, s, sum);
     tr.mark("bitsets: summary");
     DevBuf dict, rare, dcnt;
     int64_t U = 0, Ur = 0, mass = 0;
+    const int64_t T_in = T;
     dictionary_from(ctx, {SummaryView{sum.codes.as<uint64_t>(), sum.counts.as<uint32_t>(), sum.n}}, keep, T, s->nsets,
                     dict, U, rare, Ur, mass, &dcnt);
     tr.mark("bitsets: dictionary");
+    // the variant tier when kmers held by T .. Dmin - 1 sets dominate the
+    // dictionary (variant.hip); its rare threshold is at most kVariantMaxT
+    // unless given: kmers shared by a few sets stay posting lists, the rest
+    // of the non-dense kmers form the variant words
+    if (!keep) {
+        const int64_t dmin = variant_dmin(ctx, s->nsets);
+        if (variant_wanted(ctx, s->nsets, count_below(ctx, dcnt.as<uint32_t>(), U, dmin), U)) {
+            if (T_in < 0 && !ctx->has_option(OPT_RARE_T) && T > kVariantMaxT) {
+                T = kVariantMaxT;
+                dictionary_from(ctx, {SummaryView{sum.codes.as<uint64_t>(), sum.counts.as<uint32_t>(), sum.n}}, false,
+                                T, s->nsets, dict, U, rare, Ur, mass, &dcnt);
+            }
+            sum.codes.release();
+            sum.counts.release();
+            build_variant_bitsets(ctx, s, dict, dcnt, U, rare, Ur, mass, T);
+            return;
+        }
+    }
     const int64_t W = bitset_words(U);
     DevBuf perm;
     if (s->n_guide > 0 && locus_order_enabled(ctx)) {
@@ -1719,6 +1748,14 @@ static void dense_tiles(int64_t r0, int64_t r1, int64_t c0, int64_t c1, bool upp
     }
 }
 
+// the variant tier's row walk: its share of the products, and one list
+// search per (entry of the block's rows, column chunk)
+static double variant_cost_s(const gdist_sets* s, double f_area, double f_rows, double ncols) {
+    if (!s->variant) return 0.0;
+    return f_area * s->vw_products / kVariantProductsPerS +
+           f_rows * (double)s->vw_entries * std::ceil(ncols / 16384.0) / kVariantVisitsPerS;
+}
+
 double bitset_block_cost_s(const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1, bool upper,
                            bool* rare_row_major) {
     const double n = (double)s->nsets, tot = 0.5 * n * (n - 1.0);
@@ -1747,7 +1784,9 @@ double bitset_block_cost_s(const gdist_sets* s, int64_t r0, int64_t r1, int64_t 
                                 (double)s->rare_records + (double)s->rare_incs <= double(int64_t(1) << 26);
     return (off + kDiagTileShare * diag) * (double)(BT * BT) * tW / kDenseWordPairsPerS +
            (rare_in_reduce ? rc.list_s * kRareOverlapExposed : rc.cost()) +
-           sparse_block_cost_s(s, tot > 0 ? std::min(1.0, pairs / tot) : 1.0, sp_tiles);
+           sparse_block_cost_s(s, tot > 0 ? std::min(1.0, pairs / tot) : 1.0, sp_tiles) +
+           variant_cost_s(s, tot > 0 ? std::min(1.0, pairs / tot) : 1.0, n > 0 ? (double)(r1 - r0) / n : 1.0,
+                          (double)(c1 - c0));
 }
 
 double bitset_cost_s(const gdist_sets* s, double pairs) {
@@ -1756,7 +1795,8 @@ double bitset_cost_s(const gdist_sets* s, double pairs) {
     const double frac = tot > 0 ? std::min(1.0, pairs / tot) : 1.0;
     const double tW = s->sparse ? (s->sp_fold_dense ? 0.0 : (double)s->Wd) : (double)s->W;
     return pairs * tW / kDenseWordPairsPerS + rare_choice(rare_tier(s), frac, frac).cost() +
-           sparse_block_cost_s(s, frac, pairs / (double)(BT * BT) + std::sqrt(2.0 * pairs) / BT);
+           sparse_block_cost_s(s, frac, pairs / (double)(BT * BT) + std::sqrt(2.0 * pairs) / BT) +
+           variant_cost_s(s, frac, frac, (double)s->nsets);
 }
 
 double sorted_cost_s(const gdist_sets* s, double pairs) {
@@ -1767,6 +1807,7 @@ double sorted_cost_s(const gdist_sets* s, double pairs) {
 
 void free_bitsets(gdist_sets* s) {
     free_sparse(s);                      // (synchronises both streams, clears plans and graphs)
+    free_variant(s);
     s->bits.release();
     s->post_off.release();
     s->post_sets.release();
@@ -1874,8 +1915,9 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     // (round 3, C3: its scattered list reads overlap the VALU-bound tiles)
     const bool rows_side = s->n_rare > 0 && !list_major && !s->sparse && ctx->option(OPT_RARE_OVERLAP, 1) != 0;
     // The sparse words and the list-major rare kernel add atomically, like
-    // the dense tiles, so they run on the side stream beside them.
-    const bool side = overlap || s->sparse || rows_side;
+    // the dense tiles, so they run on the side stream beside them; so does
+    // the variant tier's row walk (variant.hip)
+    const bool side = overlap || s->sparse || rows_side || s->variant;
     bool rare_done = false;               // the sparse chunk reduce added the rare pairs
     auto launch_rare_rows = [&](hipStream_t rs, bool atomic_flush) {
         const int nch = (int)ceil_div(nc, RCH);
@@ -1915,6 +1957,7 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
         // sparse tiles and their reduce end: C2 0.0185 ms in line there)
         if (overlap && !s->sparse) launch_rare_pairs(ctx->side);
         if (rows_side) launch_rare_rows(ctx->side, true);
+        if (s->variant) variant_matrix(ctx, s, r0, r1, c0, c1, upper, d_I, ldI, ctx->side);
         GD_HIP(hipGetLastError());
         GD_HIP(hipEventRecord(ctx->ev_join, ctx->side));
     }
@@ -1992,7 +2035,7 @@ bool bitset_matrix_fused(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_
     // zeroing) and writes D (no epilogue launch). Only when every count of
     // the region comes from that reduce: sparse tier, no dense-word launch,
     // chunk partials, the rare pairs in its table (or no rare tier).
-    if (!s->sparse || !d_D || ctx->option(OPT_SPARSE_FUSED, 1) == 0) return false;
+    if (!s->sparse || s->variant || !d_D || ctx->option(OPT_SPARSE_FUSED, 1) == 0) return false;
     if (r1 <= r0 || c1 <= c0 || !(s->sp_fold_dense || s->Wd == 0)) return false;
     MatrixPlan& p = matrix_plan(ctx, s, r0, r1, c0, c1, upper);
     sparse_plan(ctx, s, r0, r1, c0, c1, upper, ctx->stream, p.sparse);

@@ -579,6 +579,16 @@ int gdist_sets_sparse_info(const gdist_sets* s, int64_t* sparse_words, int64_t* 
     });
 }
 
+int gdist_sets_variant_info(const gdist_sets* s, int64_t* kmers, int64_t* words, int64_t* entries, double* products) {
+    return guard([&] {
+        check_sets(s);
+        if (kmers) *kmers = s->variant ? s->vw_kmers : 0;
+        if (words) *words = s->variant ? s->vw_words : 0;
+        if (entries) *entries = s->variant ? s->vw_entries : 0;
+        if (products) *products = s->variant ? s->vw_products : 0.0;
+    });
+}
+
 int gdist_sets_sparse_sides(const gdist_sets* s, int64_t* complement_words, int64_t* positive_words) {
     return guard([&] {
         check_sets(s);

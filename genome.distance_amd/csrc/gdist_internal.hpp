@@ -8,6 +8,7 @@
 #include <rccl/rccl.h>
 
 #include <climits>
+#include <functional>
 #include <cstdint>
 #include <map>
 #include <memory>
@@ -213,7 +214,10 @@ struct Timing {
     X(PACK_CODES_BUDGET, "pack_codes_budget") /* bytes of the one-buffer pack (default 1/4 HBM; past it: grown) */\
     X(SPARSE_GROUPS, "sparse_groups")         /* 0: no group tier (clade patterns) in the sparse words */       \
     X(SPARSE_XCD, "sparse_xcd")               /* 1: chunk c of every sparse tile on XCD c mod 8 */           \
-    X(RARE_U16, "rare_u16")                   /* 0: 4-byte list members in the row-major rare walk */
+    X(RARE_U16, "rare_u16")                   /* 0: 4-byte list members in the row-major rare walk */        \
+    X(VARIANT, "variant")                     /* variant tier: 1 force, 0 off (default: by the dictionary) */ \
+    X(VARIANT_DMIN, "variant_dmin")           /* sets holding a dense-tier kmer (default N / 10) */            \
+    X(RANGE_SUMMARY, "range_summary")         /* 1: the code-range dictionary whatever the size, 0: never */
 
 enum Opt : int {
 #define GDIST_OPT_ENUM(id, name) OPT_##id,
@@ -262,7 +266,7 @@ struct gdist_ctx {
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     // option time_kernels: each kernel family's launches alone (uncaptured
     // calls), by family (GDIST_KERNEL_SPARSE / RARE / DENSE / SORTED)
-    static constexpr int kFamilies = 4;
+    static constexpr int kFamilies = 5;
     hipEvent_t ev_kf0[kFamilies] = {}, ev_kf1[kFamilies] = {};
     bool kf_timed[kFamilies] = {};
     gdist::Timing last;
@@ -364,6 +368,17 @@ struct gdist_sets {
     // chunk's summary; local_summary merges them instead of re-sorting codes
     std::vector<gdist::Summary> pack_sum;
     double sp_products = 0, sp_items = 0; // whole-triangle products / (tile, word) visits (cost model)
+    // variant tier (variant.hip): kmers held by T .. Dmin - 1 sets in 64-kmer
+    // words grouped by substitution; per word a list of (set, mask) entries,
+    // sets ascending; the set -> entry CSR for the row walk
+    bool variant = false;
+    int64_t vw_words = 0, vw_entries = 0, vw_kmers = 0, vw_dmin = 0, vw_max_list = 0;
+    double vw_products = 0;               // sum over words of z (z - 1) / 2
+    gdist::DevBuf vw_set;                 // uint32 [E] (grouped by word, ascending set)
+    gdist::DevBuf vw_mask;                // uint64 [E]
+    gdist::DevBuf vw_beg, vw_end;         // uint32 [E]: the entry's word list
+    gdist::DevBuf vs_off;                 // int64 [nsets + 1]
+    gdist::DevBuf vs_ent;                 // uint32 [E]: entries by set
     bool auto_sorted = false;             // METHOD_AUTO measured the sorted join cheaper
     // bitset_matrix launch plans by (region, kernel switches); cleared with the bitsets
     mutable std::map<std::vector<int64_t>, std::unique_ptr<gdist::MatrixPlan>> plans;
@@ -419,10 +434,14 @@ int64_t auto_rare_threshold(int64_t nsets);
 // (c = 0..nsets); the chosen T is reported by gdist_sets_rare_info
 int64_t choose_rare_threshold(const std::vector<uint64_t>& hist, int64_t nsets);
 // perm (optional): bit position of each dense rank (locus order)
+// hook (optional, default fill only): called per chunk of sets [s0, s1)
+// with the chunk's position array (u32 per code from code `base`; ~0 outside
+// the dictionary) before it is released (variant.hip: the variant records)
+using FillHook = std::function<void(const uint32_t* pos, int64_t s0, int64_t s1, int64_t base)>;
 void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_t U, int64_t W,
                unsigned long long* bits, const uint64_t* rare, int64_t Ur, int64_t id_base,
                unsigned long long* rare_out, int64_t rare_cap, int64_t* rare_written,
-               const uint32_t* perm = nullptr);
+               const uint32_t* perm = nullptr, const FillHook& hook = FillHook());
 void build_postings(gdist_ctx* ctx, gdist_sets* s, unsigned long long* recs, int64_t n, int64_t Ur);
 // Cost model (seconds), calibrated on MI355X from per-kernel rocprofv3
 // averages (scripts/calib_rare.sh; profiles/r01/rare_model): bitset = dense
@@ -509,6 +528,26 @@ void sparse_plan(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, in
 // returns true when the rare tier's pairs were added with the sparse words
 bool sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1, bool upper,
                    int32_t* d_I, int64_t ldI, hipStream_t st, SparseScratch& sc, const SparseEpilogue* ep = nullptr);
+
+// variant.hip — the variant tier
+constexpr double kVariantProductsPerS = 2.0e10;  // variant_rows_kernel: popc products (estimate)
+constexpr int64_t kVariantMaxT = 32;             // rare threshold of a variant build (unless given)
+constexpr int64_t kRangeSummaryMin = int64_t(1) << 31;   // codes past which an unsummarised collection counts by range
+constexpr double kVariantVisitsPerS = 2.0e9;     // ... (entry, column chunk) visits with their list search
+int64_t variant_dmin(const gdist_ctx* ctx, int64_t nsets);
+bool variant_wanted(const gdist_ctx* ctx, int64_t nsets, int64_t mid_kmers, int64_t dict_kmers);
+int64_t count_below(gdist_ctx* ctx, const uint32_t* dcounts, int64_t U, int64_t dmin);
+// builds bits (dense tier), the rare postings and the variant tier from the
+// dictionary (dict: codes held by >= T sets, dcounts their holders)
+void build_variant_bitsets(gdist_ctx* ctx, gdist_sets* s, DevBuf& dict, DevBuf& dcounts, int64_t U, DevBuf& rare,
+                           int64_t Ur, int64_t mass, int64_t T);
+void free_variant(gdist_sets* s);
+void variant_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1, bool upper,
+                    int32_t* d_I, int64_t ldI, hipStream_t rs);
+void variant_query(gdist_ctx* ctx, const gdist_sets* s, int64_t q, int32_t* cnt);
+// Summary of the codes held by >= min_count sets by ranges of the code space
+// (workspace: one range, not the collection: huge gathered collections)
+void range_summary(gdist_ctx* ctx, const gdist_sets* s, int min_count, Summary& out);
 
 // sorted.hip
 void build_segments(gdist_ctx* ctx, gdist_sets* s);

@@ -1,0 +1,932 @@
+// variant.hip — the variant tier of the two-tier dictionary: kmers held by
+// many sets but far from all (C4: 100,000 genomes of one 100 kbp ancestor at
+// up to 5 % substitutions, where every single-substitution kmer is shared by
+// ~500 genomes).
+//
+// Why a third tier. The dense tier costs every pair one AND+popcount per
+// 64-kmer word whether or not the pair holds any of the word's kmers; the
+// rare tier costs m(m-1)/2 increments per posting list of m sets. C4's
+// 12.6 M single-substitution kmers are neither: as dense words they would be
+// 200 K words a pair (1e15 word pairs on the triangle), as posting lists of
+// ~500 sets 1e12 increments. Grouped by the substitution that made them (a
+// substitution at one site makes the k windows covering it, on both strands,
+// 2k kmers held by nearly the same genomes), 64 to a word, each word is a
+// list of (set, 64-bit mask) entries, and a pair sharing the word adds
+// popc(mask_i & mask_j): the kmers of one substitution cost one product, not
+// 2k increments.
+//
+// Grouping needs no positions: a variant kmer's substitution shows as its
+// Hamming-1 neighbour in the dense tier (the ancestral kmer at the same
+// window), whose locus the guide sequences give (pack time, sparse.hip
+// locus_keys); (neighbour window + offset of the differing symbol, the
+// symbol) names the site and the letter on the forward strand, so both
+// strands' kmers of one substitution get one key. Kmers with no dense
+// neighbour (two substitutions in a window, no guide) keep code order after
+// the keyed ones. Any grouping is exact; it only decides how many products
+// the walk does.
+//
+// Tiers by the number of sets c holding a kmer: dense c >= Dmin (default
+// N / 10: bit columns of the tile kernels), variant T <= c < Dmin, rare
+// 2 <= c < T (posting lists), singletons dropped (they never intersect).
+//
+// Build (build_variant_bitsets, one GPU, from codes; C4 on 8 GPUs runs it on
+// every rank after the one code all-gather): a code-range dictionary
+// (range_summary: per range of the code space every set's codes of that
+// range gathered, sorted, counted, singletons dropped: the workspace is one
+// range, not the collection), the tiers, the variant keys and word order, one
+// fill pass over every set's codes (fill_bits with a hook: dense codes set
+// bits, variant codes emit (word, set, bit) records that are sorted and
+// OR-merged per set chunk), then the word lists and the set -> entry CSR.
+//
+// Walk (variant_rows_kernel, bitset_matrix): one workgroup per (row set,
+// column chunk); a wave takes one of the row's entries and its 64 lanes
+// stream the entry's word list (sets ascending, coalesced 4 + 8 bytes per
+// member) from the row's own position (upper triangle) or the chunk's first
+// column (a wave-uniform binary search), adding popc(mask_i & mask_j) into
+// LDS counters; the counters are added to I's row once.
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "gdist_internal.hpp"
+
+namespace gdist {
+namespace {
+
+inline int grid_for(int64_t n, int block = 256, int64_t cap = 256 * 32) {
+    int64_t g = ceil_div(n, block);
+    return (int)std::max<int64_t>(1, std::min<int64_t>(g, cap));
+}
+
+__device__ __forceinline__ int64_t lower_bound_u64(const uint64_t* __restrict__ a, int64_t lo, int64_t hi, uint64_t k) {
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (a[mid] < k) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+// ---- code-range dictionary ----------------------------------------------
+// splitter positions: spos[i * (P + 1) + p] = lower bound of splitter p in
+// set i's codes (p = 0: the set's start, p = P: its end)
+__global__ void range_pos_kernel(const uint64_t* __restrict__ codes, const int64_t* __restrict__ off, int64_t nsets,
+                                 const uint64_t* __restrict__ split, int P, int64_t* __restrict__ spos) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nsets * (P + 1)) return;
+    const int64_t i = t / (P + 1);
+    const int p = (int)(t % (P + 1));
+    const int64_t b = off[i], e = off[i + 1];
+    spos[t] = p == 0 ? b : p == P ? e : lower_bound_u64(codes, b, e, split[p - 1]);
+}
+
+// the sizes of range p per set -> cnt[i]
+__global__ void range_sizes_kernel(const int64_t* __restrict__ spos, int64_t nsets, int P, int p,
+                                   int64_t* __restrict__ cnt) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nsets) cnt[i] = spos[i * (P + 1) + p + 1] - spos[i * (P + 1) + p];
+}
+
+// gather range p of every set: one workgroup per set
+__global__ __launch_bounds__(256) void range_gather_kernel(const uint64_t* __restrict__ codes,
+                                                           const int64_t* __restrict__ spos, int P, int p,
+                                                           const int64_t* __restrict__ at, uint64_t* __restrict__ out) {
+    const int64_t i = blockIdx.x;
+    const int64_t b = spos[i * (P + 1) + p], e = spos[i * (P + 1) + p + 1];
+    uint64_t* o = out + at[i] - b;
+    for (int64_t x = b + threadIdx.x; x < e; x += 256) o[x] = codes[x];
+}
+
+__global__ void sample_kernel(const uint64_t* __restrict__ codes, int64_t first, int64_t stride, int64_t n,
+                              uint64_t* __restrict__ out) {
+    const int64_t gs = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gs) out[i] = codes[first + i * stride];
+}
+
+// heads of runs in sorted keys
+__global__ void heads_kernel(const uint64_t* __restrict__ k, int64_t n, int32_t* __restrict__ flag) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        flag[i] = (i == 0 || k[i] != k[i - 1]) ? 1 : 0;
+}
+
+// runs of >= min_count: (code, count) compacted; keep[] = 1 for kept heads
+__global__ void run_keep_kernel(const uint64_t* __restrict__ k, int64_t n, const int32_t* __restrict__ flag,
+                                int min_count, int32_t* __restrict__ keep, uint32_t* __restrict__ len) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        int32_t kp = 0;
+        uint32_t c = 0;
+        if (flag[i]) {
+            int64_t e = i + 1;
+            while (e < n && k[e] == k[i]) e++;
+            c = (uint32_t)(e - i);
+            kp = (int64_t)c >= min_count ? 1 : 0;
+        }
+        keep[i] = kp;
+        len[i] = c;
+    }
+}
+
+__global__ void run_emit_kernel(const uint64_t* __restrict__ k, const int32_t* __restrict__ keep,
+                                const uint32_t* __restrict__ len, const int64_t* __restrict__ pos, int64_t n,
+                                uint64_t* __restrict__ oc, uint32_t* __restrict__ on) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        if (keep[i]) { oc[pos[i]] = k[i]; on[pos[i]] = len[i]; }
+}
+
+// ---- tiers and the variant order -----------------------------------------
+__global__ void tier_flags_kernel(const uint32_t* __restrict__ cnt, int64_t n, uint32_t dmin,
+                                  int32_t* __restrict__ dense, int32_t* __restrict__ mid) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        dense[i] = cnt[i] >= dmin ? 1 : 0;
+        mid[i] = cnt[i] >= dmin ? 0 : 1;
+    }
+}
+
+__global__ void split_codes_kernel(const uint64_t* __restrict__ dict, const uint32_t* __restrict__ cnt, int64_t n,
+                                   const int32_t* __restrict__ dense, const int64_t* __restrict__ dpos,
+                                   const int64_t* __restrict__ mpos, uint64_t* __restrict__ dcodes,
+                                   uint32_t* __restrict__ dcnt, uint64_t* __restrict__ mcodes) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        if (dense[i]) { dcodes[dpos[i]] = dict[i]; dcnt[dpos[i]] = cnt[i]; }
+        else mcodes[mpos[i]] = dict[i];
+    }
+}
+
+// guide entry of every dense code (-1: no guide holds it): the locus
+__global__ void dense_entry_kernel(const uint64_t* __restrict__ dcodes, int64_t Ud,
+                                   const uint64_t* __restrict__ gcodes, const uint64_t* __restrict__ gkeys, int64_t ng,
+                                   int64_t* __restrict__ entry) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < Ud; r += stride) {
+        const int64_t g = lower_bound_u64(gcodes, 0, ng, dcodes[r]);
+        entry[r] = (g < ng && gcodes[g] == dcodes[r]) ? (int64_t)gkeys[g] : -1;
+    }
+}
+
+// Code geometry of a collection for the neighbour search: symbols of `bits`
+// bits, first symbol most significant; alphabet (the symbols a kmer can
+// hold) and the complement map of DNA.
+struct CodeGeom {
+    int k = 0, bits = 0, strands = 1;
+    int nalpha = 0;
+    uint8_t alpha[32] = {};
+    int8_t comp[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+};
+
+// Variant key of every variant-tier kmer: min over its Hamming-1 neighbours
+// in the dense tier that a guide holds of (site << 8 | forward letter), with
+// site = the neighbour's window + the offset of the differing symbol
+// (reversed on the reverse strand, whose letter is complemented); ~0 when no
+// keyed neighbour exists.
+__global__ __launch_bounds__(256) void variant_key_kernel(const uint64_t* __restrict__ mcodes, int64_t Um,
+                                                          const uint64_t* __restrict__ dcodes, int64_t Ud,
+                                                          const int64_t* __restrict__ dentry, CodeGeom g,
+                                                          uint64_t* __restrict__ vkey) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const uint64_t smask = (1ull << g.bits) - 1ull;
+    for (int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; m < Um; m += stride) {
+        const uint64_t c = mcodes[m];
+        uint64_t best = ~0ull;
+        for (int j = 0; j < g.k; j++) {
+            const int sh = (g.k - 1 - j) * g.bits;          // symbol j (0 = first, most significant)
+            const uint64_t cur = (c >> sh) & smask;
+            for (int a = 0; a < g.nalpha; a++) {
+                const uint64_t s = g.alpha[a];
+                if (s == cur) continue;
+                const uint64_t nb = (c & ~(smask << sh)) | (s << sh);
+                const int64_t r = lower_bound_u64(dcodes, 0, Ud, nb);
+                if (r >= Ud || dcodes[r] != nb || dentry[r] < 0) continue;
+                const int64_t e = dentry[r];
+                const int64_t w = e / g.strands, strand = e % g.strands;
+                int64_t site;
+                uint64_t letter;
+                if (strand == 0) { site = w + j; letter = cur; }
+                else { site = w + (g.k - 1 - j); letter = (uint64_t)(g.comp[cur] < 0 ? cur : g.comp[cur]); }
+                const uint64_t key = ((uint64_t)site << 8) | letter;
+                best = key < best ? key : best;
+            }
+        }
+        vkey[m] = best;
+    }
+}
+
+// group heads of the sorted keys (a keyless kmer is a group of its own) ->
+// words of the group: ceil(len / 64), each group starting a new word
+__global__ void group_words_kernel(const uint64_t* __restrict__ k, int64_t n, int32_t* __restrict__ head,
+                                   int64_t* __restrict__ words) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const bool h = i == 0 || k[i] != k[i - 1] || k[i] == ~0ull;
+        head[i] = h ? 1 : 0;
+        int64_t wn = 0;
+        if (h) {
+            int64_t e = i + 1;
+            if (k[i] == ~0ull) e = n;                        // the keyless kmers: one group, packed
+            else while (e < n && k[e] == k[i]) e++;
+            wn = ceil_div(e - i, 64);
+            if (k[i] == ~0ull && i > 0 && k[i - 1] == ~0ull) wn = 0;
+        }
+        words[i] = wn;
+    }
+}
+
+// the variant position of every variant kmer (sorted index q -> word of its
+// group + offset): perm over the combined dictionary's variant ranks
+__global__ void group_pos_kernel(const uint64_t* __restrict__ k, const int32_t* __restrict__ order, int64_t n,
+                                 const int64_t* __restrict__ wstart, uint32_t base, uint32_t* __restrict__ mpos) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        // the group's head: the first index with the same key (keyless: the first keyless)
+        int64_t lo = 0, hi = i;
+        const uint64_t key = k[i];
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (k[mid] < key) lo = mid + 1; else hi = mid;
+        }
+        mpos[order[i]] = base + (uint32_t)(wstart[lo] * 64 + (i - lo));
+    }
+}
+
+// combined perm over the dictionary (dense + variant ranks in code order)
+__global__ void combine_perm_kernel(const int32_t* __restrict__ dense, const int64_t* __restrict__ dpos,
+                                    const int64_t* __restrict__ mpos_idx, int64_t n,
+                                    const uint32_t* __restrict__ dperm, const uint32_t* __restrict__ mperm,
+                                    uint32_t* __restrict__ perm) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += stride)
+        perm[r] = dense[r] ? (dperm ? dperm[dpos[r]] : (uint32_t)dpos[r]) : mperm[mpos_idx[r]];
+}
+
+// ---- variant records of one fill chunk -----------------------------------
+// per set of the chunk: its variant positions (>= vbase) counted, then
+// written as keys (word << (sbits + 6) | set << 6 | bit)
+__global__ __launch_bounds__(256) void vrec_count_kernel(const uint32_t* __restrict__ pos,
+                                                         const int64_t* __restrict__ off, int64_t s0, int64_t base,
+                                                         uint32_t vbase, int64_t* __restrict__ cnt) {
+    __shared__ int64_t red[256];
+    const int64_t i = s0 + blockIdx.x;
+    int64_t c = 0;
+    for (int64_t x = off[i] - base + threadIdx.x; x < off[i + 1] - base; x += 256) {
+        const uint32_t p = pos[x];
+        c += p != ~0u && p >= vbase;
+    }
+    red[threadIdx.x] = c;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) cnt[blockIdx.x] = red[0];
+}
+
+__global__ __launch_bounds__(256) void vrec_write_kernel(const uint32_t* __restrict__ pos,
+                                                         const int64_t* __restrict__ off, int64_t s0, int64_t base,
+                                                         uint32_t vbase, int sbits, const int64_t* __restrict__ at,
+                                                         uint64_t* __restrict__ out) {
+    __shared__ int64_t wbase;
+    const int64_t i = s0 + blockIdx.x;
+    const int lane = threadIdx.x & 63;
+    if (threadIdx.x == 0) wbase = at[blockIdx.x];
+    __syncthreads();
+    const int64_t b = off[i] - base, e = off[i + 1] - base;
+    for (int64_t x0 = b; x0 < e; x0 += 256) {
+        const int64_t x = x0 + threadIdx.x;
+        const uint32_t p = x < e ? pos[x] : ~0u;
+        const bool hit = p != ~0u && p >= vbase;
+        const unsigned long long m = __ballot(hit);
+        int64_t slot = 0;
+        if (m) {
+            if (lane == __ffsll((long long)m) - 1)
+                slot = (int64_t)atomicAdd(reinterpret_cast<unsigned long long*>(&wbase), (unsigned long long)__popcll(m));
+            slot = (int64_t)__shfl((long long)slot, __ffsll((long long)m) - 1, 64);
+        }
+        if (hit) {
+            const uint64_t q = p - vbase;
+            out[slot + __popcll(m & ((1ull << lane) - 1))] =
+                ((q >> 6) << (sbits + 6)) | ((uint64_t)i << 6) | (q & 63);
+        }
+        __syncthreads();
+    }
+}
+
+// OR the bits of each (word, set) run of sorted records: (word << sbits | set, mask)
+__global__ void vrec_heads_kernel(const uint64_t* __restrict__ k, int64_t n, int32_t* __restrict__ flag) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        flag[i] = (i == 0 || (k[i] >> 6) != (k[i - 1] >> 6)) ? 1 : 0;
+}
+
+__global__ void vrec_or_kernel(const uint64_t* __restrict__ k, int64_t n, const int32_t* __restrict__ flag,
+                               const int64_t* __restrict__ pos, uint64_t* __restrict__ ekey,
+                               unsigned long long* __restrict__ emask) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        if (!flag[i]) continue;
+        const uint64_t h = k[i] >> 6;
+        unsigned long long m = 0;
+        for (int64_t e = i; e < n && (k[e] >> 6) == h; e++) m |= 1ull << (k[e] & 63);
+        ekey[pos[i]] = h;
+        emask[pos[i]] = m;
+    }
+}
+
+// ---- entries -> word lists and the set side ------------------------------
+__global__ void entry_fields_kernel(const uint64_t* __restrict__ key, const int32_t* __restrict__ idx, int64_t E,
+                                    int sbits, const unsigned long long* __restrict__ mask_in,
+                                    uint32_t* __restrict__ vset, unsigned long long* __restrict__ vmask,
+                                    uint64_t* __restrict__ skey) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += stride) {
+        const uint32_t set = (uint32_t)(key[e] & ((1ull << sbits) - 1));
+        vset[e] = set;
+        vmask[e] = mask_in[idx[e]];
+        skey[e] = ((uint64_t)set << 32) | (uint64_t)e;
+    }
+}
+
+// word w's list = entries [woff[w], woff[w + 1])
+__global__ void word_offsets_kernel(const uint64_t* __restrict__ key, int64_t E, int sbits, int64_t nw,
+                                    int64_t* __restrict__ woff) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w <= nw; w += stride) {
+        int64_t lo = 0, hi = E;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if ((int64_t)(key[mid] >> sbits) < w) lo = mid + 1; else hi = mid;
+        }
+        woff[w] = lo;
+    }
+}
+
+__global__ void entry_bounds_kernel(const uint64_t* __restrict__ key, int64_t E, int sbits,
+                                    const int64_t* __restrict__ woff, uint32_t* __restrict__ beg,
+                                    uint32_t* __restrict__ end) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += stride) {
+        const int64_t w = (int64_t)(key[e] >> sbits);
+        beg[e] = (uint32_t)woff[w];
+        end[e] = (uint32_t)woff[w + 1];
+    }
+}
+
+__global__ void set_offsets_kernel(const uint64_t* __restrict__ skey, int64_t E, int64_t nsets,
+                                   int64_t* __restrict__ soff, uint32_t* __restrict__ sent) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= nsets; i += stride) {
+        int64_t lo = 0, hi = E;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if ((int64_t)(skey[mid] >> 32) < i) lo = mid + 1; else hi = mid;
+        }
+        soff[i] = lo;
+    }
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += stride) sent[e] = (uint32_t)skey[e];
+}
+
+// products of the tier: sum over words of z (z - 1) / 2, and the longest list
+__global__ void word_products_kernel(const int64_t* __restrict__ woff, int64_t nw,
+                                     unsigned long long* __restrict__ out) {
+    unsigned long long acc = 0, mx = 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += stride) {
+        const unsigned long long z = (unsigned long long)(woff[w + 1] - woff[w]);
+        acc += z * (z - (z ? 1 : 0)) / 2;
+        mx = z > mx ? z : mx;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        acc += __shfl_xor(acc, o, 64);
+        const unsigned long long v = __shfl_xor(mx, o, 64);
+        mx = v > mx ? v : mx;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(out, acc);
+        atomicMax(out + 1, mx);
+    }
+}
+
+}  // namespace
+
+// ---- the walk --------------------------------------------------------------
+constexpr int VCH = 16384;   // columns per LDS chunk (64 KiB of counters)
+
+namespace {
+// first y in [lo, hi) with vset[y] >= t (wave-uniform)
+__device__ __forceinline__ int64_t set_lower_bound(const uint32_t* __restrict__ vset, int64_t lo, int64_t hi,
+                                                   uint32_t t) {
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (vset[mid] < t) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+// grid = rows x column chunks x nsplit slices of the row's entries
+__global__ __launch_bounds__(256) void variant_rows_kernel(const int64_t* __restrict__ soff,
+                                                           const uint32_t* __restrict__ sent,
+                                                           const uint32_t* __restrict__ vset,
+                                                           const unsigned long long* __restrict__ vmask,
+                                                           const uint32_t* __restrict__ vbeg,
+                                                           const uint32_t* __restrict__ vend, int64_t r0, int64_t r1,
+                                                           int64_t c0, int64_t c1, int nch, int nsplit, int upper,
+                                                           int32_t* __restrict__ I, int64_t ldI) {
+    __shared__ int32_t cnt[VCH];
+    const int64_t unit = blockIdx.x / nsplit;
+    const int split = blockIdx.x % nsplit;
+    const int64_t i = r0 + unit / nch;
+    const int ch = (int)(unit % nch);
+    const int64_t cb = c0 + (int64_t)ch * VCH;
+    const int64_t ce = cb + VCH < c1 ? cb + VCH : c1;
+    if (i >= r1 || cb >= ce || (upper && ce - 1 <= i)) return;
+    const int n = (int)(ce - cb);
+    for (int t = threadIdx.x; t < n; t += blockDim.x) cnt[t] = 0;
+    __syncthreads();
+    const int64_t lo = upper && i + 1 > cb ? i + 1 : cb;
+    const int64_t rb = soff[i], re = soff[i + 1];
+    const int64_t per = (re - rb + nsplit - 1) / nsplit;
+    const int64_t xb = rb + per * split;
+    const int64_t xe = xb + per < re ? xb + per : re;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int64_t x = xb + wv; x < xe; x += 4) {                // a wave per entry of the row
+        const uint32_t e = sent[x];
+        const unsigned long long mi = vmask[e];
+        // the list from the chunk's first column (upper: past the row itself)
+        int64_t y = upper ? (int64_t)e + 1 : (int64_t)vbeg[e];
+        const int64_t ye = vend[e];
+        if (ye - y > 64) y = set_lower_bound(vset, y, ye, (uint32_t)lo);
+        for (; y < ye; y += 64) {
+            const int64_t yy = y + lane;
+            const uint32_t j = yy < ye ? vset[yy] : 0xFFFFFFFFu;
+            const unsigned long long mj = yy < ye ? vmask[yy] : 0ull;
+            if ((int64_t)j >= lo && (int64_t)j < ce && (int64_t)j != i) {
+                const int v = __popcll(mi & mj);
+                if (v) atomicAdd(&cnt[j - cb], v);
+            }
+            if (!__ballot(yy < ye && (int64_t)j < ce)) break;  // lists ascend: the rest lie past the chunk
+        }
+    }
+    __syncthreads();
+    int32_t* row = I + (i - r0) * ldI + (cb - c0);
+    for (int t = threadIdx.x; t < n; t += blockDim.x) {
+        const int v = cnt[t];
+        if (v && cb + t >= lo) atomicAdd(row + t, v);
+    }
+}
+
+// one query set q against every set: cnt[t] += shared variant kmers (global atomics)
+__global__ __launch_bounds__(256) void variant_query_kernel(const int64_t* __restrict__ soff,
+                                                            const uint32_t* __restrict__ sent,
+                                                            const uint32_t* __restrict__ vset,
+                                                            const unsigned long long* __restrict__ vmask,
+                                                            const uint32_t* __restrict__ vbeg,
+                                                            const uint32_t* __restrict__ vend, int64_t q,
+                                                            int32_t* __restrict__ cnt) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t x = soff[q] + wave; x < soff[q + 1]; x += waves) {
+        const uint32_t e = sent[x];
+        const unsigned long long mi = vmask[e];
+        for (int64_t y = (int64_t)vbeg[e] + lane; y < (int64_t)vend[e]; y += 64) {
+            const uint32_t j = vset[y];
+            const int v = __popcll(mi & vmask[y]);
+            if ((int64_t)j != q && v) atomicAdd(cnt + j, v);
+        }
+    }
+}
+}  // namespace
+
+// ---- host --------------------------------------------------------------------
+
+// Summary of the collection's codes held by >= min_count sets, by ranges of
+// the code space (P splitters from a sample of every set's codes): one range
+// of every set gathered, sorted, counted at a time.
+void range_summary(gdist_ctx* ctx, const gdist_sets* s, int min_count, Summary& out) {
+    hipStream_t st = ctx->stream;
+    Trace tr(st, ctx->trace());
+    const int cbits = std::min(64, code_bits(s->kind, s->k, s->flags));
+    const int64_t N = s->nsets, total = s->total;
+    // ranges of at most ~2^28 codes (about 4 GiB of sort buffers)
+    const int64_t target = int64_t(1) << 28;
+    const int P = (int)std::max<int64_t>(1, std::min<int64_t>(4096, ceil_div(total, target)));
+    std::vector<uint64_t> split;
+    if (P > 1) {
+        // sample: the codes at a stride (every set's codes are sorted, so
+        // the sample spans each set's range), sorted on the host
+        const int64_t want = std::min<int64_t>(total, (int64_t)P * 256);
+        const int64_t stride = std::max<int64_t>(1, total / std::max<int64_t>(1, want));
+        const int64_t ns = ceil_div(total - stride / 2, stride);
+        DevBuf dsm(ns * 8 + 8, st);
+        sample_kernel<<<grid_for(ns), 256, 0, st>>>(s->codes.as<uint64_t>(), stride / 2, stride, ns,
+                                                    dsm.as<uint64_t>());
+        GD_HIP(hipGetLastError());
+        std::vector<uint64_t> smp(ns);
+        d2h(smp.data(), dsm.p, ns * 8, st);
+        std::sort(smp.begin(), smp.end());
+        for (int p = 1; p < P; p++) {
+            const uint64_t v = smp.empty() ? 0 : smp[std::min<size_t>(smp.size() - 1, smp.size() * p / P)];
+            if (split.empty() || v > split.back()) split.push_back(v);
+        }
+    }
+    const int Pe = (int)split.size() + 1;
+    DevBuf dsplit(std::max<size_t>(1, split.size()) * 8, st), spos((size_t)N * (Pe + 1) * 8, st);
+    if (!split.empty()) h2d(dsplit.p, split.data(), split.size() * 8, st);
+    range_pos_kernel<<<(unsigned)ceil_div(N * (Pe + 1), 256), 256, 0, st>>>(
+        s->codes.as<uint64_t>(), s->off.as<int64_t>(), N, dsplit.as<uint64_t>(), Pe, spos.as<int64_t>());
+    GD_HIP(hipGetLastError());
+    std::vector<Summary> parts;
+    DevBuf cnt((N + 1) * 8, st), at((N + 1) * 8, st);
+    int64_t kept = 0;
+    for (int p = 0; p < Pe; p++) {
+        range_sizes_kernel<<<(unsigned)ceil_div(N, 256), 256, 0, st>>>(spos.as<int64_t>(), N, Pe, p,
+                                                                       cnt.as<int64_t>());
+        GD_HIP(hipMemsetAsync(cnt.as<int64_t>() + N, 0, 8, st));
+        exclusive_scan_i64(ctx, cnt.as<int64_t>(), at.as<int64_t>(), (size_t)(N + 1));
+        int64_t n = 0;
+        d2h(&n, at.as<int64_t>() + N, 8, st);
+        Summary part;
+        if (n > 0) {
+            DevBuf kA(n * 8 + 8, st), kB(n * 8 + 8, st);
+            range_gather_kernel<<<(unsigned)N, 256, 0, st>>>(s->codes.as<uint64_t>(), spos.as<int64_t>(), Pe, p,
+                                                             at.as<int64_t>(), kA.as<uint64_t>());
+            GD_HIP(hipGetLastError());
+            uint64_t* keys = kA.as<uint64_t>(); uint64_t* alt = kB.as<uint64_t>();
+            sort_keys_u64(ctx, keys, alt, (size_t)n, 0, cbits);
+            DevBuf flag(n * 4 + 4, st), keep(n * 4 + 4, st), len(n * 4 + 4, st), pos(n * 8 + 8, st);
+            heads_kernel<<<grid_for(n), 256, 0, st>>>(keys, n, flag.as<int32_t>());
+            run_keep_kernel<<<grid_for(n), 256, 0, st>>>(keys, n, flag.as<int32_t>(), min_count, keep.as<int32_t>(),
+                                                         len.as<uint32_t>());
+            GD_HIP(hipGetLastError());
+            exclusive_scan_i32_to_i64(ctx, keep.as<int32_t>(), pos.as<int64_t>(), (size_t)n);
+            int64_t last = 0;
+            int32_t lf = 0;
+            d2h(&last, pos.as<int64_t>() + n - 1, 8, st);
+            d2h(&lf, keep.as<int32_t>() + n - 1, 4, st);
+            part.n = last + lf;
+            part.codes.alloc(part.n * 8 + 8, st);
+            part.counts.alloc(part.n * 4 + 4, st);
+            run_emit_kernel<<<grid_for(n), 256, 0, st>>>(keys, keep.as<int32_t>(), len.as<uint32_t>(),
+                                                         pos.as<int64_t>(), n, part.codes.as<uint64_t>(),
+                                                         part.counts.as<uint32_t>());
+            GD_HIP(hipGetLastError());
+            GD_HIP(hipStreamSynchronize(st));
+        }
+        kept += part.n;
+        parts.push_back(std::move(part));
+    }
+    // ranges ascend: the parts concatenate in code order
+    out.n = kept;
+    out.codes.alloc(kept * 8 + 8, st);
+    out.counts.alloc(kept * 4 + 4, st);
+    int64_t o = 0;
+    for (auto& pt : parts) {
+        if (pt.n) {
+            GD_HIP(hipMemcpyAsync(out.codes.as<uint64_t>() + o, pt.codes.p, pt.n * 8, hipMemcpyDeviceToDevice, st));
+            GD_HIP(hipMemcpyAsync(out.counts.as<uint32_t>() + o, pt.counts.p, pt.n * 4, hipMemcpyDeviceToDevice, st));
+        }
+        o += pt.n;
+    }
+    GD_HIP(hipStreamSynchronize(st));
+    if (ctx->trace())
+        fprintf(stderr, "gdist: range summary: %d code ranges, %lld codes held by >= %d sets\n", Pe, (long long)kept,
+                min_count);
+    tr.mark("variant: range summary");
+}
+
+static CodeGeom code_geom(const gdist_sets* s) {
+    CodeGeom g;
+    g.k = s->k;
+    const unsigned am = s->flags & GDIST_AMBIG_MASK;
+    if (s->kind == GDIST_DNA) {
+        const bool keep = am == GDIST_AMBIG_KEEP;
+        g.bits = keep ? 3 : 2;
+        g.strands = (s->flags & GDIST_STRAND_MASK) == GDIST_STRAND_BOTH ? 2 : 1;
+        if (keep) {   // A0 C1 G2 N3 R4 T5 Y6
+            const uint8_t a[7] = {0, 1, 2, 3, 4, 5, 6};
+            const int8_t c[7] = {5, 2, 1, 3, 6, 0, 4};
+            g.nalpha = 7;
+            memcpy(g.alpha, a, 7);
+            memcpy(g.comp, c, 7);
+        } else {      // A0 C1 G2 T3
+            const uint8_t a[4] = {0, 1, 2, 3};
+            const int8_t c[4] = {3, 2, 1, 0};
+            g.nalpha = 4;
+            memcpy(g.alpha, a, 4);
+            memcpy(g.comp, c, 4);
+        }
+    } else {
+        g.strands = 1;
+        if (s->k <= 8) {   // raw bytes: the 20 standard residues
+            g.bits = 8;
+            const char* aa = "ACDEFGHIKLMNPQRSTVWY";
+            g.nalpha = 20;
+            for (int i = 0; i < 20; i++) g.alpha[i] = (uint8_t)aa[i];
+        } else {           // 5-bit: * 0, A..Z 1..26
+            g.bits = 5;
+            const char* aa = "ACDEFGHIKLMNPQRSTVWY";
+            g.nalpha = 20;
+            for (int i = 0; i < 20; i++) g.alpha[i] = (uint8_t)(aa[i] - 'A' + 1);
+        }
+    }
+    return g;
+}
+
+int64_t variant_dmin(const gdist_ctx* ctx, int64_t nsets) {
+    return ctx->has_option(OPT_VARIANT_DMIN) ? std::max<int64_t>(2, ctx->option(OPT_VARIANT_DMIN, 2))
+                                             : std::max<int64_t>(2, nsets / 10);
+}
+
+void free_variant(gdist_sets* s) {
+    s->variant = false;
+    s->vw_words = s->vw_entries = s->vw_kmers = s->vw_dmin = 0;
+    s->vw_products = 0.0;
+    s->vw_max_list = 0;
+    s->vw_set.release();
+    s->vw_mask.release();
+    s->vw_beg.release();
+    s->vw_end.release();
+    s->vs_off.release();
+    s->vs_ent.release();
+}
+
+void build_variant_bitsets(gdist_ctx* ctx, gdist_sets* s, DevBuf& dict, DevBuf& dcnt, int64_t U, DevBuf& rare,
+                           int64_t Ur, int64_t mass, int64_t T) {
+    hipStream_t st = ctx->stream;
+    Trace tr(st, ctx->trace());
+    const int64_t N = s->nsets;
+    GD_REQUIRE(N < (int64_t(1) << 31), "too many sets for the variant tier");
+    // 2. tiers: dense (>= Dmin) and variant (T .. Dmin - 1), in code order within the dictionary
+    const int64_t dmin = variant_dmin(ctx, N);
+    DevBuf fd(U * 4 + 4, st), fm(U * 4 + 4, st), pd(U * 8 + 8, st), pm(U * 8 + 8, st);
+    int64_t Ud = 0, Um = 0;
+    if (U) {
+        tier_flags_kernel<<<grid_for(U), 256, 0, st>>>(dcnt.as<uint32_t>(), U, (uint32_t)dmin, fd.as<int32_t>(),
+                                                       fm.as<int32_t>());
+        GD_HIP(hipGetLastError());
+        exclusive_scan_i32_to_i64(ctx, fd.as<int32_t>(), pd.as<int64_t>(), (size_t)U);
+        exclusive_scan_i32_to_i64(ctx, fm.as<int32_t>(), pm.as<int64_t>(), (size_t)U);
+        int64_t h[2];
+        int32_t hf[2];
+        d2h(&h[0], pd.as<int64_t>() + U - 1, 8, st);
+        d2h(&h[1], pm.as<int64_t>() + U - 1, 8, st);
+        d2h(&hf[0], fd.as<int32_t>() + U - 1, 4, st);
+        d2h(&hf[1], fm.as<int32_t>() + U - 1, 4, st);
+        Ud = h[0] + hf[0];
+        Um = h[1] + hf[1];
+    }
+    DevBuf dcodes(Ud * 8 + 8, st), dcounts(Ud * 4 + 4, st), mcodes(Um * 8 + 8, st);
+    if (U)
+        split_codes_kernel<<<grid_for(U), 256, 0, st>>>(dict.as<uint64_t>(), dcnt.as<uint32_t>(), U, fd.as<int32_t>(),
+                                                        pd.as<int64_t>(), pm.as<int64_t>(), dcodes.as<uint64_t>(),
+                                                        dcounts.as<uint32_t>(), mcodes.as<uint64_t>());
+    GD_HIP(hipGetLastError());
+    // 3. dense positions: locus order of the guides (as build_bitsets)
+    DevBuf dperm;
+    if (s->n_guide > 0 && locus_order_enabled(ctx) && Ud > 0) {
+        DevBuf key;
+        locus_keys(ctx, s, dcodes.as<uint64_t>(), dcounts.as<uint32_t>(), Ud, 0, key);
+        locus_perm(ctx, key, Ud, dperm);
+    }
+    const int64_t Wd = bitset_words(Ud);
+    const uint32_t vbase = (uint32_t)(Wd * 64);
+    tr.mark("variant: tiers + dense locus order");
+    // 4. variant order: keys from the dense neighbours, groups, words
+    DevBuf mperm(Um * 4 + 4, st);
+    int64_t vwords = 0;
+    if (Um > 0) {
+        DevBuf dentry(Ud * 8 + 8, st), vkey(Um * 8 + 8, st), vkalt(Um * 8 + 8, st), ord(Um * 4 + 4, st),
+            oalt(Um * 4 + 4, st);
+        if (Ud > 0) {
+            if (s->n_guide > 0)
+                dense_entry_kernel<<<grid_for(Ud), 256, 0, st>>>(dcodes.as<uint64_t>(), Ud, s->guide_codes.as<uint64_t>(),
+                                                                 s->guide_keys.as<uint64_t>(), s->n_guide,
+                                                                 dentry.as<int64_t>());
+            else
+                GD_HIP(hipMemsetAsync(dentry.p, 0xFF, Ud * 8, st));
+        }
+        variant_key_kernel<<<grid_for(Um, 256, 256 * 64), 256, 0, st>>>(mcodes.as<uint64_t>(), Um,
+                                                                         dcodes.as<uint64_t>(), Ud,
+                                                                         dentry.as<int64_t>(), code_geom(s),
+                                                                         vkey.as<uint64_t>());
+        GD_HIP(hipGetLastError());
+        // iota values: the variant index; stable sort by key keeps code order within a group
+        {
+            std::vector<int32_t> io(Um);
+            for (int64_t m = 0; m < Um; m++) io[m] = (int32_t)m;
+            h2d(ord.p, io.data(), Um * 4, st);
+        }
+        uint64_t* k = vkey.as<uint64_t>(); uint64_t* ka = vkalt.as<uint64_t>();
+        int32_t* v = ord.as<int32_t>(); int32_t* va = oalt.as<int32_t>();
+        sort_pairs_u64_i32(ctx, k, ka, v, va, (size_t)Um, 0, 64);
+        DevBuf head(Um * 4 + 4, st), wn(Um * 8 + 8, st), wst(Um * 8 + 8, st);
+        group_words_kernel<<<grid_for(Um), 256, 0, st>>>(k, Um, head.as<int32_t>(), wn.as<int64_t>());
+        GD_HIP(hipGetLastError());
+        exclusive_scan_i64(ctx, wn.as<int64_t>(), wst.as<int64_t>(), (size_t)Um);
+        int64_t h[2];
+        d2h(&h[0], wst.as<int64_t>() + Um - 1, 8, st);
+        d2h(&h[1], wn.as<int64_t>() + Um - 1, 8, st);
+        vwords = h[0] + h[1];
+        GD_REQUIRE((double)vbase + (double)vwords * 64.0 < 4294967295.0, "variant tier too large for u32 positions");
+        group_pos_kernel<<<grid_for(Um), 256, 0, st>>>(k, v, Um, wst.as<int64_t>(), vbase, mperm.as<uint32_t>());
+        GD_HIP(hipGetLastError());
+    }
+    DevBuf perm(U * 4 + 4, st);
+    if (U)
+        combine_perm_kernel<<<grid_for(U), 256, 0, st>>>(fd.as<int32_t>(), pd.as<int64_t>(), pm.as<int64_t>(), U,
+                                                         dperm.p ? dperm.as<uint32_t>() : nullptr,
+                                                         mperm.as<uint32_t>(), perm.as<uint32_t>());
+    GD_HIP(hipGetLastError());
+    tr.mark("variant: word order");
+    // 5. one fill pass: dense bits, rare records, and per chunk the variant
+    //    records sorted and OR-merged into (word, set, mask) entries
+    int sbits = 1;
+    while ((int64_t(1) << sbits) < N) sbits++;
+    int wbits = 1;
+    while ((int64_t(1) << wbits) < std::max<int64_t>(1, vwords)) wbits++;
+    GD_REQUIRE(wbits + sbits + 6 <= 64, "variant tier too large for packed record keys");
+    std::vector<DevBuf> ekeys, emasks;
+    std::vector<int64_t> en;
+    auto hook = [&](const uint32_t* pos, int64_t s0, int64_t s1, int64_t base) {
+        if (Um == 0 || s1 <= s0) return;
+        const int64_t ns = s1 - s0;
+        DevBuf c((ns + 1) * 8, st), a((ns + 1) * 8, st);
+        vrec_count_kernel<<<(unsigned)ns, 256, 0, st>>>(pos, s->off.as<int64_t>(), s0, base, vbase, c.as<int64_t>());
+        GD_HIP(hipGetLastError());
+        GD_HIP(hipMemsetAsync(c.as<int64_t>() + ns, 0, 8, st));
+        exclusive_scan_i64(ctx, c.as<int64_t>(), a.as<int64_t>(), (size_t)(ns + 1));
+        int64_t n = 0;
+        d2h(&n, a.as<int64_t>() + ns, 8, st);
+        if (n == 0) return;
+        DevBuf rA(n * 8 + 8, st), rB(n * 8 + 8, st);
+        vrec_write_kernel<<<(unsigned)ns, 256, 0, st>>>(pos, s->off.as<int64_t>(), s0, base, vbase, sbits,
+                                                        a.as<int64_t>(), rA.as<uint64_t>());
+        GD_HIP(hipGetLastError());
+        uint64_t* rk = rA.as<uint64_t>(); uint64_t* ra = rB.as<uint64_t>();
+        sort_keys_u64(ctx, rk, ra, (size_t)n, 0, wbits + sbits + 6);
+        DevBuf flag(n * 4 + 4, st), fpos(n * 8 + 8, st);
+        vrec_heads_kernel<<<grid_for(n), 256, 0, st>>>(rk, n, flag.as<int32_t>());
+        GD_HIP(hipGetLastError());
+        exclusive_scan_i32_to_i64(ctx, flag.as<int32_t>(), fpos.as<int64_t>(), (size_t)n);
+        int64_t last = 0;
+        int32_t lf = 0;
+        d2h(&last, fpos.as<int64_t>() + n - 1, 8, st);
+        d2h(&lf, flag.as<int32_t>() + n - 1, 4, st);
+        const int64_t ne = last + lf;
+        DevBuf ek(ne * 8 + 8, st), em(ne * 8 + 8, st);
+        vrec_or_kernel<<<grid_for(n), 256, 0, st>>>(rk, n, flag.as<int32_t>(), fpos.as<int64_t>(), ek.as<uint64_t>(),
+                                                    em.as<unsigned long long>());
+        GD_HIP(hipGetLastError());
+        GD_HIP(hipStreamSynchronize(st));
+        ekeys.push_back(std::move(ek));
+        emasks.push_back(std::move(em));
+        en.push_back(ne);
+    };
+    s->bits.alloc((size_t)N * Wd * 8 + 8, st);
+    DevBuf recs(mass * 8 + 8, st);
+    int64_t written = 0;
+    fill_bits(ctx, s, dict.as<uint64_t>(), U, Wd, s->bits.as<unsigned long long>(), rare.as<uint64_t>(), Ur, 0,
+              recs.as<unsigned long long>(), mass, &written, perm.as<uint32_t>(), hook);
+    GD_REQUIRE(written == mass, "rare-tier record count mismatch");
+    tr.mark("variant: fill (dense bits, rare and variant records)");
+    build_postings(ctx, s, recs.as<unsigned long long>(), written, Ur);
+    recs.release();
+    tr.mark("variant: rare postings");
+    // 6. entries of every chunk -> one list per word (sets ascending) + the set side
+    int64_t E = 0;
+    for (int64_t n : en) E += n;
+    GD_REQUIRE(E < (int64_t(1) << 31), "variant tier: too many entries");
+    free_variant(s);
+    if (E > 0) {
+        DevBuf kA(E * 8 + 8, st), kB(E * 8 + 8, st), mall(E * 8 + 8, st), iA(E * 4 + 4, st), iB(E * 4 + 4, st);
+        int64_t o = 0;
+        for (size_t c = 0; c < en.size(); c++) {
+            GD_HIP(hipMemcpyAsync(kA.as<uint64_t>() + o, ekeys[c].p, en[c] * 8, hipMemcpyDeviceToDevice, st));
+            GD_HIP(hipMemcpyAsync(mall.as<uint64_t>() + o, emasks[c].p, en[c] * 8, hipMemcpyDeviceToDevice, st));
+            o += en[c];
+        }
+        ekeys.clear();
+        emasks.clear();
+        {
+            std::vector<int32_t> io(E);
+            for (int64_t e = 0; e < E; e++) io[e] = (int32_t)e;
+            h2d(iA.p, io.data(), E * 4, st);
+        }
+        uint64_t* k = kA.as<uint64_t>(); uint64_t* ka = kB.as<uint64_t>();
+        int32_t* v = iA.as<int32_t>(); int32_t* va = iB.as<int32_t>();
+        sort_pairs_u64_i32(ctx, k, ka, v, va, (size_t)E, 0, wbits + sbits);
+        s->vw_set.alloc(E * 4 + 16, st);
+        s->vw_mask.alloc(E * 8 + 16, st);
+        DevBuf skey(E * 8 + 8, st), skalt(E * 8 + 8, st);
+        entry_fields_kernel<<<grid_for(E), 256, 0, st>>>(k, v, E, sbits, mall.as<unsigned long long>(),
+                                                         s->vw_set.as<uint32_t>(), s->vw_mask.as<unsigned long long>(),
+                                                         skey.as<uint64_t>());
+        GD_HIP(hipGetLastError());
+        DevBuf woff((vwords + 1) * 8 + 8, st);
+        word_offsets_kernel<<<grid_for(vwords + 1), 256, 0, st>>>(k, E, sbits, vwords, woff.as<int64_t>());
+        s->vw_beg.alloc(E * 4 + 4, st);
+        s->vw_end.alloc(E * 4 + 4, st);
+        entry_bounds_kernel<<<grid_for(E), 256, 0, st>>>(k, E, sbits, woff.as<int64_t>(), s->vw_beg.as<uint32_t>(),
+                                                         s->vw_end.as<uint32_t>());
+        GD_HIP(hipGetLastError());
+        uint64_t* sk = skey.as<uint64_t>(); uint64_t* ska = skalt.as<uint64_t>();
+        sort_keys_u64(ctx, sk, ska, (size_t)E, 0, 32 + sbits);
+        s->vs_off.alloc((N + 1) * 8, st);
+        s->vs_ent.alloc(E * 4 + 4, st);
+        set_offsets_kernel<<<grid_for(std::max<int64_t>(E, N + 1)), 256, 0, st>>>(sk, E, N, s->vs_off.as<int64_t>(),
+                                                                                  s->vs_ent.as<uint32_t>());
+        GD_HIP(hipGetLastError());
+        DevBuf prod(16, st);
+        GD_HIP(hipMemsetAsync(prod.p, 0, 16, st));
+        word_products_kernel<<<grid_for(vwords, 256, 4096), 256, 0, st>>>(woff.as<int64_t>(), vwords,
+                                                                          prod.as<unsigned long long>());
+        GD_HIP(hipGetLastError());
+        unsigned long long hp[2] = {0, 0};
+        d2h(hp, prod.p, 16, st);
+        s->vw_products = (double)hp[0];
+        s->vw_max_list = (int64_t)hp[1];
+        s->variant = true;
+    }
+    GD_HIP(hipStreamSynchronize(st));
+    s->vw_words = vwords;
+    s->vw_entries = E;
+    s->vw_kmers = Um;
+    s->vw_dmin = dmin;
+    s->W = Wd;
+    s->dict_size = Ud;
+    s->rare_T = T;
+    s->bits_keep_singletons = false;
+    tr.mark("variant: word lists + set side");
+    if (ctx->trace())
+        fprintf(stderr, "gdist: variant tier: T %lld, Dmin %lld: dense %lld kmers (%lld words), variant %lld kmers in "
+                        "%lld words, %lld entries, %.3g products, longest list %lld; rare %lld kmers\n",
+                (long long)T, (long long)dmin, (long long)Ud, (long long)Wd, (long long)Um, (long long)vwords,
+                (long long)E, s->vw_products, (long long)s->vw_max_list, (long long)Ur);
+    build_sparse_words(ctx, s);
+}
+
+// Decides after the dictionary of build_bitsets whether the collection takes
+// the variant tier: option variant = 1 forces it, 0 keeps the two tiers;
+// by default when the kmers held by T .. Dmin - 1 sets are many (>= 4096)
+// and at least a quarter of the dictionary (C4: 12.6 M of 12.8 M).
+bool variant_wanted(const gdist_ctx* ctx, int64_t nsets, int64_t mid_kmers, int64_t dict_kmers) {
+    const int64_t opt = ctx->option(OPT_VARIANT, -1);
+    if (opt == 0) return false;
+    if (opt > 0) return mid_kmers > 0;
+    return mid_kmers >= 4096 && 4 * mid_kmers >= dict_kmers && nsets >= 64;
+}
+
+namespace {
+__global__ void mid_count_kernel(const uint32_t* __restrict__ cnt, int64_t n, uint32_t dmin,
+                                 unsigned long long* __restrict__ out) {
+    unsigned long long c = 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) c += cnt[i] < dmin;
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, c);
+}
+}  // namespace
+
+int64_t count_below(gdist_ctx* ctx, const uint32_t* dcounts, int64_t U, int64_t dmin) {
+    hipStream_t st = ctx->stream;
+    if (U == 0) return 0;
+    DevBuf o(8, st);
+    GD_HIP(hipMemsetAsync(o.p, 0, 8, st));
+    mid_count_kernel<<<grid_for(U, 256, 4096), 256, 0, st>>>(dcounts, U, (uint32_t)dmin, o.as<unsigned long long>());
+    GD_HIP(hipGetLastError());
+    unsigned long long h = 0;
+    d2h(&h, o.p, 8, st);
+    return (int64_t)h;
+}
+
+// the variant tier's counts of rows [r0, r1) x cols [c0, c1) added into I (atomics)
+void variant_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1, bool upper,
+                    int32_t* d_I, int64_t ldI, hipStream_t rs) {
+    if (!s->variant || r1 <= r0 || c1 <= c0) return;
+    const int nch = (int)ceil_div(c1 - c0, VCH);
+    const int64_t units = (r1 - r0) * nch;
+    // few row units: slice each row's entries over several workgroups
+    const int nsplit = (int)std::max<int64_t>(1, std::min<int64_t>(32, ceil_div((int64_t)ctx->cus * 8, units)));
+    const int64_t grid = units * nsplit;
+    GD_REQUIRE(grid < (int64_t(1) << 31), "variant-tier grid too large");
+    FamilyTimer ft(ctx, GDIST_KERNEL_VARIANT, rs);
+    variant_rows_kernel<<<(unsigned)grid, 256, 0, rs>>>(s->vs_off.as<int64_t>(), s->vs_ent.as<uint32_t>(),
+                                                        s->vw_set.as<uint32_t>(), s->vw_mask.as<unsigned long long>(),
+                                                        s->vw_beg.as<uint32_t>(), s->vw_end.as<uint32_t>(), r0, r1, c0,
+                                                        c1, nch, nsplit, upper ? 1 : 0, d_I, ldI);
+    GD_HIP(hipGetLastError());
+    ft.end();
+}
+
+// one query row's variant-tier counts against every set (cnt: int32 [nsets], added)
+void variant_query(gdist_ctx* ctx, const gdist_sets* s, int64_t q, int32_t* cnt) {
+    if (!s->variant) return;
+    variant_query_kernel<<<256, 256, 0, ctx->stream>>>(s->vs_off.as<int64_t>(), s->vs_ent.as<uint32_t>(),
+                                                       s->vw_set.as<uint32_t>(), s->vw_mask.as<unsigned long long>(),
+                                                       s->vw_beg.as<uint32_t>(), s->vw_end.as<uint32_t>(), q, cnt);
+    GD_HIP(hipGetLastError());
+}
+
+}  // namespace gdist

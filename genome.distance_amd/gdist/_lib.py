@@ -108,6 +108,7 @@ _SIGS = {
     "gdist_sets_rare_stats": (C.c_int, [_setp, _i64p, _i64p]),
     "gdist_sets_rare_kmers": (C.c_int, [_setp, _i64p]),
     "gdist_sets_sparse_info": (C.c_int, [_setp, _i64p, _i64p, _i64p]),
+    "gdist_sets_variant_info": (C.c_int, [_setp, _i64p, _i64p, _i64p, _dblp]),
     "gdist_sets_group_info": (C.c_int, [_setp, _i64p, _i64p]),
     "gdist_sets_sparse_sides": (C.c_int, [_setp, _i64p, _i64p]),
     "gdist_sets_bitset_info": (C.c_int, [_setp, _i64p, _i64p]),

@@ -109,7 +109,7 @@ class Context:
         L.check(L.lib.gdist_ctx_last_timing(self.h, C.byref(k), C.byref(c), C.byref(n)))
         return k.value, c.value, n.value
 
-    KERNEL_FAMILIES = {"sparse": 0, "rare": 1, "dense": 2, "sorted": 3}
+    KERNEL_FAMILIES = {"sparse": 0, "rare": 1, "dense": 2, "sorted": 3, "variant": 4}
 
     def kernel_ms(self, family: str) -> float:
         """HIP-event ms of one kernel family's launches (sparse / rare / dense /
@@ -397,6 +397,12 @@ class KmerSets(_Handle):
         a, b, c = C.c_int64(), C.c_int64(), C.c_int64()
         L.check(L.lib.gdist_sets_sparse_info(self.h, C.byref(a), C.byref(b), C.byref(c)))
         return a.value, b.value, c.value
+
+    def variant_info(self) -> tuple[int, int, int, float]:
+        """(kmers, words, entries, products) of the variant tier (gdist_sets_variant_info)."""
+        a, b, c, d = C.c_int64(), C.c_int64(), C.c_int64(), C.c_double()
+        L.check(L.lib.gdist_sets_variant_info(self.h, C.byref(a), C.byref(b), C.byref(c), C.byref(d)))
+        return a.value, b.value, c.value, d.value
 
     def group_info(self) -> tuple[int, int]:
         """(groups, grouped sparse words) of the group tier (gdist_sets_group_info)."""

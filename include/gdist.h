@@ -139,6 +139,7 @@ int  gdist_ctx_recent_timings(gdist_ctx* ctx, int max, double* kernel_ms, int* c
 #define GDIST_KERNEL_RARE   1
 #define GDIST_KERNEL_DENSE  2
 #define GDIST_KERNEL_SORTED 3
+#define GDIST_KERNEL_VARIANT 4
 int  gdist_ctx_kernel_ms(gdist_ctx* ctx, int family, double* ms);
 /* Tuning options of a context: the A/B switches of DESIGN.md §5 by name
  * ("rare_t", "bitset_diag", "sparse", "sparse_zmax", "sketch_k", ...;
@@ -207,6 +208,15 @@ int  gdist_sets_bitset_info(const gdist_sets* sets, int64_t* dict_size, int64_t*
  * the complement entries (0s when the split was not worth building).
  * Options "sparse" = 0 / "locus_order" = 0 switch it off (A/B). */
 int  gdist_sets_sparse_info(const gdist_sets* sets, int64_t* sparse_words, int64_t* dense_words, int64_t* entries);
+/* The variant tier: kmers held by T .. Dmin - 1 sets (Dmin:
+ * option "variant_dmin", default N / 10) grouped by the substitution that
+ * made them into 64-kmer words, each a list of (set, 64-bit mask) entries;
+ * a pair adds popc(mask_i & mask_j) per shared word. Built by the bitset
+ * build when those kmers dominate the dictionary (option "variant": 1
+ * forces, 0 never). Reports the kmers, words, entries and the walk's
+ * products (sum over words of z(z-1)/2); zeros without the tier. */
+int  gdist_sets_variant_info(const gdist_sets* sets, int64_t* kmers, int64_t* words, int64_t* entries,
+                             double* products);
 /* The sparse words by side: counted from the sets' complement words (sets
  * lacking a commonly held kmer) or from their words (sets holding a rarely
  * held one: positive-sparse). */

@@ -1,0 +1,124 @@
+"""The variant tier (csrc/variant.hip) and the code-range
+dictionary, bit-exact against the oracle.
+
+C4's structure at a size the oracle checks quickly: one ancestor, genomes
+with independent substitutions, many genomes per site so that every
+single-substitution kmer is shared by several genomes (C4: ~500 of
+100,000). Options force the tiers the full size would choose: kmers held by
+>= variant_dmin sets are dense bit columns, by rare_t .. variant_dmin - 1
+variant words (grouped by the substitution through their Hamming-1 dense
+neighbour), by 2 .. rare_t - 1 posting lists. Reference loop:
+FastaDistanceProcessor.java:157-186 (every pair of a row block).
+"""
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def bits_equal(a, b):
+    return np.array_equal(np.ascontiguousarray(a, np.float64).view(np.uint64),
+                          np.ascontiguousarray(b, np.float64).view(np.uint64))
+
+
+@pytest.fixture(scope="module")
+def c4_like():
+    from gdist import synth
+    n = 1200
+    seqs = [bytes(r) for r in synth.genomes(n, 4000, 0.03, 41)]
+    off, codes = oracle.pack(seqs, 21, 0, 0)
+    return seqs, off, codes
+
+
+REGIONS = [(0, 1200, 0, 1200, True), (37, 211, 5, 1190, False), (600, 1200, 0, 1200, True),
+           (1199, 1200, 0, 1200, False)]
+
+
+@pytest.mark.parametrize("mode", ["variant", "variant_rows_u32", "range_only", "two_tier"])
+def test_variant_tier_exact(ctx, opts, c4_like, mode):
+    """Counts and distances of the variant tier (and of the code-range
+    dictionary alone) equal the oracle's over upper triangles, rectangles,
+    unaligned row blocks and row queries; the grouping puts each
+    substitution's kmers into one word (words << kmers)."""
+    import gdist
+    seqs, off, codes = c4_like
+    n = len(seqs)
+    if mode == "two_tier":
+        opts(variant=0, rare_t=3)
+    elif mode == "range_only":
+        opts(variant=0, rare_t=3, range_summary=1)
+    else:
+        opts(variant=1, rare_t=3, variant_dmin=n // 10, range_summary=1,
+             rare_u16=0 if mode == "variant_rows_u32" else None)
+    sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
+    sets.build_bitsets()
+    vk, vw, ve, vp = sets.variant_info()
+    if mode.startswith("variant"):
+        assert vk > 1000 and ve > 0 and vp > 0, (vk, vw, ve, vp)
+        assert vw * 8 < vk, ("substitution grouping", vk, vw)
+    else:
+        assert (vk, vw, ve) == (0, 0, 0)
+    for (r0, r1, c0, c1, up) in REGIONS:
+        I, D = sets.matrix((r0, r1), (c0, c1), upper=up, method=gdist.METHOD_BITSET)
+        eI, eD = oracle.matrix(off, codes, r0, r1, c0, c1, flags=0x100 if up else 0, nthreads=8)
+        if up:
+            mask = np.fromfunction(lambda a, b: (c0 + b) > (r0 + a), (r1 - r0, c1 - c0))
+            I, D, eI, eD = I[mask], D[mask], eI[mask], eD[mask]
+        assert np.array_equal(I, eI), (mode, r0, r1, c0, c1, up, np.flatnonzero(I != eI)[:5])
+        assert bits_equal(D, eD)
+    cols = [4, n - 1, 0, 600, 600, 17]
+    d = sets.row_query(600, cols)
+    _, eD = oracle.matrix(off, codes, 600, 601, 0, n)
+    assert bits_equal(d, eD[0, cols])
+
+
+def test_variant_tier_replayed_steps(ctx, opts, c4_like):
+    """Repeated device-output calls (plan, capture, replay) of a variant-tier
+    collection: every call equals the oracle (the variant walk's atomics land
+    on a zeroed region each step)."""
+    import gdist
+    seqs, off, codes = c4_like
+    n = len(seqs)
+    opts(variant=1, rare_t=3, variant_dmin=n // 10)
+    sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
+    sets.build_bitsets()
+    assert sets.variant_info()[0] > 0
+    r0, r1 = 100, 400
+    eI, eD = oracle.matrix(off, codes, r0, r1, 0, n, flags=0x100, nthreads=8)
+    nr = r1 - r0
+    dI, dD = ctx.alloc(nr * n * 4), ctx.alloc(nr * n * 8)
+    mask = np.fromfunction(lambda a, b: b > (r0 + a), (nr, n))
+    for call in range(4):
+        sets.matrix_device(dI.ptr, dD.ptr, n, (r0, r1), (0, n), upper=True, method=gdist.METHOD_BITSET)
+        I = dI.to_host(np.int32).reshape(nr, n)
+        D = dD.to_host(np.float64).reshape(nr, n)
+        assert np.array_equal(I[mask], eI[mask]) and bits_equal(D[mask], eD[mask]), call
+    dI.free()
+    dD.free()
+
+
+def test_variant_greedy_reps(ctx, opts, c4_like):
+    """Greedy representatives (DistanceRepsProcessor.java:185-262) over a
+    variant-tier collection: the device's reps and assignments follow the
+    oracle's distances."""
+    import gdist
+    seqs, off, codes = c4_like
+    n = 300
+    opts(variant=1, rare_t=3, variant_dmin=30)
+    sets = gdist.KmerSets.from_sequences(seqs[:n], 21, gdist.KmerType.DNA, 0, ctx)
+    sets.build_bitsets()
+    assert sets.variant_info()[0] > 0
+    o2, c2 = oracle.pack(seqs[:n], 21, 0, 0)
+    _, eD = oracle.matrix(o2, c2, 0, n, 0, n, nthreads=8)
+    t = float(np.quantile(eD[np.triu_indices(n, 1)], 0.02))
+    is_rep, rep_of, rep_d = sets.greedy_reps(t, assign=True)
+    reps = []
+    for i in range(n):
+        if not any(eD[i, r] <= t for r in reps):
+            reps.append(i)
+    assert list(np.flatnonzero(is_rep)) == reps
+    for i in range(n):
+        if not is_rep[i]:
+            assert rep_d[i] == min(eD[i, r] for r in reps)
