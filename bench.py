@@ -191,6 +191,7 @@ def main():
     method = args.method or cfg["method"]
     width_words = 0
     rare = None
+    variant = None
     sparse_words = None
     auto = None
     exchange = world > 1 or args.force_exchange
@@ -215,6 +216,7 @@ def main():
             with stdout_to_stderr():
                 ctx.comm_init(obj[0], world, rank)
     xplan = None
+    codes_gathered = False
     if exchange and method in ("auto", "bitset", "sorted"):
         # the exchange every rank takes (collective): the dictionary exchange
         # when its per-rank memory estimate fits, else the code all-gather
@@ -223,7 +225,28 @@ def main():
         m, bb, bc = local.exchange_plan(want)
         xplan = {"exchange": "bitsets" if m == gdist.METHOD_BITSET else "codes",
                  "est_bytes_per_rank": {"bitsets": bb if math.isfinite(bb) else None, "codes": bc}}
-        method = "bitset" if m == gdist.METHOD_BITSET else "sorted"
+        if m == gdist.METHOD_BITSET:
+            method = "bitset"
+        else:
+            # ONE code all-gather, consuming the local shard (peak (ranks + 1) x
+            # shard); then METHOD_AUTO on the gathered collection priced on this
+            # rank's block: the dictionary tiers built from the gathered codes
+            # (C4: dense ancestral words + the variant tier), or the sorted join
+            gathered = local.allgather(consume=True)
+            if method == "sorted":
+                local = gathered
+            else:
+                if args.rows:
+                    a, b = (int(x) for x in args.rows.split(":"))
+                else:
+                    bnd = shard.triangle_bounds(n_total, world, 1)
+                    a, b = bnd[rank], bnd[rank + 1]
+                chosen, cb, cs = gathered.prepare(gdist.METHOD_AUTO, pairs=float(shard.pairs_in_rows(n_total, a, b)))
+                auto = {"chosen": {gdist.METHOD_BITSET: "bitset", gdist.METHOD_SORTED: "sorted"}[chosen],
+                        "est_bitset_s": round(cb, 4), "est_sorted_s": round(cs, 4), "after": "code all-gather"}
+                method = auto["chosen"]
+                local = gathered
+            codes_gathered = True            # the gathered collection is what the step reads
     elif method == "auto":
         # METHOD_AUTO's own decision on one GPU (gdist_sets_prepare)
         chosen, cb, cs = local.prepare(gdist.METHOD_AUTO)
@@ -231,17 +254,19 @@ def main():
                 "est_bitset_s": round(cb, 4), "est_sorted_s": round(cs, 4)}
         method = auto["chosen"]
     if method == "bitset":
-        sets = local.allgather_bitsets() if exchange else local
+        sets = local.allgather_bitsets() if exchange and not codes_gathered else local
         if not exchange and auto is None:
             sets.build_bitsets()
         dict_size, width_words = sets.bitset_info()
         rare = dict(zip(("threshold", "lists", "records"), sets.rare_info()))
         rare["kmers"] = sets.rare_kmers()
         sparse_words = dict(zip(("sparse_words", "dense_words", "entries"), sets.sparse_info()))
+        vinfo = sets.variant_info()
+        variant = dict(zip(("kmers", "words", "entries", "products"), vinfo)) if vinfo[0] else None
         mflag = gdist.METHOD_BITSET
     elif method == "sorted":
         # the code all-gather consumes the local shard: peak (ranks + 1) x shard
-        sets = local.allgather(consume=True) if exchange else local
+        sets = local.allgather(consume=True) if exchange and not codes_gathered else local
         mflag = gdist.METHOD_SORTED
     else:
         sk_local = local.sketches(cfg["width"])
@@ -494,6 +519,7 @@ def main():
                        "bitset_words_per_set": width_words or None,
                        "dictionary_size": (dict_size if method == "bitset" else None),
                        "method": method, "auto": auto, "rare_tier": rare, "complement_sparse": sparse_words,
+                       "variant_tier": variant,
                        "options": options or None},
             "roofline": roof,
             "verified": verified,

@@ -1234,6 +1234,41 @@ int gdist_sets_allgather_ex(gdist_ctx* ctx, gdist_sets* local, unsigned flags, g
             allgather(ctx, so.p, ao.p, ob);
             d2h(hoff.data(), ao.p, ob * R, st);
         }
+        // rank 0's locus guides (pack time: the first sequences' windows) travel
+        // with the gathered collection: the bitset build's locus order and the
+        // variant tier's substitution keys read them (one small all-gather of
+        // every rank's guides, padded; slot 0 kept)
+        int64_t g0 = 0;
+        DevBuf gcodes, gkeys;
+        if (local->kind != GDIST_SKETCH) {
+            DevBuf mg(8, st), ag(8 * R, st);
+            h2d(mg.p, &local->n_guide, 8, st);
+            allgather(ctx, mg.p, ag.p, 8);
+            std::vector<int64_t> hg(R);
+            d2h(hg.data(), ag.p, 8 * R, st);
+            int64_t mx = 0;
+            for (int64_t v : hg) mx = std::max(mx, v);
+            g0 = hg[0];
+            if (mx > 0) {
+                const size_t gb = (size_t)mx * 16;
+                DevBuf sg(gb, st), all(gb * R, st);
+                GD_HIP(hipMemsetAsync(sg.p, 0, gb, st));
+                if (local->n_guide) {
+                    GD_HIP(hipMemcpyAsync(sg.p, local->guide_codes.p, local->n_guide * 8, hipMemcpyDeviceToDevice, st));
+                    GD_HIP(hipMemcpyAsync(static_cast<char*>(sg.p) + mx * 8, local->guide_keys.p, local->n_guide * 8,
+                                          hipMemcpyDeviceToDevice, st));
+                }
+                allgather(ctx, sg.p, all.p, gb);
+                gcodes.alloc(g0 * 8 + 8, st);
+                gkeys.alloc(g0 * 8 + 8, st);
+                if (g0) {
+                    GD_HIP(hipMemcpyAsync(gcodes.p, all.p, g0 * 8, hipMemcpyDeviceToDevice, st));
+                    GD_HIP(hipMemcpyAsync(gkeys.p, static_cast<char*>(all.p) + mx * 8, g0 * 8, hipMemcpyDeviceToDevice,
+                                          st));
+                }
+                GD_HIP(hipStreamSynchronize(st));
+            }
+        }
         const bool consume = (flags & GDIST_ALLGATHER_CONSUME) != 0;
         DevBuf ac;
         if (consume && R == 1 && local->codes.bytes >= cb) {
@@ -1281,6 +1316,9 @@ int gdist_sets_allgather_ex(gdist_ctx* ctx, gdist_sets* local, unsigned flags, g
             GD_HIP(hipStreamSynchronize(st));
         }
         s->codes = std::move(ac);                     // R x cb bytes; the compacted codes first
+        s->guide_codes = std::move(gcodes);
+        s->guide_keys = std::move(gkeys);
+        s->n_guide = g0;
         s->off.alloc((ns + 1) * 8, st);
         h2d(s->off.p, s->h_off.data(), (ns + 1) * 8, st);
         GD_HIP(hipStreamSynchronize(st));

@@ -75,16 +75,33 @@ def main():
     log(f"consuming code all-gather done (estimates: bitsets {bb:.3g} B, codes {bc:.3g} B per rank)")
     bounds = shard.triangle_bounds(N, 8, 1)
     last = bounds[7]
+    # METHOD_AUTO on the gathered codes, priced on rank 0's block (what the
+    # 8-GPU bench asks): the dictionary tiers built from the gathered codes
+    # by code ranges — dense ancestral words, the variant tier of the
+    # single-substitution kmers, rare posting lists — against the sorted join
+    t = time.time()
+    chosen, cb, cs = gs.prepare(gdist.METHOD_AUTO, pairs=float(shard.pairs_in_rows(N, bounds[0], bounds[1])))
+    vk, vw, ve, vp = gs.variant_info()
+    log(f"METHOD_AUTO: {'bitset' if chosen == gdist.METHOD_BITSET else 'sorted'} (est. bitset {cb:.3g} s, "
+        f"sorted {cs:.3g} s, {time.time() - t:.1f} s to build); dense words {gs.bitset_info()[1]}, variant tier "
+        f"{vk} kmers in {vw} words, {ve} entries, {vp:.3g} products; rare {gs.rare_info()}")
+    assert chosen == gdist.METHOD_BITSET and vk > 1_000_000, "C4 takes the variant tier"
     slices = [(0, 64), (last, last + 16)]
     rows = {0: None, 63: None, last: None}
-    for (a, b) in slices:
-        t = time.time()
-        I, D = gs.matrix((a, b), (0, N), upper=True, method=gdist.METHOD_SORTED)
-        log(f"slice rows [{a}, {b}) x {N} columns: {time.time() - t:.2f} s")
-        for i in rows:
-            if a <= i < b:
-                rows[i] = (I[i - a].copy(), D[i - a].copy())
-        del I, D
+    for method, name in ((gdist.METHOD_BITSET, "bitset+variant"), (gdist.METHOD_SORTED, "sorted join")):
+        for (a, b) in slices:
+            t = time.time()
+            I, D = gs.matrix((a, b), (0, N), upper=True, method=method)
+            log(f"{name}: slice rows [{a}, {b}) x {N} columns: {time.time() - t:.2f} s")
+            for i in rows:
+                if a <= i < b:
+                    if rows[i] is None:
+                        rows[i] = (I[i - a].copy(), D[i - a].copy())
+                    else:                            # both methods: the same bits
+                        js = np.arange(i + 1, N)
+                        assert np.array_equal(rows[i][0][js], I[i - a][js]), (name, i)
+                        assert np.array_equal(rows[i][1][js].view(np.uint64), D[i - a][js].view(np.uint64)), (name, i)
+            del I, D
     # the oracle: every genome's codes, intersected with the three row sets
     row_ids = sorted(rows)
     row_codes = [oracle.kmer_codes(bytes(blob[off[i]:off[i + 1]]), K, 0, 0) for i in row_ids]

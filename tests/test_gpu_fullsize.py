@@ -194,7 +194,7 @@ def test_c5_full_size_vs_oracle(ctx):
 
 def test_pack_after_bitset_workload_regression(ctx):
     """The sequence that produced wrong codes under the stream-ordered pool
-    (scripts/diag/diag_pack.py): sorted and bitset matrix workloads, then a
+    (round 1's diag_pack.py diagnostic): sorted and bitset matrix workloads, then a
     pack of another collection, in one process and on one context. Codes,
     sizes and a matrix of the fresh pack equal the oracle on every trial."""
     import gdist
