@@ -32,7 +32,7 @@ from gdist import shard, synth  # noqa: E402
 CASES = {
     "base": dict(n=301, L=6000, p=0.01, cfg=11, legs=("bitset", "sorted", "sketch")),
     "sparse": dict(n=300, L=150_000, p=0.002, cfg=12, legs=("bitset",), sparse=True),
-    "c4": dict(n=200, L=100_000, p=0.05, cfg=4, legs=("auto", "sorted", "codes_plan")),
+    "c4": dict(n=200, L=100_000, p=0.05, cfg=4, legs=("auto", "sorted", "codes_plan", "codes_variant")),
 }
 SKETCH_W = 200
 
@@ -86,6 +86,22 @@ def run_case(name, c, ctx, rank, world):
                 except ValueError:
                     pass
             results[leg] = gs.matrix((r0, r1), (0, n), upper=True, method=gdist.METHOD_SORTED)
+        elif leg == "codes_variant":
+            # C4's 8-GPU path: the consuming code all-gather, then on every rank
+            # the dictionary tiers of the gathered codes with the variant tier
+            # (forced at this size: kmers of 2..19 sets are variant words),
+            # located by rank 0's guides that travel with the gather
+            own = gdist.KmerSets.from_sequences(seqs[s0:s1], 21, gdist.KmerType.DNA, 0, ctx)
+            gs = own.allgather(consume=True)
+            for k, v in (("variant", 1), ("rare_t", 2), ("variant_dmin", 20), ("range_summary", 1)):
+                ctx.set_option(k, v)
+            m, _, _ = gs.prepare(gdist.METHOD_BITSET)
+            vk, vw, ve, _ = gs.variant_info()
+            assert vk > 0 and ve > 0 and vw * 4 < vk, (rank, vk, vw, ve)
+            info["variant"] = (vk, vw, ve)
+            results[leg] = gs.matrix((r0, r1), (0, n), upper=True, method=gdist.METHOD_BITSET)
+            for k in ("variant", "rare_t", "variant_dmin", "range_summary"):
+                ctx.set_option(k, None)
         elif leg == "sketch":
             sk = local.sketches(SKETCH_W).allgather()
             assert len(sk) == n
@@ -117,7 +133,7 @@ def run_case(name, c, ctx, rank, world):
             assert np.array_equal(D[up].view(np.uint64), eD[a:b][up].view(np.uint64)), (name, m, a, b)
         rows += b - a
     assert rows == n
-    print(f"CASE_OK {name} {world} {gathered[0][3].get('sparse', '')}", flush=True)
+    print(f"CASE_OK {name} {world} {gathered[0][3].get('sparse', '')} {gathered[0][3].get('variant', '')}", flush=True)
 
 
 def main():
