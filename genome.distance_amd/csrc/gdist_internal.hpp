@@ -532,6 +532,7 @@ bool sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
 // variant.hip — the variant tier
 constexpr double kVariantProductsPerS = 2.0e10;  // variant_rows_kernel: popc products (estimate)
 constexpr int64_t kVariantMaxT = 32;             // rare threshold of a variant build (unless given)
+constexpr int64_t kVariantMinSets = 4096;        // collections the variant tier is considered for by default
 constexpr int64_t kRangeSummaryMin = int64_t(1) << 31;   // codes past which an unsummarised collection counts by range
 constexpr double kVariantVisitsPerS = 2.0e9;     // ... (entry, column chunk) visits with their list search
 int64_t variant_dmin(const gdist_ctx* ctx, int64_t nsets);

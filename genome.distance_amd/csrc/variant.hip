@@ -869,13 +869,15 @@ void build_variant_bitsets(gdist_ctx* ctx, gdist_sets* s, DevBuf& dict, DevBuf& 
 
 // Decides after the dictionary of build_bitsets whether the collection takes
 // the variant tier: option variant = 1 forces it, 0 keeps the two tiers;
-// by default when the kmers held by T .. Dmin - 1 sets are many (>= 4096)
-// and at least a quarter of the dictionary (C4: 12.6 M of 12.8 M).
+// by default for large collections (>= kVariantMinSets sets: smaller ones
+// keep the measured two-tier paths) whose kmers held by T .. Dmin - 1 sets
+// are many (>= 4096) and at least a quarter of the dictionary (C4: 12.6 M of
+// 12.8 M).
 bool variant_wanted(const gdist_ctx* ctx, int64_t nsets, int64_t mid_kmers, int64_t dict_kmers) {
     const int64_t opt = ctx->option(OPT_VARIANT, -1);
     if (opt == 0) return false;
     if (opt > 0) return mid_kmers > 0;
-    return mid_kmers >= 4096 && 4 * mid_kmers >= dict_kmers && nsets >= 64;
+    return nsets >= kVariantMinSets && mid_kmers >= 4096 && 4 * mid_kmers >= dict_kmers;
 }
 
 namespace {
