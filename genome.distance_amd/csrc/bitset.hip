@@ -1658,10 +1658,16 @@ void build_bitsets(gdist_ctx* ctx, gdist_sets* s, unsigned flags, int64_t rare_t
     // unless given: kmers shared by a few sets stay posting lists, the rest
     // of the non-dense kmers form the variant words
     if (!keep) {
+        // the variant tier's rare threshold: the model's T (which prices the
+        // kmers below Dmin as dense words or posting lists only) capped at
+        // kVariantMaxT unless given; its share of the summary decides
         const int64_t dmin = variant_dmin(ctx, s->nsets);
-        if (variant_wanted(ctx, s->nsets, count_below(ctx, dcnt.as<uint32_t>(), U, dmin), U)) {
-            if (T_in < 0 && !ctx->has_option(OPT_RARE_T) && T > kVariantMaxT) {
-                T = kVariantMaxT;
+        const int64_t Tv = (T_in >= 0 || ctx->has_option(OPT_RARE_T)) ? T : std::min<int64_t>(T, kVariantMaxT);
+        const int64_t mid = count_in_range(ctx, sum.counts.as<uint32_t>(), sum.n, Tv, dmin);
+        const int64_t ge = count_in_range(ctx, sum.counts.as<uint32_t>(), sum.n, Tv, INT64_MAX);
+        if (variant_wanted(ctx, s->nsets, mid, ge)) {
+            if (Tv != T) {
+                T = Tv;
                 dictionary_from(ctx, {SummaryView{sum.codes.as<uint64_t>(), sum.counts.as<uint32_t>(), sum.n}}, false,
                                 T, s->nsets, dict, U, rare, Ur, mass, &dcnt);
             }

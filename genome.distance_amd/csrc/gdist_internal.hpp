@@ -537,7 +537,8 @@ constexpr int64_t kRangeSummaryMin = int64_t(1) << 31;   // codes past which an 
 constexpr double kVariantVisitsPerS = 2.0e9;     // ... (entry, column chunk) visits with their list search
 int64_t variant_dmin(const gdist_ctx* ctx, int64_t nsets);
 bool variant_wanted(const gdist_ctx* ctx, int64_t nsets, int64_t mid_kmers, int64_t dict_kmers);
-int64_t count_below(gdist_ctx* ctx, const uint32_t* dcounts, int64_t U, int64_t dmin);
+// summary entries held by lo <= count < hi sets
+int64_t count_in_range(gdist_ctx* ctx, const uint32_t* counts, int64_t n, int64_t lo, int64_t hi);
 // builds bits (dense tier), the rare postings and the variant tier from the
 // dictionary (dict: codes held by >= T sets, dcounts their holders)
 void build_variant_bitsets(gdist_ctx* ctx, gdist_sets* s, DevBuf& dict, DevBuf& dcounts, int64_t U, DevBuf& rare,

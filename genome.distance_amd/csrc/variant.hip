@@ -881,22 +881,23 @@ bool variant_wanted(const gdist_ctx* ctx, int64_t nsets, int64_t mid_kmers, int6
 }
 
 namespace {
-__global__ void mid_count_kernel(const uint32_t* __restrict__ cnt, int64_t n, uint32_t dmin,
-                                 unsigned long long* __restrict__ out) {
+__global__ void range_count_kernel(const uint32_t* __restrict__ cnt, int64_t n, int64_t lo, int64_t hi,
+                                   unsigned long long* __restrict__ out) {
     unsigned long long c = 0;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) c += cnt[i] < dmin;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        c += (int64_t)cnt[i] >= lo && (int64_t)cnt[i] < hi;
     for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
     if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, c);
 }
 }  // namespace
 
-int64_t count_below(gdist_ctx* ctx, const uint32_t* dcounts, int64_t U, int64_t dmin) {
+int64_t count_in_range(gdist_ctx* ctx, const uint32_t* counts, int64_t n, int64_t lo, int64_t hi) {
     hipStream_t st = ctx->stream;
-    if (U == 0) return 0;
+    if (n == 0) return 0;
     DevBuf o(8, st);
     GD_HIP(hipMemsetAsync(o.p, 0, 8, st));
-    mid_count_kernel<<<grid_for(U, 256, 4096), 256, 0, st>>>(dcounts, U, (uint32_t)dmin, o.as<unsigned long long>());
+    range_count_kernel<<<grid_for(n, 256, 4096), 256, 0, st>>>(counts, n, lo, hi, o.as<unsigned long long>());
     GD_HIP(hipGetLastError());
     unsigned long long h = 0;
     d2h(&h, o.p, 8, st);
