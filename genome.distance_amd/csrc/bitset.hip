@@ -1285,6 +1285,18 @@ __global__ __launch_bounds__(1024) void pos_bits_kernel(const uint32_t* __restri
 // positions + LDS slices; option fill_sort 1: the chunked pairs sort + run
 // ranks + scatter; 2: the one-pass windowed searches with global atomics);
 // rare-tier records appended to rare_out (capacity cap)
+void bits_from_positions(gdist_ctx* ctx, const gdist_sets* s, const uint32_t* pos, int64_t s0, int64_t s1,
+                         int64_t base, int64_t W, unsigned long long* bits) {
+    const unsigned nslice = (unsigned)ceil_div(2 * W, kPosSlice);
+    if (W == 0) return;
+    for (int64_t c0 = s0; c0 < s1; c0 += 65535) {
+        const unsigned ny = (unsigned)std::min<int64_t>(65535, s1 - c0);
+        pos_bits_kernel<<<dim3(nslice, ny), 1024, 0, ctx->stream>>>(pos, s->off.as<int64_t>(), c0, base, W,
+                                                                     reinterpret_cast<uint32_t*>(bits));
+        GD_HIP(hipGetLastError());
+    }
+}
+
 void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_t U, int64_t W,
                unsigned long long* bits, const uint64_t* rare, int64_t Ur, int64_t id_base,
                unsigned long long* rare_out, int64_t rare_cap, int64_t* rare_written, const uint32_t* perm,

@@ -438,6 +438,10 @@ int64_t choose_rare_threshold(const std::vector<uint64_t>& hist, int64_t nsets);
 // with the chunk's position array (u32 per code from code `base`; ~0 outside
 // the dictionary) before it is released (variant.hip: the variant records)
 using FillHook = std::function<void(const uint32_t* pos, int64_t s0, int64_t s1, int64_t base)>;
+// the bits of sets [s0, s1) from their codes' positions (pos from code `base`;
+// positions past the W words and ~0 are skipped): LDS row slices, no atomics
+void bits_from_positions(gdist_ctx* ctx, const gdist_sets* s, const uint32_t* pos, int64_t s0, int64_t s1,
+                         int64_t base, int64_t W, unsigned long long* bits);
 void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_t U, int64_t W,
                unsigned long long* bits, const uint64_t* rare, int64_t Ur, int64_t id_base,
                unsigned long long* rare_out, int64_t rare_cap, int64_t* rare_written,

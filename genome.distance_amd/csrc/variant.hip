@@ -261,6 +261,89 @@ __global__ void combine_perm_kernel(const int32_t* __restrict__ dense, const int
         perm[r] = dense[r] ? (dperm ? dperm[dpos[r]] : (uint32_t)dpos[r]) : mperm[mpos_idx[r]];
 }
 
+// ---- the hash fill --------------------------------------------------------
+// The windowed fill (bitset.hip fill_pos_kernel) stages a stretch of the
+// sorted dictionary per segment of a set's codes: made for dictionaries about
+// the size of a set (C2: 4 M each). C4's dictionary of kmers held by >= 2
+// sets is 377 M codes against 200 K per set, so every segment's windows spill
+// to global walks (25 s). Here every code of the dictionary goes into an
+// open-addressing table (linear probing, load <= 1/2, 16-byte slots
+// {code, tagged value}) and each set's codes probe it: one or two lines per
+// code, coalesced reads of the codes. Values: kPosTag | bit position (dense
+// or variant), kRareTag | rare rank.
+constexpr unsigned long long kHashEmpty = ~0ull;
+constexpr unsigned long long kPosTag = 1ull << 62, kRareTag = 2ull << 62, kTagMask = 3ull << 62;
+
+__device__ __forceinline__ unsigned long long hmix(unsigned long long x) {
+    x ^= x >> 33;
+    x *= 0xFF51AFD7ED558CCDull;
+    x ^= x >> 33;
+    x *= 0xC4CEB9FE1A85EC53ull;
+    x ^= x >> 33;
+    return x;
+}
+
+// inserts codes[0, n) with values tag | (perm ? perm[i] : i)
+__global__ void hash_insert_kernel(const uint64_t* __restrict__ codes, int64_t n, const uint32_t* __restrict__ perm,
+                                   unsigned long long tag, unsigned long long* __restrict__ tab,
+                                   unsigned long long mask) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const unsigned long long code = codes[i];
+        const unsigned long long val = tag | (perm ? (unsigned long long)perm[i] : (unsigned long long)i);
+        unsigned long long slot = hmix(code) & mask;
+        for (;;) {
+            const unsigned long long prev = atomicCAS(tab + 2 * slot, kHashEmpty, code);
+            if (prev == kHashEmpty || prev == code) {
+                tab[2 * slot + 1] = val;
+                break;
+            }
+            slot = (slot + 1) & mask;
+        }
+    }
+}
+
+// one workgroup per set of the chunk: every code probes the table; positions
+// go to pos (u32, ~0: not dense / variant), rare codes append their record
+// (rare rank << 32 | set) with one atomic per wave
+__global__ __launch_bounds__(256) void hash_probe_kernel(const uint64_t* __restrict__ codes,
+                                                         const int64_t* __restrict__ off, int64_t s0, int64_t base,
+                                                         const unsigned long long* __restrict__ tab,
+                                                         unsigned long long mask, uint32_t* __restrict__ pos,
+                                                         unsigned long long* __restrict__ rare_out,
+                                                         unsigned long long* __restrict__ rare_cnt, int64_t rare_cap) {
+    const int64_t set = s0 + blockIdx.x;
+    const int lane = threadIdx.x & 63;
+    const int64_t b = off[set], e = off[set + 1];
+    for (int64_t x0 = b; x0 < e; x0 += 256) {
+        const int64_t x = x0 + threadIdx.x;
+        unsigned long long val = kHashEmpty;
+        if (x < e) {
+            const unsigned long long code = codes[x];
+            unsigned long long slot = hmix(code) & mask;
+            for (;;) {
+                const ulonglong2 kv = *reinterpret_cast<const ulonglong2*>(tab + 2 * slot);
+                if (kv.x == code) { val = kv.y; break; }
+                if (kv.x == kHashEmpty) break;
+                slot = (slot + 1) & mask;
+            }
+            pos[x - base] = (val != kHashEmpty && (val & kTagMask) == kPosTag) ? (uint32_t)(val & 0xFFFFFFFFull) : ~0u;
+        }
+        const bool rhit = val != kHashEmpty && (val & kTagMask) == kRareTag;
+        const unsigned long long m = __ballot(rhit);
+        if (m) {
+            unsigned long long b0 = 0;
+            if (lane == __ffsll((long long)m) - 1) b0 = atomicAdd(rare_cnt, (unsigned long long)__popcll(m));
+            b0 = (unsigned long long)__shfl((long long)b0, __ffsll((long long)m) - 1, 64);
+            if (rhit) {
+                const unsigned long long slotr = b0 + __popcll(m & ((1ull << lane) - 1));
+                if ((int64_t)slotr < rare_cap)
+                    rare_out[slotr] = ((val & 0xFFFFFFFFull) << 32) | (unsigned long long)(uint32_t)set;
+            }
+        }
+    }
+}
+
 // ---- variant records of one fill chunk -----------------------------------
 // per set of the chunk: its variant positions (>= vbase) counted, then
 // written as keys (word << (sbits + 6) | set << 6 | bit)
@@ -634,6 +717,48 @@ static CodeGeom code_geom(const gdist_sets* s) {
     return g;
 }
 
+// The fill of a variant build: dense bits, rare records and (through the
+// hook) the variant records of every chunk of sets, by hash probes (above)
+static void hash_fill(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_t U, const uint32_t* perm,
+                      const uint64_t* rare, int64_t Ur, int64_t W, unsigned long long* bits,
+                      unsigned long long* rare_out, int64_t rare_cap, int64_t* rare_written, const FillHook& hook) {
+    hipStream_t st = ctx->stream;
+    Trace tr(st, ctx->trace());
+    GD_REQUIRE(Ur < (int64_t(1) << 32) && U < (int64_t(1) << 32), "dictionary too large for the hash fill");
+    GD_HIP(hipMemsetAsync(bits, 0, (size_t)s->nsets * W * 8, st));
+    int64_t cap = 2;
+    while (cap < 2 * (U + Ur)) cap <<= 1;                   // load <= 1/2
+    DevBuf tab((size_t)cap * 16, st), rcnt(8, st);
+    GD_HIP(hipMemsetAsync(tab.p, 0xFF, (size_t)cap * 16, st));
+    GD_HIP(hipMemsetAsync(rcnt.p, 0, 8, st));
+    const unsigned long long mask = (unsigned long long)cap - 1;
+    if (U) hash_insert_kernel<<<grid_for(U, 256, 256 * 64), 256, 0, st>>>(dict, U, perm, kPosTag,
+                                                                           tab.as<unsigned long long>(), mask);
+    if (Ur) hash_insert_kernel<<<grid_for(Ur, 256, 256 * 64), 256, 0, st>>>(rare, Ur, nullptr, kRareTag,
+                                                                             tab.as<unsigned long long>(), mask);
+    GD_HIP(hipGetLastError());
+    tr.mark("fill: hash table");
+    int64_t s0 = 0;
+    while (s0 < s->nsets) {
+        int64_t s1 = s0 + 1;
+        while (s1 < s->nsets && s->h_off[s1 + 1] - s->h_off[s0] <= (int64_t(1) << 30)) s1++;
+        const int64_t base = s->h_off[s0], n = s->h_off[s1] - base;
+        DevBuf pos(std::max<int64_t>(1, n) * 4 + 16, st);
+        hash_probe_kernel<<<(unsigned)(s1 - s0), 256, 0, st>>>(s->codes.as<uint64_t>(), s->off.as<int64_t>(), s0, base,
+                                                               tab.as<unsigned long long>(), mask, pos.as<uint32_t>(),
+                                                               rare_out, rcnt.as<unsigned long long>(), rare_cap);
+        GD_HIP(hipGetLastError());
+        if (hook) hook(pos.as<uint32_t>(), s0, s1, base);
+        bits_from_positions(ctx, s, pos.as<uint32_t>(), s0, s1, base, W, bits);
+        GD_HIP(hipStreamSynchronize(st));
+        tr.mark("fill: probes + bits + variant records");
+        s0 = s1;
+    }
+    unsigned long long w = 0;
+    d2h(&w, rcnt.p, 8, st);
+    *rare_written = (int64_t)w;
+}
+
 int64_t variant_dmin(const gdist_ctx* ctx, int64_t nsets) {
     return ctx->has_option(OPT_VARIANT_DMIN) ? std::max<int64_t>(2, ctx->option(OPT_VARIANT_DMIN, 2))
                                              : std::max<int64_t>(2, nsets / 10);
@@ -787,8 +912,14 @@ void build_variant_bitsets(gdist_ctx* ctx, gdist_sets* s, DevBuf& dict, DevBuf& 
     s->bits.alloc((size_t)N * Wd * 8 + 8, st);
     DevBuf recs(mass * 8 + 8, st);
     int64_t written = 0;
-    fill_bits(ctx, s, dict.as<uint64_t>(), U, Wd, s->bits.as<unsigned long long>(), rare.as<uint64_t>(), Ur, 0,
-              recs.as<unsigned long long>(), mass, &written, perm.as<uint32_t>(), hook);
+    // the hash fill (default) or the windowed fill of the two-tier build
+    // (option fill_sort = 3 selects the windowed one: A/B, parity)
+    if (ctx->option(OPT_FILL_SORT, 0) == 3)
+        fill_bits(ctx, s, dict.as<uint64_t>(), U, Wd, s->bits.as<unsigned long long>(), rare.as<uint64_t>(), Ur, 0,
+                  recs.as<unsigned long long>(), mass, &written, perm.as<uint32_t>(), hook);
+    else
+        hash_fill(ctx, s, dict.as<uint64_t>(), U, perm.as<uint32_t>(), rare.as<uint64_t>(), Ur, Wd,
+                  s->bits.as<unsigned long long>(), recs.as<unsigned long long>(), mass, &written, hook);
     GD_REQUIRE(written == mass, "rare-tier record count mismatch");
     tr.mark("variant: fill (dense bits, rare and variant records)");
     build_postings(ctx, s, recs.as<unsigned long long>(), written, Ur);

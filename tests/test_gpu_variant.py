@@ -36,12 +36,13 @@ REGIONS = [(0, 1200, 0, 1200, True), (37, 211, 5, 1190, False), (600, 1200, 0, 1
            (1199, 1200, 0, 1200, False)]
 
 
-@pytest.mark.parametrize("mode", ["variant", "variant_rows_u32", "range_only", "two_tier"])
+@pytest.mark.parametrize("mode", ["variant", "variant_windowed_fill", "range_only", "two_tier"])
 def test_variant_tier_exact(ctx, opts, c4_like, mode):
-    """Counts and distances of the variant tier (and of the code-range
-    dictionary alone) equal the oracle's over upper triangles, rectangles,
-    unaligned row blocks and row queries; the grouping puts each
-    substitution's kmers into one word (words << kmers)."""
+    """Counts and distances of the variant tier (its hash fill and the
+    windowed fill; the code-range dictionary alone; the two tiers) equal the
+    oracle's over upper triangles, rectangles, unaligned row blocks and row
+    queries; the grouping puts each substitution's kmers into one word
+    (words << kmers)."""
     import gdist
     seqs, off, codes = c4_like
     n = len(seqs)
@@ -50,8 +51,9 @@ def test_variant_tier_exact(ctx, opts, c4_like, mode):
     elif mode == "range_only":
         opts(variant=0, rare_t=3, range_summary=1)
     else:
+        # the hash fill (default) or the two-tier build's windowed fill (fill_sort 3)
         opts(variant=1, rare_t=3, variant_dmin=n // 10, range_summary=1,
-             rare_u16=0 if mode == "variant_rows_u32" else None)
+             fill_sort=3 if mode == "variant_windowed_fill" else None)
     sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
     sets.build_bitsets()
     vk, vw, ve, vp = sets.variant_info()
