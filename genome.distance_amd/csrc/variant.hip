@@ -38,12 +38,13 @@
 // bits, variant codes emit (word, set, bit) records that are sorted and
 // OR-merged per set chunk), then the word lists and the set -> entry CSR.
 //
-// Walk (variant_rows_kernel, bitset_matrix): one workgroup per (row set,
-// column chunk); a wave takes one of the row's entries and its 64 lanes
-// stream the entry's word list (sets ascending, coalesced 4 + 8 bytes per
-// member) from the row's own position (upper triangle) or the chunk's first
-// column (a wave-uniform binary search), adding popc(mask_i & mask_j) into
-// LDS counters; the counters are added to I's row once.
+// Walk (variant_rows_kernel, bitset_matrix): one workgroup per row (or a
+// slice of its entries); a wave takes one of the row's entries and its 64
+// lanes stream the entry's word list (sets ascending, coalesced 4 + 8 bytes
+// per member) from the row's own position (upper triangle), adding
+// popc(mask_i & mask_j) into LDS counters of one column chunk at a time; each
+// entry's list position stays in LDS from chunk to chunk, so every list is
+// read once; each chunk's counters are added to I's row once.
 #include <algorithm>
 #include <cstring>
 #include <vector>
@@ -497,65 +498,81 @@ __global__ void word_products_kernel(const int64_t* __restrict__ woff, int64_t n
 constexpr int VCH = 16384;   // columns per LDS chunk (64 KiB of counters)
 
 namespace {
-// first y in [lo, hi) with vset[y] >= t (wave-uniform)
-__device__ __forceinline__ int64_t set_lower_bound(const uint32_t* __restrict__ vset, int64_t lo, int64_t hi,
-                                                   uint32_t t) {
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (vset[mid] < t) lo = mid + 1; else hi = mid;
-    }
-    return lo;
-}
-
-// grid = rows x column chunks x nsplit slices of the row's entries
+// grid = rows x nsplit slices of the row's entries. A workgroup takes its
+// entries in batches of VBATCH and walks the column chunks in order; each
+// entry's list position is kept in LDS between chunks (lists are sorted by
+// set), so a list is read once across all chunks and no chunk searches it.
+constexpr int VBATCH = 2048;
 __global__ __launch_bounds__(256) void variant_rows_kernel(const int64_t* __restrict__ soff,
                                                            const uint32_t* __restrict__ sent,
                                                            const uint32_t* __restrict__ vset,
                                                            const unsigned long long* __restrict__ vmask,
                                                            const uint32_t* __restrict__ vbeg,
                                                            const uint32_t* __restrict__ vend, int64_t r0, int64_t r1,
-                                                           int64_t c0, int64_t c1, int nch, int nsplit, int upper,
+                                                           int64_t c0, int64_t c1, int nsplit, int upper,
                                                            int32_t* __restrict__ I, int64_t ldI) {
     __shared__ int32_t cnt[VCH];
-    const int64_t unit = blockIdx.x / nsplit;
+    __shared__ uint32_t ypos[VBATCH];
+    const int64_t i = r0 + blockIdx.x / nsplit;
     const int split = blockIdx.x % nsplit;
-    const int64_t i = r0 + unit / nch;
-    const int ch = (int)(unit % nch);
-    const int64_t cb = c0 + (int64_t)ch * VCH;
-    const int64_t ce = cb + VCH < c1 ? cb + VCH : c1;
-    if (i >= r1 || cb >= ce || (upper && ce - 1 <= i)) return;
-    const int n = (int)(ce - cb);
-    for (int t = threadIdx.x; t < n; t += blockDim.x) cnt[t] = 0;
-    __syncthreads();
-    const int64_t lo = upper && i + 1 > cb ? i + 1 : cb;
+    if (i >= r1) return;
+    const int64_t lo = upper && i + 1 > c0 ? i + 1 : c0;      // first column of the row
+    if (lo >= c1) return;
     const int64_t rb = soff[i], re = soff[i + 1];
     const int64_t per = (re - rb + nsplit - 1) / nsplit;
     const int64_t xb = rb + per * split;
     const int64_t xe = xb + per < re ? xb + per : re;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int64_t x = xb + wv; x < xe; x += 4) {                // a wave per entry of the row
-        const uint32_t e = sent[x];
-        const unsigned long long mi = vmask[e];
-        // the list from the chunk's first column (upper: past the row itself)
-        int64_t y = upper ? (int64_t)e + 1 : (int64_t)vbeg[e];
-        const int64_t ye = vend[e];
-        if (ye - y > 64) y = set_lower_bound(vset, y, ye, (uint32_t)lo);
-        for (; y < ye; y += 64) {
-            const int64_t yy = y + lane;
-            const uint32_t j = yy < ye ? vset[yy] : 0xFFFFFFFFu;
-            const unsigned long long mj = yy < ye ? vmask[yy] : 0ull;
-            if ((int64_t)j >= lo && (int64_t)j < ce && (int64_t)j != i) {
-                const int v = __popcll(mi & mj);
-                if (v) atomicAdd(&cnt[j - cb], v);
+    int32_t* row = I + (i - r0) * ldI - c0;                   // row[j] for column j
+    for (int64_t bb = xb; bb < xe; bb += VBATCH) {
+        const int nb = (int)(xe - bb < VBATCH ? xe - bb : VBATCH);
+        // each entry's first list position at or past the row's first column
+        // (upper: the members after the row's own entry)
+        for (int t = wv; t < nb; t += 4) {
+            const uint32_t e = sent[bb + t];
+            int64_t y = upper ? (int64_t)e + 1 : (int64_t)vbeg[e];
+            const int64_t ye = vend[e];
+            if (!upper || lo > i + 1) {                        // columns below lo: one search
+                int64_t a = y, z = ye;
+                while (a < z) {
+                    const int64_t mid = (a + z) >> 1;
+                    if ((int64_t)vset[mid] < lo) a = mid + 1; else z = mid;
+                }
+                y = a;
             }
-            if (!__ballot(yy < ye && (int64_t)j < ce)) break;  // lists ascend: the rest lie past the chunk
+            if (lane == 0) ypos[t] = (uint32_t)y;
         }
-    }
-    __syncthreads();
-    int32_t* row = I + (i - r0) * ldI + (cb - c0);
-    for (int t = threadIdx.x; t < n; t += blockDim.x) {
-        const int v = cnt[t];
-        if (v && cb + t >= lo) atomicAdd(row + t, v);
+        for (int64_t cb = lo - ((lo - c0) % VCH); cb < c1; cb += VCH) {
+            const int64_t ce = cb + VCH < c1 ? cb + VCH : c1;
+            const int n = (int)(ce - cb);
+            __syncthreads();                                   // ypos written; previous chunk flushed
+            for (int t = threadIdx.x; t < n; t += blockDim.x) cnt[t] = 0;
+            __syncthreads();
+            for (int t = wv; t < nb; t += 4) {                 // a wave per entry
+                const uint32_t e = sent[bb + t];
+                const unsigned long long mi = vmask[e];
+                const int64_t ye = vend[e];
+                int64_t y = ypos[t];
+                for (; y < ye;) {
+                    const int64_t yy = y + lane;
+                    const uint32_t j = yy < ye ? vset[yy] : 0xFFFFFFFFu;
+                    const bool in = yy < ye && (int64_t)j < ce;
+                    if (in && (int64_t)j != i) {
+                        const int v = __popcll(mi & vmask[yy]);
+                        if (v) atomicAdd(&cnt[j - cb], v);
+                    }
+                    const unsigned long long m = __ballot(in);
+                    y += __popcll(m);                          // lists ascend: the in-chunk members come first
+                    if (m != ~0ull) break;
+                }
+                if (lane == 0) ypos[t] = (uint32_t)y;
+            }
+            __syncthreads();
+            for (int t = threadIdx.x; t < n; t += blockDim.x) {
+                const int v = cnt[t];
+                if (v && cb + t >= lo) atomicAdd(row + cb + t, v);
+            }
+        }
     }
 }
 
@@ -1039,17 +1056,16 @@ int64_t count_in_range(gdist_ctx* ctx, const uint32_t* counts, int64_t n, int64_
 void variant_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1, bool upper,
                     int32_t* d_I, int64_t ldI, hipStream_t rs) {
     if (!s->variant || r1 <= r0 || c1 <= c0) return;
-    const int nch = (int)ceil_div(c1 - c0, VCH);
-    const int64_t units = (r1 - r0) * nch;
-    // few row units: slice each row's entries over several workgroups
-    const int nsplit = (int)std::max<int64_t>(1, std::min<int64_t>(32, ceil_div((int64_t)ctx->cus * 8, units)));
+    const int64_t units = r1 - r0;
+    // few rows: slice each row's entries over several workgroups
+    const int nsplit = (int)std::max<int64_t>(1, std::min<int64_t>(64, ceil_div((int64_t)ctx->cus * 8, units)));
     const int64_t grid = units * nsplit;
     GD_REQUIRE(grid < (int64_t(1) << 31), "variant-tier grid too large");
     FamilyTimer ft(ctx, GDIST_KERNEL_VARIANT, rs);
     variant_rows_kernel<<<(unsigned)grid, 256, 0, rs>>>(s->vs_off.as<int64_t>(), s->vs_ent.as<uint32_t>(),
                                                         s->vw_set.as<uint32_t>(), s->vw_mask.as<unsigned long long>(),
                                                         s->vw_beg.as<uint32_t>(), s->vw_end.as<uint32_t>(), r0, r1, c0,
-                                                        c1, nch, nsplit, upper ? 1 : 0, d_I, ldI);
+                                                        c1, nsplit, upper ? 1 : 0, d_I, ldI);
     GD_HIP(hipGetLastError());
     ft.end();
 }
