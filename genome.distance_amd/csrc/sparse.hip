@@ -426,6 +426,8 @@ __host__ __device__ __forceinline__ uint32_t row_code(int s) { return ((uint32_t
 __host__ __device__ __forceinline__ uint32_t col_code(int s) {
     return ((uint32_t)(s & 1) << 4) | (((uint32_t)(s >> 1) << 2) << 16);
 }
+constexpr uint32_t kLastOfList = 32;     // column code bit 5 (above the shift, below the offset): the entry ends its (block, word) list
+constexpr int kSentinelRecs = 512;       // zero records after the entries (the virtual word's)
 // the counter add of a product of row code r and column code c (byte address r ^ c >> 16)
 __device__ __forceinline__ void cnt_add(uint32_t* cnt, uint32_t r, uint32_t c, uint32_t v) {
     atomicAdd(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(cnt) + (r ^ (c >> 16))), v << (c & 31));
@@ -449,6 +451,16 @@ __global__ void sparse_records_kernel(const unsigned long long* __restrict__ wor
         const unsigned long long w = word[e];
         ent[e] = make_ulonglong2((unsigned long long)row_code(st) | (w << 32),
                                  (w >> 32) | ((unsigned long long)col_code(st) << 32));
+    }
+}
+
+// column code bit 5 of each (block, word) list's last entry (the walk's
+// second column of an odd list's last pair is then dropped)
+__global__ void sparse_last_kernel(const int64_t* __restrict__ off, int64_t nlists, ulonglong2* __restrict__ ent) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nlists; t += stride) {
+        const int64_t b = off[t], e = off[t + 1];
+        if (e > b) ent[e - 1].y |= (unsigned long long)kLastOfList << 32;
     }
 }
 
@@ -535,20 +547,29 @@ __device__ __forceinline__ void rare_slab_row(const RareSlab& rs, int unit, int6
 // U_s - nc_i - nc_j; with several, each chunk stores its counters to `part`
 // and sparse_reduce_kernel sums them.
 //
-// The instruction stream per slot (round-2 ISA work):
-//   * diagonal and off-diagonal tiles run separate instantiations of the
-//     walk (one uniform branch per batch);
-//   * a word's walk fields are one 16-byte LDS record {first slot | ncol << 24,
-//     row start, column start, 1 / (2 ncp)}: one ds_read_b128 per slot;
+// The instruction stream per slot (round 4; ~26 VALU per 1 x 2 slot, r3: ~47):
+//   * the walk records of a batch's words sit in LDS in slot order, words
+//     without slots left out, so the word of slot f is the number of words
+//     whose last slot is below f: per group of 64 slots one ballot counts the
+//     words ending before the group and a 64-bit mask of the last slots inside
+//     it (built per window of kWinGroups groups with LDS ORs) gives the rest
+//     through mbcnt — two VALU per slot instead of a ballot + readlane search;
 //   * an off-diagonal slot is a 1 x 2 micro-tile: one row entry and a PAIR of
-//     adjacent column entries of one word, so one search and one quotient
-//     serve two products (an odd list's last pair reads the next record and
-//     adds 0); the quotient is exact without a correction step;
+//     adjacent column entries of one word; the row is q / ncp by a float
+//     reciprocal whose low 8 mantissa bits carry 2 ncp (exact: the quotient
+//     (2q + 1) / (2 ncp) stays >= 1/128 from an integer, the packed
+//     reciprocal's error is < 2^-15 relative; checked exhaustively), and the
+//     record offsets are byte offsets, so a slot's quotient and both load
+//     addresses are eight VALU;
+//   * an odd column list's last pair reads the next record as its second
+//     column: that record's product is dropped by the FIRST column's
+//     last-of-list flag (column code bit 5, set at build time), not by a
+//     compare against the list length;
+//   * slots past the batch's last word fall on a virtual word whose records
+//     are zero (the sentinel run after the entries), so no slot is masked;
 //   * an entry is one 16-byte record {row code, word, column code}: a row
 //     loads its first 12 bytes, a column its last 12 (global_load_dwordx3);
-//   * the counter add is unconditional (a zero product adds 0), so no slot
-//     waits on another's branch; idle slots read the zero sentinel record
-//     past the last entry instead of being masked.
+//   * the counter add is unconditional (a zero product adds 0).
 // Counters are 16-bit, two to an LDS dword: a chunk holds at most kChunkWords
 // sparse words, so a pair's count in one chunk is at most 64 x 1023 < 2^16
 // and a packed ds_add_u32 never carries into the neighbour (32 KiB per tile)
@@ -558,140 +579,136 @@ constexpr int kChunkWords = 1023;
 // kFoldSlabWords sparse words
 constexpr int kFoldSlabWords = 8;
 constexpr int SNW = SNT / 64;
+// a wave's LDS (1 KiB of the 8 KiB record area): kBatchWords walk records +
+// the virtual word's, then the window's last-slot masks
+constexpr int kBatchWords = 48;
+constexpr int kWinGroups = 16;
+static_assert((kBatchWords + 1) * 16 + kWinGroups * 8 <= 1024, "a wave's walk LDS");
 
 struct SparseWalk {
-    const ulonglong2* eA;                 // the chunk's row-side records
-    const ulonglong2* eB;                 // ... and column-side records
+    const char* eA;                       // the chunk's row-side records (bytes)
+    const char* eB;                       // ... and column-side records
 };
 
-// Word of slot f: #{l : incl_l <= f}. Words w0 and w0 + 1 unconditionally
-// (a word past w1 ends after f: it adds 0), the rest (more than two words
-// ending inside the slot group) in a loop.
-__device__ __forceinline__ int slot_word(int incl, int F, int f) {
-    const int w0 = __builtin_amdgcn_readfirstlane(__popcll(__ballot(incl <= F)));
-    const int w1 = __builtin_amdgcn_readfirstlane(__popcll(__ballot(incl <= F + 63)));
-    const int l1 = w0 < 63 ? w0 + 1 : 63;
-    int lo = w0 + (__builtin_amdgcn_readlane(incl, w0 < 63 ? w0 : 63) <= f) +
-             (__builtin_amdgcn_readlane(incl, l1) <= f);
-    for (int l = w0 + 2; l < w1; l++) lo += __builtin_amdgcn_readlane(incl, l) <= f;
-    return lo < 63 ? lo : 63;
+// the word (compacted record index) of slot gb + lane: words ending before
+// the group + last slots of the group below this lane
+__device__ __forceinline__ int slot_rec(int last, int gb, unsigned long long m) {
+    const int before = __popcll(__ballot(last < gb));
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, (uint32_t)before));
 }
 
-// Diagonal tiles: slot q of a word is its pair (y, x), y < x, q = x(x-1)/2 + y.
-// zc: the sentinel record relative to the side's base.
-template <int SUN>
-__device__ __forceinline__ void sparse_walk_diag(const int4* __restrict__ rec, int incl, int total, int lane,
-                                                 const SparseWalk& e, uint32_t zc, uint32_t* __restrict__ cnt,
-                                                 bool mirror, int fb0, int fb1) {
-    const char* be = reinterpret_cast<const char*>(e.eA);
-    for (int fb = fb0; fb < fb1; fb += 64 * SUN) {
-        int4 r[SUN];
-        int f[SUN];
+// Diagonal tiles: slot q of a word is its pair (y, x), y < x, q = x(x-1)/2 +
+// y; rec = {-first slot, row start (entries), -, -}
+template <int SU>
+__device__ __forceinline__ void sparse_diag_slots(const int4* __restrict__ rec,
+                                                  const unsigned long long* __restrict__ masks, int W0, int last,
+                                                  int fb, int lane, const SparseWalk& e, uint32_t* __restrict__ cnt,
+                                                  bool mirror) {
+    int4 r[SU];
+    unsigned long long m[SU];
+    const unsigned long long* mk = masks + ((fb - W0) >> 6);
 #pragma unroll
-        for (int u = 0; u < SUN; u++) {
-            f[u] = fb + 64 * u + lane;
-            r[u] = rec[slot_word(incl, fb + 64 * u, f[u])];
-        }
-        uint32_t ri[SUN], ci[SUN];
+    for (int u = 0; u < SU; u++) m[u] = mk[u];
 #pragma unroll
-        for (int u = 0; u < SUN; u++) {
-            const bool ok = f[u] < total;
-            const int q = f[u] - (r[u].x & 0xFFFFFF);
-            int x = (int)((1.0f + __builtin_amdgcn_sqrtf(1.0f + 8.0f * (float)q)) * 0.5f);
-            const int t = (int)(__umul24(x, x - 1) >> 1);
-            // x -= 1 when t > q, x += 1 when (x + 1) x / 2 <= q: arithmetic, not branches
-            const int dn = (int)(t > q), up = (int)(t + x <= q);
-            const int xc = x + up - dn;
-            const int tc = t + __mul24(up, x) - __mul24(dn, x - 1);
-            ri[u] = ok ? (uint32_t)(r[u].y + (q - tc)) : 0u;
-            ci[u] = ok ? (uint32_t)(r[u].y + xc) : zc;
-        }
-        ulonglong2 a[SUN], b[SUN];
+    for (int u = 0; u < SU; u++) r[u] = rec[slot_rec(last, fb + 64 * u, m[u])];
+    uint32_t ri[SU], ci[SU];
 #pragma unroll
-        for (int u = 0; u < SUN; u++) {
-            a[u] = *reinterpret_cast<const ulonglong2*>(be + (ri[u] << 4));
-            b[u] = *reinterpret_cast<const ulonglong2*>(be + (ci[u] << 4));
-        }
+    for (int u = 0; u < SU; u++) {
+        const int q = fb + 64 * u + lane + r[u].x;
+        int x = (int)((1.0f + __builtin_amdgcn_sqrtf(1.0f + 8.0f * (float)q)) * 0.5f);
+        const int t = (int)(__umul24(x, x - 1) >> 1);
+        // x -= 1 when t > q, x += 1 when (x + 1) x / 2 <= q: arithmetic, not branches
+        const int dn = (int)(t > q), up = (int)(t + x <= q);
+        const int xc = x + up - dn;
+        const int tc = t + __mul24(up, x) - __mul24(dn, x - 1);
+        ri[u] = (uint32_t)(r[u].y + (q - tc)) << 4;
+        ci[u] = (uint32_t)(r[u].y + xc) << 4;
+    }
+    ulonglong2 a[SU], b[SU];
 #pragma unroll
-        for (int u = 0; u < SUN; u++) {
-            const uint32_t v = (uint32_t)__popcll(rec_word(a[u]) & rec_word(b[u]));
-            cnt_add(cnt, rec_row(a[u]), rec_col(b[u]), v);
-            if (mirror) cnt_add(cnt, rec_row(b[u]), rec_col(a[u]), v);
-        }
+    for (int u = 0; u < SU; u++) {
+        a[u] = *reinterpret_cast<const ulonglong2*>(e.eA + ri[u]);
+        b[u] = *reinterpret_cast<const ulonglong2*>(e.eA + ci[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < SU; u++) {
+        const uint32_t v = (uint32_t)__popcll(rec_word(a[u]) & rec_word(b[u]));
+        cnt_add(cnt, rec_row(a[u]), rec_col(b[u]), v);
+        if (mirror) cnt_add(cnt, rec_row(b[u]), rec_col(a[u]), v);
     }
 }
 
 // Off-diagonal tiles: 1 x 2 micro-tiles, ncp = ceil(ncol / 2) slots per row
-// entry. rec.w = 1 / (2 ncp): (2q + 1) / (2 ncp) = q / ncp + (q mod ncp +
-// 1/2) / ncp stays >= 1/(2 ncp) >= 1/128 from an integer, while the float
-// error is <= (q + 1/2) / ncp * 2^-22 < 0.002 (q < 128 x 64), so the
-// truncation is the exact quotient (checked exhaustively with +-2-ulp
-// reciprocals).
-template <int SUN>
-__device__ __forceinline__ void sparse_walk_off(const int4* __restrict__ rec, int incl, int total, int lane,
-                                                const SparseWalk& e, uint32_t zc, uint32_t* __restrict__ cnt,
-                                                int fb0, int fb1) {
-    const char* beA = reinterpret_cast<const char*>(e.eA);
-    const char* beB = reinterpret_cast<const char*>(e.eB);
-    for (int fb = fb0; fb < fb1; fb += 64 * SUN) {
-        int4 r[SUN];
-        int f[SUN];
+// entry; rec = {-2 first slot, row start (bytes), column start (bytes),
+// 1 / (2 ncp) with 2 ncp in its low byte}
+template <int SU>
+__device__ __forceinline__ void sparse_off_slots(const int4* __restrict__ rec,
+                                                 const unsigned long long* __restrict__ masks, int W0, int last,
+                                                 int fb, int lane, const SparseWalk& e, uint32_t* __restrict__ cnt) {
+    int4 r[SU];
+    unsigned long long m[SU];
+    const unsigned long long* mk = masks + ((fb - W0) >> 6);
 #pragma unroll
-        for (int u = 0; u < SUN; u++) {
-            f[u] = fb + 64 * u + lane;
-            r[u] = rec[slot_word(incl, fb + 64 * u, f[u])];
-        }
-        uint32_t ri[SUN], ci[SUN];
-        int ncol[SUN];                                 // valid columns from the slot's first
+    for (int u = 0; u < SU; u++) m[u] = mk[u];
 #pragma unroll
-        for (int u = 0; u < SUN; u++) {
-            const bool ok = f[u] < total;
-            const int q = f[u] - (r[u].x & 0xFFFFFF);
-            const int ncl = (int)((uint32_t)r[u].x >> 24);
-            const int ncp = (ncl + 1) >> 1;
-            const int xc = (int)((float)(2 * q + 1) * __int_as_float(r[u].w));
-            const int yc = (q - (int)__umul24(xc, ncp)) * 2;
-            ncol[u] = ncl - yc;
-            ri[u] = ok ? (uint32_t)(r[u].y + xc) : 0u;
-            ci[u] = ok ? (uint32_t)(r[u].z + yc) : zc;
-        }
-        Rec3 a[SUN], b0[SUN], b1[SUN];                 // row {row code, word}, columns {word, column code}
+    for (int u = 0; u < SU; u++) r[u] = rec[slot_rec(last, fb + 64 * u, m[u])];
+    uint32_t ri[SU], ci[SU];
 #pragma unroll
-        for (int u = 0; u < SUN; u++) {
-            const char* pb = beB + (ci[u] << 4) + 4;
-            a[u] = *reinterpret_cast<const Rec3*>(beA + (ri[u] << 4));
-            b0[u] = *reinterpret_cast<const Rec3*>(pb);
-            b1[u] = *reinterpret_cast<const Rec3*>(pb + 16);
-        }
+    for (int u = 0; u < SU; u++) {
+        const int q2 = 2 * (fb + 64 * u) + 2 * lane + r[u].x;
+        const float rcp = __int_as_float(r[u].w);
+        const int xc = (int)__builtin_fmaf((float)q2, rcp, rcp);
+        const int yc2 = q2 - (int)__umul24((uint32_t)xc, (uint32_t)r[u].w & 0xFFu);
+        ri[u] = (uint32_t)r[u].y + ((uint32_t)xc << 4);
+        ci[u] = (uint32_t)r[u].z + ((uint32_t)yc2 << 4);
+    }
+    Rec3 a[SU], b0[SU], b1[SU];                   // row {row code, word}, columns {word, column code}
 #pragma unroll
-        for (int u = 0; u < SUN; u++) {
-            const uint32_t rc = a[u].a;
-            // the second column's word is masked, not branched on: a branch
-            // let the compiler sink that load behind it and wait on memory
-            // inside the loop (round 3 ISA)
-            const uint32_t m1 = ncol[u] > 1 ? ~0u : 0u;
-            const uint32_t v0 = (uint32_t)(__popc(a[u].b & b0[u].a) + __popc(a[u].c & b0[u].b));
-            const uint32_t v1 = (uint32_t)(__popc(a[u].b & b1[u].a & m1) + __popc(a[u].c & b1[u].b & m1));
-            cnt_add(cnt, rc, b0[u].c, v0);
-            cnt_add(cnt, rc, b1[u].c, v1);
-        }
+    for (int u = 0; u < SU; u++) {
+        const char* pb = e.eB + ci[u] + 4;
+        a[u] = *reinterpret_cast<const Rec3*>(e.eA + ri[u]);
+        b0[u] = *reinterpret_cast<const Rec3*>(pb);
+        b1[u] = *reinterpret_cast<const Rec3*>(pb + 16);
+    }
+#pragma unroll
+    for (int u = 0; u < SU; u++) {
+        const uint32_t rc = a[u].a;
+        const uint32_t v0 = (uint32_t)(__popc(a[u].b & b0[u].a) + __popc(a[u].c & b0[u].b));
+        uint32_t v1 = (uint32_t)(__popc(a[u].b & b1[u].a) + __popc(a[u].c & b1[u].b));
+        v1 &= ~(uint32_t)__builtin_amdgcn_sbfe((int)b0[u].c, 5, 1);      // kLastOfList: bit 5
+        cnt_add(cnt, rc, b0[u].c, v0);
+        cnt_add(cnt, rc, b1[u].c, v1);
     }
 }
 
-// SUN slots per lane while whole groups of 64 SUN slots remain, then one
-// 64-slot group at a time: a batch's last iteration no longer walks up to
-// 64 (SUN - 1) idle slots (~7 % of C2's slots at SUN = 3)
+// A batch's walk: windows of G groups of 64 slots (G a multiple of SUN):
+// the window's last-slot masks, then SUN groups per step while whole steps
+// remain, one group at a time after
 template <int SUN, bool DIAG>
-__device__ __forceinline__ void sparse_walk(const int4* __restrict__ rec, int incl, int total, int lane,
-                                            const SparseWalk& e, uint32_t zc, uint32_t* __restrict__ cnt,
-                                            bool mirror) {
-    const int full = total / (64 * SUN) * (64 * SUN);
-    if (DIAG) {
-        sparse_walk_diag<SUN>(rec, incl, total, lane, e, zc, cnt, mirror, 0, full);
-        if (SUN > 1) sparse_walk_diag<1>(rec, incl, total, lane, e, zc, cnt, mirror, full, total);
-    } else {
-        sparse_walk_off<SUN>(rec, incl, total, lane, e, zc, cnt, 0, full);
-        if (SUN > 1) sparse_walk_off<1>(rec, incl, total, lane, e, zc, cnt, full, total);
+__device__ __forceinline__ void sparse_walk(const int4* __restrict__ rec, unsigned long long* __restrict__ masks,
+                                            int last, int total, int lane, const SparseWalk& e,
+                                            uint32_t* __restrict__ cnt, bool mirror) {
+    constexpr int G = kWinGroups / SUN * SUN;
+    for (int W0 = 0; W0 < total; W0 += 64 * G) {
+        if (lane < G) masks[lane] = 0ull;
+        __builtin_amdgcn_wave_barrier();
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        const uint32_t rel = (uint32_t)(last - W0);
+        if (rel < 64u * G) atomicOr(&masks[rel >> 6], 1ull << (rel & 63));
+        __builtin_amdgcn_wave_barrier();
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        const int wend = total < W0 + 64 * G ? total : W0 + 64 * G;
+        int fb = W0;
+        for (; fb + 64 * SUN <= wend; fb += 64 * SUN) {
+            if (DIAG) sparse_diag_slots<SUN>(rec, masks, W0, last, fb, lane, e, cnt, mirror);
+            else sparse_off_slots<SUN>(rec, masks, W0, last, fb, lane, e, cnt);
+        }
+        for (; fb < wend; fb += 64) {
+            if (DIAG) sparse_diag_slots<1>(rec, masks, W0, last, fb, lane, e, cnt, mirror);
+            else sparse_off_slots<1>(rec, masks, W0, last, fb, lane, e, cnt);
+        }
+        __builtin_amdgcn_wave_barrier();
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
     }
 }
 
@@ -740,22 +757,26 @@ __global__ __launch_bounds__(SNT, 8) void sparse_tile_kernel(
     const int64_t sb = cbnd[ch], se = cbnd[ch + 1];          // the chunk's sparse words
     const int64_t* offA = off + A * Ws;
     const int64_t* offB = off + B * Ws;
-    const int64_t ra0 = offA[sb], cb0 = offB[sb];           // chunk bases (< 2^31 entries per chunk)
-    const SparseWalk e{ent + ra0, ent + cb0};
-    const int64_t ntot = off[(int64_t)ceil_div(N, SB) * Ws];         // entries of every block: the sentinel
+    const int64_t ra0 = offA[sb], cb0 = offB[sb];           // chunk bases (entries < 2^28 in all: byte offsets)
+    const int64_t ntot = off[(int64_t)ceil_div(N, SB) * Ws];         // entries of every block: the sentinel run
     const uint32_t zA = (uint32_t)(ntot - ra0), zB = (uint32_t)(ntot - cb0);
-    // batches of 64 consecutive words per wave
-    for (int64_t k0 = 0; sb + k0 * SNW + (int64_t)wv * 64 < se; k0 += 64) {
-        const int64_t s = sb + k0 * SNW + (int64_t)wv * 64 + lane;
+    const SparseWalk e{reinterpret_cast<const char*>(ent + ra0), reinterpret_cast<const char*>(ent + cb0)};
+    int4* wrec = &rec[wv][0];
+    unsigned long long* masks = reinterpret_cast<unsigned long long*>(&rec[wv][kBatchWords + 1]);
+    // the wave's share of the chunk's words, in batches of kBatchWords
+    const int64_t per = ceil_div(se - sb, (int64_t)SNW);
+    const int64_t wb = sb + (int64_t)wv * per, we = wb + per < se ? wb + per : se;
+    for (int64_t s0 = wb; s0 < we; s0 += kBatchWords) {
+        const int64_t s = s0 + lane;
         int64_t rb = ra0, cb = cb0;
         int nr = 0, ncl = 0;
-        if (s < se) {
+        if (lane < kBatchWords && s < we) {
             rb = offA[s]; nr = (int)(offA[s + 1] - rb);
             cb = offB[s]; ncl = (int)(offB[s + 1] - cb);
             if (rpart) {                               // lists are sorted by set: trim both ends
                 int a = 0, en = nr;
                 for (int t = 0; t < nr; t++) {
-                    const int st = (int)(rec_row(ent[rb + t]) >> 8);   // row code: set << 8 | rotation key
+                    const int st = (int)((uint32_t)ent[rb + t].x >> 8);   // row code: set << 8 | rotation key
                     a += st < rlo;
                     en -= st >= rhi;
                 }
@@ -771,14 +792,30 @@ __global__ __launch_bounds__(SNT, 8) void sparse_tile_kernel(
             const int v = __shfl_up(incl, o, 64);
             if (lane >= o) incl += v;
         }
-        // first slot < 2^24 (64 words x 128 x 128 products), ncol <= 128
-        const int rcp = __float_as_int(ncd ? __builtin_amdgcn_rcpf(2.0f * (float)ncd) : 0.0f);
-        rec[wv][lane] = make_int4((incl - P) | (ncl << 24), (int32_t)(rb - ra0), (int32_t)(cb - cb0), rcp);
         const int total = __builtin_amdgcn_readlane(incl, 63);      // uniform: the walk's loop stays scalar
+        // the records of the words with slots, compacted in slot order, and the
+        // virtual word after them (its records: the zero sentinel run)
+        const unsigned long long nz = __ballot(P > 0);
+        const int k = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(nz >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)nz, 0u));
+        if (P > 0) {
+            if (diag) {
+                wrec[k] = make_int4(-(incl - P), (int32_t)(rb - ra0), 0, 0);
+            } else {
+                const uint32_t rcp = (uint32_t)__float_as_int(__builtin_amdgcn_rcpf(2.0f * (float)ncd));
+                wrec[k] = make_int4(-2 * (incl - P), (int32_t)((rb - ra0) << 4), (int32_t)((cb - cb0) << 4),
+                                    (int32_t)((rcp & 0xFFFFFF00u) | (uint32_t)(2 * ncd)));
+            }
+        }
+        if (lane == 0) {
+            const int nw = __popcll(nz);
+            wrec[nw] = diag ? make_int4(-total, (int32_t)zA, 0, 0)
+                            : make_int4(-2 * total, (int32_t)(zA << 4), (int32_t)(zB << 4), 0);
+        }
+        const int last = P > 0 ? incl - 1 : 0x7FFFFFFF;
         __builtin_amdgcn_wave_barrier();
-        if (diag) sparse_walk<SUN, true>(rec[wv], incl, total, lane, e, zA, cnt, mirror);
-        else sparse_walk<SUN, false>(rec[wv], incl, total, lane, e, zB, cnt, false);
-        __builtin_amdgcn_wave_barrier();
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        if (diag) sparse_walk<SUN, true>(wrec, masks, last, total, lane, e, cnt, mirror);
+        else sparse_walk<SUN, false>(wrec, masks, last, total, lane, e, cnt, false);
     }
     if (ch < slabs) {
         // dense words [8 ch, 8 ch + 8) of the tile's 128 x 128 pairs: the
@@ -1212,7 +1249,15 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
     exclusive_scan_i32_to_i64(ctx, cnt.as<int32_t>(), s->sp_off.as<int64_t>(), (size_t)(nblk * Ws + 1));
     int64_t total = 0;
     d2h(&total, s->sp_off.as<int64_t>() + nblk * Ws, 8, st);
-    GD_REQUIRE(total < (int64_t(1) << 32), "sparse entries exceed 32-bit offsets");
+    // the tile kernel addresses a chunk's records by 32-bit byte offsets from
+    // its base, the sentinel run after the last entry included
+    if (total + kSentinelRecs >= (int64_t(1) << 28)) {
+        if (ctx->trace())
+            fprintf(stderr, "gdist: %lld sparse entries exceed the tile kernel's 2^28: no sparse split\n",
+                    (long long)total);
+        free_sparse(s);
+        return;
+    }
     // the entries' words and set bytes, turned into the kernel's records below
     DevBuf sp_word(total * 8 + 8, st), sp_set(total + 8, st);
     s->sp_nc.alloc(N * 4, st);
@@ -1232,12 +1277,16 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
         d2h(s->sp_bucket_bits.data(), dbb.p, (size_t)N * nbk * 4, st);
     }
     GD_HIP(hipGetLastError());
-    s->sp_ent.alloc(total * 16 + 64, st);
-    GD_HIP(hipMemsetAsync(s->sp_ent.as<ulonglong2>() + total, 0, 64, st));      // the sentinel records
-    if (total)
+    s->sp_ent.alloc((total + kSentinelRecs) * 16, st);
+    GD_HIP(hipMemsetAsync(s->sp_ent.as<ulonglong2>() + total, 0, kSentinelRecs * 16, st));   // the sentinel run
+    if (total) {
         sparse_records_kernel<<<grid_for(total), 256, 0, st>>>(sp_word.as<unsigned long long>(),
                                                                 sp_set.as<uint8_t>(), total,
                                                                 s->sp_ent.as<ulonglong2>());
+        GD_HIP(hipGetLastError());
+        sparse_last_kernel<<<grid_for(nblk * Ws), 256, 0, st>>>(s->sp_off.as<int64_t>(), nblk * Ws,
+                                                                s->sp_ent.as<ulonglong2>());
+    }
     GD_HIP(hipGetLastError());
     if (grouped) {
         // the group part of every pair: T from the pattern rows, V came with
