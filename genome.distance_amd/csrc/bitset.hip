@@ -1388,12 +1388,26 @@ void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_
                unsigned long long* rare_out, int64_t rare_cap, int64_t* rare_written, const uint32_t* perm,
                const FillHook& hook) {
     hipStream_t st = ctx->stream;
+    // Sets sparse against the dictionary (C3: 33 K codes a set against tens of
+    // millions) give the windowed fill's segments windows past its LDS caps
+    // even at 64 codes (dictionary entries per code of a set >= 12 dense or
+    // >= 32 rare): every segment would walk global memory. The hash fill
+    // probes a table of the dictionary instead. Option fill_sort: 0 or 3 the
+    // windows, 1 the sort, 2 the atomics, 4 the hash.
+    const int64_t total = s->h_off[s->nsets];
+    const double per_set = (double)total / (double)std::max<int64_t>(1, s->nsets);
+    const bool sparse_sets = (double)U > 12.0 * per_set || (double)Ur > 32.0 * per_set;
+    const int64_t opt = ctx->option(OPT_FILL_SORT, -1);
+    if (U + Ur > 0 && (opt == 4 || (opt < 0 && sparse_sets))) {
+        hash_fill(ctx, s, dict, U, perm, rare, Ur, W, bits, id_base, rare_out, rare_cap, rare_written, hook);
+        return;
+    }
     const int cbits = std::min(64, code_bits(s->kind, s->k, s->flags));
     Trace tr(st, ctx->trace());
     GD_HIP(hipMemsetAsync(bits, 0, (size_t)s->nsets * W * 8, st));
     DevBuf rcnt(8, st);
     GD_HIP(hipMemsetAsync(rcnt.p, 0, 8, st));
-    const int64_t mode = hook ? 0 : ctx->option(OPT_FILL_SORT, 0);   // the hook needs the position arrays
+    const int64_t mode = hook || opt == 3 || opt < 0 ? 0 : opt;      // the hook needs the position arrays
     if (U + Ur > 0 && mode == 0) {
         GD_REQUIRE(s->nsets < (int64_t(1) << 23) && s->h_off[s->nsets] < (int64_t(1) << 40),
                    "collection too large for packed fill segments");

@@ -206,7 +206,7 @@ struct Timing {
     X(SPARSE_RARE, "sparse_rare")             /* 0: the rare pairs by the rare kernel, not the chunk reduce */ \
     X(SPARSE_FUSED, "sparse_fused")           /* 0: zeroing, rare kernel and epilogue as their own launches */ \
     X(SPARSE_FOLD, "sparse_fold")             /* most (padded) dense words counted in the sparse tile kernel */\
-    X(FILL_SORT, "fill_sort")                 /* bitset fill: 0 positions + LDS slices, 1 sort, 2 atomics */   \
+    X(FILL_SORT, "fill_sort")                 /* bitset fill: 0/3 windows, 1 sort, 2 atomics, 4 hash (default: by size) */\
     X(PACK_SORT, "pack_sort")                 /* 1: two (code, set) pair sorts instead of packed keys */       \
     X(PACK_SUMMARY, "pack_summary")           /* 0: set|code pack keys, the bitset build re-sorts codes */     \
     X(PACK_OVERLAP, "pack_overlap")           /* 0: upload first / 1: overlapped host thread / 2: registered */\
@@ -444,6 +444,9 @@ using FillHook = std::function<void(const uint32_t* pos, int64_t s0, int64_t s1,
 // positions past the W words and ~0 are skipped): LDS row slices, no atomics
 void bits_from_positions(gdist_ctx* ctx, const gdist_sets* s, const uint32_t* pos, int64_t s0, int64_t s1,
                          int64_t base, int64_t W, unsigned long long* bits);
+void hash_fill(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_t U, const uint32_t* perm,
+               const uint64_t* rare, int64_t Ur, int64_t W, unsigned long long* bits, int64_t id_base,
+               unsigned long long* rare_out, int64_t rare_cap, int64_t* rare_written, const FillHook& hook);
 void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_t U, int64_t W,
                unsigned long long* bits, const uint64_t* rare, int64_t Ur, int64_t id_base,
                unsigned long long* rare_out, int64_t rare_cap, int64_t* rare_written,

@@ -311,7 +311,7 @@ __global__ __launch_bounds__(256) void hash_probe_kernel(const uint64_t* __restr
                                                          const int64_t* __restrict__ off, int64_t s0, int64_t base,
                                                          const unsigned long long* __restrict__ tab,
                                                          unsigned long long mask, uint32_t* __restrict__ pos,
-                                                         unsigned long long* __restrict__ rare_out,
+                                                         int64_t id_base, unsigned long long* __restrict__ rare_out,
                                                          unsigned long long* __restrict__ rare_cnt, int64_t rare_cap) {
     const int64_t set = s0 + blockIdx.x;
     const int lane = threadIdx.x & 63;
@@ -339,7 +339,7 @@ __global__ __launch_bounds__(256) void hash_probe_kernel(const uint64_t* __restr
             if (rhit) {
                 const unsigned long long slotr = b0 + __popcll(m & ((1ull << lane) - 1));
                 if ((int64_t)slotr < rare_cap)
-                    rare_out[slotr] = ((val & 0xFFFFFFFFull) << 32) | (unsigned long long)(uint32_t)set;
+                    rare_out[slotr] = ((val & 0xFFFFFFFFull) << 32) | (unsigned long long)(uint32_t)(set + id_base);
             }
         }
     }
@@ -734,11 +734,13 @@ static CodeGeom code_geom(const gdist_sets* s) {
     return g;
 }
 
-// The fill of a variant build: dense bits, rare records and (through the
-// hook) the variant records of every chunk of sets, by hash probes (above)
-static void hash_fill(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_t U, const uint32_t* perm,
-                      const uint64_t* rare, int64_t Ur, int64_t W, unsigned long long* bits,
-                      unsigned long long* rare_out, int64_t rare_cap, int64_t* rare_written, const FillHook& hook) {
+// The fill by hash probes (above): dense bits, rare records (rank << 32 |
+// set + id_base) and, through the hook, the variant records of every chunk of
+// sets. The variant build's fill, and the two-tier build's when the sets are
+// sparse against the dictionary (bitset.hip fill_bits: C3)
+void hash_fill(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_t U, const uint32_t* perm,
+               const uint64_t* rare, int64_t Ur, int64_t W, unsigned long long* bits, int64_t id_base,
+               unsigned long long* rare_out, int64_t rare_cap, int64_t* rare_written, const FillHook& hook) {
     hipStream_t st = ctx->stream;
     Trace tr(st, ctx->trace());
     GD_REQUIRE(Ur < (int64_t(1) << 32) && U < (int64_t(1) << 32), "dictionary too large for the hash fill");
@@ -763,7 +765,7 @@ static void hash_fill(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict,
         DevBuf pos(std::max<int64_t>(1, n) * 4 + 16, st);
         hash_probe_kernel<<<(unsigned)(s1 - s0), 256, 0, st>>>(s->codes.as<uint64_t>(), s->off.as<int64_t>(), s0, base,
                                                                tab.as<unsigned long long>(), mask, pos.as<uint32_t>(),
-                                                               rare_out, rcnt.as<unsigned long long>(), rare_cap);
+                                                               id_base, rare_out, rcnt.as<unsigned long long>(), rare_cap);
         GD_HIP(hipGetLastError());
         if (hook) hook(pos.as<uint32_t>(), s0, s1, base);
         bits_from_positions(ctx, s, pos.as<uint32_t>(), s0, s1, base, W, bits);
@@ -773,6 +775,7 @@ static void hash_fill(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict,
     }
     unsigned long long w = 0;
     d2h(&w, rcnt.p, 8, st);
+    GD_REQUIRE((int64_t)w <= rare_cap, "rare-tier record count exceeds its reservation");
     *rare_written = (int64_t)w;
 }
 
@@ -936,7 +939,7 @@ void build_variant_bitsets(gdist_ctx* ctx, gdist_sets* s, DevBuf& dict, DevBuf& 
                   recs.as<unsigned long long>(), mass, &written, perm.as<uint32_t>(), hook);
     else
         hash_fill(ctx, s, dict.as<uint64_t>(), U, perm.as<uint32_t>(), rare.as<uint64_t>(), Ur, Wd,
-                  s->bits.as<unsigned long long>(), recs.as<unsigned long long>(), mass, &written, hook);
+                  s->bits.as<unsigned long long>(), 0, recs.as<unsigned long long>(), mass, &written, hook);
     GD_REQUIRE(written == mass, "rare-tier record count mismatch");
     tr.mark("variant: fill (dense bits, rare and variant records)");
     build_postings(ctx, s, recs.as<unsigned long long>(), written, Ur);

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 O=gpurun_out/r04s11
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread \
-    -p no:cacheprovider -k "sparse or graph_replay or rare_tier" > $O/sparse.log 2>&1
+    -p no:cacheprovider -k "sparse or graph_replay or rare_tier or fill_routes" > $O/sparse.log 2>&1
 rc=$?; tail -4 $O/sparse.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline > $O/bench_c2.json 2> $O/bench_c2.err &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_c2 -o run -- python3 bench.py --steps 20 --warmup 3 \

@@ -750,6 +750,7 @@ SPARSE_MODES = {
     # windowed searches with global atomics, instead of merged positions + LDS slices
     "fill_sort": {"fill_sort": 1},
     "fill_direct": {"fill_sort": 2},
+    "fill_hash": {"fill_sort": 4},
     # the pack's two (code, set) pair sorts instead of one sort of set|code keys
     "pack_pairs": {"pack_sort": 1},
     # the pack without chunk summaries: the bitset build sorts every code for its dictionary
@@ -835,6 +836,36 @@ def test_sparse_equals_dense_at_size(ctx, opts):
     off, codes = oracle_pack(seqs, 21, 0, 0)
     oI, oD = oracle.matrix(off, codes, 0, n, 0, n, flags=0x100, nthreads=8)
     assert np.array_equal(I[iu], oI[iu]) and bits_equal(D[iu], oD[iu])
+
+
+@pytest.mark.parametrize("fill", [None, 0, 4, 1])
+def test_fill_routes_on_sparse_sets(ctx, opts, fill):
+    """C3-shaped proteomes (sets much smaller than the dictionary, T > N so
+    the rare tier holds every shared kmer): the bitset fill by hash probes (the
+    default for such sets: fill_sort absent, or 4), by LDS windows (0: its
+    global-walk fallback) and by the sort (1) give the same bit-exact counts
+    and distances as the oracle."""
+    import gdist
+    opts(fill_sort=fill)
+    n = 300
+    seqs = synth_sets(n, 1500, 0.10, 109, protein=True)
+    sets = gdist.KmerSets.from_sequences(seqs, 8, gdist.KmerType.PROT, 0, ctx)
+    sets.build_bitsets(rare_threshold=1000)
+    assert sets.rare_info()[1] > 0
+    off, codes = oracle_pack(seqs, 8, 1, 0)
+    for (r0, r1, c0, c1, up) in [(0, n, 0, n, True), (41, 250, 7, 290, False)]:
+        I, D = sets.matrix((r0, r1), (c0, c1), upper=up, method=gdist.METHOD_BITSET)
+        eI, eD = oracle.matrix(off, codes, r0, r1, c0, c1, flags=0x100 if up else 0)
+        if up:
+            mask = np.fromfunction(lambda a, b: (c0 + b) > (r0 + a), (r1 - r0, c1 - c0))
+            I, D, eI, eD = I[mask], D[mask], eI[mask], eD[mask]
+        assert np.array_equal(I, eI), (fill, r0, r1, c0, c1, up)
+        assert bits_equal(D, eD)
+    sets.build_bitsets(rare_threshold=3)          # dense tier + rare lists
+    I, D = sets.matrix(upper=True, method=gdist.METHOD_BITSET)
+    eI, eD = oracle.matrix(off, codes, 0, n, 0, n, flags=0x100)
+    iu = np.triu_indices(n, 1)
+    assert np.array_equal(I[iu], eI[iu]) and bits_equal(D[iu], eD[iu])
 
 
 def test_auto_method_prepare(ctx):
