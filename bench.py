@@ -328,8 +328,7 @@ def main():
     # Kernel times, after the timed region: replayed steps record no timing
     # events by default (they cost 13-18 us a step), so a short loop with
     # option step_timing = 1 reads the steps' HIP-event spans (on the
-    # library's streams), and for the sparse tier a loop with time_sparse = 1
-    # the sparse tile kernel alone
+    # library's streams); each kernel family alone below (time_kernels = 1)
     kt = max(3, min(args.steps, 20))
     prev_st = ctx.option("step_timing")
     ctx.set_option("step_timing", 1)
