@@ -1255,9 +1255,16 @@ __global__ __launch_bounds__(64) void fill_pos_kernel(
     const int64_t set = (int64_t)(sd >> 40), b = (int64_t)(sd & ((1ull << 40) - 1));
     const int64_t nd = dhi - dlo, nr = rhi - rlo, nf = (nr + kRareBucket - 1) / kRareBucket;
     if (nd <= kWinDense && nf <= kRareFences) {
-        uint64_t kk[kPosSeg / 64];
+        // lane l takes the segment's codes [8 l, 8 l + 8): one binary search
+        // for the first, then (codes ascending) a short forward walk per code
+        // from the previous code's rank — about 2 dependent LDS reads a code
+        // instead of a 10-step search each (C2: the segment's codes and its
+        // dense window are about equally dense)
+        constexpr int PL = kPosSeg / 64;
+        const int64_t i0 = b + (int64_t)PL * lane;
+        uint64_t kk[PL];
 #pragma unroll
-        for (int j = 0; j < kPosSeg / 64; j++) kk[j] = b + 64 * j + lane < e ? codes[b + 64 * j + lane] : 0;
+        for (int j = 0; j < PL; j++) kk[j] = i0 + j < e ? codes[i0 + j] : 0;
         for (int j = lane; j < nd; j += 64) {
             s_d[j] = dict[dlo + j];
             s_p[j] = perm ? perm[dlo + j] : (uint32_t)(dlo + j);
@@ -1265,15 +1272,19 @@ __global__ __launch_bounds__(64) void fill_pos_kernel(
         for (int j = lane; j < nf; j += 64) s_f[j] = rare[rlo + (int64_t)j * kRareBucket];
         __syncthreads();
         int nm = 0;   // misses listed (uniform)
+        int r = i0 < e ? lds_lower_bound(s_d, (int)nd, kk[0]) : (int)nd;
 #pragma unroll
-        for (int j = 0; j < kPosSeg / 64; j++) {
-            if (b + 64 * j >= e) break;
-            const int64_t i = b + 64 * j + lane;
+        for (int j = 0; j < PL; j++) {
+            const int64_t i = i0 + j;
             const bool valid = i < e;
             bool miss = false;
             if (valid) {
                 const uint64_t k = kk[j];
-                const int r = lds_lower_bound(s_d, (int)nd, k);
+                // forward from the previous rank: two steps, then a search of the rest
+                if (r < nd && s_d[r] < k) {
+                    r++;
+                    if (r < nd && s_d[r] < k) r = r + 1 + lds_lower_bound(s_d + r + 1, (int)nd - r - 1, k);
+                }
                 const bool hit = r < nd && s_d[r] == k;
                 pos_out[i - base] = hit ? s_p[r] : ~0u;
                 miss = !hit;
