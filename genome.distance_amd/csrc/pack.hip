@@ -105,11 +105,13 @@ __global__ void validate_kernel(const unsigned char* __restrict__ seqs, int64_t 
 
 // Window w of the chunk -> sequence s (binary search in win_off), position,
 // then the k symbols. Emits 1 or 2 (BOTH) entries per window.
-template <bool RAW8>
+// CM: the code-major sort keys code << idbits | id straight away (the
+// summary path), no id array
+template <bool RAW8, bool CM = false>
 __global__ __launch_bounds__(256) void extract_kernel(
     const unsigned char* __restrict__ seqs, const int64_t* __restrict__ seq_off,
     const int64_t* __restrict__ win_off, int nseq, int64_t nwin, int k, int bits, int strand,
-    AlphabetDev al, uint64_t* __restrict__ keys, int32_t* __restrict__ vals) {
+    AlphabetDev al, uint64_t* __restrict__ keys, int32_t* __restrict__ vals, int idbits = 0) {
     __shared__ int8_t sym[256];
     __shared__ int8_t comp[8];
     for (int t = threadIdx.x; t < 256; t += blockDim.x) sym[t] = al.sym[t];
@@ -140,6 +142,16 @@ __global__ __launch_bounds__(256) void extract_kernel(
         }
         fwd &= mask;
         const int32_t id = valid ? s : nseq;
+        if (CM) {
+            const uint64_t sid = (uint64_t)(uint32_t)id;
+            if (strand == GDIST_STRAND_BOTH) {
+                keys[2 * w] = (fwd << idbits) | sid;
+                keys[2 * w + 1] = (rc << idbits) | sid;
+            } else {
+                keys[w] = ((strand == GDIST_STRAND_CANON ? (fwd < rc ? fwd : rc) : fwd) << idbits) | sid;
+            }
+            continue;
+        }
         if (strand == GDIST_STRAND_BOTH) {
             keys[2 * w] = fwd; vals[2 * w] = id;
             keys[2 * w + 1] = rc; vals[2 * w + 1] = id;
@@ -226,34 +238,88 @@ __global__ void pack_keys_cm_kernel(const uint64_t* __restrict__ codes, const in
         keys[i] = (codes[i] << idbits) | (uint32_t)ids[i];
 }
 
-// flag word: bit 0 = the first key of its (code, set) pair and a valid
-// window; bit 32 = that, and the first of its code (invalid windows carry
-// the largest set field, so they sort after a code's valid keys and never
-// sit between two of them)
-__global__ void cm_flags_kernel(const uint64_t* __restrict__ keys, int64_t n, uint64_t smask, uint64_t invalid,
-                                int idbits, int64_t* __restrict__ flag) {
-    int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const uint64_t k = keys[i];
-        const uint64_t p = i ? keys[i - 1] : ~k;
-        const bool u = (k & smask) != invalid && k != p;
-        const bool h = u && (i == 0 || (k >> idbits) != (p >> idbits));
-        flag[i] = (int64_t)u | ((int64_t)h << 32);
-    }
+// The unique pass in two reads of the sorted keys instead of a flag array,
+// its scan and an emit pass over flags + positions (16 B of flags and 16 B
+// of positions a key): tiles of kSelTile keys; cm_count_kernel sums each
+// tile's flag words, one exclusive scan over the tiles, cm_select_kernel
+// recomputes the flags of its tile (staged in LDS with the key before it),
+// scans them within the block and writes the unique keys and the run heads.
+constexpr int kSelT = 256, kSelPer = 16, kSelTile = kSelT * kSelPer;
+
+__device__ __forceinline__ int64_t cm_flag(uint64_t k, uint64_t p, bool first, uint64_t smask, uint64_t invalid,
+                                           int idbits) {
+    const bool u = (k & smask) != invalid && (first || k != p);
+    const bool h = u && (first || (k >> idbits) != (p >> idbits));
+    return (int64_t)u | ((int64_t)h << 32);
 }
 
-// unique keys to u[], each code's first to the summary (code, start in u[])
-__global__ void cm_emit_kernel(const uint64_t* __restrict__ keys, const int64_t* __restrict__ flag,
-                               const int64_t* __restrict__ pos, int64_t n, int idbits, uint64_t* __restrict__ u,
-                               uint64_t* __restrict__ codes, int64_t* __restrict__ start) {
-    int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const int64_t f = flag[i];
-        if (!(f & 1)) continue;
-        const uint64_t k = keys[i];
-        const int64_t p = pos[i], at = p & 0xFFFFFFFFll;
-        u[at] = k;
-        if (f >> 32) { codes[p >> 32] = k >> idbits; start[p >> 32] = at; }
+// int64 sum over the block (every thread gets it) / exclusive prefix of the thread
+__device__ __forceinline__ int64_t block_excl_scan_i64(int64_t v, int64_t* red, int64_t* total) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int64_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) red[wv] = x;
+    __syncthreads();
+    int64_t before = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < kSelT / 64; w++) {
+        before += w < wv ? red[w] : 0;
+        all += red[w];
+    }
+    __syncthreads();
+    *total = all;
+    return before + x - v;
+}
+
+__global__ __launch_bounds__(kSelT) void cm_count_kernel(const uint64_t* __restrict__ keys, int64_t n, uint64_t smask,
+                                                         uint64_t invalid, int idbits, int64_t* __restrict__ bsum) {
+    __shared__ int64_t red[kSelT / 64];
+    const int64_t t0 = (int64_t)blockIdx.x * kSelTile;
+    int64_t acc = 0;
+#pragma unroll 4
+    for (int j = 0; j < kSelPer; j++) {
+        const int64_t i = t0 + j * kSelT + threadIdx.x;
+        if (i < n) acc += cm_flag(keys[i], i ? keys[i - 1] : 0, i == 0, smask, invalid, idbits);
+    }
+    int64_t total;
+    block_excl_scan_i64(acc, red, &total);
+    if (threadIdx.x == 0) bsum[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kSelT) void cm_select_kernel(const uint64_t* __restrict__ keys, int64_t n, uint64_t smask,
+                                                          uint64_t invalid, int idbits, const int64_t* __restrict__ bpre,
+                                                          uint64_t* __restrict__ u, uint64_t* __restrict__ codes,
+                                                          int64_t* __restrict__ start) {
+    __shared__ uint64_t sk[kSelTile + 1];
+    __shared__ int64_t red[kSelT / 64];
+    const int64_t t0 = (int64_t)blockIdx.x * kSelTile;
+    const int m = (int)(n - t0 < kSelTile ? n - t0 : kSelTile);
+    for (int j = threadIdx.x; j < m; j += kSelT) sk[1 + j] = keys[t0 + j];
+    if (threadIdx.x == 0) sk[0] = t0 ? keys[t0 - 1] : 0;
+    __syncthreads();
+    const int b = threadIdx.x * kSelPer;
+    int64_t f[kSelPer], tot = 0;
+#pragma unroll
+    for (int j = 0; j < kSelPer; j++) {
+        const int x = b + j;
+        f[j] = x < m ? cm_flag(sk[1 + x], sk[x], t0 + x == 0, smask, invalid, idbits) : 0;
+        tot += f[j];
+    }
+    int64_t all;
+    int64_t p = bpre[blockIdx.x] + block_excl_scan_i64(tot, red, &all);
+#pragma unroll
+    for (int j = 0; j < kSelPer; j++) {
+        if (f[j] & 1) {
+            const uint64_t k = sk[1 + b + j];
+            const int64_t at = p & 0xFFFFFFFFll;
+            u[at] = k;
+            if (f[j] >> 32) { codes[p >> 32] = k >> idbits; start[p >> 32] = at; }
+        }
+        p += f[j];
     }
 }
 
@@ -645,8 +711,29 @@ void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_se
         DevBuf cw((nc + 1) * sizeof(int64_t), st);
         h2d(cw.p, hwo.data(), (nc + 1) * sizeof(int64_t), st);
 
-        DevBuf kA(n * 8 + 8, st), kB(n * 8 + 8, st), vA(n * 4 + 4, st), vB(n * 4 + 4, st);
-        if (nw > 0) {
+        int idbits = 1;
+        while ((int64_t(1) << idbits) <= nc) idbits++;
+        const int64_t nguides = std::min<int64_t>(nc, std::max<int64_t>(0, ctx->option(OPT_GUIDES, kGuides)));
+        const bool guides_here = s0 == 0 && nw > 0 && nguides > 0 && locus_order_enabled(ctx);
+        PackDebug* dbg = (s0 == 0) ? g_pack_debug : nullptr;
+        const bool cm_path = want_sum && !dbg && cbits + idbits <= 64 && n < (int64_t(1) << 31) &&
+                             ctx->option(OPT_PACK_SORT, 0) == 0;
+        // the summary path's keys come out of the extraction (the guides need
+        // the plain code and id arrays: the first chunk extracts those)
+        const bool cm_extract = cm_path && !guides_here;
+        DevBuf kA(n * 8 + 8, st), kB(n * 8 + 8, st), vA(cm_extract ? 8 : n * 4 + 4, st),
+            vB(cm_path ? 8 : n * 4 + 4, st);
+        if (nw > 0 && cm_extract) {
+            if (raw8)
+                extract_kernel<true, true><<<grid_for(nw, 256, 256 * 64), 256, 0, st>>>(
+                    src, d_seq_off + s0, cw.as<int64_t>(), nc, nw, k, bits, strand, al, kA.as<uint64_t>(), nullptr,
+                    idbits);
+            else
+                extract_kernel<false, true><<<grid_for(nw, 256, 256 * 64), 256, 0, st>>>(
+                    src, d_seq_off + s0, cw.as<int64_t>(), nc, nw, k, bits, strand, al, kA.as<uint64_t>(), nullptr,
+                    idbits);
+            GD_HIP(hipGetLastError());
+        } else if (nw > 0) {
             if (raw8)
                 extract_kernel<true><<<grid_for(nw, 256, 256 * 64), 256, 0, st>>>(
                     src, d_seq_off + s0, cw.as<int64_t>(), nc, nw, k, bits, strand, al, kA.as<uint64_t>(),
@@ -658,38 +745,36 @@ void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_se
             GD_HIP(hipGetLastError());
         }
         tr.mark("pack: alloc+extract");
-        const int64_t nguides = std::min<int64_t>(nc, std::max<int64_t>(0, ctx->option(OPT_GUIDES, kGuides)));
-        if (s0 == 0 && nw > 0 && nguides > 0 && locus_order_enabled(ctx))
+        if (guides_here)
             guide_from_extract(ctx, kA.as<uint64_t>(), vA.as<int32_t>(), hwo[nguides] * mult, nc, cbits, out);
         uint64_t* keys = kA.as<uint64_t>(); uint64_t* keys_alt = kB.as<uint64_t>();
         int32_t* ids = vA.as<int32_t>(); int32_t* ids_alt = vB.as<int32_t>();
-        PackDebug* dbg = (s0 == 0) ? g_pack_debug : nullptr;
         if (dbg) { dbg->n = n; d2h(dbg->k_extract, keys, n * 8, st); d2h(dbg->v_extract, ids, n * 4, st); }
-        int idbits = 1;
-        while ((int64_t(1) << idbits) <= nc) idbits++;
-        if (want_sum && !dbg && cbits + idbits <= 64 && n < (int64_t(1) << 31) && ctx->option(OPT_PACK_SORT, 0) == 0) {
+        if (cm_path) {
             // code-major keys: the chunk's summary falls out of the same sort
             const uint64_t smask = (uint64_t(1) << idbits) - 1;
-            if (n > 0) {
+            if (n > 0 && !cm_extract) {
                 pack_keys_cm_kernel<<<grid_for(n), 256, 0, st>>>(keys, ids, n, idbits, keys_alt);
                 GD_HIP(hipGetLastError());
+                std::swap(keys, keys_alt);
             }
-            std::swap(keys, keys_alt);
             sort_keys_u64(ctx, keys, keys_alt, (size_t)n, 0, cbits + idbits);
             tr.mark("pack: sort by code|set");
             // one flag word per key: bit 0 = first key of its (code, set)
-            // (valid), bit 32 = first valid key of its code; one scan gives
-            // both the unique positions (low half) and the run index (high)
-            DevBuf flag(n * 8 + 8, st), pos(n * 8 + 8, st);
+            // (valid), bit 32 = first valid key of its code; their prefix sums
+            // are the unique positions (low half) and the run index (high),
+            // per tile of keys (cm_count_kernel), then within the tile
+            const int64_t ntile = ceil_div(n, (int64_t)kSelTile);
+            DevBuf bsum(ntile * 8 + 8, st), bpre(ntile * 8 + 8, st);
             int64_t uniq = 0, nruns = 0;
             if (n > 0) {
-                cm_flags_kernel<<<grid_for(n), 256, 0, st>>>(keys, n, smask, (uint64_t)nc, idbits,
-                                                             flag.as<int64_t>());
+                cm_count_kernel<<<(unsigned)ntile, kSelT, 0, st>>>(keys, n, smask, (uint64_t)nc, idbits,
+                                                                    bsum.as<int64_t>());
                 GD_HIP(hipGetLastError());
-                exclusive_scan_i64(ctx, flag.as<int64_t>(), pos.as<int64_t>(), (size_t)n);
+                exclusive_scan_i64(ctx, bsum.as<int64_t>(), bpre.as<int64_t>(), (size_t)ntile);
                 int64_t last = 0, lf = 0;
-                d2h(&last, pos.as<int64_t>() + n - 1, 8, st);
-                d2h(&lf, flag.as<int64_t>() + n - 1, 8, st);
+                d2h(&last, bpre.as<int64_t>() + ntile - 1, 8, st);
+                d2h(&lf, bsum.as<int64_t>() + ntile - 1, 8, st);
                 GD_HIP(hipStreamSynchronize(st));
                 uniq = (last + lf) & 0xFFFFFFFFll;
                 nruns = (last + lf) >> 32;
@@ -700,8 +785,9 @@ void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_se
             sum.n = nruns;
             if (uniq > 0) {
                 DevBuf start(nruns * 8 + 8, st);
-                cm_emit_kernel<<<grid_for(n), 256, 0, st>>>(keys, flag.as<int64_t>(), pos.as<int64_t>(), n, idbits,
-                                                            keys_alt, sum.codes.as<uint64_t>(), start.as<int64_t>());
+                cm_select_kernel<<<(unsigned)ntile, kSelT, 0, st>>>(keys, n, smask, (uint64_t)nc, idbits,
+                                                                     bpre.as<int64_t>(), keys_alt,
+                                                                     sum.codes.as<uint64_t>(), start.as<int64_t>());
                 GD_HIP(hipGetLastError());
                 std::swap(keys, keys_alt);                      // keys: the unique code|set keys
                 cm_run_counts_kernel<<<grid_for(nruns), 256, 0, st>>>(start.as<int64_t>(), nruns, uniq,
