@@ -217,6 +217,7 @@ struct Timing {
     X(SPARSE_XCD, "sparse_xcd")               /* 1: chunk c of every sparse tile on XCD c mod 8 */           \
     X(RARE_U16, "rare_u16")                   /* 0: 4-byte list members in the row-major rare walk */        \
     X(RARE_FLAT, "rare_flat")                 /* 0: the row-major rare walk a lane per record (A/B) */     \
+    X(SORT_RADIX, "sort_radix")               /* 10: onesweep radix sorts of u64 keys in 10-bit passes (A/B) */\
     X(VARIANT, "variant")                     /* variant tier: 1 force, 0 off (default: by the dictionary) */ \
     X(VARIANT_DMIN, "variant_dmin")           /* sets holding a dense-tier kmer (default N / 10) */            \
     X(RANGE_SUMMARY, "range_summary")         /* 1: the code-range dictionary whatever the size, 0: never */

@@ -456,14 +456,27 @@ static void sort_pairs_i32_u64(gdist_ctx* ctx, int32_t*& keys, int32_t*& keys_al
     vals = vb.current(); vals_alt = vb.alternate();
 }
 
+// option sort_radix 10: onesweep passes of 10 bits (C2's 49-bit pack keys: 5
+// passes instead of 7; A/B)
+using Onesweep10 = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<256, 12>, rocprim::kernel_config<512, 12>, 10,
+                                        rocprim::block_radix_rank_algorithm::match>>;
+
 void sort_keys_u64(gdist_ctx* ctx, uint64_t*& keys, uint64_t*& keys_alt, size_t n, int begin_bit,
                    int end_bit) {
     if (n == 0) return;
     rocprim::double_buffer<uint64_t> kb(keys, keys_alt);
     size_t tmp = 0;
-    GD_HIP(rocprim::radix_sort_keys(nullptr, tmp, kb, n, begin_bit, end_bit, ctx->stream));
-    DevBuf t(tmp, ctx->stream);
-    GD_HIP(rocprim::radix_sort_keys(t.p, tmp, kb, n, begin_bit, end_bit, ctx->stream));
+    if (ctx->option(OPT_SORT_RADIX, 8) == 10 && n > (size_t(1) << 22)) {
+        GD_HIP(rocprim::radix_sort_keys<Onesweep10>(nullptr, tmp, kb, n, begin_bit, end_bit, ctx->stream));
+        DevBuf t(tmp, ctx->stream);
+        GD_HIP(rocprim::radix_sort_keys<Onesweep10>(t.p, tmp, kb, n, begin_bit, end_bit, ctx->stream));
+    } else {
+        GD_HIP(rocprim::radix_sort_keys(nullptr, tmp, kb, n, begin_bit, end_bit, ctx->stream));
+        DevBuf t(tmp, ctx->stream);
+        GD_HIP(rocprim::radix_sort_keys(t.p, tmp, kb, n, begin_bit, end_bit, ctx->stream));
+    }
     keys = kb.current(); keys_alt = kb.alternate();
 }
 

@@ -755,6 +755,8 @@ SPARSE_MODES = {
     "pack_pairs": {"pack_sort": 1},
     # the pack without chunk summaries: the bitset build sorts every code for its dictionary
     "pack_nosummary": {"pack_summary": 0},
+    # the pack's and the dictionary's radix sorts in 10-bit onesweep passes
+    "sort_radix10": {"sort_radix": 10},
     "many_chunks": {"sparse_zmax": 100000, "sparse_chunks": 37},
     # chunk c of every tile on XCD c mod 8 (option sparse_xcd), with a chunk
     # count that leaves empty workgroups in the last group of 8, and atomics
