@@ -484,16 +484,18 @@ def main():
                 rec, incs = sets.rare_info()[2], sets.rare_stats()[0]
                 f_rows = (r1 - r0) / N
                 f_pairs = pairs_rank / max(1, N * (N - 1) // 2)
-                rare_bytes = 14.0 * rec * f_rows + 4.0 * incs * f_pairs + 8.0 * pairs_rank
+                # list members: 2 bytes for collections of <= 65,536 sets (option rare_u16)
+                mbytes = 2.0 if N <= 65536 and ctx.option("rare_u16") != 0 else 4.0
+                rare_bytes = 14.0 * rec * f_rows + mbytes * incs * f_pairs + 8.0 * pairs_rank
                 rk = "rare_rows_kernel" if sets.block_cost((r0, r1))[1] == 1 else "rare_pairs_kernel"
                 ach = rare_bytes / (r_ms * 1e-3) / 1e9
                 rare_roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(rk),
                              "kernel": f"{rk} (rare tier, beside the dense tiles)", "kernel_avg_ms": round(r_ms, 4),
                              "algo_bytes_per_launch": round(rare_bytes),
-                             "note": "algorithmic bytes = 14 B per (set, list) record of the rows + 4 B per member "
-                                     "read (pair increments) + 8 B per pair of I updated; scattered member "
-                                     "reads from short lists: each read brings a whole line"}
+                             "member_bytes": mbytes,
+                             "note": "algorithmic bytes = 14 B per (set, list) record of the rows + one list member "
+                                     "read per pair increment (member_bytes) + 8 B per pair of I updated"}
                 cands.append((r_ms, rare_roof))
             # the line's roofline is the longest kernel family's; the others ride along
             cands.sort(key=lambda c: -c[0])
