@@ -2057,7 +2057,7 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
         GD_REQUIRE(rgrid < (int64_t(1) << 31), "rare-tier grid too large");
         const size_t lds = (size_t)std::min<int64_t>(nc, RCH) * 4;
         FamilyTimer ft(ctx, GDIST_KERNEL_RARE, rs);
-        const bool flat = ctx->option(OPT_RARE_FLAT, 1) != 0;
+        const bool flat = ctx->option(OPT_RARE_FLAT, 0) != 0;   // measured slower on C3 (r04s11/ab3)
         auto go = [&](auto kern, auto* members) {
             kern<<<(unsigned)rgrid, 256, lds, rs>>>(s->srare_off.as<int64_t>(), s->srare_ent.as<uint64_t>(),
                                                     s->srare_w.as<uint32_t>(), s->srare_skip.as<uint16_t>(), members,

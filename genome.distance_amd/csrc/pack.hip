@@ -294,19 +294,29 @@ __global__ __launch_bounds__(kSelT) void cm_select_kernel(const uint64_t* __rest
                                                           uint64_t invalid, int idbits, const int64_t* __restrict__ bpre,
                                                           uint64_t* __restrict__ u, uint64_t* __restrict__ codes,
                                                           int64_t* __restrict__ start) {
-    __shared__ uint64_t sk[kSelTile + 1];
+    // slot i of the tile (i = 0: the key before it) at i + i / 16: a thread's
+    // 16 consecutive keys then sit 17 words from the next thread's (2-way
+    // bank conflicts instead of 32-way)
+    __shared__ uint64_t sk[kSelTile + 1 + (kSelTile + 1) / 16 + 1];
     __shared__ int64_t red[kSelT / 64];
     const int64_t t0 = (int64_t)blockIdx.x * kSelTile;
     const int m = (int)(n - t0 < kSelTile ? n - t0 : kSelTile);
-    for (int j = threadIdx.x; j < m; j += kSelT) sk[1 + j] = keys[t0 + j];
+    for (int j = threadIdx.x; j < m; j += kSelT) sk[(1 + j) + ((1 + j) >> 4)] = keys[t0 + j];
     if (threadIdx.x == 0) sk[0] = t0 ? keys[t0 - 1] : 0;
     __syncthreads();
     const int b = threadIdx.x * kSelPer;
     int64_t f[kSelPer], tot = 0;
+    uint64_t kv[kSelPer + 1];
+    kv[0] = sk[b + (b >> 4)];
+#pragma unroll
+    for (int j = 0; j < kSelPer; j++) {
+        const int i = b + 1 + j;
+        kv[j + 1] = sk[i + (i >> 4)];
+    }
 #pragma unroll
     for (int j = 0; j < kSelPer; j++) {
         const int x = b + j;
-        f[j] = x < m ? cm_flag(sk[1 + x], sk[x], t0 + x == 0, smask, invalid, idbits) : 0;
+        f[j] = x < m ? cm_flag(kv[j + 1], kv[j], t0 + x == 0, smask, invalid, idbits) : 0;
         tot += f[j];
     }
     int64_t all;
@@ -314,7 +324,7 @@ __global__ __launch_bounds__(kSelT) void cm_select_kernel(const uint64_t* __rest
 #pragma unroll
     for (int j = 0; j < kSelPer; j++) {
         if (f[j] & 1) {
-            const uint64_t k = sk[1 + b + j];
+            const uint64_t k = kv[j + 1];
             const int64_t at = p & 0xFFFFFFFFll;
             u[at] = k;
             if (f[j] >> 32) { codes[p >> 32] = k >> idbits; start[p >> 32] = at; }
