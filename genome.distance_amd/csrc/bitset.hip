@@ -1218,26 +1218,49 @@ __device__ __forceinline__ int lds_lower_bound(const uint64_t* a, int n, uint64_
     return lo;
 }
 
-// rare-tier records of the lanes with rhit: one atomic per wave
-__device__ __forceinline__ void append_rare(bool rhit, int64_t q, int64_t set, int64_t id_base,
+// Rare-tier records of a one-wave block, staged in LDS and appended to the
+// output with ONE atomic per kRareBuf records: C2's fill appended ~17 records
+// a segment with one atomic each on a single counter (2 M per launch), and
+// same-address atomics run at ~0.1 G/s — 84 of the fill's 112 ms.
+constexpr int kRareBuf = 256;
+struct WaveRareBuf {
+    unsigned long long* buf;              // LDS [kRareBuf]
+    int n;                                // records staged (wave-uniform)
+};
+__device__ __forceinline__ void rare_flush(WaveRareBuf& rb, unsigned long long* __restrict__ rare_out,
+                                           unsigned long long* __restrict__ rare_cnt, int64_t rare_cap) {
+    if (!rb.n) return;
+    __builtin_amdgcn_wave_barrier();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    const int lane = threadIdx.x & 63;
+    unsigned long long g = 0;
+    if (lane == 0) g = atomicAdd(rare_cnt, (unsigned long long)rb.n);
+    g = (unsigned long long)__shfl((long long)g, 0, 64);
+    for (int j = lane; j < rb.n; j += 64)
+        if ((int64_t)(g + j) < rare_cap) rare_out[g + j] = rb.buf[j];
+    __builtin_amdgcn_wave_barrier();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    rb.n = 0;
+}
+__device__ __forceinline__ void append_rare(bool rhit, int64_t q, int64_t set, int64_t id_base, WaveRareBuf& rb,
                                             unsigned long long* __restrict__ rare_out,
                                             unsigned long long* __restrict__ rare_cnt, int64_t rare_cap) {
     const unsigned long long m = __ballot(rhit);
     if (!m) return;
-    const int lane = threadIdx.x & 63;
-    unsigned long long b0 = 0;
-    if (lane == __ffsll((long long)m) - 1) b0 = atomicAdd(rare_cnt, (unsigned long long)__popcll(m));
-    b0 = (unsigned long long)__shfl((long long)b0, __ffsll((long long)m) - 1, 64);
+    const int c = __popcll(m);
+    if (rb.n + c > kRareBuf) rare_flush(rb, rare_out, rare_cnt, rare_cap);
     if (rhit) {
-        const unsigned long long slot = b0 + __popcll(m & ((1ull << lane) - 1));
-        if ((int64_t)slot < rare_cap)
-            rare_out[slot] = ((unsigned long long)q << 32) | (unsigned long long)(uint32_t)(set + id_base);
+        const int lane = threadIdx.x & 63;
+        rb.buf[rb.n + __popcll(m & ((1ull << lane) - 1))] =
+            ((unsigned long long)q << 32) | (unsigned long long)(uint32_t)(set + id_base);
     }
+    rb.n += c;
 }
 
-// one wave per block and segment
+// one wave per block; the blocks take the segments in turn (their rare
+// records staged across segments, above)
 __global__ __launch_bounds__(64) void fill_pos_kernel(
-    const uint64_t* __restrict__ codes, const int64_t* __restrict__ win, const uint64_t* __restrict__ dict,
+    const uint64_t* __restrict__ codes, const int64_t* __restrict__ win, int64_t ns, const uint64_t* __restrict__ dict,
     const uint64_t* __restrict__ rare, int64_t base, uint32_t* __restrict__ pos_out, int64_t id_base,
     unsigned long long* __restrict__ rare_out, unsigned long long* __restrict__ rare_cnt, int64_t rare_cap,
     const uint32_t* __restrict__ perm) {
@@ -1245,8 +1268,11 @@ __global__ __launch_bounds__(64) void fill_pos_kernel(
     __shared__ uint32_t s_p[kWinDense];
     __shared__ uint64_t s_f[kRareFences];
     __shared__ uint64_t s_mk[kPosSeg];
+    __shared__ unsigned long long s_rb[kRareBuf];
     const int lane = threadIdx.x;
-    const int64_t sg = blockIdx.x;
+    WaveRareBuf rb{s_rb, 0};
+    for (int64_t sg = blockIdx.x; sg < ns; sg += gridDim.x) {
+    __syncthreads();                                      // the previous segment's LDS reads are done
     const int64_t wv = lane < 6 ? win[sg * 8 + lane] : 0;
     int64_t dlo = __shfl((long long)wv, 0, 64), dhi = __shfl((long long)wv, 1, 64);
     int64_t rlo = __shfl((long long)wv, 2, 64), rhi = __shfl((long long)wv, 3, 64);
@@ -1257,9 +1283,7 @@ __global__ __launch_bounds__(64) void fill_pos_kernel(
     if (nd <= kWinDense && nf <= kRareFences) {
         // lane l takes the segment's codes [8 l, 8 l + 8): one binary search
         // for the first, then (codes ascending) a short forward walk per code
-        // from the previous code's rank — about 2 dependent LDS reads a code
-        // instead of a 10-step search each (C2: the segment's codes and its
-        // dense window are about equally dense)
+        // from the previous code's rank
         constexpr int PL = kPosSeg / 64;
         const int64_t i0 = b + (int64_t)PL * lane;
         uint64_t kk[PL];
@@ -1311,9 +1335,9 @@ __global__ __launch_bounds__(64) void fill_pos_kernel(
                         if (q0 + u < rhi && v[u] == k) { rhit = true; q = q0 + u; }
                 }
             }
-            append_rare(rhit, q, set, id_base, rare_out, rare_cnt, rare_cap);
+            append_rare(rhit, q, set, id_base, rb, rare_out, rare_cnt, rare_cap);
         }
-        return;
+        continue;
     }
     // fallback: walk the windows in global memory
     for (int64_t i0 = b; i0 < e; i0 += 64) {
@@ -1329,9 +1353,11 @@ __global__ __launch_bounds__(64) void fill_pos_kernel(
             int64_t q;
             bool rhit;
             wave_rank(rare, rlo, rhi, k, miss, q, rhit);
-            append_rare(rhit, q, set, id_base, rare_out, rare_cnt, rare_cap);
+            append_rare(rhit, q, set, id_base, rb, rare_out, rare_cnt, rare_cap);
         }
     }
+    }
+    rare_flush(rb, rare_out, rare_cnt, rare_cap);
 }
 
 __device__ __forceinline__ void pos_or(uint32_t* lds, uint32_t p, uint32_t sb) {
@@ -1452,8 +1478,10 @@ void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_
                     s->codes.as<uint64_t>(), s->off.as<int64_t>(), sg, ns, dict, U, rare, Ur, win.as<int64_t>());
                 GD_HIP(hipGetLastError());
                 GD_REQUIRE(ns < (int64_t(1) << 31), "too many fill segments in one chunk");
-                fill_pos_kernel<<<(unsigned)ns, 64, 0, st>>>(s->codes.as<uint64_t>(), win.as<int64_t>(), dict, rare,
-                                                             base, pos.as<uint32_t>(),
+                // blocks take the segments in turn (a block's rare records staged across them)
+                const int64_t nblk = std::min<int64_t>(ns, (int64_t)ctx->cus * 32);
+                fill_pos_kernel<<<(unsigned)nblk, 64, 0, st>>>(s->codes.as<uint64_t>(), win.as<int64_t>(), ns, dict,
+                                                             rare, base, pos.as<uint32_t>(),
                                                              id_base, rare_out, rcnt.as<unsigned long long>(),
                                                              rare_cap, perm);
                 GD_HIP(hipGetLastError());

@@ -306,16 +306,39 @@ __global__ void hash_insert_kernel(const uint64_t* __restrict__ codes, int64_t n
 
 // one workgroup per set of the chunk: every code probes the table; positions
 // go to pos (u32, ~0: not dense / variant), rare codes append their record
-// (rare rank << 32 | set) with one atomic per wave
+// (rare rank << 32 | set + id_base), staged in LDS and appended with one
+// atomic per kProbeBuf records (C3: one atomic per wave and round on a single
+// counter was 5 M same-address atomics, ~60 ms)
+constexpr int kProbeBuf = 2048;
+__device__ __forceinline__ void probe_flush(unsigned long long* s_rb, unsigned* s_n, unsigned long long* s_g,
+                                            unsigned long long* __restrict__ rare_out,
+                                            unsigned long long* __restrict__ rare_cnt, int64_t rare_cap) {
+    const unsigned n = *s_n;                                   // uniform: read after a barrier
+    if (!n) return;
+    if (threadIdx.x == 0) *s_g = atomicAdd(rare_cnt, (unsigned long long)n);
+    __syncthreads();
+    const unsigned long long g = *s_g;
+    for (unsigned j = threadIdx.x; j < n; j += blockDim.x)
+        if ((int64_t)(g + j) < rare_cap) rare_out[g + j] = s_rb[j];
+    __syncthreads();
+    if (threadIdx.x == 0) *s_n = 0;
+    __syncthreads();
+}
+
 __global__ __launch_bounds__(256) void hash_probe_kernel(const uint64_t* __restrict__ codes,
                                                          const int64_t* __restrict__ off, int64_t s0, int64_t base,
                                                          const unsigned long long* __restrict__ tab,
                                                          unsigned long long mask, uint32_t* __restrict__ pos,
                                                          int64_t id_base, unsigned long long* __restrict__ rare_out,
                                                          unsigned long long* __restrict__ rare_cnt, int64_t rare_cap) {
+    __shared__ unsigned long long s_rb[kProbeBuf];
+    __shared__ unsigned s_n;
+    __shared__ unsigned long long s_g;
     const int64_t set = s0 + blockIdx.x;
     const int lane = threadIdx.x & 63;
     const int64_t b = off[set], e = off[set + 1];
+    if (threadIdx.x == 0) s_n = 0;
+    __syncthreads();
     for (int64_t x0 = b; x0 < e; x0 += 256) {
         const int64_t x = x0 + threadIdx.x;
         unsigned long long val = kHashEmpty;
@@ -333,16 +356,17 @@ __global__ __launch_bounds__(256) void hash_probe_kernel(const uint64_t* __restr
         const bool rhit = val != kHashEmpty && (val & kTagMask) == kRareTag;
         const unsigned long long m = __ballot(rhit);
         if (m) {
-            unsigned long long b0 = 0;
-            if (lane == __ffsll((long long)m) - 1) b0 = atomicAdd(rare_cnt, (unsigned long long)__popcll(m));
-            b0 = (unsigned long long)__shfl((long long)b0, __ffsll((long long)m) - 1, 64);
-            if (rhit) {
-                const unsigned long long slotr = b0 + __popcll(m & ((1ull << lane) - 1));
-                if ((int64_t)slotr < rare_cap)
-                    rare_out[slotr] = ((val & 0xFFFFFFFFull) << 32) | (unsigned long long)(uint32_t)(set + id_base);
-            }
+            unsigned b0 = 0;
+            if (lane == __ffsll((long long)m) - 1) b0 = atomicAdd(&s_n, (unsigned)__popcll(m));
+            b0 = (unsigned)__shfl((int)b0, __ffsll((long long)m) - 1, 64);
+            if (rhit)
+                s_rb[b0 + __popcll(m & ((1ull << lane) - 1))] =
+                    ((val & 0xFFFFFFFFull) << 32) | (unsigned long long)(uint32_t)(set + id_base);
         }
+        __syncthreads();
+        if (s_n > (unsigned)(kProbeBuf - 256)) probe_flush(s_rb, &s_n, &s_g, rare_out, rare_cnt, rare_cap);
     }
+    probe_flush(s_rb, &s_n, &s_g, rare_out, rare_cnt, rare_cap);
 }
 
 // ---- variant records of one fill chunk -----------------------------------
