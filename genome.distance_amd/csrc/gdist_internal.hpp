@@ -195,7 +195,6 @@ struct Timing {
     X(SKETCH_CAP, "sketch_cap")               /* ring kernel: merge steps per phase (default 160) */           \
     X(SKETCH_RING, "sketch_ring")             /* ring kernel slots per sketch (default 256) */                 \
     X(SKETCH_WAIT, "sketch_wait")             /* 1: ring pairs without room wait (global reads only if stuck) */ \
-    X(SKETCH_PREFETCH, "sketch_prefetch")     /* 1: ring kernel loads the next top-up before the merge */       \
     X(SPARSE_PART_BUDGET, "sparse_part_budget") /* bytes of sparse chunk partials one region may hold */       \
     X(GUIDES, "guides")                       /* guide sequences keyed at pack time (default kGuides) */       \
     X(FORCE_EXCHANGE, "force_exchange")       /* 1: a one-rank communicator runs every collective (tests) */   \

@@ -324,16 +324,6 @@ typedef int32_t i32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 // C5: 430 vs 336 ms with a 448-slot ring, the waiting pairs add phases). Positions, steps and the
 // closed form are the merge's: results are identical
 // (test_sketch_merge_edges_vs_oracle runs rings of 16..448 slots).
-// PF (option sketch_prefetch): the next phase's top-up is loaded into
-// registers right after this phase's, before the merge, so its global latency
-// hides behind the merge instead of sitting between the phase's barriers. A
-// phase advances every open pair by at most K < RS steps, so the next top-up
-// is a stretch of at most K positions from the current top: thread (s, wave)
-// holds positions top + wave * 4 + k * NW * 4 (k < kPfLoads) and writes the
-// ones below the next phase's limit; a longer stretch (only when K exceeds
-// kPfLoads * NW * 4) falls back to the plain loads.
-constexpr int kPfLoads = 3;
-template <bool PF>
 __global__ __launch_bounds__(kSkTile * kSkTile) void sketch_ring_kernel(
     const int32_t* __restrict__ sig, const int64_t* __restrict__ off, int width, int RS, int kmax, int64_t r0,
     int64_t r1, int64_t c0, int64_t c1, int64_t tile0, int tiles_c, int upper, int jaccard, int empty_nan,
@@ -390,8 +380,6 @@ __global__ __launch_bounds__(kSkTile * kSkTile) void sketch_ring_kernel(
     const int32_t* gA = sig + s_base[ty];
     const int32_t* gB = sig + s_base[R + tx];
     bool stalled = false;
-    i32x4_a4 pf[kPfLoads];
-    int pf_from = -1;                                 // the first position the registers hold (-1: none)
     for (;;) {
         // 1. the least position of the open pairs on every sketch
         if (threadIdx.x < NS) s_min[threadIdx.x] = 0x7FFFFFFF;
@@ -412,25 +400,7 @@ __global__ __launch_bounds__(kSkTile * kSkTile) void sketch_ring_kernel(
             const int32_t* src = sig + s_base[s];
             const int M = RS - 1;                   // RS: a power of two
             int q = (lo + wave * 4) & M;
-            int t0 = lo + wave * 4;
-            if (PF && pf_from == lo && hi - lo <= kPfLoads * NW * 4) {
-                // the stretch was prefetched: write it from the registers
-#pragma unroll
-                for (int k = 0; k < kPfLoads; k++) {
-                    const int t = lo + wave * 4 + k * NW * 4;
-                    const int32_t vv[4] = {pf[k].x, pf[k].y, pf[k].z, pf[k].w};
-#pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        if (t + u < hi) {
-                            const int qu = (t + u) & M;
-                            sm[qu * NS + s] = vv[u];
-                            if (qu == 0) sm[RS * NS + s] = vv[u];
-                        }
-                    }
-                }
-                t0 = hi;                            // nothing left for the plain loads
-            }
-            for (int t = t0; t < hi; t += NW * 4) {
+            for (int t = lo + wave * 4; t < hi; t += NW * 4) {
                 i32x4_a4 v;
                 if (t + 4 <= n) {
                     v = *reinterpret_cast<const i32x4_a4*>(src + t);
@@ -453,27 +423,6 @@ __global__ __launch_bounds__(kSkTile * kSkTile) void sketch_ring_kernel(
             }
         }
         __syncthreads();
-        if (PF) {
-            // prefetch the next top-up: positions from the new top (every
-            // thread computes it for its own sketch s = lane)
-            const int s = lane;
-            const int n = s_n[s], least = s_min[s];
-            const int nt = least == 0x7FFFFFFF ? -1 : min(n + 2, least + RS);
-            const int32_t* src = sig + s_base[s];
-            pf_from = nt;
-#pragma unroll
-            for (int k = 0; k < kPfLoads; k++) {
-                const int t = nt + wave * 4 + k * NW * 4;
-                if (nt >= 0 && t + 4 <= n) {
-                    pf[k] = *reinterpret_cast<const i32x4_a4*>(src + t);
-                } else {
-                    pf[k].x = nt >= 0 && t < n ? src[t] : 0x7FFFFFFF;
-                    pf[k].y = nt >= 0 && t + 1 < n ? src[t + 1] : 0x7FFFFFFF;
-                    pf[k].z = nt >= 0 && t + 2 < n ? src[t + 2] : 0x7FFFFFFF;
-                    pf[k].w = 0x7FFFFFFF;
-                }
-            }
-        }
         if (threadIdx.x < NS && s_min[threadIdx.x] != 0x7FFFFFFF)
             s_top[threadIdx.x] = min(s_n[threadIdx.x] + 2, s_min[threadIdx.x] + RS);
         // 3. K steps per open pair
@@ -556,7 +505,7 @@ inline size_t sketch_ring_lds(int rs) { return (size_t)(rs + 1) * kSkLanes * 4; 
 
 int launch_sketch_ring(hipStream_t st, const gdist_sets* sk, int width, int rs, int kmax, int64_t r0, int64_t r1,
                         int64_t c0, int64_t c1, bool upper, int jac, int en, int32_t* d_common, double* d_D,
-                        int64_t ld, bool fallback, bool prefetch) {
+                        int64_t ld, bool fallback) {
     const size_t lds = sketch_ring_lds(rs);
     GD_REQUIRE(rs >= 16 && (rs & (rs - 1)) == 0 && kmax >= 2 && kmax < rs,
                "sketch ring: a power of two >= 16 slots, 2 <= steps per phase < slots");
@@ -568,7 +517,7 @@ int launch_sketch_ring(hipStream_t st, const gdist_sets* sk, int width, int rs, 
     const int64_t grid = tri ? (int64_t)tc * (tc + 1) / 2 : (int64_t)tr * tc;
     const int threads = kSkTile * kSkTile;
     const int64_t per = (int64_t(1) << 31) / threads;     // a dispatch holds < 2^32 work-items
-    auto kern = prefetch ? &sketch_ring_kernel<true> : &sketch_ring_kernel<false>;
+    auto kern = &sketch_ring_kernel;
     GD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)lds));
     int launches = 0;
@@ -748,8 +697,7 @@ void sketch_matrix(gdist_ctx* ctx, const gdist_sets* sk, int64_t r0, int64_t r1,
         const int kmax = (int)std::max<int64_t>(2, std::min<int64_t>(ctx->option(OPT_SKETCH_CAP, 160), 1 << 20));
         const int rs = (int)std::max<int64_t>(16, std::min<int64_t>(ctx->option(OPT_SKETCH_RING, 256), 1 << 20));
         launches = launch_sketch_ring(st, sk, width, rs, std::min(kmax, rs - 1), r0, r1, c0, c1, upper, jac, en,
-                                      d_common, d_D, ld, ctx->option(OPT_SKETCH_WAIT, 0) == 0,
-                                      ctx->option(OPT_SKETCH_PREFETCH, 0) != 0);
+                                      d_common, d_D, ld, ctx->option(OPT_SKETCH_WAIT, 0) == 0);
     } else {
         if (!only16)
             launches = launch_sketch_tiles<16, 24>(st, sk, width, r0, r1, c0, c1, upper, jac, en, d_common, d_D, ld,

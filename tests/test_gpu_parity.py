@@ -438,8 +438,6 @@ def test_sketch_matrix_vs_oracle(ctx):
     (1, None, None, 1, 2), (1, 2, 512, 1, 2), (1, 7, 512, 1, 2), (1, 64, 256, 1, 2), (1, 255, 256, 1, 2),
     (1, 5000, 128, 1, 2), (1, 15, 16, 1, 2), (1, 8, 32, 1, 2), (1, 120, 512, 1, 2), ("w", 15, 16, 1, 2),
     ("w", 8, 32, 1, 2), ("w", 64, 256, 1, 2),
-    ("p", None, None, 1, 2), ("p", 2, 512, 1, 2), ("p", 7, 512, 1, 2), ("p", 255, 256, 1, 2),
-    ("p", 15, 16, 1, 2), ("p", 300, 512, 1, 2), ("p", 5000, 128, 1, 2),
     (0, 300, None, 1, 2), (0, 300, None, 0, 2), (0, 300, None, 0, 4), (0, 300, None, 0, 1)])
 def test_sketch_merge_edges_vs_oracle(ctx, opts, phase, cap, ring, v2, k):
     """Uploaded sketches with the merge's edge cases, every pair against the
@@ -447,17 +445,14 @@ def test_sketch_merge_edges_vs_oracle(ctx, opts, phase, cap, ring, v2, k):
     sketch_ring + sketch_cap, rings of 16..512 slots with 2..5000 steps per
     phase; pairs without room in a small ring take global-memory steps, or
     with sketch_wait wait for the slower pairs until a phase makes no
-    progress; with sketch_prefetch the next top-up is loaded into registers
-    before the merge, and a top-up longer than the registers hold (300 steps)
-    takes the plain loads; sketch_phase = 0 with sketch_v2 / sketch_k: whole sketches in
+    progress; sketch_phase = 0 with sketch_v2 / sketch_k: whole sketches in
     LDS): empty and short sketches,
     identical ones, disjoint ones, INT_MIN / INT_MAX hashes (INT_MAX is the
     LDS sentinel: such pairs take the checked loop)."""
     import gdist
     wait = phase == "w"                       # ring pairs without room wait (option sketch_wait)
-    pf = phase == "p"                         # the ring kernel's prefetched top-up (option sketch_prefetch)
-    opts(sketch_phase=1 if wait or pf else phase, sketch_wait=1 if wait else None, sketch_cap=cap, sketch_ring=ring,
-         sketch_v2=v2, sketch_k=k, sketch_prefetch=1 if pf else None)
+    opts(sketch_phase=1 if wait else phase, sketch_wait=1 if wait else None, sketch_cap=cap, sketch_ring=ring,
+         sketch_v2=v2, sketch_k=k)
     rng = np.random.default_rng(1234)
     for w in (64, 1000):
         sk = []
