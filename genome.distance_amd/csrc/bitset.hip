@@ -219,30 +219,12 @@ constexpr int RCH = 16384;   // max columns per LDS chunk (64 KiB of counters)
 // 65,536 sets): the walk's scattered list reads are whole lines from HBM or
 // the Infinity Cache, and 2-byte members halve the lines a list spans and
 // let C3's lists (72 M members: 287 MB as uint32) sit in the 256 MiB cache.
-// FLAT (option rare_flat, default): the members of a batch of 64 records
-// are walked flattened — lane l of a step takes member slot f = step + l of the
-// batch's concatenated lists, so every lane has a member while any remain (a
-// lane per record idles on the wave's longest list: C3's ~13-member lists
-// after the row's own position, 1 to ~60) and consecutive lanes read
-// consecutive members of one list (coalesced). The record of slot f is found
-// as in the sparse walk (sparse.hip): records without members are compacted
-// out, and per group of 64 slots a ballot counts the records ending before
-// it and a 64-bit mask of the records' last slots inside it gives the rest by
-// mbcnt.
-constexpr int kFlatWin = 16;                     // groups of 64 slots per mask window
-constexpr int kFlatSun = 4;                      // groups per step (members in flight per lane)
-struct FlatRec {
-    int64_t base;                                // list position of slot 0 (member y = base + f)
-    int32_t w;                                   // the list's weight
-    int32_t pad;
-};
-__device__ __forceinline__ int flat_rec(int last, int gb, unsigned long long m) {
-    const int before = __popcll(__ballot(last < gb));
-    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, (uint32_t)before));
-}
-
-template <typename M, bool FLAT>
-__global__ __launch_bounds__(256) void rare_rows_kernel(const int64_t* __restrict__ soff,
+// NT threads a workgroup (option rare_rows_threads: 512 default, 256): the
+// walk is latency-bound (each record's members are a dependent load after its
+// record's), and the 40 KiB of counters of a C3 row allow 4 workgroups a CU:
+// 512 threads make that the full 32 waves a CU instead of 16
+template <typename M, int NT>
+__global__ __launch_bounds__(NT) void rare_rows_kernel(const int64_t* __restrict__ soff,
                                                         const uint64_t* __restrict__ sent,
                                                         const uint32_t* __restrict__ sw,
                                                         const uint16_t* __restrict__ sskip,
@@ -267,71 +249,7 @@ __global__ __launch_bounds__(256) void rare_rows_kernel(const int64_t* __restric
     const int64_t xb = rb + per * split;
     const int64_t xe = xb + per < re ? xb + per : re;
     const int lane = threadIdx.x & 63;
-    if (FLAT) {
-        __shared__ FlatRec frec[4][65];
-        __shared__ unsigned long long fmask[4][kFlatWin];
-        const int wv = threadIdx.x >> 6;
-        FlatRec* rec = frec[wv];
-        unsigned long long* masks = fmask[wv];
-        for (int64_t xbase = xb + wv * 64; xbase < xe; xbase += 256) {
-            const int64_t x = xbase + lane;
-            int len = 0;
-            int64_t b = 0;
-            int32_t w = 0;
-            if (x < xe) {
-                const uint64_t ent = sent[x];
-                w = (int32_t)sw[x];
-                const int64_t b0 = (int64_t)(ent >> 24), e = b0 + (int64_t)(ent & 0xFFFFFFu);
-                b = upper ? b0 + sskip[x] : b0;
-                len = e > b ? (int)(e - b) : 0;
-            }
-            int incl = len;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int v = __shfl_up(incl, o, 64);
-                if (lane >= o) incl += v;
-            }
-            const int total = __builtin_amdgcn_readlane(incl, 63);
-            const unsigned long long nz = __ballot(len > 0);
-            const int k = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(nz >> 32),
-                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)nz, 0u));
-            if (len > 0) rec[k] = FlatRec{b - (int64_t)(incl - len), w, 0};
-            if (lane == 0) rec[__popcll(nz)] = FlatRec{0, 0, 0};     // slots past the last member
-            const int last = len > 0 ? incl - 1 : 0x7FFFFFFF;
-            __builtin_amdgcn_wave_barrier();
-            __atomic_signal_fence(__ATOMIC_SEQ_CST);
-            for (int W0 = 0; W0 < total; W0 += 64 * kFlatWin) {
-                if (lane < kFlatWin) masks[lane] = 0ull;
-                __builtin_amdgcn_wave_barrier();
-                __atomic_signal_fence(__ATOMIC_SEQ_CST);
-                const uint32_t rel = (uint32_t)(last - W0);
-                if (rel < 64u * kFlatWin) atomicOr(&masks[rel >> 6], 1ull << (rel & 63));
-                __builtin_amdgcn_wave_barrier();
-                __atomic_signal_fence(__ATOMIC_SEQ_CST);
-                const int wend = total < W0 + 64 * kFlatWin ? total : W0 + 64 * kFlatWin;
-                for (int fb = W0; fb < wend; fb += 64 * kFlatSun) {
-                    FlatRec r[kFlatSun];
-                    int64_t t[kFlatSun];
-#pragma unroll
-                    for (int u = 0; u < kFlatSun; u++) {
-                        const int gb = fb + 64 * u;
-                        r[u] = rec[flat_rec(last, gb, gb < wend ? masks[(gb - W0) >> 6] : 0ull)];
-                    }
-#pragma unroll
-                    for (int u = 0; u < kFlatSun; u++) {
-                        const int f = fb + 64 * u + lane;
-                        t[u] = f < wend ? (int64_t)psets[r[u].base + f] : -1;
-                    }
-#pragma unroll
-                    for (int u = 0; u < kFlatSun; u++)
-                        if (t[u] >= lo && t[u] < ce && t[u] != i) atomicAdd(&cnt[t[u] - cb], r[u].w);
-                }
-                __builtin_amdgcn_wave_barrier();
-                __atomic_signal_fence(__ATOMIC_SEQ_CST);
-            }
-        }
-    }
-    for (int64_t xbase = xb; !FLAT && xbase < xe; xbase += blockDim.x) {   // wave-uniform trip count
+    for (int64_t xbase = xb; xbase < xe; xbase += blockDim.x) {   // wave-uniform trip count
         const int64_t x = xbase + threadIdx.x;
         const uint64_t ent = x < xe ? sent[x] : 0ull;  // coalesced: no random bounds lookup
         const int32_t w = x < xe ? (int32_t)sw[x] : 0;
@@ -2085,19 +2003,19 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
         GD_REQUIRE(rgrid < (int64_t(1) << 31), "rare-tier grid too large");
         const size_t lds = (size_t)std::min<int64_t>(nc, RCH) * 4;
         FamilyTimer ft(ctx, GDIST_KERNEL_RARE, rs);
-        const bool flat = ctx->option(OPT_RARE_FLAT, 0) != 0;   // measured slower on C3 (r04s11/ab3)
-        auto go = [&](auto kern, auto* members) {
-            kern<<<(unsigned)rgrid, 256, lds, rs>>>(s->srare_off.as<int64_t>(), s->srare_ent.as<uint64_t>(),
-                                                    s->srare_w.as<uint32_t>(), s->srare_skip.as<uint16_t>(), members,
-                                                    r0, r1, c0, c1, nch, nsplit, upper ? 1 : 0, atomic_flush ? 1 : 0,
-                                                    d_I, ldI);
+        const bool wide = ctx->option(OPT_RARE_ROWS_THREADS, 512) != 256;
+        auto go = [&](auto kern, int nt, auto* members) {
+            kern<<<(unsigned)rgrid, nt, lds, rs>>>(s->srare_off.as<int64_t>(), s->srare_ent.as<uint64_t>(),
+                                                   s->srare_w.as<uint32_t>(), s->srare_skip.as<uint16_t>(), members,
+                                                   r0, r1, c0, c1, nch, nsplit, upper ? 1 : 0, atomic_flush ? 1 : 0,
+                                                   d_I, ldI);
         };
         if (s->post_sets16.p) {
-            if (flat) go(rare_rows_kernel<uint16_t, true>, s->post_sets16.as<uint16_t>());
-            else go(rare_rows_kernel<uint16_t, false>, s->post_sets16.as<uint16_t>());
+            if (wide) go(rare_rows_kernel<uint16_t, 512>, 512, s->post_sets16.as<uint16_t>());
+            else go(rare_rows_kernel<uint16_t, 256>, 256, s->post_sets16.as<uint16_t>());
         } else {
-            if (flat) go(rare_rows_kernel<uint32_t, true>, s->post_sets.as<uint32_t>());
-            else go(rare_rows_kernel<uint32_t, false>, s->post_sets.as<uint32_t>());
+            if (wide) go(rare_rows_kernel<uint32_t, 512>, 512, s->post_sets.as<uint32_t>());
+            else go(rare_rows_kernel<uint32_t, 256>, 256, s->post_sets.as<uint32_t>());
         }
         ft.end();
     };

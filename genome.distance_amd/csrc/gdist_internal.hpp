@@ -215,7 +215,7 @@ struct Timing {
     X(SPARSE_GROUPS, "sparse_groups")         /* 0: no group tier (clade patterns) in the sparse words */       \
     X(SPARSE_XCD, "sparse_xcd")               /* 1: chunk c of every sparse tile on XCD c mod 8 */           \
     X(RARE_U16, "rare_u16")                   /* 0: 4-byte list members in the row-major rare walk */        \
-    X(RARE_FLAT, "rare_flat")                 /* 0: the row-major rare walk a lane per record (A/B) */     \
+    X(RARE_ROWS_THREADS, "rare_rows_threads") /* row-major rare walk: threads a workgroup (512 default, 256) */ \
     X(SORT_RADIX, "sort_radix")               /* 10: onesweep radix sorts of u64 keys in 10-bit passes (A/B) */\
     X(VARIANT, "variant")                     /* variant tier: 1 force, 0 off (default: by the dictionary) */ \
     X(VARIANT_DMIN, "variant_dmin")           /* sets holding a dense-tier kmer (default N / 10) */            \

@@ -677,15 +677,14 @@ def test_k32_all_ones_code(ctx, strand):
 def test_rare_tier_thresholds_exact(ctx, T, kernel, dedup, opts):
     """Dense-only (T=0), mixed, and all-rare (T > N) dictionaries give the
     same bit-exact counts and distances as the oracle, through the list-major
-    (0) and the row-major (1: 2-byte list members, 1w: 4-byte; a lane per
-    record (1l / 1lw, the default) or the members flattened over the lanes
-    (option rare_flat)) rare kernel,
+    (0) and the row-major (1: 2-byte list members, 1w: 4-byte; 512-thread
+    workgroups, or 256 as 1l / 1lw) rare kernel,
     with identical posting lists merged into weighted lists (1) or one list
     per kmer (0). T > N puts lists of up to N members in the rare tier: the
     wave-cooperative long-list walks."""
     import gdist
     opts(rare_kernel=int(kernel[0]), rare_dedup=int(dedup), rare_u16=0 if kernel.endswith("w") else None,
-         rare_flat=None if "l" in kernel else 1)
+         rare_rows_threads=256 if "l" in kernel else None)
     n = 200
     seqs = synth_sets(n, 6000, 0.01, 101)
     sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
