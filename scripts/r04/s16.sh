@@ -1,13 +1,17 @@
 #!/bin/bash
 # Round 4 session 16: the C4 per-rank slice bench line (rank 0's first 64
-# rows x 100,000 columns, the exchange through RCCL on a one-rank
+# rows (and 1,024 rows) x 100,000 columns, the exchange through RCCL on a one-rank
 # communicator, METHOD_AUTO -> the variant tier) with a rocprofv3 summary.
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r04s16
 mkdir -p $O
-timeout -k 10 600 python -u bench.py --config c4 --rows 0:64 --force-exchange --steps 5 --warmup 1 \
-    > $O/bench_c4_slice.json 2> $O/bench_c4_slice.err
+timeout -k 10 500 python -u bench.py --config c4 --rows 0:64 --force-exchange --steps 5 --warmup 1 \
+    > $O/bench_c4_slice.json 2> $O/bench_c4_slice.err &&
+timeout -k 10 500 python -u bench.py --config c4 --rows 0:1024 --force-exchange --steps 5 --warmup 1 --no-cpu-baseline \
+    > $O/bench_c4_slice1024.json 2> $O/bench_c4_slice1024.err
 rc=$?
-python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(json.dumps(d)[:3000])" $O/bench_c4_slice.json
+for f in $O/bench_c4_slice.json $O/bench_c4_slice1024.json; do
+    python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(json.dumps(d)[:2500])" $f
+done
 exit $rc
