@@ -438,27 +438,16 @@ __global__ __launch_bounds__(kSkTile * kSkTile) void sketch_ring_kernel(
                     const int ns = min(K - done, max(ina - pa, inb - pb));
                     if (ns < 2) break;
                     const int nr = ns >> 1;
-                    // stretches of two-step rounds that cannot pass the mirror
-                    // row (a round reads slots q and q + 1 and moves q by <= 2):
-                    // inside one the slot address is base + position, one VALU
-                    // instead of the ring mask and the scaling (round 4)
-                    for (int r = 0; r < nr;) {
-                        const int qa = pa & mask, qb = pb & mask;
-                        const int seg = min(nr - r, min(RS - qa + 1, RS - qb + 1) >> 1);
-                        const int32_t* baseA = Arow + (qa - pa) * NS;
-                        const int32_t* baseB = Brow + (qb - pb) * NS;
-                        for (int t = 0; t < seg; t++) {
-                            const int32_t* pA = baseA + pa * NS;      // slot RS - 1: pA[NS] is the mirror row
-                            const int32_t* pB = baseB + pb * NS;
-                            const int32_t a0 = pA[0], a1 = pA[NS], b0 = pB[0], b1 = pB[NS];
-                            const bool le = a0 <= b0, ge = b0 <= a0;
-                            const int32_t x = le ? a1 : a0, y = ge ? b1 : b0;
-                            pa += le;
-                            pb += ge;
-                            pa += x <= y;
-                            pb += y <= x;
-                        }
-                        r += seg;
+                    for (int r = 0; r < nr; r++) {
+                        const int32_t* pA = Arow + (pa & mask) * NS;      // slot RS - 1: pA[NS] is the mirror row
+                        const int32_t* pB = Brow + (pb & mask) * NS;
+                        const int32_t a0 = pA[0], a1 = pA[NS], b0 = pB[0], b1 = pB[NS];
+                        const bool le = a0 <= b0, ge = b0 <= a0;
+                        const int32_t x = le ? a1 : a0, y = ge ? b1 : b0;
+                        pa += le;
+                        pb += ge;
+                        pa += x <= y;
+                        pb += y <= x;
                     }
                     done += 2 * nr;
                 }
