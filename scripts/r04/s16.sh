@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 O=gpurun_out/r04s16
 mkdir -p $O
 timeout -k 10 60 scripts/microbench/fp4_probe > $O/fp4_probe.txt 2>&1
-cat $O/fp4_probe.txt
+rc=$?; cat $O/fp4_probe.txt; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 500 python -u bench.py --config c4 --rows 0:64 --force-exchange --steps 5 --warmup 1 \
     > $O/bench_c4_slice.json 2> $O/bench_c4_slice.err &&
 timeout -k 10 500 python -u bench.py --config c4 --rows 0:1024 --force-exchange --steps 5 --warmup 1 --no-cpu-baseline \
