@@ -540,6 +540,151 @@ __global__ __launch_bounds__(NT, 4) void bitset_tile_kernel2(
     }
 }
 
+// ---- dense tiles on the matrix cores (round 4) ------------------------------
+// |A ∩ B| over the dense words is a bit-matrix product: I = Σ_k a_ik b_jk over
+// the dictionary bits. The block-scaled MFMA v_mfma_scale_f32_32x32x64_f8f6f4
+// takes FP4 (e2m1) operands, where the codes 0x0 and 0x2 are 0.0 and 1.0:
+// with every bit stored as one nibble, one instruction is a 32 x 32 block of
+// pairs over 64 bits (one word), products and f32 sums exact (a count <=
+// 64 W < 2^24). The FP4 rate is 4x the BF16 MFMA rate, 5 P products/s
+// dense; the AND + popcount tiles are capped at 0.63 P bit-pairs/s by the
+// half-rate v_bcnt. Operand map (scripts/microbench/fp4_probe.hip, checked
+// against the CPU): lane r + 32 h holds row r's bits [32 h, 32 h + 32) of the
+// word as 16 bytes of nibbles, low nibble first; D: column lane & 31, row
+// (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5).
+// F = the dense bits expanded once per collection, [N][32 W] bytes (4x the
+// bitsets). A workgroup of 8 waves owns a 256 x 256 tile of pairs and a range
+// of words, each wave 64 rows x 128 columns (2 x 4 MFMA blocks, 128 f32
+// accumulators a lane); stages of KM words of both operands (256 rows x
+// 32 KM bytes each) are moved by global_load_lds, double buffered, with the
+// 16-byte chunk c of row g stored at c ^ ((g >> 1) & 7) (conflict-free
+// fragment reads); units split-major and XCD-remapped as the VALU tiles.
+constexpr int MT = 256;                       // tile edge (sets)
+constexpr int64_t kMfmaMinWords = 64;         // dense words from which the MFMA tiles run (option bitset_mfma)
+constexpr int MNT = 512;                      // threads
+constexpr int KM = 4;                         // words per stage
+constexpr int MROW = KM * 32;                 // bytes per row per stage (128)
+constexpr int MOPB = MT * MROW;               // one operand's stage (32 KiB)
+typedef int v8i_t __attribute__((ext_vector_type(8)));
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+typedef float v16f_t __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ uint32_t bits_to_nibbles(uint32_t byte) {   // 8 bits -> 8 nibbles 0x0 / 0x2
+    uint32_t t = (byte & 0x0Fu) | ((byte & 0xF0u) << 12);
+    t = (t | (t << 6)) & 0x03030303u;
+    t = (t | (t << 3)) & 0x11111111u;
+    return t << 1;
+}
+
+// F[i][32 w + q] for one (set, word) per thread: 32 bytes of nibbles
+__global__ void fp4_expand_kernel(const unsigned long long* __restrict__ bits, int64_t n, uint4* __restrict__ out) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += stride) {
+        const unsigned long long w = bits[t];
+        const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
+        out[2 * t] = make_uint4(bits_to_nibbles(lo & 0xFF), bits_to_nibbles((lo >> 8) & 0xFF),
+                                bits_to_nibbles((lo >> 16) & 0xFF), bits_to_nibbles(lo >> 24));
+        out[2 * t + 1] = make_uint4(bits_to_nibbles(hi & 0xFF), bits_to_nibbles((hi >> 8) & 0xFF),
+                                    bits_to_nibbles((hi >> 16) & 0xFF), bits_to_nibbles(hi >> 24));
+    }
+}
+
+__device__ __forceinline__ int mlds(int g, int c) { return g * MROW + ((c ^ ((g >> 1) & 7)) << 4); }
+
+// one operand's stage: 2048 chunks of 16 B, 4 per thread (lane-linear LDS,
+// the swizzle applied on the source address)
+__device__ __forceinline__ void mfma_stage(const unsigned char* __restrict__ F, int64_t rowbytes, int64_t set0,
+                                           int64_t lo, int64_t lim, int64_t w0, unsigned char* lds_op, int tid) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int q = i * MNT + tid;                  // 16-byte slot of the stage
+        const int g = q >> 3, sl = q & 7;
+        const int c = sl ^ ((g >> 1) & 7);            // the chunk this slot holds
+        int64_t set = set0 + g;
+        set = set < lim ? set : lim - 1;              // rows outside [lo, lim): clamped, masked at the end
+        set = set >= lo ? set : lo;
+        const unsigned char* src = F + set * rowbytes + w0 * 32 + c * 16;
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(lds_op + (i * MNT + (tid & ~63)) * 16), 16,
+                                         0, 0);
+    }
+}
+
+__global__ __launch_bounds__(MNT, 2) void bitset_mfma_kernel(
+    const unsigned char* __restrict__ F, int64_t W, const int2* __restrict__ tiles, int ntiles, int splits,
+    int64_t nstages, int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I,
+    int64_t ldI) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char mlds_buf[];     // 2 stages x (A, B) = 128 KiB
+    const int64_t G = gridDim.x, blk = blockIdx.x;
+    const int64_t xcd = blk & 7, kq = blk >> 3, qg = G >> 3, rem = G & 7;
+    const int64_t u = xcd * qg + (xcd < rem ? xcd : rem) + kq;
+    const int split = (int)(u / ntiles);
+    const int tile = (int)(u - (int64_t)split * ntiles);
+    if (split >= splits) return;
+    const int2 t = tiles[tile];
+    const int64_t row0 = r0 + (int64_t)t.x * MT, col0 = c0 + (int64_t)t.y * MT;
+    const int64_t per = ceil_div(nstages, splits);
+    const int64_t ks0 = (int64_t)split * per, ks1 = ks0 + per < nstages ? ks0 + per : nstages;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 1, wc = wave & 1;          // 4 x 2 waves of 64 rows x 128 columns
+    const int r = lane & 31, h = lane >> 5;
+    const int64_t rowbytes = W * 32;
+    v16f_t acc[2][4];
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 4; b++)
+#pragma unroll
+            for (int q = 0; q < 16; q++) acc[a][b][q] = 0.0f;
+    if (ks0 < ks1) {
+        mfma_stage(F, rowbytes, row0, r0, r1, ks0 * KM, mlds_buf, tid);
+        mfma_stage(F, rowbytes, col0, c0, c1, ks0 * KM, mlds_buf + MOPB, tid);
+    }
+    for (int64_t ks = ks0; ks < ks1; ks++) {
+        const int st = (int)((ks - ks0) & 1);
+        const unsigned char* A = mlds_buf + st * (2 * MOPB);
+        const unsigned char* B = A + MOPB;
+        if (ks + 1 < ks1) {
+            unsigned char* An = mlds_buf + (st ^ 1) * (2 * MOPB);
+            mfma_stage(F, rowbytes, row0, r0, r1, (ks + 1) * KM, An, tid);
+            mfma_stage(F, rowbytes, col0, c0, c1, (ks + 1) * KM, An + MOPB, tid);
+            asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");   // stage ks landed everywhere
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+#pragma unroll
+        for (int kk = 0; kk < KM; kk++) {
+            v4i_t af[2], bf[4];
+#pragma unroll
+            for (int a = 0; a < 2; a++)
+                af[a] = *reinterpret_cast<const v4i_t*>(A + mlds(wr * 64 + a * 32 + r, 2 * kk + h));
+#pragma unroll
+            for (int b = 0; b < 4; b++)
+                bf[b] = *reinterpret_cast<const v4i_t*>(B + mlds(wc * 128 + b * 32 + r, 2 * kk + h));
+#pragma unroll
+            for (int a = 0; a < 2; a++)
+#pragma unroll
+                for (int b = 0; b < 4; b++) {
+                    const v8i_t av = {af[a][0], af[a][1], af[a][2], af[a][3], 0, 0, 0, 0};
+                    const v8i_t bv = {bf[b][0], bf[b][1], bf[b][2], bf[b][3], 0, 0, 0, 0};
+                    acc[a][b] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(av, bv, acc[a][b], 4, 4, 0, 0, 0, 0);
+                }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // stage free for the next DMA
+    }
+    // D of block (a, b): row (q & 3) + 8 (q >> 2) + 4 h of the block, column r
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 4; b++)
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                const int64_t i = row0 + wr * 64 + a * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+                const int64_t j = col0 + wc * 128 + b * 32 + r;
+                const int v = (int)acc[a][b][q];
+                if (v && i < r1 && j < c1 && !(upper && j <= i)) atomicAdd(I + (i - r0) * ldI + (j - c0), v);
+            }
+}
+
 // Self pairs: |A ∩ A| = |A|. The pruned dictionary drops kmers held by one
 // set only, so the bitset count of a self pair misses them; take |A|.
 __global__ void self_pairs_kernel(const int64_t* __restrict__ off, int64_t lo, int64_t hi, int64_t r0, int64_t c0,
@@ -1883,6 +2028,8 @@ double sorted_cost_s(const gdist_sets* s, double pairs) {
 void free_bitsets(gdist_sets* s) {
     free_sparse(s);                      // (synchronises both streams, clears plans and graphs)
     free_variant(s);
+    s->fp4.release();
+    s->fp4_W = 0;
     s->bits.release();
     s->post_off.release();
     s->post_sets.release();
@@ -1920,7 +2067,11 @@ static MatrixPlan& matrix_plan(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, 
     // ---- the region's launch plan (built once, then reused)
     // the key holds every option the plan (and the sparse plan in it) reads,
     // so that changing one builds a new plan instead of reusing a stale one
-    const std::vector<int64_t> key{r0, r1, c0, c1, upper ? 1 : 0, split_diag ? 1 : 0, max_rr, tW,
+    // the dense tiles on the matrix cores (FP4 MFMA) when there are enough
+    // words to amortise a 256 x 256 tile's stages (option bitset_mfma 0: the
+    // AND+popcount tiles)
+    const bool use_mfma = tW >= kMfmaMinWords && ctx->option(OPT_BITSET_MFMA, 1) != 0;
+    const std::vector<int64_t> key{r0, r1, c0, c1, upper ? 1 : 0, split_diag ? 1 : 0, max_rr, tW, use_mfma ? 1 : 0,
                                    ctx->option(OPT_SPARSE_RARE, 1), ctx->option(OPT_SPARSE_CHUNKS, -1),
                                    ctx->option(OPT_SPARSE_PART_BUDGET, -1), ctx->option(OPT_SPARSE_WG_PER_CU, -1),
                                    ctx->option(OPT_SPARSE_XCD, 0)};
@@ -1955,6 +2106,34 @@ static MatrixPlan& matrix_plan(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, 
                 grp[g].push_back(make_int2(a, b));
             }
         for (int g = 0; g < 4; g++) p.at[g + 1] = p.at[g] + grp[g].size();
+        if (use_mfma) {
+            // the MFMA tiles: 256 x 256 from (r0, c0), those holding a pair of the region
+            std::vector<int2> mt;
+            const int tm = (int)ceil_div(nr, MT), tn = (int)ceil_div(c1 - c0, MT);
+            for (int a = 0; a < tm; a++)
+                for (int b = 0; b < tn; b++) {
+                    const int64_t rmin = r0 + (int64_t)a * MT;
+                    const int64_t cmax = std::min<int64_t>(c1, c0 + (int64_t)(b + 1) * MT) - 1;
+                    if (upper && cmax <= rmin) continue;
+                    mt.push_back(make_int2(a, b));
+                }
+            p.nmt = (int64_t)mt.size();
+            p.mtiles.alloc(mt.size() * sizeof(int2) + 8, st);
+            if (!mt.empty()) h2d(p.mtiles.p, mt.data(), mt.size() * sizeof(int2), st);
+            // the operand as FP4 nibbles, once per collection (the plan is
+            // built outside a graph capture; free_bitsets / free_sparse drop it)
+            if (s->fp4_W != tW) {
+                GD_REQUIRE(!ctx->capturing, "FP4 operand built inside a capture");
+                gdist_sets* ms = const_cast<gdist_sets*>(s);
+                const unsigned long long* tb = s->sparse ? s->dbits.as<unsigned long long>()
+                                                         : s->bits.as<unsigned long long>();
+                ms->fp4.alloc((size_t)s->nsets * tW * 32 + 64, st);
+                fp4_expand_kernel<<<grid_for(s->nsets * tW, 256, 256 * 256), 256, 0, st>>>(
+                    tb, s->nsets * tW, ms->fp4.as<uint4>());
+                GD_HIP(hipGetLastError());
+                ms->fp4_W = tW;
+            }
+        }
         p.tiles.alloc(p.at[4] * sizeof(int2) + 8, st);
         for (int g = 0; g < 4; g++)
             if (!grp[g].empty()) h2d(p.tiles.as<int2>() + p.at[g], grp[g].data(), grp[g].size() * sizeof(int2), st);
@@ -2064,7 +2243,21 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
         const int2* dg = p.tiles.as<int2>();
         const size_t* at = p.at;
         FamilyTimer ft(ctx, GDIST_KERNEL_DENSE, st);
-        {
+        if (p.nmt > 0) {
+            // FP4 MFMA tiles: one 128 KiB workgroup per CU; K split so that
+            // the grid fills ~4 rounds of the chip, each split >= 8 stages
+            const int64_t nst = tW / KM;
+            const int msp = (int)std::max<int64_t>(
+                1, std::min<int64_t>(std::max<int64_t>(1, nst / 8), ceil_div((int64_t)ctx->cus * 4, p.nmt)));
+            const int64_t mgrid = p.nmt * msp;
+            GD_REQUIRE(mgrid < (int64_t(1) << 31), "MFMA tile grid too large");
+            GD_REQUIRE(s->fp4_W == tW, "FP4 operand missing");
+            GD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&bitset_mfma_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 4 * MOPB));
+            bitset_mfma_kernel<<<(unsigned)mgrid, MNT, 4 * MOPB, st>>>(s->fp4.as<unsigned char>(), tW,
+                                                                       p.mtiles.as<int2>(), (int)p.nmt, msp, nst,
+                                                                       r0, r1, c0, c1, upper ? 1 : 0, d_I, ldI);
+        } else {
             launch(bitset_tile_kernel2<false>, dg, at[1]);
             launch(bitset_tile_kernel2<true>, dg + at[1], at[2] - at[1]);
             auto partial = [&](auto off_k, auto diag_k) {

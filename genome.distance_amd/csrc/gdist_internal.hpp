@@ -149,6 +149,8 @@ struct StepGraph {
 };
 struct MatrixPlan {
     DevBuf tiles;                    // the four launch groups' tiles
+    DevBuf mtiles;                   // the MFMA tiles (256 x 256) of the region (option bitset_mfma)
+    int64_t nmt = 0;
     size_t at[5] = {0, 0, 0, 0, 0};  // group bounds
     int64_t corg = 0;
     int rr = 8;
@@ -216,6 +218,7 @@ struct Timing {
     X(SPARSE_XCD, "sparse_xcd")               /* 1: chunk c of every sparse tile on XCD c mod 8 */           \
     X(RARE_U16, "rare_u16")                   /* 0: 4-byte list members in the row-major rare walk */        \
     X(RARE_ROWS_THREADS, "rare_rows_threads") /* row-major rare walk: threads a workgroup (512 default, 256) */ \
+    X(BITSET_MFMA, "bitset_mfma")             /* 0: dense tiles by AND+popcount instead of FP4 MFMA */       \
     X(SORT_RADIX, "sort_radix")               /* 10: onesweep radix sorts of u64 keys in 10-bit passes (A/B) */\
     X(VARIANT, "variant")                     /* variant tier: 1 force, 0 off (default: by the dictionary) */ \
     X(VARIANT_DMIN, "variant_dmin")           /* sets holding a dense-tier kmer (default N / 10) */            \
@@ -347,6 +350,8 @@ struct gdist_sets {
     // complement-sparse words of the dense tier (sparse.hip)
     bool sparse = false;
     gdist::DevBuf dbits;                  // uint64 [nsets][Wd]: the dense words only (tile kernels)
+    gdist::DevBuf fp4;                    // the dense tile operand as FP4 nibbles [nsets][32 fp4_W] (MFMA tiles)
+    int64_t fp4_W = 0;
     int64_t Wd = 0;                       // dense words, padded to 16 (0: none)
     int64_t Ws = 0;                       // sparse words
     gdist::DevBuf sp_off;                 // int64 [ceil(nsets/128) * Ws + 1]: (set block, sparse word) -> entries

@@ -995,6 +995,8 @@ void free_sparse(gdist_sets* s) {
         (void)hipStreamSynchronize(s->ctx->side);
         (void)hipStreamSynchronize(s->ctx->stream);
     }
+    s->fp4.release();                     // the MFMA operand expands the dense words
+    s->fp4_W = 0;
     s->graphs.clear();
     s->plans.clear();
     s->dbits.release();

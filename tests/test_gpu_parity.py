@@ -835,6 +835,36 @@ def test_sparse_equals_dense_at_size(ctx, opts):
     assert np.array_equal(I[iu], oI[iu]) and bits_equal(D[iu], oD[iu])
 
 
+@pytest.mark.parametrize("mfma", [None, 0])
+@pytest.mark.parametrize("T", [0, 3])
+def test_dense_tiles_mfma_exact(ctx, opts, mfma, T):
+    """The dense tier's tiles on the matrix cores (FP4 MFMA, 256 x 256 pairs
+    a workgroup; default from 64 dense words) and by AND+popcount (option
+    bitset_mfma 0): counts and distances bit-exact against the oracle over
+    upper triangles, whole squares, rectangles, row blocks not aligned to a
+    tile, partial tiles and one row; dense-only (T = 0) and with rare lists."""
+    import gdist
+    opts(bitset_mfma=mfma, sparse=0)
+    n = 530
+    seqs = synth_sets(n, 3000, 0.10, 111, protein=True)
+    sets = gdist.KmerSets.from_sequences(seqs, 8, gdist.KmerType.PROT, 0, ctx)
+    _, W = sets.build_bitsets(rare_threshold=T)
+    assert W >= 64, W
+    off, codes = oracle_pack(seqs, 8, 1, 0)
+    for (r0, r1, c0, c1, up) in [(0, n, 0, n, True), (0, n, 0, n, False), (37, 300, 5, 510, False),
+                                 (256, 530, 0, n, True), (100, 357, 100, 357, True), (529, 530, 0, n, False)]:
+        I, D = sets.matrix((r0, r1), (c0, c1), upper=up, method=gdist.METHOD_BITSET)
+        eI, eD = oracle.matrix(off, codes, r0, r1, c0, c1, flags=0x100 if up else 0)
+        if up:
+            mask = np.fromfunction(lambda a, b: (c0 + b) > (r0 + a), (r1 - r0, c1 - c0))
+            I, D, eI, eD = I[mask], D[mask], eI[mask], eD[mask]
+        assert np.array_equal(I, eI), (mfma, T, r0, r1, c0, c1, up, np.flatnonzero(I != eI)[:5])
+        assert bits_equal(D, eD)
+    d = sets.row_query(77, [0, 529, 77, 300])
+    _, eD = oracle.matrix(off, codes, 77, 78, 0, n)
+    assert bits_equal(d, eD[0, [0, 529, 77, 300]])
+
+
 @pytest.mark.parametrize("fill", [None, 0, 4, 1])
 def test_fill_routes_on_sparse_sets(ctx, opts, fill):
     """C3-shaped proteomes (sets much smaller than the dictionary, T > N so
