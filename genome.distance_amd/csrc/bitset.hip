@@ -2252,8 +2252,12 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
             const int64_t mgrid = p.nmt * msp;
             GD_REQUIRE(mgrid < (int64_t(1) << 31), "MFMA tile grid too large");
             GD_REQUIRE(s->fp4_W == tW, "FP4 operand missing");
-            GD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&bitset_mfma_kernel),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 4 * MOPB));
+            static bool lds_set = false;      // once per process (128 KiB of dynamic LDS)
+            if (!lds_set) {
+                GD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&bitset_mfma_kernel),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 4 * MOPB));
+                lds_set = true;
+            }
             bitset_mfma_kernel<<<(unsigned)mgrid, MNT, 4 * MOPB, st>>>(s->fp4.as<unsigned char>(), tW,
                                                                        p.mtiles.as<int2>(), (int)p.nmt, msp, nst,
                                                                        r0, r1, c0, c1, upper ? 1 : 0, d_I, ldI);
