@@ -46,9 +46,12 @@ import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0               # MI355X_MICROARCH.md chip table (spec)
 # what bounds the sparse tile kernel (v6), from its PMC passes (profiles/r02/sparse6/)
-SPARSE_LIMITER = ("vector-memory issue and latency of the product walk, not HBM bandwidth: v6 walks 1x2 "
-                  "micro-tiles (one search + quotient per two products, 3 record loads), see "
-                  "profiles/r02/sparse6/pmc_v6.txt and DESIGN.md §4")
+SPARSE_LIMITER = ("latency of the product walk, not HBM bandwidth: each 1x2 micro-tile slot waits on three "
+                  "scattered 12-byte record loads and adds two LDS counters; round 4 cut its VALU per slot "
+                  "from ~47 to ~28 (ISA) for a 5 % shorter kernel (DESIGN.md §4)")
+# FP4 MFMA (block-scaled e2m1) dense peak, MI355X_MICROARCH.md chip table: ~10 PF
+# dense = 5 P bit-products/s for the dense tiles on the matrix cores
+MFMA_FP4_PEAK_TOPS = 10000.0
 # VALU ceiling of the bitset inner step, MEASURED (scripts/microbench/valu_popc.hip,
 # profiles/r01/valu_microbench.txt): an interleaved v_and_b32 + v_bcnt_u32_b32 stream
 # issues at most 6.17e11 wave-instructions/s chip-wide (v_bcnt is half rate:
@@ -445,17 +448,31 @@ def main():
             # LONGER of the two, each timed alone by HIP events on its stream.
             d_ms, r_ms = fam_ms.get("dense", 0.0), fam_ms.get("rare", 0.0)
             wp = pairs_rank * width_words / (d_ms * 1e-3) if d_ms > 0 else 0.0
-            tops = wp * 4 / 1e12
-            dense_roof = {"bound": "valu", "achieved": round(tops, 3), "peak": round(valu_peak, 3), "unit": "TOP/s",
-                          "frac": round(tops / valu_peak, 4), "traffic": pmc_traffic("bitset_tile_kernel2"),
-                          "kernel": "bitset_tile_kernel2 (dense tier tiles)", "kernel_avg_ms": round(d_ms, 4),
-                          "ops_per_pair": 4 * width_words,
-                          "note": "lane-ops of the dense tier (pairs x W word pairs x 4) / the dense tile launches' "
-                                  "own time; peak = measured and+bcnt issue ceiling "
-                                  "(profiles/r01/valu_microbench.txt)",
-                          "hbm_streaming_model": {"achieved": round(algo_bytes / (d_ms * 1e-3) / 1e9, 1) if d_ms else 0,
-                                                  "bytes_per_pair": bytes_per_pair,
-                                                  "note": "16*W B/pair (SURVEY 8d), operands reused from LDS"}}
+            tw = sparse_words["dense_words"] if sparse_words and sparse_words["sparse_words"] else width_words
+            mfma = tw >= 64 and ctx.option("bitset_mfma") != 0
+            if mfma:
+                # the dense tiles on the matrix cores: pairs x W x 64 bit-products x 2 ops
+                tops = pairs_rank * tw * 64 * 2 / (d_ms * 1e-3) / 1e12 if d_ms > 0 else 0.0
+                dense_roof = {"bound": "mfma", "achieved": round(tops, 1), "peak": MFMA_FP4_PEAK_TOPS,
+                              "unit": "TFLOP/s", "frac": round(tops / MFMA_FP4_PEAK_TOPS, 4),
+                              "traffic": pmc_traffic("bitset_mfma_kernel"),
+                              "kernel": "bitset_mfma_kernel (dense tier tiles, FP4 MFMA 32x32x64)",
+                              "kernel_avg_ms": round(d_ms, 4), "ops_per_pair": 128 * tw,
+                              "note": "algorithmic ops = pairs x W words x 64 bit-products x 2 (multiply + add) / "
+                                      "the dense tile launch's own time; peak = the FP4 dense MFMA rate "
+                                      "(MI355X_MICROARCH.md); the bits are e2m1 0.0 / 1.0 nibbles, sums exact in f32"}
+            else:
+                tops = wp * 4 / 1e12
+                dense_roof = {"bound": "valu", "achieved": round(tops, 3), "peak": round(valu_peak, 3), "unit": "TOP/s",
+                              "frac": round(tops / valu_peak, 4), "traffic": pmc_traffic("bitset_tile_kernel2"),
+                              "kernel": "bitset_tile_kernel2 (dense tier tiles)", "kernel_avg_ms": round(d_ms, 4),
+                              "ops_per_pair": 4 * width_words,
+                              "note": "lane-ops of the dense tier (pairs x W word pairs x 4) / the dense tile launches' "
+                                      "own time; peak = measured and+bcnt issue ceiling "
+                                      "(profiles/r01/valu_microbench.txt)",
+                              "hbm_streaming_model": {"achieved": round(algo_bytes / (d_ms * 1e-3) / 1e9, 1) if d_ms else 0,
+                                                      "bytes_per_pair": bytes_per_pair,
+                                                      "note": "16*W B/pair (SURVEY 8d), operands reused from LDS"}}
             roof = dense_roof
             v_ms = fam_ms.get("variant", 0.0)
             cands = [(d_ms, dense_roof)]
