@@ -1899,6 +1899,8 @@ void build_bitsets(gdist_ctx* ctx, gdist_sets* s, unsigned flags, int64_t rare_t
         locus_perm(ctx, key, U, perm);
         tr.mark("bitsets: locus order");
     }
+    s->fp4.release();                    // the MFMA operand expanded the old bits
+    s->fp4_W = 0;
     s->bits.alloc((size_t)s->nsets * W * 8 + 8, ctx->stream);
     DevBuf recs(mass * 8 + 8, ctx->stream);
     int64_t written = 0;

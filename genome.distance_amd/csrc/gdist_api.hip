@@ -1479,6 +1479,8 @@ int gdist_sets_allgather_bitsets(gdist_ctx* ctx, const gdist_sets* local, unsign
         auto* s = new gdist_sets();
         s->ctx = ctx; s->kind = local->kind; s->k = local->k; s->flags = local->flags;
         s->nsets = N; s->has_codes = false;
+        s->fp4.release();                    // the MFMA operand expanded the old bits
+        s->fp4_W = 0;
         s->bits.alloc((size_t)N * W * 8 + 8, st);
         if (xchg) {
             DevBuf gb((size_t)mxs * W * 8 * R + 8, st);

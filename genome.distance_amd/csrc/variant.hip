@@ -953,6 +953,8 @@ void build_variant_bitsets(gdist_ctx* ctx, gdist_sets* s, DevBuf& dict, DevBuf& 
         emasks.push_back(std::move(em));
         en.push_back(ne);
     };
+    s->fp4.release();                    // the MFMA operand expanded the old bits
+    s->fp4_W = 0;
     s->bits.alloc((size_t)N * Wd * 8 + 8, st);
     DevBuf recs(mass * 8 + 8, st);
     int64_t written = 0;
