@@ -2122,19 +2122,6 @@ static MatrixPlan& matrix_plan(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, 
             p.nmt = (int64_t)mt.size();
             p.mtiles.alloc(mt.size() * sizeof(int2) + 8, st);
             if (!mt.empty()) h2d(p.mtiles.p, mt.data(), mt.size() * sizeof(int2), st);
-            // the operand as FP4 nibbles, once per collection (the plan is
-            // built outside a graph capture; free_bitsets / free_sparse drop it)
-            if (s->fp4_W != tW) {
-                GD_REQUIRE(!ctx->capturing, "FP4 operand built inside a capture");
-                gdist_sets* ms = const_cast<gdist_sets*>(s);
-                const unsigned long long* tb = s->sparse ? s->dbits.as<unsigned long long>()
-                                                         : s->bits.as<unsigned long long>();
-                ms->fp4.alloc((size_t)s->nsets * tW * 32 + 64, st);
-                fp4_expand_kernel<<<grid_for(s->nsets * tW, 256, 256 * 256), 256, 0, st>>>(
-                    tb, s->nsets * tW, ms->fp4.as<uint4>());
-                GD_HIP(hipGetLastError());
-                ms->fp4_W = tW;
-            }
         }
         p.tiles.alloc(p.at[4] * sizeof(int2) + 8, st);
         for (int g = 0; g < 4; g++)
@@ -2253,7 +2240,18 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
                 1, std::min<int64_t>(std::max<int64_t>(1, nst / 8), ceil_div((int64_t)ctx->cus * 4, p.nmt)));
             const int64_t mgrid = p.nmt * msp;
             GD_REQUIRE(mgrid < (int64_t(1) << 31), "MFMA tile grid too large");
-            GD_REQUIRE(s->fp4_W == tW, "FP4 operand missing");
+            if (s->fp4_W != tW) {
+                // the operand as FP4 nibbles, once per set of bitsets (every
+                // rebuild of the bits drops it; a capture replays a call that
+                // ran uncaptured first, so the operand exists by then)
+                GD_REQUIRE(!ctx->capturing, "FP4 operand built inside a capture");
+                gdist_sets* ms = const_cast<gdist_sets*>(s);
+                ms->fp4.alloc((size_t)s->nsets * tW * 32 + 64, st);
+                fp4_expand_kernel<<<grid_for(s->nsets * tW, 256, 256 * 256), 256, 0, st>>>(
+                    tbits, s->nsets * tW, ms->fp4.as<uint4>());
+                GD_HIP(hipGetLastError());
+                ms->fp4_W = tW;
+            }
             static bool lds_set = false;      // once per process (128 KiB of dynamic LDS)
             if (!lds_set) {
                 GD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&bitset_mfma_kernel),
