@@ -9,6 +9,8 @@ mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 200 --timeout-method thread \
     -p no:cacheprovider -k "dense_tiles_mfma" > $O/mfma.log 2>&1
 rc=$?; tail -6 $O/mfma.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 120 python -u scripts/r04/mfma_diag.py > $O/mfma_diag.txt 2>&1
+rc=$?; cat $O/mfma_diag.txt; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 700 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_variant.py tests/test_gpu_fullsize.py -m gpu -x -q \
     --timeout 300 --timeout-method thread -p no:cacheprovider -k "not c4_full" > $O/tests.log 2>&1
 rc=$?; tail -3 $O/tests.log; [ $rc -eq 0 ] || exit $rc
