@@ -284,7 +284,10 @@ __device__ __forceinline__ unsigned long long hmix(unsigned long long x) {
     return x;
 }
 
-// inserts codes[0, n) with values tag | (perm ? perm[i] : i)
+// inserts codes[0, n) with values tag | (perm ? perm[i] : i). The code ~0
+// (64-bit codes: DNA k = 32's poly-T, 8-bit protein k = 8) is the empty
+// marker, so it lives out of band: tab[2 (mask + 1)] = 1 when present,
+// tab[2 (mask + 1) + 1] = its value
 __global__ void hash_insert_kernel(const uint64_t* __restrict__ codes, int64_t n, const uint32_t* __restrict__ perm,
                                    unsigned long long tag, unsigned long long* __restrict__ tab,
                                    unsigned long long mask) {
@@ -292,6 +295,11 @@ __global__ void hash_insert_kernel(const uint64_t* __restrict__ codes, int64_t n
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const unsigned long long code = codes[i];
         const unsigned long long val = tag | (perm ? (unsigned long long)perm[i] : (unsigned long long)i);
+        if (code == kHashEmpty) {
+            tab[2 * (mask + 1) + 1] = val;
+            tab[2 * (mask + 1)] = 1ull;
+            continue;
+        }
         unsigned long long slot = hmix(code) & mask;
         for (;;) {
             const unsigned long long prev = atomicCAS(tab + 2 * slot, kHashEmpty, code);
@@ -344,12 +352,16 @@ __global__ __launch_bounds__(256) void hash_probe_kernel(const uint64_t* __restr
         unsigned long long val = kHashEmpty;
         if (x < e) {
             const unsigned long long code = codes[x];
-            unsigned long long slot = hmix(code) & mask;
-            for (;;) {
-                const ulonglong2 kv = *reinterpret_cast<const ulonglong2*>(tab + 2 * slot);
-                if (kv.x == code) { val = kv.y; break; }
-                if (kv.x == kHashEmpty) break;
-                slot = (slot + 1) & mask;
+            if (code == kHashEmpty) {                          // out of band (hash_insert_kernel)
+                if (tab[2 * (mask + 1)] == 1ull) val = tab[2 * (mask + 1) + 1];
+            } else {
+                unsigned long long slot = hmix(code) & mask;
+                for (;;) {
+                    const ulonglong2 kv = *reinterpret_cast<const ulonglong2*>(tab + 2 * slot);
+                    if (kv.x == code) { val = kv.y; break; }
+                    if (kv.x == kHashEmpty) break;
+                    slot = (slot + 1) & mask;
+                }
             }
             pos[x - base] = (val != kHashEmpty && (val & kTagMask) == kPosTag) ? (uint32_t)(val & 0xFFFFFFFFull) : ~0u;
         }
@@ -771,8 +783,8 @@ void hash_fill(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_
     GD_HIP(hipMemsetAsync(bits, 0, (size_t)s->nsets * W * 8, st));
     int64_t cap = 2;
     while (cap < 2 * (U + Ur)) cap <<= 1;                   // load <= 1/2
-    DevBuf tab((size_t)cap * 16, st), rcnt(8, st);
-    GD_HIP(hipMemsetAsync(tab.p, 0xFF, (size_t)cap * 16, st));
+    DevBuf tab((size_t)cap * 16 + 16, st), rcnt(8, st);                // + the out-of-band slot of code ~0
+    GD_HIP(hipMemsetAsync(tab.p, 0xFF, (size_t)cap * 16 + 16, st));
     GD_HIP(hipMemsetAsync(rcnt.p, 0, 8, st));
     const unsigned long long mask = (unsigned long long)cap - 1;
     if (U) hash_insert_kernel<<<grid_for(U, 256, 256 * 64), 256, 0, st>>>(dict, U, perm, kPosTag,

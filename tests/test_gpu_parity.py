@@ -663,9 +663,13 @@ def test_k32_all_ones_code(ctx, strand):
         I, D = sets.matrix(method=m)
         assert np.array_equal(I, eI) and bits_equal(D, eD), m
     for keep in (False, True):
-        sets.build_bitsets(keep_singletons=keep)
-        I, D = sets.matrix(method=gdist.METHOD_BITSET)
-        assert np.array_equal(I, eI) and bits_equal(D, eD), keep
+        # every fill route: the hash fill's empty marker is the code ~0 itself
+        # (kept out of band), the windows, the sort
+        for fill in (None, 4, 0, 1):
+            with ctx.options(fill_sort=fill):
+                sets.build_bitsets(keep_singletons=keep)
+            I, D = sets.matrix(method=gdist.METHOD_BITSET)
+            assert np.array_equal(I, eI) and bits_equal(D, eD), (keep, fill)
     d = sets.row_query(1, list(range(24)))
     assert bits_equal(d, eD[1])
 
