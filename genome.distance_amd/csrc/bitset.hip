@@ -2171,7 +2171,11 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
         GD_REQUIRE(rgrid < (int64_t(1) << 31), "rare-tier grid too large");
         const size_t lds = (size_t)std::min<int64_t>(nc, RCH) * 4;
         FamilyTimer ft(ctx, GDIST_KERNEL_RARE, rs);
-        const bool wide = ctx->option(OPT_RARE_ROWS_THREADS, 512) != 256;
+        // threads a workgroup: the LDS counters allow 4 workgroups a CU up to
+        // 40 KiB (10,240 columns: C3), 2 beyond (C4's 64 KiB chunks); 32 waves
+        // a CU either way (option rare_rows_threads 256 / 512 / 1024)
+        const int64_t nt_opt = ctx->option(OPT_RARE_ROWS_THREADS, lds > 40 * 1024 ? 1024 : 512);
+        const int rt = nt_opt == 256 ? 256 : nt_opt == 1024 ? 1024 : 512;
         auto go = [&](auto kern, int nt, auto* members) {
             kern<<<(unsigned)rgrid, nt, lds, rs>>>(s->srare_off.as<int64_t>(), s->srare_ent.as<uint64_t>(),
                                                    s->srare_w.as<uint32_t>(), s->srare_skip.as<uint16_t>(), members,
@@ -2179,10 +2183,12 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
                                                    d_I, ldI);
         };
         if (s->post_sets16.p) {
-            if (wide) go(rare_rows_kernel<uint16_t, 512>, 512, s->post_sets16.as<uint16_t>());
+            if (rt == 1024) go(rare_rows_kernel<uint16_t, 1024>, 1024, s->post_sets16.as<uint16_t>());
+            else if (rt == 512) go(rare_rows_kernel<uint16_t, 512>, 512, s->post_sets16.as<uint16_t>());
             else go(rare_rows_kernel<uint16_t, 256>, 256, s->post_sets16.as<uint16_t>());
         } else {
-            if (wide) go(rare_rows_kernel<uint32_t, 512>, 512, s->post_sets.as<uint32_t>());
+            if (rt == 1024) go(rare_rows_kernel<uint32_t, 1024>, 1024, s->post_sets.as<uint32_t>());
+            else if (rt == 512) go(rare_rows_kernel<uint32_t, 512>, 512, s->post_sets.as<uint32_t>());
             else go(rare_rows_kernel<uint32_t, 256>, 256, s->post_sets.as<uint32_t>());
         }
         ft.end();

@@ -217,7 +217,7 @@ struct Timing {
     X(SPARSE_GROUPS, "sparse_groups")         /* 0: no group tier (clade patterns) in the sparse words */       \
     X(SPARSE_XCD, "sparse_xcd")               /* 1: chunk c of every sparse tile on XCD c mod 8 */           \
     X(RARE_U16, "rare_u16")                   /* 0: 4-byte list members in the row-major rare walk */        \
-    X(RARE_ROWS_THREADS, "rare_rows_threads") /* row-major rare walk: threads a workgroup (512 default, 256) */ \
+    X(RARE_ROWS_THREADS, "rare_rows_threads") /* row-major rare walk: threads a workgroup (256/512/1024; default by LDS) */ \
     X(BITSET_MFMA, "bitset_mfma")             /* 0: dense tiles by AND+popcount instead of FP4 MFMA */       \
     X(SORT_RADIX, "sort_radix")               /* 10: onesweep radix sorts of u64 keys in 10-bit passes (A/B) */\
     X(VARIANT, "variant")                     /* variant tier: 1 force, 0 off (default: by the dictionary) */ \

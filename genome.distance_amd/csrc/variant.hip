@@ -539,7 +539,7 @@ namespace {
 // entry's list position is kept in LDS between chunks (lists are sorted by
 // set), so a list is read once across all chunks and no chunk searches it.
 constexpr int VBATCH = 2048;
-__global__ __launch_bounds__(256) void variant_rows_kernel(const int64_t* __restrict__ soff,
+__global__ __launch_bounds__(1024) void variant_rows_kernel(const int64_t* __restrict__ soff,
                                                            const uint32_t* __restrict__ sent,
                                                            const uint32_t* __restrict__ vset,
                                                            const unsigned long long* __restrict__ vmask,
@@ -558,13 +558,13 @@ __global__ __launch_bounds__(256) void variant_rows_kernel(const int64_t* __rest
     const int64_t per = (re - rb + nsplit - 1) / nsplit;
     const int64_t xb = rb + per * split;
     const int64_t xe = xb + per < re ? xb + per : re;
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, nwv = (int)(blockDim.x >> 6);
     int32_t* row = I + (i - r0) * ldI - c0;                   // row[j] for column j
     for (int64_t bb = xb; bb < xe; bb += VBATCH) {
         const int nb = (int)(xe - bb < VBATCH ? xe - bb : VBATCH);
         // each entry's first list position at or past the row's first column
         // (upper: the members after the row's own entry)
-        for (int t = wv; t < nb; t += 4) {
+        for (int t = wv; t < nb; t += nwv) {
             const uint32_t e = sent[bb + t];
             int64_t y = upper ? (int64_t)e + 1 : (int64_t)vbeg[e];
             const int64_t ye = vend[e];
@@ -584,7 +584,7 @@ __global__ __launch_bounds__(256) void variant_rows_kernel(const int64_t* __rest
             __syncthreads();                                   // ypos written; previous chunk flushed
             for (int t = threadIdx.x; t < n; t += blockDim.x) cnt[t] = 0;
             __syncthreads();
-            for (int t = wv; t < nb; t += 4) {                 // a wave per entry
+            for (int t = wv; t < nb; t += nwv) {                 // a wave per entry
                 const uint32_t e = sent[bb + t];
                 const unsigned long long mi = vmask[e];
                 const int64_t ye = vend[e];
@@ -1103,7 +1103,9 @@ void variant_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1,
     const int64_t grid = units * nsplit;
     GD_REQUIRE(grid < (int64_t(1) << 31), "variant-tier grid too large");
     FamilyTimer ft(ctx, GDIST_KERNEL_VARIANT, rs);
-    variant_rows_kernel<<<(unsigned)grid, 256, 0, rs>>>(s->vs_off.as<int64_t>(), s->vs_ent.as<uint32_t>(),
+    // 1,024 threads: the walk is latency-bound and its 72 KiB of LDS allow two
+    // workgroups a CU, so 16 waves each fill the CU's 32 wave slots
+    variant_rows_kernel<<<(unsigned)grid, 1024, 0, rs>>>(s->vs_off.as<int64_t>(), s->vs_ent.as<uint32_t>(),
                                                         s->vw_set.as<uint32_t>(), s->vw_mask.as<unsigned long long>(),
                                                         s->vw_beg.as<uint32_t>(), s->vw_end.as<uint32_t>(), r0, r1, c0,
                                                         c1, nsplit, upper ? 1 : 0, d_I, ldI);
