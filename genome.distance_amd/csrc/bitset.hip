@@ -562,9 +562,11 @@ __global__ __launch_bounds__(NT, 4) void bitset_tile_kernel2(
 constexpr int MT = 256;                       // tile edge (sets)
 constexpr int64_t kMfmaMinWords = 64;         // dense words from which the MFMA tiles run (option bitset_mfma)
 constexpr int MNT = 512;                      // threads
-constexpr int KM = 4;                         // words per stage
-constexpr int MROW = KM * 32;                 // bytes per row per stage (128)
-constexpr int MOPB = MT * MROW;               // one operand's stage (32 KiB)
+// KM words per stage (4: 2 x 32 KiB a stage, 128 KiB double-buffered; 2:
+// 64 KiB, so a row-major rare workgroup fits beside it on a CU: option
+// bitset_mfma_km)
+template <int KM> constexpr int mrow() { return KM * 32; }          // bytes per row per stage
+template <int KM> constexpr int mopb() { return MT * mrow<KM>(); }  // one operand's stage
 typedef int v8i_t __attribute__((ext_vector_type(8)));
 typedef int v4i_t __attribute__((ext_vector_type(4)));
 typedef float v16f_t __attribute__((ext_vector_type(16)));
@@ -589,17 +591,24 @@ __global__ void fp4_expand_kernel(const unsigned long long* __restrict__ bits, i
     }
 }
 
-__device__ __forceinline__ int mlds(int g, int c) { return g * MROW + ((c ^ ((g >> 1) & 7)) << 4); }
+// chunk c (16 B) of row g: KM = 4 rows of 8 chunks, c ^ ((g >> 1) & 7); KM =
+// 2 rows of 4 chunks, c ^ ((g >> 2) & 3) (conflict-free ds_read_b128 either way)
+template <int KM> __device__ __forceinline__ int mslot(int g, int c) {
+    return KM == 4 ? (c ^ ((g >> 1) & 7)) : (c ^ ((g >> 2) & 3));
+}
+template <int KM> __device__ __forceinline__ int mlds(int g, int c) { return g * mrow<KM>() + (mslot<KM>(g, c) << 4); }
 
-// one operand's stage: 2048 chunks of 16 B, 4 per thread (lane-linear LDS,
-// the swizzle applied on the source address)
+// one operand's stage: 16-byte chunks, KM per thread (lane-linear LDS, the
+// swizzle applied on the source address)
+template <int KM>
 __device__ __forceinline__ void mfma_stage(const unsigned char* __restrict__ F, int64_t rowbytes, int64_t set0,
                                            int64_t lo, int64_t lim, int64_t w0, unsigned char* lds_op, int tid) {
+    constexpr int CPR = 2 * KM;                       // chunks per row
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
+    for (int i = 0; i < KM; i++) {
         const int q = i * MNT + tid;                  // 16-byte slot of the stage
-        const int g = q >> 3, sl = q & 7;
-        const int c = sl ^ ((g >> 1) & 7);            // the chunk this slot holds
+        const int g = q / CPR, sl = q % CPR;
+        const int c = mslot<KM>(g, sl);               // the chunk this slot holds (the swizzle is an involution)
         int64_t set = set0 + g;
         set = set < lim ? set : lim - 1;              // rows outside [lo, lim): clamped, masked at the end
         set = set >= lo ? set : lo;
@@ -609,11 +618,13 @@ __device__ __forceinline__ void mfma_stage(const unsigned char* __restrict__ F, 
     }
 }
 
+template <int KM>
 __global__ __launch_bounds__(MNT, 2) void bitset_mfma_kernel(
     const unsigned char* __restrict__ F, int64_t W, const int2* __restrict__ tiles, int ntiles, int splits,
     int64_t nstages, int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I,
     int64_t ldI) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char mlds_buf[];     // 2 stages x (A, B) = 128 KiB
+    extern __shared__ __attribute__((aligned(16))) unsigned char mlds_buf[];     // 2 stages x (A, B)
+    constexpr int MOPB = mopb<KM>();
     const int64_t G = gridDim.x, blk = blockIdx.x;
     const int64_t xcd = blk & 7, kq = blk >> 3, qg = G >> 3, rem = G & 7;
     const int64_t u = xcd * qg + (xcd < rem ? xcd : rem) + kq;
@@ -636,8 +647,8 @@ __global__ __launch_bounds__(MNT, 2) void bitset_mfma_kernel(
 #pragma unroll
             for (int q = 0; q < 16; q++) acc[a][b][q] = 0.0f;
     if (ks0 < ks1) {
-        mfma_stage(F, rowbytes, row0, r0, r1, ks0 * KM, mlds_buf, tid);
-        mfma_stage(F, rowbytes, col0, c0, c1, ks0 * KM, mlds_buf + MOPB, tid);
+        mfma_stage<KM>(F, rowbytes, row0, r0, r1, ks0 * KM, mlds_buf, tid);
+        mfma_stage<KM>(F, rowbytes, col0, c0, c1, ks0 * KM, mlds_buf + MOPB, tid);
     }
     for (int64_t ks = ks0; ks < ks1; ks++) {
         const int st = (int)((ks - ks0) & 1);
@@ -645,9 +656,10 @@ __global__ __launch_bounds__(MNT, 2) void bitset_mfma_kernel(
         const unsigned char* B = A + MOPB;
         if (ks + 1 < ks1) {
             unsigned char* An = mlds_buf + (st ^ 1) * (2 * MOPB);
-            mfma_stage(F, rowbytes, row0, r0, r1, (ks + 1) * KM, An, tid);
-            mfma_stage(F, rowbytes, col0, c0, c1, (ks + 1) * KM, An + MOPB, tid);
-            asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");   // stage ks landed everywhere
+            mfma_stage<KM>(F, rowbytes, row0, r0, r1, (ks + 1) * KM, An, tid);
+            mfma_stage<KM>(F, rowbytes, col0, c0, c1, (ks + 1) * KM, An + MOPB, tid);
+            if (KM == 4) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");   // stage ks landed everywhere
+            else asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
         } else {
             asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
         }
@@ -656,10 +668,10 @@ __global__ __launch_bounds__(MNT, 2) void bitset_mfma_kernel(
             v4i_t af[2], bf[4];
 #pragma unroll
             for (int a = 0; a < 2; a++)
-                af[a] = *reinterpret_cast<const v4i_t*>(A + mlds(wr * 64 + a * 32 + r, 2 * kk + h));
+                af[a] = *reinterpret_cast<const v4i_t*>(A + mlds<KM>(wr * 64 + a * 32 + r, 2 * kk + h));
 #pragma unroll
             for (int b = 0; b < 4; b++)
-                bf[b] = *reinterpret_cast<const v4i_t*>(B + mlds(wc * 128 + b * 32 + r, 2 * kk + h));
+                bf[b] = *reinterpret_cast<const v4i_t*>(B + mlds<KM>(wc * 128 + b * 32 + r, 2 * kk + h));
 #pragma unroll
             for (int a = 0; a < 2; a++)
 #pragma unroll
@@ -2074,6 +2086,7 @@ static MatrixPlan& matrix_plan(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, 
     // AND+popcount tiles)
     const bool use_mfma = tW >= kMfmaMinWords && ctx->option(OPT_BITSET_MFMA, 1) != 0;
     const std::vector<int64_t> key{r0, r1, c0, c1, upper ? 1 : 0, split_diag ? 1 : 0, max_rr, tW, use_mfma ? 1 : 0,
+                                   ctx->option(OPT_BITSET_MFMA_GROUP, 0),
                                    ctx->option(OPT_SPARSE_RARE, 1), ctx->option(OPT_SPARSE_CHUNKS, -1),
                                    ctx->option(OPT_SPARSE_PART_BUDGET, -1), ctx->option(OPT_SPARSE_WG_PER_CU, -1),
                                    ctx->option(OPT_SPARSE_XCD, 0)};
@@ -2110,15 +2123,22 @@ static MatrixPlan& matrix_plan(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, 
         for (int g = 0; g < 4; g++) p.at[g + 1] = p.at[g] + grp[g].size();
         if (use_mfma) {
             // the MFMA tiles: 256 x 256 from (r0, c0), those holding a pair of the region
+            // (option bitset_mfma_group G > 0: the tiles in blocks of G row
+            // tiles x 2G column tiles, so the ~32 consecutive tiles an XCD runs
+            // at once share G row panels and 2G column panels in its L2)
             std::vector<int2> mt;
             const int tm = (int)ceil_div(nr, MT), tn = (int)ceil_div(c1 - c0, MT);
-            for (int a = 0; a < tm; a++)
-                for (int b = 0; b < tn; b++) {
-                    const int64_t rmin = r0 + (int64_t)a * MT;
-                    const int64_t cmax = std::min<int64_t>(c1, c0 + (int64_t)(b + 1) * MT) - 1;
-                    if (upper && cmax <= rmin) continue;
-                    mt.push_back(make_int2(a, b));
-                }
+            const int gr = (int)std::max<int64_t>(1, ctx->option(OPT_BITSET_MFMA_GROUP, 0));
+            const int gc = ctx->option(OPT_BITSET_MFMA_GROUP, 0) > 0 ? 2 * gr : tn;
+            for (int a0 = 0; a0 < tm; a0 += gr)
+                for (int b0 = 0; b0 < tn; b0 += gc)
+                    for (int a = a0; a < std::min(tm, a0 + gr); a++)
+                        for (int b = b0; b < std::min(tn, b0 + gc); b++) {
+                            const int64_t rmin = r0 + (int64_t)a * MT;
+                            const int64_t cmax = std::min<int64_t>(c1, c0 + (int64_t)(b + 1) * MT) - 1;
+                            if (upper && cmax <= rmin) continue;
+                            mt.push_back(make_int2(a, b));
+                        }
             p.nmt = (int64_t)mt.size();
             p.mtiles.alloc(mt.size() * sizeof(int2) + 8, st);
             if (!mt.empty()) h2d(p.mtiles.p, mt.data(), mt.size() * sizeof(int2), st);
@@ -2241,7 +2261,8 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
         if (p.nmt > 0) {
             // FP4 MFMA tiles: one 128 KiB workgroup per CU; K split so that
             // the grid fills ~4 rounds of the chip, each split >= 8 stages
-            const int64_t nst = tW / KM;
+            const int km = ctx->option(OPT_BITSET_MFMA_KM, 4) == 2 ? 2 : 4;
+            const int64_t nst = tW / km;
             const int msp = (int)std::max<int64_t>(
                 1, std::min<int64_t>(std::max<int64_t>(1, nst / 8), ceil_div((int64_t)ctx->cus * 4, p.nmt)));
             const int64_t mgrid = p.nmt * msp;
@@ -2258,15 +2279,22 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
                 GD_HIP(hipGetLastError());
                 ms->fp4_W = tW;
             }
-            static bool lds_set = false;      // once per process (128 KiB of dynamic LDS)
+            static bool lds_set = false;      // once per process (up to 128 KiB of dynamic LDS)
             if (!lds_set) {
-                GD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&bitset_mfma_kernel),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 4 * MOPB));
+                GD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&bitset_mfma_kernel<4>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 4 * mopb<4>()));
+                GD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&bitset_mfma_kernel<2>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 4 * mopb<2>()));
                 lds_set = true;
             }
-            bitset_mfma_kernel<<<(unsigned)mgrid, MNT, 4 * MOPB, st>>>(s->fp4.as<unsigned char>(), tW,
-                                                                       p.mtiles.as<int2>(), (int)p.nmt, msp, nst,
-                                                                       r0, r1, c0, c1, upper ? 1 : 0, d_I, ldI);
+            if (km == 4)
+                bitset_mfma_kernel<4><<<(unsigned)mgrid, MNT, 4 * mopb<4>(), st>>>(
+                    s->fp4.as<unsigned char>(), tW, p.mtiles.as<int2>(), (int)p.nmt, msp, nst, r0, r1, c0, c1,
+                    upper ? 1 : 0, d_I, ldI);
+            else
+                bitset_mfma_kernel<2><<<(unsigned)mgrid, MNT, 4 * mopb<2>(), st>>>(
+                    s->fp4.as<unsigned char>(), tW, p.mtiles.as<int2>(), (int)p.nmt, msp, nst, r0, r1, c0, c1,
+                    upper ? 1 : 0, d_I, ldI);
         } else {
             launch(bitset_tile_kernel2<false>, dg, at[1]);
             launch(bitset_tile_kernel2<true>, dg + at[1], at[2] - at[1]);

@@ -839,16 +839,21 @@ def test_sparse_equals_dense_at_size(ctx, opts):
     assert np.array_equal(I[iu], oI[iu]) and bits_equal(D[iu], oD[iu])
 
 
-@pytest.mark.parametrize("mfma", [None, 0])
+@pytest.mark.parametrize("mfma", [None, "km2_group", 0])
 @pytest.mark.parametrize("T", [0, 3])
 def test_dense_tiles_mfma_exact(ctx, opts, mfma, T):
     """The dense tier's tiles on the matrix cores (FP4 MFMA, 256 x 256 pairs
     a workgroup; default from 64 dense words) and by AND+popcount (option
     bitset_mfma 0): counts and distances bit-exact against the oracle over
     upper triangles, whole squares, rectangles, row blocks not aligned to a
-    tile, partial tiles and one row; dense-only (T = 0) and with rare lists."""
+    tile, partial tiles and one row; dense-only (T = 0) and with rare lists;
+    2-word stages with the tiles in 2 x 4 blocks (options bitset_mfma_km,
+    bitset_mfma_group)."""
     import gdist
-    opts(bitset_mfma=mfma, sparse=0)
+    if mfma == "km2_group":
+        opts(bitset_mfma_km=2, bitset_mfma_group=2, sparse=0)
+    else:
+        opts(bitset_mfma=mfma, sparse=0)
     n = 530
     seqs = synth_sets(n, 3000, 0.10, 111, protein=True)
     sets = gdist.KmerSets.from_sequences(seqs, 8, gdist.KmerType.PROT, 0, ctx)
