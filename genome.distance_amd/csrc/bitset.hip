@@ -618,12 +618,29 @@ __device__ __forceinline__ void mfma_stage(const unsigned char* __restrict__ F, 
     }
 }
 
-template <int KM>
+// the wait at the top of a stage: every stage still in flight after it may stay
+// (g = glds per stage per thread: 2 KM); a counted vmcnt keeps the later stages'
+// DMAs going across the barrier (raw s_barrier, never __syncthreads, whose
+// fence would drain them)
+template <int G>
+__device__ __forceinline__ void mfma_wait(int later) {
+    switch (later) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(G) : "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * G) : "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(3 * G) : "memory"); break;
+    }
+}
+
+// NS stages in a ring (2: double buffering; 4 with KM = 2 in the same 128
+// KiB: three stages in flight while one is computed; option bitset_mfma_km)
+template <int KM, int NS>
 __global__ __launch_bounds__(MNT, 2) void bitset_mfma_kernel(
     const unsigned char* __restrict__ F, int64_t W, const int2* __restrict__ tiles, int ntiles, int splits,
     int64_t nstages, int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I,
     int64_t ldI) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char mlds_buf[];     // 2 stages x (A, B)
+    static_assert(NS >= 2 && NS <= 4, "stage ring of 2..4");
+    extern __shared__ __attribute__((aligned(16))) unsigned char mlds_buf[];     // NS stages x (A, B)
     constexpr int MOPB = mopb<KM>();
     const int64_t G = gridDim.x, blk = blockIdx.x;
     const int64_t xcd = blk & 7, kq = blk >> 3, qg = G >> 3, rem = G & 7;
@@ -646,23 +663,19 @@ __global__ __launch_bounds__(MNT, 2) void bitset_mfma_kernel(
         for (int b = 0; b < 4; b++)
 #pragma unroll
             for (int q = 0; q < 16; q++) acc[a][b][q] = 0.0f;
-    if (ks0 < ks1) {
-        mfma_stage<KM>(F, rowbytes, row0, r0, r1, ks0 * KM, mlds_buf, tid);
-        mfma_stage<KM>(F, rowbytes, col0, c0, c1, ks0 * KM, mlds_buf + MOPB, tid);
-    }
+    auto issue = [&](int64_t ks) {
+        unsigned char* An = mlds_buf + (int)((ks - ks0) % NS) * (2 * MOPB);
+        mfma_stage<KM>(F, rowbytes, row0, r0, r1, ks * KM, An, tid);
+        mfma_stage<KM>(F, rowbytes, col0, c0, c1, ks * KM, An + MOPB, tid);
+    };
+    for (int64_t k = ks0; k < ks1 && k < ks0 + NS - 1; k++) issue(k);
     for (int64_t ks = ks0; ks < ks1; ks++) {
-        const int st = (int)((ks - ks0) & 1);
-        const unsigned char* A = mlds_buf + st * (2 * MOPB);
+        const unsigned char* A = mlds_buf + (int)((ks - ks0) % NS) * (2 * MOPB);
         const unsigned char* B = A + MOPB;
-        if (ks + 1 < ks1) {
-            unsigned char* An = mlds_buf + (st ^ 1) * (2 * MOPB);
-            mfma_stage<KM>(F, rowbytes, row0, r0, r1, (ks + 1) * KM, An, tid);
-            mfma_stage<KM>(F, rowbytes, col0, c0, c1, (ks + 1) * KM, An + MOPB, tid);
-            if (KM == 4) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");   // stage ks landed everywhere
-            else asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-        }
+        if (ks + NS - 1 < ks1) issue(ks + NS - 1);
+        // stages issued after ks: min(NS - 1, ks1 - 1 - ks)
+        const int64_t later = ks1 - 1 - ks < NS - 1 ? ks1 - 1 - ks : NS - 1;
+        mfma_wait<2 * KM>((int)later);               // stage ks landed everywhere
 #pragma unroll
         for (int kk = 0; kk < KM; kk++) {
             v4i_t af[2], bf[4];
@@ -2279,22 +2292,20 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
                 GD_HIP(hipGetLastError());
                 ms->fp4_W = tW;
             }
-            static bool lds_set = false;      // once per process (up to 128 KiB of dynamic LDS)
-            if (!lds_set) {
-                GD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&bitset_mfma_kernel<4>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 4 * mopb<4>()));
-                GD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&bitset_mfma_kernel<2>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 4 * mopb<2>()));
-                lds_set = true;
-            }
-            if (km == 4)
-                bitset_mfma_kernel<4><<<(unsigned)mgrid, MNT, 4 * mopb<4>(), st>>>(
-                    s->fp4.as<unsigned char>(), tW, p.mtiles.as<int2>(), (int)p.nmt, msp, nst, r0, r1, c0, c1,
-                    upper ? 1 : 0, d_I, ldI);
-            else
-                bitset_mfma_kernel<2><<<(unsigned)mgrid, MNT, 4 * mopb<2>(), st>>>(
-                    s->fp4.as<unsigned char>(), tW, p.mtiles.as<int2>(), (int)p.nmt, msp, nst, r0, r1, c0, c1,
-                    upper ? 1 : 0, d_I, ldI);
+            // stage ring: KM words a stage x NS stages (option bitset_mfma_ns: 2..4
+            // with KM = 2; KM = 4 only double-buffered, 128 KiB either way)
+            const int ns = km == 4 ? 2 : (int)std::max<int64_t>(2, std::min<int64_t>(4, ctx->option(OPT_BITSET_MFMA_NS, 2)));
+            auto mlaunch = [&](auto kern, int lds_bytes) {
+                GD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes));
+                kern<<<(unsigned)mgrid, MNT, lds_bytes, st>>>(s->fp4.as<unsigned char>(), tW, p.mtiles.as<int2>(),
+                                                               (int)p.nmt, msp, nst, r0, r1, c0, c1, upper ? 1 : 0, d_I,
+                                                               ldI);
+            };
+            if (km == 4) mlaunch(&bitset_mfma_kernel<4, 2>, 2 * 2 * mopb<4>());
+            else if (ns == 4) mlaunch(&bitset_mfma_kernel<2, 4>, 4 * 2 * mopb<2>());
+            else if (ns == 3) mlaunch(&bitset_mfma_kernel<2, 3>, 3 * 2 * mopb<2>());
+            else mlaunch(&bitset_mfma_kernel<2, 2>, 2 * 2 * mopb<2>());
         } else {
             launch(bitset_tile_kernel2<false>, dg, at[1]);
             launch(bitset_tile_kernel2<true>, dg + at[1], at[2] - at[1]);

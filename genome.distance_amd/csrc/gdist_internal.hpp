@@ -220,6 +220,7 @@ struct Timing {
     X(RARE_ROWS_THREADS, "rare_rows_threads") /* row-major rare walk: threads a workgroup (256/512/1024; default by LDS) */ \
     X(BITSET_MFMA, "bitset_mfma")             /* 0: dense tiles by AND+popcount instead of FP4 MFMA */       \
     X(BITSET_MFMA_KM, "bitset_mfma_km")       /* MFMA tiles: words per stage (4 default, 2: 64 KiB of LDS) */ \
+    X(BITSET_MFMA_NS, "bitset_mfma_ns")       /* MFMA tiles with 2-word stages: stages in the ring (2..4) */    \
     X(BITSET_MFMA_GROUP, "bitset_mfma_group") /* MFMA tiles: G x 2G tile blocks in launch order (0: row-major) */ \
     X(SORT_RADIX, "sort_radix")               /* 10: onesweep radix sorts of u64 keys in 10-bit passes (A/B) */\
     X(VARIANT, "variant")                     /* variant tier: 1 force, 0 off (default: by the dictionary) */ \

@@ -839,7 +839,7 @@ def test_sparse_equals_dense_at_size(ctx, opts):
     assert np.array_equal(I[iu], oI[iu]) and bits_equal(D[iu], oD[iu])
 
 
-@pytest.mark.parametrize("mfma", [None, "km2_group", 0])
+@pytest.mark.parametrize("mfma", [None, "km2_group", "km2_ns3", "km2_ns4", 0])
 @pytest.mark.parametrize("T", [0, 3])
 def test_dense_tiles_mfma_exact(ctx, opts, mfma, T):
     """The dense tier's tiles on the matrix cores (FP4 MFMA, 256 x 256 pairs
@@ -847,11 +847,13 @@ def test_dense_tiles_mfma_exact(ctx, opts, mfma, T):
     bitset_mfma 0): counts and distances bit-exact against the oracle over
     upper triangles, whole squares, rectangles, row blocks not aligned to a
     tile, partial tiles and one row; dense-only (T = 0) and with rare lists;
-    2-word stages with the tiles in 2 x 4 blocks (options bitset_mfma_km,
-    bitset_mfma_group)."""
+    2-word stages with the tiles in 2 x 4 blocks, and rings of 3 and 4
+    stages (options bitset_mfma_km, bitset_mfma_group, bitset_mfma_ns)."""
     import gdist
     if mfma == "km2_group":
         opts(bitset_mfma_km=2, bitset_mfma_group=2, sparse=0)
+    elif mfma in ("km2_ns3", "km2_ns4"):                # 3 / 4 stages in the ring
+        opts(bitset_mfma_km=2, bitset_mfma_ns=int(mfma[-1]), sparse=0)
     else:
         opts(bitset_mfma=mfma, sparse=0)
     n = 530
