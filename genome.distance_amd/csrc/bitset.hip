@@ -2276,8 +2276,10 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
             // the grid fills ~4 rounds of the chip, each split >= 8 stages
             const int km = ctx->option(OPT_BITSET_MFMA_KM, 4) == 2 ? 2 : 4;
             const int64_t nst = tW / km;
-            const int msp = (int)std::max<int64_t>(
+            int msp = (int)std::max<int64_t>(
                 1, std::min<int64_t>(std::max<int64_t>(1, nst / 8), ceil_div((int64_t)ctx->cus * 4, p.nmt)));
+            if (ctx->has_option(OPT_BITSET_MFMA_SPLITS))      // A/B: a given K split
+                msp = (int)std::max<int64_t>(1, std::min<int64_t>(nst, ctx->option(OPT_BITSET_MFMA_SPLITS, 1)));
             const int64_t mgrid = p.nmt * msp;
             GD_REQUIRE(mgrid < (int64_t(1) << 31), "MFMA tile grid too large");
             if (s->fp4_W != tW) {

@@ -221,6 +221,7 @@ struct Timing {
     X(BITSET_MFMA, "bitset_mfma")             /* 0: dense tiles by AND+popcount instead of FP4 MFMA */       \
     X(BITSET_MFMA_KM, "bitset_mfma_km")       /* MFMA tiles: words per stage (4 default, 2: 64 KiB of LDS) */ \
     X(BITSET_MFMA_NS, "bitset_mfma_ns")       /* MFMA tiles with 2-word stages: stages in the ring (2..4) */    \
+    X(BITSET_MFMA_SPLITS, "bitset_mfma_splits") /* MFMA tiles: K splits a tile (default: ~4 rounds of the chip) */ \
     X(BITSET_MFMA_GROUP, "bitset_mfma_group") /* MFMA tiles: G x 2G tile blocks in launch order (0: row-major) */ \
     X(SORT_RADIX, "sort_radix")               /* 10: onesweep radix sorts of u64 keys in 10-bit passes (A/B) */\
     X(VARIANT, "variant")                     /* variant tier: 1 force, 0 off (default: by the dictionary) */ \

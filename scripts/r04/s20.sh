@@ -10,7 +10,9 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --ti
 rc=$?; tail -4 $O/mfma.log; [ $rc -eq 0 ] || exit $rc
 AB_OUT=r04s20/ab3 bash scripts/r04/ab.sh "--config c3 --steps 10 --warmup 2 $BASE" \
     "--config c3 --steps 10 --warmup 2 $BASE --opt bitset_mfma_km=2 --opt bitset_mfma_ns=4" \
-    "--config c3 --steps 10 --warmup 2 $BASE --opt bitset_mfma_km=2 --opt bitset_mfma_ns=3" || exit $?
+    "--config c3 --steps 10 --warmup 2 $BASE --opt bitset_mfma_km=2 --opt bitset_mfma_ns=3" \
+    "--config c3 --steps 10 --warmup 2 $BASE --opt bitset_mfma_splits=1" \
+    "--config c3 --steps 10 --warmup 2 $BASE --opt rare_overlap=0" || exit $?
 for v in "" "--opt bitset_mfma_km=2 --opt bitset_mfma_ns=4"; do
     timeout -k 10 300 python -u bench.py --config c4 --rows 0:1024 --force-exchange --steps 5 --warmup 1 --no-cpu-baseline $BASE $v \
         > $O/c4.json 2> $O/c4.err || exit $?
