@@ -37,7 +37,7 @@ timeout -k 10 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_V
     SQ_WAIT_INST_ANY SQ_WAVE_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $O/c3_sq -o run -- \
     python3 bench.py $A3 > $O/c3_sq.json 2> $O/c3_sq.err &&
 python3 scripts/pmc_summary.py $O/c3_sq --kernel rare_rows_kernel > $O/c3_sq.txt &&
-python3 scripts/pmc_summary.py $O/c3_sq --kernel bitset_tile_kernel2 >> $O/c3_sq.txt &&
+python3 scripts/pmc_summary.py $O/c3_sq --kernel bitset_mfma_kernel >> $O/c3_sq.txt &&
 timeout -k 10 60 scripts/microbench/fetch_calib > $O/calib.txt 2>&1 &&
 timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/calib_fetch -o run -- \
     scripts/microbench/fetch_calib > $O/calib_fetch.log 2>&1
