@@ -58,6 +58,8 @@ MFMA_FP4_PEAK_TOPS = 10000.0
 # 5.7e11 alone vs 1.06e12 for v_and). One 64-bit word pair = 4 wave-lane
 # instructions (2 and + 2 bcnt) -> 6.17e11 * 64 / 4 word pairs/s.
 VALU_WORDPAIR_PEAK = 6.17e11 * 64 / 4.0
+# chip-wide VALU issue ceiling for plain 32-bit ops (v_and_b32 stream, same microbenchmark)
+VALU_ISSUE_PEAK = 1.06e12
 # LDS read peak for ds_read_b32-class reads (ds_read2_b32 banks as two of them):
 # MI355X_MICROARCH.md §LDS, "≈75 TB/s for ds_read_b32" with every CU streaming.
 LDS_B32_PEAK_GBS = 75000.0
@@ -264,6 +266,8 @@ def main():
         rare = dict(zip(("threshold", "lists", "records"), sets.rare_info()))
         rare["kmers"] = sets.rare_kmers()
         sparse_words = dict(zip(("sparse_words", "dense_words", "entries"), sets.sparse_info()))
+        if sparse_words["sparse_words"]:
+            sparse_words["products"] = sets.sparse_pairs()
         vinfo = sets.variant_info()
         variant = dict(zip(("kmers", "words", "entries", "products"), vinfo)) if vinfo[0] else None
         mflag = gdist.METHOD_BITSET
@@ -383,6 +387,19 @@ def main():
             bytes_per_pair = 8.0 * cfg["width"]
         algo_bytes = pairs_rank * bytes_per_pair
 
+        def pmc_sq(kern):
+            """Per-launch SQ / TA counters of `kern` (profiles/pmc_<config>_sq.json,
+            scripts/pmc_sq_json.py) with the kernel variant they were taken on."""
+            fn = os.path.join(ROOT, "profiles", f"pmc_{args.config}_sq.json")
+            try:
+                with open(fn) as f:
+                    pmc = json.load(f)
+            except Exception:
+                return None
+            if pmc.get("config") == args.config and pmc.get("n") == N and pmc.get("kernel", "").startswith(kern):
+                return pmc
+            return None
+
         def pmc_traffic(kern):
             """HBM bytes per launch of `kern` from the committed PMC passes
             (profiles/pmc_<config>*.json: FETCH_SIZE x 2 + WRITE_SIZE), only a
@@ -411,7 +428,10 @@ def main():
             # once: its row block's and column block's entries (8 B complement
             # word + 1 B set) and their (block, word) offsets (2 x 8 B), one side
             # for a whole diagonal tile.
-            kname = "sparse_tile_kernel<3> (1x2 micro-tiles, the dense words folded in, the rare rows trailing)"
+            mt = options.get("sparse_mt", 2)
+            sun = options.get("sparse_sun", 3 if mt == 2 else 4)
+            kname = (f"sparse_tile_kernel<{sun},{mt}> ({'2x2' if mt == 2 else '1x2'} micro-tiles, the dense words "
+                     "folded in, the rare rows trailing)")
             nb = -(-N // 128)
             side = sparse["entries"] / nb * 9.0 + sparse["sparse_words"] * 16.0
             algo_sparse = 0.0
@@ -424,6 +444,25 @@ def main():
                     algo_sparse += side if whole_diag else 2.0 * side
             kms = sparse_k_ms if sparse_k_ms else k_avg_ms
             ach = algo_sparse / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
+            # VALU-issue roofline: the kernel's VALU
+            # wave-instructions per launch (committed SQ pass) over the chip's
+            # measured issue rate, against the live kernel time; per 64 of the
+            # walk's products (sum over sparse words of z (z - 1) / 2)
+            sq = pmc_sq("sparse_tile_kernel")
+            valu_issue = None
+            if sq and sparse.get("products"):
+                c = sq["counters_per_launch"]
+                valu = c.get("SQ_INSTS_VALU")
+                if valu:
+                    floor_ms = valu / VALU_ISSUE_PEAK * 1e3
+                    valu_issue = {"valu_per_launch": valu, "products": sparse["products"],
+                                  "valu_per_64_products": round(valu * 64 / sparse["products"], 2),
+                                  "issue_floor_ms": round(floor_ms, 4),
+                                  "frac": round(floor_ms / kms, 3) if kms > 0 else None,
+                                  "peak_wave_instr_per_s": VALU_ISSUE_PEAK,
+                                  "ta_busy_frac": (round(c["TA_TA_BUSY_sum"] / 256 / (c["GRBM_GUI_ACTIVE"] / 8), 3)
+                                                   if c.get("TA_TA_BUSY_sum") and c.get("GRBM_GUI_ACTIVE") else None),
+                                  "counters_from": sq.get("kernel"), "source": sq.get("source")}
             dense_ops = pairs_rank * width_words * 4 / (k_avg_ms * 1e-3) / 1e12 if k_avg_ms > 0 else 0.0
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("sparse_tile_kernel"),
@@ -435,6 +474,7 @@ def main():
                             "(option time_kernels, after the timed region; its trailing workgroups recount the "
                             "rare tier's pairs of the step); step_kernel_span_ms = HIP-event span of the timed "
                             "steps' launches (sparse tiles + rare rows, then the chunk reduce that stores I and D)",
+                    "valu_issue": valu_issue,
                     "dense_equivalent": {"lane_ops_per_s_T": round(dense_ops, 2),
                                          "x_dense_valu_ceiling": round(dense_ops / valu_peak, 2),
                                          "note": "the same pairs as AND+popcount over all W bitset words "

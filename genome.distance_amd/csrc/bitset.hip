@@ -1312,8 +1312,9 @@ __device__ __forceinline__ int lds_lower_bound(const uint64_t* a, int n, uint64_
 // same-address atomics run at ~0.1 G/s — 84 of the fill's 112 ms.
 constexpr int kRareBuf = 256;
 struct WaveRareBuf {
-    unsigned long long* buf;              // LDS [kRareBuf]
+    unsigned long long* buf;              // LDS [cap]
     int n;                                // records staged (wave-uniform)
+    int cap;
 };
 __device__ __forceinline__ void rare_flush(WaveRareBuf& rb, unsigned long long* __restrict__ rare_out,
                                            unsigned long long* __restrict__ rare_cnt, int64_t rare_cap) {
@@ -1336,7 +1337,7 @@ __device__ __forceinline__ void append_rare(bool rhit, int64_t q, int64_t set, i
     const unsigned long long m = __ballot(rhit);
     if (!m) return;
     const int c = __popcll(m);
-    if (rb.n + c > kRareBuf) rare_flush(rb, rare_out, rare_cnt, rare_cap);
+    if (rb.n + c > rb.cap) rare_flush(rb, rare_out, rare_cnt, rare_cap);
     if (rhit) {
         const int lane = threadIdx.x & 63;
         rb.buf[rb.n + __popcll(m & ((1ull << lane) - 1))] =
@@ -1358,7 +1359,7 @@ __global__ __launch_bounds__(64) void fill_pos_kernel(
     __shared__ uint64_t s_mk[kPosSeg];
     __shared__ unsigned long long s_rb[kRareBuf];
     const int lane = threadIdx.x;
-    WaveRareBuf rb{s_rb, 0};
+    WaveRareBuf rb{s_rb, 0, kRareBuf};
     for (int64_t sg = blockIdx.x; sg < ns; sg += gridDim.x) {
     __syncthreads();                                      // the previous segment's LDS reads are done
     const int64_t wv = lane < 6 ? win[sg * 8 + lane] : 0;
@@ -1448,6 +1449,134 @@ __global__ __launch_bounds__(64) void fill_pos_kernel(
     rare_flush(rb, rare_out, rare_cnt, rare_cap);
 }
 
+// The default pass 1 (round 4): a 256-thread workgroup per segment of up to
+// kMSeg codes. fill_pos_kernel above runs one wave with 17 KiB of LDS, so a
+// CU holds ~9 waves and each waits out its own global and LDS latency chains
+// (C2: 21 ms per 2^30 codes). Here four waves share one staged window: the
+// dense window (padded one entry in 8 so that lanes whose ranks sit ~8 apart
+// spread over the banks instead of 16 to a bank) and the rare fences; a
+// thread takes 8 consecutive codes (one search, then the forward walk), its
+// bit positions are gathered from perm[] in global memory (8 independent
+// loads, no LDS copy), and each wave lists its misses as 16-bit offsets
+// (one list per wave: it cannot overflow) and stages its rare records in its
+// own buffer. ~37 KiB a workgroup: four workgroups, 16 waves, per CU.
+constexpr int kMNT = 256;
+constexpr int kMPT = 8;
+constexpr int kMSeg = kMNT * kMPT;           // 2048 codes
+constexpr int kMWin = 2560;                  // dense window cap
+constexpr int kMFences = 1024;               // rare window cap kMFences x kRareBucket
+constexpr int kMWaveRare = 128;              // rare records staged per wave
+__device__ __forceinline__ int mpad(int r) { return r + (r >> 3); }
+__device__ __forceinline__ int lds_lower_bound_pad(const uint64_t* a, int lo, int n, uint64_t k) {
+    for (int len = n - lo; len > 0;) {
+        const int half = len >> 1;
+        if (a[mpad(lo + half)] < k) { lo += half + 1; len -= half + 1; } else len = half;
+    }
+    return lo;
+}
+__global__ __launch_bounds__(kMNT) void fill_merge_kernel(
+    const uint64_t* __restrict__ codes, const int64_t* __restrict__ win, int64_t ns, const uint64_t* __restrict__ dict,
+    const uint64_t* __restrict__ rare, int64_t base, uint32_t* __restrict__ pos_out, int64_t id_base,
+    unsigned long long* __restrict__ rare_out, unsigned long long* __restrict__ rare_cnt, int64_t rare_cap,
+    const uint32_t* __restrict__ perm) {
+    constexpr int NW = kMNT / 64, WC = kMSeg / NW;
+    __shared__ uint64_t s_d[kMWin + kMWin / 8];
+    __shared__ uint64_t s_f[kMFences];
+    __shared__ uint16_t s_mi[NW][WC];
+    __shared__ unsigned long long s_rb[NW][kMWaveRare];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    WaveRareBuf rb{s_rb[wv], 0, kMWaveRare};
+    for (int64_t sg = blockIdx.x; sg < ns; sg += gridDim.x) {
+        const int64_t* w = win + sg * 8;
+        const int64_t dlo = w[0], dhi = w[1], rlo = w[2], rhi = w[3];
+        const uint64_t sd = (uint64_t)w[4];
+        const int64_t e = w[5];
+        const int64_t set = (int64_t)(sd >> 40), b = (int64_t)(sd & ((1ull << 40) - 1));
+        const int64_t nd = dhi - dlo, nr = rhi - rlo, nf = (nr + kRareBucket - 1) / kRareBucket;
+        __syncthreads();                                  // the previous segment's LDS reads are done
+        if (nd <= kMWin && nf <= kMFences && e - b <= kMSeg) {
+            const int64_t i0 = b + (int64_t)kMPT * threadIdx.x;
+            uint64_t kk[kMPT];
+#pragma unroll
+            for (int j = 0; j < kMPT; j++) kk[j] = i0 + j < e ? codes[i0 + j] : 0;
+            for (int j = threadIdx.x; j < nd; j += kMNT) s_d[mpad(j)] = dict[dlo + j];
+            for (int j = threadIdx.x; j < nf; j += kMNT) s_f[j] = rare[rlo + (int64_t)j * kRareBucket];
+            __syncthreads();
+            const int n = (int)nd;
+            int r = i0 < e ? lds_lower_bound_pad(s_d, 0, n, kk[0]) : n;
+            int nm = 0;                                   // the wave's misses (uniform)
+            int rk[kMPT];
+            bool hit[kMPT];
+#pragma unroll
+            for (int j = 0; j < kMPT; j++) {
+                const bool valid = i0 + j < e;
+                hit[j] = false;
+                if (valid) {
+                    const uint64_t k = kk[j];
+                    if (r < n && s_d[mpad(r)] < k) {
+                        r++;
+                        if (r < n && s_d[mpad(r)] < k) r = lds_lower_bound_pad(s_d, r + 1, n, k);
+                    }
+                    hit[j] = r < n && s_d[mpad(r)] == k;
+                }
+                rk[j] = r;
+                const bool miss = valid && !hit[j];
+                const unsigned long long m = __ballot(miss);
+                if (miss) s_mi[wv][nm + __popcll(m & ((1ull << lane) - 1))] = (uint16_t)(i0 + j - b);
+                nm += __popcll(m);
+            }
+            uint32_t pv[kMPT];
+#pragma unroll
+            for (int j = 0; j < kMPT; j++)
+                pv[j] = hit[j] ? (perm ? perm[dlo + rk[j]] : (uint32_t)(dlo + rk[j])) : ~0u;
+#pragma unroll
+            for (int j = 0; j < kMPT; j++)
+                if (i0 + j < e) pos_out[i0 + j - base] = pv[j];
+            __builtin_amdgcn_wave_barrier();
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            for (int t0 = 0; t0 < nm; t0 += 64) {
+                bool rhit = false;
+                int64_t q = 0;
+                if (t0 + lane < nm && nf > 0) {
+                    const uint64_t k = codes[b + s_mi[wv][t0 + lane]];
+                    const int g = lds_lower_bound(s_f, (int)nf, k + 1) - 1;   // last fence <= k (k = ~0: the last fence)
+                    if (g >= 0 || k == ~0ull) {
+                        const int gg = g >= 0 ? g : (int)nf - 1;
+                        const int64_t q0 = rlo + (int64_t)gg * kRareBucket;
+                        uint64_t v[kRareBucket];
+#pragma unroll
+                        for (int u = 0; u < kRareBucket; u++) v[u] = q0 + u < rhi ? rare[q0 + u] : 0;
+#pragma unroll
+                        for (int u = 0; u < kRareBucket; u++)
+                            if (q0 + u < rhi && v[u] == k) { rhit = true; q = q0 + u; }
+                    }
+                }
+                append_rare(rhit, q, set, id_base, rb, rare_out, rare_cnt, rare_cap);
+            }
+            continue;
+        }
+        // fallback: each wave walks its share of the codes over the windows in global memory
+        int64_t dp = dlo, rp = rlo;
+        for (int64_t c0 = b + 64 * wv; c0 < e; c0 += kMNT) {
+            const int64_t i = c0 + lane;
+            const bool valid = i < e;
+            const uint64_t k = valid ? codes[i] : 0;
+            int64_t r;
+            bool hit;
+            wave_rank(dict, dp, dhi, k, valid, r, hit);
+            if (valid) pos_out[i - base] = hit ? (perm ? perm[r] : (uint32_t)r) : ~0u;
+            const bool miss = valid && !hit;
+            if (__ballot(miss) && rp < rhi) {
+                int64_t q;
+                bool rhit;
+                wave_rank(rare, rp, rhi, k, miss, q, rhit);
+                append_rare(rhit, q, set, id_base, rb, rare_out, rare_cnt, rare_cap);
+            }
+        }
+    }
+    rare_flush(rb, rare_out, rare_cnt, rare_cap);
+}
+
 __device__ __forceinline__ void pos_or(uint32_t* lds, uint32_t p, uint32_t sb) {
     const uint32_t x = (p >> 5) - sb;   // ~0 positions and other slices wrap to >= kPosSlice
     if (x < (uint32_t)kPosSlice) atomicOr(lds + x, 1u << (p & 31));
@@ -1518,7 +1647,8 @@ void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_
     // even at 64 codes (dictionary entries per code of a set >= 12 dense or
     // >= 32 rare): every segment would walk global memory. The hash fill
     // probes a table of the dictionary instead. Option fill_sort: 0 or 3 the
-    // windows, 1 the sort, 2 the atomics, 4 the hash.
+    // windows, 1 the sort, 2 the atomics, 4 the hash, 5 the windows one wave a
+    // segment (round 3's pass 1).
     const int64_t total = s->h_off[s->nsets];
     const double per_set = (double)total / (double)std::max<int64_t>(1, s->nsets);
     const bool sparse_sets = (double)U > 12.0 * per_set || (double)Ur > 32.0 * per_set;
@@ -1532,7 +1662,9 @@ void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_
     GD_HIP(hipMemsetAsync(bits, 0, (size_t)s->nsets * W * 8, st));
     DevBuf rcnt(8, st);
     GD_HIP(hipMemsetAsync(rcnt.p, 0, 8, st));
-    const int64_t mode = hook || opt == 3 || opt < 0 ? 0 : opt;      // the hook needs the position arrays
+    // the hook needs the position arrays; option 5: pass 1 by fill_pos_kernel (one wave a segment)
+    const int64_t mode = hook || opt == 3 || opt == 5 || opt < 0 ? 0 : opt;
+    const bool wave_fill = opt == 5;
     if (U + Ur > 0 && mode == 0) {
         GD_REQUIRE(s->nsets < (int64_t(1) << 23) && s->h_off[s->nsets] < (int64_t(1) << 40),
                    "collection too large for packed fill segments");
@@ -1542,9 +1674,10 @@ void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_
         for (int64_t i = 0; i < s->nsets; i++) {
             first[i] = (int64_t)seg.size();
             const double ni = (double)(s->h_off[i + 1] - s->h_off[i]);
-            const double fit = 0.8 * std::min(kWinDense * ni / (double)std::max<int64_t>(1, U),
-                                              kRareFences * kRareBucket * ni / (double)std::max<int64_t>(1, Ur));
-            const int64_t L = std::max<int64_t>(64, std::min<int64_t>(kPosSeg, (int64_t)(fit / 64) * 64));
+            const double wd = wave_fill ? kWinDense : kMWin, wf = wave_fill ? kRareFences : kMFences;
+            const double fit = 0.8 * std::min(wd * ni / (double)std::max<int64_t>(1, U),
+                                              wf * kRareBucket * ni / (double)std::max<int64_t>(1, Ur));
+            const int64_t L = std::max<int64_t>(64, std::min<int64_t>(wave_fill ? kPosSeg : kMSeg, (int64_t)(fit / 64) * 64));
             for (int64_t b = s->h_off[i]; b < s->h_off[i + 1]; b += L) seg.push_back((i << 40) | b);
         }
         first[s->nsets] = (int64_t)seg.size();
@@ -1567,11 +1700,26 @@ void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_
                 GD_HIP(hipGetLastError());
                 GD_REQUIRE(ns < (int64_t(1) << 31), "too many fill segments in one chunk");
                 // blocks take the segments in turn (a block's rare records staged across them)
-                const int64_t nblk = std::min<int64_t>(ns, (int64_t)ctx->cus * 32);
-                fill_pos_kernel<<<(unsigned)nblk, 64, 0, st>>>(s->codes.as<uint64_t>(), win.as<int64_t>(), ns, dict,
-                                                             rare, base, pos.as<uint32_t>(),
-                                                             id_base, rare_out, rcnt.as<unsigned long long>(),
-                                                             rare_cap, perm);
+                if (wave_fill) {
+                    const int64_t nblk = std::min<int64_t>(ns, (int64_t)ctx->cus * 32);
+                    fill_pos_kernel<<<(unsigned)nblk, 64, 0, st>>>(s->codes.as<uint64_t>(), win.as<int64_t>(), ns,
+                                                                 dict, rare, base, pos.as<uint32_t>(), id_base,
+                                                                 rare_out, rcnt.as<unsigned long long>(), rare_cap,
+                                                                 perm);
+                } else {
+                    // persistent: exactly the resident workgroups (a block that only
+                    // starts when a resident one exits would run its share at the end)
+                    static int per_cu = 0;
+                    if (!per_cu) {
+                        GD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fill_merge_kernel, kMNT, 0));
+                        per_cu = std::max(1, per_cu);
+                    }
+                    const int64_t nblk = std::min<int64_t>(ns, (int64_t)ctx->cus * per_cu);
+                    fill_merge_kernel<<<(unsigned)nblk, kMNT, 0, st>>>(s->codes.as<uint64_t>(), win.as<int64_t>(),
+                                                                       ns, dict, rare, base, pos.as<uint32_t>(),
+                                                                       id_base, rare_out,
+                                                                       rcnt.as<unsigned long long>(), rare_cap, perm);
+                }
                 GD_HIP(hipGetLastError());
             }
             tr.mark("fill: merged positions");

@@ -589,6 +589,13 @@ int gdist_sets_variant_info(const gdist_sets* s, int64_t* kmers, int64_t* words,
     });
 }
 
+int gdist_sets_sparse_pairs(const gdist_sets* s, double* pairs) {
+    return guard([&] {
+        check_sets(s);
+        if (pairs) *pairs = s->sparse ? s->sp_pairs : 0.0;
+    });
+}
+
 int gdist_sets_sparse_sides(const gdist_sets* s, int64_t* complement_words, int64_t* positive_words) {
     return guard([&] {
         check_sets(s);

@@ -189,7 +189,8 @@ struct Timing {
     X(SPARSE, "sparse")                       /* 0: no sparse words */                                         \
     X(SPARSE_ZMAX, "sparse_zmax")             /* words with z_w <= ZMAX are sparse (forces the split) */       \
     X(SPARSE_WG_PER_CU, "sparse_wg_per_cu")   /* chunking target of the sparse tiles (default 4) */            \
-    X(SPARSE_SUN, "sparse_sun")               /* slots per lane in flight: 2 / 3 / 4 (default 3) */            \
+    X(SPARSE_SUN, "sparse_sun")               /* slots per lane in flight: 2 / 3 / 4 (default 4) */            \
+    X(SPARSE_MT, "sparse_mt")                 /* off-diagonal micro-tiles: 1 (1 x 2) / 2 (2 x 2, default) */   \
     X(SKETCH_K, "sketch_k")                   /* sketch merge window (1 / 2 / 4 / 6, default 2) */             \
     X(SKETCH_TILE, "sketch_tile")             /* 16: force the 16x16 sketch tile */                            \
     X(SKETCH_V2, "sketch_v2")                 /* 0: the round-2 lane map and checked merge loop */             \
@@ -207,10 +208,10 @@ struct Timing {
     X(SPARSE_RARE, "sparse_rare")             /* 0: the rare pairs by the rare kernel, not the chunk reduce */ \
     X(SPARSE_FUSED, "sparse_fused")           /* 0: zeroing, rare kernel and epilogue as their own launches */ \
     X(SPARSE_FOLD, "sparse_fold")             /* most (padded) dense words counted in the sparse tile kernel */\
-    X(FILL_SORT, "fill_sort")                 /* bitset fill: 0/3 windows, 1 sort, 2 atomics, 4 hash (default: by size) */\
+    X(FILL_SORT, "fill_sort")                 /* bitset fill: 0/3 windows, 1 sort, 2 atomics, 4 hash, 5 one-wave windows (default: by size) */\
     X(PACK_SORT, "pack_sort")                 /* 1: two (code, set) pair sorts instead of packed keys */       \
     X(PACK_SUMMARY, "pack_summary")           /* 0: set|code pack keys, the bitset build re-sorts codes */     \
-    X(PACK_OVERLAP, "pack_overlap")           /* 0: upload first / 1: overlapped host thread / 2: registered */\
+    X(PACK_OVERLAP, "pack_overlap")           /* 0: upload first / 1: overlapped host thread / 2: registered / 3: pinned staging, 8 threads */\
     X(PACK_CHUNK, "pack_chunk")               /* kmer windows per pack chunk (default 2^28) */                 \
     X(EXCHANGE_BUDGET, "exchange_budget")     /* device bytes an exchange may use (default 0.8 x HBM) */    \
     X(PACK_CODES_BUDGET, "pack_codes_budget") /* bytes of the one-buffer pack (default 1/4 HBM; past it: grown) */\
@@ -379,6 +380,7 @@ struct gdist_sets {
     // chunk's summary; local_summary merges them instead of re-sorting codes
     std::vector<gdist::Summary> pack_sum;
     double sp_products = 0, sp_items = 0; // whole-triangle products / (tile, word) visits (cost model)
+    double sp_pairs = 0;                  // sum over the sparse words of z (z - 1) / 2: the walk's products
     // variant tier (variant.hip): kmers held by T .. Dmin - 1 sets in 64-kmer
     // words grouped by substitution; per word a list of (set, mask) entries,
     // sets ascending; the set -> entry CSR for the row walk

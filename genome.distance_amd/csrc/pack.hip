@@ -520,12 +520,19 @@ void exclusive_scan_i32_to_i64(gdist_ctx* ctx, const int32_t* in, int64_t* out, 
 // bytes move while chunk c sorts (chunk 0's wait is the part left on the
 // clock). Pieces, not one copy per chunk, so that the pack's own small
 // read-backs interleave with the upload.
+// Option pack_overlap 3: the chunk's range in kStagePiece pieces over
+// kStageThreads host threads, each with two pinned buffers and its own
+// stream: a thread copies piece p into one buffer (CPU memcpy) while the DMA
+// of its previous piece drains from the other, so the CPU copies run in
+// parallel and the link sees back-to-back page-locked transfers.
+constexpr int kStageThreads = 8;
+constexpr int64_t kStagePiece = int64_t(4) << 20;
 class ChunkUploader {
   public:
-    // pin: register each chunk's host range (page-locked, one DMA) instead of
-    // the runtime's staged pageable copies (option pack_overlap 2)
-    ChunkUploader(int device, const char* h, char* d, std::vector<std::pair<int64_t, int64_t>> ranges, bool pin)
-        : ready_(ranges.size()), pin_(pin) {
+    // mode 1: the runtime's staged pageable copies; 2: register each chunk's
+    // host range (page-locked, one DMA); 3: the threads above
+    ChunkUploader(int device, const char* h, char* d, std::vector<std::pair<int64_t, int64_t>> ranges, int mode)
+        : ready_(ranges.size()), pin_(mode == 2), staged_(mode == 3) {
         for (auto& p : ready_) got_.push_back(p.get_future());
         th_ = std::thread([this, device, h, d, ranges] { run(device, h, d, ranges); });
     }
@@ -537,7 +544,66 @@ class ChunkUploader {
 
   private:
     static constexpr int64_t kPiece = int64_t(64) << 20;
+    // one staging thread's share of [b0, b1): pieces t, t + T, ...
+    static void stage_range(int device, const char* h, char* d, int64_t b0, int64_t b1, int t, char* buf[2],
+                            hipStream_t us, hipEvent_t ev[2]) {
+        GD_HIP(hipSetDevice(device));
+        int k = 0;
+        for (int64_t o = b0 + (int64_t)t * kStagePiece; o < b1; o += (int64_t)kStageThreads * kStagePiece) {
+            const size_t len = (size_t)std::min(kStagePiece, b1 - o);
+            GD_HIP(hipEventSynchronize(ev[k]));           // this buffer's previous DMA is done
+            std::memcpy(buf[k], h + o, len);
+            GD_HIP(hipMemcpyAsync(d + o, buf[k], len, hipMemcpyHostToDevice, us));
+            GD_HIP(hipEventRecord(ev[k], us));
+            k ^= 1;
+        }
+        GD_HIP(hipStreamSynchronize(us));
+    }
+    void run_staged(int device, const char* h, char* d, const std::vector<std::pair<int64_t, int64_t>>& ranges) {
+        size_t c = 0;
+        char* buf[kStageThreads][2] = {};
+        hipStream_t us[kStageThreads] = {};
+        hipEvent_t ev[kStageThreads][2] = {};
+        try {
+            GD_HIP(hipSetDevice(device));
+            for (int t = 0; t < kStageThreads; t++) {
+                GD_HIP(hipStreamCreateWithFlags(&us[t], hipStreamNonBlocking));
+                for (int k = 0; k < 2; k++) {
+                    GD_HIP(hipHostMalloc(reinterpret_cast<void**>(&buf[t][k]), (size_t)kStagePiece, hipHostMallocDefault));
+                    GD_HIP(hipEventCreateWithFlags(&ev[t][k], hipEventDisableTiming));
+                    GD_HIP(hipEventRecord(ev[t][k], us[t]));
+                }
+            }
+            for (; c < ranges.size() && !stop_; c++) {
+                const int64_t b0 = ranges[c].first, b1 = ranges[c].second;
+                std::vector<std::future<void>> parts;
+                for (int t = 1; t < kStageThreads; t++)
+                    parts.push_back(std::async(std::launch::async, [&, t] {
+                        stage_range(device, h, d, b0, b1, t, buf[t], us[t], ev[t]);
+                    }));
+                stage_range(device, h, d, b0, b1, 0, buf[0], us[0], ev[0]);
+                for (auto& f : parts) f.get();                // rethrows a part's error
+                ready_[c].set_value();
+            }
+        } catch (...) {
+            for (; c < ranges.size(); c++) ready_[c].set_exception(std::current_exception());
+        }
+        for (int t = 0; t < kStageThreads; t++) {
+            if (us[t]) {
+                (void)hipStreamSynchronize(us[t]);
+                (void)hipStreamDestroy(us[t]);
+            }
+            for (int k = 0; k < 2; k++) {
+                if (ev[t][k]) (void)hipEventDestroy(ev[t][k]);
+                if (buf[t][k]) (void)hipHostFree(buf[t][k]);
+            }
+        }
+    }
     void run(int device, const char* h, char* d, const std::vector<std::pair<int64_t, int64_t>>& ranges) {
+        if (staged_) {
+            run_staged(device, h, d, ranges);
+            return;
+        }
         size_t c = 0;
         hipStream_t us = nullptr;
         try {
@@ -572,7 +638,7 @@ class ChunkUploader {
     }
     std::vector<std::promise<void>> ready_;
     std::vector<std::future<void>> got_;
-    bool pin_ = false;
+    bool pin_ = false, staged_ = false;
     std::atomic<bool> stop_{false};
     std::thread th_;
 };
@@ -641,7 +707,7 @@ void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_se
         } else {
             std::vector<std::pair<int64_t, int64_t>> ranges;
             for (auto& c : chunks) ranges.push_back({h_seq_off[c.first], h_seq_off[c.second]});
-            up.reset(new ChunkUploader(ctx->device, h_seqs, dst, std::move(ranges), ctx->option(OPT_PACK_OVERLAP, 1) == 2));
+            up.reset(new ChunkUploader(ctx->device, h_seqs, dst, std::move(ranges), (int)ctx->option(OPT_PACK_OVERLAP, 1)));
         }
     }
 

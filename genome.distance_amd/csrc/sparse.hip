@@ -681,10 +681,67 @@ __device__ __forceinline__ void sparse_off_slots(const int4* __restrict__ rec,
     }
 }
 
+// Off-diagonal 2 x 2 micro-tiles (option sparse_mt 2): ceil(nrow / 2) row
+// pairs x ncp column pairs per word, the same records and quotient as above
+// with the row pair's byte offset at xc << 5. Four products a slot from four
+// record loads (1 x 2: two from three), so the walk issues a third fewer
+// scattered loads per product (the texture address unit is its busiest unit:
+// TA ~63 % busy, VALU ~28 % of its issue rate, profiles/r04/s13). The row
+// pair's second row past an odd list is the next record: its products are
+// dropped by the first row's last-of-list flag (the column code, read with
+// the first row's 16 bytes). Not for row-trimmed tiles (rpart: a trimmed
+// list's last row is not its list's last).
+template <int SU>
+__device__ __forceinline__ void sparse_off22_slots(const int4* __restrict__ rec,
+                                                   const unsigned long long* __restrict__ masks, int W0, int last,
+                                                   int fb, int lane, const SparseWalk& e, uint32_t* __restrict__ cnt) {
+    int4 r[SU];
+    unsigned long long m[SU];
+    const unsigned long long* mk = masks + ((fb - W0) >> 6);
+#pragma unroll
+    for (int u = 0; u < SU; u++) m[u] = mk[u];
+#pragma unroll
+    for (int u = 0; u < SU; u++) r[u] = rec[slot_rec(last, fb + 64 * u, m[u])];
+    uint32_t ri[SU], ci[SU];
+#pragma unroll
+    for (int u = 0; u < SU; u++) {
+        const int q2 = 2 * (fb + 64 * u) + 2 * lane + r[u].x;
+        const float rcp = __int_as_float(r[u].w);
+        const int xc = (int)__builtin_fmaf((float)q2, rcp, rcp);
+        const int yc2 = q2 - (int)__umul24((uint32_t)xc, (uint32_t)r[u].w & 0xFFu);
+        ri[u] = (uint32_t)r[u].y + ((uint32_t)xc << 5);
+        ci[u] = (uint32_t)r[u].z + ((uint32_t)yc2 << 4);
+    }
+    uint4 a0[SU];
+    Rec3 a1[SU], b0[SU], b1[SU];                   // rows {row code, word (, column code)}, columns {word, column code}
+#pragma unroll
+    for (int u = 0; u < SU; u++) {
+        const char* pa = e.eA + ri[u];
+        const char* pb = e.eB + ci[u] + 4;
+        a0[u] = *reinterpret_cast<const uint4*>(pa);
+        a1[u] = *reinterpret_cast<const Rec3*>(pa + 16);
+        b0[u] = *reinterpret_cast<const Rec3*>(pb);
+        b1[u] = *reinterpret_cast<const Rec3*>(pb + 16);
+    }
+#pragma unroll
+    for (int u = 0; u < SU; u++) {
+        const uint32_t la = ~(uint32_t)__builtin_amdgcn_sbfe((int)a0[u].w, 5, 1);    // kLastOfList: bit 5
+        const uint32_t lb = ~(uint32_t)__builtin_amdgcn_sbfe((int)b0[u].c, 5, 1);
+        const uint32_t v00 = (uint32_t)(__popc(a0[u].y & b0[u].a) + __popc(a0[u].z & b0[u].b));
+        const uint32_t v01 = (uint32_t)(__popc(a0[u].y & b1[u].a) + __popc(a0[u].z & b1[u].b)) & lb;
+        const uint32_t v10 = (uint32_t)(__popc(a1[u].b & b0[u].a) + __popc(a1[u].c & b0[u].b)) & la;
+        const uint32_t v11 = (uint32_t)(__popc(a1[u].b & b1[u].a) + __popc(a1[u].c & b1[u].b)) & (la & lb);
+        cnt_add(cnt, a0[u].x, b0[u].c, v00);
+        cnt_add(cnt, a0[u].x, b1[u].c, v01);
+        cnt_add(cnt, a1[u].a, b0[u].c, v10);
+        cnt_add(cnt, a1[u].a, b1[u].c, v11);
+    }
+}
+
 // A batch's walk: windows of G groups of 64 slots (G a multiple of SUN):
 // the window's last-slot masks, then SUN groups per step while whole steps
 // remain, one group at a time after
-template <int SUN, bool DIAG>
+template <int SUN, int MODE>
 __device__ __forceinline__ void sparse_walk(const int4* __restrict__ rec, unsigned long long* __restrict__ masks,
                                             int last, int total, int lane, const SparseWalk& e,
                                             uint32_t* __restrict__ cnt, bool mirror) {
@@ -700,19 +757,21 @@ __device__ __forceinline__ void sparse_walk(const int4* __restrict__ rec, unsign
         const int wend = total < W0 + 64 * G ? total : W0 + 64 * G;
         int fb = W0;
         for (; fb + 64 * SUN <= wend; fb += 64 * SUN) {
-            if (DIAG) sparse_diag_slots<SUN>(rec, masks, W0, last, fb, lane, e, cnt, mirror);
-            else sparse_off_slots<SUN>(rec, masks, W0, last, fb, lane, e, cnt);
+            if (MODE == 0) sparse_diag_slots<SUN>(rec, masks, W0, last, fb, lane, e, cnt, mirror);
+            else if (MODE == 1) sparse_off_slots<SUN>(rec, masks, W0, last, fb, lane, e, cnt);
+            else sparse_off22_slots<SUN>(rec, masks, W0, last, fb, lane, e, cnt);
         }
         for (; fb < wend; fb += 64) {
-            if (DIAG) sparse_diag_slots<1>(rec, masks, W0, last, fb, lane, e, cnt, mirror);
-            else sparse_off_slots<1>(rec, masks, W0, last, fb, lane, e, cnt);
+            if (MODE == 0) sparse_diag_slots<1>(rec, masks, W0, last, fb, lane, e, cnt, mirror);
+            else if (MODE == 1) sparse_off_slots<1>(rec, masks, W0, last, fb, lane, e, cnt);
+            else sparse_off22_slots<1>(rec, masks, W0, last, fb, lane, e, cnt);
         }
         __builtin_amdgcn_wave_barrier();
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
     }
 }
 
-template <int SUN>
+template <int SUN, int MT>
 __global__ __launch_bounds__(SNT, 8) void sparse_tile_kernel(
     const int64_t* __restrict__ off, const ulonglong2* __restrict__ ent, const int32_t* __restrict__ nc, int64_t Us,
     int64_t Ws, const int2* __restrict__ tiles, const int32_t* __restrict__ cbnd, int nchunks, int64_t r0, int64_t r1,
@@ -751,6 +810,7 @@ __global__ __launch_bounds__(SNT, 8) void sparse_tile_kernel(
     const int rhi = (int)(r1 - A * SB < SB ? r1 - A * SB : SB);
     const bool rpart = rlo > 0 || rhi < SB;
     const bool diag = A == B && !rpart, mirror = diag && !upper;
+    const bool r22 = MT == 2 && !diag && !rpart;             // 2 x 2 micro-tiles
     for (int t = threadIdx.x; t < SB * SB / 2; t += SNT) cnt[t] = 0;
     __syncthreads();
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -785,7 +845,7 @@ __global__ __launch_bounds__(SNT, 8) void sparse_tile_kernel(
             }
         }
         const int ncd = diag ? ncl : (ncl + 1) >> 1;   // column pairs per row (off-diagonal micro-tiles)
-        const int P = diag ? nr * (nr - 1) / 2 : nr * ncd;
+        const int P = diag ? nr * (nr - 1) / 2 : (r22 ? (nr + 1) >> 1 : nr) * ncd;
         int incl = P;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -814,8 +874,9 @@ __global__ __launch_bounds__(SNT, 8) void sparse_tile_kernel(
         const int last = P > 0 ? incl - 1 : 0x7FFFFFFF;
         __builtin_amdgcn_wave_barrier();
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        if (diag) sparse_walk<SUN, true>(wrec, masks, last, total, lane, e, cnt, mirror);
-        else sparse_walk<SUN, false>(wrec, masks, last, total, lane, e, cnt, false);
+        if (diag) sparse_walk<SUN, 0>(wrec, masks, last, total, lane, e, cnt, mirror);
+        else if (MT == 2 && r22) sparse_walk<MT == 2 ? SUN : 1, 2>(wrec, masks, last, total, lane, e, cnt, false);
+        else sparse_walk<SUN, 1>(wrec, masks, last, total, lane, e, cnt, false);
     }
     if (ch < slabs) {
         // dense words [8 ch, 8 ch + 8) of the tile's 128 x 128 pairs: the
@@ -1010,7 +1071,7 @@ void free_sparse(gdist_sets* s) {
     s->sp_pos_words = 0;
     s->sp_fold_dense = false;
     s->sp_fold_slabs = 0;
-    s->sp_products = s->sp_items = 0.0;
+    s->sp_products = s->sp_items = s->sp_pairs = 0.0;
     s->sp_grp.release();
     s->sp_V.release();
     s->sp_T.release();
@@ -1180,12 +1241,12 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
     const double dense_word_s = pairs / kDenseWordPairsPerS;
     const int64_t zmax = ctx->option(OPT_SPARSE_ZMAX, 0);
     std::vector<int32_t> sw, dw;
-    double products = 0.0;
+    double products = 0.0, zpairs = 0.0;
     for (int64_t w = 0; w < Wv; w++) {
         const double zz = (double)z[w];
         const bool sparse = zm ? z[w] <= zmax
                                : 0.5 * zz * zz / kSparseProductsPerS + tiles / kSparseItemsPerS < dense_word_s;
-        if (sparse) { sw.push_back((int32_t)w); products += 0.5 * zz * zz; }
+        if (sparse) { sw.push_back((int32_t)w); products += 0.5 * zz * zz; zpairs += 0.5 * zz * (zz - 1.0); }
         else dw.push_back((int32_t)w);
     }
     const int64_t Ws = (int64_t)sw.size(), Wd = (int64_t)dw.size();
@@ -1337,6 +1398,7 @@ void build_sparse_words(gdist_ctx* ctx, gdist_sets* s) {
     s->sp_entries = total;
     s->sp_U = Us;
     s->sp_products = products;
+    s->sp_pairs = zpairs;
     s->sp_items = tiles * (double)Ws;
     tr.mark("sparse: entries + dense words");
 }
@@ -1491,13 +1553,17 @@ bool sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     if (sc.ntiles == 0) return false;
     const int nchunks = sc.nchunks;
     const int64_t nt = sc.ntiles;
-    // 3 slots (6 products) per lane in flight (C2 A/B, profiles/r02/sparse6/).
     // __launch_bounds__'s second argument is the minimum waves per SIMD: 8
     // holds the registers under the 8-wave budget (4 workgroups per CU,
     // LDS-limited; profiles/r01/sparse/occ_{3,8}.json)
-    const int sun = (int)ctx->option(OPT_SPARSE_SUN, 3);
+    // 2 x 2 micro-tiles, 3 slots (12 products) per lane in flight; 1 x 2 with
+    // 4 (C2 A/B, profiles/r04/s21/ab, r04/s13/ab_sun: 2 x 2 with 4 spills)
+    const int mt = (int)ctx->option(OPT_SPARSE_MT, 2);
+    const int sun = (int)ctx->option(OPT_SPARSE_SUN, mt == 2 ? 3 : 4);
     GD_REQUIRE(sun >= 2 && sun <= 4, "sparse_sun: 2, 3 or 4");
-    auto kern = sun == 2 ? sparse_tile_kernel<2> : sun == 4 ? sparse_tile_kernel<4> : sparse_tile_kernel<3>;
+    GD_REQUIRE(mt == 1 || mt == 2, "sparse_mt: 1 (1 x 2 micro-tiles) or 2 (2 x 2)");
+    auto kern = mt == 2 ? (sun == 2 ? sparse_tile_kernel<2, 2> : sun == 4 ? sparse_tile_kernel<4, 2> : sparse_tile_kernel<3, 2>)
+                        : (sun == 2 ? sparse_tile_kernel<2, 1> : sun == 4 ? sparse_tile_kernel<4, 1> : sparse_tile_kernel<3, 1>);
     // the rare tier's pairs of this step: the launch's trailing workgroups
     const bool rare = sc.use_part && sc.rare_in;
     FamilyTimer ft(ctx, GDIST_KERNEL_SPARSE, st);

@@ -111,6 +111,7 @@ _SIGS = {
     "gdist_sets_variant_info": (C.c_int, [_setp, _i64p, _i64p, _i64p, _dblp]),
     "gdist_sets_group_info": (C.c_int, [_setp, _i64p, _i64p]),
     "gdist_sets_sparse_sides": (C.c_int, [_setp, _i64p, _i64p]),
+    "gdist_sets_sparse_pairs": (C.c_int, [_setp, C.POINTER(C.c_double)]),
     "gdist_sets_bitset_info": (C.c_int, [_setp, _i64p, _i64p]),
     "gdist_sets_bitset_download": (C.c_int, [_setp, _u64p]),
     "gdist_sets_concat": (C.c_int, [_setp, _setp, C.POINTER(_setp)]),

@@ -416,6 +416,12 @@ class KmerSets(_Handle):
         L.check(L.lib.gdist_sets_sparse_sides(self.h, C.byref(a), C.byref(b)))
         return a.value, b.value
 
+    def sparse_pairs(self) -> float:
+        """The sparse tile kernel's products: sum over sparse words of z (z - 1) / 2."""
+        p = C.c_double()
+        L.check(L.lib.gdist_sets_sparse_pairs(self.h, C.byref(p)))
+        return p.value
+
     def rare_kmers(self) -> int:
         """Rare-tier kmers before identical posting lists were merged."""
         n = C.c_int64()

@@ -221,6 +221,11 @@ int  gdist_sets_variant_info(const gdist_sets* sets, int64_t* kmers, int64_t* wo
  * lacking a commonly held kmer) or from their words (sets holding a rarely
  * held one: positive-sparse). */
 int  gdist_sets_sparse_sides(const gdist_sets* sets, int64_t* complement_words, int64_t* positive_words);
+/* The sparse tile kernel's products over the whole collection: the sum over
+ * the sparse words of z (z - 1) / 2 (z = the word's entries), each pair of a
+ * word's entries once (0 without the split). Diagnostics: the bench line's
+ * VALU per 64 products. */
+int  gdist_sets_sparse_pairs(const gdist_sets* sets, double* pairs);
 /* The group tier of the sparse words: groups of sets (e.g.
  * the clades of a structured collection) whose members all carry the same
  * pattern in a word; those words keep per member only the residual entries

@@ -65,6 +65,7 @@ PACK_MODES = {"default": {}, "set_major": {"pack_summary": 0},
               "chunked": {"pack_chunk": 1000}, "chunked_set_major": {"pack_chunk": 1000, "pack_summary": 0},
               "chunked_no_overlap": {"pack_chunk": 1000, "pack_overlap": 0},
               "chunked_pinned": {"pack_chunk": 1000, "pack_overlap": 2},
+              "chunked_staged": {"pack_chunk": 1000, "pack_overlap": 3},
               # the codes buffer sized from the first chunk and grown (budget 0:
               # never the one buffer for every window)
               "grown": {"pack_chunk": 1000, "pack_codes_budget": 0},
@@ -140,6 +141,24 @@ def test_chunked_pack_bitset_matrix(ctx, opts, mode):
     I, D = sets.matrix(method=gdist.METHOD_BITSET)
     eI, eD = oracle.matrix(eo, ec, 0, 120, 0, 120)
     assert np.array_equal(I, eI) and bits_equal(D, eD)
+
+
+def test_pack_staged_upload_large(ctx):
+    """The pinned staging upload (option pack_overlap 3: 8 host threads, 4 MiB
+    pieces, two pinned buffers each) of ~48 MB in two chunks, one spanning
+    every thread's pieces and both ending mid-piece, packs the same codes as
+    the upload-first path."""
+    import gdist
+    rng = np.random.default_rng(5)
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    seqs = [rng.choice(acgt, 480_000 + 37 * i).tobytes() for i in range(100)]
+    got = {}
+    for ov in (0, 3):
+        with ctx.options(pack_overlap=ov, pack_chunk=1 << 25):
+            sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
+        got[ov] = sets.download()
+        sets.free()
+    assert np.array_equal(got[0][0], got[3][0]) and np.array_equal(got[0][1], got[3][1])
 
 
 def test_pack_rejects_unencodable_and_bad_k(ctx):
@@ -248,11 +267,11 @@ def test_large_segments_and_sentinel_code(ctx):
     assert np.array_equal(I2, eI) and bits_equal(D2, eD)
 
 
-@pytest.mark.parametrize("fill", [0, 1, 2])
+@pytest.mark.parametrize("fill", [0, 1, 2, 5])
 @pytest.mark.parametrize("keep", [False, True])
 def test_bitset_fill_ragged_sets(ctx, opts, fill, keep):
-    """The three bitset fills (merged positions + LDS row slices, the sort,
-    the one-pass atomics) on ragged sets: empty sets, two-code sets that span
+    """The bitset fills (merged positions + LDS row slices: one workgroup or
+    one wave a segment; the sort; the one-pass atomics) on ragged sets: empty sets, two-code sets that span
     the whole dictionary (the merge gallops), sets far larger than a fill
     segment at unaligned offsets, and the all-ones code."""
     import gdist
@@ -665,7 +684,7 @@ def test_k32_all_ones_code(ctx, strand):
     for keep in (False, True):
         # every fill route: the hash fill's empty marker is the code ~0 itself
         # (kept out of band), the windows, the sort
-        for fill in (None, 4, 0, 1):
+        for fill in (None, 4, 0, 5, 1):
             with ctx.options(fill_sort=fill):
                 sets.build_bitsets(keep_singletons=keep)
             I, D = sets.matrix(method=gdist.METHOD_BITSET)
@@ -731,9 +750,17 @@ SPARSE_MODES = {
     "no_locus": {"locus_order": 0, "sparse_zmax": 40}, "off": {"sparse": 0},
     # chunks flush with atomics (no partials within a zero budget)
     "atomic_flush": {"sparse_zmax": 100000, "sparse_part_budget": 0, "sparse_chunks": 5},
-    # 1 x 2 micro-tiles with 2 / 3 (default) / 4 slots per lane in flight
-    "rows_sun2": {"sparse_zmax": 40, "sparse_sun": 2},
-    "sun4": {"sparse_zmax": 100000, "sparse_sun": 4, "sparse_chunks": 7},
+    # 1 x 2 micro-tiles (option sparse_mt 1) with 2 / 3 / 4 slots per lane in flight
+    "rows_sun2": {"sparse_zmax": 40, "sparse_mt": 1, "sparse_sun": 2},
+    "sun4": {"sparse_zmax": 100000, "sparse_mt": 1, "sparse_sun": 4, "sparse_chunks": 7},
+    "sun3": {"sparse_zmax": 100000, "sparse_mt": 1, "sparse_sun": 3},
+    "mt1_default": {"sparse_mt": 1},
+    # 2 x 2 micro-tiles off the diagonal (default; row-trimmed tiles of the
+    # unaligned regions below keep 1 x 2) with 4 / 3 (default) / 2 slots
+    "mt2": {"sparse_zmax": 100000, "sparse_mt": 2, "sparse_sun": 4},
+    "mt2_sun3": {"sparse_zmax": 100000, "sparse_mt": 2, "sparse_sun": 3, "sparse_chunks": 7},
+    "mt2_sun2_atomic": {"sparse_zmax": 100000, "sparse_mt": 2, "sparse_sun": 2, "sparse_part_budget": 0,
+                        "sparse_chunks": 3},
     "sun2_atomic": {"sparse_zmax": 100000, "sparse_sun": 2, "sparse_part_budget": 0, "sparse_chunks": 3},
     # the dense words counted inside the tile kernel, 8 per chunk (partials / atomic flush),
     # or by their own tile launch
@@ -784,7 +811,8 @@ def test_sparse_complement_words_exact(ctx, mode, opts):
     sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
     _, W = sets.build_bitsets()
     ws, wd, ent = sets.sparse_info()
-    if mode in ("all_sparse", "atomic_flush", "many_chunks", "sun4", "sun2_atomic"):
+    if mode in ("all_sparse", "atomic_flush", "many_chunks", "sun4", "sun3", "sun2_atomic", "mt2", "mt2_sun3",
+                "mt2_sun2_atomic"):
         assert ws > 0 and wd == 0 and ent > 0
     elif mode in ("mixed", "mixed_slabs", "mixed_slabs_atomic", "mixed_tiles"):
         assert ws > 0 and wd > 0
@@ -876,7 +904,7 @@ def test_dense_tiles_mfma_exact(ctx, opts, mfma, T):
     assert bits_equal(d, eD[0, [0, 529, 77, 300]])
 
 
-@pytest.mark.parametrize("fill", [None, 0, 4, 1])
+@pytest.mark.parametrize("fill", [None, 0, 5, 4, 1])
 def test_fill_routes_on_sparse_sets(ctx, opts, fill):
     """C3-shaped proteomes (sets much smaller than the dictionary, T > N so
     the rare tier holds every shared kmer): the bitset fill by hash probes (the
