@@ -514,25 +514,20 @@ void exclusive_scan_i32_to_i64(gdist_ctx* ctx, const int32_t* in, int64_t* out, 
 // Overlapped upload of host sequence bytes: a host thread copies each pack
 // chunk's byte range on its own stream in 64 MiB pieces (the runtime's
 // pageable path, ~6 GB/s on the box: faster than our own pinned staging with
-// a CPU memcpy and than registering the range, both measured),
+// a CPU memcpy — one thread, or round 4's eight threads with two pinned 4 MiB
+// buffers each (pack 0.38-0.42 s vs 0.32-0.33 s, profiles/r04/s22/abs) — and
+// than registering the range, all measured),
 // synchronises, then signals the chunk; the
 // pack waits for chunk c's signal before its extraction, so chunk c + 1's
 // bytes move while chunk c sorts (chunk 0's wait is the part left on the
 // clock). Pieces, not one copy per chunk, so that the pack's own small
 // read-backs interleave with the upload.
-// Option pack_overlap 3: the chunk's range in kStagePiece pieces over
-// kStageThreads host threads, each with two pinned buffers and its own
-// stream: a thread copies piece p into one buffer (CPU memcpy) while the DMA
-// of its previous piece drains from the other, so the CPU copies run in
-// parallel and the link sees back-to-back page-locked transfers.
-constexpr int kStageThreads = 8;
-constexpr int64_t kStagePiece = int64_t(4) << 20;
 class ChunkUploader {
   public:
     // mode 1: the runtime's staged pageable copies; 2: register each chunk's
-    // host range (page-locked, one DMA); 3: the threads above
+    // host range (page-locked, one DMA)
     ChunkUploader(int device, const char* h, char* d, std::vector<std::pair<int64_t, int64_t>> ranges, int mode)
-        : ready_(ranges.size()), pin_(mode == 2), staged_(mode == 3) {
+        : ready_(ranges.size()), pin_(mode == 2) {
         for (auto& p : ready_) got_.push_back(p.get_future());
         th_ = std::thread([this, device, h, d, ranges] { run(device, h, d, ranges); });
     }
@@ -544,66 +539,7 @@ class ChunkUploader {
 
   private:
     static constexpr int64_t kPiece = int64_t(64) << 20;
-    // one staging thread's share of [b0, b1): pieces t, t + T, ...
-    static void stage_range(int device, const char* h, char* d, int64_t b0, int64_t b1, int t, char* buf[2],
-                            hipStream_t us, hipEvent_t ev[2]) {
-        GD_HIP(hipSetDevice(device));
-        int k = 0;
-        for (int64_t o = b0 + (int64_t)t * kStagePiece; o < b1; o += (int64_t)kStageThreads * kStagePiece) {
-            const size_t len = (size_t)std::min(kStagePiece, b1 - o);
-            GD_HIP(hipEventSynchronize(ev[k]));           // this buffer's previous DMA is done
-            std::memcpy(buf[k], h + o, len);
-            GD_HIP(hipMemcpyAsync(d + o, buf[k], len, hipMemcpyHostToDevice, us));
-            GD_HIP(hipEventRecord(ev[k], us));
-            k ^= 1;
-        }
-        GD_HIP(hipStreamSynchronize(us));
-    }
-    void run_staged(int device, const char* h, char* d, const std::vector<std::pair<int64_t, int64_t>>& ranges) {
-        size_t c = 0;
-        char* buf[kStageThreads][2] = {};
-        hipStream_t us[kStageThreads] = {};
-        hipEvent_t ev[kStageThreads][2] = {};
-        try {
-            GD_HIP(hipSetDevice(device));
-            for (int t = 0; t < kStageThreads; t++) {
-                GD_HIP(hipStreamCreateWithFlags(&us[t], hipStreamNonBlocking));
-                for (int k = 0; k < 2; k++) {
-                    GD_HIP(hipHostMalloc(reinterpret_cast<void**>(&buf[t][k]), (size_t)kStagePiece, hipHostMallocDefault));
-                    GD_HIP(hipEventCreateWithFlags(&ev[t][k], hipEventDisableTiming));
-                    GD_HIP(hipEventRecord(ev[t][k], us[t]));
-                }
-            }
-            for (; c < ranges.size() && !stop_; c++) {
-                const int64_t b0 = ranges[c].first, b1 = ranges[c].second;
-                std::vector<std::future<void>> parts;
-                for (int t = 1; t < kStageThreads; t++)
-                    parts.push_back(std::async(std::launch::async, [&, t] {
-                        stage_range(device, h, d, b0, b1, t, buf[t], us[t], ev[t]);
-                    }));
-                stage_range(device, h, d, b0, b1, 0, buf[0], us[0], ev[0]);
-                for (auto& f : parts) f.get();                // rethrows a part's error
-                ready_[c].set_value();
-            }
-        } catch (...) {
-            for (; c < ranges.size(); c++) ready_[c].set_exception(std::current_exception());
-        }
-        for (int t = 0; t < kStageThreads; t++) {
-            if (us[t]) {
-                (void)hipStreamSynchronize(us[t]);
-                (void)hipStreamDestroy(us[t]);
-            }
-            for (int k = 0; k < 2; k++) {
-                if (ev[t][k]) (void)hipEventDestroy(ev[t][k]);
-                if (buf[t][k]) (void)hipHostFree(buf[t][k]);
-            }
-        }
-    }
     void run(int device, const char* h, char* d, const std::vector<std::pair<int64_t, int64_t>>& ranges) {
-        if (staged_) {
-            run_staged(device, h, d, ranges);
-            return;
-        }
         size_t c = 0;
         hipStream_t us = nullptr;
         try {
@@ -638,7 +574,7 @@ class ChunkUploader {
     }
     std::vector<std::promise<void>> ready_;
     std::vector<std::future<void>> got_;
-    bool pin_ = false, staged_ = false;
+    bool pin_ = false;
     std::atomic<bool> stop_{false};
     std::thread th_;
 };

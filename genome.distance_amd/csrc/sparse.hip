@@ -583,7 +583,7 @@ constexpr int SNW = SNT / 64;
 // the virtual word's, then the window's last-slot masks
 constexpr int kBatchWords = 48;
 constexpr int kWinGroups = 16;
-static_assert((kBatchWords + 1) * 16 + kWinGroups * 8 <= 1024, "a wave's walk LDS");
+static_assert((kBatchWords + 1) * 16 + kWinGroups * 8 <= 1024 - 16, "a wave's walk LDS (its last 16 bytes spare: wave 0's hold the batch counter)");
 
 struct SparseWalk {
     const char* eA;                       // the chunk's row-side records (bytes)
@@ -771,17 +771,100 @@ __device__ __forceinline__ void sparse_walk(const int4* __restrict__ rec, unsign
     }
 }
 
+// The tile being walked (sparse_tile_kernel): its blocks' (block, word)
+// offsets, bases of the chunk's records, row trimming, shape flags.
+struct TileWalk {
+    const int64_t* offA;
+    const int64_t* offB;
+    const ulonglong2* ent;
+    int64_t ra0, cb0;                     // chunk bases (entries < 2^28 in all: byte offsets)
+    uint32_t zA, zB;                      // the sentinel run from those bases
+    SparseWalk e;
+    int rlo, rhi;
+    bool rpart, diag, mirror, r22;
+};
+
+// One batch of up to kBatchWords words [s0, we) walked over global memory
+// (only >= 0: that lane's word alone)
+template <int SUN, int MT>
+__device__ __forceinline__ void global_batch(const TileWalk& tc, int64_t s0, int64_t we, int only, int lane,
+                                             int4* __restrict__ wrec, unsigned long long* __restrict__ masks,
+                                             uint32_t* __restrict__ cnt) {
+    const int64_t* offA = tc.offA;
+    const int64_t* offB = tc.offB;
+    const ulonglong2* ent = tc.ent;
+    const int64_t ra0 = tc.ra0, cb0 = tc.cb0;
+    const uint32_t zA = tc.zA, zB = tc.zB;
+    const SparseWalk& e = tc.e;
+    const int rlo = tc.rlo, rhi = tc.rhi;
+    const bool rpart = tc.rpart, diag = tc.diag, mirror = tc.mirror, r22 = tc.r22;
+    const int64_t s = s0 + lane;
+    int64_t rb = ra0, cb = cb0;
+    int nr = 0, ncl = 0;
+    if (lane < kBatchWords && s < we && (only < 0 || lane == only)) {
+        rb = offA[s]; nr = (int)(offA[s + 1] - rb);
+        cb = offB[s]; ncl = (int)(offB[s + 1] - cb);
+        if (rpart) {                               // lists are sorted by set: trim both ends
+            int a = 0, en = nr;
+            for (int t = 0; t < nr; t++) {
+                const int st = (int)((uint32_t)ent[rb + t].x >> 8);   // row code: set << 8 | rotation key
+                a += st < rlo;
+                en -= st >= rhi;
+            }
+            rb += a;
+            nr = en > a ? en - a : 0;
+        }
+    }
+    const int ncd = diag ? ncl : (ncl + 1) >> 1;   // column pairs per row (off-diagonal micro-tiles)
+    const int P = diag ? nr * (nr - 1) / 2 : (r22 ? (nr + 1) >> 1 : nr) * ncd;
+    int incl = P;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += v;
+    }
+    const int total = __builtin_amdgcn_readlane(incl, 63);      // uniform: the walk's loop stays scalar
+    // the records of the words with slots, compacted in slot order, and the
+    // virtual word after them (its records: the zero sentinel run)
+    const unsigned long long nz = __ballot(P > 0);
+    const int k = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(nz >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)nz, 0u));
+    if (P > 0) {
+        if (diag) {
+            wrec[k] = make_int4(-(incl - P), (int32_t)(rb - ra0), 0, 0);
+        } else {
+            const uint32_t rcp = (uint32_t)__float_as_int(__builtin_amdgcn_rcpf(2.0f * (float)ncd));
+            wrec[k] = make_int4(-2 * (incl - P), (int32_t)((rb - ra0) << 4), (int32_t)((cb - cb0) << 4),
+                                (int32_t)((rcp & 0xFFFFFF00u) | (uint32_t)(2 * ncd)));
+        }
+    }
+    if (lane == 0) {
+        const int nw = __popcll(nz);
+        wrec[nw] = diag ? make_int4(-total, (int32_t)zA, 0, 0)
+                        : make_int4(-2 * total, (int32_t)(zA << 4), (int32_t)(zB << 4), 0);
+    }
+    const int last = P > 0 ? incl - 1 : 0x7FFFFFFF;
+    __builtin_amdgcn_wave_barrier();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    if (diag) sparse_walk<SUN, 0>(wrec, masks, last, total, lane, e, cnt, mirror);
+    else if (MT == 2 && r22) sparse_walk<MT == 2 ? SUN : 1, 2>(wrec, masks, last, total, lane, e, cnt, false);
+    else sparse_walk<SUN, 1>(wrec, masks, last, total, lane, e, cnt, false);
+}
+
 template <int SUN, int MT>
 __global__ __launch_bounds__(SNT, 8) void sparse_tile_kernel(
     const int64_t* __restrict__ off, const ulonglong2* __restrict__ ent, const int32_t* __restrict__ nc, int64_t Us,
     int64_t Ws, const int2* __restrict__ tiles, const int32_t* __restrict__ cbnd, int nchunks, int64_t r0, int64_t r1,
     int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I, int64_t ldI, int32_t* __restrict__ part, int64_t Wdp,
     int64_t N, const unsigned long long* __restrict__ slab_bits, int slabs, GroupPart gp, int xmap, int ntiles,
-    RareSlab rs) {
+    RareSlab rs, int dyn) {
     // gp: the group tier's part of every pair, added with the constant part
     // slab_bits / slabs: the in-kernel fold's dense words (set-major [N][Wdp])
     __shared__ uint32_t cnt[SB * SB / 2];                  // 32 KiB, 16-bit counters (cnt_index layout)
     __shared__ int4 rec[SNW][64];                          // 8 KiB: the batch's walk records
+    // dyn: the chunk's next unclaimed batch, in wave 0's unused last record
+    // (an LDS variable of its own would take the workgroup past 40 KiB: 3
+    // workgroups a CU instead of 4, and the compiler then spends 80 VGPRs)
+    int& next_batch = rec[0][63].w;
     // the rare rows of this step (above) are the launch's LAST workgroups:
     // they fill the CUs the tile workgroups' last round leaves idle
     const unsigned ntw = gridDim.x - (unsigned)rs.nrare;
@@ -812,6 +895,7 @@ __global__ __launch_bounds__(SNT, 8) void sparse_tile_kernel(
     const bool diag = A == B && !rpart, mirror = diag && !upper;
     const bool r22 = MT == 2 && !diag && !rpart;             // 2 x 2 micro-tiles
     for (int t = threadIdx.x; t < SB * SB / 2; t += SNT) cnt[t] = 0;
+    if (threadIdx.x == 0) next_batch = SNW;
     __syncthreads();
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int64_t sb = cbnd[ch], se = cbnd[ch + 1];          // the chunk's sparse words
@@ -820,63 +904,27 @@ __global__ __launch_bounds__(SNT, 8) void sparse_tile_kernel(
     const int64_t ra0 = offA[sb], cb0 = offB[sb];           // chunk bases (entries < 2^28 in all: byte offsets)
     const int64_t ntot = off[(int64_t)ceil_div(N, SB) * Ws];         // entries of every block: the sentinel run
     const uint32_t zA = (uint32_t)(ntot - ra0), zB = (uint32_t)(ntot - cb0);
-    const SparseWalk e{reinterpret_cast<const char*>(ent + ra0), reinterpret_cast<const char*>(ent + cb0)};
+    const TileWalk tc{offA, offB, ent, ra0, cb0, zA, zB,
+                      SparseWalk{reinterpret_cast<const char*>(ent + ra0), reinterpret_cast<const char*>(ent + cb0)},
+                      rlo, rhi, rpart, diag, mirror, r22};
     int4* wrec = &rec[wv][0];
     unsigned long long* masks = reinterpret_cast<unsigned long long*>(&rec[wv][kBatchWords + 1]);
-    // the wave's share of the chunk's words, in batches of kBatchWords
+    // the wave's share of the chunk's words, in batches of kBatchWords: an
+    // equal run of words per wave, or (dyn, default) batch wv first and then
+    // the next unclaimed one (an LDS counter), so that a wave that drew light
+    // words takes more of them instead of idling until the heaviest wave ends
     const int64_t per = ceil_div(se - sb, (int64_t)SNW);
-    const int64_t wb = sb + (int64_t)wv * per, we = wb + per < se ? wb + per : se;
-    for (int64_t s0 = wb; s0 < we; s0 += kBatchWords) {
-        const int64_t s = s0 + lane;
-        int64_t rb = ra0, cb = cb0;
-        int nr = 0, ncl = 0;
-        if (lane < kBatchWords && s < we) {
-            rb = offA[s]; nr = (int)(offA[s + 1] - rb);
-            cb = offB[s]; ncl = (int)(offB[s + 1] - cb);
-            if (rpart) {                               // lists are sorted by set: trim both ends
-                int a = 0, en = nr;
-                for (int t = 0; t < nr; t++) {
-                    const int st = (int)((uint32_t)ent[rb + t].x >> 8);   // row code: set << 8 | rotation key
-                    a += st < rlo;
-                    en -= st >= rhi;
-                }
-                rb += a;
-                nr = en > a ? en - a : 0;
-            }
+    const int64_t wb = dyn ? sb + (int64_t)wv * kBatchWords : sb + (int64_t)wv * per;
+    const int64_t we = dyn ? se : (wb + per < se ? wb + per : se);
+    for (int64_t s0 = wb; s0 < we;) {
+        global_batch<SUN, MT>(tc, s0, we, -1, lane, wrec, masks, cnt);
+        if (dyn) {
+            int nb = 0;
+            if (lane == 0) nb = atomicAdd(&next_batch, 1);
+            s0 = sb + (int64_t)__builtin_amdgcn_readfirstlane(__shfl(nb, 0, 64)) * kBatchWords;
+        } else {
+            s0 += kBatchWords;
         }
-        const int ncd = diag ? ncl : (ncl + 1) >> 1;   // column pairs per row (off-diagonal micro-tiles)
-        const int P = diag ? nr * (nr - 1) / 2 : (r22 ? (nr + 1) >> 1 : nr) * ncd;
-        int incl = P;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int v = __shfl_up(incl, o, 64);
-            if (lane >= o) incl += v;
-        }
-        const int total = __builtin_amdgcn_readlane(incl, 63);      // uniform: the walk's loop stays scalar
-        // the records of the words with slots, compacted in slot order, and the
-        // virtual word after them (its records: the zero sentinel run)
-        const unsigned long long nz = __ballot(P > 0);
-        const int k = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(nz >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)nz, 0u));
-        if (P > 0) {
-            if (diag) {
-                wrec[k] = make_int4(-(incl - P), (int32_t)(rb - ra0), 0, 0);
-            } else {
-                const uint32_t rcp = (uint32_t)__float_as_int(__builtin_amdgcn_rcpf(2.0f * (float)ncd));
-                wrec[k] = make_int4(-2 * (incl - P), (int32_t)((rb - ra0) << 4), (int32_t)((cb - cb0) << 4),
-                                    (int32_t)((rcp & 0xFFFFFF00u) | (uint32_t)(2 * ncd)));
-            }
-        }
-        if (lane == 0) {
-            const int nw = __popcll(nz);
-            wrec[nw] = diag ? make_int4(-total, (int32_t)zA, 0, 0)
-                            : make_int4(-2 * total, (int32_t)(zA << 4), (int32_t)(zB << 4), 0);
-        }
-        const int last = P > 0 ? incl - 1 : 0x7FFFFFFF;
-        __builtin_amdgcn_wave_barrier();
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        if (diag) sparse_walk<SUN, 0>(wrec, masks, last, total, lane, e, cnt, mirror);
-        else if (MT == 2 && r22) sparse_walk<MT == 2 ? SUN : 1, 2>(wrec, masks, last, total, lane, e, cnt, false);
-        else sparse_walk<SUN, 1>(wrec, masks, last, total, lane, e, cnt, false);
     }
     if (ch < slabs) {
         // dense words [8 ch, 8 ch + 8) of the tile's 128 x 128 pairs: the
@@ -1586,7 +1634,8 @@ bool sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
                                          s->sp_U, s->Ws, sc.tiles.as<int2>(), sc.bounds.as<int32_t>(), nchunks, r0, r1,
                                          c0, c1, upper ? 1 : 0, d_I, ldI, sc.use_part ? sc.part.as<int32_t>() : nullptr,
                                          s->Wd, s->nsets, s->dbits.as<unsigned long long>(), s->sp_fold_slabs,
-                                         group_part(s), xmap ? 1 : 0, (int)nt, rs);
+                                         group_part(s), xmap ? 1 : 0, (int)nt, rs,
+                                         (int)ctx->option(OPT_SPARSE_DYN, 1));
     GD_HIP(hipGetLastError());
     ft.end();
     if (sc.use_part) {

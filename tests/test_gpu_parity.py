@@ -65,7 +65,6 @@ PACK_MODES = {"default": {}, "set_major": {"pack_summary": 0},
               "chunked": {"pack_chunk": 1000}, "chunked_set_major": {"pack_chunk": 1000, "pack_summary": 0},
               "chunked_no_overlap": {"pack_chunk": 1000, "pack_overlap": 0},
               "chunked_pinned": {"pack_chunk": 1000, "pack_overlap": 2},
-              "chunked_staged": {"pack_chunk": 1000, "pack_overlap": 3},
               # the codes buffer sized from the first chunk and grown (budget 0:
               # never the one buffer for every window)
               "grown": {"pack_chunk": 1000, "pack_codes_budget": 0},
@@ -141,24 +140,6 @@ def test_chunked_pack_bitset_matrix(ctx, opts, mode):
     I, D = sets.matrix(method=gdist.METHOD_BITSET)
     eI, eD = oracle.matrix(eo, ec, 0, 120, 0, 120)
     assert np.array_equal(I, eI) and bits_equal(D, eD)
-
-
-def test_pack_staged_upload_large(ctx):
-    """The pinned staging upload (option pack_overlap 3: 8 host threads, 4 MiB
-    pieces, two pinned buffers each) of ~48 MB in two chunks, one spanning
-    every thread's pieces and both ending mid-piece, packs the same codes as
-    the upload-first path."""
-    import gdist
-    rng = np.random.default_rng(5)
-    acgt = np.frombuffer(b"ACGT", np.uint8)
-    seqs = [rng.choice(acgt, 480_000 + 37 * i).tobytes() for i in range(100)]
-    got = {}
-    for ov in (0, 3):
-        with ctx.options(pack_overlap=ov, pack_chunk=1 << 25):
-            sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
-        got[ov] = sets.download()
-        sets.free()
-    assert np.array_equal(got[0][0], got[3][0]) and np.array_equal(got[0][1], got[3][1])
 
 
 def test_pack_rejects_unencodable_and_bad_k(ctx):
@@ -755,6 +736,9 @@ SPARSE_MODES = {
     "sun4": {"sparse_zmax": 100000, "sparse_mt": 1, "sparse_sun": 4, "sparse_chunks": 7},
     "sun3": {"sparse_zmax": 100000, "sparse_mt": 1, "sparse_sun": 3},
     "mt1_default": {"sparse_mt": 1},
+    # a tile workgroup's waves take equal runs of words instead of claiming batches in turn
+    "dyn_off": {"sparse_zmax": 100000, "sparse_dyn": 0},
+    "dyn_off_default": {"sparse_dyn": 0, "sparse_chunks": 5},
     # 2 x 2 micro-tiles off the diagonal (default; row-trimmed tiles of the
     # unaligned regions below keep 1 x 2) with 4 / 3 (default) / 2 slots
     "mt2": {"sparse_zmax": 100000, "sparse_mt": 2, "sparse_sun": 4},
@@ -812,7 +796,7 @@ def test_sparse_complement_words_exact(ctx, mode, opts):
     _, W = sets.build_bitsets()
     ws, wd, ent = sets.sparse_info()
     if mode in ("all_sparse", "atomic_flush", "many_chunks", "sun4", "sun3", "sun2_atomic", "mt2", "mt2_sun3",
-                "mt2_sun2_atomic"):
+                "mt2_sun2_atomic", "dyn_off"):
         assert ws > 0 and wd == 0 and ent > 0
     elif mode in ("mixed", "mixed_slabs", "mixed_slabs_atomic", "mixed_tiles"):
         assert ws > 0 and wd > 0
