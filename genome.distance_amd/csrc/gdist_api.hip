@@ -427,6 +427,20 @@ int gdist_memcpy_h2d(gdist_ctx* ctx, void* dst, const void* src, int64_t bytes) 
 }
 
 // ---------------------------------------------------------------------------
+int gdist_host_alloc(int64_t bytes, void** hptr) {
+    return guard([&] {
+        GD_REQUIRE(hptr && bytes >= 0, "bad host allocation arguments");
+        *hptr = nullptr;
+        GD_HIP(hipHostMalloc(hptr, (size_t)std::max<int64_t>(1, bytes), hipHostMallocDefault));
+    });
+}
+
+int gdist_host_free(void* hptr) {
+    return guard([&] {
+        if (hptr) GD_HIP(hipHostFree(hptr));
+    });
+}
+
 int gdist_sets_pack(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* seqs, const int64_t* seq_off,
                     int64_t nseqs, gdist_sets** out) {
     return guard([&] {

@@ -191,6 +191,7 @@ struct Timing {
     X(SPARSE_WG_PER_CU, "sparse_wg_per_cu")   /* chunking target of the sparse tiles (default 4) */            \
     X(SPARSE_SUN, "sparse_sun")               /* slots per lane in flight: 2 / 3 / 4 (default 4) */            \
     X(SPARSE_DYN, "sparse_dyn")               /* 1 (default): a tile workgroup's waves claim word batches in turn; 0: equal runs */ \
+    X(SPARSE_DIAG22, "sparse_diag22")         /* 1 (default): diagonal tiles in 2 x 2 micro-tiles too (sparse_mt 2) */ \
     X(SPARSE_MT, "sparse_mt")                 /* off-diagonal micro-tiles: 1 (1 x 2) / 2 (2 x 2, default) */   \
     X(SKETCH_K, "sketch_k")                   /* sketch merge window (1 / 2 / 4 / 6, default 2) */             \
     X(SKETCH_TILE, "sketch_tile")             /* 16: force the 16x16 sketch tile */                            \
@@ -212,6 +213,7 @@ struct Timing {
     X(FILL_SORT, "fill_sort")                 /* bitset fill: 0/3 windows, 1 sort, 2 atomics, 4 hash, 5 one-wave windows (default: by size) */\
     X(PACK_SORT, "pack_sort")                 /* 1: two (code, set) pair sorts instead of packed keys */       \
     X(PACK_SUMMARY, "pack_summary")           /* 0: set|code pack keys, the bitset build re-sorts codes */     \
+    X(PACK_CODE_SORT, "pack_code_sort")       /* 1 (default): the code-major sort on the code bits when no window was skipped */ \
     X(PACK_OVERLAP, "pack_overlap")           /* 0: upload first / 1: overlapped host thread / 2: registered */\
     X(PACK_CHUNK, "pack_chunk")               /* kmer windows per pack chunk (default 2^28) */                 \
     X(EXCHANGE_BUDGET, "exchange_budget")     /* device bytes an exchange may use (default 0.8 x HBM) */    \

@@ -106,12 +106,14 @@ __global__ void validate_kernel(const unsigned char* __restrict__ seqs, int64_t 
 // Window w of the chunk -> sequence s (binary search in win_off), position,
 // then the k symbols. Emits 1 or 2 (BOTH) entries per window.
 // CM: the code-major sort keys code << idbits | id straight away (the
-// summary path), no id array
+// summary path), no id array; any_invalid (CM) is set to 1 when a window was
+// skipped (plain stores, every writer writes 1)
 template <bool RAW8, bool CM = false>
 __global__ __launch_bounds__(256) void extract_kernel(
     const unsigned char* __restrict__ seqs, const int64_t* __restrict__ seq_off,
     const int64_t* __restrict__ win_off, int nseq, int64_t nwin, int k, int bits, int strand,
-    AlphabetDev al, uint64_t* __restrict__ keys, int32_t* __restrict__ vals, int idbits = 0) {
+    AlphabetDev al, uint64_t* __restrict__ keys, int32_t* __restrict__ vals, int idbits = 0,
+    int* __restrict__ any_invalid = nullptr) {
     __shared__ int8_t sym[256];
     __shared__ int8_t comp[8];
     for (int t = threadIdx.x; t < 256; t += blockDim.x) sym[t] = al.sym[t];
@@ -143,6 +145,7 @@ __global__ __launch_bounds__(256) void extract_kernel(
         fwd &= mask;
         const int32_t id = valid ? s : nseq;
         if (CM) {
+            if (!valid) *any_invalid = 1;
             const uint64_t sid = (uint64_t)(uint32_t)id;
             if (strand == GDIST_STRAND_BOTH) {
                 keys[2 * w] = (fwd << idbits) | sid;
@@ -522,12 +525,26 @@ void exclusive_scan_i32_to_i64(gdist_ctx* ctx, const int32_t* in, int64_t* out, 
 // bytes move while chunk c sorts (chunk 0's wait is the part left on the
 // clock). Pieces, not one copy per chunk, so that the pack's own small
 // read-backs interleave with the upload.
+// true when p lies in page-locked host memory (gdist_host_alloc): the
+// upload is then one DMA per chunk at the link's rate (~50 GB/s) instead of
+// the runtime's staged pageable copies (~6 GB/s, the C2 pack's bound)
+static bool host_pinned(const void* p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
 class ChunkUploader {
   public:
     // mode 1: the runtime's staged pageable copies; 2: register each chunk's
-    // host range (page-locked, one DMA)
-    ChunkUploader(int device, const char* h, char* d, std::vector<std::pair<int64_t, int64_t>> ranges, int mode)
-        : ready_(ranges.size()), pin_(mode == 2) {
+    // host range (page-locked, one DMA); pinned: the caller's buffer is
+    // page-locked already (gdist_host_alloc): one DMA per chunk
+    ChunkUploader(int device, const char* h, char* d, std::vector<std::pair<int64_t, int64_t>> ranges, int mode,
+                  bool pinned)
+        : ready_(ranges.size()), pin_(mode == 2 && !pinned), src_pinned_(pinned) {
         for (auto& p : ready_) got_.push_back(p.get_future());
         th_ = std::thread([this, device, h, d, ranges] { run(device, h, d, ranges); });
     }
@@ -552,7 +569,7 @@ class ChunkUploader {
                            hipHostRegister(const_cast<char*>(h) + b0, (size_t)(b1 - b0), hipHostRegisterDefault) ==
                                hipSuccess;
                 if (pin_ && !reg) (void)hipGetLastError();
-                if (reg) {
+                if (reg || (src_pinned_ && b1 > b0)) {
                     GD_HIP(hipMemcpyAsync(d + b0, h + b0, (size_t)(b1 - b0), hipMemcpyHostToDevice, us));
                 } else {
                     for (int64_t o = b0; o < b1; o += kPiece) {
@@ -574,7 +591,7 @@ class ChunkUploader {
     }
     std::vector<std::promise<void>> ready_;
     std::vector<std::future<void>> got_;
-    bool pin_ = false;
+    bool pin_ = false, src_pinned_ = false;
     std::atomic<bool> stop_{false};
     std::thread th_;
 };
@@ -643,7 +660,8 @@ void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_se
         } else {
             std::vector<std::pair<int64_t, int64_t>> ranges;
             for (auto& c : chunks) ranges.push_back({h_seq_off[c.first], h_seq_off[c.second]});
-            up.reset(new ChunkUploader(ctx->device, h_seqs, dst, std::move(ranges), (int)ctx->option(OPT_PACK_OVERLAP, 1)));
+            up.reset(new ChunkUploader(ctx->device, h_seqs, dst, std::move(ranges), (int)ctx->option(OPT_PACK_OVERLAP, 1),
+                                       host_pinned(h_seqs)));
         }
     }
 
@@ -748,15 +766,19 @@ void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_se
         const bool cm_extract = cm_path && !guides_here;
         DevBuf kA(n * 8 + 8, st), kB(n * 8 + 8, st), vA(cm_extract ? 8 : n * 4 + 4, st),
             vB(cm_path ? 8 : n * 4 + 4, st);
+        // CM keys: whether a window was skipped (its key's set field is the
+        // invalid id nc; see the sort below)
+        DevBuf inv(cm_extract ? 4 : 0, st);
+        if (cm_extract) GD_HIP(hipMemsetAsync(inv.p, 0, 4, st));
         if (nw > 0 && cm_extract) {
             if (raw8)
                 extract_kernel<true, true><<<grid_for(nw, 256, 256 * 64), 256, 0, st>>>(
                     src, d_seq_off + s0, cw.as<int64_t>(), nc, nw, k, bits, strand, al, kA.as<uint64_t>(), nullptr,
-                    idbits);
+                    idbits, inv.as<int>());
             else
                 extract_kernel<false, true><<<grid_for(nw, 256, 256 * 64), 256, 0, st>>>(
                     src, d_seq_off + s0, cw.as<int64_t>(), nc, nw, k, bits, strand, al, kA.as<uint64_t>(), nullptr,
-                    idbits);
+                    idbits, inv.as<int>());
             GD_HIP(hipGetLastError());
         } else if (nw > 0) {
             if (raw8)
@@ -783,7 +805,18 @@ void pack_sets(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_se
                 GD_HIP(hipGetLastError());
                 std::swap(keys, keys_alt);
             }
-            sort_keys_u64(ctx, keys, keys_alt, (size_t)n, 0, cbits + idbits);
+            // The extraction writes each set's keys after the previous set's
+            // (windows in order), so a stable radix sort on the code bits
+            // alone leaves equal codes in set order: C2's 42-bit codes sort
+            // in 6 passes instead of 7 for code|set. A skipped window's key
+            // (set field nc) would sit inside its code's run in input order,
+            // not last, so a chunk with skipped windows sorts the set bits too
+            int hinv = 1;
+            if (cm_extract && n > 0 && ctx->option(OPT_PACK_CODE_SORT, 1) != 0) {
+                d2h(&hinv, inv.p, 4, st);
+                GD_HIP(hipStreamSynchronize(st));
+            }
+            sort_keys_u64(ctx, keys, keys_alt, (size_t)n, hinv ? 0 : idbits, cbits + idbits);
             tr.mark("pack: sort by code|set");
             // one flag word per key: bit 0 = first key of its (code, set)
             // (valid), bit 32 = first valid key of its code; their prefix sums

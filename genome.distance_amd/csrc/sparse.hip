@@ -738,6 +738,68 @@ __device__ __forceinline__ void sparse_off22_slots(const int4* __restrict__ rec,
     }
 }
 
+// Diagonal tiles in 2 x 2 micro-tiles (with sparse_mt 2): the word's n
+// entries as m = ceil(n / 2) pairs; slot q is the pair of pairs (Y, X), Y <=
+// X, q = X (X + 1) / 2 + Y. X > Y: all four products are pairs y < x (the
+// column pair's second entry past an odd list dropped by the first's
+// last-of-list flag); X == Y: only (2Y, 2Y + 1). Three products a slot on
+// average instead of one, from four loads instead of two; rec as
+// sparse_diag_slots.
+template <int SU>
+__device__ __forceinline__ void sparse_diag22_slots(const int4* __restrict__ rec,
+                                                    const unsigned long long* __restrict__ masks, int W0, int last,
+                                                    int fb, int lane, const SparseWalk& e, uint32_t* __restrict__ cnt,
+                                                    bool mirror) {
+    int4 r[SU];
+    unsigned long long m[SU];
+    const unsigned long long* mk = masks + ((fb - W0) >> 6);
+#pragma unroll
+    for (int u = 0; u < SU; u++) m[u] = mk[u];
+#pragma unroll
+    for (int u = 0; u < SU; u++) r[u] = rec[slot_rec(last, fb + 64 * u, m[u])];
+    uint32_t ri[SU], ci[SU], ne[SU];
+#pragma unroll
+    for (int u = 0; u < SU; u++) {
+        const int q = fb + 64 * u + lane + r[u].x;
+        int x = (int)((__builtin_amdgcn_sqrtf(1.0f + 8.0f * (float)q) - 1.0f) * 0.5f);
+        const int t = (int)(__umul24(x, x + 1) >> 1);
+        // x -= 1 when t > q, x += 1 when (x + 1)(x + 2) / 2 <= q
+        const int dn = (int)(t > q), up = (int)(t + x + 1 <= q);
+        const int xc = x + up - dn;
+        const int tc = t + __mul24(up, x + 1) - __mul24(dn, x);
+        const int yc = q - tc;
+        ri[u] = (uint32_t)(r[u].y + 2 * yc) << 4;
+        ci[u] = (uint32_t)(r[u].y + 2 * xc) << 4;
+        ne[u] = xc != yc ? ~0u : 0u;
+    }
+    uint4 a0[SU], a1[SU], b0[SU], b1[SU];         // {row code, word lo, word hi, column code}
+#pragma unroll
+    for (int u = 0; u < SU; u++) {
+        a0[u] = *reinterpret_cast<const uint4*>(e.eA + ri[u]);
+        a1[u] = *reinterpret_cast<const uint4*>(e.eA + ri[u] + 16);
+        b0[u] = *reinterpret_cast<const uint4*>(e.eA + ci[u]);
+        b1[u] = *reinterpret_cast<const uint4*>(e.eA + ci[u] + 16);
+    }
+#pragma unroll
+    for (int u = 0; u < SU; u++) {
+        const uint32_t lb = ~(uint32_t)__builtin_amdgcn_sbfe((int)b0[u].w, 5, 1);    // kLastOfList: bit 5
+        const uint32_t v00 = (uint32_t)(__popc(a0[u].y & b0[u].y) + __popc(a0[u].z & b0[u].z)) & ne[u];
+        const uint32_t v01 = (uint32_t)(__popc(a0[u].y & b1[u].y) + __popc(a0[u].z & b1[u].z)) & lb;
+        const uint32_t v10 = (uint32_t)(__popc(a1[u].y & b0[u].y) + __popc(a1[u].z & b0[u].z)) & ne[u];
+        const uint32_t v11 = (uint32_t)(__popc(a1[u].y & b1[u].y) + __popc(a1[u].z & b1[u].z)) & (ne[u] & lb);
+        cnt_add(cnt, a0[u].x, b0[u].w, v00);
+        cnt_add(cnt, a0[u].x, b1[u].w, v01);
+        cnt_add(cnt, a1[u].x, b0[u].w, v10);
+        cnt_add(cnt, a1[u].x, b1[u].w, v11);
+        if (mirror) {
+            cnt_add(cnt, b0[u].x, a0[u].w, v00);
+            cnt_add(cnt, b1[u].x, a0[u].w, v01);
+            cnt_add(cnt, b0[u].x, a1[u].w, v10);
+            cnt_add(cnt, b1[u].x, a1[u].w, v11);
+        }
+    }
+}
+
 // A batch's walk: windows of G groups of 64 slots (G a multiple of SUN):
 // the window's last-slot masks, then SUN groups per step while whole steps
 // remain, one group at a time after
@@ -759,12 +821,14 @@ __device__ __forceinline__ void sparse_walk(const int4* __restrict__ rec, unsign
         for (; fb + 64 * SUN <= wend; fb += 64 * SUN) {
             if (MODE == 0) sparse_diag_slots<SUN>(rec, masks, W0, last, fb, lane, e, cnt, mirror);
             else if (MODE == 1) sparse_off_slots<SUN>(rec, masks, W0, last, fb, lane, e, cnt);
-            else sparse_off22_slots<SUN>(rec, masks, W0, last, fb, lane, e, cnt);
+            else if (MODE == 2) sparse_off22_slots<SUN>(rec, masks, W0, last, fb, lane, e, cnt);
+            else sparse_diag22_slots<SUN>(rec, masks, W0, last, fb, lane, e, cnt, mirror);
         }
         for (; fb < wend; fb += 64) {
             if (MODE == 0) sparse_diag_slots<1>(rec, masks, W0, last, fb, lane, e, cnt, mirror);
             else if (MODE == 1) sparse_off_slots<1>(rec, masks, W0, last, fb, lane, e, cnt);
-            else sparse_off22_slots<1>(rec, masks, W0, last, fb, lane, e, cnt);
+            else if (MODE == 2) sparse_off22_slots<1>(rec, masks, W0, last, fb, lane, e, cnt);
+            else sparse_diag22_slots<1>(rec, masks, W0, last, fb, lane, e, cnt, mirror);
         }
         __builtin_amdgcn_wave_barrier();
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
@@ -782,6 +846,7 @@ struct TileWalk {
     SparseWalk e;
     int rlo, rhi;
     bool rpart, diag, mirror, r22;
+    bool d22;                             // diagonal tiles in 2 x 2 micro-tiles (MT 2, option sparse_diag22)
 };
 
 // One batch of up to kBatchWords words [s0, we) walked over global memory
@@ -798,6 +863,7 @@ __device__ __forceinline__ void global_batch(const TileWalk& tc, int64_t s0, int
     const SparseWalk& e = tc.e;
     const int rlo = tc.rlo, rhi = tc.rhi;
     const bool rpart = tc.rpart, diag = tc.diag, mirror = tc.mirror, r22 = tc.r22;
+    const bool d22 = MT == 2 && tc.d22;
     const int64_t s = s0 + lane;
     int64_t rb = ra0, cb = cb0;
     int nr = 0, ncl = 0;
@@ -816,7 +882,9 @@ __device__ __forceinline__ void global_batch(const TileWalk& tc, int64_t s0, int
         }
     }
     const int ncd = diag ? ncl : (ncl + 1) >> 1;   // column pairs per row (off-diagonal micro-tiles)
-    const int P = diag ? nr * (nr - 1) / 2 : (r22 ? (nr + 1) >> 1 : nr) * ncd;
+    const int hp = (nr + 1) >> 1;                 // 2 x 2 diagonal: pairs of entries
+    const int P = diag ? (d22 ? (nr >= 2 ? hp * (hp + 1) / 2 : 0) : nr * (nr - 1) / 2)
+                       : (r22 ? hp : nr) * ncd;
     int incl = P;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -845,7 +913,8 @@ __device__ __forceinline__ void global_batch(const TileWalk& tc, int64_t s0, int
     const int last = P > 0 ? incl - 1 : 0x7FFFFFFF;
     __builtin_amdgcn_wave_barrier();
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    if (diag) sparse_walk<SUN, 0>(wrec, masks, last, total, lane, e, cnt, mirror);
+    if (MT == 2 && diag && d22) sparse_walk<2, 3>(wrec, masks, last, total, lane, e, cnt, mirror);
+    else if (diag) sparse_walk<SUN, 0>(wrec, masks, last, total, lane, e, cnt, mirror);
     else if (MT == 2 && r22) sparse_walk<MT == 2 ? SUN : 1, 2>(wrec, masks, last, total, lane, e, cnt, false);
     else sparse_walk<SUN, 1>(wrec, masks, last, total, lane, e, cnt, false);
 }
@@ -856,7 +925,7 @@ __global__ __launch_bounds__(SNT, 8) void sparse_tile_kernel(
     int64_t Ws, const int2* __restrict__ tiles, const int32_t* __restrict__ cbnd, int nchunks, int64_t r0, int64_t r1,
     int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I, int64_t ldI, int32_t* __restrict__ part, int64_t Wdp,
     int64_t N, const unsigned long long* __restrict__ slab_bits, int slabs, GroupPart gp, int xmap, int ntiles,
-    RareSlab rs, int dyn) {
+    RareSlab rs, int dyn, int diag22) {
     // gp: the group tier's part of every pair, added with the constant part
     // slab_bits / slabs: the in-kernel fold's dense words (set-major [N][Wdp])
     __shared__ uint32_t cnt[SB * SB / 2];                  // 32 KiB, 16-bit counters (cnt_index layout)
@@ -906,7 +975,7 @@ __global__ __launch_bounds__(SNT, 8) void sparse_tile_kernel(
     const uint32_t zA = (uint32_t)(ntot - ra0), zB = (uint32_t)(ntot - cb0);
     const TileWalk tc{offA, offB, ent, ra0, cb0, zA, zB,
                       SparseWalk{reinterpret_cast<const char*>(ent + ra0), reinterpret_cast<const char*>(ent + cb0)},
-                      rlo, rhi, rpart, diag, mirror, r22};
+                      rlo, rhi, rpart, diag, mirror, r22, diag22 != 0};
     int4* wrec = &rec[wv][0];
     unsigned long long* masks = reinterpret_cast<unsigned long long*>(&rec[wv][kBatchWords + 1]);
     // the wave's share of the chunk's words, in batches of kBatchWords: an
@@ -1635,7 +1704,7 @@ bool sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
                                          c0, c1, upper ? 1 : 0, d_I, ldI, sc.use_part ? sc.part.as<int32_t>() : nullptr,
                                          s->Wd, s->nsets, s->dbits.as<unsigned long long>(), s->sp_fold_slabs,
                                          group_part(s), xmap ? 1 : 0, (int)nt, rs,
-                                         (int)ctx->option(OPT_SPARSE_DYN, 1));
+                                         (int)ctx->option(OPT_SPARSE_DYN, 1), (int)ctx->option(OPT_SPARSE_DIAG22, 1));
     GD_HIP(hipGetLastError());
     ft.end();
     if (sc.use_part) {

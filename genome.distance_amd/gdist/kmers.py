@@ -168,6 +168,38 @@ class Context:
         return x.value
 
 
+class HostBuffer:
+    """Page-locked host memory (gdist_host_alloc) for sequence bytes: fill
+    `array` (uint8) in place, e.g. with a FASTA reader, and pass it to
+    KmerSets.from_blob: the pack uploads it with one DMA per chunk instead of
+    the runtime's staged pageable copies. `array` must not be used after
+    free() / the with-block."""
+
+    def __init__(self, nbytes: int):
+        p = C.c_void_p()
+        L.check(L.lib.gdist_host_alloc(int(nbytes), C.byref(p)))
+        self.ptr, self.nbytes = p.value or 0, int(nbytes)
+        self.array = np.ctypeslib.as_array((C.c_uint8 * max(1, self.nbytes)).from_address(self.ptr))[:self.nbytes]
+
+    def free(self):
+        if self.ptr:
+            self.array = None
+            L.check(L.lib.gdist_host_free(self.ptr))
+            self.ptr = 0
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.free()
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
 class DeviceBuffer:
     def __init__(self, ctx: Context, nbytes: int):
         p = C.c_void_p()

@@ -161,6 +161,11 @@ int  gdist_dev_alloc(gdist_ctx* ctx, int64_t bytes, void** dptr);
 int  gdist_dev_free(gdist_ctx* ctx, void* dptr);
 int  gdist_memcpy_d2h(gdist_ctx* ctx, void* dst, const void* src, int64_t bytes);
 int  gdist_memcpy_h2d(gdist_ctx* ctx, void* dst, const void* src, int64_t bytes);
+/* Page-locked host memory for sequence bytes (a FASTA reader fills it in
+ * place): gdist_sets_pack uploads such a buffer with one DMA per pack chunk
+ * at the link's rate instead of the runtime's staged pageable copies. */
+int  gdist_host_alloc(int64_t bytes, void** hptr);
+int  gdist_host_free(void* hptr);
 
 /* ---- kmer sets ------------------------------------------------------- */
 /* Build kmer sets of nseqs sequences on the device. seqs is the byte
@@ -168,6 +173,7 @@ int  gdist_memcpy_h2d(gdist_ctx* ctx, void* dst, const void* src, int64_t bytes)
  * is synchronous; inside it a short-lived host thread of the library
  * uploads the bytes of pack chunk c + 1 while chunk c is packed (option
  * "pack_overlap"), so seqs is read until the call returns. */
+/* seqs in a gdist_host_alloc buffer: one DMA per chunk (detected). */
 int  gdist_sets_pack(gdist_ctx* ctx, int kind, int k, unsigned flags,
                      const char* seqs, const int64_t* seq_off, int64_t nseqs,
                      gdist_sets** out);

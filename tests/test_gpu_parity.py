@@ -65,6 +65,8 @@ PACK_MODES = {"default": {}, "set_major": {"pack_summary": 0},
               "chunked": {"pack_chunk": 1000}, "chunked_set_major": {"pack_chunk": 1000, "pack_summary": 0},
               "chunked_no_overlap": {"pack_chunk": 1000, "pack_overlap": 0},
               "chunked_pinned": {"pack_chunk": 1000, "pack_overlap": 2},
+              # the code-major sort over code|set even where no window was skipped
+              "chunked_full_key_sort": {"pack_chunk": 1000, "pack_code_sort": 0},
               # the codes buffer sized from the first chunk and grown (budget 0:
               # never the one buffer for every window)
               "grown": {"pack_chunk": 1000, "pack_codes_budget": 0},
@@ -140,6 +142,29 @@ def test_chunked_pack_bitset_matrix(ctx, opts, mode):
     I, D = sets.matrix(method=gdist.METHOD_BITSET)
     eI, eD = oracle.matrix(eo, ec, 0, 120, 0, 120)
     assert np.array_equal(I, eI) and bits_equal(D, eD)
+
+
+def test_pack_pinned_source_large(ctx):
+    """Sequence bytes in a page-locked host buffer from gdist_host_alloc
+    (gdist.HostBuffer) upload with one DMA per chunk: ~140 MB in two chunks,
+    the first ending mid-sequence, pack the same codes as the same bytes in
+    pageable memory (the runtime's staged copies) and as upload-first."""
+    import gdist
+    rng = np.random.default_rng(5)
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    lens = [1_000_000 + 37 * i for i in range(140)]
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    flat = rng.choice(acgt, int(off[-1]))
+    got = {}
+    with gdist.HostBuffer(int(off[-1])) as hb:
+        hb.array[:] = flat
+        for name, blob, ov in (("pinned", hb.array, 1), ("pageable", flat, 1), ("first", flat, 0)):
+            with ctx.options(pack_overlap=ov, pack_chunk=1 << 27):
+                sets = gdist.KmerSets.from_blob(blob, off, 21, gdist.KmerType.DNA, 0, ctx)
+            got[name] = sets.download()
+            sets.free()
+    for name in ("pageable", "first"):
+        assert np.array_equal(got["pinned"][0], got[name][0]) and np.array_equal(got["pinned"][1], got[name][1])
 
 
 def test_pack_rejects_unencodable_and_bad_k(ctx):
@@ -745,6 +770,9 @@ SPARSE_MODES = {
     "mt2_sun3": {"sparse_zmax": 100000, "sparse_mt": 2, "sparse_sun": 3, "sparse_chunks": 7},
     "mt2_sun2_atomic": {"sparse_zmax": 100000, "sparse_mt": 2, "sparse_sun": 2, "sparse_part_budget": 0,
                         "sparse_chunks": 3},
+    # 2 x 2 off the diagonal, one product a slot on it (option sparse_diag22 0)
+    "diag11": {"sparse_zmax": 100000, "sparse_diag22": 0},
+    "diag11_default": {"sparse_diag22": 0},
     "sun2_atomic": {"sparse_zmax": 100000, "sparse_sun": 2, "sparse_part_budget": 0, "sparse_chunks": 3},
     # the dense words counted inside the tile kernel, 8 per chunk (partials / atomic flush),
     # or by their own tile launch
@@ -796,7 +824,7 @@ def test_sparse_complement_words_exact(ctx, mode, opts):
     _, W = sets.build_bitsets()
     ws, wd, ent = sets.sparse_info()
     if mode in ("all_sparse", "atomic_flush", "many_chunks", "sun4", "sun3", "sun2_atomic", "mt2", "mt2_sun3",
-                "mt2_sun2_atomic", "dyn_off"):
+                "mt2_sun2_atomic", "dyn_off", "diag11"):
         assert ws > 0 and wd == 0 and ent > 0
     elif mode in ("mixed", "mixed_slabs", "mixed_slabs_atomic", "mixed_tiles"):
         assert ws > 0 and wd > 0
