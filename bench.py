@@ -46,9 +46,10 @@ import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0               # MI355X_MICROARCH.md chip table (spec)
 # what bounds the sparse tile kernel (v6), from its PMC passes (profiles/r02/sparse6/)
-SPARSE_LIMITER = ("latency of the product walk, not HBM bandwidth: each 1x2 micro-tile slot waits on three "
-                  "scattered 12-byte record loads and adds two LDS counters; round 4 cut its VALU per slot "
-                  "from ~47 to ~28 (ISA) for a 5 % shorter kernel (DESIGN.md §4)")
+SPARSE_LIMITER = ("latency of the product walk's scattered record loads, not HBM bandwidth or VALU issue: "
+                  "a 2x2 micro-tile slot waits on four 12-16-byte record loads and adds four LDS counters "
+                  "(VALU ~0.3 of its issue rate, TA ~0.5 busy, HBM traffic ~1.0x the algorithmic bytes; "
+                  "DESIGN.md §4)")
 # FP4 MFMA (block-scaled e2m1) dense peak, MI355X_MICROARCH.md chip table: ~10 PF
 # dense = 5 P bit-products/s for the dense tiles on the matrix cores
 MFMA_FP4_PEAK_TOPS = 10000.0

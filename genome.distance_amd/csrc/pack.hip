@@ -323,17 +323,26 @@ __global__ __launch_bounds__(kSelT) void cm_select_kernel(const uint64_t* __rest
         tot += f[j];
     }
     int64_t all;
-    int64_t p = bpre[blockIdx.x] + block_excl_scan_i64(tot, red, &all);
+    const int64_t excl = block_excl_scan_i64(tot, red, &all);   // every thread's keys are in registers
+    int64_t p = bpre[blockIdx.x] + excl;
+    // the tile's unique keys are one contiguous run of u: gathered in LDS (the
+    // key tile, free after the scan) and stored coalesced, not 16 keys a
+    // thread at 128-byte strides
+    int lp = (int)(excl & 0xFFFFFFFFll);
 #pragma unroll
     for (int j = 0; j < kSelPer; j++) {
         if (f[j] & 1) {
             const uint64_t k = kv[j + 1];
-            const int64_t at = p & 0xFFFFFFFFll;
-            u[at] = k;
-            if (f[j] >> 32) { codes[p >> 32] = k >> idbits; start[p >> 32] = at; }
+            sk[lp + (lp >> 4)] = k;
+            lp++;
+            if (f[j] >> 32) { codes[p >> 32] = k >> idbits; start[p >> 32] = p & 0xFFFFFFFFll; }
         }
         p += f[j];
     }
+    __syncthreads();
+    const int64_t ub = bpre[blockIdx.x] & 0xFFFFFFFFll;
+    const int nu = (int)(all & 0xFFFFFFFFll);
+    for (int i = threadIdx.x; i < nu; i += kSelT) u[ub + i] = sk[i + (i >> 4)];
 }
 
 __global__ void cm_run_counts_kernel(const int64_t* __restrict__ start, int64_t nruns, int64_t n,
