@@ -435,6 +435,14 @@ int gdist_host_alloc(int64_t bytes, void** hptr) {
     });
 }
 
+int gdist_release_cache(int device) {
+    return guard([&] {
+        GD_HIP(hipSetDevice(device));
+        GD_HIP(hipDeviceSynchronize());
+        gdist::cache_trim(device);
+    });
+}
+
 int gdist_host_free(void* hptr) {
     return guard([&] {
         if (hptr) GD_HIP(hipHostFree(hptr));

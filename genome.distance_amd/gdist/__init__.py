@@ -10,7 +10,7 @@ from ._lib import (AMBIG_DEFAULT, AMBIG_KEEP, AMBIG_SKIP, BITSET_KEEP_SINGLETONS
                    SKETCH_JACCARD, STRAND_BOTH, STRAND_CANON, STRAND_FWD, UPPER_TRIANGLE, GdistError)
 from .fasta import Sequence, read_fasta, write_fasta
 from .javafmt import java_double, java_doubles
-from .kmers import (Context, DeviceBuffer, HostBuffer, KmerSets, KmerType, LSHIndex, SequenceKmers, SketchSets, option_names,
+from .kmers import (Context, DeviceBuffer, HostBuffer, release_device_cache, KmerSets, KmerType, LSHIndex, SequenceKmers, SketchSets, option_names,
                     options_from_env, triangle_partition)
 
 __version__ = _lib.lib.gdist_version().decode()

@@ -96,6 +96,7 @@ _SIGS = {
     "gdist_memcpy_h2d": (C.c_int, [_ctxp, _vp, _vp, _i64]),
     "gdist_host_alloc": (C.c_int, [_i64, C.POINTER(C.c_void_p)]),
     "gdist_host_free": (C.c_int, [_vp]),
+    "gdist_release_cache": (C.c_int, [C.c_int]),
     "gdist_sets_pack": (C.c_int, [_ctxp, C.c_int, C.c_int, _u32, C.c_char_p, _i64p, _i64, C.POINTER(_setp)]),
     "gdist_sets_pack_device": (C.c_int, [_ctxp, C.c_int, C.c_int, _u32, _vp, _vp, _i64, _i64,
                                          C.POINTER(_setp)]),

@@ -168,6 +168,12 @@ class Context:
         return x.value
 
 
+def release_device_cache(device: int = 0) -> None:
+    """gdist_release_cache: hand the library's cached device blocks back to
+    the driver (before another process takes the GPU)."""
+    L.check(L.lib.gdist_release_cache(int(device)))
+
+
 class HostBuffer:
     """Page-locked host memory (gdist_host_alloc) for sequence bytes: fill
     `array` (uint8) in place, e.g. with a FASTA reader, and pass it to

@@ -165,6 +165,10 @@ int  gdist_memcpy_h2d(gdist_ctx* ctx, void* dst, const void* src, int64_t bytes)
  * place): gdist_sets_pack uploads such a buffer with one DMA per pack chunk
  * at the link's rate instead of the runtime's staged pageable copies. */
 int  gdist_host_alloc(int64_t bytes, void** hptr);
+/* Return the library's cached device blocks of `device` (freed buffers it
+ * keeps for reuse) to the driver, e.g. before another process takes the
+ * GPU. Blocks in use are untouched. */
+int  gdist_release_cache(int device);
 int  gdist_host_free(void* hptr);
 
 /* ---- kmer sets ------------------------------------------------------- */

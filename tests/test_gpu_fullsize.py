@@ -222,6 +222,14 @@ def test_pack_after_bitset_workload_regression(ctx):
 @pytest.mark.timeout(1150)
 def test_c4_full_size_slices_vs_oracle():
     """C4 (BASELINE configs[3]) at its size: see tests/c4_worker.py."""
+    import gc
+
+    import gdist
+    # the worker needs most of the GPU: this process's cached device blocks
+    # (the full-size tests above freed tens of GB into the library's cache)
+    # go back to the driver first
+    gc.collect()
+    gdist.release_device_cache(0)
     here = os.path.dirname(os.path.abspath(__file__))
     r = subprocess.run([sys.executable, "-u", os.path.join(here, "c4_worker.py")], capture_output=True, text=True,
                        timeout=1100)
