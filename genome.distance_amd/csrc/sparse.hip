@@ -800,58 +800,6 @@ __device__ __forceinline__ void sparse_diag22_slots(const int4* __restrict__ rec
     }
 }
 
-// Off-diagonal 2 x 4 micro-tiles (option sparse_mt 4): a row pair x a
-// column quad, eight products from six record loads; records and quotient as
-// sparse_off_slots with ncq = ceil(ncol / 4) quads (the quad's byte offset
-// at yq << 6). A quad past its list's end drops the products of its entries
-// after the first last-of-list flag.
-template <int SU>
-__device__ __forceinline__ void sparse_off24_slots(const int4* __restrict__ rec,
-                                                   const unsigned long long* __restrict__ masks, int W0, int last,
-                                                   int fb, int lane, const SparseWalk& e, uint32_t* __restrict__ cnt) {
-    int4 r[SU];
-    unsigned long long m[SU];
-    const unsigned long long* mk = masks + ((fb - W0) >> 6);
-#pragma unroll
-    for (int u = 0; u < SU; u++) m[u] = mk[u];
-#pragma unroll
-    for (int u = 0; u < SU; u++) r[u] = rec[slot_rec(last, fb + 64 * u, m[u])];
-    uint32_t ri[SU], ci[SU];
-#pragma unroll
-    for (int u = 0; u < SU; u++) {
-        const int q2 = 2 * (fb + 64 * u) + 2 * lane + r[u].x;
-        const float rcp = __int_as_float(r[u].w);
-        const int xc = (int)__builtin_fmaf((float)q2, rcp, rcp);
-        const int yc2 = q2 - (int)__umul24((uint32_t)xc, (uint32_t)r[u].w & 0xFFu);
-        ri[u] = (uint32_t)r[u].y + ((uint32_t)xc << 5);
-        ci[u] = (uint32_t)r[u].z + ((uint32_t)yc2 << 5);
-    }
-    uint4 a0[SU];
-    Rec3 a1[SU], b[SU][4];
-#pragma unroll
-    for (int u = 0; u < SU; u++) {
-        const char* pa = e.eA + ri[u];
-        const char* pb = e.eB + ci[u] + 4;
-        a0[u] = *reinterpret_cast<const uint4*>(pa);
-        a1[u] = *reinterpret_cast<const Rec3*>(pa + 16);
-#pragma unroll
-        for (int j = 0; j < 4; j++) b[u][j] = *reinterpret_cast<const Rec3*>(pb + 16 * j);
-    }
-#pragma unroll
-    for (int u = 0; u < SU; u++) {
-        const uint32_t la = ~(uint32_t)__builtin_amdgcn_sbfe((int)a0[u].w, 5, 1);    // kLastOfList: bit 5
-        uint32_t l = ~0u;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint32_t v0 = (uint32_t)(__popc(a0[u].y & b[u][j].a) + __popc(a0[u].z & b[u][j].b)) & l;
-            const uint32_t v1 = (uint32_t)(__popc(a1[u].b & b[u][j].a) + __popc(a1[u].c & b[u][j].b)) & (l & la);
-            cnt_add(cnt, a0[u].x, b[u][j].c, v0);
-            cnt_add(cnt, a1[u].a, b[u][j].c, v1);
-            l &= ~(uint32_t)__builtin_amdgcn_sbfe((int)b[u][j].c, 5, 1);
-        }
-    }
-}
-
 // A batch's walk: windows of G groups of 64 slots (G a multiple of SUN):
 // the window's last-slot masks, then SUN groups per step while whole steps
 // remain, one group at a time after
@@ -874,15 +822,13 @@ __device__ __forceinline__ void sparse_walk(const int4* __restrict__ rec, unsign
             if (MODE == 0) sparse_diag_slots<SUN>(rec, masks, W0, last, fb, lane, e, cnt, mirror);
             else if (MODE == 1) sparse_off_slots<SUN>(rec, masks, W0, last, fb, lane, e, cnt);
             else if (MODE == 2) sparse_off22_slots<SUN>(rec, masks, W0, last, fb, lane, e, cnt);
-            else if (MODE == 3) sparse_diag22_slots<SUN>(rec, masks, W0, last, fb, lane, e, cnt, mirror);
-            else sparse_off24_slots<SUN>(rec, masks, W0, last, fb, lane, e, cnt);
+            else sparse_diag22_slots<SUN>(rec, masks, W0, last, fb, lane, e, cnt, mirror);
         }
         for (; fb < wend; fb += 64) {
             if (MODE == 0) sparse_diag_slots<1>(rec, masks, W0, last, fb, lane, e, cnt, mirror);
             else if (MODE == 1) sparse_off_slots<1>(rec, masks, W0, last, fb, lane, e, cnt);
             else if (MODE == 2) sparse_off22_slots<1>(rec, masks, W0, last, fb, lane, e, cnt);
-            else if (MODE == 3) sparse_diag22_slots<1>(rec, masks, W0, last, fb, lane, e, cnt, mirror);
-            else sparse_off24_slots<1>(rec, masks, W0, last, fb, lane, e, cnt);
+            else sparse_diag22_slots<1>(rec, masks, W0, last, fb, lane, e, cnt, mirror);
         }
         __builtin_amdgcn_wave_barrier();
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
@@ -917,7 +863,7 @@ __device__ __forceinline__ void global_batch(const TileWalk& tc, int64_t s0, int
     const SparseWalk& e = tc.e;
     const int rlo = tc.rlo, rhi = tc.rhi;
     const bool rpart = tc.rpart, diag = tc.diag, mirror = tc.mirror, r22 = tc.r22;
-    const bool d22 = MT >= 2 && tc.d22;
+    const bool d22 = MT == 2 && tc.d22;
     const int64_t s = s0 + lane;
     int64_t rb = ra0, cb = cb0;
     int nr = 0, ncl = 0;
@@ -935,8 +881,7 @@ __device__ __forceinline__ void global_batch(const TileWalk& tc, int64_t s0, int
             nr = en > a ? en - a : 0;
         }
     }
-    // column pairs (quads: 2 x 4) per row pair / row (off-diagonal micro-tiles)
-    const int ncd = diag ? ncl : (MT == 4 && r22) ? (ncl + 3) >> 2 : (ncl + 1) >> 1;
+    const int ncd = diag ? ncl : (ncl + 1) >> 1;   // column pairs per row (pair) (off-diagonal micro-tiles)
     const int hp = (nr + 1) >> 1;                 // 2 x 2 diagonal: pairs of entries
     const int P = diag ? (d22 ? (nr >= 2 ? hp * (hp + 1) / 2 : 0) : nr * (nr - 1) / 2)
                        : (r22 ? hp : nr) * ncd;
@@ -968,10 +913,9 @@ __device__ __forceinline__ void global_batch(const TileWalk& tc, int64_t s0, int
     const int last = P > 0 ? incl - 1 : 0x7FFFFFFF;
     __builtin_amdgcn_wave_barrier();
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    if (MT >= 2 && diag && d22) sparse_walk<2, 3>(wrec, masks, last, total, lane, e, cnt, mirror);
+    if (MT == 2 && diag && d22) sparse_walk<2, 3>(wrec, masks, last, total, lane, e, cnt, mirror);
     else if (diag) sparse_walk<SUN, 0>(wrec, masks, last, total, lane, e, cnt, mirror);
     else if (MT == 2 && r22) sparse_walk<MT == 2 ? SUN : 1, 2>(wrec, masks, last, total, lane, e, cnt, false);
-    else if (MT == 4 && r22) sparse_walk<MT == 4 ? 2 : 1, 4>(wrec, masks, last, total, lane, e, cnt, false);
     else sparse_walk<SUN, 1>(wrec, masks, last, total, lane, e, cnt, false);
 }
 
@@ -1018,7 +962,7 @@ __global__ __launch_bounds__(SNT, 8) void sparse_tile_kernel(
     const int rhi = (int)(r1 - A * SB < SB ? r1 - A * SB : SB);
     const bool rpart = rlo > 0 || rhi < SB;
     const bool diag = A == B && !rpart, mirror = diag && !upper;
-    const bool r22 = MT >= 2 && !diag && !rpart;             // 2 x 2 (2 x 4) micro-tiles
+    const bool r22 = MT == 2 && !diag && !rpart;             // 2 x 2 micro-tiles
     for (int t = threadIdx.x; t < SB * SB / 2; t += SNT) cnt[t] = 0;
     if (threadIdx.x == 0) next_batch = SNW;
     __syncthreads();
@@ -1732,14 +1676,10 @@ bool sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     // 2 x 2 micro-tiles, 3 slots (12 products) per lane in flight; 1 x 2 with
     // 4 (C2 A/B, profiles/r04/s21/ab, r04/s13/ab_sun: 2 x 2 with 4 spills)
     const int mt = (int)ctx->option(OPT_SPARSE_MT, 2);
-    const int sun = (int)ctx->option(OPT_SPARSE_SUN, mt == 4 ? 2 : mt == 2 ? 3 : 4);
+    const int sun = (int)ctx->option(OPT_SPARSE_SUN, mt == 2 ? 3 : 4);
     GD_REQUIRE(sun >= 2 && sun <= 4, "sparse_sun: 2, 3 or 4");
-    GD_REQUIRE(mt == 1 || mt == 2 || mt == 4, "sparse_mt: 1 (1 x 2 micro-tiles), 2 (2 x 2) or 4 (2 x 4)");
-    // 2 x 4: two slots a lane (the virtual word's quads then stay inside the
-    // kSentinelRecs zero records: 2 x (2 x 64 x 2 - 2) + 3 < 512)
-    GD_REQUIRE(mt != 4 || sun == 2, "sparse_mt 4 runs 2 slots a lane");
-    auto kern = mt == 4 ? sparse_tile_kernel<2, 4>
-              : mt == 2 ? (sun == 2 ? sparse_tile_kernel<2, 2> : sun == 4 ? sparse_tile_kernel<4, 2> : sparse_tile_kernel<3, 2>)
+    GD_REQUIRE(mt == 1 || mt == 2, "sparse_mt: 1 (1 x 2 micro-tiles) or 2 (2 x 2)");
+    auto kern = mt == 2 ? (sun == 2 ? sparse_tile_kernel<2, 2> : sun == 4 ? sparse_tile_kernel<4, 2> : sparse_tile_kernel<3, 2>)
                         : (sun == 2 ? sparse_tile_kernel<2, 1> : sun == 4 ? sparse_tile_kernel<4, 1> : sparse_tile_kernel<3, 1>);
     // the rare tier's pairs of this step: the launch's trailing workgroups
     const bool rare = sc.use_part && sc.rare_in;
