@@ -960,7 +960,9 @@ __global__ __launch_bounds__(SNT, 8) void sparse_tile_kernel(
     const int64_t A = tiles[tile].x, B = tiles[tile].y;
     const int rlo = (int)(r0 - A * SB > 0 ? r0 - A * SB : 0);
     const int rhi = (int)(r1 - A * SB < SB ? r1 - A * SB : SB);
-    const bool rpart = rlo > 0 || rhi < SB;
+    // rows trimmed only where the region cuts a block's existing rows: the
+    // collection's last, partial block ending at r1 = N needs no trimming
+    const bool rpart = rlo > 0 || (rhi < SB && r1 < N);
     const bool diag = A == B && !rpart, mirror = diag && !upper;
     const bool r22 = MT == 2 && !diag && !rpart;             // 2 x 2 micro-tiles
     for (int t = threadIdx.x; t < SB * SB / 2; t += SNT) cnt[t] = 0;
