@@ -925,7 +925,7 @@ __global__ __launch_bounds__(SNT, 8) void sparse_tile_kernel(
     int64_t Ws, const int2* __restrict__ tiles, const int32_t* __restrict__ cbnd, int nchunks, int64_t r0, int64_t r1,
     int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I, int64_t ldI, int32_t* __restrict__ part, int64_t Wdp,
     int64_t N, const unsigned long long* __restrict__ slab_bits, int slabs, GroupPart gp, int xmap, int ntiles,
-    RareSlab rs, int dyn, int diag22) {
+    RareSlab rs, int dyn, int diag22, int rpart22) {
     // gp: the group tier's part of every pair, added with the constant part
     // slab_bits / slabs: the in-kernel fold's dense words (set-major [N][Wdp])
     __shared__ uint32_t cnt[SB * SB / 2];                  // 32 KiB, 16-bit counters (cnt_index layout)
@@ -964,7 +964,10 @@ __global__ __launch_bounds__(SNT, 8) void sparse_tile_kernel(
     // collection's last, partial block ending at r1 = N needs no trimming
     const bool rpart = rlo > 0 || (rhi < SB && r1 < N);
     const bool diag = A == B && !rpart, mirror = diag && !upper;
-    const bool r22 = MT == 2 && !diag && !rpart;             // 2 x 2 micro-tiles
+    // 2 x 2 micro-tiles, row-trimmed tiles too (option sparse_rpart22): a
+    // trimmed list's odd last pair reads the entry after the range as its
+    // second row — a row outside the region, whose counters no store reads
+    const bool r22 = MT == 2 && !diag && (!rpart || rpart22);
     for (int t = threadIdx.x; t < SB * SB / 2; t += SNT) cnt[t] = 0;
     if (threadIdx.x == 0) next_batch = SNW;
     __syncthreads();
@@ -1706,7 +1709,8 @@ bool sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
                                          c0, c1, upper ? 1 : 0, d_I, ldI, sc.use_part ? sc.part.as<int32_t>() : nullptr,
                                          s->Wd, s->nsets, s->dbits.as<unsigned long long>(), s->sp_fold_slabs,
                                          group_part(s), xmap ? 1 : 0, (int)nt, rs,
-                                         (int)ctx->option(OPT_SPARSE_DYN, 1), (int)ctx->option(OPT_SPARSE_DIAG22, 1));
+                                         (int)ctx->option(OPT_SPARSE_DYN, 1), (int)ctx->option(OPT_SPARSE_DIAG22, 1),
+                                         (int)ctx->option(OPT_SPARSE_RPART22, 1));
     GD_HIP(hipGetLastError());
     ft.end();
     if (sc.use_part) {

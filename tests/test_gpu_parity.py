@@ -770,6 +770,8 @@ SPARSE_MODES = {
     "mt2_sun3": {"sparse_zmax": 100000, "sparse_mt": 2, "sparse_sun": 3, "sparse_chunks": 7},
     "mt2_sun2_atomic": {"sparse_zmax": 100000, "sparse_mt": 2, "sparse_sun": 2, "sparse_part_budget": 0,
                         "sparse_chunks": 3},
+    # row-trimmed tiles (the unaligned regions below) in 1 x 2 micro-tiles (option sparse_rpart22 0)
+    "rpart12": {"sparse_zmax": 100000, "sparse_rpart22": 0},
     # 2 x 2 off the diagonal, one product a slot on it (option sparse_diag22 0)
     "diag11": {"sparse_zmax": 100000, "sparse_diag22": 0},
     "diag11_default": {"sparse_diag22": 0},
@@ -824,7 +826,7 @@ def test_sparse_complement_words_exact(ctx, mode, opts):
     _, W = sets.build_bitsets()
     ws, wd, ent = sets.sparse_info()
     if mode in ("all_sparse", "atomic_flush", "many_chunks", "sun4", "sun3", "sun2_atomic", "mt2", "mt2_sun3",
-                "mt2_sun2_atomic", "dyn_off", "diag11"):
+                "mt2_sun2_atomic", "dyn_off", "diag11", "rpart12"):
         assert ws > 0 and wd == 0 and ent > 0
     elif mode in ("mixed", "mixed_slabs", "mixed_slabs_atomic", "mixed_tiles"):
         assert ws > 0 and wd > 0
