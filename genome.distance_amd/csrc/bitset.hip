@@ -562,6 +562,15 @@ __global__ __launch_bounds__(NT, 4) void bitset_tile_kernel2(
 constexpr int MT = 256;                       // tile edge (sets)
 constexpr int64_t kMfmaMinWords = 64;         // dense words from which the MFMA tiles run (option bitset_mfma)
 constexpr int MNT = 512;                      // threads
+// f32 is exact for integers <= 2^24: one K split's count of shared bits is
+// <= 64 x its words, so a split spans at most 2^18 words
+constexpr int64_t kMfmaMaxSplitWords = int64_t(1) << 18;
+// the fewest K splits (of nst stages of km words) that keep every split's
+// count exact in f32
+static inline int64_t mfma_min_splits(int64_t nst, int km) {
+    const int64_t per_max = kMfmaMaxSplitWords / km;                 // stages a split may span
+    return nst <= per_max ? 1 : (nst + per_max - 1) / per_max;
+}
 // KM words per stage (4: 2 x 32 KiB a stage, 128 KiB double-buffered; 2:
 // 64 KiB, so a row-major rare workgroup fits beside it on a CU: option
 // bitset_mfma_km)
@@ -2024,6 +2033,11 @@ void build_postings(gdist_ctx* ctx, gdist_sets* s, unsigned long long* recs, int
 void build_bitsets(gdist_ctx* ctx, gdist_sets* s, unsigned flags, int64_t rare_threshold) {
     const bool keep = (flags & GDIST_BITSET_KEEP_SINGLETONS) != 0;
     int64_t T = keep ? 0 : rare_threshold;     // < 0: cost-optimal from the count histogram
+    // a rebuild replaces every tier: the old variant lists, sparse words,
+    // plans and FP4 operand must not survive into the new representation
+    // (a two-tier rebuild of a variant collection would add its stale
+    // variant counts on top of the new bits); synchronises both streams
+    free_bitsets(s);
     Trace tr(ctx->stream, ctx->trace());
     Summary sum;
     // a collection without pack summaries and too many codes for one sort
@@ -2428,6 +2442,12 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
                 1, std::min<int64_t>(std::max<int64_t>(1, nst / 8), ceil_div((int64_t)ctx->cus * 4, p.nmt)));
             if (ctx->has_option(OPT_BITSET_MFMA_SPLITS))      // A/B: a given K split
                 msp = (int)std::max<int64_t>(1, std::min<int64_t>(nst, ctx->option(OPT_BITSET_MFMA_SPLITS, 1)));
+            // exactness: a split's f32 accumulator sums at most 64 x (its
+            // words) bits; f32 holds every integer <= 2^24 exactly, so no
+            // split may span more than kMfmaMaxSplitWords words (a pair of
+            // ~10 Mbp genomes on both strands shares > 2^24 dense kmers)
+            msp = (int)std::max<int64_t>(msp, mfma_min_splits(nst, km));
+            GD_REQUIRE(ceil_div(nst, (int64_t)msp) * km <= kMfmaMaxSplitWords, "MFMA K split past the f32 exact bound");
             const int64_t mgrid = p.nmt * msp;
             GD_REQUIRE(mgrid < (int64_t(1) << 31), "MFMA tile grid too large");
             if (s->fp4_W != tW) {

@@ -436,11 +436,16 @@ int gdist_host_alloc(int64_t bytes, void** hptr) {
 }
 
 int gdist_release_cache(int device) {
-    return guard([&] {
+    // the caller's current device is restored on every exit (as use_device)
+    int prev = -1;
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    const int rc = guard([&] {
         GD_HIP(hipSetDevice(device));
         GD_HIP(hipDeviceSynchronize());
         gdist::cache_trim(device);
     });
+    if (prev >= 0 && prev != device) (void)hipSetDevice(prev);
+    return rc;
 }
 
 int gdist_host_free(void* hptr) {

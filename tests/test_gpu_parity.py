@@ -918,6 +918,38 @@ def test_dense_tiles_mfma_exact(ctx, opts, mfma, T):
     assert bits_equal(d, eD[0, [0, 529, 77, 300]])
 
 
+@pytest.mark.parametrize("splits", [1, None])
+def test_dense_tiles_mfma_past_f32_bound(ctx, opts, splits):
+    """the FP4 MFMA tiles accumulate in f32, exact only
+    for counts <= 2^24. Four near-identical 10 Mbp genomes (DNA k=21, both
+    strands: ~20 M kmers each, GenomeProcessor.java:139-140's scale) share
+    more than 2^24 dense kmers a pair; with one K split asked for (option
+    bitset_mfma_splits 1) the launch must still split K so that no split
+    sums more than 2^18 words, and I and D equal the oracle bit for bit
+    (and the AND + popcount tiles, option bitset_mfma 0)."""
+    import gdist
+    opts(sparse=0, bitset_mfma_splits=splits)
+    n = 4
+    seqs = synth_sets(n, 10_000_000, 0.001, 131)
+    sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
+    _, W = sets.build_bitsets(rare_threshold=0)
+    assert W > (1 << 18), W                      # one split would pass the f32 bound
+    off, codes = oracle_pack(seqs, 21, 0, 0)
+    eI, eD = oracle.matrix(off, codes, 0, n, 0, n, flags=0, nthreads=4)
+    iu = np.triu_indices(n, 1)
+    assert eI[iu].min() > (1 << 24), eI[iu]       # the premise: counts past 2^24
+    for mfma in (None, 0):
+        opts(bitset_mfma=mfma)
+        for up in (True, False):
+            I, D = sets.matrix(upper=up, method=gdist.METHOD_BITSET)
+            if up:
+                assert np.array_equal(I[iu], eI[iu]), (mfma, I[iu], eI[iu])
+                assert bits_equal(D[iu], eD[iu])
+            else:
+                assert np.array_equal(I, eI), (mfma, I, eI)
+                assert bits_equal(D, eD)
+
+
 @pytest.mark.parametrize("fill", [None, 0, 5, 4, 1])
 def test_fill_routes_on_sparse_sets(ctx, opts, fill):
     """C3-shaped proteomes (sets much smaller than the dictionary, T > N so

@@ -76,6 +76,46 @@ def test_variant_tier_exact(ctx, opts, c4_like, mode):
     assert bits_equal(d, eD[0, cols])
 
 
+def test_rebuild_drops_variant_tier(ctx, opts, c4_like):
+    """a collection built with the variant tier and then
+    rebuilt without it (option variant 0, another rare threshold, or kept
+    singletons) must not keep the old variant lists: every rebuild equals
+    the oracle, and variant_info reports the new tiers only."""
+    import gdist
+    seqs, off, codes = c4_like
+    n = len(seqs)
+    opts(variant=1, rare_t=3, variant_dmin=n // 10)
+    sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
+    sets.build_bitsets()
+    assert sets.variant_info()[0] > 0
+    r0, r1 = 300, 700
+    eI, eD = oracle.matrix(off, codes, r0, r1, 0, n, flags=0x100, nthreads=8)
+    mask = np.fromfunction(lambda a, b: b > (r0 + a), (r1 - r0, n))
+
+    def check(tag):
+        I, D = sets.matrix((r0, r1), (0, n), upper=True, method=gdist.METHOD_BITSET)
+        assert np.array_equal(I[mask], eI[mask]), (tag, np.flatnonzero(I[mask] != eI[mask])[:5])
+        assert bits_equal(D[mask], eD[mask]), tag
+        d = sets.row_query(500, [0, 17, n - 1, 500])
+        assert bits_equal(d, oracle.matrix(off, codes, 500, 501, 0, n)[1][0, [0, 17, n - 1, 500]]), tag
+
+    check("variant")
+    opts(variant=0)
+    sets.build_bitsets()                          # two tiers, same rare_t
+    assert sets.variant_info()[:3] == (0, 0, 0)
+    check("two-tier rebuild")
+    opts(variant=1)
+    sets.build_bitsets()
+    assert sets.variant_info()[0] > 0
+    check("variant again")
+    opts(variant=None, rare_t=None)
+    sets.build_bitsets(rare_threshold=5)          # a given threshold
+    check("rare_t 5")
+    sets.build_bitsets(keep_singletons=True)
+    assert sets.variant_info()[:3] == (0, 0, 0)
+    check("keep singletons")
+
+
 def test_variant_tier_replayed_steps(ctx, opts, c4_like):
     """Repeated device-output calls (plan, capture, replay) of a variant-tier
     collection: every call equals the oracle (the variant walk's atomics land
