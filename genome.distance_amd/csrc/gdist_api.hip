@@ -483,6 +483,68 @@ int gdist_sets_pack(gdist_ctx* ctx, int kind, int k, unsigned flags, const char*
     });
 }
 
+int gdist_sets_append(gdist_ctx* ctx, gdist_sets* sets, const char* seqs, const int64_t* seq_off, int64_t nseqs,
+                      int64_t* first) {
+    return guard([&] {
+        use_device(ctx);
+        std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+        check_codes(sets);
+        GD_REQUIRE(sets->ctx == ctx, "sets belong to another context");
+        GD_REQUIRE(sets->kind != GDIST_SKETCH, "sketch collections are built, not appended to");
+        GD_REQUIRE(nseqs >= 0 && (nseqs == 0 || (seqs && seq_off)), "bad append arguments");
+        if (first) *first = sets->nsets;
+        if (nseqs == 0) return;
+        std::vector<int64_t> h(nseqs + 1, 0);
+        const int64_t base = seq_off[0];
+        for (int64_t i = 0; i <= nseqs; i++) h[i] = seq_off[i] - base;
+        for (int64_t i = 0; i < nseqs; i++) GD_REQUIRE(h[i + 1] >= h[i], "sequence offsets must be non-decreasing");
+        hipStream_t st = ctx->stream;
+        gdist_sets add;                        // the new sequences, packed with the collection's kmer spec
+        add.ctx = ctx;
+        {
+            DevBuf dseq(h[nseqs] + 1, st), doff((nseqs + 1) * 8, st);
+            h2d(doff.p, h.data(), (nseqs + 1) * 8, st);
+            pack_sets(ctx, sets->kind, sets->k, sets->flags, dseq.as<char>(), doff.as<int64_t>(), h, &add, seqs + base);
+        }
+        // every representation derived from the old sets is stale (dictionary,
+        // tiers, plans, captured steps, the sorted join's segment index, the
+        // pack summaries the dictionary merges)
+        free_bitsets(sets);
+        sets->segoff.release();
+        sets->nseg = 0;
+        sets->max_seg = 0;
+        sets->auto_sorted = false;
+        sets->pack_sum.clear();
+        // codes: in place while the buffer's size class has room, else a
+        // buffer of twice the need (n appends copy O(n) codes in all)
+        const int64_t total = sets->total + add.total;
+        if ((size_t)(total * 8 + 8) > sets->codes.cls) {
+            DevBuf grown((size_t)total * 16 + 8, st);
+            if (sets->total)
+                GD_HIP(hipMemcpyAsync(grown.p, sets->codes.p, sets->total * 8, hipMemcpyDeviceToDevice, st));
+            sets->codes = std::move(grown);
+        } else {
+            sets->codes.bytes = std::max(sets->codes.bytes, (size_t)(total * 8 + 8));
+        }
+        if (add.total)
+            GD_HIP(hipMemcpyAsync(sets->codes.as<uint64_t>() + sets->total, add.codes.p, add.total * 8,
+                                  hipMemcpyDeviceToDevice, st));
+        for (int64_t i = 1; i <= add.nsets; i++) sets->h_off.push_back(add.h_off[i] + sets->total);
+        sets->nsets += add.nsets;
+        sets->total = total;
+        sets->off.alloc((sets->nsets + 1) * 8, st);
+        h2d(sets->off.p, sets->h_off.data(), (sets->nsets + 1) * 8, st);
+        // locus guides: the collection's first sequences (the new ones only
+        // when it had none)
+        if (sets->n_guide == 0 && add.n_guide) {
+            sets->guide_codes = std::move(add.guide_codes);
+            sets->guide_keys = std::move(add.guide_keys);
+            sets->n_guide = add.n_guide;
+        }
+        GD_HIP(hipStreamSynchronize(st));
+    });
+}
+
 int gdist_sets_pack_device(gdist_ctx* ctx, int kind, int k, unsigned flags, const char* d_seqs,
                            const int64_t* d_seq_off, int64_t nseqs, int64_t total_bytes, gdist_sets** out) {
     return guard([&] {

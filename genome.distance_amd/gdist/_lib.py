@@ -100,6 +100,7 @@ _SIGS = {
     "gdist_sets_pack": (C.c_int, [_ctxp, C.c_int, C.c_int, _u32, C.c_char_p, _i64p, _i64, C.POINTER(_setp)]),
     "gdist_sets_pack_device": (C.c_int, [_ctxp, C.c_int, C.c_int, _u32, _vp, _vp, _i64, _i64,
                                          C.POINTER(_setp)]),
+    "gdist_sets_append": (C.c_int, [_ctxp, _setp, C.c_char_p, _i64p, _i64, _i64p]),
     "gdist_sets_upload": (C.c_int, [_ctxp, C.c_int, C.c_int, _i64, _i64p, _u64p, C.POINTER(_setp)]),
     "gdist_sets_free": (C.c_int, [_setp]),
     "gdist_sets_info": (C.c_int, [_setp, C.POINTER(C.c_int), C.POINTER(C.c_int), _i64p, _i64p]),

@@ -328,6 +328,19 @@ class KmerSets(_Handle):
                                       len(bs), C.byref(h)))
         return cls(ctx, h)
 
+    def append(self, seqs: Sequence) -> int:
+        """gdist_sets_append: pack `seqs` with this collection's kmer spec and
+        append them as new sets; returns the index of the first one. Every
+        derived representation is rebuilt on the next distance call."""
+        bs = [_as_bytes(s) for s in seqs]
+        off = np.zeros(len(bs) + 1, dtype=np.int64)
+        if bs:
+            off[1:] = np.cumsum([len(b) for b in bs])
+        blob = b"".join(bs) or b"\0"
+        first = C.c_int64()
+        L.check(L.lib.gdist_sets_append(self.ctx.h, self.h, blob, L.ptr(off, C.c_int64), len(bs), C.byref(first)))
+        return first.value
+
     @classmethod
     def from_blob(cls, blob, offsets, k: int, kmer_type: KmerType = KmerType.DNA, flags: int = 0,
                   ctx: Context | None = None) -> "KmerSets":

@@ -185,6 +185,15 @@ int  gdist_sets_pack(gdist_ctx* ctx, int kind, int k, unsigned flags,
 int  gdist_sets_pack_device(gdist_ctx* ctx, int kind, int k, unsigned flags,
                             const char* d_seqs, const int64_t* d_seq_off, int64_t nseqs,
                             int64_t total_bytes, gdist_sets** out);
+/* Pack nseqs more sequences with the collection's kmer spec (kind, k, flags)
+ * and append them as sets nsets .. nsets + nseqs - 1 (*first = the old nsets).
+ * Replaces `new GenomeKmers(genome)` for a genome seen for the first time by
+ * a cache that packs each genome once (MethodTableProcessor.java:261-275 via
+ * jni/GpuKmerMethod.java). Every derived representation (bitsets, tiers,
+ * plans, the sorted join's index) is dropped and rebuilt on the next call;
+ * the codes grow in place, doubling when full. */
+int  gdist_sets_append(gdist_ctx* ctx, gdist_sets* sets, const char* seqs, const int64_t* seq_off,
+                       int64_t nseqs, int64_t* first);
 /* Adopt caller-packed sets: CSR of sorted, unique codes (host arrays, copied). */
 int  gdist_sets_upload(gdist_ctx* ctx, int kind, int k, int64_t nsets,
                        const int64_t* offsets, const uint64_t* codes, gdist_sets** out);

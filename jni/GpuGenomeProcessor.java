@@ -105,11 +105,14 @@ public class GpuGenomeProcessor extends BaseReportProcessor {
         writer.println("genome1\tgenome2\tdistance");
         final int nMain = this.baseIds.size();
         long compares = 0;
-        try (GpuKmerSets.Context ctx = new GpuKmerSets.Context(this.device)) {
+        try (GpuKmerSets.Context ctx = new GpuKmerSets.Context(this.device);
+             GpuKmerSets base = new GpuKmerSets(ctx, GpuKmerSets.DNA, this.kmerSize,
+                                                this.baseSeqs.toArray(new byte[0][]))) {
+            // the base genomes are packed once (mainKmers, GenomeProcessor.java:100-111)
             for (File dir : this.genomeDirs) {
                 GenomeSource genomes = this.sourceType.create(dir);
                 List<String> ids = new ArrayList<String>(genomes.size());
-                List<byte[]> seqs = new ArrayList<byte[]>(genomes.size() + nMain);
+                List<byte[]> seqs = new ArrayList<byte[]>(genomes.size());
                 for (Genome genome : genomes) {
                     ids.add(genome.getId());
                     seqs.add(contigBytes(genome));
@@ -117,20 +120,30 @@ public class GpuGenomeProcessor extends BaseReportProcessor {
                 final int m = ids.size();
                 if (m == 0)
                     continue;
-                // rows 0..m-1: this directory's genomes; columns m..m+nMain-1: the base genomes
-                seqs.addAll(this.baseSeqs);
-                try (GpuKmerSets sets = new GpuKmerSets(ctx, GpuKmerSets.DNA, this.kmerSize,
-                                                        seqs.toArray(new byte[0][]))) {
-                    double[] d = new double[m * nMain];
-                    sets.distances(0, m, m, m + nMain, false, d, nMain);
-                    for (int r = 0; r < m; r++)
-                        for (int i = 0; i < nMain; i++) {
-                            writer.println(ids.get(r) + "\t" + this.baseIds.get(i) + "\t" + d[r * nMain + i]);
-                            compares++;
-                        }
+                // rows 0..m-1: this directory's genomes; columns m..m+nMain-1: the
+                // base genomes' sets, copied on the device (gdist_sets_concat), not re-packed
+                try (GpuKmerSets dirSets = new GpuKmerSets(ctx, GpuKmerSets.DNA, this.kmerSize,
+                                                           seqs.toArray(new byte[0][]));
+                     GpuKmerSets sets = dirSets.concat(base)) {
+                    // row blocks of at most ROW_BLOCK_CELLS distances (no int overflow
+                    // of m * nMain, bounded host memory)
+                    final int rows = (int) Math.max(1, Math.min(m, ROW_BLOCK_CELLS / Math.max(1, nMain)));
+                    double[] d = new double[rows * nMain];
+                    for (int r0 = 0; r0 < m; r0 += rows) {
+                        final int r1 = Math.min(m, r0 + rows);
+                        sets.distances(r0, r1, m, m + nMain, false, d, nMain);
+                        for (int r = r0; r < r1; r++)
+                            for (int i = 0; i < nMain; i++) {
+                                writer.println(ids.get(r) + "\t" + this.baseIds.get(i) + "\t" + d[(r - r0) * nMain + i]);
+                                compares++;
+                            }
+                    }
                 }
             }
         }
         log.info("{} comparisons output.", compares);
     }
+
+    /** distances per device call (and host buffer): 2^24 doubles = 128 MiB */
+    private static final long ROW_BLOCK_CELLS = 1L << 24;
 }

@@ -22,10 +22,14 @@ import org.theseed.genome.distance.methods.Measurer;
  * (:200-203): "KMER_GPU_K21".
  *
  * getDistance is called from the ForkJoin pool (one thread per method of a
- * pair); the context serialises device calls. Each call packs the measurer's
- * genome and genome2 as one two-set collection and computes their distance
- * (gdist_sets_pack + gdist_intersect_matrix): exact, the Java expression
- * 1 - I / (|A| + |B| - I) in fp64 on the device.
+ * pair); the context serialises device calls. The method keeps ONE genome
+ * cache for the run: a device collection to which each genome is appended
+ * the first time it is seen (gdist_sets_append, keyed by genome id), so a
+ * genome is packed once however many pairs name it; GenomePairList.prepare
+ * groups the pairs by id1 (:240), whose measurer holds id1's set. getDistance
+ * is then one row query of id1's set against id2's cached set
+ * (gdist_row_query): exact, the Java expression 1 - I / (|A| + |B| - I) in
+ * fp64 on the device.
  */
 public class GpuKmerMethod extends DistanceMethod {
 
@@ -33,6 +37,9 @@ public class GpuKmerMethod extends DistanceMethod {
     private int kind = GpuKmerSets.DNA;
     private int device = 0;
     private GpuKmerSets.Context ctx;
+    // the genome cache: one collection, genome id -> set index
+    private GpuKmerSets cache;
+    private final Map<String, Integer> setIndex = new HashMap<String, Integer>();
 
     @Override
     public void parseParmString(String parms) {
@@ -63,6 +70,29 @@ public class GpuKmerMethod extends DistanceMethod {
 
     int kind() { return this.kind; }
 
+    /** the set of a genome in the cache, packed and appended on first sight */
+    synchronized int setOf(Genome genome) {
+        Integer i = this.setIndex.get(genome.getId());
+        if (i == null) {
+            byte[][] seq = { GpuGenomeProcessor.contigBytes(genome) };
+            if (this.cache == null) {
+                this.cache = new GpuKmerSets(this.context(), this.kind, this.k, seq);
+                i = 0;
+            } else {
+                i = (int) this.cache.append(seq);
+            }
+            this.setIndex.put(genome.getId(), i);
+        }
+        return i;
+    }
+
+    /** the distance of cached sets i and j (one device row query) */
+    synchronized double distance(int i, int j) {
+        double[] d = new double[1];
+        this.cache.row(i, new long[] { j }, d);
+        return d[0];
+    }
+
     @Override
     public Measurer getMeasurer(Genome genome) {
         return new GpuMeasurer(this, genome);
@@ -80,6 +110,11 @@ public class GpuKmerMethod extends DistanceMethod {
 
     @Override
     public synchronized void close() {
+        if (this.cache != null) {
+            this.cache.close();
+            this.cache = null;
+            this.setIndex.clear();
+        }
         if (this.ctx != null) {
             this.ctx.close();
             this.ctx = null;

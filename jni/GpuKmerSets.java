@@ -20,6 +20,8 @@ public final class GpuKmerSets implements AutoCloseable {
     static native void nCtxDestroy(long ctx);
     static native void nSetOption(long ctx, String name, long value);
     static native long nPack(long ctx, int kind, int k, int flags, byte[][] seqs);
+    static native long nAppend(long ctx, long sets, byte[][] seqs);
+    static native long nConcat(long a, long b);
     static native void nFree(long sets);
     static native long nSize(long sets);
     static native void nSizes(long sets, long[] out);
@@ -33,6 +35,8 @@ public final class GpuKmerSets implements AutoCloseable {
     static native long nGreedyReps(long ctx, long sets, double t, long[] tieRank, int[] isRep, long[] repOf,
                                    double[] repDist);
     static native long nSketch(long ctx, long sets, int width);
+    static native long nTotal(long sets);
+    static native void nSketchDownload(long sk, long[] off, int[] sigs);
     static native void nSketchMatrix(long ctx, long sk, long r0, long r1, long c0, long c1, int flags,
                                      double[] out, int ld);
 
@@ -60,6 +64,14 @@ public final class GpuKmerSets implements AutoCloseable {
         this.ctx = ctx;
         this.handle = handle;
     }
+
+    /** kmer sets of `seqs` packed with this collection's spec and appended
+     *  (gdist_sets_append); returns the index of the first new set */
+    public long append(byte[][] seqs) { return nAppend(ctx, handle, seqs); }
+
+    /** a new collection: this one's sets, then other's (gdist_sets_concat; codes
+     *  copied on the device, nothing re-packed) */
+    public GpuKmerSets concat(GpuKmerSets other) { return new GpuKmerSets(ctx, nConcat(handle, other.handle)); }
 
     /** the number of sets */
     public long size() { return nSize(handle); }
@@ -108,6 +120,19 @@ public final class GpuKmerSets implements AutoCloseable {
      *  (WidthProcessor.java:183-185), row-major with stride ld */
     public void sketchDistances(long r0, long r1, long c0, long c1, boolean upperTriangle, double[] out, int ld) {
         nSketchMatrix(ctx, handle, r0, r1, c0, c1, upperTriangle ? UPPER_TRIANGLE : 0, out, ld);
+    }
+
+    /** the signatures of a sketch collection (hashSet(width) of each set,
+     *  ascending ints; shorter than the width for a small set: a "dwarf") */
+    public int[][] signatures() {
+        final int n = (int) size();
+        long[] off = new long[n + 1];
+        int[] sigs = new int[(int) nTotal(handle)];
+        nSketchDownload(handle, off, sigs);
+        int[][] out = new int[n][];
+        for (int i = 0; i < n; i++)
+            out[i] = java.util.Arrays.copyOfRange(sigs, (int) off[i], (int) off[i + 1]);
+        return out;
     }
 
     @Override

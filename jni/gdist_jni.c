@@ -86,11 +86,13 @@ JNIEXPORT void JNICALL JFN(nSetOption)(JNIEnv* env, jclass c, jlong ctx, jstring
 }
 
 /* ---- kmer sets: KmerType.createKmers / new GenomeKmers / new ProteinKmers - */
-JNIEXPORT jlong JNICALL JFN(nPack)(JNIEnv* env, jclass c, jlong ctx, jint kind, jint k, jint flags,
-                                   jobjectArray seqs) {
+/* The byte arrays of seqs as one buffer + int64 offsets (n + 1), copied out
+ * with GetByteArrayRegion (no array pinned across a library call). Returns
+ * the element count, -1 with an exception pending. */
+static jsize gather_seqs(JNIEnv* env, jobjectArray seqs, char** blob_out, int64_t** off_out) {
     const jsize n = (*env)->GetArrayLength(env, seqs);
     int64_t* off = malloc(((size_t)n + 1) * sizeof(int64_t));
-    if (!off) { throw_oom(env); return 0; }
+    if (!off) { throw_oom(env); return -1; }
     off[0] = 0;
     for (jsize i = 0; i < n; i++) {
         jbyteArray a = (*env)->GetObjectArrayElement(env, seqs, i);
@@ -98,19 +100,52 @@ JNIEXPORT jlong JNICALL JFN(nPack)(JNIEnv* env, jclass c, jlong ctx, jint kind, 
         if (a) (*env)->DeleteLocalRef(env, a);
     }
     char* blob = malloc((size_t)off[n] + 1);
-    if (!blob) { free(off); throw_oom(env); return 0; }
+    if (!blob) { free(off); throw_oom(env); return -1; }
     for (jsize i = 0; i < n; i++) {
         jbyteArray a = (*env)->GetObjectArrayElement(env, seqs, i);
         if (a) {
             (*env)->GetByteArrayRegion(env, a, 0, (jsize)(off[i + 1] - off[i]), (jbyte*)blob + off[i]);
             (*env)->DeleteLocalRef(env, a);
-            if ((*env)->ExceptionCheck(env)) { free(blob); free(off); return 0; }
+            if ((*env)->ExceptionCheck(env)) { free(blob); free(off); return -1; }
         }
     }
+    *blob_out = blob;
+    *off_out = off;
+    return n;
+}
+
+JNIEXPORT jlong JNICALL JFN(nPack)(JNIEnv* env, jclass c, jlong ctx, jint kind, jint k, jint flags,
+                                   jobjectArray seqs) {
+    char* blob = NULL;
+    int64_t* off = NULL;
+    const jsize n = gather_seqs(env, seqs, &blob, &off);
+    if (n < 0) return 0;
     gdist_sets* s = NULL;
     int rc = gdist_sets_pack(CTX(ctx), kind, k, (unsigned)flags, blob, off, n, &s);
     free(blob);
     free(off);
+    if (rc) { throw_for(env, rc); return 0; }
+    return (jlong)(intptr_t)s;
+}
+
+/* more sequences packed into an existing collection (a genome cache that
+ * packs each genome once): the index of the first new set */
+JNIEXPORT jlong JNICALL JFN(nAppend)(JNIEnv* env, jclass c, jlong ctx, jlong sets, jobjectArray seqs) {
+    char* blob = NULL;
+    int64_t* off = NULL;
+    const jsize n = gather_seqs(env, seqs, &blob, &off);
+    if (n < 0) return 0;
+    int64_t first = 0;
+    int rc = gdist_sets_append(CTX(ctx), SETS(sets), blob, off, n, &first);
+    free(blob);
+    free(off);
+    if (rc) { throw_for(env, rc); return 0; }
+    return (jlong)first;
+}
+
+JNIEXPORT jlong JNICALL JFN(nConcat)(JNIEnv* env, jclass c, jlong a, jlong b) {
+    gdist_sets* s = NULL;
+    int rc = gdist_sets_concat(SETS(a), SETS(b), &s);
     if (rc) { throw_for(env, rc); return 0; }
     return (jlong)(intptr_t)s;
 }
@@ -269,6 +304,38 @@ JNIEXPORT jlong JNICALL JFN(nSketch)(JNIEnv* env, jclass c, jlong ctx, jlong set
     int rc = gdist_sketch_build(CTX(ctx), SETS(sets), width, &sk);
     if (rc) { throw_for(env, rc); return 0; }
     return (jlong)(intptr_t)sk;
+}
+
+/* the total number of codes (hashes, for a sketch collection) */
+JNIEXPORT jlong JNICALL JFN(nTotal)(JNIEnv* env, jclass c, jlong sets) {
+    int kind = 0, k = 0;
+    int64_t n = 0, total = 0;
+    int rc = gdist_sets_info(SETS(sets), &kind, &k, &n, &total);
+    if (rc) { throw_for(env, rc); return 0; }
+    return (jlong)total;
+}
+
+/* the signatures of a sketch collection (Sketch.getSignature of each set,
+ * SketchProcessor.java:88): off[nsets + 1] and sigs[total], ascending ints */
+JNIEXPORT void JNICALL JFN(nSketchDownload)(JNIEnv* env, jclass c, jlong sk, jlongArray off, jintArray sigs) {
+    int kind = 0, k = 0;
+    int64_t n = 0, total = 0;
+    int rc = gdist_sets_info(SETS(sk), &kind, &k, &n, &total);
+    if (rc) { throw_for(env, rc); return; }
+    if (too_short(env, off, n + 1, "off shorter than the number of sets + 1") ||
+        too_short(env, sigs, total, "sigs shorter than the collection's hashes"))
+        return;
+    int64_t* o = malloc(((size_t)n + 1) * sizeof(int64_t));
+    int32_t* v = malloc(((size_t)total + 1) * sizeof(int32_t));
+    if (!o || !v) { free(o); free(v); throw_oom(env); return; }
+    rc = gdist_sketch_download(SETS(sk), o, v);
+    if (!rc) {
+        (*env)->SetLongArrayRegion(env, off, 0, (jsize)(n + 1), (const jlong*)o);
+        if (!(*env)->ExceptionCheck(env)) (*env)->SetIntArrayRegion(env, sigs, 0, (jsize)total, (const jint*)v);
+    }
+    free(o);
+    free(v);
+    if (rc) throw_for(env, rc);
 }
 
 JNIEXPORT void JNICALL JFN(nSketchMatrix)(JNIEnv* env, jclass c, jlong ctx, jlong sk, jlong r0, jlong r1, jlong c0,

@@ -207,3 +207,121 @@ def test_shim_on_device_vs_oracle(jvm):
         assert jvm.exception() is None
     jvm.call("nCtxDestroy", None, ctx)
     assert jvm.exception() is None
+
+
+class _KmerMethodMirror:
+    """jni/GpuKmerMethod.java + GpuMeasurer.java, statement for statement, over
+    the shim's natives: setOf packs a genome the first time its id is seen
+    (nPack for the first, nAppend after), getMeasurer holds id1's set,
+    getDistance is one nRow of id1's set against id2's."""
+
+    def __init__(self, jvm, ctx, k):
+        self.jvm, self.ctx, self.k = jvm, ctx, k
+        self.cache = 0
+        self.set_index = {}
+        self.packs = 0
+
+    def set_of(self, gid, seq):
+        import ctypes as C
+        i = self.set_index.get(gid)
+        if i is None:
+            arr = self.jvm.byte_arrays([seq])
+            if self.cache == 0:
+                self.cache = self.jvm.call_i("nPack", C.c_int64, [C.c_int64, C.c_int32, C.c_int32, C.c_int32,
+                                                                  C.c_void_p], self.ctx, 0, self.k, 0, arr)
+                i = 0
+            else:
+                i = self.jvm.call("nAppend", C.c_int64, self.ctx, self.cache, C.c_void_p(arr))
+            assert self.jvm.exception() is None
+            self.packs += 1
+            self.set_index[gid] = i
+        return i
+
+    def distance(self, i, j):
+        import ctypes as C
+        from jni_harness.harness import LONG, DOUBLE
+        d = self.jvm.zeros(DOUBLE, 1)
+        self.jvm.call("nRow", None, self.ctx, self.cache, i, C.c_void_p(self.jvm.array(LONG, [j])), C.c_void_p(d))
+        assert self.jvm.exception() is None
+        return self.jvm.read(d, DOUBLE, 1)[0]
+
+
+@pytest.mark.gpu
+def test_java_measurer_packs_each_genome_once(jvm):
+    """the `methods` drop-in (GpuKmerMethod / GpuMeasurer)
+    driven as MethodTableProcessor drives it (pairs grouped by id1,
+    GenomePairList.prepare :240; getMeasurer per group :261-265; getDistance
+    per pair :275): every genome is packed exactly once (nPack / nAppend),
+    however many pairs name it, and every distance equals the oracle's."""
+    import ctypes as C
+    import random
+    import oracle
+    from gdist import synth
+    n = 24
+    seqs = [bytes(r) for r in synth.genomes(n, 6000, 0.03, 37)]
+    off, codes = oracle.pack(seqs, 21, 0, 0)
+    _, eD = oracle.matrix(off, codes, 0, n, 0, n)
+    rng = random.Random(5)
+    pairs = sorted({(rng.randrange(n), rng.randrange(n)) for _ in range(120)})   # grouped by id1
+    ctx = jvm.call_i("nCtxCreate", C.c_int64, [C.c_int32], 0)
+    m = _KmerMethodMirror(jvm, ctx, 21)
+    id1, set1 = None, None
+    seen = set()
+    for a, b in pairs:
+        if a != id1:                                    # a new first genome: getMeasurer
+            id1, set1 = a, m.set_of(f"g{a}", seqs[a])
+        seen.update((a, b))
+        d = m.distance(set1, m.set_of(f"g{b}", seqs[b]))
+        assert np.float64(d).view(np.uint64) == eD[a, b].view(np.uint64), (a, b, d, eD[a, b])
+    assert m.packs == len(seen)                         # once per genome
+    assert jvm.call("nSize", C.c_int64, m.cache) == len(seen)
+    jvm.call("nFree", None, m.cache)
+    jvm.call("nCtxDestroy", None, ctx)
+    assert jvm.exception() is None
+
+
+@pytest.mark.gpu
+def test_java_genome_and_sketch_natives(jvm):
+    """GpuGenomeProcessor's per-directory step (the base packed once,
+    nConcat of the directory's sets and the base, row blocks of nMatrix) and
+    GpuSketchProcessor's signatures (nSketch + nTotal + nSketchDownload)
+    against the oracle."""
+    import ctypes as C
+    import oracle
+    from gdist import synth
+    from jni_harness.harness import LONG, DOUBLE, INT
+    base = [bytes(r) for r in synth.genomes(9, 5000, 0.04, 38)]
+    comp = [bytes(r) for r in synth.genomes(5, 5000, 0.04, 39)]
+    ctx = jvm.call_i("nCtxCreate", C.c_int64, [C.c_int32], 0)
+    pk = [C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_void_p]
+    hb = jvm.call_i("nPack", C.c_int64, pk, ctx, 0, 21, 0, jvm.byte_arrays(base))
+    hc = jvm.call_i("nPack", C.c_int64, pk, ctx, 0, 21, 0, jvm.byte_arrays(comp))
+    both = jvm.call("nConcat", C.c_int64, hc, hb)
+    assert jvm.exception() is None and jvm.call("nSize", C.c_int64, both) == 14
+    m, nb = len(comp), len(base)
+    off, codes = oracle.pack(comp + base, 21, 0, 0)
+    _, eD = oracle.matrix(off, codes, 0, m, m, m + nb)
+    rows = 2                                            # ROW_BLOCK_CELLS / nMain, scaled down
+    for r0 in range(0, m, rows):
+        r1 = min(m, r0 + rows)
+        d = jvm.zeros(DOUBLE, rows * nb)
+        jvm.call_i("nMatrix", None, [C.c_int64] * 6 + [C.c_int32, C.c_int32, C.c_void_p, C.c_int32],
+                   ctx, both, r0, r1, m, m + nb, 0, 0, d, nb)
+        assert jvm.exception() is None
+        got = np.array(jvm.read(d, DOUBLE, (r1 - r0) * nb)).reshape(r1 - r0, nb)
+        assert np.array_equal(got.view(np.uint64), eD[r0:r1].view(np.uint64))
+    sk = jvm.call_i("nSketch", C.c_int64, [C.c_int64, C.c_int64, C.c_int32], ctx, hb, 100)
+    total = jvm.call("nTotal", C.c_int64, sk)
+    so, sv = jvm.zeros(LONG, nb + 1), jvm.zeros(INT, total)
+    jvm.call("nSketchDownload", None, sk, C.c_void_p(so), C.c_void_p(sv))
+    assert jvm.exception() is None
+    o, v = jvm.read(so, LONG, nb + 1), jvm.read(sv, INT, total)
+    bo, bc = oracle.pack(base, 21, 0, 0)
+    for i in range(nb):
+        assert v[o[i]:o[i + 1]] == list(oracle.sketch(bc[bo[i]:bo[i + 1]], 21, 0, 100)), i
+    jvm.call("nSketchDownload", None, sk, C.c_void_p(jvm.zeros(LONG, nb)), C.c_void_p(sv))
+    assert jvm.exception() == ("java/lang/IllegalArgumentException", "off shorter than the number of sets + 1")
+    for h in (sk, both, hc, hb):
+        jvm.call("nFree", None, h)
+    jvm.call("nCtxDestroy", None, ctx)
+    assert jvm.exception() is None
