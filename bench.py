@@ -235,6 +235,7 @@ def main():
             with stdout_to_stderr():
                 ctx.comm_init(obj[0], world, rank)
     xplan = None
+    build_t = None
     codes_gathered = False
     if exchange and method in ("auto", "bitset", "sorted"):
         # the exchange every rank takes (collective): the dictionary exchange
@@ -265,6 +266,11 @@ def main():
                         "est_bitset_s": round(cb, 4), "est_sorted_s": round(cs, 4), "after": "code all-gather"}
                 method = auto["chosen"]
                 local = gathered
+                if method == "bitset":
+                    # the tiers are built (split by rank on a multi-rank
+                    # communicator): the gathered codes are not read again
+                    build_t = gathered.build_timing()
+                    gathered.release_codes()
             codes_gathered = True            # the gathered collection is what the step reads
     elif method == "auto":
         # METHOD_AUTO's own decision on one GPU (gdist_sets_prepare)
@@ -618,7 +624,9 @@ def main():
             "cpu_baseline": cpu,
             "cpu_optimized": cpu_opt,
             "setup_s": {"generate": round(gen_s, 2), "host_free": round(free_s, 3), "pack": round(pack_s, 2), "represent": round(represent_s, 2),
-                        "total": round(setup_s, 2)},
+                        "total": round(setup_s, 2),
+                        "build": ({k: (round(v, 1) if isinstance(v, float) else v) for k, v in build_t.items()}
+                                  if build_t else None)},
             "end_to_end": {"pairs_per_s": round(pairs_job / e2e_s, 1), "seconds": round(e2e_s, 3),
                            "first_call_s": round(first_call_s, 4) if first_call_s is not None else None,
                            "plan_s": (round(first_call_s - elapsed_max / args.steps, 4)

@@ -292,6 +292,65 @@ __global__ __launch_bounds__(NT) void rare_rows_kernel(const int64_t* __restrict
     }
 }
 
+// Rare tier, row-major over a wide column range (round 5; C4's 100,000
+// columns would need 7 LDS chunks, and rare_rows_kernel walks every list of
+// the row once PER CHUNK, filtering its members to the chunk: 10.2 ms on the
+// C4 slice for 0.9 GB of algorithmic bytes). Here each (set, list) record of
+// the row is walked ONCE and every member in [lo, c1) adds the list's weight
+// straight into I's row with a device-scope atomic (the dense tiles and the
+// variant walk beside it add atomically too). A thread takes one record
+// (16-byte member loads, as rare_rows_kernel); long lists go to the whole
+// wave. Grid: rows x nsplit slices of the row's records.
+template <typename M>
+__global__ __launch_bounds__(256) void rare_rows_direct_kernel(const int64_t* __restrict__ soff,
+                                                               const uint64_t* __restrict__ sent,
+                                                               const uint32_t* __restrict__ sw,
+                                                               const uint16_t* __restrict__ sskip,
+                                                               const M* __restrict__ psets, int64_t r0, int64_t r1,
+                                                               int64_t c0, int64_t c1, int nsplit, int upper,
+                                                               int32_t* __restrict__ I, int64_t ldI) {
+    constexpr int PER = 16 / (int)sizeof(M);
+    const int64_t i = r0 + blockIdx.x / nsplit;
+    const int split = blockIdx.x % nsplit;
+    if (i >= r1) return;
+    const int64_t lo = upper && i + 1 > c0 ? i + 1 : c0;
+    if (lo >= c1) return;
+    int32_t* row = I + (i - r0) * ldI - c0;                 // row[t] for column t
+    const int64_t rb = soff[i], re = soff[i + 1];
+    const int64_t per = (re - rb + nsplit - 1) / nsplit;
+    const int64_t xb = rb + per * split;
+    const int64_t xe = xb + per < re ? xb + per : re;
+    const int lane = threadIdx.x & 63;
+    for (int64_t xbase = xb; xbase < xe; xbase += blockDim.x) {   // wave-uniform trip count
+        const int64_t x = xbase + threadIdx.x;
+        const uint64_t ent = x < xe ? sent[x] : 0ull;
+        const int32_t w = x < xe ? (int32_t)sw[x] : 0;
+        const int64_t b0 = (int64_t)(ent >> 24), e = b0 + (int64_t)(ent & 0xFFFFFFu);
+        const int64_t b = upper && x < xe ? b0 + sskip[x] : b0;
+        const bool lng = e - b >= kLongList;
+        for (unsigned long long m = __ballot(lng); m; m &= m - 1) {
+            const int l = __ffsll((long long)m) - 1;
+            const int64_t lb = __shfl((long long)b, l, 64), le = __shfl((long long)e, l, 64);
+            const int32_t lw = __shfl(w, l, 64);
+            for (int64_t y = lb + lane; y < le; y += 64) {
+                const int64_t t = psets[y];
+                if (t >= lo && t < c1 && t != i) atomicAdd(row + t, lw);
+            }
+        }
+        if (lng) continue;
+#pragma unroll 2
+        for (int64_t y = b; y < e; y += PER) {
+            M mem[PER];
+            __builtin_memcpy(mem, psets + y, 16);
+#pragma unroll
+            for (int u = 0; u < PER; u++) {
+                const int64_t t = mem[u];
+                if (y + u < e && t >= lo && t < c1 && t != i) atomicAdd(row + t, w);
+            }
+        }
+    }
+}
+
 // Rare tier of one query set q: cnt[t] += shared rare kmers of q and t
 // (global atomics, one row's worth); gather_add adds cnt[cols[c]] to I[c]
 // for every requested column position (duplicates included).
@@ -1649,8 +1708,10 @@ void bits_from_positions(gdist_ctx* ctx, const gdist_sets* s, const uint32_t* po
 void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_t U, int64_t W,
                unsigned long long* bits, const uint64_t* rare, int64_t Ur, int64_t id_base,
                unsigned long long* rare_out, int64_t rare_cap, int64_t* rare_written, const uint32_t* perm,
-               const FillHook& hook) {
+               const FillHook& hook, int64_t sa, int64_t sb) {
     hipStream_t st = ctx->stream;
+    if (sb < 0) sb = s->nsets;
+    GD_REQUIRE(0 <= sa && sa <= sb && sb <= s->nsets, "fill set range outside the collection");
     // Sets sparse against the dictionary (C3: 33 K codes a set against tens of
     // millions) give the windowed fill's segments windows past its LDS caps
     // even at 64 codes (dictionary entries per code of a set >= 12 dense or
@@ -1663,12 +1724,12 @@ void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_
     const bool sparse_sets = (double)U > 12.0 * per_set || (double)Ur > 32.0 * per_set;
     const int64_t opt = ctx->option(OPT_FILL_SORT, -1);
     if (U + Ur > 0 && (opt == 4 || (opt < 0 && sparse_sets))) {
-        hash_fill(ctx, s, dict, U, perm, rare, Ur, W, bits, id_base, rare_out, rare_cap, rare_written, hook);
+        hash_fill(ctx, s, dict, U, perm, rare, Ur, W, bits, id_base, rare_out, rare_cap, rare_written, hook, sa, sb);
         return;
     }
     const int cbits = std::min(64, code_bits(s->kind, s->k, s->flags));
     Trace tr(st, ctx->trace());
-    GD_HIP(hipMemsetAsync(bits, 0, (size_t)s->nsets * W * 8, st));
+    GD_HIP(hipMemsetAsync(bits + (size_t)sa * W, 0, (size_t)(sb - sa) * W * 8, st));
     DevBuf rcnt(8, st);
     GD_HIP(hipMemsetAsync(rcnt.p, 0, 8, st));
     // the hook needs the position arrays; option 5: pass 1 by fill_pos_kernel (one wave a segment)
@@ -1680,7 +1741,7 @@ void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_
         GD_REQUIRE(U <= (int64_t(1) << 31), "dense tier too large for u32 positions");   // keeps ~0 out of every row
         // segment length per set: its windows should fit the LDS caps (window ~ length x dictionary / set size)
         std::vector<int64_t> seg, first(s->nsets + 1, 0);
-        for (int64_t i = 0; i < s->nsets; i++) {
+        for (int64_t i = sa; i < sb; i++) {
             first[i] = (int64_t)seg.size();
             const double ni = (double)(s->h_off[i + 1] - s->h_off[i]);
             const double wd = wave_fill ? kWinDense : kMWin, wf = wave_fill ? kRareFences : kMFences;
@@ -1689,14 +1750,14 @@ void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_
             const int64_t L = std::max<int64_t>(64, std::min<int64_t>(wave_fill ? kPosSeg : kMSeg, (int64_t)(fit / 64) * 64));
             for (int64_t b = s->h_off[i]; b < s->h_off[i + 1]; b += L) seg.push_back((i << 40) | b);
         }
-        first[s->nsets] = (int64_t)seg.size();
+        first[sb] = (int64_t)seg.size();
         DevBuf dseg(std::max<int64_t>(1, (int64_t)seg.size()) * 8, st);
         if (!seg.empty()) h2d(dseg.p, seg.data(), seg.size() * 8, st);
         const unsigned nslice = (unsigned)ceil_div(2 * W, kPosSlice);
-        int64_t s0 = 0;
-        while (s0 < s->nsets) {
+        int64_t s0 = sa;
+        while (s0 < sb) {
             int64_t s1 = s0 + 1;
-            while (s1 < s->nsets && s->h_off[s1 + 1] - s->h_off[s0] <= kFillPosChunk) s1++;
+            while (s1 < sb && s->h_off[s1 + 1] - s->h_off[s0] <= kFillPosChunk) s1++;
             const int64_t base = s->h_off[s0], n = s->h_off[s1] - base, ns = first[s1] - first[s0];
             // sized like the summary's per-chunk key buffers (8 B a code) so that the caching
             // allocator hands back one of those blocks: a fresh 4 GiB block costs ~25 ms
@@ -1748,7 +1809,7 @@ void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_
         GD_REQUIRE(s->nsets < (int64_t(1) << 23) && s->h_off[s->nsets] < (int64_t(1) << 40),
                    "collection too large for packed fill segments");
         std::vector<int64_t> seg;
-        for (int64_t i = 0; i < s->nsets; i++)
+        for (int64_t i = sa; i < sb; i++)
             for (int64_t b = s->h_off[i]; b < s->h_off[i + 1]; b += kFillSeg) seg.push_back((i << 40) | b);
         const int64_t nseg = (int64_t)seg.size();
         if (nseg) {
@@ -1763,10 +1824,10 @@ void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_
         }
         tr.mark("fill: windowed searches + scatter");
     } else if (U + Ur > 0) {
-        int64_t s0 = 0;
-        while (s0 < s->nsets) {
+        int64_t s0 = sa;
+        while (s0 < sb) {
             int64_t s1 = s0 + 1;
-            while (s1 < s->nsets && s->h_off[s1 + 1] - s->h_off[s0] <= kBitsChunk) s1++;
+            while (s1 < sb && s->h_off[s1 + 1] - s->h_off[s0] <= kBitsChunk) s1++;
             const int64_t b = s->h_off[s0], n = s->h_off[s1] - b;
             if (n) {
                 DevBuf kA(n * 8, st), kB(n * 8, st), vA(n * 4, st), vB(n * 4, st);
@@ -2039,13 +2100,30 @@ void build_bitsets(gdist_ctx* ctx, gdist_sets* s, unsigned flags, int64_t rare_t
     // variant counts on top of the new bits); synchronises both streams
     free_bitsets(s);
     Trace tr(ctx->stream, ctx->trace());
+    const auto t_build = std::chrono::steady_clock::now();
+    BuildSplit sp = build_split(ctx, s);
+    // the build's wall time and its split stages (gdist_sets_build_timing)
+    struct BuildClock {
+        gdist_sets* s; BuildSplit& sp; hipStream_t st; std::chrono::steady_clock::time_point t0;
+        ~BuildClock() {
+            (void)hipStreamSynchronize(st);
+            s->build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            s->build_shares = sp.R;
+            s->build_split_ms = s->build_share_max_ms = 0;
+            for (double v : sp.share_ms) {
+                s->build_split_ms += v;
+                s->build_share_max_ms = std::max(s->build_share_max_ms, v);
+            }
+        }
+    } clock{s, sp, ctx->stream, t_build};
     Summary sum;
     // a collection without pack summaries and too many codes for one sort
     // (a gathered 8-GPU collection: C4's 2e10 codes) is counted by code
-    // ranges, singletons dropped as they are counted (option range_summary)
+    // ranges, singletons dropped as they are counted (option range_summary);
+    // a split build counts by ranges (its shares are code ranges)
     const int64_t rs_opt = ctx->option(OPT_RANGE_SUMMARY, -1);
-    const bool by_range = rs_opt > 0 || (rs_opt < 0 && s->pack_sum.empty() && s->total > kRangeSummaryMin);
-    if (by_range) range_summary(ctx, s, keep ? 1 : 2, sum);
+    const bool by_range = rs_opt > 0 || (rs_opt < 0 && ((s->pack_sum.empty() && s->total > kRangeSummaryMin) || sp.R > 1));
+    if (by_range) range_summary(ctx, s, keep ? 1 : 2, sum, sp);
     else local_summary(ctx, s, sum);
     tr.mark("bitsets: summary");
     DevBuf dict, rare, dcnt;
@@ -2074,7 +2152,7 @@ void build_bitsets(gdist_ctx* ctx, gdist_sets* s, unsigned flags, int64_t rare_t
             }
             sum.codes.release();
             sum.counts.release();
-            build_variant_bitsets(ctx, s, dict, dcnt, U, rare, Ur, mass, T);
+            build_variant_bitsets(ctx, s, dict, dcnt, U, rare, Ur, mass, T, sp);
             return;
         }
     }
@@ -2088,12 +2166,24 @@ void build_bitsets(gdist_ctx* ctx, gdist_sets* s, unsigned flags, int64_t rare_t
     }
     s->fp4.release();                    // the MFMA operand expanded the old bits
     s->fp4_W = 0;
-    s->bits.alloc((size_t)s->nsets * W * 8 + 8, ctx->stream);
+    // rows of R equal shares (split build): slot r of the in-place all-gather
+    const int64_t mrows = BuildSplit::ceil_div_h(s->nsets, sp.R);
+    s->bits.alloc((size_t)sp.R * mrows * W * 8 + 8, ctx->stream);
     DevBuf recs(mass * 8 + 8, ctx->stream);
     int64_t written = 0;
     tr.mark("bitsets: alloc");
-    fill_bits(ctx, s, dict.as<uint64_t>(), U, W, s->bits.as<unsigned long long>(), rare.as<uint64_t>(), Ur, 0,
-              recs.as<unsigned long long>(), mass, &written, perm.as<uint32_t>());
+    for (int r = sp.first(); r < sp.last(); r++) {
+        ShareClock clk(sp, r, ctx->stream);
+        int64_t w = 0;
+        fill_bits(ctx, s, dict.as<uint64_t>(), U, W, s->bits.as<unsigned long long>(), rare.as<uint64_t>(), Ur, 0,
+                  recs.as<unsigned long long>() + written, mass - written, &w, perm.as<uint32_t>(), FillHook(),
+                  sp.set_lo(r, s->nsets), sp.set_hi(r, s->nsets));
+        written += w;
+    }
+    if (sp.real) {
+        comm_allgather_inplace(ctx, s->bits.p, (size_t)mrows * W * 8);
+        written = allgather_concat(ctx, recs, written, 8);
+    }
     tr.mark("bitsets: fill");
     GD_REQUIRE(written == mass, "rare-tier record count mismatch");
     build_postings(ctx, s, recs.as<unsigned long long>(), written, Ur);
@@ -2359,6 +2449,28 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     bool rare_done = false;               // the sparse chunk reduce added the rare pairs
     auto launch_rare_rows = [&](hipStream_t rs, bool atomic_flush) {
         const int nch = (int)ceil_div(nc, RCH);
+        // past one LDS chunk of columns every record once, members added to I
+        // by atomics (option rare_direct; the LDS kernel re-walks the row's
+        // lists once per chunk)
+        if (ctx->option(OPT_RARE_DIRECT, nch > 1 ? 1 : 0) != 0) {
+            const int dsplit = (int)std::max<int64_t>(1, std::min<int64_t>(64, ceil_div((int64_t)ctx->cus * 8, nr)));
+            const int64_t dgrid = nr * dsplit;
+            GD_REQUIRE(dgrid < (int64_t(1) << 31), "rare-tier grid too large");
+            FamilyTimer ft(ctx, GDIST_KERNEL_RARE, rs);
+            if (s->post_sets16.p)
+                rare_rows_direct_kernel<uint16_t><<<(unsigned)dgrid, 256, 0, rs>>>(
+                    s->srare_off.as<int64_t>(), s->srare_ent.as<uint64_t>(), s->srare_w.as<uint32_t>(),
+                    s->srare_skip.as<uint16_t>(), s->post_sets16.as<uint16_t>(), r0, r1, c0, c1, dsplit,
+                    upper ? 1 : 0, d_I, ldI);
+            else
+                rare_rows_direct_kernel<uint32_t><<<(unsigned)dgrid, 256, 0, rs>>>(
+                    s->srare_off.as<int64_t>(), s->srare_ent.as<uint64_t>(), s->srare_w.as<uint32_t>(),
+                    s->srare_skip.as<uint16_t>(), s->post_sets.as<uint32_t>(), r0, r1, c0, c1, dsplit,
+                    upper ? 1 : 0, d_I, ldI);
+            GD_HIP(hipGetLastError());
+            ft.end();
+            return;
+        }
         const int64_t units = nr * nch;
         // few rows (C2: 1000): slice each row's rare kmers over several workgroups
         const int nsplit = (int)std::max<int64_t>(1, std::min<int64_t>(16, ceil_div((int64_t)ctx->cus * 8, units)));

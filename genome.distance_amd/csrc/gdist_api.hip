@@ -211,6 +211,81 @@ static void finish_timing(gdist_ctx* ctx, bool kernel_recorded, bool async = fal
     if (!async) settle_timing(ctx);
 }
 
+bool comm_active(const gdist_ctx* ctx) { return has_comm(ctx) && ctx->nranks > 1; }
+
+void comm_allgather_inplace(gdist_ctx* ctx, void* d_buf, size_t bytes) { allgather_inplace(ctx, d_buf, bytes); }
+
+int64_t allgather_concat(gdist_ctx* ctx, DevBuf& buf, int64_t n, size_t es) {
+    hipStream_t st = ctx->stream;
+    const int R = ctx->nranks, me = ctx->rank;
+    std::vector<int64_t> hn(R);
+    {
+        DevBuf mine(8, st), all(8 * R, st);
+        h2d(mine.p, &n, 8, st);
+        allgather(ctx, mine.p, all.p, 8);
+        d2h(hn.data(), all.p, 8 * R, st);
+    }
+    int64_t mx = 0, tot = 0;
+    for (int64_t v : hn) { mx = std::max(mx, v); tot += v; }
+    const size_t slot = (size_t)mx * es;
+    DevBuf g(slot * R + 8, st);
+    if (n) GD_HIP(hipMemcpyAsync(static_cast<char*>(g.p) + slot * me, buf.p, (size_t)n * es, hipMemcpyDeviceToDevice, st));
+    buf.release();
+    if (slot) allgather_inplace(ctx, g.p, slot);
+    // slot r's elements move down to the sum of the earlier counts (staged
+    // when source and destination overlap)
+    DevBuf stage;
+    int64_t at = 0;
+    for (int r = 0; r < R; r++) {
+        char* src = static_cast<char*>(g.p) + slot * r;
+        char* dst = static_cast<char*>(g.p) + (size_t)at * es;
+        const size_t b = (size_t)hn[r] * es;
+        if (b && src != dst) {
+            if (dst + b <= src) {
+                GD_HIP(hipMemcpyAsync(dst, src, b, hipMemcpyDeviceToDevice, st));
+            } else {
+                if (!stage.p) stage.alloc(slot + 8, st);
+                GD_HIP(hipMemcpyAsync(stage.p, src, b, hipMemcpyDeviceToDevice, st));
+                GD_HIP(hipMemcpyAsync(dst, stage.p, b, hipMemcpyDeviceToDevice, st));
+            }
+        }
+        at += hn[r];
+    }
+    GD_HIP(hipStreamSynchronize(st));
+    buf = std::move(g);
+    return tot;
+}
+
+BuildSplit build_split(const gdist_ctx* ctx, const gdist_sets* s) {
+    BuildSplit sp;
+    const int64_t opt = ctx->option(OPT_SPLIT_BUILD, -1);
+    if (opt != 0 && s->replicated && comm_active(ctx)) {
+        sp.R = ctx->nranks;
+        sp.me = ctx->rank;
+        sp.real = true;
+    } else if (opt >= 2 && !comm_active(ctx)) {
+        sp.R = (int)std::min<int64_t>(opt, 1024);
+    }
+    sp.share_ms.assign(sp.R, 0.0);
+    return sp;
+}
+
+// one flag over the communicator: true when any rank's is
+static bool comm_any(gdist_ctx* ctx, bool v) {
+    hipStream_t st = ctx->stream;
+    const int R = ctx->nranks;
+    int32_t h = v ? 1 : 0;
+    DevBuf d(4, st), all(4 * R, st);
+    h2d(d.p, &h, 4, st);
+    allgather(ctx, d.p, all.p, 4);
+    std::vector<int32_t> hv(R);
+    d2h(hv.data(), all.p, 4 * R, st);
+    GD_HIP(hipStreamSynchronize(st));
+    for (int32_t x : hv)
+        if (x) return true;
+    return false;
+}
+
 }  // namespace gdist
 
 using namespace gdist;
@@ -515,6 +590,7 @@ int gdist_sets_append(gdist_ctx* ctx, gdist_sets* sets, const char* seqs, const 
         sets->max_seg = 0;
         sets->auto_sorted = false;
         sets->pack_sum.clear();
+        sets->replicated = false;             // this rank's sets only from here
         // codes: in place while the buffer's size class has room, else a
         // buffer of twice the need (n appends copy O(n) codes in all)
         const int64_t total = sets->total + add.total;
@@ -647,6 +723,35 @@ int gdist_sets_build_bitsets_ex(gdist_sets* s, unsigned flags, int64_t rare_thre
         use_device(s->ctx);
         std::lock_guard<std::recursive_mutex> lk(s->ctx->mu);
         build_bitsets(s->ctx, s, flags, rare_threshold);
+    });
+}
+
+int gdist_sets_release_codes(gdist_sets* s) {
+    return guard([&] {
+        check_sets(s);
+        GD_REQUIRE(s->kind != GDIST_SKETCH, "sketch collections hold signatures, not codes");
+        GD_REQUIRE(s->bits.p, "the collection holds no bitsets: its codes are its only representation");
+        use_device(s->ctx);
+        std::lock_guard<std::recursive_mutex> lk(s->ctx->mu);
+        GD_HIP(hipStreamSynchronize(s->ctx->stream));
+        s->codes.release();
+        s->segoff.release();
+        s->nseg = 0;
+        s->max_seg = 0;
+        s->pack_sum.clear();
+        s->has_codes = false;
+        gdist::cache_trim(s->ctx->device);
+    });
+}
+
+int gdist_sets_build_timing(const gdist_sets* s, double* build_ms, double* split_ms, double* share_max_ms,
+                            int* shares) {
+    return guard([&] {
+        check_sets(s);
+        if (build_ms) *build_ms = s->build_ms;
+        if (split_ms) *split_ms = s->build_split_ms;
+        if (share_max_ms) *share_max_ms = s->build_share_max_ms;
+        if (shares) *shares = s->build_shares;
     });
 }
 
@@ -788,7 +893,12 @@ int gdist_sets_concat(const gdist_sets* a, const gdist_sets* b, gdist_sets** out
 static int resolve_method(gdist_ctx* ctx, gdist_sets* s, int method, double pairs) {
     int m = method;
     if (m == GDIST_METHOD_AUTO) {
-        if (!s->bits.p && !s->auto_sorted && !s->segoff.p && s->has_codes && sorted_cost_s(s, pairs) >= 0.02) {
+        bool want = !s->bits.p && !s->auto_sorted && !s->segoff.p && s->has_codes && sorted_cost_s(s, pairs) >= 0.02;
+        // a gathered collection's build is collective (split by rank): every
+        // rank builds when any rank's region asks for it
+        if (s->replicated && comm_active(ctx) && ctx->option(OPT_SPLIT_BUILD, -1) != 0 && !s->bits.p && s->has_codes)
+            want = comm_any(ctx, want);
+        if (want) {
             try {
                 build_bitsets(ctx, s, 0);
             } catch (const Error& e) {
@@ -1412,6 +1522,7 @@ int gdist_sets_allgather_ex(gdist_ctx* ctx, gdist_sets* local, unsigned flags, g
             GD_HIP(hipStreamSynchronize(st));
         }
         s->codes = std::move(ac);                     // R x cb bytes; the compacted codes first
+        s->replicated = true;                         // the same collection on every rank
         s->guide_codes = std::move(gcodes);
         s->guide_keys = std::move(gkeys);
         s->n_guide = g0;

@@ -223,6 +223,7 @@ struct Timing {
     X(SPARSE_XCD, "sparse_xcd")               /* 1: chunk c of every sparse tile on XCD c mod 8 */           \
     X(RARE_U16, "rare_u16")                   /* 0: 4-byte list members in the row-major rare walk */        \
     X(RARE_ROWS_THREADS, "rare_rows_threads") /* row-major rare walk: threads a workgroup (256/512/1024; default by LDS) */ \
+    X(RARE_DIRECT, "rare_direct")             /* row-major rare walk: 1 every record once, members added to I by atomics; 0 LDS column chunks (default: direct past one chunk) */ \
     X(BITSET_MFMA, "bitset_mfma")             /* 0: dense tiles by AND+popcount instead of FP4 MFMA */       \
     X(BITSET_MFMA_KM, "bitset_mfma_km")       /* MFMA tiles: words per stage (4 default, 2: 64 KiB of LDS) */ \
     X(BITSET_MFMA_NS, "bitset_mfma_ns")       /* MFMA tiles with 2-word stages: stages in the ring (2..4) */    \
@@ -231,7 +232,8 @@ struct Timing {
     X(SORT_RADIX, "sort_radix")               /* 10: onesweep radix sorts of u64 keys in 10-bit passes (A/B) */\
     X(VARIANT, "variant")                     /* variant tier: 1 force, 0 off (default: by the dictionary) */ \
     X(VARIANT_DMIN, "variant_dmin")           /* sets holding a dense-tier kmer (default N / 10) */            \
-    X(RANGE_SUMMARY, "range_summary")         /* 1: the code-range dictionary whatever the size, 0: never */
+    X(RANGE_SUMMARY, "range_summary")         /* 1: the code-range dictionary whatever the size, 0: never */  \
+    X(SPLIT_BUILD, "split_build")             /* gathered collection on R ranks: each builds 1/R and all-gathers (default); 0 every rank all; k >= 2 without peers: k shares in turn here */
 
 enum Opt : int {
 #define GDIST_OPT_ENUM(id, name) OPT_##id,
@@ -332,6 +334,12 @@ struct gdist_sets {
     int nseg = 0;
     int64_t max_seg = 0;
     bool has_codes = true;                // false for all-gathered bitset-only collections
+    bool replicated = false;              // every rank of the communicator holds this same collection
+                                          // (the code all-gather's result): its build is split by rank
+    // the last bitset build: wall time, the split stages' time per share
+    // (summary ranges + fill sets; one rank's projection = the rest + the largest share)
+    double build_ms = 0, build_split_ms = 0, build_share_max_ms = 0;
+    int build_shares = 0;
     // rare tier of the dictionary: kmers held by 2..rare_T-1 sets as posting lists
     gdist::DevBuf post_off;               // int64 [n_rare+1]
     gdist::DevBuf post_sets;              // uint32 [rare_records], ascending within a list
@@ -459,13 +467,15 @@ using FillHook = std::function<void(const uint32_t* pos, int64_t s0, int64_t s1,
 // positions past the W words and ~0 are skipped): LDS row slices, no atomics
 void bits_from_positions(gdist_ctx* ctx, const gdist_sets* s, const uint32_t* pos, int64_t s0, int64_t s1,
                          int64_t base, int64_t W, unsigned long long* bits);
+// sets [sa, sb) (sb < 0: to the end): their rows of bits, their rare records
 void hash_fill(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_t U, const uint32_t* perm,
                const uint64_t* rare, int64_t Ur, int64_t W, unsigned long long* bits, int64_t id_base,
-               unsigned long long* rare_out, int64_t rare_cap, int64_t* rare_written, const FillHook& hook);
+               unsigned long long* rare_out, int64_t rare_cap, int64_t* rare_written, const FillHook& hook,
+               int64_t sa = 0, int64_t sb = -1);
 void fill_bits(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_t U, int64_t W,
                unsigned long long* bits, const uint64_t* rare, int64_t Ur, int64_t id_base,
                unsigned long long* rare_out, int64_t rare_cap, int64_t* rare_written,
-               const uint32_t* perm = nullptr, const FillHook& hook = FillHook());
+               const uint32_t* perm = nullptr, const FillHook& hook = FillHook(), int64_t sa = 0, int64_t sb = -1);
 void build_postings(gdist_ctx* ctx, gdist_sets* s, unsigned long long* recs, int64_t n, int64_t Ur);
 // Cost model (seconds), calibrated on MI355X from per-kernel rocprofv3
 // averages (scripts/calib_rare.sh; profiles/r01/rare_model): bitset = dense
@@ -553,6 +563,44 @@ void sparse_plan(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, in
 bool sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1, bool upper,
                    int32_t* d_I, int64_t ldI, hipStream_t st, SparseScratch& sc, const SparseEpilogue* ep = nullptr);
 
+// The bitset build of a replicated collection split by rank (option
+// split_build): share r counts the code ranges [Pe r / R, Pe (r + 1) / R) of
+// the summary and fills the sets [r m, (r + 1) m), m = ceil(N / R); the
+// summary, bits, rare records and variant entries are all-gathered. Without
+// peers (real = false) every share runs here in turn (option split_build = k:
+// the one-rank timing and parity of the split).
+struct BuildSplit {
+    int R = 1, me = 0;
+    bool real = false;
+    std::vector<double> share_ms;         // per share: the split stages' time
+    int first() const { return real ? me : 0; }
+    int last() const { return real ? me + 1 : R; }
+    int64_t set_lo(int r, int64_t n) const { return std::min<int64_t>(n, (int64_t)r * ceil_div_h(n, R)); }
+    int64_t set_hi(int r, int64_t n) const { return std::min<int64_t>(n, (int64_t)(r + 1) * ceil_div_h(n, R)); }
+    static int64_t ceil_div_h(int64_t a, int64_t b) { return (a + b - 1) / b; }
+};
+BuildSplit build_split(const gdist_ctx* ctx, const gdist_sets* s);
+// wall time of one share's stage (synchronises the stream at both ends)
+struct ShareClock {
+    BuildSplit& sp;
+    int r;
+    hipStream_t st;
+    std::chrono::steady_clock::time_point t;
+    ShareClock(BuildSplit& b, int share, hipStream_t s) : sp(b), r(share), st(s) {
+        GD_HIP(hipStreamSynchronize(st));
+        t = std::chrono::steady_clock::now();
+    }
+    ~ShareClock() {
+        (void)hipStreamSynchronize(st);
+        sp.share_ms[r] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+    }
+};
+// communicator (gdist_api.hip): true with peers (RCCL or the host transport)
+bool comm_active(const gdist_ctx* ctx);
+void comm_allgather_inplace(gdist_ctx* ctx, void* d_buf, size_t bytes);
+// every rank's n elements of es bytes (buf) concatenated in rank order into
+// buf; returns the total (one all-gather of the counts, one padded in place)
+int64_t allgather_concat(gdist_ctx* ctx, DevBuf& buf, int64_t n, size_t es);
 // variant.hip — the variant tier
 constexpr double kVariantProductsPerS = 2.0e10;  // variant_rows_kernel: popc products (estimate)
 constexpr int64_t kVariantMaxT = 32;             // rare threshold of a variant build (unless given)
@@ -566,14 +614,15 @@ int64_t count_in_range(gdist_ctx* ctx, const uint32_t* counts, int64_t n, int64_
 // builds bits (dense tier), the rare postings and the variant tier from the
 // dictionary (dict: codes held by >= T sets, dcounts their holders)
 void build_variant_bitsets(gdist_ctx* ctx, gdist_sets* s, DevBuf& dict, DevBuf& dcounts, int64_t U, DevBuf& rare,
-                           int64_t Ur, int64_t mass, int64_t T);
+                           int64_t Ur, int64_t mass, int64_t T, BuildSplit& sp);
 void free_variant(gdist_sets* s);
 void variant_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1, bool upper,
                     int32_t* d_I, int64_t ldI, hipStream_t rs);
 void variant_query(gdist_ctx* ctx, const gdist_sets* s, int64_t q, int32_t* cnt);
 // Summary of the codes held by >= min_count sets by ranges of the code space
-// (workspace: one range, not the collection: huge gathered collections)
-void range_summary(gdist_ctx* ctx, const gdist_sets* s, int min_count, Summary& out);
+// (workspace: one range, not the collection: huge gathered collections);
+// the ranges of this rank's shares, all-gathered when split
+void range_summary(gdist_ctx* ctx, const gdist_sets* s, int min_count, Summary& out, BuildSplit& sp);
 
 // sorted.hip
 void build_segments(gdist_ctx* ctx, gdist_sets* s);

@@ -589,17 +589,29 @@ __global__ __launch_bounds__(1024) void variant_rows_kernel(const int64_t* __res
                 const unsigned long long mi = vmask[e];
                 const int64_t ye = vend[e];
                 int64_t y = ypos[t];
-                for (; y < ye;) {
-                    const int64_t yy = y + lane;
-                    const uint32_t j = yy < ye ? vset[yy] : 0xFFFFFFFFu;
-                    const bool in = yy < ye && (int64_t)j < ce;
-                    if (in && (int64_t)j != i) {
-                        const int v = __popcll(mi & vmask[yy]);
-                        if (v) atomicAdd(&cnt[j - cb], v);
+                if (y < ye) {
+                    // the next 64 members are loaded before this step's are
+                    // counted (two steps of loads in flight a wave; round 5:
+                    // the walk waited out one load round trip per 64 members)
+                    int64_t yy = y + lane;
+                    uint32_t j = yy < ye ? vset[yy] : 0xFFFFFFFFu;
+                    unsigned long long mj = yy < ye ? vmask[yy] : 0ull;
+                    for (;;) {
+                        const bool in = yy < ye && (int64_t)j < ce;
+                        const int64_t yn = yy + 64;
+                        const uint32_t jn = yn < ye ? vset[yn] : 0xFFFFFFFFu;
+                        const unsigned long long mn = yn < ye ? vmask[yn] : 0ull;
+                        if (in && (int64_t)j != i) {
+                            const int v = __popcll(mi & mj);
+                            if (v) atomicAdd(&cnt[j - cb], v);
+                        }
+                        const unsigned long long m = __ballot(in);
+                        y += __popcll(m);                      // lists ascend: the in-chunk members come first
+                        if (m != ~0ull) break;
+                        yy = yn;
+                        j = jn;
+                        mj = mn;
                     }
-                    const unsigned long long m = __ballot(in);
-                    y += __popcll(m);                          // lists ascend: the in-chunk members come first
-                    if (m != ~0ull) break;
                 }
                 if (lane == 0) ypos[t] = (uint32_t)y;
             }
@@ -633,6 +645,10 @@ __global__ __launch_bounds__(256) void variant_query_kernel(const int64_t* __res
         }
     }
 }
+__global__ void viota_kernel(int32_t* __restrict__ p, int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = (int32_t)i;
+}
 }  // namespace
 
 // ---- host --------------------------------------------------------------------
@@ -640,14 +656,16 @@ __global__ __launch_bounds__(256) void variant_query_kernel(const int64_t* __res
 // Summary of the collection's codes held by >= min_count sets, by ranges of
 // the code space (P splitters from a sample of every set's codes): one range
 // of every set gathered, sorted, counted at a time.
-void range_summary(gdist_ctx* ctx, const gdist_sets* s, int min_count, Summary& out) {
+void range_summary(gdist_ctx* ctx, const gdist_sets* s, int min_count, Summary& out, BuildSplit& sp) {
     hipStream_t st = ctx->stream;
     Trace tr(st, ctx->trace());
     const int cbits = std::min(64, code_bits(s->kind, s->k, s->flags));
     const int64_t N = s->nsets, total = s->total;
-    // ranges of at most ~2^28 codes (about 4 GiB of sort buffers)
+    // ranges of at most ~2^28 codes (about 4 GiB of sort buffers), at least
+    // one per share of a split build; the sample and so the splitters are the
+    // same on every rank (the same codes)
     const int64_t target = int64_t(1) << 28;
-    const int P = (int)std::max<int64_t>(1, std::min<int64_t>(4096, ceil_div(total, target)));
+    const int P = (int)std::max<int64_t>(sp.R, std::min<int64_t>(4096, ceil_div(total, target)));
     std::vector<uint64_t> split;
     if (P > 1) {
         // sample: the codes at a stride (every set's codes are sorted, so
@@ -676,7 +694,8 @@ void range_summary(gdist_ctx* ctx, const gdist_sets* s, int min_count, Summary& 
     std::vector<Summary> parts;
     DevBuf cnt((N + 1) * 8, st), at((N + 1) * 8, st);
     int64_t kept = 0;
-    for (int p = 0; p < Pe; p++) {
+    // one code range of every set gathered, sorted, counted, the kept runs emitted
+    auto count_range = [&](int p) {
         range_sizes_kernel<<<(unsigned)ceil_div(N, 256), 256, 0, st>>>(spos.as<int64_t>(), N, Pe, p,
                                                                        cnt.as<int64_t>());
         GD_HIP(hipMemsetAsync(cnt.as<int64_t>() + N, 0, 8, st));
@@ -712,8 +731,12 @@ void range_summary(gdist_ctx* ctx, const gdist_sets* s, int min_count, Summary& 
         }
         kept += part.n;
         parts.push_back(std::move(part));
+    };
+    for (int r = sp.first(); r < sp.last(); r++) {
+        ShareClock clk(sp, r, st);
+        for (int p = (int)((int64_t)Pe * r / sp.R); p < (int)((int64_t)Pe * (r + 1) / sp.R); p++) count_range(p);
     }
-    // ranges ascend: the parts concatenate in code order
+    // ranges ascend (shares too): the parts concatenate in code order
     out.n = kept;
     out.codes.alloc(kept * 8 + 8, st);
     out.counts.alloc(kept * 4 + 4, st);
@@ -725,10 +748,18 @@ void range_summary(gdist_ctx* ctx, const gdist_sets* s, int min_count, Summary& 
         }
         o += pt.n;
     }
+    parts.clear();
+    if (sp.real) {
+        // the shares of every rank, in rank order: the whole summary
+        const int64_t mine = kept;
+        kept = allgather_concat(ctx, out.codes, mine, 8);
+        allgather_concat(ctx, out.counts, mine, 4);
+        out.n = kept;
+    }
     GD_HIP(hipStreamSynchronize(st));
     if (ctx->trace())
-        fprintf(stderr, "gdist: range summary: %d code ranges, %lld codes held by >= %d sets\n", Pe, (long long)kept,
-                min_count);
+        fprintf(stderr, "gdist: range summary: %d code ranges in %d shares, %lld codes held by >= %d sets\n", Pe, sp.R,
+                (long long)kept, min_count);
     tr.mark("variant: range summary");
 }
 
@@ -776,11 +807,14 @@ static CodeGeom code_geom(const gdist_sets* s) {
 // sparse against the dictionary (bitset.hip fill_bits: C3)
 void hash_fill(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_t U, const uint32_t* perm,
                const uint64_t* rare, int64_t Ur, int64_t W, unsigned long long* bits, int64_t id_base,
-               unsigned long long* rare_out, int64_t rare_cap, int64_t* rare_written, const FillHook& hook) {
+               unsigned long long* rare_out, int64_t rare_cap, int64_t* rare_written, const FillHook& hook,
+               int64_t sa, int64_t sb) {
     hipStream_t st = ctx->stream;
     Trace tr(st, ctx->trace());
+    if (sb < 0) sb = s->nsets;
+    GD_REQUIRE(0 <= sa && sa <= sb && sb <= s->nsets, "fill set range outside the collection");
     GD_REQUIRE(Ur < (int64_t(1) << 32) && U < (int64_t(1) << 32), "dictionary too large for the hash fill");
-    GD_HIP(hipMemsetAsync(bits, 0, (size_t)s->nsets * W * 8, st));
+    GD_HIP(hipMemsetAsync(bits + (size_t)sa * W, 0, (size_t)(sb - sa) * W * 8, st));
     int64_t cap = 2;
     while (cap < 2 * (U + Ur)) cap <<= 1;                   // load <= 1/2
     DevBuf tab((size_t)cap * 16 + 16, st), rcnt(8, st);                // + the out-of-band slot of code ~0
@@ -793,10 +827,10 @@ void hash_fill(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_
                                                                              tab.as<unsigned long long>(), mask);
     GD_HIP(hipGetLastError());
     tr.mark("fill: hash table");
-    int64_t s0 = 0;
-    while (s0 < s->nsets) {
+    int64_t s0 = sa;
+    while (s0 < sb) {
         int64_t s1 = s0 + 1;
-        while (s1 < s->nsets && s->h_off[s1 + 1] - s->h_off[s0] <= (int64_t(1) << 30)) s1++;
+        while (s1 < sb && s->h_off[s1 + 1] - s->h_off[s0] <= (int64_t(1) << 30)) s1++;
         const int64_t base = s->h_off[s0], n = s->h_off[s1] - base;
         DevBuf pos(std::max<int64_t>(1, n) * 4 + 16, st);
         hash_probe_kernel<<<(unsigned)(s1 - s0), 256, 0, st>>>(s->codes.as<uint64_t>(), s->off.as<int64_t>(), s0, base,
@@ -834,7 +868,7 @@ void free_variant(gdist_sets* s) {
 }
 
 void build_variant_bitsets(gdist_ctx* ctx, gdist_sets* s, DevBuf& dict, DevBuf& dcnt, int64_t U, DevBuf& rare,
-                           int64_t Ur, int64_t mass, int64_t T) {
+                           int64_t Ur, int64_t mass, int64_t T, BuildSplit& sp) {
     hipStream_t st = ctx->stream;
     Trace tr(st, ctx->trace());
     const int64_t N = s->nsets;
@@ -894,11 +928,7 @@ void build_variant_bitsets(gdist_ctx* ctx, gdist_sets* s, DevBuf& dict, DevBuf& 
                                                                          vkey.as<uint64_t>());
         GD_HIP(hipGetLastError());
         // iota values: the variant index; stable sort by key keeps code order within a group
-        {
-            std::vector<int32_t> io(Um);
-            for (int64_t m = 0; m < Um; m++) io[m] = (int32_t)m;
-            h2d(ord.p, io.data(), Um * 4, st);
-        }
+        viota_kernel<<<grid_for(Um), 256, 0, st>>>(ord.as<int32_t>(), Um);
         uint64_t* k = vkey.as<uint64_t>(); uint64_t* ka = vkalt.as<uint64_t>();
         int32_t* v = ord.as<int32_t>(); int32_t* va = oalt.as<int32_t>();
         sort_pairs_u64_i32(ctx, k, ka, v, va, (size_t)Um, 0, 64);
@@ -967,42 +997,64 @@ void build_variant_bitsets(gdist_ctx* ctx, gdist_sets* s, DevBuf& dict, DevBuf& 
     };
     s->fp4.release();                    // the MFMA operand expanded the old bits
     s->fp4_W = 0;
-    s->bits.alloc((size_t)N * Wd * 8 + 8, st);
+    // rows of R equal shares (m = ceil(N / R) sets, the last padded): share r's
+    // rows are slot r of the in-place all-gather
+    const int64_t mrows = BuildSplit::ceil_div_h(N, sp.R);
+    s->bits.alloc((size_t)sp.R * mrows * Wd * 8 + 8, st);
     DevBuf recs(mass * 8 + 8, st);
     int64_t written = 0;
-    // the hash fill (default) or the windowed fill of the two-tier build
-    // (option fill_sort = 3 selects the windowed one: A/B, parity)
-    if (ctx->option(OPT_FILL_SORT, 0) == 3)
-        fill_bits(ctx, s, dict.as<uint64_t>(), U, Wd, s->bits.as<unsigned long long>(), rare.as<uint64_t>(), Ur, 0,
-                  recs.as<unsigned long long>(), mass, &written, perm.as<uint32_t>(), hook);
-    else
-        hash_fill(ctx, s, dict.as<uint64_t>(), U, perm.as<uint32_t>(), rare.as<uint64_t>(), Ur, Wd,
-                  s->bits.as<unsigned long long>(), 0, recs.as<unsigned long long>(), mass, &written, hook);
+    for (int r = sp.first(); r < sp.last(); r++) {
+        ShareClock clk(sp, r, st);
+        const int64_t sa = sp.set_lo(r, N), sb = sp.set_hi(r, N);
+        int64_t w = 0;
+        // the hash fill (default) or the windowed fill of the two-tier build
+        // (option fill_sort = 3 selects the windowed one: A/B, parity)
+        if (ctx->option(OPT_FILL_SORT, 0) == 3)
+            fill_bits(ctx, s, dict.as<uint64_t>(), U, Wd, s->bits.as<unsigned long long>(), rare.as<uint64_t>(), Ur, 0,
+                      recs.as<unsigned long long>() + written, mass - written, &w, perm.as<uint32_t>(), hook, sa, sb);
+        else
+            hash_fill(ctx, s, dict.as<uint64_t>(), U, perm.as<uint32_t>(), rare.as<uint64_t>(), Ur, Wd,
+                      s->bits.as<unsigned long long>(), 0, recs.as<unsigned long long>() + written, mass - written, &w,
+                      hook, sa, sb);
+        written += w;
+    }
+    if (sp.real) {
+        // every rank's rows and rare records
+        comm_allgather_inplace(ctx, s->bits.p, (size_t)mrows * Wd * 8);
+        written = allgather_concat(ctx, recs, written, 8);
+    }
     GD_REQUIRE(written == mass, "rare-tier record count mismatch");
     tr.mark("variant: fill (dense bits, rare and variant records)");
     build_postings(ctx, s, recs.as<unsigned long long>(), written, Ur);
     recs.release();
     tr.mark("variant: rare postings");
-    // 6. entries of every chunk -> one list per word (sets ascending) + the set side
+    // 6. entries of every chunk (every rank's: keys are unique, (word, set),
+    //    and sorted next) -> one list per word (sets ascending) + the set side
     int64_t E = 0;
     for (int64_t n : en) E += n;
-    GD_REQUIRE(E < (int64_t(1) << 31), "variant tier: too many entries");
-    free_variant(s);
-    if (E > 0) {
-        DevBuf kA(E * 8 + 8, st), kB(E * 8 + 8, st), mall(E * 8 + 8, st), iA(E * 4 + 4, st), iB(E * 4 + 4, st);
+    DevBuf kA(E * 8 + 8, st), mall(E * 8 + 8, st);
+    {
         int64_t o = 0;
         for (size_t c = 0; c < en.size(); c++) {
             GD_HIP(hipMemcpyAsync(kA.as<uint64_t>() + o, ekeys[c].p, en[c] * 8, hipMemcpyDeviceToDevice, st));
             GD_HIP(hipMemcpyAsync(mall.as<uint64_t>() + o, emasks[c].p, en[c] * 8, hipMemcpyDeviceToDevice, st));
             o += en[c];
         }
+        GD_HIP(hipStreamSynchronize(st));
         ekeys.clear();
         emasks.clear();
-        {
-            std::vector<int32_t> io(E);
-            for (int64_t e = 0; e < E; e++) io[e] = (int32_t)e;
-            h2d(iA.p, io.data(), E * 4, st);
-        }
+    }
+    if (sp.real) {
+        const int64_t mine = E;
+        E = allgather_concat(ctx, kA, mine, 8);
+        allgather_concat(ctx, mall, mine, 8);
+    }
+    tr.mark("variant: entries (gathered)");
+    GD_REQUIRE(E < (int64_t(1) << 31), "variant tier: too many entries");
+    free_variant(s);
+    if (E > 0) {
+        DevBuf kB(E * 8 + 8, st), iA(E * 4 + 4, st), iB(E * 4 + 4, st);
+        viota_kernel<<<grid_for(E), 256, 0, st>>>(iA.as<int32_t>(), E);
         uint64_t* k = kA.as<uint64_t>(); uint64_t* ka = kB.as<uint64_t>();
         int32_t* v = iA.as<int32_t>(); int32_t* va = iB.as<int32_t>();
         sort_pairs_u64_i32(ctx, k, ka, v, va, (size_t)E, 0, wbits + sbits);

@@ -108,6 +108,8 @@ _SIGS = {
     "gdist_sets_download": (C.c_int, [_setp, _i64p, _u64p]),
     "gdist_sets_build_bitsets": (C.c_int, [_setp, _u32]),
     "gdist_sets_build_bitsets_ex": (C.c_int, [_setp, _u32, _i64]),
+    "gdist_sets_release_codes": (C.c_int, [_setp]),
+    "gdist_sets_build_timing": (C.c_int, [_setp, _dblp, _dblp, _dblp, C.POINTER(C.c_int)]),
     "gdist_sets_rare_info": (C.c_int, [_setp, _i64p, _i64p, _i64p]),
     "gdist_sets_rare_stats": (C.c_int, [_setp, _i64p, _i64p]),
     "gdist_sets_rare_kmers": (C.c_int, [_setp, _i64p]),

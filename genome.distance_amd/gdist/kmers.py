@@ -401,6 +401,19 @@ class KmerSets(_Handle):
                                                   rare_threshold))
         return self.bitset_info()
 
+    def release_codes(self) -> None:
+        """Drop the codes of a collection whose bitsets are built (gdist_sets_release_codes)."""
+        L.check(L.lib.gdist_sets_release_codes(self.h))
+
+    def build_timing(self) -> dict:
+        """The last bitset build (gdist_sets_build_timing): wall ms, the split stages'
+        ms over all shares and of the largest share, the shares, and one rank's
+        projected build (wall - split + largest share)."""
+        b, sp, mx, n = C.c_double(), C.c_double(), C.c_double(), C.c_int()
+        L.check(L.lib.gdist_sets_build_timing(self.h, C.byref(b), C.byref(sp), C.byref(mx), C.byref(n)))
+        return {"build_ms": b.value, "split_ms": sp.value, "share_max_ms": mx.value, "shares": n.value,
+                "rank_ms": b.value - sp.value + mx.value}
+
     def prepare(self, method: int = L.METHOD_AUTO, pairs: float = -1.0) -> tuple[int, float, float]:
         """Build the representation `method` needs for `pairs` pairs (-1: the whole
         triangle); returns (method a matrix call will run, bitset cost estimate s

@@ -209,6 +209,29 @@ int  gdist_sets_download(const gdist_sets* sets, int64_t* offsets, uint64_t* cod
  * every distinct kmer. */
 int  gdist_sets_build_bitsets(gdist_sets* sets, unsigned flags);
 int  gdist_sets_build_bitsets_ex(gdist_sets* sets, unsigned flags, int64_t rare_threshold);
+/* A collection the code all-gather returned (gdist_sets_allgather_ex) is the
+ * same on every rank; its bitset build is then collective and split by rank
+ * (option "split_build", default on): rank r counts 1/R of the code ranges
+ * of the dictionary summary and fills the tiers of sets [r m, (r + 1) m),
+ * m = ceil(N / R); the summary, bitset rows, rare records and variant entries
+ * are all-gathered, and every rank holds the whole representation (the same
+ * on every rank as a one-rank build). Every rank must make the build call
+ * (build_bitsets, prepare, or a BITSET/AUTO matrix call that builds; AUTO
+ * builds on every rank when any rank's region asks for it). The setup step of
+ * FastaDistanceProcessor.java:150-155 (the reference builds every batch's
+ * kmer sets on one host). */
+/* Release the codes of a collection whose bitsets are built (the C4 code
+ * all-gather's 160 GB per rank): the collection keeps its bitset tiers and
+ * sizes and answers METHOD_BITSET / AUTO calls; the sorted join, sketches, a
+ * rebuild and appends need codes and refuse it (EINVAL). */
+int  gdist_sets_release_codes(gdist_sets* sets);
+/* The last bitset build: wall time (ms), the time of its split stages (the
+ * summary's code ranges and the fill's sets, all shares) and of the largest
+ * share, and the shares (1: not split). One rank of a split build ran one
+ * share; option "split_build" = k on one rank runs k shares in turn, so that
+ * build_ms - split_ms + share_max_ms is one rank's build of 1/k of the sets. */
+int  gdist_sets_build_timing(const gdist_sets* sets, double* build_ms, double* split_ms, double* share_max_ms,
+                             int* shares);
 /* Rare tier: threshold T, distinct posting lists and their member records.
  * Kmers with identical posting lists (e.g. every kmer covering one shared
  * variant) are one list weighted by their number (option "rare_dedup" = 0: one

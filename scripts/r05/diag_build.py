@@ -9,6 +9,10 @@ libgdist.so carries the hash of its own modified sources). Variants:
       records (cache hits instead of gathers)
   d4  d2 + d3
   d5  no walk at all (each batch's setup only: list bounds, prefix sums, records)
+  d6  d5 without the counters' zeroing and the chunk partial's store
+  d7  no batches at all (the chunk's workgroup: zeroing, barriers, partial store)
+  d8  the trailing rare-row workgroups return at once
+  d9  d7 + d8
 Usage: python scripts/r05/diag_build.py d1 d2 ...
 """
 import os, shutil, subprocess, sys
@@ -31,6 +35,14 @@ RI22_D3 = ("        ci[u] = (uint32_t)r[u].z + ((uint32_t)yc2 << 4);\n        ri
            "    }\n    uint4 a0[SU];")
 WALK = "    if (MT == 2 && diag && d22) sparse_walk<2, 3>"
 WALK_D5 = "    if (total != 0x7FFFFFF3) return;\n    if (MT == 2 && diag && d22) sparse_walk<2, 3>"
+ZERO = "    for (int t = threadIdx.x; t < SB * SB / 2; t += SNT) cnt[t] = 0;\n    if (threadIdx.x == 0) next_batch"
+ZERO_D6 = "    if (threadIdx.x == 0) next_batch"
+STORE = "        for (int t = threadIdx.x; t < SB * SB / 2; t += SNT) dst[t] = cnt[t];"
+STORE_D6 = "        if (threadIdx.x == 0x7FFF) dst[0] = cnt[0];"
+BATCH = "        global_batch<SUN, MT>(tc, s0, we, -1, lane, wrec, masks, cnt);"
+BATCH_D7 = "        if (s0 == 0x7FFFFFF3) global_batch<SUN, MT>(tc, s0, we, -1, lane, wrec, masks, cnt);"
+RARE = "        rare_slab_row(rs, (int)(blockIdx.x - ntw), r0, c0, c1, upper, cnt);"
+RARE_D8 = "        if (r0 == 0x7FFFFFF3) rare_slab_row(rs, (int)(blockIdx.x - ntw), r0, c0, c1, upper, cnt);"
 DG22 = "        ne[u] = xc != yc ? ~0u : 0u;\n"
 DG22_D3 = "        ne[u] = xc != yc ? ~0u : 0u;\n        ri[u] &= 0x3FF0u; ci[u] &= 0x3FF0u;\n"
 
@@ -48,6 +60,15 @@ def build(v):
         s = s.replace(CNT_ADD, D1)
     if v in ("d2", "d4"):
         s = s.replace(CNT_ADD, D2)
+    if v == "d6":
+        assert ZERO in s and STORE in s
+        s = s.replace(WALK, WALK_D5).replace(ZERO, ZERO_D6).replace(STORE, STORE_D6)
+    if v in ("d7", "d9"):
+        assert BATCH in s
+        s = s.replace(BATCH, BATCH_D7)
+    if v in ("d8", "d9"):
+        assert RARE in s
+        s = s.replace(RARE, RARE_D8)
     if v == "d5":
         assert WALK in s
         s = s.replace(WALK, WALK_D5)

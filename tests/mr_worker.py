@@ -32,7 +32,8 @@ from gdist import shard, synth  # noqa: E402
 CASES = {
     "base": dict(n=301, L=6000, p=0.01, cfg=11, legs=("bitset", "sorted", "sketch")),
     "sparse": dict(n=300, L=150_000, p=0.002, cfg=12, legs=("bitset",), sparse=True),
-    "c4": dict(n=200, L=100_000, p=0.05, cfg=4, legs=("auto", "sorted", "codes_plan", "codes_variant")),
+    "c4": dict(n=200, L=100_000, p=0.05, cfg=4,
+               legs=("auto", "sorted", "codes_plan", "codes_variant", "codes_two_tier")),
 }
 SKETCH_W = 200
 
@@ -99,8 +100,32 @@ def run_case(name, c, ctx, rank, world):
             vk, vw, ve, _ = gs.variant_info()
             assert vk > 0 and ve > 0 and vw * 4 < vk, (rank, vk, vw, ve)
             info["variant"] = (vk, vw, ve)
+            # round 5: the gathered collection's build is split by rank (each
+            # rank 1/R of the code ranges and of the sets' fill, the tiers
+            # all-gathered), then the codes are released
+            bt = gs.build_timing()
+            assert bt["shares"] == world, (rank, bt)
+            gs.release_codes()
             results[leg] = gs.matrix((r0, r1), (0, n), upper=True, method=gdist.METHOD_BITSET)
+            try:
+                gs.matrix((r0, r1), (0, n), upper=True, method=gdist.METHOD_SORTED)
+                raise AssertionError("released codes must refuse the sorted join")
+            except ValueError:
+                pass
             for k in ("variant", "rare_t", "variant_dmin", "range_summary"):
+                ctx.set_option(k, None)
+        elif leg == "codes_two_tier":
+            # the two-tier build of a gathered collection, split by rank (the
+            # windowed fill of each rank's sets, rows and rare records gathered)
+            own = gdist.KmerSets.from_sequences(seqs[s0:s1], 21, gdist.KmerType.DNA, 0, ctx)
+            gs = own.allgather(consume=True)
+            for k, v in (("variant", 0), ("rare_t", 3)):
+                ctx.set_option(k, v)
+            gs.build_bitsets()
+            assert gs.variant_info()[0] == 0 and gs.rare_info()[1] > 0, (rank, gs.rare_info())
+            assert gs.build_timing()["shares"] == world
+            results[leg] = gs.matrix((r0, r1), (0, n), upper=True, method=gdist.METHOD_BITSET)
+            for k in ("variant", "rare_t"):
                 ctx.set_option(k, None)
         elif leg == "sketch":
             sk = local.sketches(SKETCH_W).allgather()

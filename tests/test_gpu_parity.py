@@ -701,19 +701,21 @@ def test_k32_all_ones_code(ctx, strand):
 
 # ---------------------------------------------------------------- two-tier dictionary
 @pytest.mark.parametrize("dedup", ["1", "0"])
-@pytest.mark.parametrize("kernel", ["0", "1", "1w", "1l", "1lw", "1x"])
+@pytest.mark.parametrize("kernel", ["0", "1", "1w", "1l", "1lw", "1x", "1d", "1dw"])
 @pytest.mark.parametrize("T", [0, 3, 8, 1000])
 def test_rare_tier_thresholds_exact(ctx, T, kernel, dedup, opts):
     """Dense-only (T=0), mixed, and all-rare (T > N) dictionaries give the
     same bit-exact counts and distances as the oracle, through the list-major
     (0) and the row-major (1: 2-byte list members, 1w: 4-byte; 512-thread
-    workgroups, 256 as 1l / 1lw, 1,024 as 1x) rare kernel,
+    workgroups, 256 as 1l / 1lw, 1,024 as 1x; 1d / 1dw: every record once,
+    members added to I by atomics, option rare_direct — C4's wide rows) rare kernel,
     with identical posting lists merged into weighted lists (1) or one list
     per kmer (0). T > N puts lists of up to N members in the rare tier: the
     wave-cooperative long-list walks."""
     import gdist
     opts(rare_kernel=int(kernel[0]), rare_dedup=int(dedup), rare_u16=0 if kernel.endswith("w") else None,
-         rare_rows_threads=256 if "l" in kernel else 1024 if "x" in kernel else None)
+         rare_rows_threads=256 if "l" in kernel else 1024 if "x" in kernel else None,
+         rare_direct=1 if "d" in kernel else None)
     n = 200
     seqs = synth_sets(n, 6000, 0.01, 101)
     sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)

@@ -164,3 +164,93 @@ def test_variant_greedy_reps(ctx, opts, c4_like):
     for i in range(n):
         if not is_rep[i]:
             assert rep_d[i] == min(eD[i, r] for r in reps)
+
+
+def test_variant_walk_across_column_chunks(ctx, opts):
+    """The variant row walk counts a row against its columns in LDS chunks of
+    16,384 (VCH) and keeps each list's position from chunk to chunk (C4:
+    100,000 columns, 7 chunks); round 5 loads the next 64 members of a list
+    before counting the current ones. 17,000 sets: rows whose lists cross
+    chunk boundaries, both rare walks (LDS chunks and direct atomics), equal
+    the oracle."""
+    import gdist
+    from gdist import synth
+    n = 17000
+    seqs = [bytes(r) for r in synth.genomes(n, 600, 0.03, 43)]
+    off, codes = oracle.pack(seqs, 21, 0, 0)
+    opts(variant=1, rare_t=3, variant_dmin=n // 10, range_summary=1)
+    sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
+    sets.build_bitsets()
+    vk, vw, ve, vp = sets.variant_info()
+    assert vk > 0 and ve > 0, (vk, vw, ve)
+    for direct in (None, 0, 1):
+        opts(rare_direct=direct)
+        for (r0, r1, up) in [(0, 24, True), (16370, 16400, True), (500, 520, False)]:
+            I, D = sets.matrix((r0, r1), (0, n), upper=up, method=gdist.METHOD_BITSET)
+            eI, eD = oracle.matrix(off, codes, r0, r1, 0, n, flags=0x100 if up else 0, nthreads=8)
+            if up:
+                mask = np.fromfunction(lambda a, b: b > (r0 + a), (r1 - r0, n))
+                I, D, eI, eD = I[mask], D[mask], eI[mask], eD[mask]
+            assert np.array_equal(I, eI), (direct, r0, r1, np.flatnonzero(I != eI)[:5])
+            assert bits_equal(D, eD), (direct, r0, r1)
+
+
+@pytest.mark.parametrize("mode", ["variant", "variant_windowed_fill", "two_tier", "two_tier_sort_fill"])
+def test_split_build_equals_whole_build(ctx, opts, c4_like, mode):
+    """the build of a gathered collection split by rank.
+    Option split_build = 3 runs the three ranks' shares in turn on this GPU
+    (share r: 1/3 of the summary's code ranges, the fill of sets [400 r,
+    400 (r + 1))) and concatenates what the all-gathers would: the bitsets,
+    tiers and counts equal the one-share build's and the oracle's."""
+    import gdist
+    seqs, off, codes = c4_like
+    n = len(seqs)
+    if mode.startswith("variant"):
+        base = dict(variant=1, rare_t=3, variant_dmin=n // 10, range_summary=1,
+                    fill_sort=3 if mode == "variant_windowed_fill" else None)
+    else:
+        base = dict(variant=0, rare_t=3, fill_sort=1 if mode == "two_tier_sort_fill" else None)
+    built = {}
+    for split in (None, 3):
+        opts(split_build=split, **base)
+        sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
+        sets.build_bitsets()
+        bt = sets.build_timing()
+        assert bt["shares"] == (split or 1), bt
+        assert 0 <= bt["share_max_ms"] <= bt["split_ms"] <= bt["build_ms"], bt
+        built[split] = (sets.bitsets(), sets.variant_info(), sets.rare_info(), sets)
+    (b0, v0, r0_, _), (b3, v3, r3, s3) = built[None], built[3]
+    assert np.array_equal(b0, b3) and v0 == v3 and r0_ == r3, (mode, v0, v3, r0_, r3)
+    for (a, b, c0, c1, up) in REGIONS[:2]:
+        I, D = s3.matrix((a, b), (c0, c1), upper=up, method=gdist.METHOD_BITSET)
+        eI, eD = oracle.matrix(off, codes, a, b, c0, c1, flags=0x100 if up else 0, nthreads=8)
+        if up:
+            mask = np.fromfunction(lambda x, y: (c0 + y) > (a + x), (b - a, c1 - c0))
+            I, D, eI, eD = I[mask], D[mask], eI[mask], eD[mask]
+        assert np.array_equal(I, eI), (mode, a, b)
+        assert bits_equal(D, eD)
+
+
+def test_release_codes(ctx, opts, c4_like):
+    """gdist_sets_release_codes: a built collection drops its codes and keeps
+    answering bitset calls (the C4 ranks' 160 GB of gathered codes); calls that
+    need codes refuse it."""
+    import gdist
+    seqs, off, codes = c4_like
+    n = len(seqs)
+    opts(variant=1, rare_t=3, variant_dmin=n // 10)
+    sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
+    fresh = gdist.KmerSets.from_sequences(seqs[:5], 21, gdist.KmerType.DNA, 0, ctx)
+    with pytest.raises(ValueError):
+        fresh.release_codes()                      # no bitsets: the codes are all it has
+    sets.build_bitsets()
+    sets.release_codes()
+    I, D = sets.matrix((0, 50), (0, n), upper=True, method=gdist.METHOD_AUTO)
+    eI, eD = oracle.matrix(off, codes, 0, 50, 0, n, flags=0x100, nthreads=8)
+    mask = np.fromfunction(lambda a, b: b > a, (50, n))
+    assert np.array_equal(I[mask], eI[mask]) and bits_equal(D[mask], eD[mask])
+    for call in (lambda: sets.matrix((0, 5), (0, n), method=gdist.METHOD_SORTED),
+                 lambda: sets.build_bitsets(),
+                 lambda: sets.download()):
+        with pytest.raises(ValueError):
+            call()
