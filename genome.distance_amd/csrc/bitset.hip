@@ -700,9 +700,25 @@ __device__ __forceinline__ void mfma_wait(int later) {
     }
 }
 
+// Round 5 (RAW): the operand is the bitsets themselves, not the nibbles. A
+// stage of the same 128 bytes per row holds 16 words instead of 4, so a tile
+// moves a quarter of the bytes global -> LDS (C4: 80 -> 20 GB a 1,024-row
+// step; the nibble operand was 4x the bitsets in HBM and in every L2), and
+// each lane expands its fragment in registers: MFMA step m of a stage takes
+// lane (r, h)'s dword 4 q + m of its half h of row r (chunk 4 h + q), and
+// nibble j of fragment dword k holds bit 4 j + k of that dword as 0x0 / 0x2
+// (x << 1, x, x >> 1, x >> 2 under 0x22222222: 7 VALU per dword). Any
+// assignment of bits to K positions is exact as long as both operands use
+// the same one.
+__device__ __forceinline__ v4i_t raw_nibbles(uint32_t x) {
+    const v4i_t f = {(int)((x << 1) & 0x22222222u), (int)(x & 0x22222222u), (int)((x >> 1) & 0x22222222u),
+                     (int)((x >> 2) & 0x22222222u)};
+    return f;
+}
+
 // NS stages in a ring (2: double buffering; 4 with KM = 2 in the same 128
 // KiB: three stages in flight while one is computed; option bitset_mfma_km)
-template <int KM, int NS>
+template <int KM, int NS, bool RAW = false>
 __global__ __launch_bounds__(MNT, 2) void bitset_mfma_kernel(
     const unsigned char* __restrict__ F, int64_t W, const int2* __restrict__ tiles, int ntiles, int splits,
     int64_t nstages, int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I,
@@ -723,7 +739,7 @@ __global__ __launch_bounds__(MNT, 2) void bitset_mfma_kernel(
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wr = wave >> 1, wc = wave & 1;          // 4 x 2 waves of 64 rows x 128 columns
     const int r = lane & 31, h = lane >> 5;
-    const int64_t rowbytes = W * 32;
+    const int64_t rowbytes = RAW ? W * 8 : W * 32;
     v16f_t acc[2][4];
 #pragma unroll
     for (int a = 0; a < 2; a++)
@@ -744,6 +760,36 @@ __global__ __launch_bounds__(MNT, 2) void bitset_mfma_kernel(
         // stages issued after ks: min(NS - 1, ks1 - 1 - ks)
         const int64_t later = ks1 - 1 - ks < NS - 1 ? ks1 - 1 - ks : NS - 1;
         mfma_wait<2 * KM>((int)later);               // stage ks landed everywhere
+        if constexpr (RAW) {
+            static_assert(!RAW || KM == 4, "raw stages are 128-byte rows");
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                v4i_t af[2], bf[4];
+#pragma unroll
+                for (int a = 0; a < 2; a++)
+                    af[a] = *reinterpret_cast<const v4i_t*>(A + mlds<KM>(wr * 64 + a * 32 + r, 4 * h + q));
+#pragma unroll
+                for (int b = 0; b < 4; b++)
+                    bf[b] = *reinterpret_cast<const v4i_t*>(B + mlds<KM>(wc * 128 + b * 32 + r, 4 * h + q));
+#pragma unroll
+                for (int m = 0; m < 4; m++) {
+                    v4i_t an[2], bn[4];
+#pragma unroll
+                    for (int a = 0; a < 2; a++) an[a] = raw_nibbles((uint32_t)af[a][m]);
+#pragma unroll
+                    for (int b = 0; b < 4; b++) bn[b] = raw_nibbles((uint32_t)bf[b][m]);
+#pragma unroll
+                    for (int a = 0; a < 2; a++)
+#pragma unroll
+                        for (int b = 0; b < 4; b++) {
+                            const v8i_t av = {an[a][0], an[a][1], an[a][2], an[a][3], 0, 0, 0, 0};
+                            const v8i_t bv = {bn[b][0], bn[b][1], bn[b][2], bn[b][3], 0, 0, 0, 0};
+                            acc[a][b] =
+                                __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(av, bv, acc[a][b], 4, 4, 0, 0, 0, 0);
+                        }
+                }
+            }
+        } else
 #pragma unroll
         for (int kk = 0; kk < KM; kk++) {
             v4i_t af[2], bf[4];
@@ -2548,7 +2594,11 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
         if (p.nmt > 0) {
             // FP4 MFMA tiles: one 128 KiB workgroup per CU; K split so that
             // the grid fills ~4 rounds of the chip, each split >= 8 stages
-            const int km = ctx->option(OPT_BITSET_MFMA_KM, 4) == 2 ? 2 : 4;
+            // option bitset_mfma_raw (default 1): stages of the bitsets
+            // themselves, 16 words a stage, expanded in registers; 0: the FP4
+            // nibble operand (KM = 4 or 2 words a stage)
+            const bool raw = ctx->option(OPT_BITSET_MFMA_RAW, 1) != 0;
+            const int km = raw ? 16 : ctx->option(OPT_BITSET_MFMA_KM, 4) == 2 ? 2 : 4;
             const int64_t nst = tW / km;
             int msp = (int)std::max<int64_t>(
                 1, std::min<int64_t>(std::max<int64_t>(1, nst / 8), ceil_div((int64_t)ctx->cus * 4, p.nmt)));
@@ -2562,7 +2612,7 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
             GD_REQUIRE(ceil_div(nst, (int64_t)msp) * km <= kMfmaMaxSplitWords, "MFMA K split past the f32 exact bound");
             const int64_t mgrid = p.nmt * msp;
             GD_REQUIRE(mgrid < (int64_t(1) << 31), "MFMA tile grid too large");
-            if (s->fp4_W != tW) {
+            if (!raw && s->fp4_W != tW) {
                 // the operand as FP4 nibbles, once per set of bitsets (every
                 // rebuild of the bits drops it; a capture replays a call that
                 // ran uncaptured first, so the operand exists by then)
@@ -2576,15 +2626,16 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
             }
             // stage ring: KM words a stage x NS stages (option bitset_mfma_ns: 2..4
             // with KM = 2; KM = 4 only double-buffered, 128 KiB either way)
-            const int ns = km == 4 ? 2 : (int)std::max<int64_t>(2, std::min<int64_t>(4, ctx->option(OPT_BITSET_MFMA_NS, 2)));
+            const int ns = km != 2 ? 2 : (int)std::max<int64_t>(2, std::min<int64_t>(4, ctx->option(OPT_BITSET_MFMA_NS, 2)));
             auto mlaunch = [&](auto kern, int lds_bytes) {
                 GD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes));
-                kern<<<(unsigned)mgrid, MNT, lds_bytes, st>>>(s->fp4.as<unsigned char>(), tW, p.mtiles.as<int2>(),
-                                                               (int)p.nmt, msp, nst, r0, r1, c0, c1, upper ? 1 : 0, d_I,
-                                                               ldI);
+                const unsigned char* op = raw ? reinterpret_cast<const unsigned char*>(tbits) : s->fp4.as<unsigned char>();
+                kern<<<(unsigned)mgrid, MNT, lds_bytes, st>>>(op, tW, p.mtiles.as<int2>(), (int)p.nmt, msp, nst, r0,
+                                                               r1, c0, c1, upper ? 1 : 0, d_I, ldI);
             };
-            if (km == 4) mlaunch(&bitset_mfma_kernel<4, 2>, 2 * 2 * mopb<4>());
+            if (raw) mlaunch(&bitset_mfma_kernel<4, 2, true>, 2 * 2 * mopb<4>());
+            else if (km == 4) mlaunch(&bitset_mfma_kernel<4, 2>, 2 * 2 * mopb<4>());
             else if (ns == 4) mlaunch(&bitset_mfma_kernel<2, 4>, 4 * 2 * mopb<2>());
             else if (ns == 3) mlaunch(&bitset_mfma_kernel<2, 3>, 3 * 2 * mopb<2>());
             else mlaunch(&bitset_mfma_kernel<2, 2>, 2 * 2 * mopb<2>());

@@ -225,6 +225,7 @@ struct Timing {
     X(RARE_ROWS_THREADS, "rare_rows_threads") /* row-major rare walk: threads a workgroup (256/512/1024; default by LDS) */ \
     X(RARE_DIRECT, "rare_direct")             /* row-major rare walk: 1 every record once, members added to I by atomics; 0 LDS column chunks (default: direct past one chunk) */ \
     X(BITSET_MFMA, "bitset_mfma")             /* 0: dense tiles by AND+popcount instead of FP4 MFMA */       \
+    X(BITSET_MFMA_RAW, "bitset_mfma_raw")     /* MFMA tiles: 1 (default) stages of the bitsets, nibbles in registers; 0 the FP4 operand */ \
     X(BITSET_MFMA_KM, "bitset_mfma_km")       /* MFMA tiles: words per stage (4 default, 2: 64 KiB of LDS) */ \
     X(BITSET_MFMA_NS, "bitset_mfma_ns")       /* MFMA tiles with 2-word stages: stages in the ring (2..4) */    \
     X(BITSET_MFMA_SPLITS, "bitset_mfma_splits") /* MFMA tiles: K splits a tile (default: ~4 rounds of the chip) */ \
@@ -233,6 +234,7 @@ struct Timing {
     X(VARIANT, "variant")                     /* variant tier: 1 force, 0 off (default: by the dictionary) */ \
     X(VARIANT_DMIN, "variant_dmin")           /* sets holding a dense-tier kmer (default N / 10) */            \
     X(RANGE_SUMMARY, "range_summary")         /* 1: the code-range dictionary whatever the size, 0: never */  \
+    X(VARIANT_WALK, "variant_walk")           /* variant walk: 1 (default) a lane per entry, 0 a wave per entry */ \
     X(SPLIT_BUILD, "split_build")             /* gathered collection on R ranks: each builds 1/R and all-gathers (default); 0 every rank all; k >= 2 without peers: k shares in turn here */
 
 enum Opt : int {

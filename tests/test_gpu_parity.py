@@ -883,7 +883,7 @@ def test_sparse_equals_dense_at_size(ctx, opts):
     assert np.array_equal(I[iu], oI[iu]) and bits_equal(D[iu], oD[iu])
 
 
-@pytest.mark.parametrize("mfma", [None, "km2_group", "km2_ns3", "km2_ns4", 0])
+@pytest.mark.parametrize("mfma", [None, "nibble", "km2_group", "km2_ns3", "km2_ns4", "raw_group", 0])
 @pytest.mark.parametrize("T", [0, 3])
 def test_dense_tiles_mfma_exact(ctx, opts, mfma, T):
     """The dense tier's tiles on the matrix cores (FP4 MFMA, 256 x 256 pairs
@@ -891,13 +891,20 @@ def test_dense_tiles_mfma_exact(ctx, opts, mfma, T):
     bitset_mfma 0): counts and distances bit-exact against the oracle over
     upper triangles, whole squares, rectangles, row blocks not aligned to a
     tile, partial tiles and one row; dense-only (T = 0) and with rare lists;
-    2-word stages with the tiles in 2 x 4 blocks, and rings of 3 and 4
-    stages (options bitset_mfma_km, bitset_mfma_group, bitset_mfma_ns)."""
+    the default stages of the bitsets themselves (nibbles made in registers,
+    round 5) and the FP4 nibble operand (option bitset_mfma_raw 0) with
+    4-word stages, 2-word stages with the tiles in 2 x 4 blocks, and rings
+    of 3 and 4 stages (options bitset_mfma_km, bitset_mfma_group,
+    bitset_mfma_ns)."""
     import gdist
-    if mfma == "km2_group":
-        opts(bitset_mfma_km=2, bitset_mfma_group=2, sparse=0)
+    if mfma == "nibble":
+        opts(bitset_mfma_raw=0, sparse=0)
+    elif mfma == "raw_group":
+        opts(bitset_mfma_group=2, sparse=0)
+    elif mfma == "km2_group":
+        opts(bitset_mfma_raw=0, bitset_mfma_km=2, bitset_mfma_group=2, sparse=0)
     elif mfma in ("km2_ns3", "km2_ns4"):                # 3 / 4 stages in the ring
-        opts(bitset_mfma_km=2, bitset_mfma_ns=int(mfma[-1]), sparse=0)
+        opts(bitset_mfma_raw=0, bitset_mfma_km=2, bitset_mfma_ns=int(mfma[-1]), sparse=0)
     else:
         opts(bitset_mfma=mfma, sparse=0)
     n = 530
@@ -928,7 +935,8 @@ def test_dense_tiles_mfma_past_f32_bound(ctx, opts, splits):
     more than 2^24 dense kmers a pair; with one K split asked for (option
     bitset_mfma_splits 1) the launch must still split K so that no split
     sums more than 2^18 words, and I and D equal the oracle bit for bit
-    (and the AND + popcount tiles, option bitset_mfma 0)."""
+    (the raw-stage and nibble-operand MFMA tiles, and the AND + popcount
+    tiles, option bitset_mfma 0)."""
     import gdist
     opts(sparse=0, bitset_mfma_splits=splits)
     n = 4
@@ -940,8 +948,8 @@ def test_dense_tiles_mfma_past_f32_bound(ctx, opts, splits):
     eI, eD = oracle.matrix(off, codes, 0, n, 0, n, flags=0, nthreads=4)
     iu = np.triu_indices(n, 1)
     assert eI[iu].min() > (1 << 24), eI[iu]       # the premise: counts past 2^24
-    for mfma in (None, 0):
-        opts(bitset_mfma=mfma)
+    for mfma, raw in ((None, None), (None, 0), (0, None)):
+        opts(bitset_mfma=mfma, bitset_mfma_raw=raw)
         for up in (True, False):
             I, D = sets.matrix(upper=up, method=gdist.METHOD_BITSET)
             if up:
