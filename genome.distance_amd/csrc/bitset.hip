@@ -2151,8 +2151,16 @@ void build_bitsets(gdist_ctx* ctx, gdist_sets* s, unsigned flags, int64_t rare_t
     // the build's wall time and its split stages (gdist_sets_build_timing)
     struct BuildClock {
         gdist_sets* s; BuildSplit& sp; hipStream_t st; std::chrono::steady_clock::time_point t0;
+        AllocStats a0;
+        bool trace;
         ~BuildClock() {
             (void)hipStreamSynchronize(st);
+            if (trace) {
+                const AllocStats& a = alloc_stats();
+                fprintf(stderr, "gdist: build allocations: %lld fresh blocks, %.2f GB, %.1f ms in hipMalloc; %lld cache trims\n",
+                        (long long)(a.fresh - a0.fresh), (a.fresh_bytes - a0.fresh_bytes) / 1e9, a.fresh_ms - a0.fresh_ms,
+                        (long long)(a.trims - a0.trims));
+            }
             s->build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
             s->build_shares = sp.R;
             s->build_split_ms = s->build_share_max_ms = 0;
@@ -2161,7 +2169,7 @@ void build_bitsets(gdist_ctx* ctx, gdist_sets* s, unsigned flags, int64_t rare_t
                 s->build_share_max_ms = std::max(s->build_share_max_ms, v);
             }
         }
-    } clock{s, sp, ctx->stream, t_build};
+    } clock{s, sp, ctx->stream, t_build, alloc_stats(), ctx->trace()};
     Summary sum;
     // a collection without pack summaries and too many codes for one sort
     // (a gathered 8-GPU collection: C4's 2e10 codes) is counted by code
@@ -2555,17 +2563,22 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     };
     if (!ctx->capturing) GD_HIP(hipEventRecord(ctx->ev_k0, st));
     if (side) {
+        // option serial_step = 1: the side stream's families run on the main
+        // stream before the dense tiles, one after another (each family's
+        // time alone: the C4 slice's MFMA tiles and variant walk otherwise
+        // share the CUs)
+        hipStream_t sd = ctx->option(OPT_SERIAL_STEP, 0) != 0 ? st : ctx->side;
         GD_HIP(hipEventRecord(ctx->ev_fork, st));
-        GD_HIP(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
-        if (s->sparse) rare_done = sparse_matrix(ctx, s, r0, r1, c0, c1, upper, d_I, ldI, ctx->side, p.sparse);
+        GD_HIP(hipStreamWaitEvent(sd, ctx->ev_fork, 0));
+        if (s->sparse) rare_done = sparse_matrix(ctx, s, r0, r1, c0, c1, upper, d_I, ldI, sd, p.sparse);
         // beside the sparse kernel the list-major rare kernel goes to the main
         // stream after the dense tiles (the side stream is busy until the
         // sparse tiles and their reduce end: C2 0.0185 ms in line there)
-        if (overlap && !s->sparse) launch_rare_pairs(ctx->side);
-        if (rows_side) launch_rare_rows(ctx->side, true);
-        if (s->variant) variant_matrix(ctx, s, r0, r1, c0, c1, upper, d_I, ldI, ctx->side);
+        if (overlap && !s->sparse) launch_rare_pairs(sd);
+        if (rows_side) launch_rare_rows(sd, true);
+        if (s->variant) variant_matrix(ctx, s, r0, r1, c0, c1, upper, d_I, ldI, sd);
         GD_HIP(hipGetLastError());
-        GD_HIP(hipEventRecord(ctx->ev_join, ctx->side));
+        GD_HIP(hipEventRecord(ctx->ev_join, sd));
     }
     if (tW == 0 || (s->sparse && s->sp_fold_dense)) {
         // no dense words, or so few that the sparse flush counts them

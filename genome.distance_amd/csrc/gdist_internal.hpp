@@ -62,6 +62,13 @@ void set_last_error(const std::string& msg);
 void* cache_alloc(int device, size_t bytes, size_t* cls_out);
 void cache_free(int device, void* p, size_t cls);
 void cache_trim(int device);     // hipFree every cached block of the device
+// fresh hipMallocs of the caching allocator (count, bytes, wall ms) and cache
+// trims: the trace prints them at the end of a build
+struct AllocStats {
+    int64_t fresh = 0, trims = 0;
+    double fresh_bytes = 0, fresh_ms = 0;
+};
+AllocStats& alloc_stats();
 
 struct DevBuf {
     void* p = nullptr;
@@ -235,6 +242,7 @@ struct Timing {
     X(VARIANT_DMIN, "variant_dmin")           /* sets holding a dense-tier kmer (default N / 10) */            \
     X(RANGE_SUMMARY, "range_summary")         /* 1: the code-range dictionary whatever the size, 0: never */  \
     X(VARIANT_WALK, "variant_walk")           /* variant walk: 1 (default) a lane per entry, 0 a wave per entry */ \
+    X(SERIAL_STEP, "serial_step")             /* 1: the side stream's kernel families on the main stream, in turn (timing) */ \
     X(SPLIT_BUILD, "split_build")             /* gathered collection on R ranks: each builds 1/R and all-gathers (default); 0 every rank all; k >= 2 without peers: k shares in turn here */
 
 enum Opt : int {

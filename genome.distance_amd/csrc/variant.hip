@@ -953,7 +953,10 @@ void hash_fill(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_
     int64_t s0 = sa;
     while (s0 < sb) {
         int64_t s1 = s0 + 1;
-        while (s1 < sb && s->h_off[s1 + 1] - s->h_off[s0] <= (int64_t(1) << 30)) s1++;
+        // chunks of <= 2^28 codes: their 1 GiB position buffer and record
+        // sorts reuse the code-range summary's cached blocks (fresh device
+        // memory costs ~0.2 s a GB: C4's first 2^30-code chunk took 2.8 s)
+        while (s1 < sb && s->h_off[s1 + 1] - s->h_off[s0] <= (int64_t(1) << 28)) s1++;
         const int64_t base = s->h_off[s0], n = s->h_off[s1] - base;
         DevBuf pos(std::max<int64_t>(1, n) * 4 + 16, st);
         hash_probe_kernel<<<(unsigned)(s1 - s0), 256, 0, st>>>(s->codes.as<uint64_t>(), s->off.as<int64_t>(), s0, base,
@@ -1181,6 +1184,7 @@ void build_variant_bitsets(gdist_ctx* ctx, gdist_sets* s, DevBuf& dict, DevBuf& 
         uint64_t* k = kA.as<uint64_t>(); uint64_t* ka = kB.as<uint64_t>();
         int32_t* v = iA.as<int32_t>(); int32_t* va = iB.as<int32_t>();
         sort_pairs_u64_i32(ctx, k, ka, v, va, (size_t)E, 0, wbits + sbits);
+        tr.mark("variant: entries sorted by (word, set)");
         s->vw_set.alloc(E * 4 + 32, st);                    // 4-wide loads read up to 3 entries past a list
         s->vw_mask.alloc(E * 8 + 32, st);
         DevBuf skey(E * 8 + 8, st), skalt(E * 8 + 8, st);
@@ -1199,8 +1203,10 @@ void build_variant_bitsets(gdist_ctx* ctx, gdist_sets* s, DevBuf& dict, DevBuf& 
         set_keys_kernel<<<grid_for(E), 256, 0, st>>>(s->vw_set.as<uint32_t>(), s->vw_beg.as<uint32_t>(),
                                                      s->vw_end.as<uint32_t>(), E, lbits, skey.as<uint64_t>());
         GD_HIP(hipGetLastError());
+        tr.mark("variant: word lists");
         uint64_t* sk = skey.as<uint64_t>(); uint64_t* ska = skalt.as<uint64_t>();
         sort_keys_u64(ctx, sk, ska, (size_t)E, 0, 31 + lbits + sbits);
+        tr.mark("variant: set side sorted");
         s->vs_off.alloc((N + 1) * 8, st);
         s->vs_ent.alloc(E * 4 + 4, st);
         set_offsets_kernel<<<grid_for(std::max<int64_t>(E, N + 1)), 256, 0, st>>>(sk, E, N, 31 + lbits,
