@@ -223,7 +223,11 @@ constexpr int RCH = 16384;   // max columns per LDS chunk (64 KiB of counters)
 // walk is latency-bound (each record's members are a dependent load after its
 // record's), and the 40 KiB of counters of a C3 row allow 4 workgroups a CU:
 // 512 threads make that the full 32 waves a CU instead of 16
-template <typename M, int NT>
+// C16 (round 5): 16-bit counters, two to an LDS dword, when no row's rare
+// kmers weigh 65,536 or more (rare_row_wmax, build time: a count never
+// carries into its neighbour) — C3's 10,000 columns take 20 KiB instead of
+// 40, so a workgroup fits on a CU beside an MFMA dense-tile workgroup.
+template <typename M, int NT, bool C16 = false>
 __global__ __launch_bounds__(NT) void rare_rows_kernel(const int64_t* __restrict__ soff,
                                                         const uint64_t* __restrict__ sent,
                                                         const uint32_t* __restrict__ sw,
@@ -241,8 +245,13 @@ __global__ __launch_bounds__(NT) void rare_rows_kernel(const int64_t* __restrict
     const int64_t ce = cb + RCH < c1 ? cb + RCH : c1;
     if (i >= r1 || cb >= ce || (upper && ce - 1 <= i)) return;
     const int n = (int)(ce - cb);
-    for (int t = threadIdx.x; t < n; t += blockDim.x) cnt[t] = 0;
+    const int nw = C16 ? (n + 1) >> 1 : n;
+    for (int t = threadIdx.x; t < nw; t += blockDim.x) cnt[t] = 0;
     __syncthreads();
+    auto add = [&](int64_t t, int32_t v) {
+        if (C16) atomicAdd(&cnt[(t - cb) >> 1], v << (((t - cb) & 1) << 4));
+        else atomicAdd(&cnt[t - cb], v);
+    };
     const int64_t lo = upper && i + 1 > cb ? i + 1 : cb;
     const int64_t rb = soff[i], re = soff[i + 1];
     const int64_t per = (re - rb + nsplit - 1) / nsplit;
@@ -263,7 +272,7 @@ __global__ __launch_bounds__(NT) void rare_rows_kernel(const int64_t* __restrict
             const int32_t lw = __shfl(w, l, 64);
             for (int64_t y = lb + lane; y < le; y += 64) {
                 const int64_t t = psets[y];
-                if (t >= lo && t < ce && t != i) atomicAdd(&cnt[t - cb], lw);
+                if (t >= lo && t < ce && t != i) add(t, lw);
             }
         }
         if (lng) continue;
@@ -277,14 +286,14 @@ __global__ __launch_bounds__(NT) void rare_rows_kernel(const int64_t* __restrict
 #pragma unroll
             for (int u = 0; u < PER; u++) {
                 const int64_t t = mem[u];
-                if (y + u < e && t >= lo && t < ce && t != i) atomicAdd(&cnt[t - cb], w);
+                if (y + u < e && t >= lo && t < ce && t != i) add(t, w);
             }
         }
     }
     __syncthreads();
     int32_t* row = I + (i - r0) * ldI + (cb - c0);
     for (int t = threadIdx.x; t < n; t += blockDim.x) {
-        const int v = cnt[t];
+        const int v = C16 ? (int)(((uint32_t)cnt[t >> 1] >> ((t & 1) << 4)) & 0xFFFFu) : cnt[t];
         if (v && cb + t >= lo) {
             if (nsplit > 1 || atomic_flush) atomicAdd(row + t, v);
             else row[t] += v;
@@ -2003,6 +2012,24 @@ __global__ void entry_weights_kernel(const uint64_t* __restrict__ keys, int64_t 
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) sw[i] = pw[(uint32_t)keys[i]];
 }
 
+// the heaviest row of the set side: max over sets of the sum of their
+// entries' list weights (a pair's rare count is at most its row's)
+__global__ void row_weight_max_kernel(const int64_t* __restrict__ soff, const uint32_t* __restrict__ sw,
+                                      int64_t nsets, unsigned long long* __restrict__ out) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    unsigned long long mx = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nsets; i += stride) {
+        unsigned long long t = 0;
+        for (int64_t x = soff[i]; x < soff[i + 1]; x++) t += sw[x];
+        mx = t > mx ? t : mx;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long v = __shfl_xor(mx, o, 64);
+        mx = v > mx ? v : mx;
+    }
+    if ((threadIdx.x & 63) == 0) atomicMax(out, mx);
+}
+
 }  // namespace
 
 // rare records (rank << 32 | set) -> posting lists CSR on `s`, identical
@@ -2016,6 +2043,7 @@ void build_postings(gdist_ctx* ctx, gdist_sets* s, unsigned long long* recs, int
     s->post_off.alloc((Ur + 1) * 8, st);
     s->post_sets.alloc(n * 4 + 16, st);          // padded: the row walk reads 16 bytes at a time
     s->rare_incs = s->rare_max_list = s->rare_incs_long = 0;
+    s->rare_row_wmax = 0;
     if (Ur == 0 || n == 0) {
         GD_HIP(hipMemsetAsync(s->post_off.p, 0, (Ur + 1) * 8, st));
         s->post_w.alloc(Ur * 4 + 4, st);
@@ -2134,6 +2162,16 @@ void build_postings(gdist_ctx* ctx, gdist_sets* s, unsigned long long* recs, int
     s->rare_incs = (int64_t)hi[0];
     s->rare_max_list = (int64_t)hi[1];
     s->rare_incs_long = (int64_t)hi[2];
+    {
+        DevBuf wm(8, st);
+        GD_HIP(hipMemsetAsync(wm.p, 0, 8, st));
+        row_weight_max_kernel<<<grid_for(s->nsets, 256, 4096), 256, 0, st>>>(
+            s->srare_off.as<int64_t>(), s->srare_w.as<uint32_t>(), s->nsets, wm.as<unsigned long long>());
+        GD_HIP(hipGetLastError());
+        unsigned long long h = 0;
+        d2h(&h, wm.p, 8, st);
+        s->rare_row_wmax = (int64_t)h;
+    }
     tr.mark("postings: set side");
 }
 
@@ -2374,6 +2412,7 @@ void free_bitsets(gdist_sets* s) {
     s->srare_skip.release();
     s->W = s->dict_size = 0;
     s->n_rare = s->rare_T = s->rare_records = s->rare_incs = s->rare_max_list = s->rare_incs_long = 0;
+    s->rare_row_wmax = 0;
     s->rare_kmers = 0;
 }
 
@@ -2530,7 +2569,9 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
         const int nsplit = (int)std::max<int64_t>(1, std::min<int64_t>(16, ceil_div((int64_t)ctx->cus * 8, units)));
         const int64_t rgrid = units * nsplit;
         GD_REQUIRE(rgrid < (int64_t(1) << 31), "rare-tier grid too large");
-        const size_t lds = (size_t)std::min<int64_t>(nc, RCH) * 4;
+        // 16-bit counters when no row can reach 2^16 (option rare_c16, default on)
+        const bool c16 = s->rare_row_wmax < 65536 && ctx->option(OPT_RARE_C16, 1) != 0;
+        const size_t lds = c16 ? (size_t)((std::min<int64_t>(nc, RCH) + 1) / 2) * 4 : (size_t)std::min<int64_t>(nc, RCH) * 4;
         FamilyTimer ft(ctx, GDIST_KERNEL_RARE, rs);
         // threads a workgroup: the LDS counters allow 4 workgroups a CU up to
         // 40 KiB (10,240 columns: C3), 2 beyond (C4's 64 KiB chunks); 32 waves
@@ -2543,7 +2584,11 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
                                                    r0, r1, c0, c1, nch, nsplit, upper ? 1 : 0, atomic_flush ? 1 : 0,
                                                    d_I, ldI);
         };
-        if (s->post_sets16.p) {
+        if (s->post_sets16.p && c16) {
+            if (rt == 1024) go(rare_rows_kernel<uint16_t, 1024, true>, 1024, s->post_sets16.as<uint16_t>());
+            else if (rt == 512) go(rare_rows_kernel<uint16_t, 512, true>, 512, s->post_sets16.as<uint16_t>());
+            else go(rare_rows_kernel<uint16_t, 256, true>, 256, s->post_sets16.as<uint16_t>());
+        } else if (s->post_sets16.p) {
             if (rt == 1024) go(rare_rows_kernel<uint16_t, 1024>, 1024, s->post_sets16.as<uint16_t>());
             else if (rt == 512) go(rare_rows_kernel<uint16_t, 512>, 512, s->post_sets16.as<uint16_t>());
             else go(rare_rows_kernel<uint16_t, 256>, 256, s->post_sets16.as<uint16_t>());

@@ -649,7 +649,14 @@ __global__ __launch_bounds__(1024) void variant_rows_kernel(const int64_t* __res
 // whole wave's 64 lists are in flight at once. The build orders each set's
 // entries by list length, so a wave's lanes walk lists of similar length.
 // Same grid, batches, chunks and per-entry positions as variant_rows_kernel.
-__global__ __launch_bounds__(1024) void variant_lanes_kernel(const int64_t* __restrict__ soff,
+// Template: NT threads, CH columns of int32 counters per chunk, VB entries a
+// batch. <1024, VCH, VBATCH>: 72 KiB (two workgroups a CU); <256, 6144, 1024>
+// (option variant_small, default): 28 KiB and one wave a SIMD, so that a
+// workgroup fits on a CU beside an MFMA dense-tile workgroup (128 KiB of LDS;
+// 2 waves a SIMD of 208 VGPRs leave 96 of the SIMD's 512: one 56-VGPR wave):
+// the C4 step's two launches then share every CU instead of taking turns.
+template <int NT, int CH, int VB>
+__global__ __launch_bounds__(NT) void variant_lanes_kernel(const int64_t* __restrict__ soff,
                                                             const uint32_t* __restrict__ sent,
                                                             const uint32_t* __restrict__ vset,
                                                             const unsigned long long* __restrict__ vmask,
@@ -657,8 +664,8 @@ __global__ __launch_bounds__(1024) void variant_lanes_kernel(const int64_t* __re
                                                             const uint32_t* __restrict__ vend, int64_t r0, int64_t r1,
                                                             int64_t c0, int64_t c1, int nsplit, int upper,
                                                             int32_t* __restrict__ I, int64_t ldI) {
-    __shared__ int32_t cnt[VCH];
-    __shared__ uint32_t ypos[VBATCH];
+    __shared__ int32_t cnt[CH];
+    __shared__ uint32_t ypos[VB];
     const int64_t i = r0 + blockIdx.x / nsplit;
     const int split = blockIdx.x % nsplit;
     if (i >= r1) return;
@@ -669,8 +676,8 @@ __global__ __launch_bounds__(1024) void variant_lanes_kernel(const int64_t* __re
     const int64_t xb = rb + per * split;
     const int64_t xe = xb + per < re ? xb + per : re;
     int32_t* row = I + (i - r0) * ldI - c0;
-    for (int64_t bb = xb; bb < xe; bb += VBATCH) {
-        const int nb = (int)(xe - bb < VBATCH ? xe - bb : VBATCH);
+    for (int64_t bb = xb; bb < xe; bb += VB) {
+        const int nb = (int)(xe - bb < VB ? xe - bb : VB);
         for (int t = threadIdx.x; t < nb; t += blockDim.x) {
             const uint32_t e = sent[bb + t];
             int64_t y = upper ? (int64_t)e + 1 : (int64_t)vbeg[e];
@@ -685,8 +692,8 @@ __global__ __launch_bounds__(1024) void variant_lanes_kernel(const int64_t* __re
             }
             ypos[t] = (uint32_t)y;
         }
-        for (int64_t cb = lo - ((lo - c0) % VCH); cb < c1; cb += VCH) {
-            const int64_t ce = cb + VCH < c1 ? cb + VCH : c1;
+        for (int64_t cb = lo - ((lo - c0) % CH); cb < c1; cb += CH) {
+            const int64_t ce = cb + CH < c1 ? cb + CH : c1;
             const int n = (int)(ce - cb);
             __syncthreads();
             for (int t = threadIdx.x; t < n; t += blockDim.x) cnt[t] = 0;
@@ -1291,11 +1298,15 @@ void variant_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1,
     FamilyTimer ft(ctx, GDIST_KERNEL_VARIANT, rs);
     // 1,024 threads: the walk is latency-bound and its 72 KiB of LDS allow two
     // workgroups a CU, so 16 waves each fill the CU's 32 wave slots
-    // option variant_walk: 1 (default) a lane per entry, 0 a wave per entry
-    auto* kern = ctx->option(OPT_VARIANT_WALK, 1) != 0 ? variant_lanes_kernel : variant_rows_kernel;
-    kern<<<(unsigned)grid, 1024, 0, rs>>>(s->vs_off.as<int64_t>(), s->vs_ent.as<uint32_t>(), s->vw_set.as<uint32_t>(),
+    // option variant_walk: 1 (default) a lane per entry, 0 a wave per entry;
+    // variant_small (default 1): the lane walk's 28 KiB workgroups
+    const bool lanes = ctx->option(OPT_VARIANT_WALK, 1) != 0, small = lanes && ctx->option(OPT_VARIANT_SMALL, 1) != 0;
+    auto* kern = !lanes ? variant_rows_kernel
+                        : small ? variant_lanes_kernel<256, 6144, 1024> : variant_lanes_kernel<1024, VCH, VBATCH>;
+    kern<<<(unsigned)(small ? 4 * grid : grid), small ? 256 : 1024, 0, rs>>>(s->vs_off.as<int64_t>(), s->vs_ent.as<uint32_t>(), s->vw_set.as<uint32_t>(),
                                           s->vw_mask.as<unsigned long long>(), s->vw_beg.as<uint32_t>(),
-                                          s->vw_end.as<uint32_t>(), r0, r1, c0, c1, nsplit, upper ? 1 : 0, d_I, ldI);
+                                          s->vw_end.as<uint32_t>(), r0, r1, c0, c1, small ? 4 * nsplit : nsplit,
+                                          upper ? 1 : 0, d_I, ldI);
     GD_HIP(hipGetLastError());
     ft.end();
 }

@@ -701,21 +701,22 @@ def test_k32_all_ones_code(ctx, strand):
 
 # ---------------------------------------------------------------- two-tier dictionary
 @pytest.mark.parametrize("dedup", ["1", "0"])
-@pytest.mark.parametrize("kernel", ["0", "1", "1w", "1l", "1lw", "1x", "1d", "1dw"])
+@pytest.mark.parametrize("kernel", ["0", "1", "1w", "1l", "1lw", "1x", "1d", "1dw", "1n"])
 @pytest.mark.parametrize("T", [0, 3, 8, 1000])
 def test_rare_tier_thresholds_exact(ctx, T, kernel, dedup, opts):
     """Dense-only (T=0), mixed, and all-rare (T > N) dictionaries give the
     same bit-exact counts and distances as the oracle, through the list-major
     (0) and the row-major (1: 2-byte list members, 1w: 4-byte; 512-thread
     workgroups, 256 as 1l / 1lw, 1,024 as 1x; 1d / 1dw: every record once,
-    members added to I by atomics, option rare_direct — C4's wide rows) rare kernel,
+    members added to I by atomics, option rare_direct — C4's wide rows; the
+    LDS walk's counters 16-bit by default, 1n: 32-bit, option rare_c16) rare kernel,
     with identical posting lists merged into weighted lists (1) or one list
     per kmer (0). T > N puts lists of up to N members in the rare tier: the
     wave-cooperative long-list walks."""
     import gdist
     opts(rare_kernel=int(kernel[0]), rare_dedup=int(dedup), rare_u16=0 if kernel.endswith("w") else None,
          rare_rows_threads=256 if "l" in kernel else 1024 if "x" in kernel else None,
-         rare_direct=1 if "d" in kernel else None)
+         rare_direct=1 if "d" in kernel else None, rare_c16=0 if "n" in kernel else None)
     n = 200
     seqs = synth_sets(n, 6000, 0.01, 101)
     sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
@@ -750,6 +751,31 @@ def test_rare_tier_thresholds_exact(ctx, T, kernel, dedup, opts):
     d = sets.row_query(77, cols)
     _, eD = oracle.matrix(off, codes, 77, 78, 0, n)
     assert bits_equal(d, eD[0, cols])
+
+
+@pytest.mark.parametrize("c16", [None, 0])
+def test_rare_rows_heavy_rows_exact(ctx, opts, c16):
+    """The row-major rare walk's 16-bit LDS counters (round 5, option
+    rare_c16) are used only while every row's rare weight stays below 2^16:
+    six 120 kbp genomes of one ancestor with rare_t 7 put every shared kmer
+    (~240 K a genome, both strands) in the rare tier, merged into a few
+    heavy lists, so a row weighs > 65,536 and the walk must keep 32-bit
+    counters; counts and distances equal the oracle."""
+    import gdist
+    opts(rare_kernel=1, rare_c16=c16)
+    n = 6
+    seqs = synth_sets(n, 120_000, 0.002, 141)
+    sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
+    sets.build_bitsets(rare_threshold=7)
+    assert sets.rare_kmers() > 65536
+    off, codes = oracle_pack(seqs, 21, 0, 0)
+    eI, eD = oracle.matrix(off, codes, 0, n, 0, n, flags=0, nthreads=4)
+    assert eI[0, 1] > 65536                          # the premise: pair counts past 2^16
+    for up in (True, False):
+        I, D = sets.matrix(upper=up, method=gdist.METHOD_BITSET)
+        iu = np.triu_indices(n, 1) if up else np.where(np.ones((n, n), bool))
+        assert np.array_equal(I[iu], eI[iu]), (c16, up)
+        assert bits_equal(D[iu], eD[iu])
 
 
 SPARSE_MODES = {

@@ -184,16 +184,17 @@ def test_variant_walk_across_column_chunks(ctx, opts):
     sets.build_bitsets()
     vk, vw, ve, vp = sets.variant_info()
     assert vk > 0 and ve > 0, (vk, vw, ve)
-    for walk, direct in ((None, None), (0, None), (None, 0), (None, 1), (0, 1)):
-        # variant_walk 0: a wave per entry; default: a lane per entry (4-wide loads)
-        opts(rare_direct=direct, variant_walk=walk)
+    for walk, direct, small in ((None, None, None), (0, None, None), (None, 0, 0), (None, 1, None), (0, 1, None)):
+        # variant_walk 0: a wave per entry; default: a lane per entry (4-wide
+        # loads) in 256-thread 28 KiB workgroups (variant_small 0: 1,024 threads, 72 KiB)
+        opts(rare_direct=direct, variant_walk=walk, variant_small=small)
         for (r0, r1, up) in [(0, 24, True), (16370, 16400, True), (500, 520, False), (0, 8, False)]:
             I, D = sets.matrix((r0, r1), (0, n), upper=up, method=gdist.METHOD_BITSET)
             eI, eD = oracle.matrix(off, codes, r0, r1, 0, n, flags=0x100 if up else 0, nthreads=8)
             if up:
                 mask = np.fromfunction(lambda a, b: b > (r0 + a), (r1 - r0, n))
                 I, D, eI, eD = I[mask], D[mask], eI[mask], eD[mask]
-            assert np.array_equal(I, eI), (walk, direct, r0, r1, np.flatnonzero(I != eI)[:5])
+            assert np.array_equal(I, eI), (walk, direct, small, r0, r1, np.flatnonzero(I != eI)[:5])
             assert bits_equal(D, eD), (walk, direct, r0, r1)
 
 
