@@ -241,8 +241,6 @@ struct Timing {
     X(VARIANT, "variant")                     /* variant tier: 1 force, 0 off (default: by the dictionary) */ \
     X(VARIANT_DMIN, "variant_dmin")           /* sets holding a dense-tier kmer (default N / 10) */            \
     X(RANGE_SUMMARY, "range_summary")         /* 1: the code-range dictionary whatever the size, 0: never */  \
-    X(VARIANT_WALK, "variant_walk")           /* variant walk: 1 (default) a lane per entry, 0 a wave per entry */ \
-    X(VARIANT_SMALL, "variant_small")         /* lane walk: 1 (default) 256-thread 28 KiB workgroups beside the MFMA tiles, 0 1024-thread 72 KiB */ \
     X(RARE_C16, "rare_c16")                   /* row-major rare walk: 1 (default) 16-bit LDS counters when every row's rare weight < 2^16, 0 32-bit */ \
     X(SERIAL_STEP, "serial_step")             /* 1: the side stream's kernel families on the main stream, in turn (timing) */ \
     X(SPLIT_BUILD, "split_build")             /* gathered collection on R ranks: each builds 1/R and all-gathers (default); 0 every rank all; k >= 2 without peers: k shares in turn here */

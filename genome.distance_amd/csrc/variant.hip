@@ -466,22 +466,11 @@ __global__ void entry_fields_kernel(const uint64_t* __restrict__ key, const int3
     }
 }
 
-// set-side keys (set, list-length class, entry): a set's entries ordered by
-// the length of their word lists (8-bit class: octave and 3 bits under it),
-// so the lanes of a wave (variant_lanes_kernel) walk lists of similar length;
-// lbits = 0 when the set index leaves no room
-__global__ void set_keys_kernel(const uint32_t* __restrict__ vset, const uint32_t* __restrict__ beg,
-                                const uint32_t* __restrict__ end, int64_t E, int lbits, uint64_t* __restrict__ skey) {
+// set-side keys (set, entry)
+__global__ void set_keys_kernel(const uint32_t* __restrict__ vset, int64_t E, uint64_t* __restrict__ skey) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += stride) {
-        const uint32_t len = end[e] - beg[e];
-        uint64_t c = 0;
-        if (lbits && len) {
-            const int lg = 31 - __clz(len);
-            c = lg < 3 ? len : ((uint64_t)lg << 3) | ((len >> (lg - 3)) & 7u);
-        }
-        skey[e] = ((uint64_t)vset[e] << (31 + lbits)) | (c << 31) | (uint64_t)e;
-    }
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += stride)
+        skey[e] = ((uint64_t)vset[e] << 32) | (uint64_t)e;
 }
 
 // word w's list = entries [woff[w], woff[w + 1])
@@ -630,120 +619,6 @@ __global__ __launch_bounds__(1024) void variant_rows_kernel(const int64_t* __res
                     }
                 }
                 if (lane == 0) ypos[t] = (uint32_t)y;
-            }
-            __syncthreads();
-            for (int t = threadIdx.x; t < n; t += blockDim.x) {
-                const int v = cnt[t];
-                if (v && cb + t >= lo) atomicAdd(row + cb + t, v);
-            }
-        }
-    }
-}
-
-// Round 5: a lane per entry. On C4 about 82 members of an entry's list fall
-// in one 16,384-column chunk, so the wave-per-entry walk above ran its lanes
-// at ~64 % and waited one dependent load round trip per 64 members (0.21 of
-// HBM, 13.6 ms on the 1,024-row slice). Here each lane streams its own
-// entry's list four members a step (one 16-byte load of sets, two of
-// masks), loading the next four before counting these: the loads of the
-// whole wave's 64 lists are in flight at once. The build orders each set's
-// entries by list length, so a wave's lanes walk lists of similar length.
-// Same grid, batches, chunks and per-entry positions as variant_rows_kernel.
-// Template: NT threads, CH columns of int32 counters per chunk, VB entries a
-// batch. <1024, VCH, VBATCH>: 72 KiB (two workgroups a CU); <256, 6144, 1024>
-// (option variant_small, default): 28 KiB and one wave a SIMD, so that a
-// workgroup fits on a CU beside an MFMA dense-tile workgroup (128 KiB of LDS;
-// 2 waves a SIMD of 208 VGPRs leave 96 of the SIMD's 512: one 56-VGPR wave):
-// the C4 step's two launches then share every CU instead of taking turns.
-template <int NT, int CH, int VB>
-__global__ __launch_bounds__(NT) void variant_lanes_kernel(const int64_t* __restrict__ soff,
-                                                            const uint32_t* __restrict__ sent,
-                                                            const uint32_t* __restrict__ vset,
-                                                            const unsigned long long* __restrict__ vmask,
-                                                            const uint32_t* __restrict__ vbeg,
-                                                            const uint32_t* __restrict__ vend, int64_t r0, int64_t r1,
-                                                            int64_t c0, int64_t c1, int nsplit, int upper,
-                                                            int32_t* __restrict__ I, int64_t ldI) {
-    __shared__ int32_t cnt[CH];
-    __shared__ uint32_t ypos[VB];
-    const int64_t i = r0 + blockIdx.x / nsplit;
-    const int split = blockIdx.x % nsplit;
-    if (i >= r1) return;
-    const int64_t lo = upper && i + 1 > c0 ? i + 1 : c0;
-    if (lo >= c1) return;
-    const int64_t rb = soff[i], re = soff[i + 1];
-    const int64_t per = (re - rb + nsplit - 1) / nsplit;
-    const int64_t xb = rb + per * split;
-    const int64_t xe = xb + per < re ? xb + per : re;
-    int32_t* row = I + (i - r0) * ldI - c0;
-    for (int64_t bb = xb; bb < xe; bb += VB) {
-        const int nb = (int)(xe - bb < VB ? xe - bb : VB);
-        for (int t = threadIdx.x; t < nb; t += blockDim.x) {
-            const uint32_t e = sent[bb + t];
-            int64_t y = upper ? (int64_t)e + 1 : (int64_t)vbeg[e];
-            const int64_t ye = vend[e];
-            if (!upper || lo > i + 1) {
-                int64_t a = y, z = ye;
-                while (a < z) {
-                    const int64_t mid = (a + z) >> 1;
-                    if ((int64_t)vset[mid] < lo) a = mid + 1; else z = mid;
-                }
-                y = a;
-            }
-            ypos[t] = (uint32_t)y;
-        }
-        for (int64_t cb = lo - ((lo - c0) % CH); cb < c1; cb += CH) {
-            const int64_t ce = cb + CH < c1 ? cb + CH : c1;
-            const int n = (int)(ce - cb);
-            __syncthreads();
-            for (int t = threadIdx.x; t < n; t += blockDim.x) cnt[t] = 0;
-            __syncthreads();
-            for (int t = threadIdx.x; t < nb; t += blockDim.x) {
-                const uint32_t e = sent[bb + t];
-                const unsigned long long mi = vmask[e];
-                const int64_t ye = vend[e];
-                int64_t y = ypos[t];
-                if (y < ye) {
-                    // groups of four from the aligned index at or below y
-                    // (the lists' arrays carry 4 slack entries past E)
-                    int64_t q = y & ~int64_t(3);
-                    uint4 js = *reinterpret_cast<const uint4*>(vset + q);
-                    ulonglong2 ma = *reinterpret_cast<const ulonglong2*>(vmask + q);
-                    ulonglong2 mb = *reinterpret_cast<const ulonglong2*>(vmask + q + 2);
-                    for (;;) {
-                        const int64_t qn = q + 4;
-                        // the next group holds members of this chunk: all four here are below ce
-                        const bool go = qn < ye && (int64_t)js.w < ce;
-                        uint4 jn = js;
-                        ulonglong2 na = ma, nbm = mb;
-                        if (go) {
-                            jn = *reinterpret_cast<const uint4*>(vset + qn);
-                            na = *reinterpret_cast<const ulonglong2*>(vmask + qn);
-                            nbm = *reinterpret_cast<const ulonglong2*>(vmask + qn + 2);
-                        }
-                        const uint32_t jj[4] = {js.x, js.y, js.z, js.w};
-                        const unsigned long long mm[4] = {ma.x, ma.y, mb.x, mb.y};
-                        int64_t ny = qn < ye ? qn : ye;
-#pragma unroll
-                        for (int k = 3; k >= 0; k--) {
-                            const int64_t x = q + k;
-                            if (x < y || x >= ye) continue;
-                            if ((int64_t)jj[k] >= ce) {
-                                ny = x;                        // lists ascend: the first member past the chunk
-                            } else if ((int64_t)jj[k] != i) {
-                                const int v = __popcll(mi & mm[k]);
-                                if (v) atomicAdd(&cnt[jj[k] - cb], v);
-                            }
-                        }
-                        y = ny;
-                        if (!go) break;
-                        q = qn;
-                        js = jn;
-                        ma = na;
-                        mb = nbm;
-                    }
-                }
-                ypos[t] = (uint32_t)y;
             }
             __syncthreads();
             for (int t = threadIdx.x; t < n; t += blockDim.x) {
@@ -1192,8 +1067,8 @@ void build_variant_bitsets(gdist_ctx* ctx, gdist_sets* s, DevBuf& dict, DevBuf& 
         int32_t* v = iA.as<int32_t>(); int32_t* va = iB.as<int32_t>();
         sort_pairs_u64_i32(ctx, k, ka, v, va, (size_t)E, 0, wbits + sbits);
         tr.mark("variant: entries sorted by (word, set)");
-        s->vw_set.alloc(E * 4 + 32, st);                    // 4-wide loads read up to 3 entries past a list
-        s->vw_mask.alloc(E * 8 + 32, st);
+        s->vw_set.alloc(E * 4 + 16, st);
+        s->vw_mask.alloc(E * 8 + 16, st);
         DevBuf skey(E * 8 + 8, st), skalt(E * 8 + 8, st);
         entry_fields_kernel<<<grid_for(E), 256, 0, st>>>(k, v, E, sbits, mall.as<unsigned long long>(),
                                                          s->vw_set.as<uint32_t>(), s->vw_mask.as<unsigned long long>());
@@ -1205,18 +1080,14 @@ void build_variant_bitsets(gdist_ctx* ctx, gdist_sets* s, DevBuf& dict, DevBuf& 
         entry_bounds_kernel<<<grid_for(E), 256, 0, st>>>(k, E, sbits, woff.as<int64_t>(), s->vw_beg.as<uint32_t>(),
                                                          s->vw_end.as<uint32_t>());
         GD_HIP(hipGetLastError());
-        // the set side: each set's entries by list length (8 class bits when the set index leaves room)
-        const int lbits = 31 + 8 + sbits <= 64 ? 8 : 0;
-        set_keys_kernel<<<grid_for(E), 256, 0, st>>>(s->vw_set.as<uint32_t>(), s->vw_beg.as<uint32_t>(),
-                                                     s->vw_end.as<uint32_t>(), E, lbits, skey.as<uint64_t>());
+        set_keys_kernel<<<grid_for(E), 256, 0, st>>>(s->vw_set.as<uint32_t>(), E, skey.as<uint64_t>());
         GD_HIP(hipGetLastError());
-        tr.mark("variant: word lists");
         uint64_t* sk = skey.as<uint64_t>(); uint64_t* ska = skalt.as<uint64_t>();
-        sort_keys_u64(ctx, sk, ska, (size_t)E, 0, 31 + lbits + sbits);
+        sort_keys_u64(ctx, sk, ska, (size_t)E, 0, 32 + sbits);
         tr.mark("variant: set side sorted");
         s->vs_off.alloc((N + 1) * 8, st);
         s->vs_ent.alloc(E * 4 + 4, st);
-        set_offsets_kernel<<<grid_for(std::max<int64_t>(E, N + 1)), 256, 0, st>>>(sk, E, N, 31 + lbits,
+        set_offsets_kernel<<<grid_for(std::max<int64_t>(E, N + 1)), 256, 0, st>>>(sk, E, N, 32,
                                                                                   s->vs_off.as<int64_t>(),
                                                                                   s->vs_ent.as<uint32_t>());
         GD_HIP(hipGetLastError());
@@ -1298,15 +1169,10 @@ void variant_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1,
     FamilyTimer ft(ctx, GDIST_KERNEL_VARIANT, rs);
     // 1,024 threads: the walk is latency-bound and its 72 KiB of LDS allow two
     // workgroups a CU, so 16 waves each fill the CU's 32 wave slots
-    // option variant_walk: 1 (default) a lane per entry, 0 a wave per entry;
-    // variant_small (default 1): the lane walk's 28 KiB workgroups
-    const bool lanes = ctx->option(OPT_VARIANT_WALK, 1) != 0, small = lanes && ctx->option(OPT_VARIANT_SMALL, 1) != 0;
-    auto* kern = !lanes ? variant_rows_kernel
-                        : small ? variant_lanes_kernel<256, 6144, 1024> : variant_lanes_kernel<1024, VCH, VBATCH>;
-    kern<<<(unsigned)(small ? 4 * grid : grid), small ? 256 : 1024, 0, rs>>>(s->vs_off.as<int64_t>(), s->vs_ent.as<uint32_t>(), s->vw_set.as<uint32_t>(),
-                                          s->vw_mask.as<unsigned long long>(), s->vw_beg.as<uint32_t>(),
-                                          s->vw_end.as<uint32_t>(), r0, r1, c0, c1, small ? 4 * nsplit : nsplit,
-                                          upper ? 1 : 0, d_I, ldI);
+    variant_rows_kernel<<<(unsigned)grid, 1024, 0, rs>>>(s->vs_off.as<int64_t>(), s->vs_ent.as<uint32_t>(),
+                                                        s->vw_set.as<uint32_t>(), s->vw_mask.as<unsigned long long>(),
+                                                        s->vw_beg.as<uint32_t>(), s->vw_end.as<uint32_t>(), r0, r1, c0,
+                                                        c1, nsplit, upper ? 1 : 0, d_I, ldI);
     GD_HIP(hipGetLastError());
     ft.end();
 }

@@ -1,7 +1,7 @@
 """In-process A/B of context options (gdist_ctx_set_option, named GDIST_<OPTION> here):
 interleaved rounds on one collection; every setting's counts must equal the
 first one's. AB_ENVS="K=V,K=V;K=V;..." (";" separates settings, "" = defaults),
-AB_N sets (C2-like 2 Mbp genomes), AB_BLOCKS="r0:r1 ..." row blocks (default
+AB_N sets (C2-like 2 Mbp genomes; AB_CONFIG=c2r: C2-realistic), AB_BLOCKS="r0:r1 ..." row blocks (default
 the whole triangle), or AB_RANKS=G: the G blocks of the cost-balanced partition."""
 import os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -15,10 +15,15 @@ settings = [s for s in os.environ.get("AB_ENVS", "").split(";")]
 rounds = int(os.environ.get("AB_ROUNDS", "5"))
 ctx = gdist.Context(0)
 ctx.set_option("step_timing", 1)     # graph-replayed steps record their kernel times too
-g = synth.genomes(n, 2_000_000, 0.002, 2)
-blob, off = synth.to_blob(g); del g
-sets = gdist.KmerSets.from_sequences([blob[off[i]:off[i + 1]] for i in range(n)], 21, gdist.KmerType.DNA, 0, ctx)
-del blob
+if os.environ.get("AB_CONFIG", "c2") == "c2r":       # C2-realistic (bench.py CONFIGS["c2r"])
+    seqs = synth.realistic_genomes(n, 2_000_000, 0.002, 2)
+    sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
+    del seqs
+else:
+    g = synth.genomes(n, 2_000_000, 0.002, 2)
+    blob, off = synth.to_blob(g); del g
+    sets = gdist.KmerSets.from_sequences([blob[off[i]:off[i + 1]] for i in range(n)], 21, gdist.KmerType.DNA, 0, ctx)
+    del blob
 sets.build_bitsets()
 blocks = []
 for b in os.environ.get("AB_BLOCKS", f"0:{n}").split():

@@ -171,9 +171,8 @@ def test_variant_walk_across_column_chunks(ctx, opts):
     16,384 (VCH) and keeps each list's position from chunk to chunk (C4:
     100,000 columns, 7 chunks); round 5 loads the next 64 members of a list
     before counting the current ones. 17,000 sets: rows whose lists cross
-    chunk boundaries, both rare walks (LDS chunks and direct atomics) and
-    both variant walks (a wave per entry, a lane per entry), equal the
-    oracle."""
+    chunk boundaries, both rare walks (LDS chunks and direct atomics), equal
+    the oracle."""
     import gdist
     from gdist import synth
     n = 17000
@@ -184,18 +183,16 @@ def test_variant_walk_across_column_chunks(ctx, opts):
     sets.build_bitsets()
     vk, vw, ve, vp = sets.variant_info()
     assert vk > 0 and ve > 0, (vk, vw, ve)
-    for walk, direct, small in ((None, None, None), (0, None, None), (None, 0, 0), (None, 1, None), (0, 1, None)):
-        # variant_walk 0: a wave per entry; default: a lane per entry (4-wide
-        # loads) in 256-thread 28 KiB workgroups (variant_small 0: 1,024 threads, 72 KiB)
-        opts(rare_direct=direct, variant_walk=walk, variant_small=small)
+    for direct in (None, 0, 1):
+        opts(rare_direct=direct)
         for (r0, r1, up) in [(0, 24, True), (16370, 16400, True), (500, 520, False), (0, 8, False)]:
             I, D = sets.matrix((r0, r1), (0, n), upper=up, method=gdist.METHOD_BITSET)
             eI, eD = oracle.matrix(off, codes, r0, r1, 0, n, flags=0x100 if up else 0, nthreads=8)
             if up:
                 mask = np.fromfunction(lambda a, b: b > (r0 + a), (r1 - r0, n))
                 I, D, eI, eD = I[mask], D[mask], eI[mask], eD[mask]
-            assert np.array_equal(I, eI), (walk, direct, small, r0, r1, np.flatnonzero(I != eI)[:5])
-            assert bits_equal(D, eD), (walk, direct, r0, r1)
+            assert np.array_equal(I, eI), (direct, r0, r1, np.flatnonzero(I != eI)[:5])
+            assert bits_equal(D, eD), (direct, r0, r1)
 
 
 @pytest.mark.parametrize("mode", ["variant", "variant_windowed_fill", "two_tier", "two_tier_sort_fill"])
