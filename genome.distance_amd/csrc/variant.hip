@@ -544,6 +544,12 @@ namespace {
 // entry's list position is kept in LDS between chunks (lists are sorted by
 // set), so a list is read once across all chunks and no chunk searches it.
 constexpr int VBATCH = 2048;
+// C16 (round 5, option variant_c16): 16-bit counters, two to a dword, so a
+// chunk is 32,768 columns (C4's 100,000 in 4 chunks instead of 7: fewer
+// (entry, chunk) visits, fuller 64-member steps); a batch then holds at most
+// 1,023 entries, so a pair's count in it is at most 1,023 x 64 < 2^16 (a
+// set holds one entry per word, and each entry adds at most 64).
+template <bool C16>
 __global__ __launch_bounds__(1024) void variant_rows_kernel(const int64_t* __restrict__ soff,
                                                            const uint32_t* __restrict__ sent,
                                                            const uint32_t* __restrict__ vset,
@@ -552,6 +558,7 @@ __global__ __launch_bounds__(1024) void variant_rows_kernel(const int64_t* __res
                                                            const uint32_t* __restrict__ vend, int64_t r0, int64_t r1,
                                                            int64_t c0, int64_t c1, int nsplit, int upper,
                                                            int32_t* __restrict__ I, int64_t ldI) {
+    constexpr int CH = C16 ? 2 * VCH : VCH, VB = C16 ? 1023 : VBATCH;
     __shared__ int32_t cnt[VCH];
     __shared__ uint32_t ypos[VBATCH];
     const int64_t i = r0 + blockIdx.x / nsplit;
@@ -565,8 +572,8 @@ __global__ __launch_bounds__(1024) void variant_rows_kernel(const int64_t* __res
     const int64_t xe = xb + per < re ? xb + per : re;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, nwv = (int)(blockDim.x >> 6);
     int32_t* row = I + (i - r0) * ldI - c0;                   // row[j] for column j
-    for (int64_t bb = xb; bb < xe; bb += VBATCH) {
-        const int nb = (int)(xe - bb < VBATCH ? xe - bb : VBATCH);
+    for (int64_t bb = xb; bb < xe; bb += VB) {
+        const int nb = (int)(xe - bb < VB ? xe - bb : VB);
         // each entry's first list position at or past the row's first column
         // (upper: the members after the row's own entry)
         for (int t = wv; t < nb; t += nwv) {
@@ -583,11 +590,11 @@ __global__ __launch_bounds__(1024) void variant_rows_kernel(const int64_t* __res
             }
             if (lane == 0) ypos[t] = (uint32_t)y;
         }
-        for (int64_t cb = lo - ((lo - c0) % VCH); cb < c1; cb += VCH) {
-            const int64_t ce = cb + VCH < c1 ? cb + VCH : c1;
+        for (int64_t cb = lo - ((lo - c0) % CH); cb < c1; cb += CH) {
+            const int64_t ce = cb + CH < c1 ? cb + CH : c1;
             const int n = (int)(ce - cb);
             __syncthreads();                                   // ypos written; previous chunk flushed
-            for (int t = threadIdx.x; t < n; t += blockDim.x) cnt[t] = 0;
+            for (int t = threadIdx.x; t < (C16 ? (n + 1) >> 1 : n); t += blockDim.x) cnt[t] = 0;
             __syncthreads();
             for (int t = wv; t < nb; t += nwv) {                 // a wave per entry
                 const uint32_t e = sent[bb + t];
@@ -608,7 +615,10 @@ __global__ __launch_bounds__(1024) void variant_rows_kernel(const int64_t* __res
                         const unsigned long long mn = yn < ye ? vmask[yn] : 0ull;
                         if (in && (int64_t)j != i) {
                             const int v = __popcll(mi & mj);
-                            if (v) atomicAdd(&cnt[j - cb], v);
+                            if (v) {
+                                if (C16) atomicAdd(&cnt[(j - cb) >> 1], v << (((j - cb) & 1) << 4));
+                                else atomicAdd(&cnt[j - cb], v);
+                            }
                         }
                         const unsigned long long m = __ballot(in);
                         y += __popcll(m);                      // lists ascend: the in-chunk members come first
@@ -622,7 +632,7 @@ __global__ __launch_bounds__(1024) void variant_rows_kernel(const int64_t* __res
             }
             __syncthreads();
             for (int t = threadIdx.x; t < n; t += blockDim.x) {
-                const int v = cnt[t];
+                const int v = C16 ? (int)(((uint32_t)cnt[t >> 1] >> ((t & 1) << 4)) & 0xFFFFu) : cnt[t];
                 if (v && cb + t >= lo) atomicAdd(row + cb + t, v);
             }
         }
@@ -1163,13 +1173,18 @@ void variant_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1,
     if (!s->variant || r1 <= r0 || c1 <= c0) return;
     const int64_t units = r1 - r0;
     // few rows: slice each row's entries over several workgroups
-    const int nsplit = (int)std::max<int64_t>(1, std::min<int64_t>(64, ceil_div((int64_t)ctx->cus * 8, units)));
+    // (option variant_split: a given number of slices a row)
+    const int nsplit = ctx->has_option(OPT_VARIANT_SPLIT)
+                           ? (int)std::max<int64_t>(1, std::min<int64_t>(64, ctx->option(OPT_VARIANT_SPLIT, 1)))
+                           : (int)std::max<int64_t>(1, std::min<int64_t>(64, ceil_div((int64_t)ctx->cus * 8, units)));
     const int64_t grid = units * nsplit;
     GD_REQUIRE(grid < (int64_t(1) << 31), "variant-tier grid too large");
     FamilyTimer ft(ctx, GDIST_KERNEL_VARIANT, rs);
     // 1,024 threads: the walk is latency-bound and its 72 KiB of LDS allow two
     // workgroups a CU, so 16 waves each fill the CU's 32 wave slots
-    variant_rows_kernel<<<(unsigned)grid, 1024, 0, rs>>>(s->vs_off.as<int64_t>(), s->vs_ent.as<uint32_t>(),
+    // option variant_c16: 16-bit counters, 32,768-column chunks
+    auto* kern = ctx->option(OPT_VARIANT_C16, 0) != 0 ? variant_rows_kernel<true> : variant_rows_kernel<false>;
+    kern<<<(unsigned)grid, 1024, 0, rs>>>(s->vs_off.as<int64_t>(), s->vs_ent.as<uint32_t>(),
                                                         s->vw_set.as<uint32_t>(), s->vw_mask.as<unsigned long long>(),
                                                         s->vw_beg.as<uint32_t>(), s->vw_end.as<uint32_t>(), r0, r1, c0,
                                                         c1, nsplit, upper ? 1 : 0, d_I, ldI);

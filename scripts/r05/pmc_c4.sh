@@ -9,7 +9,7 @@ set -o pipefail
 export TMPDIR=/tmp
 OUT=$1; EXTRA=${2:-}
 ARGS="--config c4 --rows 0:1024 --force-exchange --steps 3 --warmup 1 --no-cpu-baseline $EXTRA"
-RX="variant_|rare_rows|bitset_mfma"
+RX="variant_rows|rare_rows|bitset_mfma"
 mkdir -p $OUT
 run() {   # name, then rocprofv3 options
     local name=$1; shift
@@ -24,7 +24,7 @@ run sq1 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_
     SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE TA_TA_BUSY_sum --kernel-trace --kernel-include-regex "$RX" &&
 run sq2 --pmc SQ_INSTS_VMEM_RD SQ_INST_LEVEL_VMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_SALU \
     SQ_WAIT_ANY --kernel-trace --kernel-include-regex "$RX" || exit 1
-for k in variant_ rare_rows bitset_mfma_kernel; do
+for k in variant_rows_kernel rare_rows bitset_mfma_kernel; do
     python3 scripts/pmc_json.py $OUT/fetch $OUT/write $k $OUT/pmc_c4_${k%_}.json c4 100000 1 > /dev/null &&
     python3 scripts/pmc_sq_json.py $OUT/pmc_c4_${k%_}_sq.json c4 100000 $k $OUT/sq1 $OUT/sq2 > /dev/null ||
     echo "no counters for $k"
