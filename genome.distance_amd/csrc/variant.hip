@@ -544,13 +544,17 @@ namespace {
 // entry's list position is kept in LDS between chunks (lists are sorted by
 // set), so a list is read once across all chunks and no chunk searches it.
 constexpr int VBATCH = 2048;
-// C16 (round 5, option variant_c16): 16-bit counters, two to a dword, so a
+// C16 (round 5, option variant_c16, default): 16-bit counters, two to a dword, so a
 // chunk is 32,768 columns (C4's 100,000 in 4 chunks instead of 7: fewer
 // (entry, chunk) visits, fuller 64-member steps); a batch then holds at most
 // 1,023 entries, so a pair's count in it is at most 1,023 x 64 < 2^16 (a
 // set holds one entry per word, and each entry adds at most 64).
-template <bool C16>
-__global__ __launch_bounds__(1024) void variant_rows_kernel(const int64_t* __restrict__ soff,
+// VW counter dwords of LDS and NT threads: <.., VCH, 1024> (72 KiB, two
+// workgroups a CU), or <true, 7168, 512> (option variant_cores: 32 KiB and
+// two 40-VGPR waves a SIMD, so a workgroup fits on a CU beside an MFMA
+// dense-tile workgroup's 128 KiB and 2 x 208 VGPRs a SIMD)
+template <bool C16, int VW, int NT>
+__global__ __launch_bounds__(NT) void variant_rows_kernel(const int64_t* __restrict__ soff,
                                                            const uint32_t* __restrict__ sent,
                                                            const uint32_t* __restrict__ vset,
                                                            const unsigned long long* __restrict__ vmask,
@@ -558,9 +562,9 @@ __global__ __launch_bounds__(1024) void variant_rows_kernel(const int64_t* __res
                                                            const uint32_t* __restrict__ vend, int64_t r0, int64_t r1,
                                                            int64_t c0, int64_t c1, int nsplit, int upper,
                                                            int32_t* __restrict__ I, int64_t ldI) {
-    constexpr int CH = C16 ? 2 * VCH : VCH, VB = C16 ? 1023 : VBATCH;
-    __shared__ int32_t cnt[VCH];
-    __shared__ uint32_t ypos[VBATCH];
+    constexpr int CH = C16 ? 2 * VW : VW, VB = C16 ? 1023 : VBATCH;
+    __shared__ int32_t cnt[VW];
+    __shared__ uint32_t ypos[VB];
     const int64_t i = r0 + blockIdx.x / nsplit;
     const int split = blockIdx.x % nsplit;
     if (i >= r1) return;
@@ -1182,9 +1186,12 @@ void variant_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1,
     FamilyTimer ft(ctx, GDIST_KERNEL_VARIANT, rs);
     // 1,024 threads: the walk is latency-bound and its 72 KiB of LDS allow two
     // workgroups a CU, so 16 waves each fill the CU's 32 wave slots
-    // option variant_c16: 16-bit counters, 32,768-column chunks
-    auto* kern = ctx->option(OPT_VARIANT_C16, 0) != 0 ? variant_rows_kernel<true> : variant_rows_kernel<false>;
-    kern<<<(unsigned)grid, 1024, 0, rs>>>(s->vs_off.as<int64_t>(), s->vs_ent.as<uint32_t>(),
+    // option variant_c16 (default 1): 16-bit counters, 32,768-column chunks;
+    // variant_cores = 1: 512-thread 32 KiB workgroups (beside the MFMA tiles)
+    const bool c16 = ctx->option(OPT_VARIANT_C16, 1) != 0, cores = c16 && ctx->option(OPT_VARIANT_CORES, 0) != 0;
+    auto* kern = cores ? variant_rows_kernel<true, 7168, 512>
+                       : c16 ? variant_rows_kernel<true, VCH, 1024> : variant_rows_kernel<false, VCH, 1024>;
+    kern<<<(unsigned)grid, cores ? 512 : 1024, 0, rs>>>(s->vs_off.as<int64_t>(), s->vs_ent.as<uint32_t>(),
                                                         s->vw_set.as<uint32_t>(), s->vw_mask.as<unsigned long long>(),
                                                         s->vw_beg.as<uint32_t>(), s->vw_end.as<uint32_t>(), r0, r1, c0,
                                                         c1, nsplit, upper ? 1 : 0, d_I, ldI);
