@@ -564,10 +564,14 @@ def main():
                 # list members: 2 bytes for collections of <= 65,536 sets (option rare_u16)
                 mbytes = 2.0 if N <= 65536 and ctx.option("rare_u16") != 0 else 4.0
                 rare_bytes = 14.0 * rec * f_rows + mbytes * incs * f_pairs + 8.0 * pairs_rank
-                rk = "rare_rows_kernel" if sets.block_cost((r0, r1))[1] == 1 else "rare_pairs_kernel"
+                # row-major: past one 16,384-column LDS chunk the direct walk
+                # (every record once, atomics into I; option rare_direct)
+                rk = "rare_pairs_kernel"
+                if sets.block_cost((r0, r1))[1] == 1:
+                    rk = "rare_rows_direct_kernel" if N > 16384 and ctx.option("rare_direct") != 0 else "rare_rows_kernel"
                 ach = rare_bytes / (r_ms * 1e-3) / 1e9
                 rare_roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(rk),
+                             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(rk.rsplit("_kernel", 1)[0]),
                              "kernel": f"{rk} (rare tier, beside the dense tiles)", "kernel_avg_ms": round(r_ms, 4),
                              "algo_bytes_per_launch": round(rare_bytes),
                              "member_bytes": mbytes,
