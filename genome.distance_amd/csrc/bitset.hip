@@ -258,13 +258,23 @@ __global__ __launch_bounds__(NT) void rare_rows_kernel(const int64_t* __restrict
     const int64_t xb = rb + per * split;
     const int64_t xe = xb + per < re ? xb + per : re;
     const int lane = threadIdx.x & 63;
-    for (int64_t xbase = xb; xbase < xe; xbase += blockDim.x) {   // wave-uniform trip count
-        const int64_t x = xbase + threadIdx.x;
-        const uint64_t ent = x < xe ? sent[x] : 0ull;  // coalesced: no random bounds lookup
-        const int32_t w = x < xe ? (int32_t)sw[x] : 0;
+    // round 5: the thread's next record is loaded before this one's list is
+    // walked, so a record costs one dependent round trip (its list), not two
+    int64_t x = xb + threadIdx.x;
+    uint64_t ent_n = x < xe ? sent[x] : 0ull;
+    int32_t w_n = x < xe ? (int32_t)sw[x] : 0;
+    int32_t sk_n = upper && x < xe ? (int32_t)sskip[x] : 0;
+    for (int64_t xbase = xb; xbase < xe; xbase += blockDim.x, x += blockDim.x) {   // wave-uniform trip count
+        const uint64_t ent = ent_n;                    // coalesced: no random bounds lookup
+        const int32_t w = w_n;
+        const int32_t skip = sk_n;
+        const int64_t xn = x + blockDim.x;
+        ent_n = xn < xe ? sent[xn] : 0ull;
+        w_n = xn < xe ? (int32_t)sw[xn] : 0;
+        sk_n = upper && xn < xe ? (int32_t)sskip[xn] : 0;
         const int64_t b0 = (int64_t)(ent >> 24), e = b0 + (int64_t)(ent & 0xFFFFFFu);
         // upper triangle: only the members after the row's own set (ascending lists)
-        const int64_t b = upper && x < xe ? b0 + sskip[x] : b0;
+        const int64_t b = b0 + skip;
         const bool lng = e - b >= kLongList;
         for (unsigned long long m = __ballot(lng); m; m &= m - 1) {   // long lists: the wave walks them
             const int l = __ffsll((long long)m) - 1;
