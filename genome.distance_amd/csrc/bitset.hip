@@ -258,23 +258,13 @@ __global__ __launch_bounds__(NT) void rare_rows_kernel(const int64_t* __restrict
     const int64_t xb = rb + per * split;
     const int64_t xe = xb + per < re ? xb + per : re;
     const int lane = threadIdx.x & 63;
-    // round 5: the thread's next record is loaded before this one's list is
-    // walked, so a record costs one dependent round trip (its list), not two
-    int64_t x = xb + threadIdx.x;
-    uint64_t ent_n = x < xe ? sent[x] : 0ull;
-    int32_t w_n = x < xe ? (int32_t)sw[x] : 0;
-    int32_t sk_n = upper && x < xe ? (int32_t)sskip[x] : 0;
-    for (int64_t xbase = xb; xbase < xe; xbase += blockDim.x, x += blockDim.x) {   // wave-uniform trip count
-        const uint64_t ent = ent_n;                    // coalesced: no random bounds lookup
-        const int32_t w = w_n;
-        const int32_t skip = sk_n;
-        const int64_t xn = x + blockDim.x;
-        ent_n = xn < xe ? sent[xn] : 0ull;
-        w_n = xn < xe ? (int32_t)sw[xn] : 0;
-        sk_n = upper && xn < xe ? (int32_t)sskip[xn] : 0;
+    for (int64_t xbase = xb; xbase < xe; xbase += blockDim.x) {   // wave-uniform trip count
+        const int64_t x = xbase + threadIdx.x;
+        const uint64_t ent = x < xe ? sent[x] : 0ull;  // coalesced: no random bounds lookup
+        const int32_t w = x < xe ? (int32_t)sw[x] : 0;
         const int64_t b0 = (int64_t)(ent >> 24), e = b0 + (int64_t)(ent & 0xFFFFFFu);
         // upper triangle: only the members after the row's own set (ascending lists)
-        const int64_t b = b0 + skip;
+        const int64_t b = upper && x < xe ? b0 + sskip[x] : b0;
         const bool lng = e - b >= kLongList;
         for (unsigned long long m = __ballot(lng); m; m &= m - 1) {   // long lists: the wave walks them
             const int l = __ffsll((long long)m) - 1;
@@ -639,6 +629,7 @@ __global__ __launch_bounds__(NT, 4) void bitset_tile_kernel2(
 // fragment reads); units split-major and XCD-remapped as the VALU tiles.
 constexpr int MT = 256;                       // tile edge (sets)
 constexpr int64_t kMfmaMinWords = 64;         // dense words from which the MFMA tiles run (option bitset_mfma)
+constexpr int64_t kMfmaMinTiles = 64;         // ... and 256 x 256 tiles in the region (a quarter of the CUs)
 constexpr int MNT = 512;                      // threads
 // f32 is exact for integers <= 2^24: one K split's count of shared bits is
 // <= 64 x its words, so a split spans at most 2^18 words
@@ -2450,9 +2441,17 @@ static MatrixPlan& matrix_plan(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, 
     // the key holds every option the plan (and the sparse plan in it) reads,
     // so that changing one builds a new plan instead of reusing a stale one
     // the dense tiles on the matrix cores (FP4 MFMA) when there are enough
-    // words to amortise a 256 x 256 tile's stages (option bitset_mfma 0: the
-    // AND+popcount tiles)
-    const bool use_mfma = tW >= kMfmaMinWords && ctx->option(OPT_BITSET_MFMA, 1) != 0;
+    // words to amortise a 256 x 256 tile's stages and enough such tiles to
+    // fill the chip with one workgroup a CU: a region of few tiles (C2-
+    // realistic: 1,000 sets, 10 tiles, 1,936 dense words) leaves most CUs
+    // idle or splits K into slivers whose every split adds 65,536 counts
+    // atomically, where the 128 x 128 AND+popcount tiles have 4x the
+    // workgroups (option bitset_mfma: 0 the AND+popcount tiles, 1 MFMA
+    // whatever the tiles)
+    const int64_t mfma_opt = ctx->option(OPT_BITSET_MFMA, -1);
+    const int64_t t256r = ceil_div(r1 - r0, (int64_t)MT), t256c = ceil_div(c1 - c0, (int64_t)MT);
+    const int64_t t256 = upper && r0 == c0 && r1 == c1 ? t256r * (t256r + 1) / 2 : t256r * t256c;
+    const bool use_mfma = tW >= kMfmaMinWords && mfma_opt != 0 && (mfma_opt == 1 || t256 >= kMfmaMinTiles);
     const std::vector<int64_t> key{r0, r1, c0, c1, upper ? 1 : 0, split_diag ? 1 : 0, max_rr, tW, use_mfma ? 1 : 0,
                                    ctx->option(OPT_BITSET_MFMA_GROUP, 0),
                                    ctx->option(OPT_SPARSE_RARE, 1), ctx->option(OPT_SPARSE_CHUNKS, -1),

@@ -549,12 +549,8 @@ constexpr int VBATCH = 2048;
 // (entry, chunk) visits, fuller 64-member steps); a batch then holds at most
 // 1,023 entries, so a pair's count in it is at most 1,023 x 64 < 2^16 (a
 // set holds one entry per word, and each entry adds at most 64).
-// VW counter dwords of LDS and NT threads: <.., VCH, 1024> (72 KiB, two
-// workgroups a CU), or <true, 7168, 512> (option variant_cores: 32 KiB and
-// two 40-VGPR waves a SIMD, so a workgroup fits on a CU beside an MFMA
-// dense-tile workgroup's 128 KiB and 2 x 208 VGPRs a SIMD)
-template <bool C16, int VW, int NT>
-__global__ __launch_bounds__(NT) void variant_rows_kernel(const int64_t* __restrict__ soff,
+template <bool C16>
+__global__ __launch_bounds__(1024) void variant_rows_kernel(const int64_t* __restrict__ soff,
                                                            const uint32_t* __restrict__ sent,
                                                            const uint32_t* __restrict__ vset,
                                                            const unsigned long long* __restrict__ vmask,
@@ -562,8 +558,8 @@ __global__ __launch_bounds__(NT) void variant_rows_kernel(const int64_t* __restr
                                                            const uint32_t* __restrict__ vend, int64_t r0, int64_t r1,
                                                            int64_t c0, int64_t c1, int nsplit, int upper,
                                                            int32_t* __restrict__ I, int64_t ldI) {
-    constexpr int CH = C16 ? 2 * VW : VW, VB = C16 ? 1023 : VBATCH;
-    __shared__ int32_t cnt[VW];
+    constexpr int CH = C16 ? 2 * VCH : VCH, VB = C16 ? 1023 : VBATCH;
+    __shared__ int32_t cnt[VCH];
     __shared__ uint32_t ypos[VB];
     const int64_t i = r0 + blockIdx.x / nsplit;
     const int split = blockIdx.x % nsplit;
@@ -1186,15 +1182,15 @@ void variant_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1,
     FamilyTimer ft(ctx, GDIST_KERNEL_VARIANT, rs);
     // 1,024 threads: the walk is latency-bound and its 72 KiB of LDS allow two
     // workgroups a CU, so 16 waves each fill the CU's 32 wave slots
-    // option variant_c16 (default 1): 16-bit counters, 32,768-column chunks;
-    // variant_cores = 1: 512-thread 32 KiB workgroups (beside the MFMA tiles)
-    const bool c16 = ctx->option(OPT_VARIANT_C16, 1) != 0, cores = c16 && ctx->option(OPT_VARIANT_CORES, 0) != 0;
-    auto* kern = cores ? variant_rows_kernel<true, 7168, 512>
-                       : c16 ? variant_rows_kernel<true, VCH, 1024> : variant_rows_kernel<false, VCH, 1024>;
-    kern<<<(unsigned)grid, cores ? 512 : 1024, 0, rs>>>(s->vs_off.as<int64_t>(), s->vs_ent.as<uint32_t>(),
-                                                        s->vw_set.as<uint32_t>(), s->vw_mask.as<unsigned long long>(),
-                                                        s->vw_beg.as<uint32_t>(), s->vw_end.as<uint32_t>(), r0, r1, c0,
-                                                        c1, nsplit, upper ? 1 : 0, d_I, ldI);
+    // option variant_c16 (default 1): 16-bit counters, 32,768-column chunks
+    // (a workgroup of 32 KiB that fits beside an MFMA tile workgroup, 512
+    // threads and 14,336-column chunks: 12.4 vs 8.6 ms alone, step 20.3 vs
+    // 16.0 ms, profiles/r05/s10/ab_c4.txt; dropped)
+    auto* kern = ctx->option(OPT_VARIANT_C16, 1) != 0 ? variant_rows_kernel<true> : variant_rows_kernel<false>;
+    kern<<<(unsigned)grid, 1024, 0, rs>>>(s->vs_off.as<int64_t>(), s->vs_ent.as<uint32_t>(),
+                                          s->vw_set.as<uint32_t>(), s->vw_mask.as<unsigned long long>(),
+                                          s->vw_beg.as<uint32_t>(), s->vw_end.as<uint32_t>(), r0, r1, c0,
+                                          c1, nsplit, upper ? 1 : 0, d_I, ldI);
     GD_HIP(hipGetLastError());
     ft.end();
 }

@@ -909,7 +909,7 @@ def test_sparse_equals_dense_at_size(ctx, opts):
     assert np.array_equal(I[iu], oI[iu]) and bits_equal(D[iu], oD[iu])
 
 
-@pytest.mark.parametrize("mfma", [None, "nibble", "km2_group", "km2_ns3", "km2_ns4", "raw_group", 0])
+@pytest.mark.parametrize("mfma", [1, "nibble", "km2_group", "km2_ns3", "km2_ns4", "raw_group", 0, None])
 @pytest.mark.parametrize("T", [0, 3])
 def test_dense_tiles_mfma_exact(ctx, opts, mfma, T):
     """The dense tier's tiles on the matrix cores (FP4 MFMA, 256 x 256 pairs
@@ -923,14 +923,16 @@ def test_dense_tiles_mfma_exact(ctx, opts, mfma, T):
     of 3 and 4 stages (options bitset_mfma_km, bitset_mfma_group,
     bitset_mfma_ns)."""
     import gdist
+    # (a region of fewer than 64 256 x 256 tiles takes the AND+popcount
+    # tiles by default, None: the MFMA modes force them, option bitset_mfma 1)
     if mfma == "nibble":
-        opts(bitset_mfma_raw=0, sparse=0)
+        opts(bitset_mfma=1, bitset_mfma_raw=0, sparse=0)
     elif mfma == "raw_group":
-        opts(bitset_mfma_group=2, sparse=0)
+        opts(bitset_mfma=1, bitset_mfma_group=2, sparse=0)
     elif mfma == "km2_group":
-        opts(bitset_mfma_raw=0, bitset_mfma_km=2, bitset_mfma_group=2, sparse=0)
+        opts(bitset_mfma=1, bitset_mfma_raw=0, bitset_mfma_km=2, bitset_mfma_group=2, sparse=0)
     elif mfma in ("km2_ns3", "km2_ns4"):                # 3 / 4 stages in the ring
-        opts(bitset_mfma_raw=0, bitset_mfma_km=2, bitset_mfma_ns=int(mfma[-1]), sparse=0)
+        opts(bitset_mfma=1, bitset_mfma_raw=0, bitset_mfma_km=2, bitset_mfma_ns=int(mfma[-1]), sparse=0)
     else:
         opts(bitset_mfma=mfma, sparse=0)
     n = 530
@@ -965,7 +967,7 @@ def test_dense_tiles_mfma_past_f32_bound(ctx, opts, splits):
     tiles, option bitset_mfma 0)."""
     import gdist
     opts(sparse=0, bitset_mfma_splits=splits)
-    n = 4
+    n = 4                                        # one 256 x 256 tile: MFMA forced below (bitset_mfma 1)
     seqs = synth_sets(n, 10_000_000, 0.001, 131)
     sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
     _, W = sets.build_bitsets(rare_threshold=0)
@@ -974,7 +976,7 @@ def test_dense_tiles_mfma_past_f32_bound(ctx, opts, splits):
     eI, eD = oracle.matrix(off, codes, 0, n, 0, n, flags=0, nthreads=4)
     iu = np.triu_indices(n, 1)
     assert eI[iu].min() > (1 << 24), eI[iu]       # the premise: counts past 2^24
-    for mfma, raw in ((None, None), (None, 0), (0, None)):
+    for mfma, raw in ((1, None), (1, 0), (0, None)):
         opts(bitset_mfma=mfma, bitset_mfma_raw=raw)
         for up in (True, False):
             I, D = sets.matrix(upper=up, method=gdist.METHOD_BITSET)
