@@ -509,12 +509,7 @@ def main():
             d_ms, r_ms = fam_ms.get("dense", 0.0), fam_ms.get("rare", 0.0)
             wp = pairs_rank * width_words / (d_ms * 1e-3) if d_ms > 0 else 0.0
             tw = sparse_words["dense_words"] if sparse_words and sparse_words["sparse_words"] else width_words
-            # the library's choice (bitset.hip): MFMA from 64 dense words and
-            # 64 tiles of 256 x 256 pairs in the region (option bitset_mfma)
-            t_r, t_c = -(-(r1 - r0) // 256), -(-N // 256)
-            t256 = t_r * (t_r + 1) // 2 if (r0, r1) == (0, N) else t_r * t_c
-            mopt = ctx.option("bitset_mfma")
-            mfma = tw >= 64 and mopt != 0 and (mopt == 1 or t256 >= 64)
+            mfma = tw >= 64 and ctx.option("bitset_mfma") != 0
             if mfma:
                 # the dense tiles on the matrix cores: pairs x W x 64 bit-products x 2 ops
                 tops = pairs_rank * tw * 64 * 2 / (d_ms * 1e-3) / 1e12 if d_ms > 0 else 0.0

@@ -629,7 +629,6 @@ __global__ __launch_bounds__(NT, 4) void bitset_tile_kernel2(
 // fragment reads); units split-major and XCD-remapped as the VALU tiles.
 constexpr int MT = 256;                       // tile edge (sets)
 constexpr int64_t kMfmaMinWords = 64;         // dense words from which the MFMA tiles run (option bitset_mfma)
-constexpr int64_t kMfmaMinTiles = 64;         // ... and 256 x 256 tiles in the region (a quarter of the CUs)
 constexpr int MNT = 512;                      // threads
 // f32 is exact for integers <= 2^24: one K split's count of shared bits is
 // <= 64 x its words, so a split spans at most 2^18 words
@@ -2441,17 +2440,11 @@ static MatrixPlan& matrix_plan(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, 
     // the key holds every option the plan (and the sparse plan in it) reads,
     // so that changing one builds a new plan instead of reusing a stale one
     // the dense tiles on the matrix cores (FP4 MFMA) when there are enough
-    // words to amortise a 256 x 256 tile's stages and enough such tiles to
-    // fill the chip with one workgroup a CU: a region of few tiles (C2-
-    // realistic: 1,000 sets, 10 tiles, 1,936 dense words) leaves most CUs
-    // idle or splits K into slivers whose every split adds 65,536 counts
-    // atomically, where the 128 x 128 AND+popcount tiles have 4x the
-    // workgroups (option bitset_mfma: 0 the AND+popcount tiles, 1 MFMA
-    // whatever the tiles)
-    const int64_t mfma_opt = ctx->option(OPT_BITSET_MFMA, -1);
-    const int64_t t256r = ceil_div(r1 - r0, (int64_t)MT), t256c = ceil_div(c1 - c0, (int64_t)MT);
-    const int64_t t256 = upper && r0 == c0 && r1 == c1 ? t256r * (t256r + 1) / 2 : t256r * t256c;
-    const bool use_mfma = tW >= kMfmaMinWords && mfma_opt != 0 && (mfma_opt == 1 || t256 >= kMfmaMinTiles);
+    // words to amortise a 256 x 256 tile's stages, however few the tiles
+    // (C2-realistic: 10 tiles of 1,936 dense words, step 0.317 ms against
+    // 0.442 with the AND+popcount tiles, profiles/r05/s12/ab_c2r.txt;
+    // option bitset_mfma 0: the AND+popcount tiles)
+    const bool use_mfma = tW >= kMfmaMinWords && ctx->option(OPT_BITSET_MFMA, 1) != 0;
     const std::vector<int64_t> key{r0, r1, c0, c1, upper ? 1 : 0, split_diag ? 1 : 0, max_rr, tW, use_mfma ? 1 : 0,
                                    ctx->option(OPT_BITSET_MFMA_GROUP, 0),
                                    ctx->option(OPT_SPARSE_RARE, 1), ctx->option(OPT_SPARSE_CHUNKS, -1),

@@ -909,7 +909,7 @@ def test_sparse_equals_dense_at_size(ctx, opts):
     assert np.array_equal(I[iu], oI[iu]) and bits_equal(D[iu], oD[iu])
 
 
-@pytest.mark.parametrize("mfma", [1, "nibble", "km2_group", "km2_ns3", "km2_ns4", "raw_group", 0, None])
+@pytest.mark.parametrize("mfma", [None, "nibble", "km2_group", "km2_ns3", "km2_ns4", "raw_group", 0])
 @pytest.mark.parametrize("T", [0, 3])
 def test_dense_tiles_mfma_exact(ctx, opts, mfma, T):
     """The dense tier's tiles on the matrix cores (FP4 MFMA, 256 x 256 pairs
@@ -923,8 +923,6 @@ def test_dense_tiles_mfma_exact(ctx, opts, mfma, T):
     of 3 and 4 stages (options bitset_mfma_km, bitset_mfma_group,
     bitset_mfma_ns)."""
     import gdist
-    # (a region of fewer than 64 256 x 256 tiles takes the AND+popcount
-    # tiles by default, None: the MFMA modes force them, option bitset_mfma 1)
     if mfma == "nibble":
         opts(bitset_mfma=1, bitset_mfma_raw=0, sparse=0)
     elif mfma == "raw_group":
@@ -967,7 +965,7 @@ def test_dense_tiles_mfma_past_f32_bound(ctx, opts, splits):
     tiles, option bitset_mfma 0)."""
     import gdist
     opts(sparse=0, bitset_mfma_splits=splits)
-    n = 4                                        # one 256 x 256 tile: MFMA forced below (bitset_mfma 1)
+    n = 4
     seqs = synth_sets(n, 10_000_000, 0.001, 131)
     sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
     _, W = sets.build_bitsets(rare_threshold=0)
