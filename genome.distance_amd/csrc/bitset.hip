@@ -2609,13 +2609,16 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
         ft.end();
     };
     if (!ctx->capturing) GD_HIP(hipEventRecord(ctx->ev_k0, st));
-    if (side) {
-        // option serial_step = 1: the side stream's families run on the main
-        // stream before the dense tiles, one after another (each family's
-        // time alone: the C4 slice's MFMA tiles and variant walk otherwise
-        // share the CUs)
-        hipStream_t sd = ctx->option(OPT_SERIAL_STEP, 0) != 0 ? st : ctx->side;
-        GD_HIP(hipEventRecord(ctx->ev_fork, st));
+    // option serial_step = 1: the side stream's families run on the main
+    // stream before the dense tiles, one after another (each family's time
+    // alone: the C4 slice's MFMA tiles and variant walk otherwise share the
+    // CUs); option dense_first = 1: the dense tiles are issued before the
+    // side stream's launches (which still wait only for the fork)
+    const bool serial = ctx->option(OPT_SERIAL_STEP, 0) != 0;
+    const bool dense_first = side && !serial && ctx->option(OPT_DENSE_FIRST, 0) != 0;
+    if (side) GD_HIP(hipEventRecord(ctx->ev_fork, st));
+    auto launch_side = [&]() {
+        hipStream_t sd = serial ? st : ctx->side;
         GD_HIP(hipStreamWaitEvent(sd, ctx->ev_fork, 0));
         if (s->sparse) rare_done = sparse_matrix(ctx, s, r0, r1, c0, c1, upper, d_I, ldI, sd, p.sparse);
         // beside the sparse kernel the list-major rare kernel goes to the main
@@ -2626,7 +2629,8 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
         if (s->variant) variant_matrix(ctx, s, r0, r1, c0, c1, upper, d_I, ldI, sd);
         GD_HIP(hipGetLastError());
         GD_HIP(hipEventRecord(ctx->ev_join, sd));
-    }
+    };
+    if (side && !dense_first) launch_side();
     if (tW == 0 || (s->sparse && s->sp_fold_dense)) {
         // no dense words, or so few that the sparse flush counts them
     } else {
@@ -2719,6 +2723,7 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
         }
         ft.end();
     }
+    if (dense_first) launch_side();
     if (overlap && s->sparse && !rare_done) launch_rare_pairs(st);
     GD_HIP(hipGetLastError());
     ctx->last.launches = 1;

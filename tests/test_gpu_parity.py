@@ -780,6 +780,8 @@ def test_rare_rows_heavy_rows_exact(ctx, opts, c16):
 
 SPARSE_MODES = {
     "auto": {},
+    # the dense tiles issued before the sparse launch (option dense_first)
+    "dense_first": {"sparse_zmax": 12, "sparse_fold": 0, "dense_first": 1},
     "all_sparse": {"sparse_zmax": 100000}, "mixed": {"sparse_zmax": 12},
     "no_locus": {"locus_order": 0, "sparse_zmax": 40}, "off": {"sparse": 0},
     # chunks flush with atomics (no partials within a zero budget)
@@ -856,7 +858,7 @@ def test_sparse_complement_words_exact(ctx, mode, opts):
     if mode in ("all_sparse", "atomic_flush", "many_chunks", "sun4", "sun3", "sun2_atomic", "mt2", "mt2_sun3",
                 "mt2_sun2_atomic", "dyn_off", "diag11", "rpart12"):
         assert ws > 0 and wd == 0 and ent > 0
-    elif mode in ("mixed", "mixed_slabs", "mixed_slabs_atomic", "mixed_tiles"):
+    elif mode in ("mixed", "mixed_slabs", "mixed_slabs_atomic", "mixed_tiles", "dense_first"):
         assert ws > 0 and wd > 0
     elif mode == "off":
         assert ws == 0 and wd == W
