@@ -2612,10 +2612,13 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     // option serial_step = 1: the side stream's families run on the main
     // stream before the dense tiles, one after another (each family's time
     // alone: the C4 slice's MFMA tiles and variant walk otherwise share the
-    // CUs); option dense_first = 1: the dense tiles are issued before the
-    // side stream's launches (which still wait only for the fork)
+    // CUs); option dense_first: the dense tiles are issued before the side
+    // stream's launches (which still wait only for the fork) — by default
+    // unless the side stream carries the sparse tiles (C3: step 2.51 vs
+    // 2.63 ms, C4 slice 15.8 vs 16.0 ms; C2-realistic's sparse launch first:
+    // 0.321 vs 0.353 ms, profiles/r05/s16/)
     const bool serial = ctx->option(OPT_SERIAL_STEP, 0) != 0;
-    const bool dense_first = side && !serial && ctx->option(OPT_DENSE_FIRST, 0) != 0;
+    const bool dense_first = side && !serial && ctx->option(OPT_DENSE_FIRST, s->sparse ? 0 : 1) != 0;
     if (side) GD_HIP(hipEventRecord(ctx->ev_fork, st));
     auto launch_side = [&]() {
         hipStream_t sd = serial ? st : ctx->side;

@@ -244,7 +244,7 @@ struct Timing {
     X(RARE_C16, "rare_c16")                   /* row-major rare walk: 1 (default) 16-bit LDS counters when every row's rare weight < 2^16, 0 32-bit */ \
     X(VARIANT_C16, "variant_c16")             /* variant walk: 1 (default) 16-bit counters in 32,768-column chunks, 0 32-bit in 16,384 */ \
     X(VARIANT_SPLIT, "variant_split")         /* variant walk: workgroups a row (default: ~8 a CU over the rows) */ \
-    X(DENSE_FIRST, "dense_first")             /* 1: the dense tiles issued before the side stream's launches */ \
+    X(DENSE_FIRST, "dense_first")             /* the dense tiles issued before the side stream's launches (default: without sparse words) */ \
     X(SERIAL_STEP, "serial_step")             /* 1: the side stream's kernel families on the main stream, in turn (timing) */ \
     X(SPLIT_BUILD, "split_build")             /* gathered collection on R ranks: each builds 1/R and all-gathers (default); 0 every rank all; k >= 2 without peers: k shares in turn here */
 
