@@ -243,7 +243,6 @@ struct Timing {
     X(RANGE_SUMMARY, "range_summary")         /* 1: the code-range dictionary whatever the size, 0: never */  \
     X(RARE_C16, "rare_c16")                   /* row-major rare walk: 1 (default) 16-bit LDS counters when every row's rare weight < 2^16, 0 32-bit */ \
     X(VARIANT_C16, "variant_c16")             /* variant walk: 1 (default) 16-bit counters in 32,768-column chunks, 0 32-bit in 16,384 */ \
-    X(VARIANT_PAIR, "variant_pair")           /* variant walk: 1 two entries a wave in flight */ \
     X(VARIANT_SPLIT, "variant_split")         /* variant walk: workgroups a row (default: ~8 a CU over the rows) */ \
     X(DENSE_FIRST, "dense_first")             /* the dense tiles issued before the side stream's launches (default: without sparse words) */ \
     X(SERIAL_STEP, "serial_step")             /* 1: the side stream's kernel families on the main stream, in turn (timing) */ \

@@ -549,56 +549,7 @@ constexpr int VBATCH = 2048;
 // (entry, chunk) visits, fuller 64-member steps); a batch then holds at most
 // 1,023 entries, so a pair's count in it is at most 1,023 x 64 < 2^16 (a
 // set holds one entry per word, and each entry adds at most 64).
-// one entry's walk through its word list inside a column chunk: the next 64
-// members are loaded before this step's are counted (two steps of loads in
-// flight; round 5: the walk waited out one load round trip per 64 members)
-struct VWalk {
-    unsigned long long mi, mj;
-    int64_t y, ye, yy;
-    uint32_t j;
-    bool act;
-};
-__device__ __forceinline__ VWalk vwalk_open(const uint32_t* __restrict__ sent, const unsigned long long* __restrict__ vmask,
-                                            const uint32_t* __restrict__ vset, const uint32_t* __restrict__ vend,
-                                            const uint32_t* ypos, int64_t bb, int t, int lane) {
-    VWalk w;
-    const uint32_t e = sent[bb + t];
-    w.mi = vmask[e];
-    w.ye = vend[e];
-    w.y = ypos[t];
-    w.act = w.y < w.ye;
-    w.yy = w.y + lane;
-    w.j = w.act && w.yy < w.ye ? vset[w.yy] : 0xFFFFFFFFu;
-    w.mj = w.act && w.yy < w.ye ? vmask[w.yy] : 0ull;
-    return w;
-}
 template <bool C16>
-__device__ __forceinline__ void vwalk_step(VWalk& w, const uint32_t* __restrict__ vset,
-                                           const unsigned long long* __restrict__ vmask, int64_t ce, int64_t cb,
-                                           int64_t i, int32_t* cnt) {
-    const bool in = w.yy < w.ye && (int64_t)w.j < ce;
-    const int64_t yn = w.yy + 64;
-    const uint32_t jn = yn < w.ye ? vset[yn] : 0xFFFFFFFFu;
-    const unsigned long long mn = yn < w.ye ? vmask[yn] : 0ull;
-    if (in && (int64_t)w.j != i) {
-        const int v = __popcll(w.mi & w.mj);
-        if (v) {
-            if (C16) atomicAdd(&cnt[(w.j - cb) >> 1], v << (((w.j - cb) & 1) << 4));
-            else atomicAdd(&cnt[w.j - cb], v);
-        }
-    }
-    const unsigned long long m = __ballot(in);
-    w.y += __popcll(m);                                // lists ascend: the in-chunk members come first
-    if (m != ~0ull) {
-        w.act = false;
-        return;
-    }
-    w.yy = yn;
-    w.j = jn;
-    w.mj = mn;
-}
-
-template <bool C16, bool PAIR>
 __global__ __launch_bounds__(1024) void variant_rows_kernel(const int64_t* __restrict__ soff,
                                                            const uint32_t* __restrict__ sent,
                                                            const uint32_t* __restrict__ vset,
@@ -645,21 +596,39 @@ __global__ __launch_bounds__(1024) void variant_rows_kernel(const int64_t* __res
             __syncthreads();                                   // ypos written; previous chunk flushed
             for (int t = threadIdx.x; t < (C16 ? (n + 1) >> 1 : n); t += blockDim.x) cnt[t] = 0;
             __syncthreads();
-            // a wave per entry (PAIR: two entries a wave, stepped in turn, so
-            // two lists' loads are in flight at once)
-            for (int t = wv; t < nb; t += (PAIR ? 2 : 1) * nwv) {
-                VWalk A = vwalk_open(sent, vmask, vset, vend, ypos, bb, t, lane);
-                VWalk B;
-                B.act = false;
-                if (PAIR && t + nwv < nb) B = vwalk_open(sent, vmask, vset, vend, ypos, bb, t + nwv, lane);
-                while (A.act || B.act) {
-                    if (A.act) vwalk_step<C16>(A, vset, vmask, ce, cb, i, cnt);
-                    if (PAIR && B.act) vwalk_step<C16>(B, vset, vmask, ce, cb, i, cnt);
+            for (int t = wv; t < nb; t += nwv) {                 // a wave per entry
+                const uint32_t e = sent[bb + t];
+                const unsigned long long mi = vmask[e];
+                const int64_t ye = vend[e];
+                int64_t y = ypos[t];
+                if (y < ye) {
+                    // the next 64 members are loaded before this step's are
+                    // counted (two steps of loads in flight a wave; round 5:
+                    // the walk waited out one load round trip per 64 members)
+                    int64_t yy = y + lane;
+                    uint32_t j = yy < ye ? vset[yy] : 0xFFFFFFFFu;
+                    unsigned long long mj = yy < ye ? vmask[yy] : 0ull;
+                    for (;;) {
+                        const bool in = yy < ye && (int64_t)j < ce;
+                        const int64_t yn = yy + 64;
+                        const uint32_t jn = yn < ye ? vset[yn] : 0xFFFFFFFFu;
+                        const unsigned long long mn = yn < ye ? vmask[yn] : 0ull;
+                        if (in && (int64_t)j != i) {
+                            const int v = __popcll(mi & mj);
+                            if (v) {
+                                if (C16) atomicAdd(&cnt[(j - cb) >> 1], v << (((j - cb) & 1) << 4));
+                                else atomicAdd(&cnt[j - cb], v);
+                            }
+                        }
+                        const unsigned long long m = __ballot(in);
+                        y += __popcll(m);                      // lists ascend: the in-chunk members come first
+                        if (m != ~0ull) break;
+                        yy = yn;
+                        j = jn;
+                        mj = mn;
+                    }
                 }
-                if (lane == 0) {
-                    ypos[t] = (uint32_t)A.y;
-                    if (PAIR && t + nwv < nb) ypos[t + nwv] = (uint32_t)B.y;
-                }
+                if (lane == 0) ypos[t] = (uint32_t)y;
             }
             __syncthreads();
             for (int t = threadIdx.x; t < n; t += blockDim.x) {
@@ -1217,10 +1186,7 @@ void variant_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1,
     // (a workgroup of 32 KiB that fits beside an MFMA tile workgroup, 512
     // threads and 14,336-column chunks: 12.4 vs 8.6 ms alone, step 20.3 vs
     // 16.0 ms, profiles/r05/s10/ab_c4.txt; dropped)
-    // option variant_pair: two entries a wave in flight
-    const bool c16 = ctx->option(OPT_VARIANT_C16, 1) != 0, pair = ctx->option(OPT_VARIANT_PAIR, 0) != 0;
-    auto* kern = c16 ? (pair ? variant_rows_kernel<true, true> : variant_rows_kernel<true, false>)
-                     : (pair ? variant_rows_kernel<false, true> : variant_rows_kernel<false, false>);
+    auto* kern = ctx->option(OPT_VARIANT_C16, 1) != 0 ? variant_rows_kernel<true> : variant_rows_kernel<false>;
     kern<<<(unsigned)grid, 1024, 0, rs>>>(s->vs_off.as<int64_t>(), s->vs_ent.as<uint32_t>(),
                                           s->vw_set.as<uint32_t>(), s->vw_mask.as<unsigned long long>(),
                                           s->vw_beg.as<uint32_t>(), s->vw_end.as<uint32_t>(), r0, r1, c0,

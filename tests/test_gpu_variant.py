@@ -183,19 +183,17 @@ def test_variant_walk_across_column_chunks(ctx, opts):
     sets.build_bitsets()
     vk, vw, ve, vp = sets.variant_info()
     assert vk > 0 and ve > 0, (vk, vw, ve)
-    for direct, c16, split, pair in ((None, None, None, None), (0, 0, None, 1), (1, None, 1, None), (None, 0, 3, None),
-                                     (None, None, None, 1)):
+    for direct, c16, split in ((None, None, None), (0, 0, None), (1, None, 1), (None, 0, 3)):
         # option variant_c16 (default): 16-bit counters in 32,768-column
-        # chunks (0: 32-bit in 16,384); variant_split: slices a row;
-        # variant_pair: two entries a wave in flight
-        opts(rare_direct=direct, variant_c16=c16, variant_split=split, variant_pair=pair)
+        # chunks (0: 32-bit in 16,384); variant_split: slices a row
+        opts(rare_direct=direct, variant_c16=c16, variant_split=split)
         for (r0, r1, up) in [(0, 24, True), (16370, 16400, True), (500, 520, False), (0, 8, False)]:
             I, D = sets.matrix((r0, r1), (0, n), upper=up, method=gdist.METHOD_BITSET)
             eI, eD = oracle.matrix(off, codes, r0, r1, 0, n, flags=0x100 if up else 0, nthreads=8)
             if up:
                 mask = np.fromfunction(lambda a, b: b > (r0 + a), (r1 - r0, n))
                 I, D, eI, eD = I[mask], D[mask], eI[mask], eD[mask]
-            assert np.array_equal(I, eI), (direct, c16, split, pair, r0, r1, np.flatnonzero(I != eI)[:5])
+            assert np.array_equal(I, eI), (direct, c16, split, r0, r1, np.flatnonzero(I != eI)[:5])
             assert bits_equal(D, eD), (direct, r0, r1)
 
 
