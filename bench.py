@@ -369,8 +369,12 @@ def main():
     # tile launch, the rare-tier kernel, the dense tiles, the sorted join
     fam_ms = {}
     if method in ("bitset", "sorted"):
-        prev = ctx.option("time_kernels")
+        # each family ALONE (option serial_step: the side stream's families
+        # run on the main stream in turn), so that a kernel's roofline is its
+        # own launch time, not its time while sharing the CUs with another
+        prev, prev_serial = ctx.option("time_kernels"), ctx.option("serial_step")
         ctx.set_option("time_kernels", 1)
+        ctx.set_option("serial_step", 1)
         acc = {f: [] for f in ctx.KERNEL_FAMILIES}
         for it in range(max(3, min(args.steps, 20))):
             step()
@@ -379,6 +383,7 @@ def main():
                 if it > 0 and v > 0:                       # the first call builds nothing new, but warms
                     acc[f].append(v)
         ctx.set_option("time_kernels", prev)
+        ctx.set_option("serial_step", prev_serial)
         fam_ms = {f: float(np.mean(v)) for f, v in acc.items() if v}
     sparse_k_ms = fam_ms.get("sparse")
     pairs_all = N * (N - 1) // 2
@@ -519,7 +524,7 @@ def main():
                               "kernel": "bitset_mfma_kernel (dense tier tiles, FP4 MFMA 32x32x64)",
                               "kernel_avg_ms": round(d_ms, 4), "ops_per_pair": 128 * tw,
                               "note": "algorithmic ops = pairs x W words x 64 bit-products x 2 (multiply + add) / "
-                                      "the dense tile launch's own time; peak = the FP4 dense MFMA rate "
+                                      "the dense tile launch's own time (each kernel family timed alone: option serial_step); peak = the FP4 dense MFMA rate "
                                       "(MI355X_MICROARCH.md); the bits are e2m1 0.0 / 1.0 nibbles, sums exact in f32"}
             else:
                 tops = wp * 4 / 1e12
@@ -547,7 +552,7 @@ def main():
                 cands.append((v_ms, {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                      "frac": round(ach / HBM_PEAK_GBS, 4),
                                      "traffic": pmc_traffic("variant_rows_kernel"),
-                                     "kernel": "variant_rows_kernel (variant tier, beside the dense tiles)",
+                                     "kernel": "variant_rows_kernel (variant tier; in the step beside the dense tiles, timed alone)",
                                      "kernel_avg_ms": round(v_ms, 4), "algo_bytes_per_launch": round(v_bytes),
                                      "note": "algorithmic bytes = 12 B per product (the list member's set and mask) "
                                              "+ 20 B per row entry; products = the block's share of the tier's "
@@ -572,7 +577,7 @@ def main():
                 ach = rare_bytes / (r_ms * 1e-3) / 1e9
                 rare_roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(rk.rsplit("_kernel", 1)[0]),
-                             "kernel": f"{rk} (rare tier, beside the dense tiles)", "kernel_avg_ms": round(r_ms, 4),
+                             "kernel": f"{rk} (rare tier; in the step beside the dense tiles, timed alone)", "kernel_avg_ms": round(r_ms, 4),
                              "algo_bytes_per_launch": round(rare_bytes),
                              "member_bytes": mbytes,
                              "note": "algorithmic bytes = 14 B per (set, list) record of the rows + one list member "
