@@ -233,6 +233,8 @@ bool comm_active(const gdist_ctx* ctx) { return has_comm(ctx) && ctx->nranks > 1
 
 void comm_allgather_inplace(gdist_ctx* ctx, void* d_buf, size_t bytes) { allgather_inplace(ctx, d_buf, bytes); }
 
+void comm_allgather(gdist_ctx* ctx, const void* d_send, void* d_recv, size_t bytes) { allgather(ctx, d_send, d_recv, bytes); }
+
 int64_t allgather_concat(gdist_ctx* ctx, DevBuf& buf, int64_t n, size_t es) {
     hipStream_t st = ctx->stream;
     const int R = ctx->nranks, me = ctx->rank;

@@ -245,6 +245,7 @@ struct Timing {
     X(VARIANT_C16, "variant_c16")             /* variant walk: 1 (default) 16-bit counters in 32,768-column chunks, 0 32-bit in 16,384 */ \
     X(VARIANT_SPLIT, "variant_split")         /* variant walk: workgroups a row (default: ~8 a CU over the rows) */ \
     X(DENSE_FIRST, "dense_first")             /* the dense tiles issued before the side stream's launches (default: without sparse words) */ \
+    X(REPS_SPLIT, "reps_split")               /* greedy reps of a gathered collection: 1 (default) columns sharded over the ranks, 0 every rank all */ \
     X(SERIAL_STEP, "serial_step")             /* 1: the side stream's kernel families on the main stream, in turn (timing) */ \
     X(SPLIT_BUILD, "split_build")             /* gathered collection on R ranks: each builds 1/R and all-gathers (default); 0 every rank all; k >= 2 without peers: k shares in turn here */
 
@@ -612,6 +613,7 @@ struct ShareClock {
 // communicator (gdist_api.hip): true with peers (RCCL or the host transport)
 bool comm_active(const gdist_ctx* ctx);
 void comm_allgather_inplace(gdist_ctx* ctx, void* d_buf, size_t bytes);
+void comm_allgather(gdist_ctx* ctx, const void* d_send, void* d_recv, size_t bytes);
 // every rank's n elements of es bytes (buf) concatenated in rank order into
 // buf; returns the total (one all-gather of the counts, one padded in place)
 int64_t allgather_concat(gdist_ctx* ctx, DevBuf& buf, int64_t n, size_t es);

@@ -22,33 +22,34 @@
 namespace gdist {
 namespace {
 
-// cov[k] = 1 if some r < b0 with is_rep[r] has D[k][r] <= t (one wave per row)
+// cov[k] = 1 if some r in [c0, c1) with is_rep[r] has D[k][r - c0] <= t (one wave per row)
 __global__ __launch_bounds__(256) void cover_kernel(const double* __restrict__ D, int64_t ldD, int64_t nrows,
-                                                    int64_t b0, const int32_t* __restrict__ is_rep, double t,
-                                                    int32_t* __restrict__ cov) {
+                                                    int64_t c0, int64_t c1, const int32_t* __restrict__ is_rep,
+                                                    double t, int32_t* __restrict__ cov) {
     const int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (k >= nrows) return;
-    const double* row = D + k * ldD;
+    const double* row = D + k * ldD - c0;
     bool hit = false;
-    for (int64_t r = lane; r < b0 && !hit; r += 64) hit = is_rep[r] && row[r] <= t;
+    for (int64_t r = c0 + lane; r < c1 && !hit; r += 64) hit = is_rep[r] && row[r] <= t;
     const unsigned long long any = __ballot(hit);
     if (lane == 0) cov[k] = any != 0ull;
 }
 
 // closest representative of each row: min (d, rank) over columns with
 // is_rep and d < 1.0; -1 / 1.0 when none (one wave per row)
+// (columns [c0, c1), D's column 0 is c0; best_rk: the winner's tie rank)
 __global__ __launch_bounds__(256) void closest_rep_kernel(const double* __restrict__ D, int64_t ldD, int64_t nrows,
-                                                          int64_t ncols, const int32_t* __restrict__ is_rep,
+                                                          int64_t c0, int64_t c1, const int32_t* __restrict__ is_rep,
                                                           const int64_t* __restrict__ rank, int64_t* __restrict__ best,
-                                                          double* __restrict__ best_d) {
+                                                          double* __restrict__ best_d, int64_t* __restrict__ best_rk) {
     const int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (k >= nrows) return;
-    const double* row = D + k * ldD;
+    const double* row = D + k * ldD - c0;
     double bd = 1.0;
     int64_t br = INT64_MAX, bi = -1;
-    for (int64_t c = lane; c < ncols; c += 64) {
+    for (int64_t c = c0 + lane; c < c1; c += 64) {
         if (!is_rep[c]) continue;
         const double d = row[c];
         const int64_t rk = rank ? rank[c] : c;
@@ -63,23 +64,31 @@ __global__ __launch_bounds__(256) void closest_rep_kernel(const double* __restri
     if (lane == 0) {
         best[k] = bi;
         best_d[k] = bi < 0 ? 1.0 : bd;
+        if (best_rk) best_rk[k] = bi < 0 ? INT64_MAX : br;
     }
 }
 
-// distances of rows [b0, b1) x columns [0, nc) into D (device, ld = ldD)
-void distance_rows(gdist_ctx* ctx, gdist_sets* s, int method, int64_t b0, int64_t b1, int64_t nc, int32_t* dI,
-                   double* dD, int64_t ldD) {
+// distances of rows [b0, b1) x columns [c0, c1) into D (device, ld = ldD)
+void distance_rows(gdist_ctx* ctx, gdist_sets* s, int method, int64_t b0, int64_t b1, int64_t c0, int64_t c1,
+                   int32_t* dI, double* dD, int64_t ldD) {
+    if (c1 <= c0 || b1 <= b0) return;
     if (method == GDIST_METHOD_BITSET) {
-        zero_counts(ctx, b0, b1, 0, nc, false, dI, ldD);
-        bitset_matrix(ctx, s, b0, b1, 0, nc, false, dI, ldD);
+        zero_counts(ctx, b0, b1, c0, c1, false, dI, ldD);
+        bitset_matrix(ctx, s, b0, b1, c0, c1, false, dI, ldD);
     } else {
-        sorted_matrix(ctx, s, b0, b1, 0, nc, false, dI, ldD);
+        sorted_matrix(ctx, s, b0, b1, c0, c1, false, dI, ldD);
     }
-    distance_epilogue(ctx, s, b0, b1, 0, nc, false, 0, dI, ldD, dD, ldD);
+    distance_epilogue(ctx, s, b0, b1, c0, c1, false, 0, dI, ldD, dD, ldD);
 }
 
 }  // namespace
 
+// A gathered collection on R ranks: the columns are sharded.
+// Every rank computes a block's distances to its 1/R of the columns (pass 1:
+// of the earlier sets; pass 2: of all sets); the cover flags (any: OR) and
+// the closest representatives (min (d, tie rank)) of the block's rows are
+// combined through one all-gather per block, so every rank takes the same
+// decisions. The in-block tile (B x B) is computed on every rank.
 void greedy_reps(gdist_ctx* ctx, gdist_sets* s, int method, double t, const int64_t* tie_rank, int32_t* is_rep,
                  int64_t* rep_of, double* rep_dist, int64_t* nreps) {
     hipStream_t st = ctx->stream;
@@ -87,6 +96,8 @@ void greedy_reps(gdist_ctx* ctx, gdist_sets* s, int method, double t, const int6
     std::fill(is_rep, is_rep + n, 0);
     if (nreps) *nreps = 0;
     if (n == 0) return;
+    const bool split = s->replicated && comm_active(ctx) && ctx->option(OPT_REPS_SPLIT, 1) != 0;
+    const int R = split ? ctx->nranks : 1, me = split ? ctx->rank : 0;
     // row block: B x N counts + distances within ~1.5 GiB, a multiple of 128 rows
     int64_t B = std::max<int64_t>(128, std::min<int64_t>(4096, ((int64_t(1) << 27) / n) / 128 * 128));
     B = std::min<int64_t>(B, ceil_div(n, 128) * 128);
@@ -95,23 +106,45 @@ void greedy_reps(gdist_ctx* ctx, gdist_sets* s, int method, double t, const int6
     GD_HIP(hipMemsetAsync(drep.p, 0, n * 4, st));
     std::vector<int32_t> cov(B);
     std::vector<double> tile((size_t)B * B);
+    DevBuf gcov(split ? (size_t)R * B * 4 + 4 : 4, st);
+    std::vector<int32_t> hcov(split ? (size_t)R * B : 1);
     int64_t count = 0;
     for (int64_t b0 = 0; b0 < n; b0 += B) {
         const int64_t b1 = std::min(n, b0 + B), nb = b1 - b0;
-        distance_rows(ctx, s, method, b0, b1, b1, dI.as<int32_t>(), dD.as<double>(), b1);
-        if (b0 > 0) {
-            cover_kernel<<<(unsigned)ceil_div(nb, 4), 256, 0, st>>>(dD.as<double>(), b1, nb, b0, drep.as<int32_t>(), t,
-                                                                    dcov.as<int32_t>());
-            GD_HIP(hipGetLastError());
-            d2h(cov.data(), dcov.p, nb * 4, st);
+        std::fill(cov.begin(), cov.begin() + nb, 0);
+        if (!split) {
+            distance_rows(ctx, s, method, b0, b1, 0, b1, dI.as<int32_t>(), dD.as<double>(), b1);
+            if (b0 > 0) {
+                cover_kernel<<<(unsigned)ceil_div(nb, 4), 256, 0, st>>>(dD.as<double>(), b1, nb, 0, b0,
+                                                                        drep.as<int32_t>(), t, dcov.as<int32_t>());
+                GD_HIP(hipGetLastError());
+                d2h(cov.data(), dcov.p, nb * 4, st);
+            }
+            // the in-block tile D[b0..b1) x [b0..b1)
+            GD_HIP(hipStreamSynchronize(st));
+            GD_HIP(hipMemcpy2DAsync(tile.data(), nb * 8, dD.as<double>() + b0, b1 * 8, nb * 8, nb,
+                                    hipMemcpyDeviceToHost, st));
+            GD_HIP(hipStreamSynchronize(st));
         } else {
-            std::fill(cov.begin(), cov.begin() + nb, 0);
+            distance_rows(ctx, s, method, b0, b1, b0, b1, dI.as<int32_t>(), dD.as<double>(), nb);
+            GD_HIP(hipStreamSynchronize(st));
+            d2h(tile.data(), dD.p, (size_t)nb * nb * 8, st);
+            // this rank's share of the earlier columns, then OR over ranks
+            const int64_t lo = b0 * me / R, hi = b0 * (me + 1) / R;
+            GD_HIP(hipMemsetAsync(dcov.p, 0, B * 4, st));
+            if (hi > lo) {
+                distance_rows(ctx, s, method, b0, b1, lo, hi, dI.as<int32_t>(), dD.as<double>(), hi - lo);
+                cover_kernel<<<(unsigned)ceil_div(nb, 4), 256, 0, st>>>(dD.as<double>(), hi - lo, nb, lo, hi,
+                                                                        drep.as<int32_t>(), t, dcov.as<int32_t>());
+                GD_HIP(hipGetLastError());
+            }
+            if (b0 > 0) {
+                comm_allgather(ctx, dcov.p, gcov.p, (size_t)B * 4);
+                d2h(hcov.data(), gcov.p, (size_t)R * B * 4, st);
+                for (int r = 0; r < R; r++)
+                    for (int64_t k = 0; k < nb; k++) cov[k] |= hcov[(size_t)r * B + k];
+            }
         }
-        // the in-block tile D[b0..b1) x [b0..b1)
-        GD_HIP(hipStreamSynchronize(st));
-        GD_HIP(hipMemcpy2DAsync(tile.data(), nb * 8, dD.as<double>() + b0, b1 * 8, nb * 8, nb, hipMemcpyDeviceToHost,
-                                st));
-        GD_HIP(hipStreamSynchronize(st));
         for (int64_t k = 0; k < nb; k++) {
             bool covered = cov[k] != 0;
             for (int64_t j = 0; j < k && !covered; j++)
@@ -122,22 +155,61 @@ void greedy_reps(gdist_ctx* ctx, gdist_sets* s, int method, double t, const int6
     }
     if (nreps) *nreps = count;
     if (!rep_of && !rep_dist) return;
-    DevBuf drank, dbest(B * 8 + 8, st), dbd(B * 8 + 8, st);
+    DevBuf drank, dbest(B * 8 + 8, st), dbd(B * 8 + 8, st), dbr(B * 8 + 8, st);
     if (tie_rank) {
         drank.alloc(n * 8, st);
         h2d(drank.p, tie_rank, n * 8, st);
     }
-    std::vector<int64_t> hb(B);
+    // pass 2: columns [lo, hi) of this rank (all of them on one rank)
+    const int64_t lo = n * me / R, hi = n * (me + 1) / R;
+    DevBuf pack(split ? (size_t)B * 24 + 8 : 8, st), gpack(split ? (size_t)R * (B * 24 + 8) : 8, st);
+    std::vector<char> hpack(split ? (size_t)R * (B * 24 + 8) : 1);
+    std::vector<int64_t> hb(B), hr(B);
     std::vector<double> hd(B);
     for (int64_t b0 = 0; b0 < n; b0 += B) {
         const int64_t b1 = std::min(n, b0 + B), nb = b1 - b0;
-        distance_rows(ctx, s, method, b0, b1, n, dI.as<int32_t>(), dD.as<double>(), n);
-        closest_rep_kernel<<<(unsigned)ceil_div(nb, 4), 256, 0, st>>>(dD.as<double>(), n, nb, n, drep.as<int32_t>(),
-                                                                       tie_rank ? drank.as<int64_t>() : nullptr,
-                                                                       dbest.as<int64_t>(), dbd.as<double>());
-        GD_HIP(hipGetLastError());
-        d2h(hb.data(), dbest.p, nb * 8, st);
-        d2h(hd.data(), dbd.p, nb * 8, st);
+        if (hi > lo) {
+            distance_rows(ctx, s, method, b0, b1, lo, hi, dI.as<int32_t>(), dD.as<double>(), hi - lo);
+            closest_rep_kernel<<<(unsigned)ceil_div(nb, 4), 256, 0, st>>>(
+                dD.as<double>(), hi - lo, nb, lo, hi, drep.as<int32_t>(), tie_rank ? drank.as<int64_t>() : nullptr,
+                dbest.as<int64_t>(), dbd.as<double>(), dbr.as<int64_t>());
+            GD_HIP(hipGetLastError());
+        } else {
+            std::vector<int64_t> none(nb, -1), inf(nb, INT64_MAX);
+            std::vector<double> one(nb, 1.0);
+            h2d(dbest.p, none.data(), nb * 8, st);
+            h2d(dbd.p, one.data(), nb * 8, st);
+            h2d(dbr.p, inf.data(), nb * 8, st);
+        }
+        if (!split) {
+            d2h(hb.data(), dbest.p, nb * 8, st);
+            d2h(hd.data(), dbd.p, nb * 8, st);
+        } else {
+            // every rank's (index, d, tie rank) of the block's rows; the
+            // least d wins, equal d < 1.0 the lower tie rank (the kernel's rule)
+            const size_t per = (size_t)B * 24 + 8;
+            GD_HIP(hipMemcpyAsync(pack.p, dbest.p, B * 8, hipMemcpyDeviceToDevice, st));
+            GD_HIP(hipMemcpyAsync(static_cast<char*>(pack.p) + B * 8, dbd.p, B * 8, hipMemcpyDeviceToDevice, st));
+            GD_HIP(hipMemcpyAsync(static_cast<char*>(pack.p) + B * 16, dbr.p, B * 8, hipMemcpyDeviceToDevice, st));
+            comm_allgather(ctx, pack.p, gpack.p, per);
+            d2h(hpack.data(), gpack.p, per * R, st);
+            for (int64_t k = 0; k < nb; k++) {
+                int64_t bi = -1, br = INT64_MAX;
+                double bd = 1.0;
+                for (int r = 0; r < R; r++) {
+                    const char* base = hpack.data() + per * r;
+                    int64_t ci, crk;
+                    double cd;
+                    memcpy(&ci, base + k * 8, 8);
+                    memcpy(&cd, base + B * 8 + k * 8, 8);
+                    memcpy(&crk, base + B * 16 + k * 8, 8);
+                    if (ci < 0) continue;
+                    if (cd < bd || (cd == bd && cd < 1.0 && crk < br)) { bd = cd; br = crk; bi = ci; }
+                }
+                hb[k] = bi;
+                hd[k] = bi < 0 ? 1.0 : bd;
+            }
+        }
         GD_HIP(hipStreamSynchronize(st));
         for (int64_t k = 0; k < nb; k++) {
             const int64_t g = b0 + k;

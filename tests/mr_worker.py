@@ -30,12 +30,13 @@ import oracle  # noqa: E402  (test infrastructure: the checker)
 from gdist import shard, synth  # noqa: E402
 
 CASES = {
-    "base": dict(n=301, L=6000, p=0.01, cfg=11, legs=("bitset", "sorted", "sketch")),
+    "base": dict(n=301, L=6000, p=0.01, cfg=11, legs=("bitset", "sorted", "sketch", "reps")),
     "sparse": dict(n=300, L=150_000, p=0.002, cfg=12, legs=("bitset",), sparse=True),
     "c4": dict(n=200, L=100_000, p=0.05, cfg=4,
                legs=("auto", "sorted", "codes_plan", "codes_variant", "codes_two_tier")),
 }
 SKETCH_W = 200
+REPS_T = 0.35
 
 
 def run_case(name, c, ctx, rank, world):
@@ -127,6 +128,16 @@ def run_case(name, c, ctx, rank, world):
             results[leg] = gs.matrix((r0, r1), (0, n), upper=True, method=gdist.METHOD_BITSET)
             for k in ("variant", "rare_t"):
                 ctx.set_option(k, None)
+        elif leg == "reps":
+            # greedy representatives of a gathered collection:
+            # every rank computes each block against its 1/R of the columns,
+            # cover flags and closest representatives combined by all-gathers
+            gs = local.allgather()
+            ctx.set_option("reps_block", 100)                   # four blocks of rows
+            is_rep, rep_of, rep_d = gs.greedy_reps(REPS_T, assign=True, method=gdist.METHOD_BITSET)
+            ctx.set_option("reps_block", None)
+            info["reps"] = (is_rep.tolist(), rep_of.tolist(), rep_d.tolist())
+            continue
         elif leg == "sketch":
             sk = local.sketches(SKETCH_W).allgather()
             assert len(sk) == n
@@ -142,6 +153,21 @@ def run_case(name, c, ctx, rank, world):
     eI, eD = oracle.matrix(off, codes, 0, n, 0, n, flags=0x100, nthreads=8)
     esk = [oracle.sketch(codes[off[i]:off[i + 1]], 21, 0, SKETCH_W) for i in range(n)] \
         if "sketch" in c["legs"] else None
+    if "reps" in c["legs"]:
+        # every rank the same answer, equal to the greedy pass over the oracle's distances
+        first = gathered[0][3]["reps"]
+        assert all(g[3]["reps"] == first for g in gathered), (name, "ranks disagree on the representatives")
+        is_rep, rep_of, rep_d = first
+        reps = []
+        for i in range(n):
+            if not any(eD[i, r] <= REPS_T for r in reps):
+                reps.append(i)
+        assert [i for i in range(n) if is_rep[i]] == reps, (name, "representatives")
+        for i in range(n):
+            if not is_rep[i]:
+                cand = [(eD[i, r], r) for r in reps if eD[i, r] < 1.0]
+                best = min(cand) if cand else (1.0, -1)
+                assert rep_d[i] == best[0] and rep_of[i] == best[1], (name, i, rep_of[i], rep_d[i], best)
     rows = 0
     for (a, b, res, inf) in gathered:
         up = np.fromfunction(lambda x, y: y > (a + x), (b - a, n))
