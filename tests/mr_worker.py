@@ -158,14 +158,15 @@ def run_case(name, c, ctx, rank, world):
         first = gathered[0][3]["reps"]
         assert all(g[3]["reps"] == first for g in gathered), (name, "ranks disagree on the representatives")
         is_rep, rep_of, rep_d = first
+        sD = np.triu(eD, 1) + np.triu(eD, 1).T          # eD holds the upper triangle only
         reps = []
         for i in range(n):
-            if not any(eD[i, r] <= REPS_T for r in reps):
+            if not any(sD[i, r] <= REPS_T for r in reps):
                 reps.append(i)
         assert [i for i in range(n) if is_rep[i]] == reps, (name, "representatives")
         for i in range(n):
             if not is_rep[i]:
-                cand = [(eD[i, r], r) for r in reps if eD[i, r] < 1.0]
+                cand = [(sD[i, r], r) for r in reps if sD[i, r] < 1.0]
                 best = min(cand) if cand else (1.0, -1)
                 assert rep_d[i] == best[0] and rep_of[i] == best[1], (name, i, rep_of[i], rep_d[i], best)
     rows = 0
