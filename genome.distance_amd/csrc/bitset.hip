@@ -2247,6 +2247,29 @@ void build_bitsets(gdist_ctx* ctx, gdist_sets* s, unsigned flags, int64_t rare_t
             build_variant_bitsets(ctx, s, dict, dcnt, U, rare, Ur, mass, T, sp);
             return;
         }
+        // The grouped rare tier (round 5, option rare_group): the kmers of 2 ..
+        // T - 1 sets as variant words of 16 kmers, one substitution a word
+        // (its k windows held by nearly the same sets), walked a thread an
+        // entry from packed (set | mask << 16) lists. C3: 71.9 M posting
+        // records (Σ m(m−1)/2 ≈ 0.5 G increments of 2-byte members, each record
+        // a random line) become 22.7 M entries and 0.28 G products. By default
+        // for 4,096 .. 65,536 sets with locus guides and many rare records; the
+        // dense tier keeps its threshold T (option variant = 0 keeps the two
+        // tiers unless rare_group = 1).
+        const int64_t rg = ctx->option(OPT_RARE_GROUP, -1);
+        const bool group = s->nsets <= 65536 && T > 2 && mass > 0 &&
+                           (rg > 0 || (rg < 0 && ctx->option(OPT_VARIANT, -1) != 0 && s->nsets >= kVariantMinSets &&
+                                       s->n_guide > 0 && locus_order_enabled(ctx) && mass >= 64 * s->nsets));
+        if (group) {
+            const int64_t dmin = T;
+            T = 2;
+            dictionary_from(ctx, {SummaryView{sum.codes.as<uint64_t>(), sum.counts.as<uint32_t>(), sum.n}}, false, T,
+                            s->nsets, dict, U, rare, Ur, mass, &dcnt);
+            sum.codes.release();
+            sum.counts.release();
+            build_variant_bitsets(ctx, s, dict, dcnt, U, rare, Ur, mass, T, sp, dmin, 16);
+            return;
+        }
     }
     const int64_t W = bitset_words(U);
     DevBuf perm;

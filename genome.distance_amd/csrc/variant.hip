@@ -216,8 +216,9 @@ __global__ __launch_bounds__(256) void variant_key_kernel(const uint64_t* __rest
 }
 
 // group heads of the sorted keys (a keyless kmer is a group of its own) ->
-// words of the group: ceil(len / 64), each group starting a new word
-__global__ void group_words_kernel(const uint64_t* __restrict__ k, int64_t n, int32_t* __restrict__ head,
+// words of the group: ceil(len / wb), each group starting a new word (wb:
+// kmers a word, 64, or 16 for the short-list walk's packed entries)
+__global__ void group_words_kernel(const uint64_t* __restrict__ k, int64_t n, int wb, int32_t* __restrict__ head,
                                    int64_t* __restrict__ words) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -228,7 +229,7 @@ __global__ void group_words_kernel(const uint64_t* __restrict__ k, int64_t n, in
             int64_t e = i + 1;
             if (k[i] == ~0ull) e = n;                        // the keyless kmers: one group, packed
             else while (e < n && k[e] == k[i]) e++;
-            wn = ceil_div(e - i, 64);
+            wn = ceil_div(e - i, wb);
             if (k[i] == ~0ull && i > 0 && k[i - 1] == ~0ull) wn = 0;
         }
         words[i] = wn;
@@ -238,7 +239,7 @@ __global__ void group_words_kernel(const uint64_t* __restrict__ k, int64_t n, in
 // the variant position of every variant kmer (sorted index q -> word of its
 // group + offset): perm over the combined dictionary's variant ranks
 __global__ void group_pos_kernel(const uint64_t* __restrict__ k, const int32_t* __restrict__ order, int64_t n,
-                                 const int64_t* __restrict__ wstart, uint32_t base, uint32_t* __restrict__ mpos) {
+                                 const int64_t* __restrict__ wstart, int wb, uint32_t base, uint32_t* __restrict__ mpos) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         // the group's head: the first index with the same key (keyless: the first keyless)
@@ -248,7 +249,7 @@ __global__ void group_pos_kernel(const uint64_t* __restrict__ k, const int32_t* 
             const int64_t mid = (lo + hi) >> 1;
             if (k[mid] < key) lo = mid + 1; else hi = mid;
         }
-        mpos[order[i]] = base + (uint32_t)(wstart[lo] * 64 + (i - lo));
+        mpos[order[i]] = base + (uint32_t)(wstart[lo] * wb + (i - lo));
     }
 }
 
@@ -383,7 +384,8 @@ __global__ __launch_bounds__(256) void hash_probe_kernel(const uint64_t* __restr
 
 // ---- variant records of one fill chunk -----------------------------------
 // per set of the chunk: its variant positions (>= vbase) counted, then
-// written as keys (word << (sbits + 6) | set << 6 | bit)
+// written as keys (word << (sbits + 6) | set << 6 | bit), word = q >> lg and
+// bit = q & (2^lg - 1) for words of 2^lg kmers
 __global__ __launch_bounds__(256) void vrec_count_kernel(const uint32_t* __restrict__ pos,
                                                          const int64_t* __restrict__ off, int64_t s0, int64_t base,
                                                          uint32_t vbase, int64_t* __restrict__ cnt) {
@@ -405,8 +407,8 @@ __global__ __launch_bounds__(256) void vrec_count_kernel(const uint32_t* __restr
 
 __global__ __launch_bounds__(256) void vrec_write_kernel(const uint32_t* __restrict__ pos,
                                                          const int64_t* __restrict__ off, int64_t s0, int64_t base,
-                                                         uint32_t vbase, int sbits, const int64_t* __restrict__ at,
-                                                         uint64_t* __restrict__ out) {
+                                                         uint32_t vbase, int sbits, int lg,
+                                                         const int64_t* __restrict__ at, uint64_t* __restrict__ out) {
     __shared__ int64_t wbase;
     const int64_t i = s0 + blockIdx.x;
     const int lane = threadIdx.x & 63;
@@ -427,7 +429,7 @@ __global__ __launch_bounds__(256) void vrec_write_kernel(const uint32_t* __restr
         if (hit) {
             const uint64_t q = p - vbase;
             out[slot + __popcll(m & ((1ull << lane) - 1))] =
-                ((q >> 6) << (sbits + 6)) | ((uint64_t)i << 6) | (q & 63);
+                ((q >> lg) << (sbits + 6)) | ((uint64_t)i << 6) | (q & ((1u << lg) - 1));
         }
         __syncthreads();
     }
@@ -531,6 +533,45 @@ __global__ void word_products_kernel(const int64_t* __restrict__ woff, int64_t n
         atomicAdd(out, acc);
         atomicMax(out + 1, mx);
     }
+}
+
+// (set | mask << 16) of every entry of a 16-kmer-word tier of <= 65,536 sets
+__global__ void pack_entries_kernel(const uint32_t* __restrict__ vset, const unsigned long long* __restrict__ vmask,
+                                    int64_t E, uint32_t* __restrict__ pack) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += stride)
+        pack[e] = (vset[e] & 0xFFFFu) | ((uint32_t)(vmask[e] & 0xFFFFull) << 16);
+}
+
+// the short walk's set-side records, coalesced by the set's position: entry
+// e (31 bits) | the members after it, end - e (17 bits) | its position in its
+// list, e - beg (16 bits): a row reads no random bounds (lists of <= 65,536
+// sets)
+__global__ void pack_set_side_kernel(const uint32_t* __restrict__ sent, const uint32_t* __restrict__ beg,
+                                     const uint32_t* __restrict__ end, int64_t E, uint64_t* __restrict__ out) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < E; x += stride) {
+        const uint64_t e = sent[x];
+        out[x] = e | ((uint64_t)(end[e] - e) << 31) | ((uint64_t)(e - beg[e]) << 48);
+    }
+}
+
+// max over sets of the popcounts of their entries' masks
+__global__ void row_vweight_kernel(const int64_t* __restrict__ soff, const uint32_t* __restrict__ sent,
+                                   const unsigned long long* __restrict__ vmask, int64_t nsets,
+                                   unsigned long long* __restrict__ out) {
+    unsigned long long mx = 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nsets; i += stride) {
+        unsigned long long w = 0;
+        for (int64_t x = soff[i]; x < soff[i + 1]; x++) w += (unsigned long long)__popcll(vmask[sent[x]]);
+        mx = w > mx ? w : mx;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long v = __shfl_xor(mx, o, 64);
+        mx = v > mx ? v : mx;
+    }
+    if ((threadIdx.x & 63) == 0) atomicMax(out, mx);
 }
 
 }  // namespace
@@ -660,6 +701,92 @@ __global__ __launch_bounds__(256) void variant_query_kernel(const int64_t* __res
         }
     }
 }
+// Short-list walk of a grouped rare tier (round 5; C3: 22.7 M entries whose
+// word lists hold ~20 sets). The wave-per-entry walk above leaves most of a
+// wave's 64 lanes idle on such lists; here, as in the rare tier's row walk
+// (bitset.hip rare_rows_kernel), a thread takes one entry of the row and
+// walks its list from the row's own position (upper triangle) four packed
+// members (set | mask << 16) a 16-byte load, adding popc(mask_i & mask_j)
+// into LDS counters of one column chunk; lists of kLongList+ entries are
+// walked by the whole wave. Grid: rows x column chunks x nsplit slices of the
+// row's entries; the chunk's counters are added to I's row once (atomics:
+// the other families add beside it). C16: two 16-bit counters a dword
+// (vw_row_wmax < 2^16 bounds every pair's count).
+constexpr int VSCH = 16384;   // columns per LDS chunk
+template <int NT, bool C16>
+__global__ __launch_bounds__(NT) void variant_short_kernel(const int64_t* __restrict__ soff,
+                                                           const uint64_t* __restrict__ spent,
+                                                           const uint32_t* __restrict__ vpack, int64_t r0, int64_t r1,
+                                                           int64_t c0, int64_t c1, int nch, int nsplit, int upper,
+                                                           int32_t* __restrict__ I, int64_t ldI) {
+    extern __shared__ int32_t vcnt[];
+    const int64_t unit = blockIdx.x / nsplit;
+    const int split = blockIdx.x % nsplit;
+    const int64_t i = r0 + unit / nch;
+    const int ch = (int)(unit % nch);
+    const int64_t cb = c0 + (int64_t)ch * VSCH;
+    const int64_t ce = cb + VSCH < c1 ? cb + VSCH : c1;
+    if (i >= r1 || cb >= ce || (upper && ce - 1 <= i)) return;
+    const int n = (int)(ce - cb);
+    const int nw = C16 ? (n + 1) >> 1 : n;
+    for (int t = threadIdx.x; t < nw; t += NT) vcnt[t] = 0;
+    __syncthreads();
+    auto add = [&](int64_t t, int32_t v) {
+        if (C16) atomicAdd(&vcnt[(t - cb) >> 1], v << (((t - cb) & 1) << 4));
+        else atomicAdd(&vcnt[t - cb], v);
+    };
+    const int64_t lo = upper && i + 1 > cb ? i + 1 : cb;
+    const int64_t rb = soff[i], re = soff[i + 1];
+    const int64_t per = (re - rb + nsplit - 1) / nsplit;
+    const int64_t xb = rb + per * split;
+    const int64_t xe = xb + per < re ? xb + per : re;
+    const int lane = threadIdx.x & 63;
+    for (int64_t xbase = xb; xbase < xe; xbase += NT) {          // wave-uniform trip count
+        const int64_t x = xbase + threadIdx.x;
+        int64_t b = 0, ee = 0;
+        uint32_t mi = 0;
+        if (x < xe) {
+            // (entry, members after it, position in its list): coalesced; the
+            // entry's own mask shares a line with its list's next members
+            const uint64_t r = spent[x];
+            const int64_t e = (int64_t)(r & 0x7FFFFFFFull);
+            mi = vpack[e] >> 16;
+            b = upper ? e + 1 : e - (int64_t)(r >> 48);
+            ee = e + (int64_t)((r >> 31) & 0x1FFFFull);
+        }
+        const bool lng = ee - b >= kLongList;
+        for (unsigned long long m = __ballot(lng); m; m &= m - 1) {  // long lists: the wave walks them
+            const int l = __ffsll((long long)m) - 1;
+            const int64_t lb = __shfl((long long)b, l, 64), le = __shfl((long long)ee, l, 64);
+            const uint32_t lm = (uint32_t)__shfl((int)mi, l, 64);
+            for (int64_t y = lb + lane; y < le; y += 64) {
+                const uint32_t p = vpack[y];
+                const int64_t t = p & 0xFFFFu;
+                const int v = __popc(lm & (p >> 16));
+                if (v && t >= lo && t < ce && t != i) add(t, v);
+            }
+        }
+        if (lng) continue;
+#pragma unroll 2
+        for (int64_t y = b; y < ee; y += 4) {
+            uint32_t mem[4];
+            __builtin_memcpy(mem, vpack + y, 16);                 // the array is padded past its end
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int64_t t = mem[u] & 0xFFFFu;
+                const int v = __popc(mi & (mem[u] >> 16));
+                if (y + u < ee && v && t >= lo && t < ce && t != i) add(t, v);
+            }
+        }
+    }
+    __syncthreads();
+    int32_t* row = I + (i - r0) * ldI + (cb - c0);
+    for (int t = threadIdx.x; t < n; t += NT) {
+        const int v = C16 ? (int)(((uint32_t)vcnt[t >> 1] >> ((t & 1) << 4)) & 0xFFFFu) : vcnt[t];
+        if (v && cb + t >= lo) atomicAdd(row + t, v);
+    }
+}
+
 __global__ void viota_kernel(int32_t* __restrict__ p, int64_t n) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = (int32_t)i;
@@ -874,6 +1001,10 @@ int64_t variant_dmin(const gdist_ctx* ctx, int64_t nsets) {
 
 void free_variant(gdist_sets* s) {
     s->variant = false;
+    s->vw_pack.release();
+    s->vs_pent.release();
+    s->vw_row_wmax = 0;
+    s->vw_bits = 64;
     s->vw_words = s->vw_entries = s->vw_kmers = s->vw_dmin = 0;
     s->vw_products = 0.0;
     s->vw_max_list = 0;
@@ -886,13 +1017,15 @@ void free_variant(gdist_sets* s) {
 }
 
 void build_variant_bitsets(gdist_ctx* ctx, gdist_sets* s, DevBuf& dict, DevBuf& dcnt, int64_t U, DevBuf& rare,
-                           int64_t Ur, int64_t mass, int64_t T, BuildSplit& sp) {
+                           int64_t Ur, int64_t mass, int64_t T, BuildSplit& sp, int64_t dmin_in, int wb) {
     hipStream_t st = ctx->stream;
     Trace tr(st, ctx->trace());
     const int64_t N = s->nsets;
     GD_REQUIRE(N < (int64_t(1) << 31), "too many sets for the variant tier");
+    GD_REQUIRE(wb == 16 || wb == 64, "variant words hold 16 or 64 kmers");
+    const int lg = wb == 16 ? 4 : 6;
     // 2. tiers: dense (>= Dmin) and variant (T .. Dmin - 1), in code order within the dictionary
-    const int64_t dmin = variant_dmin(ctx, N);
+    const int64_t dmin = dmin_in > 0 ? dmin_in : variant_dmin(ctx, N);
     DevBuf fd(U * 4 + 4, st), fm(U * 4 + 4, st), pd(U * 8 + 8, st), pm(U * 8 + 8, st);
     int64_t Ud = 0, Um = 0;
     if (U) {
@@ -951,15 +1084,15 @@ void build_variant_bitsets(gdist_ctx* ctx, gdist_sets* s, DevBuf& dict, DevBuf& 
         int32_t* v = ord.as<int32_t>(); int32_t* va = oalt.as<int32_t>();
         sort_pairs_u64_i32(ctx, k, ka, v, va, (size_t)Um, 0, 64);
         DevBuf head(Um * 4 + 4, st), wn(Um * 8 + 8, st), wst(Um * 8 + 8, st);
-        group_words_kernel<<<grid_for(Um), 256, 0, st>>>(k, Um, head.as<int32_t>(), wn.as<int64_t>());
+        group_words_kernel<<<grid_for(Um), 256, 0, st>>>(k, Um, wb, head.as<int32_t>(), wn.as<int64_t>());
         GD_HIP(hipGetLastError());
         exclusive_scan_i64(ctx, wn.as<int64_t>(), wst.as<int64_t>(), (size_t)Um);
         int64_t h[2];
         d2h(&h[0], wst.as<int64_t>() + Um - 1, 8, st);
         d2h(&h[1], wn.as<int64_t>() + Um - 1, 8, st);
         vwords = h[0] + h[1];
-        GD_REQUIRE((double)vbase + (double)vwords * 64.0 < 4294967295.0, "variant tier too large for u32 positions");
-        group_pos_kernel<<<grid_for(Um), 256, 0, st>>>(k, v, Um, wst.as<int64_t>(), vbase, mperm.as<uint32_t>());
+        GD_REQUIRE((double)vbase + (double)vwords * wb < 4294967295.0, "variant tier too large for u32 positions");
+        group_pos_kernel<<<grid_for(Um), 256, 0, st>>>(k, v, Um, wst.as<int64_t>(), wb, vbase, mperm.as<uint32_t>());
         GD_HIP(hipGetLastError());
     }
     DevBuf perm(U * 4 + 4, st);
@@ -990,7 +1123,7 @@ void build_variant_bitsets(gdist_ctx* ctx, gdist_sets* s, DevBuf& dict, DevBuf& 
         d2h(&n, a.as<int64_t>() + ns, 8, st);
         if (n == 0) return;
         DevBuf rA(n * 8 + 8, st), rB(n * 8 + 8, st);
-        vrec_write_kernel<<<(unsigned)ns, 256, 0, st>>>(pos, s->off.as<int64_t>(), s0, base, vbase, sbits,
+        vrec_write_kernel<<<(unsigned)ns, 256, 0, st>>>(pos, s->off.as<int64_t>(), s0, base, vbase, sbits, lg,
                                                         a.as<int64_t>(), rA.as<uint64_t>());
         GD_HIP(hipGetLastError());
         uint64_t* rk = rA.as<uint64_t>(); uint64_t* ra = rB.as<uint64_t>();
@@ -1111,12 +1244,38 @@ void build_variant_bitsets(gdist_ctx* ctx, gdist_sets* s, DevBuf& dict, DevBuf& 
         s->vw_products = (double)hp[0];
         s->vw_max_list = (int64_t)hp[1];
         s->variant = true;
+        // 16-kmer words of at most 65,536 sets: every entry packed in one
+        // dword (set | mask << 16) for the short-list walk, and the largest
+        // row weight (sum of its entries' popcounts: a bound on any pair's
+        // count, so 16-bit LDS counters hold it when below 2^16)
+        if (wb == 16 && N <= 65536) {
+            s->vw_pack.alloc(E * 4 + 64, st);
+            GD_HIP(hipMemsetAsync(s->vw_pack.p, 0, E * 4 + 64, st));   // padded: 16-byte loads past a list's end
+            pack_entries_kernel<<<grid_for(E), 256, 0, st>>>(s->vw_set.as<uint32_t>(),
+                                                             s->vw_mask.as<unsigned long long>(), E,
+                                                             s->vw_pack.as<uint32_t>());
+            GD_HIP(hipGetLastError());
+            s->vs_pent.alloc(E * 8 + 8, st);
+            pack_set_side_kernel<<<grid_for(E), 256, 0, st>>>(s->vs_ent.as<uint32_t>(), s->vw_beg.as<uint32_t>(),
+                                                              s->vw_end.as<uint32_t>(), E, s->vs_pent.as<uint64_t>());
+            GD_HIP(hipGetLastError());
+            DevBuf wmax(8, st);
+            GD_HIP(hipMemsetAsync(wmax.p, 0, 8, st));
+            row_vweight_kernel<<<grid_for(N), 256, 0, st>>>(s->vs_off.as<int64_t>(), s->vs_ent.as<uint32_t>(),
+                                                            s->vw_mask.as<unsigned long long>(), N,
+                                                            wmax.as<unsigned long long>());
+            GD_HIP(hipGetLastError());
+            unsigned long long hw = 0;
+            d2h(&hw, wmax.p, 8, st);
+            s->vw_row_wmax = (int64_t)hw;
+        }
     }
     GD_HIP(hipStreamSynchronize(st));
     s->vw_words = vwords;
     s->vw_entries = E;
     s->vw_kmers = Um;
     s->vw_dmin = dmin;
+    s->vw_bits = wb;
     s->W = Wd;
     s->dict_size = Ud;
     s->rare_T = T;
@@ -1124,9 +1283,10 @@ void build_variant_bitsets(gdist_ctx* ctx, gdist_sets* s, DevBuf& dict, DevBuf& 
     tr.mark("variant: word lists + set side");
     if (ctx->trace())
         fprintf(stderr, "gdist: variant tier: T %lld, Dmin %lld: dense %lld kmers (%lld words), variant %lld kmers in "
-                        "%lld words, %lld entries, %.3g products, longest list %lld; rare %lld kmers\n",
-                (long long)T, (long long)dmin, (long long)Ud, (long long)Wd, (long long)Um, (long long)vwords,
-                (long long)E, s->vw_products, (long long)s->vw_max_list, (long long)Ur);
+                        "%lld words of %d, %lld entries, %.3g products, longest list %lld%s; rare %lld kmers\n",
+                (long long)T, (long long)dmin, (long long)Ud, (long long)Wd, (long long)Um, (long long)vwords, wb,
+                (long long)E, s->vw_products, (long long)s->vw_max_list, s->vw_pack.p ? " (packed)" : "",
+                (long long)Ur);
     build_sparse_words(ctx, s);
 }
 
@@ -1172,6 +1332,36 @@ void variant_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1,
                     int32_t* d_I, int64_t ldI, hipStream_t rs) {
     if (!s->variant || r1 <= r0 || c1 <= c0) return;
     const int64_t units = r1 - r0;
+    if (s->vw_pack.p && ctx->option(OPT_VARIANT_SHORT, 1) != 0) {
+        // packed 16-kmer words: a thread an entry (the short-list walk)
+        const int64_t nc = c1 - c0;
+        const int nch = (int)ceil_div(nc, VSCH);
+        const int64_t su = units * nch;
+        // slices a row: ~8 workgroups a CU over few rows, else ~1,536 of a
+        // row's entries a slice (C3: 2,266 a row; walk alone 0.81 ms with 2
+        // slices, 0.85 with 3, 0.88 with 1: profiles/r05/s21)
+        const int64_t per_row = ceil_div(s->vw_entries, std::max<int64_t>(1, s->nsets));
+        const int nsplit = ctx->has_option(OPT_VARIANT_SPLIT)
+                               ? (int)std::max<int64_t>(1, std::min<int64_t>(64, ctx->option(OPT_VARIANT_SPLIT, 1)))
+                               : (int)std::max<int64_t>(1, std::min<int64_t>(16, std::max(ceil_div((int64_t)ctx->cus * 8, su),
+                                                                                         ceil_div(per_row, 1536))));
+        const int64_t grid = su * nsplit;
+        GD_REQUIRE(grid < (int64_t(1) << 31), "variant-tier grid too large");
+        const bool c16 = s->vw_row_wmax < 65536 && ctx->option(OPT_VARIANT_C16, 1) != 0;
+        const int64_t cols = std::min<int64_t>(nc, VSCH);
+        const size_t lds = c16 ? (size_t)((cols + 1) / 2) * 4 : (size_t)cols * 4;
+        FamilyTimer ft(ctx, GDIST_KERNEL_VARIANT, rs);
+        auto go = [&](auto kern, int nt) {
+            kern<<<(unsigned)grid, nt, lds, rs>>>(s->vs_off.as<int64_t>(), s->vs_pent.as<uint64_t>(),
+                                                  s->vw_pack.as<uint32_t>(), r0, r1, c0, c1, nch, nsplit,
+                                                  upper ? 1 : 0, d_I, ldI);
+        };
+        if (c16) go(variant_short_kernel<512, true>, 512);
+        else go(variant_short_kernel<512, false>, 512);
+        GD_HIP(hipGetLastError());
+        ft.end();
+        return;
+    }
     // few rows: slice each row's entries over several workgroups
     // (option variant_split: a given number of slices a row)
     const int nsplit = ctx->has_option(OPT_VARIANT_SPLIT)

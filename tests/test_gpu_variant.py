@@ -197,6 +197,79 @@ def test_variant_walk_across_column_chunks(ctx, opts):
             assert bits_equal(D, eD), (direct, r0, r1)
 
 
+@pytest.fixture(scope="module")
+def c3_like():
+    """C3's structure (one ancestral proteome, independent substitutions, a
+    few sets a substitution) at 1,500 x 3,000 aa."""
+    from gdist import synth
+    n = 1500
+    seqs = [bytes(r) for r in synth.genomes(n, 3000, 0.10, 45, protein=True)]
+    off, codes = oracle.pack(seqs, 8, 1, 0)
+    return seqs, off, codes
+
+
+@pytest.mark.parametrize("data,walk", [("protein", "short"), ("protein", "short_c32"), ("protein", "short_split"),
+                                       ("protein", "wave"), ("dna", "short"), ("dna", "wave")])
+def test_grouped_rare_tier_exact(ctx, opts, c3_like, c4_like, data, walk):
+    """Round 5, option rare_group: the kmers of 2 .. T - 1 sets as 16-kmer
+    variant words (one substitution a word; DNA's 42 kmers of a substitution
+    in three) walked a thread an entry over packed (set | mask << 16) lists,
+    16-bit (default) or 32-bit LDS counters, several slices a row, or by the
+    wave-per-entry walk; counts and distances equal the oracle's over upper
+    triangles, rectangles, unaligned row blocks and row queries, and the rare
+    posting tier is empty."""
+    import gdist
+    seqs, off, codes = c3_like if data == "protein" else c4_like
+    n = len(seqs)
+    opts(variant=0, rare_group=1, variant_short=0 if walk == "wave" else None,
+         variant_c16=0 if walk == "short_c32" else None, variant_split=3 if walk == "short_split" else None)
+    kind, k = (gdist.KmerType.PROT, 8) if data == "protein" else (gdist.KmerType.DNA, 21)
+    sets = gdist.KmerSets.from_sequences(seqs, k, kind, 0, ctx)
+    sets.build_bitsets()
+    vk, vw, ve, vp = sets.variant_info()
+    thr, lists, recs = sets.rare_info()
+    assert vk > 1000 and ve > 0 and lists == 0 and thr == 2, (vk, vw, ve, thr, lists)
+    assert vw * 3 < vk, ("substitution grouping", vk, vw)
+    for (r0, r1, c0, c1, up) in [(0, n, 0, n, True), (37, 211, 5, n - 10, False), (n // 2, n, 0, n, True),
+                                 (n - 1, n, 0, n, False)]:
+        I, D = sets.matrix((r0, r1), (c0, c1), upper=up, method=gdist.METHOD_BITSET)
+        eI, eD = oracle.matrix(off, codes, r0, r1, c0, c1, flags=0x100 if up else 0, nthreads=8)
+        if up:
+            mask = np.fromfunction(lambda a, b: (c0 + b) > (r0 + a), (r1 - r0, c1 - c0))
+            I, D, eI, eD = I[mask], D[mask], eI[mask], eD[mask]
+        assert np.array_equal(I, eI), (data, walk, r0, r1, c0, c1, up, np.flatnonzero(I != eI)[:5])
+        assert bits_equal(D, eD)
+    cols = [4, n - 1, 0, 600, 600, 17]
+    d = sets.row_query(600, cols)
+    _, eD = oracle.matrix(off, codes, 600, 601, 0, n)
+    assert bits_equal(d, eD[0, cols])
+
+
+def test_grouped_rare_walk_across_column_chunks(ctx, opts):
+    """The short-list walk over 17,000 columns: two 16,384-column LDS chunks,
+    rows whose lists cross the boundary, equal the oracle."""
+    import gdist
+    from gdist import synth
+    n = 17000
+    seqs = [bytes(r) for r in synth.genomes(n, 600, 0.03, 43)]
+    off, codes = oracle.pack(seqs, 21, 0, 0)
+    opts(variant=0, rare_group=1)
+    sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
+    sets.build_bitsets()
+    vk, vw, ve, vp = sets.variant_info()
+    assert vk > 0 and ve > 0 and sets.rare_info()[1] == 0, (vk, vw, ve)
+    for c16 in (None, 0):
+        opts(variant_c16=c16)
+        for (r0, r1, up) in [(0, 24, True), (16370, 16400, True), (500, 520, False)]:
+            I, D = sets.matrix((r0, r1), (0, n), upper=up, method=gdist.METHOD_BITSET)
+            eI, eD = oracle.matrix(off, codes, r0, r1, 0, n, flags=0x100 if up else 0, nthreads=8)
+            if up:
+                mask = np.fromfunction(lambda a, b: b > (r0 + a), (r1 - r0, n))
+                I, D, eI, eD = I[mask], D[mask], eI[mask], eD[mask]
+            assert np.array_equal(I, eI), (c16, r0, r1, np.flatnonzero(I != eI)[:5])
+            assert bits_equal(D, eD), (c16, r0, r1)
+
+
 @pytest.mark.parametrize("mode", ["variant", "variant_windowed_fill", "two_tier", "two_tier_sort_fill"])
 def test_split_build_equals_whole_build(ctx, opts, c4_like, mode):
     """the build of a gathered collection split by rank.
