@@ -290,6 +290,8 @@ def main():
             sparse_words["products"] = sets.sparse_pairs()
         vinfo = sets.variant_info()
         variant = dict(zip(("kmers", "words", "entries", "products"), vinfo)) if vinfo[0] else None
+        if variant:
+            variant["word_kmers"], variant["packed"], variant["row_weight_max"] = sets.variant_layout()
         mflag = gdist.METHOD_BITSET
     elif method == "sorted":
         # the code all-gather consumes the local shard: peak (ranks + 1) x shard
@@ -542,21 +544,33 @@ def main():
             v_ms = fam_ms.get("variant", 0.0)
             cands = [(d_ms, dense_roof)]
             if v_ms > 0 and variant:
-                # variant tier (C4): each product reads one list member (4 B set +
-                # 8 B mask, coalesced along the word's list) for a row entry (its
-                # record: 4 B entry + 8 B mask + 8 B list bounds)
                 f_pairs = pairs_rank / max(1, N * (N - 1) // 2)
                 f_rows = (r1 - r0) / N
-                v_bytes = 12.0 * variant["products"] * f_pairs + 20.0 * variant["entries"] * f_rows
+                if variant.get("packed") and ctx.option("variant_short") != 0:
+                    # grouped rare tier (C3): the short-list walk reads one packed
+                    # member (4 B: set | mask << 16) per product and per row entry
+                    # its set-side record (8 B) and its own packed mask (4 B)
+                    v_bytes = 4.0 * variant["products"] * f_pairs + 12.0 * variant["entries"] * f_rows
+                    vk = "variant_short_kernel"
+                    vnote = ("algorithmic bytes = 4 B per product (the packed list member) + 12 B per row entry "
+                             "(set-side record + its own mask); products = the block's share of the tier's sum "
+                             "over words of z(z-1)/2")
+                else:
+                    # variant tier (C4): each product reads one list member (4 B set +
+                    # 8 B mask, coalesced along the word's list) for a row entry (its
+                    # record: 4 B entry + 8 B mask + 8 B list bounds)
+                    v_bytes = 12.0 * variant["products"] * f_pairs + 20.0 * variant["entries"] * f_rows
+                    vk = "variant_rows_kernel"
+                    vnote = ("algorithmic bytes = 12 B per product (the list member's set and mask) "
+                             "+ 20 B per row entry; products = the block's share of the tier's "
+                             "sum over words of z(z-1)/2")
                 ach = v_bytes / (v_ms * 1e-3) / 1e9
                 cands.append((v_ms, {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                      "frac": round(ach / HBM_PEAK_GBS, 4),
-                                     "traffic": pmc_traffic("variant_rows_kernel"),
-                                     "kernel": "variant_rows_kernel (variant tier; in the step beside the dense tiles, timed alone)",
+                                     "traffic": pmc_traffic(vk),
+                                     "kernel": f"{vk} (variant tier; in the step beside the dense tiles, timed alone)",
                                      "kernel_avg_ms": round(v_ms, 4), "algo_bytes_per_launch": round(v_bytes),
-                                     "note": "algorithmic bytes = 12 B per product (the list member's set and mask) "
-                                             "+ 20 B per row entry; products = the block's share of the tier's "
-                                             "sum over words of z(z-1)/2"}))
+                                     "note": vnote}))
             if r_ms > 0 and rare:
                 # rare tier, row-major walk (rare_rows_kernel) or list-major
                 # (rare_pairs_kernel): its useful bytes = the rows' (set, list)

@@ -803,6 +803,15 @@ int gdist_sets_variant_info(const gdist_sets* s, int64_t* kmers, int64_t* words,
     });
 }
 
+int gdist_sets_variant_layout(const gdist_sets* s, int* word_kmers, int* packed, int64_t* row_weight_max) {
+    return guard([&] {
+        check_sets(s);
+        if (word_kmers) *word_kmers = s->variant ? s->vw_bits : 0;
+        if (packed) *packed = s->variant && s->vw_pack.p ? 1 : 0;
+        if (row_weight_max) *row_weight_max = s->variant ? s->vw_row_wmax : 0;
+    });
+}
+
 int gdist_sets_sparse_pairs(const gdist_sets* s, double* pairs) {
     return guard([&] {
         check_sets(s);

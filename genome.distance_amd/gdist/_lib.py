@@ -115,6 +115,7 @@ _SIGS = {
     "gdist_sets_rare_kmers": (C.c_int, [_setp, _i64p]),
     "gdist_sets_sparse_info": (C.c_int, [_setp, _i64p, _i64p, _i64p]),
     "gdist_sets_variant_info": (C.c_int, [_setp, _i64p, _i64p, _i64p, _dblp]),
+    "gdist_sets_variant_layout": (C.c_int, [_setp, C.POINTER(C.c_int), C.POINTER(C.c_int), _i64p]),
     "gdist_sets_group_info": (C.c_int, [_setp, _i64p, _i64p]),
     "gdist_sets_sparse_sides": (C.c_int, [_setp, _i64p, _i64p]),
     "gdist_sets_sparse_pairs": (C.c_int, [_setp, C.POINTER(C.c_double)]),

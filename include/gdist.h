@@ -259,6 +259,12 @@ int  gdist_sets_sparse_info(const gdist_sets* sets, int64_t* sparse_words, int64
  * products (sum over words of z(z-1)/2); zeros without the tier. */
 int  gdist_sets_variant_info(const gdist_sets* sets, int64_t* kmers, int64_t* words, int64_t* entries,
                              double* products);
+/* The variant tier's layout: kmers a word (64; 16 for the grouped rare tier,
+ * option rare_group), whether its entries are packed (set | mask << 16) for
+ * the short-list walk (16-kmer words of <= 65,536 sets), and the largest
+ * sum of a set's entry popcounts (the bound that allows 16-bit counters).
+ * Zeros without a variant tier. Diagnostics (bench roofline). */
+int  gdist_sets_variant_layout(const gdist_sets* sets, int* word_kmers, int* packed, int64_t* row_weight_max);
 /* The sparse words by side: counted from the sets' complement words (sets
  * lacking a commonly held kmer) or from their words (sets holding a rarely
  * held one: positive-sparse). */

@@ -230,6 +230,8 @@ def test_grouped_rare_tier_exact(ctx, opts, c3_like, c4_like, data, walk):
     thr, lists, recs = sets.rare_info()
     assert vk > 1000 and ve > 0 and lists == 0 and thr == 2, (vk, vw, ve, thr, lists)
     assert vw * 3 < vk, ("substitution grouping", vk, vw)
+    wk, packed, wmax = sets.variant_layout()
+    assert wk == 16 and packed and 0 < wmax < 65536, (wk, packed, wmax)
     for (r0, r1, c0, c1, up) in [(0, n, 0, n, True), (37, 211, 5, n - 10, False), (n // 2, n, 0, n, True),
                                  (n - 1, n, 0, n, False)]:
         I, D = sets.matrix((r0, r1), (c0, c1), upper=up, method=gdist.METHOD_BITSET)
