@@ -291,7 +291,7 @@ def main():
         vinfo = sets.variant_info()
         variant = dict(zip(("kmers", "words", "entries", "products"), vinfo)) if vinfo[0] else None
         if variant:
-            variant["word_kmers"], variant["packed"], variant["row_weight_max"] = sets.variant_layout()
+            variant["word_kmers"], variant["member_bytes"], variant["row_weight_max"] = sets.variant_layout()
         mflag = gdist.METHOD_BITSET
     elif method == "sorted":
         # the code all-gather consumes the local shard: peak (ranks + 1) x shard
@@ -546,7 +546,8 @@ def main():
             if v_ms > 0 and variant:
                 f_pairs = pairs_rank / max(1, N * (N - 1) // 2)
                 f_rows = (r1 - r0) / N
-                if variant.get("packed") and ctx.option("variant_short") != 0:
+                mb = variant.get("member_bytes", 12) if ctx.option("variant_short") != 0 else 12
+                if mb == 4:
                     # grouped rare tier (C3): the short-list walk reads one packed
                     # member (4 B: set | mask << 16) per product and per row entry
                     # its set-side record (8 B) and its own packed mask (4 B)
@@ -556,12 +557,13 @@ def main():
                              "(set-side record + its own mask); products = the block's share of the tier's sum "
                              "over words of z(z-1)/2")
                 else:
-                    # variant tier (C4): each product reads one list member (4 B set +
-                    # 8 B mask, coalesced along the word's list) for a row entry (its
-                    # record: 4 B entry + 8 B mask + 8 B list bounds)
-                    v_bytes = 12.0 * variant["products"] * f_pairs + 20.0 * variant["entries"] * f_rows
+                    # variant tier (C4): each product reads one list member (8 B packed
+                    # set << 47 | mask, or 4 B set + 8 B mask, coalesced along the
+                    # word's list) for a row entry (its record: 4 B entry + 8 B mask
+                    # + 8 B list bounds)
+                    v_bytes = float(mb) * variant["products"] * f_pairs + 20.0 * variant["entries"] * f_rows
                     vk = "variant_rows_kernel"
-                    vnote = ("algorithmic bytes = 12 B per product (the list member's set and mask) "
+                    vnote = (f"algorithmic bytes = {mb} B per product (the list member's set and mask) "
                              "+ 20 B per row entry; products = the block's share of the tier's "
                              "sum over words of z(z-1)/2")
                 ach = v_bytes / (v_ms * 1e-3) / 1e9

@@ -770,16 +770,18 @@ __global__ __launch_bounds__(MNT, 2) void bitset_mfma_kernel(
         const int64_t later = ks1 - 1 - ks < NS - 1 ? ks1 - 1 - ks : NS - 1;
         mfma_wait<2 * KM>((int)later);               // stage ks landed everywhere
         if constexpr (RAW) {
-            static_assert(!RAW || KM == 4, "raw stages are 128-byte rows");
+            // KM = 4: 128-byte rows (16 words a stage); KM = 2: 64-byte rows
+            // (8 words), a 64 KiB double-buffered ring (option bitset_mfma_km 2)
+            // lane half h takes chunks KM h .. KM h + KM - 1 of its row
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
+            for (int q = 0; q < KM; q++) {
                 v4i_t af[2], bf[4];
 #pragma unroll
                 for (int a = 0; a < 2; a++)
-                    af[a] = *reinterpret_cast<const v4i_t*>(A + mlds<KM>(wr * 64 + a * 32 + r, 4 * h + q));
+                    af[a] = *reinterpret_cast<const v4i_t*>(A + mlds<KM>(wr * 64 + a * 32 + r, KM * h + q));
 #pragma unroll
                 for (int b = 0; b < 4; b++)
-                    bf[b] = *reinterpret_cast<const v4i_t*>(B + mlds<KM>(wc * 128 + b * 32 + r, 4 * h + q));
+                    bf[b] = *reinterpret_cast<const v4i_t*>(B + mlds<KM>(wc * 128 + b * 32 + r, KM * h + q));
 #pragma unroll
                 for (int m = 0; m < 4; m++) {
                     v4i_t an[2], bn[4];
@@ -2244,7 +2246,14 @@ void build_bitsets(gdist_ctx* ctx, gdist_sets* s, unsigned flags, int64_t rare_t
             }
             sum.codes.release();
             sum.counts.release();
-            build_variant_bitsets(ctx, s, dict, dcnt, U, rare, Ur, mass, T, sp);
+            // 47-kmer words (option variant_bits, default): a substitution's k
+            // windows on each strand fit one word when k x strands <= 47, and
+            // with < 2^17 sets a list member packs into 8 bytes (C4: 42 kmers
+            // a substitution, 100,000 sets); else 64-kmer words of 12-byte members
+            const int strands = (s->kind == GDIST_DNA && (s->flags & GDIST_STRAND_MASK) == GDIST_STRAND_BOTH) ? 2 : 1;
+            const int64_t vb = ctx->option(OPT_VARIANT_BITS, (s->nsets < (int64_t(1) << 17) &&
+                                                              (int64_t)s->k * strands <= 47) ? 47 : 64);
+            build_variant_bitsets(ctx, s, dict, dcnt, U, rare, Ur, mass, T, sp, -1, vb == 47 ? 47 : 64);
             return;
         }
         // The grouped rare tier (round 5, option rare_group): the kmers of 2 ..
@@ -2688,7 +2697,9 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
             // themselves, 16 words a stage, expanded in registers; 0: the FP4
             // nibble operand (KM = 4 or 2 words a stage)
             const bool raw = ctx->option(OPT_BITSET_MFMA_RAW, 1) != 0;
-            const int km = raw ? 16 : ctx->option(OPT_BITSET_MFMA_KM, 4) == 2 ? 2 : 4;
+            const bool km2 = ctx->option(OPT_BITSET_MFMA_KM, 4) == 2;
+            // words a stage: raw 16 (8 with bitset_mfma_km 2), nibbles 4 (2)
+            const int km = raw ? (km2 ? 8 : 16) : km2 ? 2 : 4;
             const int64_t nst = tW / km;
             int msp = (int)std::max<int64_t>(
                 1, std::min<int64_t>(std::max<int64_t>(1, nst / 8), ceil_div((int64_t)ctx->cus * 4, p.nmt)));
@@ -2716,7 +2727,7 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
             }
             // stage ring: KM words a stage x NS stages (option bitset_mfma_ns: 2..4
             // with KM = 2; KM = 4 only double-buffered, 128 KiB either way)
-            const int ns = km != 2 ? 2 : (int)std::max<int64_t>(2, std::min<int64_t>(4, ctx->option(OPT_BITSET_MFMA_NS, 2)));
+            const int ns = !km2 ? 2 : (int)std::max<int64_t>(2, std::min<int64_t>(4, ctx->option(OPT_BITSET_MFMA_NS, 2)));
             auto mlaunch = [&](auto kern, int lds_bytes) {
                 GD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes));
@@ -2724,7 +2735,10 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
                 kern<<<(unsigned)mgrid, MNT, lds_bytes, st>>>(op, tW, p.mtiles.as<int2>(), (int)p.nmt, msp, nst, r0,
                                                                r1, c0, c1, upper ? 1 : 0, d_I, ldI);
             };
-            if (raw) mlaunch(&bitset_mfma_kernel<4, 2, true>, 2 * 2 * mopb<4>());
+            if (raw && !km2) mlaunch(&bitset_mfma_kernel<4, 2, true>, 2 * 2 * mopb<4>());
+            else if (raw && ns == 4) mlaunch(&bitset_mfma_kernel<2, 4, true>, 4 * 2 * mopb<2>());
+            else if (raw && ns == 3) mlaunch(&bitset_mfma_kernel<2, 3, true>, 3 * 2 * mopb<2>());
+            else if (raw) mlaunch(&bitset_mfma_kernel<2, 2, true>, 2 * 2 * mopb<2>());
             else if (km == 4) mlaunch(&bitset_mfma_kernel<4, 2>, 2 * 2 * mopb<4>());
             else if (ns == 4) mlaunch(&bitset_mfma_kernel<2, 4>, 4 * 2 * mopb<2>());
             else if (ns == 3) mlaunch(&bitset_mfma_kernel<2, 3>, 3 * 2 * mopb<2>());

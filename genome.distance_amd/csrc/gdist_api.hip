@@ -803,11 +803,11 @@ int gdist_sets_variant_info(const gdist_sets* s, int64_t* kmers, int64_t* words,
     });
 }
 
-int gdist_sets_variant_layout(const gdist_sets* s, int* word_kmers, int* packed, int64_t* row_weight_max) {
+int gdist_sets_variant_layout(const gdist_sets* s, int* word_kmers, int* member_bytes, int64_t* row_weight_max) {
     return guard([&] {
         check_sets(s);
         if (word_kmers) *word_kmers = s->variant ? s->vw_bits : 0;
-        if (packed) *packed = s->variant && s->vw_pack.p ? 1 : 0;
+        if (member_bytes) *member_bytes = !s->variant ? 0 : s->vw_pack.p ? 4 : s->vw_pk64.p ? 8 : 12;
         if (row_weight_max) *row_weight_max = s->variant ? s->vw_row_wmax : 0;
     });
 }

@@ -245,7 +245,8 @@ struct Timing {
     X(VARIANT_C16, "variant_c16")             /* variant walk: 1 (default) 16-bit counters in 32,768-column chunks, 0 32-bit in 16,384 */ \
     X(VARIANT_SPLIT, "variant_split")         /* variant walk: workgroups a row (default: ~8 a CU over the rows) */ \
     X(RARE_GROUP, "rare_group")               /* 1: the rare kmers as 16-kmer variant words (short-list walk), 0 never (default: 4,096..65,536 sets with guides) */ \
-    X(VARIANT_SHORT, "variant_short")         /* packed variant entries: 1 (default) the lane-per-entry walk, 0 the wave-per-entry walk */ \
+    X(VARIANT_SHORT, "variant_short")         /* packed variant entries: 1 (default) the lane-per-entry walk / 8-byte members, 0 the wave-per-entry walk over the 4 + 8-byte arrays */ \
+    X(VARIANT_BITS, "variant_bits")           /* kmers a variant word: 64 or 47 (default 47: < 2^17 sets, k x strands <= 47) */ \
     X(DENSE_FIRST, "dense_first")             /* the dense tiles issued before the side stream's launches (default: without sparse words) */ \
     X(REPS_SPLIT, "reps_split")               /* greedy reps of a gathered collection: 1 (default) columns sharded over the ranks, 0 every rank all */ \
     X(SERIAL_STEP, "serial_step")             /* 1: the side stream's kernel families on the main stream, in turn (timing) */ \
@@ -421,8 +422,9 @@ struct gdist_sets {
     gdist::DevBuf vw_beg, vw_end;         // uint32 [E]: the entry's word list
     gdist::DevBuf vs_off;                 // int64 [nsets + 1]
     gdist::DevBuf vs_ent;                 // uint32 [E]: entries by set
-    int vw_bits = 64;                     // kmers a variant word (64, or 16: grouped rare tier)
+    int vw_bits = 64;                     // kmers a variant word (64, 47: packed 8-byte members, 16: grouped rare tier)
     gdist::DevBuf vw_pack;                // uint32 [E] (16-kmer words, <= 65,536 sets): set | mask << 16
+    gdist::DevBuf vw_pk64;                // uint64 [E] (47-kmer words, < 2^17 sets): set << 47 | mask
     gdist::DevBuf vs_pent;                // uint64 [E] by set: entry | (end - entry) << 31 | (entry - beg) << 48
     int64_t vw_row_wmax = 0;              // max over sets of their entries' popcounts
     bool auto_sorted = false;             // METHOD_AUTO measured the sorted join cheaper
@@ -636,7 +638,8 @@ int64_t count_in_range(gdist_ctx* ctx, const uint32_t* counts, int64_t n, int64_
 // builds bits (dense tier), the rare postings and the variant tier from the
 // dictionary (dict: codes held by >= T sets, dcounts their holders)
 // (dmin_in > 0: the dense tier's threshold, else variant_dmin; wb: kmers a
-// variant word, 64, or 16: the packed entries of the short-list walk)
+// variant word, 64, 47 (8-byte packed members) or 16 (the packed entries of
+// the short-list walk))
 void build_variant_bitsets(gdist_ctx* ctx, gdist_sets* s, DevBuf& dict, DevBuf& dcounts, int64_t U, DevBuf& rare,
                            int64_t Ur, int64_t mass, int64_t T, BuildSplit& sp, int64_t dmin_in = -1, int wb = 64);
 void free_variant(gdist_sets* s);

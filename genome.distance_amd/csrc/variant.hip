@@ -384,8 +384,8 @@ __global__ __launch_bounds__(256) void hash_probe_kernel(const uint64_t* __restr
 
 // ---- variant records of one fill chunk -----------------------------------
 // per set of the chunk: its variant positions (>= vbase) counted, then
-// written as keys (word << (sbits + 6) | set << 6 | bit), word = q >> lg and
-// bit = q & (2^lg - 1) for words of 2^lg kmers
+// written as keys (word << (sbits + 6) | set << 6 | bit), word = q / wb and
+// bit = q mod wb for words of wb kmers (shifts when wb = 2^lg, lg >= 0)
 __global__ __launch_bounds__(256) void vrec_count_kernel(const uint32_t* __restrict__ pos,
                                                          const int64_t* __restrict__ off, int64_t s0, int64_t base,
                                                          uint32_t vbase, int64_t* __restrict__ cnt) {
@@ -407,7 +407,7 @@ __global__ __launch_bounds__(256) void vrec_count_kernel(const uint32_t* __restr
 
 __global__ __launch_bounds__(256) void vrec_write_kernel(const uint32_t* __restrict__ pos,
                                                          const int64_t* __restrict__ off, int64_t s0, int64_t base,
-                                                         uint32_t vbase, int sbits, int lg,
+                                                         uint32_t vbase, int sbits, int lg, uint32_t wb,
                                                          const int64_t* __restrict__ at, uint64_t* __restrict__ out) {
     __shared__ int64_t wbase;
     const int64_t i = s0 + blockIdx.x;
@@ -429,7 +429,8 @@ __global__ __launch_bounds__(256) void vrec_write_kernel(const uint32_t* __restr
         if (hit) {
             const uint64_t q = p - vbase;
             out[slot + __popcll(m & ((1ull << lane) - 1))] =
-                ((q >> lg) << (sbits + 6)) | ((uint64_t)i << 6) | (q & ((1u << lg) - 1));
+                (lg >= 0 ? ((q >> lg) << (sbits + 6)) | ((uint64_t)i << 6) | (q & ((1u << lg) - 1))
+                         : ((q / wb) << (sbits + 6)) | ((uint64_t)i << 6) | (q % wb));
         }
         __syncthreads();
     }
@@ -543,6 +544,15 @@ __global__ void pack_entries_kernel(const uint32_t* __restrict__ vset, const uns
         pack[e] = (vset[e] & 0xFFFFu) | ((uint32_t)(vmask[e] & 0xFFFFull) << 16);
 }
 
+// 47-kmer words of < 2^17 sets: every entry in one 8-byte member (set << 47
+// | mask) for the wave-per-entry walk (C4: 12 -> 8 bytes a product)
+__global__ void pack64_entries_kernel(const uint32_t* __restrict__ vset, const unsigned long long* __restrict__ vmask,
+                                      int64_t E, unsigned long long* __restrict__ pk) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += stride)
+        pk[e] = ((unsigned long long)vset[e] << 47) | (vmask[e] & ((1ull << 47) - 1));
+}
+
 // the short walk's set-side records, coalesced by the set's position: entry
 // e (31 bits) | the members after it, end - e (17 bits) | its position in its
 // list, e - beg (16 bits): a row reads no random bounds (lists of <= 65,536
@@ -590,11 +600,14 @@ constexpr int VBATCH = 2048;
 // (entry, chunk) visits, fuller 64-member steps); a batch then holds at most
 // 1,023 entries, so a pair's count in it is at most 1,023 x 64 < 2^16 (a
 // set holds one entry per word, and each entry adds at most 64).
-template <bool C16>
+// PK (round 5): members packed as set << 47 | mask (47-kmer words of < 2^17
+// sets, vw_pk64): one 8-byte load a member instead of 4 + 8
+template <bool C16, bool PK = false>
 __global__ __launch_bounds__(1024) void variant_rows_kernel(const int64_t* __restrict__ soff,
                                                            const uint32_t* __restrict__ sent,
                                                            const uint32_t* __restrict__ vset,
                                                            const unsigned long long* __restrict__ vmask,
+                                                           const unsigned long long* __restrict__ vpk,
                                                            const uint32_t* __restrict__ vbeg,
                                                            const uint32_t* __restrict__ vend, int64_t r0, int64_t r1,
                                                            int64_t c0, int64_t c1, int nsplit, int upper,
@@ -625,7 +638,8 @@ __global__ __launch_bounds__(1024) void variant_rows_kernel(const int64_t* __res
                 int64_t a = y, z = ye;
                 while (a < z) {
                     const int64_t mid = (a + z) >> 1;
-                    if ((int64_t)vset[mid] < lo) a = mid + 1; else z = mid;
+                    const int64_t js = PK ? (int64_t)(vpk[mid] >> 47) : (int64_t)vset[mid];
+                    if (js < lo) a = mid + 1; else z = mid;
                 }
                 y = a;
             }
@@ -639,21 +653,35 @@ __global__ __launch_bounds__(1024) void variant_rows_kernel(const int64_t* __res
             __syncthreads();
             for (int t = wv; t < nb; t += nwv) {                 // a wave per entry
                 const uint32_t e = sent[bb + t];
-                const unsigned long long mi = vmask[e];
+                constexpr unsigned long long M47 = (1ull << 47) - 1;
+                const unsigned long long mi = PK ? (vpk[e] & M47) : vmask[e];
                 const int64_t ye = vend[e];
                 int64_t y = ypos[t];
+                // member y: (set, mask) from one packed load or two
+                auto member = [&](int64_t yy, uint32_t& jj, unsigned long long& mm) {
+                    if (PK) {
+                        const unsigned long long p = yy < ye ? vpk[yy] : ~0ull;
+                        jj = yy < ye ? (uint32_t)(p >> 47) : 0xFFFFFFFFu;
+                        mm = p & M47;
+                    } else {
+                        jj = yy < ye ? vset[yy] : 0xFFFFFFFFu;
+                        mm = yy < ye ? vmask[yy] : 0ull;
+                    }
+                };
                 if (y < ye) {
                     // the next 64 members are loaded before this step's are
                     // counted (two steps of loads in flight a wave; round 5:
                     // the walk waited out one load round trip per 64 members)
                     int64_t yy = y + lane;
-                    uint32_t j = yy < ye ? vset[yy] : 0xFFFFFFFFu;
-                    unsigned long long mj = yy < ye ? vmask[yy] : 0ull;
+                    uint32_t j;
+                    unsigned long long mj;
+                    member(yy, j, mj);
                     for (;;) {
                         const bool in = yy < ye && (int64_t)j < ce;
                         const int64_t yn = yy + 64;
-                        const uint32_t jn = yn < ye ? vset[yn] : 0xFFFFFFFFu;
-                        const unsigned long long mn = yn < ye ? vmask[yn] : 0ull;
+                        uint32_t jn;
+                        unsigned long long mn;
+                        member(yn, jn, mn);
                         if (in && (int64_t)j != i) {
                             const int v = __popcll(mi & mj);
                             if (v) {
@@ -1002,6 +1030,7 @@ int64_t variant_dmin(const gdist_ctx* ctx, int64_t nsets) {
 void free_variant(gdist_sets* s) {
     s->variant = false;
     s->vw_pack.release();
+    s->vw_pk64.release();
     s->vs_pent.release();
     s->vw_row_wmax = 0;
     s->vw_bits = 64;
@@ -1022,8 +1051,8 @@ void build_variant_bitsets(gdist_ctx* ctx, gdist_sets* s, DevBuf& dict, DevBuf& 
     Trace tr(st, ctx->trace());
     const int64_t N = s->nsets;
     GD_REQUIRE(N < (int64_t(1) << 31), "too many sets for the variant tier");
-    GD_REQUIRE(wb == 16 || wb == 64, "variant words hold 16 or 64 kmers");
-    const int lg = wb == 16 ? 4 : 6;
+    GD_REQUIRE(wb == 16 || wb == 47 || wb == 64, "variant words hold 16, 47 or 64 kmers");
+    const int lg = wb == 16 ? 4 : wb == 64 ? 6 : -1;
     // 2. tiers: dense (>= Dmin) and variant (T .. Dmin - 1), in code order within the dictionary
     const int64_t dmin = dmin_in > 0 ? dmin_in : variant_dmin(ctx, N);
     DevBuf fd(U * 4 + 4, st), fm(U * 4 + 4, st), pd(U * 8 + 8, st), pm(U * 8 + 8, st);
@@ -1124,6 +1153,7 @@ void build_variant_bitsets(gdist_ctx* ctx, gdist_sets* s, DevBuf& dict, DevBuf& 
         if (n == 0) return;
         DevBuf rA(n * 8 + 8, st), rB(n * 8 + 8, st);
         vrec_write_kernel<<<(unsigned)ns, 256, 0, st>>>(pos, s->off.as<int64_t>(), s0, base, vbase, sbits, lg,
+                                                        (uint32_t)wb,
                                                         a.as<int64_t>(), rA.as<uint64_t>());
         GD_HIP(hipGetLastError());
         uint64_t* rk = rA.as<uint64_t>(); uint64_t* ra = rB.as<uint64_t>();
@@ -1269,6 +1299,13 @@ void build_variant_bitsets(gdist_ctx* ctx, gdist_sets* s, DevBuf& dict, DevBuf& 
             d2h(&hw, wmax.p, 8, st);
             s->vw_row_wmax = (int64_t)hw;
         }
+        if (wb == 47 && N < (int64_t(1) << 17)) {
+            s->vw_pk64.alloc(E * 8 + 64, st);
+            pack64_entries_kernel<<<grid_for(E), 256, 0, st>>>(s->vw_set.as<uint32_t>(),
+                                                               s->vw_mask.as<unsigned long long>(), E,
+                                                               s->vw_pk64.as<unsigned long long>());
+            GD_HIP(hipGetLastError());
+        }
     }
     GD_HIP(hipStreamSynchronize(st));
     s->vw_words = vwords;
@@ -1285,7 +1322,8 @@ void build_variant_bitsets(gdist_ctx* ctx, gdist_sets* s, DevBuf& dict, DevBuf& 
         fprintf(stderr, "gdist: variant tier: T %lld, Dmin %lld: dense %lld kmers (%lld words), variant %lld kmers in "
                         "%lld words of %d, %lld entries, %.3g products, longest list %lld%s; rare %lld kmers\n",
                 (long long)T, (long long)dmin, (long long)Ud, (long long)Wd, (long long)Um, (long long)vwords, wb,
-                (long long)E, s->vw_products, (long long)s->vw_max_list, s->vw_pack.p ? " (packed)" : "",
+                (long long)E, s->vw_products, (long long)s->vw_max_list,
+                s->vw_pack.p ? " (packed 4 B)" : s->vw_pk64.p ? " (packed 8 B)" : "",
                 (long long)Ur);
     build_sparse_words(ctx, s);
 }
@@ -1376,9 +1414,14 @@ void variant_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1,
     // (a workgroup of 32 KiB that fits beside an MFMA tile workgroup, 512
     // threads and 14,336-column chunks: 12.4 vs 8.6 ms alone, step 20.3 vs
     // 16.0 ms, profiles/r05/s10/ab_c4.txt; dropped)
-    auto* kern = ctx->option(OPT_VARIANT_C16, 1) != 0 ? variant_rows_kernel<true> : variant_rows_kernel<false>;
+    // packed 8-byte members (47-kmer words of < 2^17 sets; option variant_short 0 reads the two arrays)
+    const bool pk = s->vw_pk64.p && ctx->option(OPT_VARIANT_SHORT, 1) != 0;
+    const bool c16 = ctx->option(OPT_VARIANT_C16, 1) != 0;
+    auto* kern = c16 ? (pk ? variant_rows_kernel<true, true> : variant_rows_kernel<true, false>)
+                     : (pk ? variant_rows_kernel<false, true> : variant_rows_kernel<false, false>);
     kern<<<(unsigned)grid, 1024, 0, rs>>>(s->vs_off.as<int64_t>(), s->vs_ent.as<uint32_t>(),
                                           s->vw_set.as<uint32_t>(), s->vw_mask.as<unsigned long long>(),
+                                          s->vw_pk64.as<unsigned long long>(),
                                           s->vw_beg.as<uint32_t>(), s->vw_end.as<uint32_t>(), r0, r1, c0,
                                           c1, nsplit, upper ? 1 : 0, d_I, ldI);
     GD_HIP(hipGetLastError());

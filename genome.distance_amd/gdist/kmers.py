@@ -468,13 +468,14 @@ class KmerSets(_Handle):
         L.check(L.lib.gdist_sets_variant_info(self.h, C.byref(a), C.byref(b), C.byref(c), C.byref(d)))
         return a.value, b.value, c.value, d.value
 
-    def variant_layout(self) -> tuple[int, bool, int]:
-        """(kmers a word, packed short-list entries, largest row weight) of the
-        variant tier (gdist_sets_variant_layout): (16, True, w) for the grouped
-        rare tier of <= 65,536 sets (option rare_group)."""
-        wk, pk, rw = C.c_int(), C.c_int(), C.c_int64()
-        L.check(L.lib.gdist_sets_variant_layout(self.h, C.byref(wk), C.byref(pk), C.byref(rw)))
-        return wk.value, bool(pk.value), rw.value
+    def variant_layout(self) -> tuple[int, int, int]:
+        """(kmers a word, bytes a list member, largest row weight) of the
+        variant tier (gdist_sets_variant_layout): (16, 4, w) for the grouped
+        rare tier of <= 65,536 sets (option rare_group), (47, 8, 0) for C4's
+        packed members, (64, 12, 0) unpacked."""
+        wk, mb, rw = C.c_int(), C.c_int(), C.c_int64()
+        L.check(L.lib.gdist_sets_variant_layout(self.h, C.byref(wk), C.byref(mb), C.byref(rw)))
+        return wk.value, mb.value, rw.value
 
     def group_info(self) -> tuple[int, int]:
         """(groups, grouped sparse words) of the group tier (gdist_sets_group_info)."""

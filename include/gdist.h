@@ -259,12 +259,14 @@ int  gdist_sets_sparse_info(const gdist_sets* sets, int64_t* sparse_words, int64
  * products (sum over words of z(z-1)/2); zeros without the tier. */
 int  gdist_sets_variant_info(const gdist_sets* sets, int64_t* kmers, int64_t* words, int64_t* entries,
                              double* products);
-/* The variant tier's layout: kmers a word (64; 16 for the grouped rare tier,
- * option rare_group), whether its entries are packed (set | mask << 16) for
- * the short-list walk (16-kmer words of <= 65,536 sets), and the largest
- * sum of a set's entry popcounts (the bound that allows 16-bit counters).
+/* The variant tier's layout: kmers a word (47 or 64, option variant_bits;
+ * 16 for the grouped rare tier, option rare_group), the bytes of a list
+ * member the walk reads (4: set | mask << 16 of the short-list walk, 16-kmer
+ * words of <= 65,536 sets; 8: set << 47 | mask, 47-kmer words of < 2^17
+ * sets; 12: the 4-byte set and 8-byte mask arrays), and the largest sum of a
+ * set's entry popcounts (16-bit counters below 2^16; 4-byte layout only).
  * Zeros without a variant tier. Diagnostics (bench roofline). */
-int  gdist_sets_variant_layout(const gdist_sets* sets, int* word_kmers, int* packed, int64_t* row_weight_max);
+int  gdist_sets_variant_layout(const gdist_sets* sets, int* word_kmers, int* member_bytes, int64_t* row_weight_max);
 /* The sparse words by side: counted from the sets' complement words (sets
  * lacking a commonly held kmer) or from their words (sets holding a rarely
  * held one: positive-sparse). */

@@ -911,7 +911,8 @@ def test_sparse_equals_dense_at_size(ctx, opts):
     assert np.array_equal(I[iu], oI[iu]) and bits_equal(D[iu], oD[iu])
 
 
-@pytest.mark.parametrize("mfma", [None, "nibble", "km2_group", "km2_ns3", "km2_ns4", "raw_group", 0])
+@pytest.mark.parametrize("mfma", [None, "nibble", "km2_group", "km2_ns3", "km2_ns4", "raw_group", "raw_km2",
+                                  "raw_km2_ns3", 0])
 @pytest.mark.parametrize("T", [0, 3])
 def test_dense_tiles_mfma_exact(ctx, opts, mfma, T):
     """The dense tier's tiles on the matrix cores (FP4 MFMA, 256 x 256 pairs
@@ -923,9 +924,14 @@ def test_dense_tiles_mfma_exact(ctx, opts, mfma, T):
     round 5) and the FP4 nibble operand (option bitset_mfma_raw 0) with
     4-word stages, 2-word stages with the tiles in 2 x 4 blocks, and rings
     of 3 and 4 stages (options bitset_mfma_km, bitset_mfma_group,
-    bitset_mfma_ns)."""
+    bitset_mfma_ns); raw stages of 8 words (a 64 KiB ring, bitset_mfma_km 2)
+    in rings of 2 and 3."""
     import gdist
-    if mfma == "nibble":
+    if mfma == "raw_km2":
+        opts(bitset_mfma=1, bitset_mfma_km=2, sparse=0)
+    elif mfma == "raw_km2_ns3":
+        opts(bitset_mfma=1, bitset_mfma_km=2, bitset_mfma_ns=3, sparse=0)
+    elif mfma == "nibble":
         opts(bitset_mfma=1, bitset_mfma_raw=0, sparse=0)
     elif mfma == "raw_group":
         opts(bitset_mfma=1, bitset_mfma_group=2, sparse=0)
@@ -976,8 +982,8 @@ def test_dense_tiles_mfma_past_f32_bound(ctx, opts, splits):
     eI, eD = oracle.matrix(off, codes, 0, n, 0, n, flags=0, nthreads=4)
     iu = np.triu_indices(n, 1)
     assert eI[iu].min() > (1 << 24), eI[iu]       # the premise: counts past 2^24
-    for mfma, raw in ((1, None), (1, 0), (0, None)):
-        opts(bitset_mfma=mfma, bitset_mfma_raw=raw)
+    for mfma, raw, km in ((1, None, None), (1, None, 2), (1, 0, None), (0, None, None)):
+        opts(bitset_mfma=mfma, bitset_mfma_raw=raw, bitset_mfma_km=km)
         for up in (True, False):
             I, D = sets.matrix(upper=up, method=gdist.METHOD_BITSET)
             if up:

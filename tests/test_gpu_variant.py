@@ -36,13 +36,16 @@ REGIONS = [(0, 1200, 0, 1200, True), (37, 211, 5, 1190, False), (600, 1200, 0, 1
            (1199, 1200, 0, 1200, False)]
 
 
-@pytest.mark.parametrize("mode", ["variant", "variant_windowed_fill", "range_only", "two_tier"])
+@pytest.mark.parametrize("mode", ["variant", "variant_windowed_fill", "variant_w64", "variant_unpacked", "range_only",
+                                  "two_tier"])
 def test_variant_tier_exact(ctx, opts, c4_like, mode):
     """Counts and distances of the variant tier (its hash fill and the
-    windowed fill; the code-range dictionary alone; the two tiers) equal the
-    oracle's over upper triangles, rectangles, unaligned row blocks and row
-    queries; the grouping puts each substitution's kmers into one word
-    (words << kmers)."""
+    windowed fill; 47-kmer words of 8-byte packed members (default), 64-kmer
+    words (option variant_bits 64), the packed words walked from the 4 +
+    8-byte arrays (variant_short 0); the code-range dictionary alone; the two
+    tiers) equal the oracle's over upper triangles, rectangles, unaligned row
+    blocks and row queries; the grouping puts each substitution's kmers into
+    one word (words << kmers)."""
     import gdist
     seqs, off, codes = c4_like
     n = len(seqs)
@@ -53,13 +56,17 @@ def test_variant_tier_exact(ctx, opts, c4_like, mode):
     else:
         # the hash fill (default) or the two-tier build's windowed fill (fill_sort 3)
         opts(variant=1, rare_t=3, variant_dmin=n // 10, range_summary=1,
-             fill_sort=3 if mode == "variant_windowed_fill" else None)
+             fill_sort=3 if mode == "variant_windowed_fill" else None,
+             variant_bits=64 if mode == "variant_w64" else None,
+             variant_short=0 if mode == "variant_unpacked" else None)
     sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
     sets.build_bitsets()
     vk, vw, ve, vp = sets.variant_info()
     if mode.startswith("variant"):
         assert vk > 1000 and ve > 0 and vp > 0, (vk, vw, ve, vp)
         assert vw * 8 < vk, ("substitution grouping", vk, vw)
+        wk, mb, _ = sets.variant_layout()
+        assert (wk, mb) == ((64, 12) if mode == "variant_w64" else (47, 8)), (mode, wk, mb)
     else:
         assert (vk, vw, ve) == (0, 0, 0)
     for (r0, r1, c0, c1, up) in REGIONS:
@@ -230,8 +237,8 @@ def test_grouped_rare_tier_exact(ctx, opts, c3_like, c4_like, data, walk):
     thr, lists, recs = sets.rare_info()
     assert vk > 1000 and ve > 0 and lists == 0 and thr == 2, (vk, vw, ve, thr, lists)
     assert vw * 3 < vk, ("substitution grouping", vk, vw)
-    wk, packed, wmax = sets.variant_layout()
-    assert wk == 16 and packed and 0 < wmax < 65536, (wk, packed, wmax)
+    wk, mb, wmax = sets.variant_layout()
+    assert wk == 16 and mb == 4 and 0 < wmax < 65536, (wk, mb, wmax)
     for (r0, r1, c0, c1, up) in [(0, n, 0, n, True), (37, 211, 5, n - 10, False), (n // 2, n, 0, n, True),
                                  (n - 1, n, 0, n, False)]:
         I, D = sets.matrix((r0, r1), (c0, c1), upper=up, method=gdist.METHOD_BITSET)
