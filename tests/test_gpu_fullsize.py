@@ -102,26 +102,18 @@ def _full_row(M, i):
 
 
 @pytest.mark.timeout(900)
-def test_c3_full_size_auto_vs_oracle(ctx):
+def test_c3_full_size_auto_vs_oracle(ctx, opts):
+    """C3 at full size through METHOD_AUTO: the grouped rare tier (round 5,
+    the default at this size: the rare kmers as 16-kmer variant words, the
+    short-list walk) and the two-tier dictionary with posting lists (option
+    rare_group 0); rows 0, 4999 and 9998 in full against the oracle."""
     import gdist
     from gdist import synth
     n, L = 10000, 33_333
     g = synth.genomes(n, L, 0.10, 3, protein=True)           # bench.py's C3 workload (cfg seed 3)
     blob, off = synth.to_blob(g)
     del g
-    sets = gdist.KmerSets.from_blob(blob, off, 8, gdist.KmerType.PROT, 0, ctx)
-    chosen, cb, cs = sets.prepare(gdist.METHOD_AUTO)
-    assert chosen == gdist.METHOD_BITSET and 0 < cb < cs, (chosen, cb, cs)
-    thr, lists, recs = sets.rare_info()
-    assert thr > 2 and lists > 0 and recs > lists, "C3 must run the two-tier dictionary with a rare tier"
-    dI, dD = ctx.alloc(n * n * 4), ctx.alloc(n * n * 8)
-    for _ in range(3):                                       # plan + capture + replay, as the bench steps
-        sets.matrix_device(dI.ptr, dD.ptr, n, (0, n), (0, n), upper=True, method=gdist.METHOD_AUTO)
-    I = dI.to_host(np.int32).reshape(n, n)
-    D = dD.to_host(np.float64).reshape(n, n)
-    dI.free(); dD.free()
     seqs = [bytes(blob[off[i]:off[i + 1]]) for i in range(n)]
-    del blob
     rows = (0, 4999, 9998)
     with cf.ThreadPoolExecutor(_threads()) as ex:
         row_codes = list(ex.map(lambda i: oracle.kmer_codes(seqs[i], 8, 1, 0), rows))
@@ -130,13 +122,33 @@ def test_c3_full_size_auto_vs_oracle(ctx):
             cj = oracle.kmer_codes(seqs[j], 8, 1, 0)
             return [(oracle.intersect(rc, cj), len(cj)) for rc in row_codes]
         cols = list(ex.map(column, range(n)))
-    for r, (i, rc) in enumerate(zip(rows, row_codes)):
-        eI = np.array([cols[j][r][0] for j in range(n)], np.int64)
-        eD = np.array([oracle.distance(int(eI[j]), len(rc), int(cols[j][r][1])) for j in range(n)])
-        m = np.arange(n) != i
-        gi, gd = _full_row(I, i).astype(np.int64), _full_row(D, i)
-        assert np.array_equal(gi[m], eI[m]), (i, np.flatnonzero((gi != eI) & m)[:8])
-        assert bits_equal(gd[m], eD[m]), i
+    del seqs
+    for tier in ("grouped", "two_tier"):
+        opts(rare_group=0 if tier == "two_tier" else None)
+        sets = gdist.KmerSets.from_blob(blob, off, 8, gdist.KmerType.PROT, 0, ctx)
+        chosen, cb, cs = sets.prepare(gdist.METHOD_AUTO)
+        assert chosen == gdist.METHOD_BITSET and 0 < cb < cs, (tier, chosen, cb, cs)
+        thr, lists, recs = sets.rare_info()
+        if tier == "grouped":
+            wk, mb, _ = sets.variant_layout()
+            assert thr == 2 and lists == 0 and (wk, mb) == (16, 4), (thr, lists, wk, mb)
+        else:
+            assert thr > 2 and lists > 0 and recs > lists, "C3 must run the two-tier dictionary with a rare tier"
+        dI, dD = ctx.alloc(n * n * 4), ctx.alloc(n * n * 8)
+        for _ in range(3):                                   # plan + capture + replay, as the bench steps
+            sets.matrix_device(dI.ptr, dD.ptr, n, (0, n), (0, n), upper=True, method=gdist.METHOD_AUTO)
+        I = dI.to_host(np.int32).reshape(n, n)
+        D = dD.to_host(np.float64).reshape(n, n)
+        dI.free(); dD.free()
+        del sets
+        for r, (i, rc) in enumerate(zip(rows, row_codes)):
+            eI = np.array([cols[j][r][0] for j in range(n)], np.int64)
+            eD = np.array([oracle.distance(int(eI[j]), len(rc), int(cols[j][r][1])) for j in range(n)])
+            m = np.arange(n) != i
+            gi, gd = _full_row(I, i).astype(np.int64), _full_row(D, i)
+            assert np.array_equal(gi[m], eI[m]), (tier, i, np.flatnonzero((gi != eI) & m)[:8])
+            assert bits_equal(gd[m], eD[m]), (tier, i)
+        del I, D
 
 
 @pytest.mark.timeout(900)
