@@ -727,7 +727,10 @@ __device__ __forceinline__ v4i_t raw_nibbles(uint32_t x) {
 
 // NS stages in a ring (2: double buffering; 4 with KM = 2 in the same 128
 // KiB: three stages in flight while one is computed; option bitset_mfma_km)
-template <int KM, int NS, bool RAW = false>
+// STORE (round 5, option bitset_mfma_store): one K split, every pair of the
+// tile STORED (the tile is its only writer; the other families add after it
+// in stream order) instead of 64 K device atomics a tile
+template <int KM, int NS, bool RAW = false, bool STORE = false>
 __global__ __launch_bounds__(MNT, 2) void bitset_mfma_kernel(
     const unsigned char* __restrict__ F, int64_t W, const int2* __restrict__ tiles, int ntiles, int splits,
     int64_t nstages, int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I,
@@ -831,7 +834,11 @@ __global__ __launch_bounds__(MNT, 2) void bitset_mfma_kernel(
                 const int64_t i = row0 + wr * 64 + a * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
                 const int64_t j = col0 + wc * 128 + b * 32 + r;
                 const int v = (int)acc[a][b][q];
-                if (v && i < r1 && j < c1 && !(upper && j <= i)) atomicAdd(I + (i - r0) * ldI + (j - c0), v);
+                if (STORE) {
+                    if (i < r1 && j < c1 && !(upper && j <= i)) I[(i - r0) * ldI + (j - c0)] = v;
+                } else if (v && i < r1 && j < c1 && !(upper && j <= i)) {
+                    atomicAdd(I + (i - r0) * ldI + (j - c0), v);
+                }
             }
 }
 
@@ -2650,8 +2657,16 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     // 2.63 ms, C4 slice 15.8 vs 16.0 ms; C2-realistic's sparse launch first:
     // 0.321 vs 0.353 ms, profiles/r05/s16/)
     const bool serial = ctx->option(OPT_SERIAL_STEP, 0) != 0;
-    const bool dense_first = side && !serial && ctx->option(OPT_DENSE_FIRST, s->sparse ? 0 : 1) != 0;
-    if (side) GD_HIP(hipEventRecord(ctx->ev_fork, st));
+    // option bitset_mfma_store: the MFMA tiles store their counts (one K
+    // split; the side families then start after them: the fork is recorded
+    // after the dense launch). Off by default: the tiles alone gain (C3 0.71
+    // vs 0.76 ms) but the step loses its overlap (C3 1.81 vs 1.67 ms, C4
+    // slice span 16.9 vs 14.8 ms; profiles/r05/s26)
+    const int64_t tWm = s->sparse ? s->Wd : s->W;
+    const bool mstore = p.nmt > 0 && !s->sparse && ctx->option(OPT_BITSET_MFMA_STORE, 0) != 0 &&
+                        mfma_min_splits(tWm / (ctx->option(OPT_BITSET_MFMA_RAW, 1) != 0 ? 16 : 4), 16) == 1;
+    const bool dense_first = side && (mstore || (!serial && ctx->option(OPT_DENSE_FIRST, s->sparse ? 0 : 1) != 0));
+    if (side && !mstore) GD_HIP(hipEventRecord(ctx->ev_fork, st));
     auto launch_side = [&]() {
         hipStream_t sd = serial ? st : ctx->side;
         GD_HIP(hipStreamWaitEvent(sd, ctx->ev_fork, 0));
@@ -2701,10 +2716,15 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
             // words a stage: raw 16 (8 with bitset_mfma_km 2), nibbles 4 (2)
             const int km = raw ? (km2 ? 8 : 16) : km2 ? 2 : 4;
             const int64_t nst = tW / km;
+            // (~2 rounds when side-stream families run beside the tiles: C3's
+            // 820 tiles unsplit, step 1.61 vs 1.67 ms with 2 splits, the walk
+            // keeping more of the CUs; profiles/r05/s26)
+            const int64_t rounds = side ? 2 : 4;
             int msp = (int)std::max<int64_t>(
-                1, std::min<int64_t>(std::max<int64_t>(1, nst / 8), ceil_div((int64_t)ctx->cus * 4, p.nmt)));
+                1, std::min<int64_t>(std::max<int64_t>(1, nst / 8), ceil_div((int64_t)ctx->cus * rounds, p.nmt)));
             if (ctx->has_option(OPT_BITSET_MFMA_SPLITS))      // A/B: a given K split
                 msp = (int)std::max<int64_t>(1, std::min<int64_t>(nst, ctx->option(OPT_BITSET_MFMA_SPLITS, 1)));
+            if (mstore) msp = 1;                              // stores: one writer a pair
             // exactness: a split's f32 accumulator sums at most 64 x (its
             // words) bits; f32 holds every integer <= 2^24 exactly, so no
             // split may span more than kMfmaMaxSplitWords words (a pair of
@@ -2735,7 +2755,8 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
                 kern<<<(unsigned)mgrid, MNT, lds_bytes, st>>>(op, tW, p.mtiles.as<int2>(), (int)p.nmt, msp, nst, r0,
                                                                r1, c0, c1, upper ? 1 : 0, d_I, ldI);
             };
-            if (raw && !km2) mlaunch(&bitset_mfma_kernel<4, 2, true>, 2 * 2 * mopb<4>());
+            if (raw && !km2 && mstore) mlaunch(&bitset_mfma_kernel<4, 2, true, true>, 2 * 2 * mopb<4>());
+            else if (raw && !km2) mlaunch(&bitset_mfma_kernel<4, 2, true>, 2 * 2 * mopb<4>());
             else if (raw && ns == 4) mlaunch(&bitset_mfma_kernel<2, 4, true>, 4 * 2 * mopb<2>());
             else if (raw && ns == 3) mlaunch(&bitset_mfma_kernel<2, 3, true>, 3 * 2 * mopb<2>());
             else if (raw) mlaunch(&bitset_mfma_kernel<2, 2, true>, 2 * 2 * mopb<2>());
@@ -2763,6 +2784,7 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
         }
         ft.end();
     }
+    if (side && mstore) GD_HIP(hipEventRecord(ctx->ev_fork, st));   // after the stored tiles
     if (dense_first) launch_side();
     if (overlap && s->sparse && !rare_done) launch_rare_pairs(st);
     GD_HIP(hipGetLastError());

@@ -912,7 +912,7 @@ def test_sparse_equals_dense_at_size(ctx, opts):
 
 
 @pytest.mark.parametrize("mfma", [None, "nibble", "km2_group", "km2_ns3", "km2_ns4", "raw_group", "raw_km2",
-                                  "raw_km2_ns3", 0])
+                                  "raw_km2_ns3", "store", 0])
 @pytest.mark.parametrize("T", [0, 3])
 def test_dense_tiles_mfma_exact(ctx, opts, mfma, T):
     """The dense tier's tiles on the matrix cores (FP4 MFMA, 256 x 256 pairs
@@ -925,9 +925,12 @@ def test_dense_tiles_mfma_exact(ctx, opts, mfma, T):
     4-word stages, 2-word stages with the tiles in 2 x 4 blocks, and rings
     of 3 and 4 stages (options bitset_mfma_km, bitset_mfma_group,
     bitset_mfma_ns); raw stages of 8 words (a 64 KiB ring, bitset_mfma_km 2)
-    in rings of 2 and 3."""
+    in rings of 2 and 3; one K split storing its counts, the rare tier after
+    it (option bitset_mfma_store)."""
     import gdist
-    if mfma == "raw_km2":
+    if mfma == "store":
+        opts(bitset_mfma=1, bitset_mfma_store=1, sparse=0)
+    elif mfma == "raw_km2":
         opts(bitset_mfma=1, bitset_mfma_km=2, sparse=0)
     elif mfma == "raw_km2_ns3":
         opts(bitset_mfma=1, bitset_mfma_km=2, bitset_mfma_ns=3, sparse=0)

@@ -36,8 +36,8 @@ REGIONS = [(0, 1200, 0, 1200, True), (37, 211, 5, 1190, False), (600, 1200, 0, 1
            (1199, 1200, 0, 1200, False)]
 
 
-@pytest.mark.parametrize("mode", ["variant", "variant_windowed_fill", "variant_w64", "variant_unpacked", "range_only",
-                                  "two_tier"])
+@pytest.mark.parametrize("mode", ["variant", "variant_windowed_fill", "variant_w64", "variant_unpacked", "variant_store",
+                                  "range_only", "two_tier"])
 def test_variant_tier_exact(ctx, opts, c4_like, mode):
     """Counts and distances of the variant tier (its hash fill and the
     windowed fill; 47-kmer words of 8-byte packed members (default), 64-kmer
@@ -58,7 +58,8 @@ def test_variant_tier_exact(ctx, opts, c4_like, mode):
         opts(variant=1, rare_t=3, variant_dmin=n // 10, range_summary=1,
              fill_sort=3 if mode == "variant_windowed_fill" else None,
              variant_bits=64 if mode == "variant_w64" else None,
-             variant_short=0 if mode == "variant_unpacked" else None)
+             variant_short=0 if mode == "variant_unpacked" else None,
+             bitset_mfma_store=1 if mode == "variant_store" else None)
     sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
     sets.build_bitsets()
     vk, vw, ve, vp = sets.variant_info()
@@ -216,7 +217,7 @@ def c3_like():
 
 
 @pytest.mark.parametrize("data,walk", [("protein", "short"), ("protein", "short_c32"), ("protein", "short_split"),
-                                       ("protein", "wave"), ("dna", "short"), ("dna", "wave")])
+                                       ("protein", "wave"), ("protein", "store"), ("dna", "short"), ("dna", "wave")])
 def test_grouped_rare_tier_exact(ctx, opts, c3_like, c4_like, data, walk):
     """Round 5, option rare_group: the kmers of 2 .. T - 1 sets as 16-kmer
     variant words (one substitution a word; DNA's 42 kmers of a substitution
@@ -229,7 +230,8 @@ def test_grouped_rare_tier_exact(ctx, opts, c3_like, c4_like, data, walk):
     seqs, off, codes = c3_like if data == "protein" else c4_like
     n = len(seqs)
     opts(variant=0, rare_group=1, variant_short=0 if walk == "wave" else None,
-         variant_c16=0 if walk == "short_c32" else None, variant_split=3 if walk == "short_split" else None)
+         variant_c16=0 if walk == "short_c32" else None, variant_split=3 if walk == "short_split" else None,
+         bitset_mfma_store=1 if walk == "store" else None)
     kind, k = (gdist.KmerType.PROT, 8) if data == "protein" else (gdist.KmerType.DNA, 21)
     sets = gdist.KmerSets.from_sequences(seqs, k, kind, 0, ctx)
     sets.build_bitsets()
