@@ -677,20 +677,20 @@ template <int KM> __device__ __forceinline__ int mlds(int g, int c) { return g *
 
 // one operand's stage: 16-byte chunks, KM per thread (lane-linear LDS, the
 // swizzle applied on the source address)
-template <int KM>
+template <int KM, int NT = MNT>
 __device__ __forceinline__ void mfma_stage(const unsigned char* __restrict__ F, int64_t rowbytes, int64_t set0,
                                            int64_t lo, int64_t lim, int64_t w0, unsigned char* lds_op, int tid) {
     constexpr int CPR = 2 * KM;                       // chunks per row
 #pragma unroll
-    for (int i = 0; i < KM; i++) {
-        const int q = i * MNT + tid;                  // 16-byte slot of the stage
+    for (int i = 0; i < KM * (MNT / NT); i++) {
+        const int q = i * NT + tid;                   // 16-byte slot of the stage
         const int g = q / CPR, sl = q % CPR;
         const int c = mslot<KM>(g, sl);               // the chunk this slot holds (the swizzle is an involution)
         int64_t set = set0 + g;
         set = set < lim ? set : lim - 1;              // rows outside [lo, lim): clamped, masked at the end
         set = set >= lo ? set : lo;
         const unsigned char* src = F + set * rowbytes + w0 * 32 + c * 16;
-        __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(lds_op + (i * MNT + (tid & ~63)) * 16), 16,
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(lds_op + (i * NT + (tid & ~63)) * 16), 16,
                                          0, 0);
     }
 }
