@@ -247,6 +247,7 @@ struct Timing {
     X(VARIANT_SPLIT, "variant_split")         /* variant walk: workgroups a row (default: ~8 a CU over the rows) */ \
     X(RARE_GROUP, "rare_group")               /* 1: the rare kmers as 16-kmer variant words (short-list walk), 0 never (default: 4,096..65,536 sets with guides) */ \
     X(VARIANT_SHORT, "variant_short")         /* packed variant entries: 1 (default) the lane-per-entry walk / 8-byte members, 0 the wave-per-entry walk over the 4 + 8-byte arrays */ \
+    X(EPILOGUE_ROWS, "epilogue_rows")         /* distance epilogue: 1 (default) a block a row, 0 the flat kernel */ \
     X(VARIANT_BITS, "variant_bits")           /* kmers a variant word: 64 or 47 (default 47: < 2^17 sets, k x strands <= 47) */ \
     X(DENSE_FIRST, "dense_first")             /* the dense tiles issued before the side stream's launches (default: without sparse words) */ \
     X(REPS_SPLIT, "reps_split")               /* greedy reps of a gathered collection: 1 (default) columns sharded over the ranks, 0 every rank all */ \
