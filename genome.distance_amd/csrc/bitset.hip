@@ -2310,10 +2310,16 @@ void build_bitsets(gdist_ctx* ctx, gdist_sets* s, unsigned flags, int64_t rare_t
             T = 2;
             dictionary_from(ctx, {SummaryView{sum.codes.as<uint64_t>(), sum.counts.as<uint32_t>(), sum.n}}, false, T,
                             s->nsets, dict, U, rare, Ur, mass, &dcnt);
-            sum.codes.release();
-            sum.counts.release();
-            build_variant_bitsets(ctx, s, dict, dcnt, U, rare, Ur, mass, T, sp, dmin, 16);
-            return;
+            // (probing by default and with rare_group = 2; 1 forces the tier)
+            if (build_variant_bitsets(ctx, s, dict, dcnt, U, rare, Ur, mass, T, sp, dmin, 16, rg <= 0 || rg == 2)) {
+                sum.codes.release();
+                sum.counts.release();
+                return;
+            }
+            // keyless kmers dominate (no substitution structure): the two tiers
+            T = dmin;
+            dictionary_from(ctx, {SummaryView{sum.codes.as<uint64_t>(), sum.counts.as<uint32_t>(), sum.n}}, false, T,
+                            s->nsets, dict, U, rare, Ur, mass, &dcnt);
         }
     }
     const int64_t W = bitset_words(U);

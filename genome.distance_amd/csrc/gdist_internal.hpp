@@ -245,9 +245,10 @@ struct Timing {
     X(RARE_C16, "rare_c16")                   /* row-major rare walk: 1 (default) 16-bit LDS counters when every row's rare weight < 2^16, 0 32-bit */ \
     X(VARIANT_C16, "variant_c16")             /* variant walk: 1 (default) 16-bit counters in 32,768-column chunks, 0 32-bit in 16,384 */ \
     X(VARIANT_SPLIT, "variant_split")         /* variant walk: workgroups a row (default: ~8 a CU over the rows) */ \
-    X(RARE_GROUP, "rare_group")               /* 1: the rare kmers as 16-kmer variant words (short-list walk), 0 never (default: 4,096..65,536 sets with guides) */ \
+    X(RARE_GROUP, "rare_group")               /* 1: the rare kmers as 16-kmer variant words (short-list walk), 2: the same unless keyless kmers are most of them, 0 never (default: as 2 for 4,096..65,536 sets with guides) */ \
     X(VARIANT_SHORT, "variant_short")         /* packed variant entries: 1 (default) the lane-per-entry walk / 8-byte members, 0 the wave-per-entry walk over the 4 + 8-byte arrays */ \
     X(EPILOGUE_ROWS, "epilogue_rows")         /* distance epilogue: 1 (default) a block a row, 0 the flat kernel */ \
+    X(VARIANT_PACK_KEYLESS, "variant_pack_keyless") /* 1 (default): keyless variant kmers packed a word-width at a time in code order; 0 a word each */ \
     X(VARIANT_BITS, "variant_bits")           /* kmers a variant word: 64 or 47 (default 47: < 2^17 sets, k x strands <= 47) */ \
     X(DENSE_FIRST, "dense_first")             /* the dense tiles issued before the side stream's launches (default: without sparse words) */ \
     X(REPS_SPLIT, "reps_split")               /* greedy reps of a gathered collection: 1 (default) columns sharded over the ranks, 0 every rank all */ \
@@ -642,8 +643,11 @@ int64_t count_in_range(gdist_ctx* ctx, const uint32_t* counts, int64_t n, int64_
 // (dmin_in > 0: the dense tier's threshold, else variant_dmin; wb: kmers a
 // variant word, 64, 47 (8-byte packed members) or 16 (the packed entries of
 // the short-list walk))
-void build_variant_bitsets(gdist_ctx* ctx, gdist_sets* s, DevBuf& dict, DevBuf& dcounts, int64_t U, DevBuf& rare,
-                           int64_t Ur, int64_t mass, int64_t T, BuildSplit& sp, int64_t dmin_in = -1, int wb = 64);
+// probe: a grouped rare tier chosen by default — false (nothing built or
+// changed) when keyless kmers are most of the tier
+bool build_variant_bitsets(gdist_ctx* ctx, gdist_sets* s, DevBuf& dict, DevBuf& dcounts, int64_t U, DevBuf& rare,
+                           int64_t Ur, int64_t mass, int64_t T, BuildSplit& sp, int64_t dmin_in = -1, int wb = 64,
+                           bool probe = false);
 void free_variant(gdist_sets* s);
 void variant_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1, bool upper,
                     int32_t* d_I, int64_t ldI, hipStream_t rs);

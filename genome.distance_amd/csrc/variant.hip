@@ -218,8 +218,10 @@ __global__ __launch_bounds__(256) void variant_key_kernel(const uint64_t* __rest
 // group heads of the sorted keys (a keyless kmer is a group of its own) ->
 // words of the group: ceil(len / wb), each group starting a new word (wb:
 // kmers a word, 64, or 16 for the short-list walk's packed entries)
-__global__ void group_words_kernel(const uint64_t* __restrict__ k, int64_t n, int wb, int32_t* __restrict__ head,
-                                   int64_t* __restrict__ words) {
+// (pack = 0: every keyless kmer a word of its own — unrelated kmers never
+// share a word's entry list)
+__global__ void group_words_kernel(const uint64_t* __restrict__ k, int64_t n, int wb, int pack,
+                                   int32_t* __restrict__ head, int64_t* __restrict__ words) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const bool h = i == 0 || k[i] != k[i - 1] || k[i] == ~0ull;
@@ -227,10 +229,10 @@ __global__ void group_words_kernel(const uint64_t* __restrict__ k, int64_t n, in
         int64_t wn = 0;
         if (h) {
             int64_t e = i + 1;
-            if (k[i] == ~0ull) e = n;                        // the keyless kmers: one group, packed
+            if (k[i] == ~0ull) e = pack ? n : i + 1;         // the keyless kmers: one group, packed
             else while (e < n && k[e] == k[i]) e++;
             wn = ceil_div(e - i, wb);
-            if (k[i] == ~0ull && i > 0 && k[i - 1] == ~0ull) wn = 0;
+            if (pack && k[i] == ~0ull && i > 0 && k[i - 1] == ~0ull) wn = 0;
         }
         words[i] = wn;
     }
@@ -239,12 +241,17 @@ __global__ void group_words_kernel(const uint64_t* __restrict__ k, int64_t n, in
 // the variant position of every variant kmer (sorted index q -> word of its
 // group + offset): perm over the combined dictionary's variant ranks
 __global__ void group_pos_kernel(const uint64_t* __restrict__ k, const int32_t* __restrict__ order, int64_t n,
-                                 const int64_t* __restrict__ wstart, int wb, uint32_t base, uint32_t* __restrict__ mpos) {
+                                 const int64_t* __restrict__ wstart, int wb, int pack, uint32_t base,
+                                 uint32_t* __restrict__ mpos) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         // the group's head: the first index with the same key (keyless: the first keyless)
         int64_t lo = 0, hi = i;
         const uint64_t key = k[i];
+        if (!pack && key == ~0ull) {                         // a keyless kmer's own word
+            mpos[order[i]] = base + (uint32_t)(wstart[i] * wb);
+            continue;
+        }
         while (lo < hi) {
             const int64_t mid = (lo + hi) >> 1;
             if (k[mid] < key) lo = mid + 1; else hi = mid;
@@ -825,6 +832,16 @@ __global__ __launch_bounds__(NT) void variant_short_kernel(const int64_t* __rest
     }
 }
 
+// the first index of a sorted key array holding ~0 (n if none): one thread
+__global__ void first_keyless_kernel(const uint64_t* __restrict__ k, int64_t n, int64_t* __restrict__ out) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (k[mid] != ~0ull) lo = mid + 1; else hi = mid;
+    }
+    *out = lo;
+}
+
 __global__ void viota_kernel(int32_t* __restrict__ p, int64_t n) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = (int32_t)i;
@@ -1055,14 +1072,21 @@ void free_variant(gdist_sets* s) {
     s->vs_ent.release();
 }
 
-void build_variant_bitsets(gdist_ctx* ctx, gdist_sets* s, DevBuf& dict, DevBuf& dcnt, int64_t U, DevBuf& rare,
-                           int64_t Ur, int64_t mass, int64_t T, BuildSplit& sp, int64_t dmin_in, int wb) {
+bool build_variant_bitsets(gdist_ctx* ctx, gdist_sets* s, DevBuf& dict, DevBuf& dcnt, int64_t U, DevBuf& rare,
+                           int64_t Ur, int64_t mass, int64_t T, BuildSplit& sp, int64_t dmin_in, int wb, bool probe) {
     hipStream_t st = ctx->stream;
     Trace tr(st, ctx->trace());
     const int64_t N = s->nsets;
     GD_REQUIRE(N < (int64_t(1) << 31), "too many sets for the variant tier");
     GD_REQUIRE(wb == 16 || wb == 47 || wb == 64, "variant words hold 16, 47 or 64 kmers");
     const int lg = wb == 16 ? 4 : wb == 64 ? 6 : -1;
+    // keyless kmers (no keyed dense neighbour: two substitutions in a window,
+    // or no guide) packed wb to a word in code order (option
+    // variant_pack_keyless, default), or each in a word of its own
+    // (16-kmer words of the grouped rare tier: packed only while keyless
+    // kmers are <= 1/4 of the tier — C3 ~9 % — so that unrelated kmers never
+    // make one long list; without locus keys, packed, C3 took 15.1 ms a step)
+    int pack = ctx->option(OPT_VARIANT_PACK_KEYLESS, 1) != 0 ? 1 : 0;
     // 2. tiers: dense (>= Dmin) and variant (T .. Dmin - 1), in code order within the dictionary
     const int64_t dmin = dmin_in > 0 ? dmin_in : variant_dmin(ctx, N);
     DevBuf fd(U * 4 + 4, st), fm(U * 4 + 4, st), pd(U * 8 + 8, st), pm(U * 8 + 8, st);
@@ -1122,8 +1146,27 @@ void build_variant_bitsets(gdist_ctx* ctx, gdist_sets* s, DevBuf& dict, DevBuf& 
         uint64_t* k = vkey.as<uint64_t>(); uint64_t* ka = vkalt.as<uint64_t>();
         int32_t* v = ord.as<int32_t>(); int32_t* va = oalt.as<int32_t>();
         sort_pairs_u64_i32(ctx, k, ka, v, va, (size_t)Um, 0, 64);
+        if (wb == 16) {
+            // keyless kmers sort last (key ~0): their share decides the packing,
+            // and a probing build (the grouped rare tier chosen by default)
+            // gives up when they are most of the tier: the grouping would not
+            // pay (C3 without locus keys: 3.59 ms a step, the two tiers 2.28)
+            DevBuf fk(8, st);
+            first_keyless_kernel<<<1, 1, 0, st>>>(k, Um, fk.as<int64_t>());
+            GD_HIP(hipGetLastError());
+            int64_t first = Um;
+            d2h(&first, fk.p, 8, st);
+            const int64_t keyless = Um - first;
+            if (!ctx->has_option(OPT_VARIANT_PACK_KEYLESS)) pack = 4 * keyless <= Um ? 1 : 0;
+            if (probe && 2 * keyless > Um) {
+                if (ctx->trace())
+                    fprintf(stderr, "gdist: grouped rare tier: %lld of %lld kmers keyless, two tiers instead\n",
+                            (long long)keyless, (long long)Um);
+                return false;
+            }
+        }
         DevBuf head(Um * 4 + 4, st), wn(Um * 8 + 8, st), wst(Um * 8 + 8, st);
-        group_words_kernel<<<grid_for(Um), 256, 0, st>>>(k, Um, wb, head.as<int32_t>(), wn.as<int64_t>());
+        group_words_kernel<<<grid_for(Um), 256, 0, st>>>(k, Um, wb, pack, head.as<int32_t>(), wn.as<int64_t>());
         GD_HIP(hipGetLastError());
         exclusive_scan_i64(ctx, wn.as<int64_t>(), wst.as<int64_t>(), (size_t)Um);
         int64_t h[2];
@@ -1131,7 +1174,8 @@ void build_variant_bitsets(gdist_ctx* ctx, gdist_sets* s, DevBuf& dict, DevBuf& 
         d2h(&h[1], wn.as<int64_t>() + Um - 1, 8, st);
         vwords = h[0] + h[1];
         GD_REQUIRE((double)vbase + (double)vwords * wb < 4294967295.0, "variant tier too large for u32 positions");
-        group_pos_kernel<<<grid_for(Um), 256, 0, st>>>(k, v, Um, wst.as<int64_t>(), wb, vbase, mperm.as<uint32_t>());
+        group_pos_kernel<<<grid_for(Um), 256, 0, st>>>(k, v, Um, wst.as<int64_t>(), wb, pack, vbase,
+                                                       mperm.as<uint32_t>());
         GD_HIP(hipGetLastError());
     }
     DevBuf perm(U * 4 + 4, st);
@@ -1336,6 +1380,7 @@ void build_variant_bitsets(gdist_ctx* ctx, gdist_sets* s, DevBuf& dict, DevBuf& 
                 s->vw_pack.p ? " (packed 4 B)" : s->vw_pk64.p ? " (packed 8 B)" : "",
                 (long long)Ur);
     build_sparse_words(ctx, s);
+    return true;
 }
 
 // Decides after the dictionary of build_bitsets whether the collection takes

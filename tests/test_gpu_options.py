@@ -20,7 +20,7 @@ def test_option_roundtrip_and_errors(ctx):
     for n in ("rare_t", "rare_kernel", "bitset_diag", "sparse", "sparse_zmax", "sketch_k", "reps_block",
               "locus_order", "guides", "sparse_part_budget", "sparse_groups", "sketch_v2", "sketch_phase",
               "sketch_cap", "sketch_ring", "sketch_wait", "sparse_xcd", "time_kernels",
-              "rare_u16", "rare_rows_threads", "rare_direct", "split_build", "variant_c16", "variant_split", "rare_group", "variant_short", "variant_bits", "bitset_mfma_store", "epilogue_rows", "bitset_mfma_raw", "serial_step", "dense_first", "reps_split", "rare_c16", "sort_radix", "bitset_mfma", "bitset_mfma_km", "bitset_mfma_group", "bitset_mfma_ns", "bitset_mfma_splits", "sparse_mt", "sparse_sun", "sparse_dyn", "sparse_diag22", "sparse_rpart22", "pack_code_sort", "variant", "variant_dmin", "range_summary"):
+              "rare_u16", "rare_rows_threads", "rare_direct", "split_build", "variant_c16", "variant_split", "rare_group", "variant_short", "variant_bits", "bitset_mfma_store", "variant_pack_keyless", "epilogue_rows", "bitset_mfma_raw", "serial_step", "dense_first", "reps_split", "rare_c16", "sort_radix", "bitset_mfma", "bitset_mfma_km", "bitset_mfma_group", "bitset_mfma_ns", "bitset_mfma_splits", "sparse_mt", "sparse_sun", "sparse_dyn", "sparse_diag22", "sparse_rpart22", "pack_code_sort", "variant", "variant_dmin", "range_summary"):
         assert n in names
     # round 3: superseded kernel variants and the result-changing ablation
     # switch are gone; every remaining option preserves results

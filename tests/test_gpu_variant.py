@@ -217,7 +217,8 @@ def c3_like():
 
 
 @pytest.mark.parametrize("data,walk", [("protein", "short"), ("protein", "short_c32"), ("protein", "short_split"),
-                                       ("protein", "wave"), ("protein", "store"), ("dna", "short"), ("dna", "wave")])
+                                       ("protein", "wave"), ("protein", "store"), ("protein", "own_words"),
+                                       ("dna", "short"), ("dna", "wave")])
 def test_grouped_rare_tier_exact(ctx, opts, c3_like, c4_like, data, walk):
     """Round 5, option rare_group: the kmers of 2 .. T - 1 sets as 16-kmer
     variant words (one substitution a word; DNA's 42 kmers of a substitution
@@ -231,7 +232,7 @@ def test_grouped_rare_tier_exact(ctx, opts, c3_like, c4_like, data, walk):
     n = len(seqs)
     opts(variant=0, rare_group=1, variant_short=0 if walk == "wave" else None,
          variant_c16=0 if walk == "short_c32" else None, variant_split=3 if walk == "short_split" else None,
-         bitset_mfma_store=1 if walk == "store" else None)
+         bitset_mfma_store=1 if walk == "store" else None, variant_pack_keyless=0 if walk == "own_words" else None)
     kind, k = (gdist.KmerType.PROT, 8) if data == "protein" else (gdist.KmerType.DNA, 21)
     sets = gdist.KmerSets.from_sequences(seqs, k, kind, 0, ctx)
     sets.build_bitsets()
@@ -254,6 +255,32 @@ def test_grouped_rare_tier_exact(ctx, opts, c3_like, c4_like, data, walk):
     d = sets.row_query(600, cols)
     _, eD = oracle.matrix(off, codes, 600, 601, 0, n)
     assert bits_equal(d, eD[0, cols])
+
+
+def test_grouped_rare_tier_keyless(ctx, opts, c3_like):
+    """Without locus keys (no guide sequences: option guides 0) every rare
+    kmer is keyless. A probing grouped build (the default choice; option
+    rare_group 2) then keeps the two tiers; a forced one (rare_group 1) gives
+    each keyless kmer a word of its own instead of packing unrelated kmers
+    into one list. Both equal the oracle."""
+    import gdist
+    seqs, off, codes = c3_like
+    n = len(seqs)
+    eI, eD = oracle.matrix(off, codes, 0, n, 0, n, flags=0x100, nthreads=8)
+    iu = np.triu_indices(n, 1)
+    for rg in (2, 1):
+        opts(variant=None, rare_group=rg, guides=0)
+        sets = gdist.KmerSets.from_sequences(seqs, 8, gdist.KmerType.PROT, 0, ctx)
+        sets.build_bitsets()
+        vk, vw, ve, _ = sets.variant_info()
+        thr, lists, _ = sets.rare_info()
+        if rg == 2:
+            assert vk == 0 and lists > 0 and thr > 2, (vk, thr, lists)
+        else:
+            assert vk > 0 and vw == vk and lists == 0, ("a word each", vk, vw, lists)
+        I, D = sets.matrix(upper=True, method=gdist.METHOD_BITSET)
+        assert np.array_equal(I[iu], eI[iu]), (rg, np.flatnonzero(I[iu] != eI[iu])[:5])
+        assert bits_equal(D[iu], eD[iu]), rg
 
 
 def test_grouped_rare_walk_across_column_chunks(ctx, opts):
