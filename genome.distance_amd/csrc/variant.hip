@@ -1459,9 +1459,11 @@ void variant_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1,
     }
     // few rows: slice each row's entries over several workgroups
     // (option variant_split: a given number of slices a row)
+    // (~16 workgroups a CU over few rows: the C4 slice's 1,024 rows in 4
+    // slices, walk alone 7.35 vs 7.5 ms with 2, 8.2 with 1; profiles/r05/s35)
     const int nsplit = ctx->has_option(OPT_VARIANT_SPLIT)
                            ? (int)std::max<int64_t>(1, std::min<int64_t>(64, ctx->option(OPT_VARIANT_SPLIT, 1)))
-                           : (int)std::max<int64_t>(1, std::min<int64_t>(64, ceil_div((int64_t)ctx->cus * 8, units)));
+                           : (int)std::max<int64_t>(1, std::min<int64_t>(64, ceil_div((int64_t)ctx->cus * 16, units)));
     const int64_t grid = units * nsplit;
     GD_REQUIRE(grid < (int64_t(1) << 31), "variant-tier grid too large");
     FamilyTimer ft(ctx, GDIST_KERNEL_VARIANT, rs);
