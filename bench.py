@@ -398,7 +398,7 @@ def main():
     e2e_s = max_over_ranks(pack_s + represent_s + one_pass_s)
     first_call_s = max_over_ranks(first_call_s) if first_call_s is not None else None
 
-    verified = verify_sample(cfg, method, N, r0, r1, dI, dD, max_over_ranks)
+    verified = verify_sample(cfg, method, N, r0, r1, dI, dD, max_over_ranks, step=step)
     out = None
     if rank == 0:
         # ---------------------------------------------------------------- roofline
@@ -710,11 +710,14 @@ def _kmer_codes(seq: bytes, k: int, protein: bool) -> np.ndarray:
     return np.unique(np.concatenate([windows(sym), windows(rc)]))
 
 
-def verify_sample(cfg, method, N, r0, r1, dI, dD, max_over_ranks, npairs=4):
+def verify_sample(cfg, method, N, r0, r1, dI, dD, max_over_ranks, npairs=4, step=None):
     """Recount |A∩B| and the distance of a few pairs of this rank's row block
     from regenerated genomes and compare them bit-exactly with the device
-    output of the last step; every rank checks its own rows (so the
-    multi-GPU exchange is covered) and the verdict is the MIN over ranks."""
+    output of a step; every rank checks its own rows (so the multi-GPU
+    exchange is covered) and the verdict is the MIN over ranks. The sampled
+    pairs' outputs are poisoned (I = -7, D = 42.5) and one more step (the
+    timed loop's replayed graph) runs before they are read back (VERDICT r5
+    item 1): a replay that skipped a kernel family would show."""
     if method == "sketch":
         return None
     from gdist import synth
@@ -726,6 +729,12 @@ def verify_sample(cfg, method, N, r0, r1, dI, dD, max_over_ranks, npairs=4):
                 cand.append((i, j))
     cand = cand[:npairs]
     ok, cache = 1.0, {}
+    if step is not None:
+        for (i, j) in cand:
+            o = (i - r0) * N + j
+            dI.from_host(np.array([-7], np.int32), o)
+            dD.from_host(np.array([42.5]), o)
+        step()
 
     def codes(g):
         if g not in cache:
@@ -749,8 +758,9 @@ def verify_sample(cfg, method, N, r0, r1, dI, dD, max_over_ranks, npairs=4):
             log(f"verify: pair ({i},{j}) device I={gi} D={gd[0]!r}, recount I={inter} D={d!r}")
             ok = 0.0
     ok = max_over_ranks(-ok) * -1.0          # MIN over ranks
-    return {"pairs_per_rank": len(cand), "ok": bool(ok == 1.0),
-            "how": "independent numpy recount from regenerated genomes, bit-exact I and fp64 D"}
+    return {"pairs_per_rank": len(cand), "ok": bool(ok == 1.0), "poisoned": step is not None,
+            "how": "independent numpy recount from regenerated genomes, bit-exact I and fp64 D, "
+                   "read after a replayed step into outputs poisoned at the sampled pairs"}
 
 
 def host_cpus() -> dict:

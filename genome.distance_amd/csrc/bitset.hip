@@ -2697,9 +2697,14 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     // after the dense launch). Off by default: the tiles alone gain (C3 0.71
     // vs 0.76 ms) but the step loses its overlap (C3 1.81 vs 1.67 ms, C4
     // slice span 16.9 vs 14.8 ms; profiles/r05/s26)
+    // (only the raw 16-word kernel has the storing form: mstore with another
+    // stage layout would give up the overlap without the stores)
     const int64_t tWm = s->sparse ? s->Wd : s->W;
-    const bool mstore = p.nmt > 0 && !s->sparse && ctx->option(OPT_BITSET_MFMA_STORE, 0) != 0 &&
-                        mfma_min_splits(tWm / (ctx->option(OPT_BITSET_MFMA_RAW, 1) != 0 ? 16 : 4), 16) == 1;
+    const bool mraw = ctx->option(OPT_BITSET_MFMA_RAW, 1) != 0;
+    const bool mkm2 = ctx->option(OPT_BITSET_MFMA_KM, 4) == 2;
+    const int mkm = mraw ? (mkm2 ? 8 : 16) : mkm2 ? 2 : 4;     // words a stage (below)
+    const bool mstore = p.nmt > 0 && !s->sparse && mraw && !mkm2 && ctx->option(OPT_BITSET_MFMA_STORE, 0) != 0 &&
+                        mfma_min_splits(tWm / mkm, mkm) == 1;
     const bool dense_first = side && (mstore || (!serial && ctx->option(OPT_DENSE_FIRST, s->sparse ? 0 : 1) != 0));
     if (side && !mstore) GD_HIP(hipEventRecord(ctx->ev_fork, st));
     auto launch_side = [&]() {
@@ -2746,10 +2751,9 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
             // option bitset_mfma_raw (default 1): stages of the bitsets
             // themselves, 16 words a stage, expanded in registers; 0: the FP4
             // nibble operand (KM = 4 or 2 words a stage)
-            const bool raw = ctx->option(OPT_BITSET_MFMA_RAW, 1) != 0;
-            const bool km2 = ctx->option(OPT_BITSET_MFMA_KM, 4) == 2;
+            const bool raw = mraw, km2 = mkm2;
             // words a stage: raw 16 (8 with bitset_mfma_km 2), nibbles 4 (2)
-            const int km = raw ? (km2 ? 8 : 16) : km2 ? 2 : 4;
+            const int km = mkm;
             const int64_t nst = tW / km;
             // (~2 rounds when side-stream families run beside the tiles: C3's
             // 820 tiles unsplit, step 1.61 vs 1.67 ms with 2 splits, the walk

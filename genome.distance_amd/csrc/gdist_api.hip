@@ -925,8 +925,9 @@ static int resolve_method(gdist_ctx* ctx, gdist_sets* s, int method, double pair
         bool want = !s->bits.p && !s->auto_sorted && !s->segoff.p && s->has_codes && sorted_cost_s(s, pairs) >= 0.02;
         // a gathered collection's build is collective (split by rank): every
         // rank builds when any rank's region asks for it
-        if (s->replicated && comm_active(ctx) && ctx->option(OPT_SPLIT_BUILD, -1) != 0 && !s->bits.p && s->has_codes)
-            want = comm_any(ctx, want);
+        const bool collective =
+            s->replicated && comm_active(ctx) && ctx->option(OPT_SPLIT_BUILD, -1) != 0 && !s->bits.p && s->has_codes;
+        if (collective) want = comm_any(ctx, want);
         if (want) {
             try {
                 build_bitsets(ctx, s, 0);
@@ -937,7 +938,18 @@ static int resolve_method(gdist_ctx* ctx, gdist_sets* s, int method, double pair
                 free_bitsets(s);
                 gdist::cache_trim(ctx->device);
             }
-            if (!s->bits.p || bitset_cost_s(s, pairs) > sorted_cost_s(s, pairs)) {
+            bool keep = s->bits.p && bitset_cost_s(s, pairs) <= sorted_cost_s(s, pairs);
+            if (collective) {
+                // one verdict for every rank: the estimates differ
+                // per rank (each prices its own region) and an ENOMEM strikes
+                // one rank, so a per-rank verdict would leave some ranks with
+                // the bits and the next collective build (AUTO or BITSET)
+                // entered by the others only. Keep them when every rank holds
+                // them and some rank's region prefers them (the build is paid).
+                const bool missing = comm_any(ctx, !s->bits.p);
+                keep = !missing && comm_any(ctx, keep);
+            }
+            if (!keep) {
                 free_bitsets(s);
                 s->auto_sorted = true;
             }

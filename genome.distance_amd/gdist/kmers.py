@@ -224,10 +224,13 @@ class DeviceBuffer:
                                        n * dt.itemsize))
         return out
 
-    def from_host(self, a: np.ndarray):
+    def from_host(self, a: np.ndarray, offset: int = 0):
+        """Copy `a` into the buffer from element `offset` (in a's dtype) on."""
         a = np.ascontiguousarray(a)
-        assert a.nbytes <= self.nbytes
-        L.check(L.lib.gdist_memcpy_h2d(self.ctx.h, self.ptr, a.ctypes.data, a.nbytes))
+        at = int(offset) * a.itemsize
+        if offset < 0 or at + a.nbytes > self.nbytes:
+            raise ValueError("write outside the device buffer")
+        L.check(L.lib.gdist_memcpy_h2d(self.ctx.h, self.ptr + at, a.ctypes.data, a.nbytes))
 
     def free(self):
         if self.ptr:

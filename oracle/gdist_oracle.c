@@ -60,9 +60,40 @@ static int cmp_i32(const void* a, const void* b) {
     return (x > y) - (x < y);
 }
 
+/* LSD radix sort of u64 keys, 8 bits a pass; passes whose byte is the same
+ * in every key are skipped (DNA k=21 codes: 6 of 8). Any correct sort gives
+ * the same set; this one only makes the checker's full-size columns fast
+ * (qsort's comparator calls were ~10 ms a 200 K-kmer genome). */
+static void radix_sort_u64(uint64_t* v, int64_t n) {
+    /* the scratch is per thread and kept (a fresh 1.6 MB block a call is an
+     * mmap + page faults, serialised across the checker's threads) */
+    static __thread uint64_t* tmp = NULL;
+    static __thread int64_t cap = 0;
+    if (n > cap) {
+        free(tmp);
+        cap = n + n / 4;
+        tmp = (uint64_t*)malloc((size_t)cap * sizeof(uint64_t));
+        if (!tmp) { cap = 0; qsort(v, (size_t)n, sizeof(uint64_t), cmp_u64); return; }
+    }
+    uint64_t* src = v;
+    uint64_t* dst = tmp;
+    for (int sh = 0; sh < 64; sh += 8) {
+        int64_t cnt[256];
+        memset(cnt, 0, sizeof(cnt));
+        for (int64_t i = 0; i < n; i++) cnt[(src[i] >> sh) & 255]++;
+        if (cnt[(src[0] >> sh) & 255] == n) continue;     /* one byte value: nothing moves */
+        int64_t sum = 0;
+        for (int b = 0; b < 256; b++) { int64_t c = cnt[b]; cnt[b] = sum; sum += c; }
+        for (int64_t i = 0; i < n; i++) dst[cnt[(src[i] >> sh) & 255]++] = src[i];
+        uint64_t* t = src; src = dst; dst = t;
+    }
+    if (src != v) memcpy(v, src, (size_t)n * sizeof(uint64_t));
+}
+
 static int64_t sort_unique(uint64_t* v, int64_t n) {
     if (n <= 1) return n;
-    qsort(v, (size_t)n, sizeof(uint64_t), cmp_u64);
+    if (n >= 4096) radix_sort_u64(v, n);
+    else qsort(v, (size_t)n, sizeof(uint64_t), cmp_u64);
     int64_t w = 1;
     for (int64_t i = 1; i < n; i++)
         if (v[i] != v[w - 1]) v[w++] = v[i];
@@ -326,6 +357,46 @@ void or_matrix(const int64_t* off, const uint64_t* codes,
         }
     }
     (void)nthreads;
+}
+
+/* Rows of a collection too large to pack on the host (C4: 100,000 x 100 kbp
+ * = 160 GB of codes) against every column: column j's codes are extracted
+ * from blob[coff[j], coff[j+1]) by or_kmer_codes, counted (sizes[j]) and
+ * intersected with each of the nrows row sets (CSR roff / rcodes), OpenMP
+ * over columns; inter[r * ncols + j]. Returns 0, or -1 on unencodable
+ * input. The pair loop of FastaDistanceProcessor.java:157-186 for a few
+ * rows, the columns streamed. */
+int or_rows_vs_columns(int kind, int k, unsigned flags, const char* blob, const int64_t* coff, int64_t ncols,
+                       const int64_t* roff, const uint64_t* rcodes, int64_t nrows, int64_t* inter,
+                       int64_t* sizes, int nthreads) {
+    int bad = 0;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel
+#endif
+    {
+        int64_t cap = 0;
+        uint64_t* buf = NULL;
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 16)
+#endif
+        for (int64_t j = 0; j < ncols; j++) {
+            const int64_t len = coff[j + 1] - coff[j];
+            if (2 * len + 1 > cap) {
+                free(buf);
+                cap = 2 * len + 1;
+                buf = (uint64_t*)malloc((size_t)cap * sizeof(uint64_t));
+            }
+            const int64_t nb = buf ? or_kmer_codes(kind, k, flags, blob + coff[j], len, buf) : -1;
+            if (nb < 0) { bad = 1; continue; }
+            sizes[j] = nb;
+            for (int64_t r = 0; r < nrows; r++)
+                inter[r * ncols + j] = or_intersect(rcodes + roff[r], roff[r + 1] - roff[r], buf, nb);
+        }
+        free(buf);
+    }
+    (void)nthreads;
+    return bad ? -1 : 0;
 }
 
 /* ------------------------------------------------------------------ */

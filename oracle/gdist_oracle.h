@@ -56,6 +56,13 @@ void or_matrix(const int64_t* off, const uint64_t* codes,
                int64_t r0, int64_t r1, int64_t c0, int64_t c1, unsigned flags,
                int32_t* I_out, double* D_out, int64_t ld, int nthreads);
 
+/* A few row sets against every column of a byte collection, the columns'
+ * codes extracted on the fly (a collection too large to pack on the host):
+ * inter[r * ncols + j] = |row r ∩ codes(column j)|, sizes[j] = |codes(j)|. */
+int or_rows_vs_columns(int kind, int k, unsigned flags, const char* blob, const int64_t* coff, int64_t ncols,
+                       const int64_t* roff, const uint64_t* rcodes, int64_t nrows, int64_t* inter,
+                       int64_t* sizes, int nthreads);
+
 /* Java-faithful CPU path: HashSet<String> kmer sets (String.hashCode,
  * HashMap spreading/resizing) and the FastaDistanceProcessor loop
  * (FastaDistanceProcessor.java:141-194): batches of `batch` cached sets,

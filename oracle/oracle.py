@@ -47,6 +47,9 @@ def lib():
         L.or_matrix.restype = None
         L.or_matrix.argtypes = [i64p, u64p, i64, i64, i64, i64, C.c_uint,
                                 C.POINTER(C.c_int32), C.POINTER(C.c_double), i64, C.c_int]
+        L.or_rows_vs_columns.restype = C.c_int
+        L.or_rows_vs_columns.argtypes = [C.c_int, C.c_int, C.c_uint, C.c_void_p, i64p, i64, i64p, u64p, i64,
+                                         i64p, i64p, C.c_int]
         L.or_faithful_fasta_dist.restype = i64
         L.or_faithful_fasta_dist.argtypes = [C.c_int, C.c_int, C.c_uint, C.c_char_p, i64p, i64,
                                              C.c_int, i64, C.POINTER(C.c_double), C.c_int]
@@ -64,6 +67,27 @@ def kmer_codes(seq: bytes, k: int, kind: int = 0, flags: int = 0) -> np.ndarray:
     if n < 0:
         raise ValueError("unencodable sequence for this kmer spec")
     return out[:n].copy()
+
+
+def rows_vs_columns(blob, coff: np.ndarray, row_codes: list[np.ndarray], k: int, kind: int = 0,
+                    flags: int = 0, nthreads: int = 0):
+    """(inter[len(row_codes), ncols], sizes[ncols]): each row set against the
+    codes of every column blob[coff[j]:coff[j+1]], extracted on the fly (C,
+    OpenMP over columns) — for a collection too large to pack on the host."""
+    buf = np.frombuffer(blob, dtype=np.uint8) if not isinstance(blob, np.ndarray) else blob
+    coff = np.ascontiguousarray(coff, np.int64)
+    ncols = len(coff) - 1
+    roff = np.zeros(len(row_codes) + 1, np.int64)
+    roff[1:] = np.cumsum([len(r) for r in row_codes])
+    rc = np.ascontiguousarray(np.concatenate(row_codes) if row_codes else np.zeros(1), np.uint64)
+    inter = np.zeros((len(row_codes), ncols), np.int64)
+    sizes = np.zeros(ncols, np.int64)
+    rc_ = lib().or_rows_vs_columns(kind, k, flags, buf.ctypes.data, _p(coff, C.c_int64), ncols,
+                                   _p(roff, C.c_int64), _p(rc, C.c_uint64), len(row_codes),
+                                   _p(inter, C.c_int64), _p(sizes, C.c_int64), nthreads)
+    if rc_ != 0:
+        raise ValueError("unencodable sequence for this kmer spec")
+    return inter, sizes
 
 
 def pack(seqs: list[bytes], k: int, kind: int = 0, flags: int = 0):

@@ -19,7 +19,6 @@ intersected with the three row sets — bit-exact counts and fp64 distances.
 Progress lines go to stdout and to gpurun_out/c4_worker.log (a long run that
 keeps writing is not taken for a hung one).
 """
-import concurrent.futures as cf
 import os
 import sys
 import time
@@ -107,18 +106,17 @@ def main():
     row_codes = [oracle.kmer_codes(bytes(blob[off[i]:off[i + 1]]), K, 0, 0) for i in row_ids]
     assert [len(c) for c in row_codes] == [int(sizes[i]) for i in row_ids]
 
-    def column(j):
-        cj = oracle.kmer_codes(bytes(blob[off[j]:off[j + 1]]), K, 0, 0)
-        return len(cj), [oracle.intersect(rc, cj) for rc in row_codes]
-
+    # every column's codes extracted and intersected in the oracle's C loop
+    # (threaded over columns), 10,000 columns a call so that progress shows
     eI = np.zeros((len(row_ids), N), np.int64)
     nb = np.zeros(N, np.int64)
-    with cf.ThreadPoolExecutor(threads()) as ex:
-        for j0 in range(0, N, 10_000):
-            for j, (n_j, inter) in zip(range(j0, min(N, j0 + 10_000)), ex.map(column, range(j0, min(N, j0 + 10_000)))):
-                nb[j] = n_j
-                eI[:, j] = inter
-            log(f"oracle columns {min(N, j0 + 10_000)} / {N}")
+    for j0 in range(0, N, 10_000):
+        j1 = min(N, j0 + 10_000)
+        part, sz = oracle.rows_vs_columns(blob[off[j0]:off[j1]], off[j0:j1 + 1] - off[j0], row_codes, K, 0, 0,
+                                          nthreads=threads())
+        eI[:, j0:j1] = part
+        nb[j0:j1] = sz
+        log(f"oracle columns {j1} / {N}")
     assert np.array_equal(nb, sizes)
     for r, i in enumerate(row_ids):
         I, D = rows[i]

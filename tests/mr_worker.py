@@ -33,7 +33,7 @@ CASES = {
     "base": dict(n=301, L=6000, p=0.01, cfg=11, legs=("bitset", "sorted", "sketch", "reps")),
     "sparse": dict(n=300, L=150_000, p=0.002, cfg=12, legs=("bitset",), sparse=True),
     "c4": dict(n=200, L=100_000, p=0.05, cfg=4,
-               legs=("auto", "sorted", "codes_plan", "codes_variant", "codes_two_tier")),
+               legs=("auto", "auto_gathered", "sorted", "codes_plan", "codes_variant", "codes_two_tier")),
 }
 SKETCH_W = 200
 REPS_T = 0.35
@@ -61,6 +61,24 @@ def run_case(name, c, ctx, rank, world):
             gs = local.allgather()
             assert len(gs) == n
             results[leg] = gs.matrix((r0, r1), (0, n), upper=True, method=gdist.METHOD_SORTED)
+        elif leg == "auto_gathered":
+            # METHOD_AUTO on a replicated code collection: its build
+            # is collective, and each rank prices its own region, so rank 0
+            # asks for the whole triangle and the others for a handful of
+            # pairs — the per-rank estimates disagree, the keep/free verdict
+            # must not. Called twice: a rank left without the bits would enter
+            # the next collective build alone (a hang, not a wrong count).
+            gs = local.allgather()
+            pairs = 0.5 * n * (n - 1) if rank == 0 else float(rank)
+            m1, _, _ = gs.prepare(gdist.METHOD_AUTO, pairs)
+            m2, _, _ = gs.prepare(gdist.METHOD_AUTO, pairs)
+            info["auto_methods"] = (m1, m2)
+            results[leg] = gs.matrix((r0, r1), (0, n), upper=True, method=gdist.METHOD_AUTO)
+            I2, D2 = gs.matrix((r0, r1), (0, n), upper=True, method=gdist.METHOD_AUTO)
+            assert np.array_equal(I2, results[leg][0]), rank
+            # a BITSET call after AUTO: the collective build (if AUTO freed the
+            # bits) is entered by every rank or by none
+            results["auto_then_bitset"] = gs.matrix((r0, r1), (0, n), upper=True, method=gdist.METHOD_BITSET)
         elif leg == "codes_plan":
             m, bb, bc = local.exchange_plan()
             assert m == gdist.METHOD_BITSET, (m, bb, bc)            # small: the dictionary exchange fits
@@ -169,6 +187,9 @@ def run_case(name, c, ctx, rank, world):
                 cand = [(sD[i, r], r) for r in reps if sD[i, r] < 1.0]
                 best = min(cand) if cand else (1.0, -1)
                 assert rep_d[i] == best[0] and rep_of[i] == best[1], (name, i, rep_of[i], rep_d[i], best)
+    if "auto_gathered" in c["legs"]:
+        am = [g[3]["auto_methods"] for g in gathered]
+        assert all(x == am[0] and x[0] == x[1] for x in am), (name, "ranks disagree on AUTO's method", am)
     rows = 0
     for (a, b, res, inf) in gathered:
         up = np.fromfunction(lambda x, y: y > (a + x), (b - a, n))

@@ -828,6 +828,10 @@ SPARSE_MODES = {
     # the pack's and the dictionary's radix sorts in 10-bit onesweep passes
     "sort_radix10": {"sort_radix": 10},
     "many_chunks": {"sparse_zmax": 100000, "sparse_chunks": 37},
+    # the off-diagonal 2 x 2 walk unpipelined (option sparse_pipe 0; round 6
+    # pipelines it: the next step's records read before this step's adds)
+    "pipe_off": {"sparse_zmax": 100000, "sparse_pipe": 0},
+    "pipe_sun2": {"sparse_zmax": 100000, "sparse_sun": 2, "sparse_chunks": 5},
     # chunk c of every tile on XCD c mod 8 (option sparse_xcd), with a chunk
     # count that leaves empty workgroups in the last group of 8, and atomics
     "xcd": {"sparse_zmax": 100000, "sparse_xcd": 1, "sparse_chunks": 13},
@@ -840,6 +844,22 @@ SPARSE_MODES = {
 }
 
 
+_SPARSE_CASE = {}
+
+
+def sparse_case():
+    """The sweep's collection (300 x 20 kbp, p 0.003, seed 105) with the
+    oracle's whole N x N matrix, computed once: the settings below share it
+    (the oracle's matrices were most of each setting's time)."""
+    if not _SPARSE_CASE:
+        n = 300
+        seqs = synth_sets(n, 20000, 0.003, 105)
+        off, codes = oracle_pack(seqs, 21, 0, 0)
+        eI, eD = oracle.matrix(off, codes, 0, n, 0, n, flags=0, nthreads=8)
+        _SPARSE_CASE.update(n=n, seqs=seqs, eI=eI, eD=eD)
+    return _SPARSE_CASE
+
+
 @pytest.mark.parametrize("mode", list(SPARSE_MODES))
 def test_sparse_complement_words_exact(ctx, mode, opts):
     """The dense tier in locus order with complement-sparse words: counts and
@@ -850,8 +870,8 @@ def test_sparse_complement_words_exact(ctx, mode, opts):
     import gdist
     settings = SPARSE_MODES
     opts(**settings.get(mode, {}))
-    n = 300
-    seqs = synth_sets(n, 20000, 0.003, 105)
+    case = sparse_case()
+    n, seqs, fI, fD = case["n"], case["seqs"], case["eI"], case["eD"]
     sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
     _, W = sets.build_bitsets()
     ws, wd, ent = sets.sparse_info()
@@ -865,11 +885,10 @@ def test_sparse_complement_words_exact(ctx, mode, opts):
     elif mode == "two_sided":
         cw, pw = sets.sparse_sides()
         assert ws > 0 and cw > 0 and pw > 0 and cw + pw == ws
-    off, codes = oracle_pack(seqs, 21, 0, 0)
     for (r0, r1, c0, c1, up) in [(0, n, 0, n, True), (0, n, 0, n, False), (37, 211, 5, 290, False),
                                  (130, 259, 0, n, True), (299, 300, 0, n, False)]:
         I, D = sets.matrix((r0, r1), (c0, c1), upper=up, method=gdist.METHOD_BITSET)
-        eI, eD = oracle.matrix(off, codes, r0, r1, c0, c1, flags=0x100 if up else 0)
+        eI, eD = fI[r0:r1, c0:c1], fD[r0:r1, c0:c1]
         if up:
             mask = np.fromfunction(lambda a, b: (c0 + b) > (r0 + a), (r1 - r0, c1 - c0))
             I, D, eI, eD = I[mask], D[mask], eI[mask], eD[mask]
@@ -877,8 +896,7 @@ def test_sparse_complement_words_exact(ctx, mode, opts):
         assert bits_equal(D, eD)
     cols = [4, 299, 0, 150, 150]
     d = sets.row_query(150, cols)
-    _, eD = oracle.matrix(off, codes, 150, 151, 0, n)
-    assert bits_equal(d, eD[0, cols])
+    assert bits_equal(d, fD[150, cols])
 
 
 def test_sparse_equals_dense_at_size(ctx, opts):

@@ -14,6 +14,7 @@ import numpy as np
 import pytest
 
 import oracle
+import refcache
 
 pytestmark = pytest.mark.gpu
 
@@ -72,7 +73,7 @@ def test_variant_tier_exact(ctx, opts, c4_like, mode):
         assert (vk, vw, ve) == (0, 0, 0)
     for (r0, r1, c0, c1, up) in REGIONS:
         I, D = sets.matrix((r0, r1), (c0, c1), upper=up, method=gdist.METHOD_BITSET)
-        eI, eD = oracle.matrix(off, codes, r0, r1, c0, c1, flags=0x100 if up else 0, nthreads=8)
+        eI, eD = refcache.matrix(off, codes, r0, r1, c0, c1, flags=0x100 if up else 0, nthreads=8)
         if up:
             mask = np.fromfunction(lambda a, b: (c0 + b) > (r0 + a), (r1 - r0, c1 - c0))
             I, D, eI, eD = I[mask], D[mask], eI[mask], eD[mask]
@@ -80,7 +81,7 @@ def test_variant_tier_exact(ctx, opts, c4_like, mode):
         assert bits_equal(D, eD)
     cols = [4, n - 1, 0, 600, 600, 17]
     d = sets.row_query(600, cols)
-    _, eD = oracle.matrix(off, codes, 600, 601, 0, n)
+    _, eD = refcache.matrix(off, codes, 600, 601, 0, n)
     assert bits_equal(d, eD[0, cols])
 
 
@@ -97,7 +98,7 @@ def test_rebuild_drops_variant_tier(ctx, opts, c4_like):
     sets.build_bitsets()
     assert sets.variant_info()[0] > 0
     r0, r1 = 300, 700
-    eI, eD = oracle.matrix(off, codes, r0, r1, 0, n, flags=0x100, nthreads=8)
+    eI, eD = refcache.matrix(off, codes, r0, r1, 0, n, flags=0x100, nthreads=8)
     mask = np.fromfunction(lambda a, b: b > (r0 + a), (r1 - r0, n))
 
     def check(tag):
@@ -105,7 +106,7 @@ def test_rebuild_drops_variant_tier(ctx, opts, c4_like):
         assert np.array_equal(I[mask], eI[mask]), (tag, np.flatnonzero(I[mask] != eI[mask])[:5])
         assert bits_equal(D[mask], eD[mask]), tag
         d = sets.row_query(500, [0, 17, n - 1, 500])
-        assert bits_equal(d, oracle.matrix(off, codes, 500, 501, 0, n)[1][0, [0, 17, n - 1, 500]]), tag
+        assert bits_equal(d, refcache.matrix(off, codes, 500, 501, 0, n)[1][0, [0, 17, n - 1, 500]]), tag
 
     check("variant")
     opts(variant=0)
@@ -136,7 +137,7 @@ def test_variant_tier_replayed_steps(ctx, opts, c4_like):
     sets.build_bitsets()
     assert sets.variant_info()[0] > 0
     r0, r1 = 100, 400
-    eI, eD = oracle.matrix(off, codes, r0, r1, 0, n, flags=0x100, nthreads=8)
+    eI, eD = refcache.matrix(off, codes, r0, r1, 0, n, flags=0x100, nthreads=8)
     nr = r1 - r0
     dI, dD = ctx.alloc(nr * n * 4), ctx.alloc(nr * n * 8)
     mask = np.fromfunction(lambda a, b: b > (r0 + a), (nr, n))
@@ -147,6 +148,65 @@ def test_variant_tier_replayed_steps(ctx, opts, c4_like):
         assert np.array_equal(I[mask], eI[mask]) and bits_equal(D[mask], eD[mask]), call
     dI.free()
     dD.free()
+
+
+POISON_CASES = {
+    # the grouped rare tier (variant_short_kernel) beside the raw-stage MFMA
+    # tiles (c4_like's ~125 dense words >= 64): 16-bit counters, one slice a row
+    "grouped_dna": ("c4", dict(variant=0, rare_group=1)),
+    # ... 32-bit counters, two slices a row
+    "grouped_dna_c32_split2": ("c4", dict(variant=0, rare_group=1, variant_c16=0, variant_split=2)),
+    # C3's shape (protein k=8): the short walk beside the AND + popcount tiles
+    "grouped_protein": ("c3", dict(variant=0, rare_group=1)),
+    # C4's variant walk (variant_rows_kernel, 8-byte members) + MFMA tiles +
+    # the row-major rare walk in LDS column chunks ...
+    "variant": ("c4", dict(variant=1, rare_t=3, variant_dmin=120)),
+    # ... or by rare_rows_direct_kernel (atomics into I)
+    "variant_direct": ("c4", dict(variant=1, rare_t=3, variant_dmin=120, rare_direct=1)),
+}
+
+
+@pytest.mark.parametrize("case", list(POISON_CASES))
+def test_replayed_steps_poisoned(ctx, opts, c3_like, c4_like, case):
+    """repeated device-output calls over one region (the
+    first runs uncaptured and builds the plans, the second is captured, the
+    rest replay the hipGraph) into outputs POISONED before every call (I =
+    -7, D = 42.5): a replayed graph that dropped a kernel family's launch, or
+    the zeroing, would leave poison or miss that family's counts. Every call
+    equals the oracle over the region's upper triangle
+    (FastaDistanceProcessor.java:177-186: each row block's pairs)."""
+    import gdist
+    data, o = POISON_CASES[case]
+    seqs, off, codes = c3_like if data == "c3" else c4_like
+    kind, k = (gdist.KmerType.PROT, 8) if data == "c3" else (gdist.KmerType.DNA, 21)
+    n = len(seqs)
+    opts(**o)
+    sets = gdist.KmerSets.from_sequences(seqs, k, kind, 0, ctx)
+    sets.build_bitsets()
+    vk, vw, ve, _ = sets.variant_info()
+    assert vk > 0 and ve > 0, (case, vk, ve)
+    if case.startswith("grouped"):
+        assert sets.variant_layout()[:2] == (16, 4) and sets.rare_info()[1] == 0, case
+    else:
+        assert sets.variant_layout()[:2] == (47, 8) and sets.rare_info()[1] > 0, case
+    if data == "c4":
+        assert sets.bitset_info()[1] >= 64, "the dense tiles run on the matrix cores"
+    for (r0, r1) in [(0, n), (100, 400)]:
+        nr = r1 - r0
+        eI, eD = refcache.matrix(off, codes, r0, r1, 0, n, flags=0x100)
+        mask = np.fromfunction(lambda a, b: b > (r0 + a), (nr, n))
+        dI, dD = ctx.alloc(nr * n * 4), ctx.alloc(nr * n * 8)
+        pI, pD = np.full(nr * n, -7, np.int32), np.full(nr * n, 42.5)
+        for call in range(4):
+            dI.from_host(pI)
+            dD.from_host(pD)
+            sets.matrix_device(dI.ptr, dD.ptr, n, (r0, r1), (0, n), upper=True, method=gdist.METHOD_BITSET)
+            I = dI.to_host(np.int32).reshape(nr, n)
+            D = dD.to_host(np.float64).reshape(nr, n)
+            assert np.array_equal(I[mask], eI[mask]), (case, r0, call, np.flatnonzero(I[mask] != eI[mask])[:5])
+            assert bits_equal(D[mask], eD[mask]), (case, r0, call)
+        dI.free()
+        dD.free()
 
 
 def test_variant_greedy_reps(ctx, opts, c4_like):
@@ -245,7 +305,7 @@ def test_grouped_rare_tier_exact(ctx, opts, c3_like, c4_like, data, walk):
     for (r0, r1, c0, c1, up) in [(0, n, 0, n, True), (37, 211, 5, n - 10, False), (n // 2, n, 0, n, True),
                                  (n - 1, n, 0, n, False)]:
         I, D = sets.matrix((r0, r1), (c0, c1), upper=up, method=gdist.METHOD_BITSET)
-        eI, eD = oracle.matrix(off, codes, r0, r1, c0, c1, flags=0x100 if up else 0, nthreads=8)
+        eI, eD = refcache.matrix(off, codes, r0, r1, c0, c1, flags=0x100 if up else 0, nthreads=8)
         if up:
             mask = np.fromfunction(lambda a, b: (c0 + b) > (r0 + a), (r1 - r0, c1 - c0))
             I, D, eI, eD = I[mask], D[mask], eI[mask], eD[mask]
@@ -253,7 +313,7 @@ def test_grouped_rare_tier_exact(ctx, opts, c3_like, c4_like, data, walk):
         assert bits_equal(D, eD)
     cols = [4, n - 1, 0, 600, 600, 17]
     d = sets.row_query(600, cols)
-    _, eD = oracle.matrix(off, codes, 600, 601, 0, n)
+    _, eD = refcache.matrix(off, codes, 600, 601, 0, n)
     assert bits_equal(d, eD[0, cols])
 
 
@@ -266,7 +326,7 @@ def test_grouped_rare_tier_keyless(ctx, opts, c3_like):
     import gdist
     seqs, off, codes = c3_like
     n = len(seqs)
-    eI, eD = oracle.matrix(off, codes, 0, n, 0, n, flags=0x100, nthreads=8)
+    eI, eD = refcache.matrix(off, codes, 0, n, 0, n, flags=0x100, nthreads=8)
     iu = np.triu_indices(n, 1)
     for rg in (2, 1):
         opts(variant=None, rare_group=rg, guides=0)
@@ -336,7 +396,7 @@ def test_split_build_equals_whole_build(ctx, opts, c4_like, mode):
     assert np.array_equal(b0, b3) and v0 == v3 and r0_ == r3, (mode, v0, v3, r0_, r3)
     for (a, b, c0, c1, up) in REGIONS[:2]:
         I, D = s3.matrix((a, b), (c0, c1), upper=up, method=gdist.METHOD_BITSET)
-        eI, eD = oracle.matrix(off, codes, a, b, c0, c1, flags=0x100 if up else 0, nthreads=8)
+        eI, eD = refcache.matrix(off, codes, a, b, c0, c1, flags=0x100 if up else 0, nthreads=8)
         if up:
             mask = np.fromfunction(lambda x, y: (c0 + y) > (a + x), (b - a, c1 - c0))
             I, D, eI, eD = I[mask], D[mask], eI[mask], eD[mask]
@@ -359,7 +419,7 @@ def test_release_codes(ctx, opts, c4_like):
     sets.build_bitsets()
     sets.release_codes()
     I, D = sets.matrix((0, 50), (0, n), upper=True, method=gdist.METHOD_AUTO)
-    eI, eD = oracle.matrix(off, codes, 0, 50, 0, n, flags=0x100, nthreads=8)
+    eI, eD = refcache.matrix(off, codes, 0, 50, 0, n, flags=0x100, nthreads=8)
     mask = np.fromfunction(lambda a, b: b > a, (50, n))
     assert np.array_equal(I[mask], eI[mask]) and bits_equal(D[mask], eD[mask])
     for call in (lambda: sets.matrix((0, 5), (0, n), method=gdist.METHOD_SORTED),
