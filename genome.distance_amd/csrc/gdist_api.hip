@@ -602,12 +602,18 @@ int gdist_sets_append(gdist_ctx* ctx, gdist_sets* sets, const char* seqs, const 
             pack_sets(ctx, sets->kind, sets->k, sets->flags, dseq.as<char>(), doff.as<int64_t>(), h, &add, seqs + base);
         }
         // every representation derived from the old sets is stale (dictionary,
-        // tiers, plans, captured steps, the sorted join's segment index, the
-        // pack summaries the dictionary merges)
+        // tiers, plans, captured steps, the pack summaries the dictionary
+        // merges) — except the sorted join's segment index, which is extended
+        // below with the new sets' rows (round 6)
         free_bitsets(sets);
-        sets->segoff.release();
-        sets->nseg = 0;
-        sets->max_seg = 0;
+        const int64_t n_old = sets->nsets;
+        const bool extend_seg = sets->segoff.p && sets->nseg >= 1 && (sets->nseg == 1 || sets->seg_split.p);
+        if (!extend_seg) {
+            sets->segoff.release();
+            sets->seg_split.release();
+            sets->nseg = 0;
+            sets->max_seg = 0;
+        }
         sets->auto_sorted = false;
         sets->pack_sum.clear();
         sets->replicated = false;             // this rank's sets only from here
@@ -637,6 +643,7 @@ int gdist_sets_append(gdist_ctx* ctx, gdist_sets* sets, const char* seqs, const 
             sets->guide_keys = std::move(add.guide_keys);
             sets->n_guide = add.n_guide;
         }
+        if (extend_seg) extend_segments(ctx, sets, n_old);
         GD_HIP(hipStreamSynchronize(st));
     });
 }
@@ -756,6 +763,7 @@ int gdist_sets_release_codes(gdist_sets* s) {
         GD_HIP(hipStreamSynchronize(s->ctx->stream));
         s->codes.release();
         s->segoff.release();
+        s->seg_split.release();
         s->nseg = 0;
         s->max_seg = 0;
         s->pack_sum.clear();

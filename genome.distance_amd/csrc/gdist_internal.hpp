@@ -352,6 +352,7 @@ struct gdist_sets {
     bool bits_keep_singletons = false;
     // segment index of the sorted path
     gdist::DevBuf segoff;                 // int64 [nsets][nseg+1]
+    gdist::DevBuf seg_split;              // its nseg - 1 splitters (kept: appended sets are indexed by them)
     int nseg = 0;
     int64_t max_seg = 0;
     bool has_codes = true;                // false for all-gathered bitset-only collections
@@ -660,6 +661,8 @@ void range_summary(gdist_ctx* ctx, const gdist_sets* s, int min_count, Summary& 
 
 // sorted.hip
 void build_segments(gdist_ctx* ctx, gdist_sets* s);
+// the segment index rows of sets [n_old, nsets) appended to an indexed collection (same splitters)
+void extend_segments(gdist_ctx* ctx, gdist_sets* s, int64_t n_old);
 void sorted_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0,
                    int64_t c1, bool upper, int32_t* d_I, int64_t ldI);
 void sorted_row(gdist_ctx* ctx, const gdist_sets* s, int64_t q, const int64_t* d_cols, int64_t ncols,

@@ -210,6 +210,33 @@ void build_segments(gdist_ctx* ctx, gdist_sets* s) {
         for (int t = 0; t < nseg; t++) mx = std::max(mx, h[e * (nseg + 1) + t + 1] - h[e * (nseg + 1) + t]);
     s->nseg = nseg;
     s->max_seg = mx;
+    s->seg_split = std::move(dsplit);
+}
+
+// Sets appended to an indexed collection (gdist_sets_append: the Java
+// methods drop-in's genome cache, one genome at a time) get their rows with
+// the collection's splitters; the old rows stay valid (they hold code
+// positions, which an append does not move). ADVICE r5: rebuilding the whole
+// index after every append cost O(genomes x total codes) over a pair list.
+// The splitters were sampled from the old sets only: any splitters give an
+// exact join, they only set how evenly the segments split.
+void extend_segments(gdist_ctx* ctx, gdist_sets* s, int64_t n_old) {
+    hipStream_t st = ctx->stream;
+    const int nseg = s->nseg;
+    const int64_t per = nseg + 1, nadd = s->nsets - n_old;
+    if (nadd <= 0) return;
+    DevBuf grown((size_t)(s->nsets * per) * 8 + 8, st);
+    if (n_old) GD_HIP(hipMemcpyAsync(grown.p, s->segoff.p, (size_t)(n_old * per) * 8, hipMemcpyDeviceToDevice, st));
+    segoff_kernel<<<(int)ceil_div(nadd * per, 256), 256, 0, st>>>(
+        s->codes.as<uint64_t>(), s->off.as<int64_t>() + n_old, nadd, s->seg_split.as<uint64_t>(), nseg,
+        grown.as<int64_t>() + n_old * per);
+    GD_HIP(hipGetLastError());
+    std::vector<int64_t> h(nadd * per);
+    d2h(h.data(), grown.as<int64_t>() + n_old * per, nadd * per * 8, st);
+    GD_HIP(hipStreamSynchronize(st));
+    for (int64_t e = 0; e < nadd; e++)
+        for (int t = 0; t < nseg; t++) s->max_seg = std::max(s->max_seg, h[e * per + t + 1] - h[e * per + t]);
+    s->segoff = std::move(grown);
 }
 
 static void launch_join(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, int64_t c0, int64_t c1,

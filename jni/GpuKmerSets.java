@@ -37,6 +37,7 @@ public final class GpuKmerSets implements AutoCloseable {
     static native long nSketch(long ctx, long sets, int width);
     static native long nTotal(long sets);
     static native void nSketchDownload(long sk, long[] off, int[] sigs);
+    static native long nSketchUpload(long ctx, int width, long[] off, int[] sigs);
     static native void nSketchMatrix(long ctx, long sk, long r0, long r1, long c0, long c1, int flags,
                                      double[] out, int ld);
 
@@ -120,6 +121,18 @@ public final class GpuKmerSets implements AutoCloseable {
      *  (WidthProcessor.java:183-185), row-major with stride ld */
     public void sketchDistances(long r0, long r1, long c0, long c1, boolean upperTriangle, double[] out, int ld) {
         nSketchMatrix(ctx, handle, r0, r1, c0, c1, upperTriangle ? UPPER_TRIANGLE : 0, out, ld);
+    }
+
+    /** a sketch collection of given signatures (each ascending; Sketch.getSignature
+     *  of a Bucket's sketches, TuningProcessor.java:114-131), width = the sketch size */
+    public static GpuKmerSets fromSignatures(Context ctx, int width, int[][] sigs) {
+        long[] off = new long[sigs.length + 1];
+        for (int i = 0; i < sigs.length; i++)
+            off[i + 1] = off[i] + sigs[i].length;
+        int[] all = new int[(int) off[sigs.length]];
+        for (int i = 0; i < sigs.length; i++)
+            System.arraycopy(sigs[i], 0, all, (int) off[i], sigs[i].length);
+        return new GpuKmerSets(ctx.h, nSketchUpload(ctx.h, width, off, all));
     }
 
     /** the signatures of a sketch collection (hashSet(width) of each set,

@@ -306,6 +306,40 @@ JNIEXPORT jlong JNICALL JFN(nSketch)(JNIEnv* env, jclass c, jlong ctx, jlong set
     return (jlong)(intptr_t)sk;
 }
 
+/* a sketch collection from signatures (Sketch.getSignature of each sketch of
+ * a Bucket, TuningProcessor.java:114-119): off[nsets + 1], sigs[off[nsets]],
+ * each signature ascending */
+JNIEXPORT jlong JNICALL JFN(nSketchUpload)(JNIEnv* env, jclass c, jlong ctx, jint width, jlongArray off,
+                                           jintArray sigs) {
+    const jsize n1 = (*env)->GetArrayLength(env, off);
+    if (n1 < 1) {
+        jclass e = (*env)->FindClass(env, "java/lang/IllegalArgumentException");
+        if (e) (*env)->ThrowNew(env, e, "off needs nsets + 1 entries");
+        return 0;
+    }
+    int64_t* o = malloc((size_t)n1 * sizeof(int64_t));
+    if (!o) { throw_oom(env); return 0; }
+    (*env)->GetLongArrayRegion(env, off, 0, n1, (jlong*)o);
+    if ((*env)->ExceptionCheck(env)) { free(o); return 0; }
+    const int64_t total = o[n1 - 1];
+    if (total < 0 || (*env)->GetArrayLength(env, sigs) < total) {
+        free(o);
+        jclass e = (*env)->FindClass(env, "java/lang/IllegalArgumentException");
+        if (e) (*env)->ThrowNew(env, e, "sigs shorter than off[nsets]");
+        return 0;
+    }
+    int32_t* v = malloc(((size_t)total + 1) * sizeof(int32_t));
+    if (!v) { free(o); throw_oom(env); return 0; }
+    (*env)->GetIntArrayRegion(env, sigs, 0, (jsize)total, (jint*)v);
+    if ((*env)->ExceptionCheck(env)) { free(o); free(v); return 0; }
+    gdist_sets* sk = NULL;
+    int rc = gdist_sketch_upload(CTX(ctx), width, (int64_t)n1 - 1, o, v, &sk);
+    free(o);
+    free(v);
+    if (rc) { throw_for(env, rc); return 0; }
+    return (jlong)(intptr_t)sk;
+}
+
 /* the total number of codes (hashes, for a sketch collection) */
 JNIEXPORT jlong JNICALL JFN(nTotal)(JNIEnv* env, jclass c, jlong sets) {
     int kind = 0, k = 0;

@@ -8,6 +8,7 @@ O=gpurun_out/r06s2
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest -x -v --timeout 600 --timeout-method thread --durations=30 -p no:cacheprovider \
     tests/test_gpu_variant.py tests/test_multirank_gpu.py "tests/test_gpu_parity.py::test_sparse_complement_words_exact" \
+    tests/test_jni_shim.py tests/test_gpu_parity.py::test_append_extends_segment_index \
     tests/test_gpu_fullsize.py::test_c3_full_size_auto_vs_oracle tests/test_gpu_fullsize.py::test_c4_full_size_slices_vs_oracle \
     > $O/tests.log 2>&1
 rc=$?; tail -3 $O/tests.log

@@ -95,6 +95,7 @@ static void JNICALL ReleaseStringUTFChars(JNIEnv* env, jstring s, const char* c)
 #define GDIST_COPY_(a, buf, start, len, T) memcpy(buf, (T*)(a)->data + (start), (size_t)(len) * sizeof(T))
 #define GDIST_COPY_const(a, buf, start, len, T) memcpy((T*)(a)->data + (start), buf, (size_t)(len) * sizeof(T))
 REGION(GetByteArrayRegion, K_BYTE, jbyte, )
+REGION(GetIntArrayRegion, K_INT, jint, )
 REGION(GetLongArrayRegion, K_LONG, jlong, )
 REGION(GetDoubleArrayRegion, K_DOUBLE, jdouble, )
 REGION(SetIntArrayRegion, K_INT, jint, const)
@@ -103,7 +104,8 @@ REGION(SetDoubleArrayRegion, K_DOUBLE, jdouble, const)
 
 static const struct JNINativeInterface_ g_table = {
     FindClass, ThrowNew, ExceptionCheck, DeleteLocalRef, GetArrayLength, GetObjectArrayElement,
-    GetStringUTFChars, ReleaseStringUTFChars, GetByteArrayRegion, GetLongArrayRegion, GetDoubleArrayRegion,
+    GetStringUTFChars, ReleaseStringUTFChars, GetByteArrayRegion, GetIntArrayRegion, GetLongArrayRegion,
+    GetDoubleArrayRegion,
     SetIntArrayRegion, SetLongArrayRegion, SetDoubleArrayRegion,
 };
 static JNIEnv g_env = &g_table;

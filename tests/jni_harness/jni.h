@@ -47,6 +47,7 @@ struct JNINativeInterface_ {
     const char* (JNICALL* GetStringUTFChars)(JNIEnv* env, jstring str, jboolean* isCopy);
     void (JNICALL* ReleaseStringUTFChars)(JNIEnv* env, jstring str, const char* chars);
     void (JNICALL* GetByteArrayRegion)(JNIEnv* env, jbyteArray array, jsize start, jsize len, jbyte* buf);
+    void (JNICALL* GetIntArrayRegion)(JNIEnv* env, jintArray array, jsize start, jsize len, jint* buf);
     void (JNICALL* GetLongArrayRegion)(JNIEnv* env, jlongArray array, jsize start, jsize len, jlong* buf);
     void (JNICALL* GetDoubleArrayRegion)(JNIEnv* env, jdoubleArray array, jsize start, jsize len, jdouble* buf);
     void (JNICALL* SetIntArrayRegion)(JNIEnv* env, jintArray array, jsize start, jsize len, const jint* buf);

@@ -1198,3 +1198,31 @@ def test_from_blob_equals_from_sequences(ctx):
         assert np.array_equal(s.sizes(), ref.sizes())
         I, D = s.matrix(method=gdist.METHOD_SORTED)
         assert np.array_equal(I, eI) and bits_equal(D, eD)
+
+
+def test_append_extends_segment_index(ctx):
+    """gdist_sets_append on a collection whose sorted-join segment index is
+    built (the Java methods drop-in's genome cache): the new sets' index rows
+    are added with the collection's splitters instead of rebuilding the index
+    (ADVICE r5), so sets larger than every old one (longer segments), an
+    empty one and one at a time all join exactly; the bitset path after the
+    appends agrees (GenomeProcessor.java:140, MethodTableProcessor.java:275)."""
+    import gdist
+    seqs = synth_sets(12, 6000, 0.03, 131)
+    extra = synth_sets(4, 30000, 0.03, 132) + [b""] + synth_sets(2, 3000, 0.05, 133)
+    sets = gdist.KmerSets.from_sequences(seqs[:8], 21, gdist.KmerType.DNA, 0, ctx)
+    sets.matrix(method=gdist.METHOD_SORTED)              # builds the segment index
+    have = list(seqs[:8])
+    for batch in ([seqs[8]], seqs[9:12], extra[:1], extra[1:5], extra[5:]):
+        first = sets.append(batch)
+        assert first == len(have)
+        have += batch
+        n = len(have)
+        off, codes = oracle_pack(have, 21, 0, 0)
+        eI, eD = oracle.matrix(off, codes, 0, n, 0, n)
+        I, D = sets.matrix(method=gdist.METHOD_SORTED)
+        assert np.array_equal(I, eI) and bits_equal(D, eD), n
+        d = sets.row_query(n - 1, list(range(n)))
+        assert bits_equal(d, eD[n - 1])
+    I, D = sets.matrix(method=gdist.METHOD_BITSET)
+    assert np.array_equal(I[np.triu_indices(len(have), 1)], eI[np.triu_indices(len(have), 1)])

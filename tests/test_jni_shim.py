@@ -212,14 +212,20 @@ def test_shim_on_device_vs_oracle(jvm):
 class _KmerMethodMirror:
     """jni/GpuKmerMethod.java + GpuMeasurer.java, statement for statement, over
     the shim's natives: setOf packs a genome the first time its id is seen
-    (nPack for the first, nAppend after), getMeasurer holds id1's set,
-    getDistance is one nRow of id1's set against id2's."""
+    (nPack for the first, nAppend after); getMeasurer restarts a full cache
+    (parameter cache=N) and holds id1's set; a measurer's first getDistance
+    takes id1's row against every cached genome (one nMatrix of one row) and
+    answers later pairs from it, asking again only for a genome appended
+    after the row was taken."""
 
-    def __init__(self, jvm, ctx, k):
+    def __init__(self, jvm, ctx, k, cache_limit=4096):
         self.jvm, self.ctx, self.k = jvm, ctx, k
         self.cache = 0
         self.set_index = {}
         self.packs = 0
+        self.cache_limit = cache_limit
+        self.generation = 0
+        self.device_calls = 0
 
     def set_of(self, gid, seq):
         import ctypes as C
@@ -237,22 +243,56 @@ class _KmerMethodMirror:
             self.set_index[gid] = i
         return i
 
-    def distance(self, i, j):
+    def row(self, i):
+        """GpuKmerMethod.row: distances(i, i + 1, 0, n, false, d, n) -> nMatrix, METHOD_AUTO"""
         import ctypes as C
-        from jni_harness.harness import LONG, DOUBLE
-        d = self.jvm.zeros(DOUBLE, 1)
-        self.jvm.call("nRow", None, self.ctx, self.cache, i, C.c_void_p(self.jvm.array(LONG, [j])), C.c_void_p(d))
+        from jni_harness.harness import DOUBLE
+        n = self.jvm.call("nSize", C.c_int64, self.cache)
+        d = self.jvm.zeros(DOUBLE, max(n, 1))
+        self.jvm.call_i("nMatrix", None, [C.c_int64] * 6 + [C.c_int32, C.c_int32, C.c_void_p, C.c_int32],
+                        self.ctx, self.cache, i, i + 1, 0, n, 0, 0, d, n)
         assert self.jvm.exception() is None
-        return self.jvm.read(d, DOUBLE, 1)[0]
+        self.device_calls += 1
+        return self.jvm.read(d, DOUBLE, n)
+
+    def get_measurer(self, gid, seq):
+        if self.cache != 0 and len(self.set_index) >= self.cache_limit:
+            self.jvm.call("nFree", None, self.cache)
+            self.cache = 0
+            self.set_index.clear()
+            self.generation += 1
+        return _MeasurerMirror(self, gid, seq)
+
+
+class _MeasurerMirror:
+    def __init__(self, method, gid, seq):
+        self.method, self.gid, self.seq = method, gid, seq
+        self.set1 = method.set_of(gid, seq)
+        self.gen = method.generation
+        self.row = None
+
+    def distance_to(self, gid2, seq2):
+        if self.gen != self.method.generation:
+            self.set1 = self.method.set_of(self.gid, self.seq)
+            self.gen = self.method.generation
+            self.row = None
+        j = self.method.set_of(gid2, seq2)
+        if self.row is None or j >= len(self.row):
+            self.row = self.method.row(self.set1)
+        return self.row[j]
 
 
 @pytest.mark.gpu
-def test_java_measurer_packs_each_genome_once(jvm):
-    """the `methods` drop-in (GpuKmerMethod / GpuMeasurer)
-    driven as MethodTableProcessor drives it (pairs grouped by id1,
-    GenomePairList.prepare :240; getMeasurer per group :261-265; getDistance
-    per pair :275): every genome is packed exactly once (nPack / nAppend),
-    however many pairs name it, and every distance equals the oracle's."""
+@pytest.mark.parametrize("cache_limit", [4096, 8])
+def test_java_measurer_packs_each_genome_once(jvm, cache_limit):
+    """the `methods` drop-in (GpuKmerMethod /
+    GpuMeasurer) driven as MethodTableProcessor drives it (pairs grouped by
+    id1, GenomePairList.prepare :240; getMeasurer per group :261-265;
+    getDistance per pair :275): every genome is packed once (nPack / nAppend)
+    while the cache holds it, a group whose second genomes are all cached
+    costs ONE device call (its id1 row), and every distance equals the
+    oracle's. With a small cache bound the cache restarts between
+    groups and the distances stay exact."""
     import ctypes as C
     import random
     import oracle
@@ -263,19 +303,27 @@ def test_java_measurer_packs_each_genome_once(jvm):
     _, eD = oracle.matrix(off, codes, 0, n, 0, n)
     rng = random.Random(5)
     pairs = sorted({(rng.randrange(n), rng.randrange(n)) for _ in range(120)})   # grouped by id1
+    groups = len({a for a, _ in pairs})
     ctx = jvm.call_i("nCtxCreate", C.c_int64, [C.c_int32], 0)
-    m = _KmerMethodMirror(jvm, ctx, 21)
-    id1, set1 = None, None
-    seen = set()
-    for a, b in pairs:
-        if a != id1:                                    # a new first genome: getMeasurer
-            id1, set1 = a, m.set_of(f"g{a}", seqs[a])
-        seen.update((a, b))
-        d = m.distance(set1, m.set_of(f"g{b}", seqs[b]))
-        assert np.float64(d).view(np.uint64) == eD[a, b].view(np.uint64), (a, b, d, eD[a, b])
-    assert m.packs == len(seen)                         # once per genome
-    assert jvm.call("nSize", C.c_int64, m.cache) == len(seen)
-    jvm.call("nFree", None, m.cache)
+    m = _KmerMethodMirror(jvm, ctx, 21, cache_limit)
+    for rnd in range(2):                                # the second pass: every genome cached
+        calls0, packs0 = m.device_calls, m.packs
+        id1, meas = None, None
+        for a, b in pairs:
+            if a != id1:                                # a new first genome: getMeasurer
+                id1, meas = a, m.get_measurer(f"g{a}", seqs[a])
+            d = meas.distance_to(f"g{b}", seqs[b])
+            assert np.float64(d).view(np.uint64) == eD[a, b].view(np.uint64), (a, b, d, eD[a, b])
+        if cache_limit >= n:
+            if rnd == 0:
+                assert m.packs == len({x for p in pairs for x in p})          # once per genome
+            else:
+                assert m.packs == packs0 and m.device_calls - calls0 == groups, (m.device_calls - calls0, groups)
+        else:
+            assert m.generation > 0
+    if m.cache:
+        assert jvm.call("nSize", C.c_int64, m.cache) == len(m.set_index)
+        jvm.call("nFree", None, m.cache)
     jvm.call("nCtxDestroy", None, ctx)
     assert jvm.exception() is None
 
@@ -323,5 +371,62 @@ def test_java_genome_and_sketch_natives(jvm):
     assert jvm.exception() == ("java/lang/IllegalArgumentException", "off shorter than the number of sets + 1")
     for h in (sk, both, hc, hb):
         jvm.call("nFree", None, h)
+    jvm.call("nCtxDestroy", None, ctx)
+    assert jvm.exception() is None
+
+
+def test_sketch_upload_validates_arrays(jvm):
+    """nSketchUpload refuses an empty offsets array and signatures shorter than
+    off[nsets] before any library call (IllegalArgumentException)."""
+    import ctypes as C
+    from jni_harness.harness import LONG, INT
+    up = [C.c_int64, C.c_int32, C.c_void_p, C.c_void_p]
+    assert jvm.call_i("nSketchUpload", C.c_int64, up, 0, 10, jvm.zeros(LONG, 0), jvm.zeros(INT, 1)) == 0
+    assert jvm.exception() == ("java/lang/IllegalArgumentException", "off needs nsets + 1 entries")
+    assert jvm.call_i("nSketchUpload", C.c_int64, up, 0, 10, jvm.array(LONG, [0, 3, 5]), jvm.zeros(INT, 4)) == 0
+    assert jvm.exception() == ("java/lang/IllegalArgumentException", "sigs shorter than off[nsets]")
+
+
+@pytest.mark.gpu
+def test_java_tuning_close_counts(jvm):
+    """GpuTuningProcessor.closeCounts — the tune command's
+    pair count (TuningProcessor.java:125-139: for each sketch the later
+    sketches with distance < target) as one nSketchUpload of the Bucket's
+    signatures and upper-triangle nSketchMatrix row blocks, counted per row —
+    equals the reference loop restated over the oracle's Sketch.distance."""
+    import ctypes as C
+    import oracle
+    from gdist import synth
+    from jni_harness.harness import LONG, INT, DOUBLE
+    n, width, target = 60, 120, 0.7
+    prots = [bytes(r) for r in synth.genomes(n, 900, 0.25, 77, protein=True)]
+    off, codes = oracle.pack(prots, 8, 1, 0)
+    sigs = [oracle.sketch(codes[off[i]:off[i + 1]], 8, 1, width) for i in range(n)]
+    sigs[7] = sigs[7][:40]                                # a dwarf
+    # the restated reference loop
+    expected = [sum(1 for j in range(i + 1, n) if oracle.sketch_distance(sigs[i], sigs[j], width)[0] < target)
+                for i in range(n)]
+    assert sum(expected) > 0 and sum(1 for e in expected if e == 0) > 0
+    # closeCounts, statement for statement: width = the longest signature
+    w = max(len(s) for s in sigs)
+    so = np.zeros(n + 1, np.int64)
+    so[1:] = np.cumsum([len(s) for s in sigs])
+    ctx = jvm.call_i("nCtxCreate", C.c_int64, [C.c_int32], 0)
+    sk = jvm.call_i("nSketchUpload", C.c_int64, [C.c_int64, C.c_int32, C.c_void_p, C.c_void_p], ctx, w,
+                    jvm.array(LONG, so.tolist()), jvm.array(INT, [int(x) for s in sigs for x in s]))
+    assert jvm.exception() is None and sk
+    rows = 16                                             # ROW_BLOCK_CELLS / n, scaled down
+    got = [0] * n
+    d = jvm.zeros(DOUBLE, rows * n)
+    for r0 in range(0, n, rows):
+        r1 = min(n, r0 + rows)
+        jvm.call_i("nSketchMatrix", None, [C.c_int64] * 6 + [C.c_int32, C.c_void_p, C.c_int32],
+                   ctx, sk, r0, r1, 0, n, 0x100, d, n)
+        assert jvm.exception() is None
+        D = np.array(jvm.read(d, DOUBLE, rows * n)).reshape(rows, n)
+        for i in range(r0, r1):
+            got[i] = int(np.sum(D[i - r0, i + 1:] < target))
+    assert got == expected
+    jvm.call("nFree", None, sk)
     jvm.call("nCtxDestroy", None, ctx)
     assert jvm.exception() is None
