@@ -72,6 +72,12 @@ CONFIGS = {
     "c2r": dict(n=1000, length=2_000_000, p_max=0.002, protein=False, k=21, method="bitset", cfg=2, realistic=True,
                 desc="C2-realistic: 1000 synthetic ~2 Mbp genomes in 8 clades with short indels and segment "
                      "moves / inversions (gdist.synth.realistic_genome), DNA k=21 both strands, bitsets"),
+    "c3r": dict(n=10000, length=33_333, p_max=0.10, protein=True, k=8, method="auto", cfg=3, realistic=True,
+                desc="C3-realistic: 10000 synthetic ~33 kaa proteomes in 8 clades with short indels and segment "
+                     "moves (gdist.synth.realistic_genome, protein), protein k=8, METHOD_AUTO"),
+    "c4r": dict(n=100000, length=100_000, p_max=0.05, protein=False, k=21, method="auto", cfg=4, realistic=True,
+                desc="C4-realistic: 100000 synthetic ~100 kbp genomes in 8 clades with short indels and segment "
+                     "moves / inversions, DNA k=21 both strands, METHOD_AUTO (a one-GPU slice with --rows)"),
     "c3": dict(n=10000, length=33_333, p_max=0.10, protein=True, k=8, method="auto", cfg=3,
                desc="10000 synthetic 33,333-aa proteomes, protein k=8, sorted uint64 sets "
                     "(METHOD_AUTO: two-tier bitsets built from them, or the LDS hash-join)"),
@@ -177,7 +183,8 @@ def main():
     s0, s1 = shard.shard_of_sets(n_total, world)[rank]
     t = time.time()
     if cfg.get("realistic"):
-        rs = synth.realistic_genomes(s1 - s0, cfg["length"], cfg["p_max"], cfg["cfg"], first=s0)
+        rs = synth.realistic_genomes(s1 - s0, cfg["length"], cfg["p_max"], cfg["cfg"], first=s0,
+                                     protein=cfg["protein"])
         blob = b"".join(rs)
         off = np.zeros(len(rs) + 1, dtype=np.int64)
         off[1:] = np.cumsum([len(x) for x in rs])
@@ -423,14 +430,22 @@ def main():
                     pmc = json.load(f)
             except Exception:
                 return None
-            if pmc.get("config") == args.config and pmc.get("n") == N and pmc.get("kernel", "").startswith(kern):
+            pk = pmc.get("kernel", "")
+            ok = pk.replace(" ", "") == kern.replace(" ", "") if "<" in kern else pk.startswith(kern)
+            if pmc.get("config") == args.config and pmc.get("n") == N and ok:
                 return pmc
             return None
 
+        traffic_readings = {}
+
         def pmc_traffic(kern):
             """HBM bytes per launch of `kern` from the committed PMC passes
-            (profiles/pmc_<config>*.json: FETCH_SIZE x 2 + WRITE_SIZE), only a
-            summary taken on this kernel at this collection size."""
+            (profiles/pmc_<config>*.json: FETCH_SIZE x F + WRITE_SIZE), only a
+            summary taken on this kernel at this collection size — with a
+            template instantiation named (`kern` holding '<'), only one taken
+            on that instantiation. Both FETCH readings (x1: scattered record
+            loads, x2: the guide's streaming correction) are kept in
+            traffic_readings for the line."""
             import glob
             files = [args.pmc_json] if args.pmc_json else \
                 sorted(glob.glob(os.path.join(ROOT, "profiles", f"pmc_{args.config}*.json")))
@@ -440,8 +455,13 @@ def main():
                         pmc = json.load(f)
                 except Exception:
                     continue
-                if pmc.get("config") == args.config and pmc.get("n") == N and \
-                        pmc.get("kernel", "").startswith(kern):
+                pk = pmc.get("kernel", "")
+                ok = pk.split(" (")[0].replace(" ", "") == kern.replace(" ", "") if "<" in kern else pk.startswith(kern)
+                if pmc.get("config") == args.config and pmc.get("n") == N and ok:
+                    traffic_readings.update({"x1": pmc.get("hbm_bytes_x1"), "x2": pmc.get("hbm_bytes_x2"),
+                                             "used": pmc.get("correction", "").split(",")[0],
+                                             "kernel": pk.split(" (")[0],
+                                             "source": os.path.relpath(fn, ROOT)})
                     return pmc.get("hbm_bytes_per_launch")
             return None
 
@@ -457,8 +477,9 @@ def main():
             # for a whole diagonal tile.
             mt = options.get("sparse_mt", 2)
             sun = options.get("sparse_sun", 3 if mt == 2 else 4)
-            kname = (f"sparse_tile_kernel<{sun},{mt}> ({'2x2' if mt == 2 else '1x2'} micro-tiles, the dense words "
-                     "folded in, the rare rows trailing)")
+            kinst = f"sparse_tile_kernel<{sun}, {mt}>"
+            kname = (f"{kinst} ({'2x2' if mt == 2 else '1x2'} micro-tiles, the dense words folded in, the rare rows "
+                     "trailing)")
             nb = -(-N // 128)
             side = sparse["entries"] / nb * 9.0 + sparse["sparse_words"] * 16.0
             algo_sparse = 0.0
@@ -475,7 +496,7 @@ def main():
             # wave-instructions per launch (committed SQ pass) over the chip's
             # measured issue rate, against the live kernel time; per 64 of the
             # walk's products (sum over sparse words of z (z - 1) / 2)
-            sq = pmc_sq("sparse_tile_kernel")
+            sq = pmc_sq(kinst)
             valu_issue = None
             if sq and sparse.get("products"):
                 c = sq["counters_per_launch"]
@@ -492,7 +513,7 @@ def main():
                                   "counters_from": sq.get("kernel"), "source": sq.get("source")}
             dense_ops = pairs_rank * width_words * 4 / (k_avg_ms * 1e-3) / 1e12 if k_avg_ms > 0 else 0.0
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("sparse_tile_kernel"),
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(kinst),
                     "kernel": kname, "kernel_avg_ms": round(kms, 4), "step_kernel_span_ms": round(k_avg_ms, 4),
                     "algo_bytes_per_launch": round(algo_sparse),
                     "limiter": SPARSE_LIMITER,
@@ -644,7 +665,7 @@ def main():
                        "method": method, "auto": auto, "rare_tier": rare, "complement_sparse": sparse_words,
                        "variant_tier": variant,
                        "options": options or None},
-            "roofline": roof,
+            "roofline": dict(roof, traffic_readings=(traffic_readings or None)) if isinstance(roof, dict) else roof,
             "verified": verified,
             "cpu_baseline": cpu,
             "cpu_optimized": cpu_opt,
@@ -739,7 +760,7 @@ def verify_sample(cfg, method, N, r0, r1, dI, dD, max_over_ranks, npairs=4, step
     def codes(g):
         if g not in cache:
             if cfg.get("realistic"):
-                s = synth.realistic_genome(g, cfg["length"], cfg["p_max"], cfg["cfg"])
+                s = synth.realistic_genome(g, cfg["length"], cfg["p_max"], cfg["cfg"], protein=cfg["protein"])
             else:
                 s = bytes(synth.genomes(1, cfg["length"], cfg["p_max"], cfg["cfg"], protein=cfg["protein"],
                                         first=g)[0])
@@ -803,7 +824,7 @@ def cpu_baselines(cfg, threads, host=None, target_s=10.0, cap=6000, batch=20):
 
     def genomes(n):
         if cfg.get("realistic"):
-            return synth.realistic_genomes(n, cfg["length"], cfg["p_max"], cfg["cfg"])
+            return synth.realistic_genomes(n, cfg["length"], cfg["p_max"], cfg["cfg"], protein=cfg["protein"])
         return [bytes(r) for r in synth.genomes(n, cfg["length"], cfg["p_max"], cfg["cfg"], protein=cfg["protein"])]
 
     def faithful(n):

@@ -200,7 +200,6 @@ struct Timing {
     X(SPARSE_DYN, "sparse_dyn")               /* 1 (default): a tile workgroup's waves claim word batches in turn; 0: equal runs */ \
     X(SPARSE_DIAG22, "sparse_diag22")         /* 1 (default): diagonal tiles in 2 x 2 micro-tiles too (sparse_mt 2) */ \
     X(SPARSE_RPART22, "sparse_rpart22")       /* 1 (default): row-trimmed sparse tiles in 2 x 2 micro-tiles too */ \
-    X(SPARSE_PIPE, "sparse_pipe")             /* 1 (default): the off-diagonal 2 x 2 walk reads the next step's records before this step's counter adds */ \
     X(SPARSE_MT, "sparse_mt")                 /* off-diagonal micro-tiles: 1 (1 x 2) / 2 (2 x 2, default) */   \
     X(SKETCH_K, "sketch_k")                   /* sketch merge window (1 / 2 / 4 / 6, default 2) */             \
     X(SKETCH_TILE, "sketch_tile")             /* 16: force the 16x16 sketch tile */                            \

@@ -738,81 +738,6 @@ __device__ __forceinline__ void sparse_off22_slots(const int4* __restrict__ rec,
     }
 }
 
-// The off-diagonal 2 x 2 walk, pipelined (round 6, option sparse_pipe).
-// LDS completes in order, so in sparse_off22_slots a step's first LDS read
-// (its slots' walk records) waits behind the previous step's twelve counter
-// adds, and the scattered record loads cannot issue until that chain — adds
-// queued behind the other waves' bank-conflicting adds, the mask read, the
-// record read — has drained: one LDS round trip plus the adds' queue per step
-// on every wave's critical path (profiles/pmc_c2_sq.json: 0.58 of the LDS
-// cycles are conflict cycles). Here a step's record loads are issued first,
-// then the NEXT step's walk records are read and its addresses computed
-// while those loads are in flight, and only then are this step's products
-// added: the adds drain in the shadow of the next step's loads. The window's
-// last-slot masks sit in a register (lane g holds group g's mask; a step
-// reads its groups' masks with v_readlane), so a step has one LDS read.
-__device__ __forceinline__ unsigned long long group_mask(unsigned long long wm, int g) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)wm, g);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(wm >> 32), g);
-    return ((unsigned long long)hi << 32) | lo;
-}
-template <int SU>
-__device__ __forceinline__ void off22_addr(const int4* __restrict__ rec, unsigned long long wm, int W0, int last,
-                                           int fb, int lane, uint32_t* ri, uint32_t* ci) {
-    int4 r[SU];
-#pragma unroll
-    for (int u = 0; u < SU; u++) r[u] = rec[slot_rec(last, fb + 64 * u, group_mask(wm, ((fb - W0) >> 6) + u))];
-#pragma unroll
-    for (int u = 0; u < SU; u++) {
-        const int q2 = 2 * (fb + 64 * u) + 2 * lane + r[u].x;
-        const float rcp = __int_as_float(r[u].w);
-        const int xc = (int)__builtin_fmaf((float)q2, rcp, rcp);
-        const int yc2 = q2 - (int)__umul24((uint32_t)xc, (uint32_t)r[u].w & 0xFFu);
-        ri[u] = (uint32_t)r[u].y + ((uint32_t)xc << 5);
-        ci[u] = (uint32_t)r[u].z + ((uint32_t)yc2 << 4);
-    }
-}
-template <int SUN>
-__device__ __forceinline__ void sparse_off22_pipe(const int4* __restrict__ rec, unsigned long long wm, int W0,
-                                                  int last, int& fb, int wend, int lane, const SparseWalk& e,
-                                                  uint32_t* __restrict__ cnt) {
-    if (fb + 64 * SUN > wend) return;
-    uint32_t ri[SUN], ci[SUN];
-    off22_addr<SUN>(rec, wm, W0, last, fb, lane, ri, ci);
-    for (;;) {
-        uint4 a0[SUN];
-        Rec3 a1[SUN], b0[SUN], b1[SUN];
-#pragma unroll
-        for (int u = 0; u < SUN; u++) {
-            const char* pa = e.eA + ri[u];
-            const char* pb = e.eB + ci[u] + 4;
-            a0[u] = *reinterpret_cast<const uint4*>(pa);
-            a1[u] = *reinterpret_cast<const Rec3*>(pa + 16);
-            b0[u] = *reinterpret_cast<const Rec3*>(pb);
-            b1[u] = *reinterpret_cast<const Rec3*>(pb + 16);
-        }
-        fb += 64 * SUN;
-        const bool more = fb + 64 * SUN <= wend;          // uniform
-        // the next step's walk records: read before this step's adds enter the LDS queue
-        if (more) off22_addr<SUN>(rec, wm, W0, last, fb, lane, ri, ci);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int u = 0; u < SUN; u++) {
-            const uint32_t la = ~(uint32_t)__builtin_amdgcn_sbfe((int)a0[u].w, 5, 1);    // kLastOfList: bit 5
-            const uint32_t lb = ~(uint32_t)__builtin_amdgcn_sbfe((int)b0[u].c, 5, 1);
-            const uint32_t v00 = (uint32_t)(__popc(a0[u].y & b0[u].a) + __popc(a0[u].z & b0[u].b));
-            const uint32_t v01 = (uint32_t)(__popc(a0[u].y & b1[u].a) + __popc(a0[u].z & b1[u].b)) & lb;
-            const uint32_t v10 = (uint32_t)(__popc(a1[u].b & b0[u].a) + __popc(a1[u].c & b0[u].b)) & la;
-            const uint32_t v11 = (uint32_t)(__popc(a1[u].b & b1[u].a) + __popc(a1[u].c & b1[u].b)) & (la & lb);
-            cnt_add(cnt, a0[u].x, b0[u].c, v00);
-            cnt_add(cnt, a0[u].x, b1[u].c, v01);
-            cnt_add(cnt, a1[u].a, b0[u].c, v10);
-            cnt_add(cnt, a1[u].a, b1[u].c, v11);
-        }
-        if (!more) break;
-    }
-}
-
 // Diagonal tiles in 2 x 2 micro-tiles (with sparse_mt 2): the word's n
 // entries as m = ceil(n / 2) pairs; slot q is the pair of pairs (Y, X), Y <=
 // X, q = X (X + 1) / 2 + Y. X > Y: all four products are pairs y < x (the
@@ -893,20 +818,16 @@ __device__ __forceinline__ void sparse_walk(const int4* __restrict__ rec, unsign
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         const int wend = total < W0 + 64 * G ? total : W0 + 64 * G;
         int fb = W0;
-        if (MODE == 4) {                           // pipelined 2 x 2 (option sparse_pipe)
-            const unsigned long long wm = lane < G ? masks[lane] : 0ull;
-            sparse_off22_pipe<SUN>(rec, wm, W0, last, fb, wend, lane, e, cnt);
-        }
         for (; fb + 64 * SUN <= wend; fb += 64 * SUN) {
             if (MODE == 0) sparse_diag_slots<SUN>(rec, masks, W0, last, fb, lane, e, cnt, mirror);
             else if (MODE == 1) sparse_off_slots<SUN>(rec, masks, W0, last, fb, lane, e, cnt);
-            else if (MODE == 2 || MODE == 4) sparse_off22_slots<SUN>(rec, masks, W0, last, fb, lane, e, cnt);
+            else if (MODE == 2) sparse_off22_slots<SUN>(rec, masks, W0, last, fb, lane, e, cnt);
             else sparse_diag22_slots<SUN>(rec, masks, W0, last, fb, lane, e, cnt, mirror);
         }
         for (; fb < wend; fb += 64) {
             if (MODE == 0) sparse_diag_slots<1>(rec, masks, W0, last, fb, lane, e, cnt, mirror);
             else if (MODE == 1) sparse_off_slots<1>(rec, masks, W0, last, fb, lane, e, cnt);
-            else if (MODE == 2 || MODE == 4) sparse_off22_slots<1>(rec, masks, W0, last, fb, lane, e, cnt);
+            else if (MODE == 2) sparse_off22_slots<1>(rec, masks, W0, last, fb, lane, e, cnt);
             else sparse_diag22_slots<1>(rec, masks, W0, last, fb, lane, e, cnt, mirror);
         }
         __builtin_amdgcn_wave_barrier();
@@ -926,7 +847,6 @@ struct TileWalk {
     int rlo, rhi;
     bool rpart, diag, mirror, r22;
     bool d22;                             // diagonal tiles in 2 x 2 micro-tiles (MT 2, option sparse_diag22)
-    bool pipe;                            // off-diagonal 2 x 2 walk pipelined (option sparse_pipe)
 };
 
 // One batch of up to kBatchWords words [s0, we) walked over global memory
@@ -995,7 +915,6 @@ __device__ __forceinline__ void global_batch(const TileWalk& tc, int64_t s0, int
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     if (MT == 2 && diag && d22) sparse_walk<2, 3>(wrec, masks, last, total, lane, e, cnt, mirror);
     else if (diag) sparse_walk<SUN, 0>(wrec, masks, last, total, lane, e, cnt, mirror);
-    else if (MT == 2 && r22 && tc.pipe) sparse_walk<MT == 2 ? SUN : 1, 4>(wrec, masks, last, total, lane, e, cnt, false);
     else if (MT == 2 && r22) sparse_walk<MT == 2 ? SUN : 1, 2>(wrec, masks, last, total, lane, e, cnt, false);
     else sparse_walk<SUN, 1>(wrec, masks, last, total, lane, e, cnt, false);
 }
@@ -1006,7 +925,7 @@ __global__ __launch_bounds__(SNT, 8) void sparse_tile_kernel(
     int64_t Ws, const int2* __restrict__ tiles, const int32_t* __restrict__ cbnd, int nchunks, int64_t r0, int64_t r1,
     int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I, int64_t ldI, int32_t* __restrict__ part, int64_t Wdp,
     int64_t N, const unsigned long long* __restrict__ slab_bits, int slabs, GroupPart gp, int xmap, int ntiles,
-    RareSlab rs, int dyn, int diag22, int rpart22, int pipe) {
+    RareSlab rs, int dyn, int diag22, int rpart22) {
     // gp: the group tier's part of every pair, added with the constant part
     // slab_bits / slabs: the in-kernel fold's dense words (set-major [N][Wdp])
     __shared__ uint32_t cnt[SB * SB / 2];                  // 32 KiB, 16-bit counters (cnt_index layout)
@@ -1061,7 +980,7 @@ __global__ __launch_bounds__(SNT, 8) void sparse_tile_kernel(
     const uint32_t zA = (uint32_t)(ntot - ra0), zB = (uint32_t)(ntot - cb0);
     const TileWalk tc{offA, offB, ent, ra0, cb0, zA, zB,
                       SparseWalk{reinterpret_cast<const char*>(ent + ra0), reinterpret_cast<const char*>(ent + cb0)},
-                      rlo, rhi, rpart, diag, mirror, r22, diag22 != 0, pipe != 0};
+                      rlo, rhi, rpart, diag, mirror, r22, diag22 != 0};
     int4* wrec = &rec[wv][0];
     unsigned long long* masks = reinterpret_cast<unsigned long long*>(&rec[wv][kBatchWords + 1]);
     // the wave's share of the chunk's words, in batches of kBatchWords: an
@@ -1791,7 +1710,7 @@ bool sparse_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
                                          s->Wd, s->nsets, s->dbits.as<unsigned long long>(), s->sp_fold_slabs,
                                          group_part(s), xmap ? 1 : 0, (int)nt, rs,
                                          (int)ctx->option(OPT_SPARSE_DYN, 1), (int)ctx->option(OPT_SPARSE_DIAG22, 1),
-                                         (int)ctx->option(OPT_SPARSE_RPART22, 1), (int)ctx->option(OPT_SPARSE_PIPE, 1));
+                                         (int)ctx->option(OPT_SPARSE_RPART22, 1));
     GD_HIP(hipGetLastError());
     ft.end();
     if (sc.use_part) {

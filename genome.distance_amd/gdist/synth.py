@@ -4,7 +4,8 @@ PRNG: splitmix64, master seed 0x5EED_0000 + cfg, per-genome substream
 seed ^ (g * 0x9E3779B97F4A7C15). DNA: an ancestor i.i.d. uniform over ACGT;
 genome g is the ancestor with round(p_g * L) substitutions at splitmix
 positions, p_g = u_g * p_max. Protein: the same over the 20 standard amino
-acids. Fixed lengths (no indels).
+acids. Fixed lengths (no indels). realistic_genome(): clades, indels and segment
+moves over either alphabet (the C2 / C3 / C4 realistic twins).
 """
 from __future__ import annotations
 
@@ -72,27 +73,32 @@ for _a, _b in zip(b"ACGT", b"TGCA"):
 
 
 def realistic_genome(g: int, length: int, p_max: float, cfg: int, clades: int = 8, p_clade: float = 0.004,
-                     indel_rate: float = 2e-5, blocks: int = 16, p_rearrange: float = 0.5) -> bytes:
+                     indel_rate: float = 2e-5, blocks: int = 16, p_rearrange: float = 0.5,
+                     protein: bool = False) -> bytes:
     """Genome g of a collection that is NOT one ancestor plus independent
     substitutions (the structure the locus order was tuned on):
       * clades: the ancestor gets p_clade substitutions per clade (genome g
         belongs to clade g mod `clades`), so genomes share variants in groups
         and the first sequences (the guides) are ordinary clade members;
       * substitutions of its own at p_g ~ U[0, p_max];
-      * short indels (1-10 bp, rate indel_rate per site each way), so genome
+      * short indels (1-10 symbols, rate indel_rate per site each way), so
         lengths and kmer windows shift;
       * with probability p_rearrange, 1-3 moves of one of `blocks` equal
-        segments to another position, reverse-complemented half the time.
-    Deterministic per (cfg, g): splitmix64 substreams as genomes()."""
-    seed = master_seed(cfg) ^ 0x5EA1
+        segments to another position, DNA reverse-complemented half the time.
+    protein=True: the same over the 20 amino acids (a proteome; moved
+    segments are not reversed). Deterministic per (cfg, g, kind): splitmix64
+    substreams as genomes()."""
+    alpha = AA_ALPHA if protein else DNA_ALPHA
+    na = len(alpha)
+    seed = master_seed(cfg) ^ (0x5EA1 if not protein else 0x5EA2)
     c = g % clades
     with np.errstate(over="ignore"):
         sc = int(np.uint64(seed) ^ (np.uint64(0xC1ADE + c) * GOLDEN))
         sg = int(np.uint64(seed) ^ (np.uint64(g) * GOLDEN))
-    key = (seed, length)
+    key = (seed, length, na)
     if key not in _ANCESTORS:
         _ANCESTORS.clear()
-        _ANCESTORS[key] = (splitmix64(seed, length) % np.uint64(4)).astype(np.uint8)
+        _ANCESTORS[key] = (splitmix64(seed, length) % np.uint64(na)).astype(np.uint8)
     idx = _ANCESTORS[key].copy()
 
     def substitute(idx, s, m, start):
@@ -100,12 +106,12 @@ def realistic_genome(g: int, length: int, p_max: float, cfg: int, clades: int = 
             return
         x = splitmix64(s, 2 * m, start=start)
         pos = (x[:m] % np.uint64(len(idx))).astype(np.int64)
-        idx[pos] = (idx[pos] + (x[m:] % np.uint64(3)).astype(np.uint8) + 1) % 4
+        idx[pos] = (idx[pos] + (x[m:] % np.uint64(na - 1)).astype(np.uint8) + 1) % na
 
     substitute(idx, sc, int(round(p_clade * length)), 1)
     p = float(_uniform(splitmix64(sg, 1))[0]) * p_max
     substitute(idx, sg, int(round(p * length)), 1)
-    seq = DNA_ALPHA[idx]
+    seq = alpha[idx]
     # indels at distinct sorted positions: even events delete 1-10 bp, odd
     # events insert 1-10 random bp; assembled in one pass
     ne = int(round(indel_rate * length))
@@ -122,7 +128,7 @@ def realistic_genome(g: int, length: int, p_max: float, cfg: int, clades: int = 
             if k % 2 == 0:
                 at = q + ln                                   # deletion
             else:
-                pieces.append(DNA_ALPHA[(splitmix64(sg ^ 0x1D, ln, start=int(q)) % np.uint64(4)).astype(np.uint8)])
+                pieces.append(alpha[(splitmix64(sg ^ 0x1D, ln, start=int(q)) % np.uint64(na)).astype(np.uint8)])
                 at = q
         pieces.append(seq[at:])
         seq = np.concatenate(pieces)
@@ -134,7 +140,7 @@ def realistic_genome(g: int, length: int, p_max: float, cfg: int, clades: int = 
             a = int(r[2 + t] % np.uint64(len(segs)))
             b = int((r[2 + t] >> np.uint64(20)) % np.uint64(len(segs)))
             s = segs.pop(a)
-            if (r[2 + t] >> np.uint64(40)) & np.uint64(1):
+            if not protein and (r[2 + t] >> np.uint64(40)) & np.uint64(1):
                 s = _COMP[s[::-1]]
             segs.insert(b, s)
         seq = np.concatenate(segs)

@@ -14,11 +14,16 @@ import statistics
 import sys
 
 
+NAMES = set()
+
+
 def per_launch(d, counter, kern):
     vals = {}
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
             if kern in r["Kernel_Name"] and r["Counter_Name"] == counter:
+                kn = r["Kernel_Name"]
+                NAMES.add(kn[kn.index(kern):].split("(")[0].strip())
                 key = (r.get("Dispatch_Id") or r.get("Correlation_Id") or len(vals))
                 vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])
     return list(vals.values())
@@ -31,7 +36,10 @@ def main():
     fx = float(sys.argv[7]) if len(sys.argv) > 7 else 2.0
     f = statistics.median(per_launch(fd, "FETCH_SIZE", kern))
     w = statistics.median(per_launch(wd, "WRITE_SIZE", kern))
-    res = {"config": config, "n": n, "kernel": f"{kern} (per launch, median over the profiled launches)",
+    # the kernel's own (template) name when one instantiation ran, so that
+    # bench.py quotes the counters only beside the kernel they were taken on
+    kname = next(iter(NAMES)) if len(NAMES) == 1 else kern
+    res = {"config": config, "n": n, "kernel": f"{kname} (per launch, median over the profiled launches)",
            "fetch_size_kb": f, "write_size_kb": w,
            "correction": (f"FETCH_SIZE x{fx:g} + WRITE_SIZE, x1024 B/KB (x2: coalesced streaming reads, "
                           "MI355X_MICROARCH.md HBM section; x1: scattered record loads, "

@@ -828,10 +828,7 @@ SPARSE_MODES = {
     # the pack's and the dictionary's radix sorts in 10-bit onesweep passes
     "sort_radix10": {"sort_radix": 10},
     "many_chunks": {"sparse_zmax": 100000, "sparse_chunks": 37},
-    # the off-diagonal 2 x 2 walk unpipelined (option sparse_pipe 0; round 6
-    # pipelines it: the next step's records read before this step's adds)
-    "pipe_off": {"sparse_zmax": 100000, "sparse_pipe": 0},
-    "pipe_sun2": {"sparse_zmax": 100000, "sparse_sun": 2, "sparse_chunks": 5},
+    "mt2_sun2": {"sparse_zmax": 100000, "sparse_sun": 2, "sparse_chunks": 5},
     # chunk c of every tile on XCD c mod 8 (option sparse_xcd), with a chunk
     # count that leaves empty workgroups in the last group of 8, and atomics
     "xcd": {"sparse_zmax": 100000, "sparse_xcd": 1, "sparse_chunks": 13},

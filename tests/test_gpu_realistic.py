@@ -82,3 +82,68 @@ def test_realistic_group_tier_exact(ctx, opts, groups):
         opts(**mode)
         I2, _ = sets.matrix(upper=True, method=gdist.METHOD_BITSET)
         assert np.array_equal(I2[iu], eI[iu]), mode
+
+
+_TWINS = {}
+
+
+def _twin(kind):
+    """The realistic C3 / C4 twins at a size the oracle checks quickly, with
+    the oracle's whole matrix (tests/refcache.py): proteomes and 100 kbp-
+    shaped genomes in 8 clades with indels and segment moves."""
+    import refcache
+    from gdist import synth
+    if kind not in _TWINS:
+        if kind == "c3r":
+            seqs = synth.realistic_genomes(1500, 3000, 0.10, 45, protein=True, p_clade=0.01, indel_rate=2e-4)
+            off, codes = oracle.pack(seqs, 8, 1, 0)
+        else:
+            seqs = synth.realistic_genomes(1200, 4000, 0.03, 41, p_clade=0.004, indel_rate=2e-4)
+            off, codes = oracle.pack(seqs, 21, 0, 0)
+        _TWINS[kind] = (seqs, off, codes, refcache.full(off, codes))
+    return _TWINS[kind]
+
+
+@pytest.mark.parametrize("twin,mode", [("c3r", "auto"), ("c3r", "grouped"), ("c3r", "two_tier"),
+                                       ("c4r", "auto"), ("c4r", "variant"), ("c4r", "variant_direct")])
+def test_realistic_twins_exact(ctx, opts, twin, mode):
+    """C3's grouped rare tier (rare kmers as 16-kmer
+    variant words keyed by their substitution site) and C4's variant tier off
+    the star phylogeny — proteomes / genomes in clades, with indels (windows
+    shift, so fewer kmers have a keyed dense neighbour) and segment moves:
+    METHOD_AUTO's choice, the forced tiers and the two-tier fallback are all
+    bit-exact against the oracle over upper triangles, row blocks and
+    rectangles (GenomeProcessor.java:25-26, FastaDistanceProcessor.java:177-186)."""
+    import gdist
+    seqs, off, codes, (fI, fD) = _twin(twin)
+    n = len(seqs)
+    o = {"auto": {}, "grouped": dict(variant=0, rare_group=1), "two_tier": dict(variant=0, rare_group=0),
+         "variant": dict(variant=1, rare_t=3, variant_dmin=n // 10),
+         "variant_direct": dict(variant=1, rare_t=3, variant_dmin=n // 10, rare_direct=1)}[mode]
+    opts(**o)
+    kind, k = (gdist.KmerType.PROT, 8) if twin == "c3r" else (gdist.KmerType.DNA, 21)
+    assert len({len(s) for s in seqs}) > 1                    # indels: lengths differ
+    sets = gdist.KmerSets.from_sequences(seqs, k, kind, 0, ctx)
+    if mode == "auto":
+        m, cb, cs = sets.prepare(gdist.METHOD_AUTO)
+        method = gdist.METHOD_AUTO
+    else:                                                   # the tiers built whatever AUTO would price
+        sets.build_bitsets()
+        m, cb, cs = sets.prepare(gdist.METHOD_BITSET)
+        method = gdist.METHOD_BITSET
+    vk, vw, ve, _ = sets.variant_info()
+    print(f"{twin} {mode}: AUTO -> {m} (bitset {cb:.3g} s, sorted {cs:.3g} s), variant {vk} kmers "
+          f"{vw} words {ve} entries, rare {sets.rare_info()}")
+    if mode in ("grouped", "variant", "variant_direct"):
+        assert vk > 0 and ve > 0, (twin, mode, vk, ve)
+        assert vw < vk, ("kmers grouped into words", vk, vw)
+    if mode == "two_tier":
+        assert vk == 0
+    for (r0, r1, c0, c1, up) in [(0, n, 0, n, True), (100, 400, 0, n, True), (37, 211, 5, n - 10, False)]:
+        I, D = sets.matrix((r0, r1), (c0, c1), upper=up, method=method)
+        eI, eD = fI[r0:r1, c0:c1], fD[r0:r1, c0:c1]
+        if up:
+            mask = np.fromfunction(lambda a, b: (c0 + b) > (r0 + a), (r1 - r0, c1 - c0))
+            I, D, eI, eD = I[mask], D[mask], eI[mask], eD[mask]
+        assert np.array_equal(I, eI), (twin, mode, r0, r1, np.flatnonzero(I != eI)[:5])
+        assert bits_equal(D, eD), (twin, mode, r0, r1)
