@@ -249,6 +249,8 @@ struct Timing {
     X(VARIANT_SHORT, "variant_short")         /* packed variant entries: 1 (default) the lane-per-entry walk / 8-byte members, 0 the wave-per-entry walk over the 4 + 8-byte arrays */ \
     X(EPILOGUE_ROWS, "epilogue_rows")         /* distance epilogue: 1 (default) a block a row, 0 the flat kernel */ \
     X(VARIANT_PACK_KEYLESS, "variant_pack_keyless") /* 1 (default): keyless variant kmers packed a word-width at a time in code order; 0 a word each */ \
+    X(VARIANT_KEY2, "variant_key2")           /* 1 (default): second-level variant keys (a keyless kmer keyed by the pair of sites of its keyed variant neighbours); 0 first level only */ \
+    X(VARIANT_KEYLESS_RARE, "variant_keyless_rare") /* 1: keyless kmers of the 47 / 64-kmer variant tier as rare posting lists instead of packed words (default off) */ \
     X(VARIANT_BITS, "variant_bits")           /* kmers a variant word: 64 or 47 (default 47: < 2^17 sets, k x strands <= 47) */ \
     X(DENSE_FIRST, "dense_first")             /* the dense tiles issued before the side stream's launches (default: without sparse words) */ \
     X(REPS_SPLIT, "reps_split")               /* greedy reps of a gathered collection: 1 (default) columns sharded over the ranks, 0 every rank all */ \

@@ -183,15 +183,26 @@ struct CodeGeom {
 // site = the neighbour's window + the offset of the differing symbol
 // (reversed on the reverse strand, whose letter is complemented); ~0 when no
 // keyed neighbour exists.
+// (site << 8 | forward letter) of a kmer's symbol j when its window is the
+// guide entry e (window << 1 | strand for two strands)
+__device__ __forceinline__ uint64_t site_key(const CodeGeom& g, int64_t e, int j, uint64_t cur) {
+    const int64_t w = e / g.strands, strand = e % g.strands;
+    int64_t site;
+    uint64_t letter;
+    if (strand == 0) { site = w + j; letter = cur; }
+    else { site = w + (g.k - 1 - j); letter = (uint64_t)(g.comp[cur] < 0 ? cur : g.comp[cur]); }
+    return ((uint64_t)site << 8) | letter;
+}
 __global__ __launch_bounds__(256) void variant_key_kernel(const uint64_t* __restrict__ mcodes, int64_t Um,
                                                           const uint64_t* __restrict__ dcodes, int64_t Ud,
                                                           const int64_t* __restrict__ dentry, CodeGeom g,
-                                                          uint64_t* __restrict__ vkey) {
+                                                          uint64_t* __restrict__ vkey, int64_t* __restrict__ went) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     const uint64_t smask = (1ull << g.bits) - 1ull;
     for (int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; m < Um; m += stride) {
         const uint64_t c = mcodes[m];
         uint64_t best = ~0ull;
+        int64_t be = -1;
         for (int j = 0; j < g.k; j++) {
             const int sh = (g.k - 1 - j) * g.bits;          // symbol j (0 = first, most significant)
             const uint64_t cur = (c >> sh) & smask;
@@ -201,17 +212,59 @@ __global__ __launch_bounds__(256) void variant_key_kernel(const uint64_t* __rest
                 const uint64_t nb = (c & ~(smask << sh)) | (s << sh);
                 const int64_t r = lower_bound_u64(dcodes, 0, Ud, nb);
                 if (r >= Ud || dcodes[r] != nb || dentry[r] < 0) continue;
-                const int64_t e = dentry[r];
-                const int64_t w = e / g.strands, strand = e % g.strands;
-                int64_t site;
-                uint64_t letter;
-                if (strand == 0) { site = w + j; letter = cur; }
-                else { site = w + (g.k - 1 - j); letter = (uint64_t)(g.comp[cur] < 0 ? cur : g.comp[cur]); }
-                const uint64_t key = ((uint64_t)site << 8) | letter;
-                best = key < best ? key : best;
+                const uint64_t key = site_key(g, dentry[r], j, cur);
+                if (key < best) { best = key; be = dentry[r]; }
             }
         }
         vkey[m] = best;
+        if (went) went[m] = be;          // the window (guide entry) the key was read in
+    }
+}
+
+// Round 6: second-level keys of the keyless variant kmers (a substitution
+// inside a window that a first-level variant already changed: C4-realistic's
+// clade-specific kmers are held by ~7.5 K of 100 K genomes, below Dmin, so an
+// individual substitution next to a clade substitution has no dense
+// neighbour). Such a kmer x has keyed variant neighbours: y (x with the
+// individual substitution reverted; y's key is the clade site C, its window
+// known) and x' (the clade substitution reverted; key I). Through y, x's
+// differing symbol in y's window names I; through x', C — so the unordered
+// pair {C, I} keys every window that holds both substitutions, and they share
+// a word (their holders: one clade's genomes with that substitution). The
+// key is a 63-bit mix of the pair with the top bit set (first-level keys
+// have it clear; ~0 stays "keyless"); any grouping is exact.
+__device__ __forceinline__ uint64_t pair_key(uint64_t a, uint64_t b) {
+    const uint64_t lo = a < b ? a : b, hi = a < b ? b : a;
+    uint64_t z = lo * 0x9E3779B97F4A7C15ull ^ (hi + 0x632BE59BD9B4E019ull);
+    z ^= z >> 31; z *= 0xBF58476D1CE4E5B9ull; z ^= z >> 29; z *= 0x94D049BB133111EBull; z ^= z >> 32;
+    const uint64_t k = (1ull << 63) | (z >> 1);
+    return k == ~0ull ? k - 1 : k;
+}
+__global__ __launch_bounds__(256) void variant_key2_kernel(const uint64_t* __restrict__ mcodes, int64_t Um,
+                                                           const uint64_t* __restrict__ vkey,
+                                                           const int64_t* __restrict__ went, CodeGeom g,
+                                                           uint64_t* __restrict__ vkey2) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const uint64_t smask = (1ull << g.bits) - 1ull;
+    for (int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; m < Um; m += stride) {
+        uint64_t best = vkey[m];
+        if (best == ~0ull) {
+            const uint64_t c = mcodes[m];
+            for (int j = 0; j < g.k; j++) {
+                const int sh = (g.k - 1 - j) * g.bits;
+                const uint64_t cur = (c >> sh) & smask;
+                for (int a = 0; a < g.nalpha; a++) {
+                    const uint64_t s = g.alpha[a];
+                    if (s == cur) continue;
+                    const uint64_t nb = (c & ~(smask << sh)) | (s << sh);
+                    const int64_t r = lower_bound_u64(mcodes, 0, Um, nb);
+                    if (r >= Um || mcodes[r] != nb || went[r] < 0) continue;
+                    const uint64_t key = pair_key(vkey[r], site_key(g, went[r], j, cur));
+                    best = key < best ? key : best;
+                }
+            }
+        }
+        vkey2[m] = best;
     }
 }
 
@@ -842,6 +895,38 @@ __global__ void first_keyless_kernel(const uint64_t* __restrict__ k, int64_t n, 
     *out = lo;
 }
 
+// Keyless variant kmers routed to the rare tier (round 6, option
+// variant_keyless_rare): flag[idx[t]] = 1 for the routed variant indices
+__global__ void mark_idx_kernel(const int32_t* __restrict__ idx, int64_t n, int32_t* __restrict__ flag) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += stride) flag[idx[t]] = 1;
+}
+// g[i] = 1 for the dictionary codes that are routed variant kmers
+__global__ void routed_flags_kernel(const int32_t* __restrict__ fm, const int64_t* __restrict__ pm,
+                                    const int32_t* __restrict__ kl, int64_t U, int32_t* __restrict__ g) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < U; i += stride)
+        g[i] = fm[i] && kl[pm[i]] ? 1 : 0;
+}
+// the routed codes appended to the rare codes (ranks Ur + gp[i]) and their
+// holders counted (the rare records they will write): a sum per wave, one
+// atomic a wave
+__global__ __launch_bounds__(256) void routed_emit_kernel(const uint64_t* __restrict__ dict,
+                                                          const uint32_t* __restrict__ dcnt,
+                                                          const int32_t* __restrict__ g, const int64_t* __restrict__ gp,
+                                                          int64_t U, uint64_t* __restrict__ out,
+                                                          unsigned long long* __restrict__ msum) {
+    unsigned long long c = 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < U; i += stride)
+        if (g[i]) {
+            out[gp[i]] = dict[i];
+            c += dcnt[i];
+        }
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(msum, c);
+}
+
 __global__ void viota_kernel(int32_t* __restrict__ p, int64_t n) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = (int32_t)i;
@@ -1136,11 +1221,23 @@ bool build_variant_bitsets(gdist_ctx* ctx, gdist_sets* s, DevBuf& dict, DevBuf& 
             else
                 GD_HIP(hipMemsetAsync(dentry.p, 0xFF, Ud * 8, st));
         }
+        // option variant_key2 (round 6, default 1): second-level keys for the
+        // kmers the first level leaves keyless
+        const bool key2 = ctx->option(OPT_VARIANT_KEY2, 1) != 0;
+        DevBuf went(key2 ? Um * 8 + 8 : 8, st);
         variant_key_kernel<<<grid_for(Um, 256, 256 * 64), 256, 0, st>>>(mcodes.as<uint64_t>(), Um,
                                                                          dcodes.as<uint64_t>(), Ud,
                                                                          dentry.as<int64_t>(), code_geom(s),
-                                                                         vkey.as<uint64_t>());
+                                                                         key2 ? vkalt.as<uint64_t>() : vkey.as<uint64_t>(),
+                                                                         key2 ? went.as<int64_t>() : nullptr);
         GD_HIP(hipGetLastError());
+        if (key2) {
+            variant_key2_kernel<<<grid_for(Um, 256, 256 * 64), 256, 0, st>>>(mcodes.as<uint64_t>(), Um,
+                                                                              vkalt.as<uint64_t>(),
+                                                                              went.as<int64_t>(), code_geom(s),
+                                                                              vkey.as<uint64_t>());
+            GD_HIP(hipGetLastError());
+        }
         // iota values: the variant index; stable sort by key keeps code order within a group
         viota_kernel<<<grid_for(Um), 256, 0, st>>>(ord.as<int32_t>(), Um);
         uint64_t* k = vkey.as<uint64_t>(); uint64_t* ka = vkalt.as<uint64_t>();
@@ -1165,18 +1262,75 @@ bool build_variant_bitsets(gdist_ctx* ctx, gdist_sets* s, DevBuf& dict, DevBuf& 
                 return false;
             }
         }
-        DevBuf head(Um * 4 + 4, st), wn(Um * 8 + 8, st), wst(Um * 8 + 8, st);
-        group_words_kernel<<<grid_for(Um), 256, 0, st>>>(k, Um, wb, pack, head.as<int32_t>(), wn.as<int64_t>());
-        GD_HIP(hipGetLastError());
-        exclusive_scan_i64(ctx, wn.as<int64_t>(), wst.as<int64_t>(), (size_t)Um);
-        int64_t h[2];
-        d2h(&h[0], wst.as<int64_t>() + Um - 1, 8, st);
-        d2h(&h[1], wn.as<int64_t>() + Um - 1, 8, st);
-        vwords = h[0] + h[1];
-        GD_REQUIRE((double)vbase + (double)vwords * wb < 4294967295.0, "variant tier too large for u32 positions");
-        group_pos_kernel<<<grid_for(Um), 256, 0, st>>>(k, v, Um, wst.as<int64_t>(), wb, pack, vbase,
-                                                       mperm.as<uint32_t>());
-        GD_HIP(hipGetLastError());
+        // Round 6 (option variant_keyless_rare = 1): keyless kmers of the 47 /
+        // 64-kmer tier go to the rare posting lists instead of words, on the
+        // premise that they are segment-move junctions (~40 a junction, held
+        // by the same genomes that share the move): packed wb to a word in
+        // code order a word joins unrelated kmers and its list the union of
+        // their holders (C4-realistic slice: 855 M entries, 1.3e12 products,
+        // 61 ms a step). As posting lists kmers of one junction have identical
+        // holders and merge into one weighted list (option rare_dedup). Off
+        // by default: measured on the C4-realistic slice the routed kmers
+        // were not junctions but the clade-context substitutions the
+        // second-level keys now group (their lists barely merged: 7.7 M
+        // kmers in 3.7 M lists; the direct rare walk 52 ms, the step 76 vs
+        // 68.5 ms). The hash fill only: the windowed fill looks codes up in
+        // the sorted rare codes.
+        int64_t Ug = Um;
+        if (wb != 16) {
+            DevBuf fk(8, st);
+            first_keyless_kernel<<<1, 1, 0, st>>>(k, Um, fk.as<int64_t>());
+            GD_HIP(hipGetLastError());
+            int64_t first = Um;
+            d2h(&first, fk.p, 8, st);
+            const int64_t keyless = Um - first;
+            const int64_t kr = ctx->option(OPT_VARIANT_KEYLESS_RARE, -1);
+            const bool route = keyless > 0 && ctx->option(OPT_FILL_SORT, 0) != 3 && kr > 0;
+            if (ctx->trace())
+                fprintf(stderr, "gdist: variant tier: %lld of %lld kmers keyless%s\n", (long long)keyless,
+                        (long long)Um, route ? ", to the rare tier" : "");
+            if (route) {
+                DevBuf kl(Um * 4 + 4, st), g(U * 4 + 4, st), gp(U * 8 + 8, st), msum(8, st);
+                GD_HIP(hipMemsetAsync(kl.p, 0, Um * 4 + 4, st));
+                mark_idx_kernel<<<grid_for(keyless), 256, 0, st>>>(v + first, keyless, kl.as<int32_t>());
+                routed_flags_kernel<<<grid_for(U), 256, 0, st>>>(fm.as<int32_t>(), pm.as<int64_t>(), kl.as<int32_t>(),
+                                                                 U, g.as<int32_t>());
+                GD_HIP(hipGetLastError());
+                exclusive_scan_i32_to_i64(ctx, g.as<int32_t>(), gp.as<int64_t>(), (size_t)U);
+                DevBuf r2((Ur + keyless) * 8 + 8, st);
+                if (Ur) GD_HIP(hipMemcpyAsync(r2.p, rare.p, Ur * 8, hipMemcpyDeviceToDevice, st));
+                GD_HIP(hipMemsetAsync(msum.p, 0, 8, st));
+                routed_emit_kernel<<<grid_for(U), 256, 0, st>>>(dict.as<uint64_t>(), dcnt.as<uint32_t>(),
+                                                                g.as<int32_t>(), gp.as<int64_t>(), U,
+                                                                r2.as<uint64_t>() + Ur, msum.as<unsigned long long>());
+                GD_HIP(hipGetLastError());
+                unsigned long long hm = 0;
+                d2h(&hm, msum.p, 8, st);
+                GD_HIP(hipStreamSynchronize(st));
+                rare = std::move(r2);
+                Ur += keyless;
+                mass += (int64_t)hm;
+                Ug = first;
+                // the routed kmers keep no bit position (the rare tag the hash
+                // fill inserts after the dictionary's replaces theirs)
+                GD_HIP(hipMemsetAsync(mperm.p, 0xFF, Um * 4 + 4, st));
+            }
+        }
+        if (Ug > 0) {
+            DevBuf head(Ug * 4 + 4, st), wn(Ug * 8 + 8, st), wst(Ug * 8 + 8, st);
+            group_words_kernel<<<grid_for(Ug), 256, 0, st>>>(k, Ug, wb, pack, head.as<int32_t>(), wn.as<int64_t>());
+            GD_HIP(hipGetLastError());
+            exclusive_scan_i64(ctx, wn.as<int64_t>(), wst.as<int64_t>(), (size_t)Ug);
+            int64_t h[2];
+            d2h(&h[0], wst.as<int64_t>() + Ug - 1, 8, st);
+            d2h(&h[1], wn.as<int64_t>() + Ug - 1, 8, st);
+            vwords = h[0] + h[1];
+            GD_REQUIRE((double)vbase + (double)vwords * wb < 4294967295.0, "variant tier too large for u32 positions");
+            group_pos_kernel<<<grid_for(Ug), 256, 0, st>>>(k, v, Ug, wst.as<int64_t>(), wb, pack, vbase,
+                                                           mperm.as<uint32_t>());
+            GD_HIP(hipGetLastError());
+        }
+        Um = Ug;
     }
     DevBuf perm(U * 4 + 4, st);
     if (U)

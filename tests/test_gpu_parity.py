@@ -1223,3 +1223,44 @@ def test_append_extends_segment_index(ctx):
         assert bits_equal(d, eD[n - 1])
     I, D = sets.matrix(method=gdist.METHOD_BITSET)
     assert np.array_equal(I[np.triu_indices(len(have), 1)], eI[np.triu_indices(len(have), 1)])
+
+
+@pytest.mark.parametrize("mode", [1, 0])
+def test_distance_epilogue_modes(ctx, opts, mode):
+    """The distance epilogue (the Java expression of SequenceKmers.distance,
+    FastaDistanceProcessor.java:186) by rows (option epilogue_rows 1,
+    default) and the flat kernel (0): bit-exact over upper triangles and
+    rectangles whose rows start at every alignment, odd column counts, host
+    and device outputs (poisoned first), with empty sets under both
+    empty-set readings (GDIST_EMPTY_NAN). (Round 6 measured a four-column
+    form slower on C3 — 1.54 vs 1.50 ms a step — and removed it.)"""
+    import gdist
+    opts(epilogue_rows=mode, sparse=0)                      # no fused sparse step: the epilogue kernels
+    seqs = synth_sets(53, 3000, 0.04, 141)
+    seqs[7] = b""
+    seqs[30] = b"ACGT"                                          # shorter than k: empty
+    off, codes = oracle_pack(seqs, 21, 0, 0)
+    n = len(seqs)
+    sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
+    sets.build_bitsets()
+    for flags in (0, 0x400):
+        for (r0, r1, c0, c1, up) in [(0, n, 0, n, True), (1, 50, 3, 52, True), (5, 38, 2, 51, False),
+                                     (30, 33, 0, n, False), (52, 53, 0, n, False)]:
+            fl = flags | (0x100 if up else 0)
+            eI, eD = oracle.matrix(off, codes, r0, r1, c0, c1, flags=fl)
+            I, D = sets.matrix((r0, r1), (c0, c1), upper=up, method=gdist.METHOD_BITSET, flags=flags)
+            m = np.fromfunction(lambda a, b: (c0 + b) > (r0 + a), (r1 - r0, c1 - c0)) if up else \
+                np.ones((r1 - r0, c1 - c0), bool)
+            assert np.array_equal(I[m], eI[m]), (mode, flags, r0, r1, c0, c1)
+            assert bits_equal(D[m], eD[m]), (mode, flags, r0, r1, c0, c1)
+            # device outputs (the bench's form), poisoned first
+            nr, nc = r1 - r0, c1 - c0
+            dI, dD = ctx.alloc(nr * nc * 4), ctx.alloc(nr * nc * 8)
+            dI.from_host(np.full(nr * nc, -7, np.int32))
+            dD.from_host(np.full(nr * nc, 42.5))
+            sets.matrix_device(dI.ptr, dD.ptr, nc, (r0, r1), (c0, c1), upper=up, method=gdist.METHOD_BITSET,
+                               flags=flags)
+            gI = dI.to_host(np.int32).reshape(nr, nc)
+            gD = dD.to_host(np.float64).reshape(nr, nc)
+            assert np.array_equal(gI[m], eI[m]) and bits_equal(gD[m], eD[m]), (mode, flags, r0, "device")
+            dI.free(); dD.free()

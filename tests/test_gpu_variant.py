@@ -38,7 +38,8 @@ REGIONS = [(0, 1200, 0, 1200, True), (37, 211, 5, 1190, False), (600, 1200, 0, 1
 
 
 @pytest.mark.parametrize("mode", ["variant", "variant_windowed_fill", "variant_w64", "variant_unpacked", "variant_store",
-                                  "range_only", "two_tier"])
+                                  "variant_keyless_rare", "variant_keyless_words", "variant_key1", "range_only",
+                                  "two_tier"])
 def test_variant_tier_exact(ctx, opts, c4_like, mode):
     """Counts and distances of the variant tier (its hash fill and the
     windowed fill; 47-kmer words of 8-byte packed members (default), 64-kmer
@@ -60,7 +61,11 @@ def test_variant_tier_exact(ctx, opts, c4_like, mode):
              fill_sort=3 if mode == "variant_windowed_fill" else None,
              variant_bits=64 if mode == "variant_w64" else None,
              variant_short=0 if mode == "variant_unpacked" else None,
-             bitset_mfma_store=1 if mode == "variant_store" else None)
+             bitset_mfma_store=1 if mode == "variant_store" else None,
+             # round 6: keyless kmers as rare posting lists (forced) or words
+             variant_keyless_rare={"variant_keyless_rare": 1, "variant_keyless_words": 0}.get(mode),
+             # round 6: second-level keys (default) or the first level only
+             variant_key2=0 if mode == "variant_key1" else None)
     sets = gdist.KmerSets.from_sequences(seqs, 21, gdist.KmerType.DNA, 0, ctx)
     sets.build_bitsets()
     vk, vw, ve, vp = sets.variant_info()
@@ -368,7 +373,8 @@ def test_grouped_rare_walk_across_column_chunks(ctx, opts):
             assert bits_equal(D, eD), (c16, r0, r1)
 
 
-@pytest.mark.parametrize("mode", ["variant", "variant_windowed_fill", "two_tier", "two_tier_sort_fill"])
+@pytest.mark.parametrize("mode", ["variant", "variant_windowed_fill", "variant_keyless_rare", "two_tier",
+                                  "two_tier_sort_fill"])
 def test_split_build_equals_whole_build(ctx, opts, c4_like, mode):
     """the build of a gathered collection split by rank.
     Option split_build = 3 runs the three ranks' shares in turn on this GPU
@@ -380,7 +386,8 @@ def test_split_build_equals_whole_build(ctx, opts, c4_like, mode):
     n = len(seqs)
     if mode.startswith("variant"):
         base = dict(variant=1, rare_t=3, variant_dmin=n // 10, range_summary=1,
-                    fill_sort=3 if mode == "variant_windowed_fill" else None)
+                    fill_sort=3 if mode == "variant_windowed_fill" else None,
+                    variant_keyless_rare=1 if mode == "variant_keyless_rare" else None)
     else:
         base = dict(variant=0, rare_t=3, fill_sort=1 if mode == "two_tier_sort_fill" else None)
     built = {}
