@@ -240,7 +240,7 @@ struct Timing {
     X(BITSET_MFMA_STORE, "bitset_mfma_store") /* MFMA tiles: 1 one K split storing its counts, the side families after it; 0 atomics */ \
     X(SORT_RADIX, "sort_radix")               /* 10: onesweep radix sorts of u64 keys in 10-bit passes (A/B) */\
     X(VARIANT, "variant")                     /* variant tier: 1 force, 0 off (default: by the dictionary) */ \
-    X(VARIANT_DMIN, "variant_dmin")           /* sets holding a dense-tier kmer (default N / 10) */            \
+    X(VARIANT_DMIN, "variant_dmin")           /* sets holding a dense-tier kmer (default N / 20; N / 10 before round 6) */            \
     X(RANGE_SUMMARY, "range_summary")         /* 1: the code-range dictionary whatever the size, 0: never */  \
     X(RARE_C16, "rare_c16")                   /* row-major rare walk: 1 (default) 16-bit LDS counters when every row's rare weight < 2^16, 0 32-bit */ \
     X(VARIANT_C16, "variant_c16")             /* variant walk: 1 (default) 16-bit counters in 32,768-column chunks, 0 32-bit in 16,384 */ \

@@ -21,13 +21,23 @@
 // locus_keys); (neighbour window + offset of the differing symbol, the
 // symbol) names the site and the letter on the forward strand, so both
 // strands' kmers of one substitution get one key. Kmers with no dense
-// neighbour (two substitutions in a window, no guide) keep code order after
-// the keyed ones. Any grouping is exact; it only decides how many products
-// the walk does.
+// neighbour get a second-level key when a keyed VARIANT neighbour exists
+// (round 6: the unordered pair of the two substitution sites, see
+// variant_key2_kernel); the rest (no guide, three substitutions in a
+// window) keep code order after the keyed ones. Any grouping is exact; it
+// only decides how many products the walk does.
 //
 // Tiers by the number of sets c holding a kmer: dense c >= Dmin (default
-// N / 10: bit columns of the tile kernels), variant T <= c < Dmin, rare
-// 2 <= c < T (posting lists), singletons dropped (they never intersect).
+// N / 20 since round 6, was N / 10: bit columns of the tile kernels),
+// variant T <= c < Dmin, rare 2 <= c < T (posting lists), singletons
+// dropped (they never intersect). Dmin prices a kmer as a bit column of
+// every pair (N^2 / 2 bit-products on the matrix cores, ~4e-16 s each) or as
+// a share of a variant word (~c^2 / (2 x 47) products of the walk, ~4e-12 s
+// each): the break-even holder count is ~0.07 N for kmers grouped 47 to a
+// word. The C4-realistic slice (clade-specific kmers held by ~7.5 K of
+// 100 K genomes) measured 68.5 ms at N / 10 with first-level keys, 31.1 ms
+// with second-level keys, 21.0 ms at N / 20; C4 (nothing held by 5-10 % of
+// the genomes) is the same at both (profiles/r06/s8, s9).
 //
 // Build (build_variant_bitsets, one GPU, from codes; C4 on 8 GPUs runs it on
 // every rank after the one code all-gather): a code-range dictionary
@@ -1136,7 +1146,7 @@ void hash_fill(gdist_ctx* ctx, const gdist_sets* s, const uint64_t* dict, int64_
 
 int64_t variant_dmin(const gdist_ctx* ctx, int64_t nsets) {
     return ctx->has_option(OPT_VARIANT_DMIN) ? std::max<int64_t>(2, ctx->option(OPT_VARIANT_DMIN, 2))
-                                             : std::max<int64_t>(2, nsets / 10);
+                                             : std::max<int64_t>(2, nsets / 20);
 }
 
 void free_variant(gdist_sets* s) {

@@ -107,6 +107,7 @@ def _twin(kind):
 @pytest.mark.parametrize("twin,mode", [("c3r", "auto"), ("c3r", "grouped"), ("c3r", "two_tier"),
                                        ("c4r", "auto"), ("c4r", "variant"), ("c4r", "variant_direct"),
                                        ("c4r", "keyless_rare"), ("c4r", "keyless_words"), ("c4r", "key1"),
+                                       ("c4r", "variant_dmin_default"),
                                        ("c3r", "grouped_key1")])
 def test_realistic_twins_exact(ctx, opts, twin, mode):
     """C3's grouped rare tier (rare kmers as 16-kmer
@@ -128,6 +129,7 @@ def test_realistic_twins_exact(ctx, opts, twin, mode):
          "keyless_words": dict(variant=1, rare_t=3, variant_dmin=n // 10, variant_keyless_rare=0),
          # the first-level keys only (option variant_key2 = 0)
          "key1": dict(variant=1, rare_t=3, variant_dmin=n // 10, variant_key2=0),
+         "variant_dmin_default": dict(variant=1, rare_t=3),             # Dmin = N / 20 (round 6)
          "grouped_key1": dict(variant=0, rare_group=1, variant_key2=0)}[mode]
     opts(**o)
     kind, k = (gdist.KmerType.PROT, 8) if twin == "c3r" else (gdist.KmerType.DNA, 21)
@@ -143,7 +145,8 @@ def test_realistic_twins_exact(ctx, opts, twin, mode):
     vk, vw, ve, _ = sets.variant_info()
     print(f"{twin} {mode}: AUTO -> {m} (bitset {cb:.3g} s, sorted {cs:.3g} s), variant {vk} kmers "
           f"{vw} words {ve} entries, rare {sets.rare_info()}")
-    if mode in ("grouped", "variant", "variant_direct", "keyless_rare", "keyless_words", "key1", "grouped_key1"):
+    if mode in ("grouped", "variant", "variant_direct", "keyless_rare", "keyless_words", "key1", "grouped_key1",
+                "variant_dmin_default"):
         assert vk > 0 and ve > 0, (twin, mode, vk, ve)
         assert vw < vk, ("kmers grouped into words", vk, vw)
     if mode == "two_tier":
