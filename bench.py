@@ -458,10 +458,10 @@ def main():
                 pk = pmc.get("kernel", "")
                 ok = pk.split(" (")[0].replace(" ", "") == kern.replace(" ", "") if "<" in kern else pk.startswith(kern)
                 if pmc.get("config") == args.config and pmc.get("n") == N and ok:
-                    traffic_readings.update({"x1": pmc.get("hbm_bytes_x1"), "x2": pmc.get("hbm_bytes_x2"),
-                                             "used": pmc.get("correction", "").split(",")[0],
-                                             "kernel": pk.split(" (")[0],
-                                             "source": os.path.relpath(fn, ROOT)})
+                    traffic_readings[kern] = {"x1": pmc.get("hbm_bytes_x1"), "x2": pmc.get("hbm_bytes_x2"),
+                                              "used": pmc.get("correction", "").split(",")[0],
+                                              "kernel": pk.split(" (")[0],
+                                              "source": os.path.relpath(fn, ROOT)}
                     return pmc.get("hbm_bytes_per_launch")
             return None
 
@@ -539,12 +539,23 @@ def main():
             tw = sparse_words["dense_words"] if sparse_words and sparse_words["sparse_words"] else width_words
             mfma = tw >= 64 and ctx.option("bitset_mfma") != 0
             if mfma:
+                # the launched instantiation (bitset.hip bitset_mfma_kernel<KM, NS,
+                # RAW, STORE, SPREAD>), so that traffic comes only from a PMC pass
+                # taken on it; the default: raw 16-word stages, the next stage's DMA
+                # spread between the MFMAs (round 6)
+                def _o(name, dflt):
+                    v = ctx.option(name)
+                    return dflt if v is None else v
+                if _o("bitset_mfma_raw", 1) and _o("bitset_mfma_km", 4) != 2 and not _o("bitset_mfma_store", 0):
+                    mfma_kinst = f"bitset_mfma_kernel<4, 2, true, false, {'true' if _o('bitset_mfma_sched', 1) else 'false'}>"
+                else:
+                    mfma_kinst = "bitset_mfma_kernel"
                 # the dense tiles on the matrix cores: pairs x W x 64 bit-products x 2 ops
                 tops = pairs_rank * tw * 64 * 2 / (d_ms * 1e-3) / 1e12 if d_ms > 0 else 0.0
                 dense_roof = {"bound": "mfma", "achieved": round(tops, 1), "peak": MFMA_FP4_PEAK_TOPS,
                               "unit": "TFLOP/s", "frac": round(tops / MFMA_FP4_PEAK_TOPS, 4),
-                              "traffic": pmc_traffic("bitset_mfma_kernel"),
-                              "kernel": "bitset_mfma_kernel (dense tier tiles, FP4 MFMA 32x32x64)",
+                              "traffic": pmc_traffic(mfma_kinst),
+                              "kernel": f"{mfma_kinst} (dense tier tiles, FP4 MFMA 32x32x64)",
                               "kernel_avg_ms": round(d_ms, 4), "ops_per_pair": 128 * tw,
                               "note": "algorithmic ops = pairs x W words x 64 bit-products x 2 (multiply + add) / "
                                       "the dense tile launch's own time (each kernel family timed alone: option serial_step); peak = the FP4 dense MFMA rate "
@@ -637,6 +648,19 @@ def main():
                     "unit": "GB/s", "frac": round(achieved / peak, 4), "traffic": pmc_traffic(kname.split(" ")[0]),
                     "kernel": kname, "kernel_avg_ms": round(kms, 4), "step_kernel_span_ms": round(k_avg_ms, 4),
                     "algo_bytes_per_launch": algo_bytes, "bytes_per_pair": bytes_per_pair}
+        def with_readings(rf):
+            """A roofline (and its `other` families) with the PMC readings of
+            ITS kernel: each pmc_traffic(kern) lookup filed its own."""
+            if not isinstance(rf, dict):
+                return rf
+            name = rf.get("kernel", "").split(" (")[0].replace(" ", "")
+            rd = next((v for k, v in traffic_readings.items()
+                       if name == k.replace(" ", "") or ("<" not in k and name.startswith(k))), None)
+            out_rf = dict(rf, traffic_readings=rd)
+            if isinstance(rf.get("other"), list):
+                out_rf["other"] = [with_readings(o) for o in rf["other"]]
+            return out_rf
+
         # ---------------------------------------------------------------- CPU baseline
         cpu = None
         cpu_opt = None
@@ -665,7 +689,7 @@ def main():
                        "method": method, "auto": auto, "rare_tier": rare, "complement_sparse": sparse_words,
                        "variant_tier": variant,
                        "options": options or None},
-            "roofline": dict(roof, traffic_readings=(traffic_readings or None)) if isinstance(roof, dict) else roof,
+            "roofline": with_readings(roof),
             "verified": verified,
             "cpu_baseline": cpu,
             "cpu_optimized": cpu_opt,

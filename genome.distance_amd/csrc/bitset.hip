@@ -695,6 +695,24 @@ __device__ __forceinline__ void mfma_stage(const unsigned char* __restrict__ F, 
     }
 }
 
+// piece i (0 .. KM - 1) of one operand's stage: the i-th iteration of
+// mfma_stage, so that a stage's DMA can be spread between MFMAs
+template <int KM>
+__device__ __forceinline__ void mfma_piece(const unsigned char* __restrict__ F, int64_t rowbytes, int64_t set0,
+                                           int64_t lo, int64_t lim, int64_t w0, unsigned char* lds_op, int tid,
+                                           int i) {
+    constexpr int CPR = 2 * KM;
+    const int q = i * MNT + tid;
+    const int g = q / CPR, sl = q % CPR;
+    const int c = mslot<KM>(g, sl);
+    int64_t set = set0 + g;
+    set = set < lim ? set : lim - 1;
+    set = set >= lo ? set : lo;
+    const unsigned char* src = F + set * rowbytes + w0 * 32 + c * 16;
+    __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(lds_op + (i * MNT + (tid & ~63)) * 16), 16, 0,
+                                     0);
+}
+
 // the wait at the top of a stage: every stage still in flight after it may stay
 // (g = glds per stage per thread: 2 KM); a counted vmcnt keeps the later stages'
 // DMAs going across the barrier (raw s_barrier, never __syncthreads, whose
@@ -730,7 +748,16 @@ __device__ __forceinline__ v4i_t raw_nibbles(uint32_t x) {
 // STORE (round 5, option bitset_mfma_store): one K split, every pair of the
 // tile STORED (the tile is its only writer; the other families add after it
 // in stream order) instead of 64 K device atomics a tile
-template <int KM, int NS, bool RAW = false, bool STORE = false>
+// SPREAD (round 6, raw KM = 4 double-buffered only; option bitset_mfma_sched,
+// default 1): the next stage's DMA spread between the current stage's MFMAs
+// (one piece after each MFMA step of its first two fragment reads) with ONE
+// barrier a stage — the barrier at the top of stage ks says both that stage
+// ks landed and that every wave is done with stage ks - 1's buffer, which the
+// pieces of stage ks + 1 then overwrite. Before, every wave issued its 8
+// pieces at the top of the stage, where the CU's 64 KiB of requests held
+// the MFMA pipe (tiles alone: C4 slice 7.45 vs 7.98 ms, C3 0.72 vs 0.79;
+// profiles/r06/s12)
+template <int KM, int NS, bool RAW = false, bool STORE = false, bool SPREAD = false>
 __global__ __launch_bounds__(MNT, 2) void bitset_mfma_kernel(
     const unsigned char* __restrict__ F, int64_t W, const int2* __restrict__ tiles, int ntiles, int splits,
     int64_t nstages, int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I,
@@ -759,6 +786,55 @@ __global__ __launch_bounds__(MNT, 2) void bitset_mfma_kernel(
         for (int b = 0; b < 4; b++)
 #pragma unroll
             for (int q = 0; q < 16; q++) acc[a][b][q] = 0.0f;
+    if constexpr (SPREAD) {
+        static_assert(RAW && KM == 4 && NS == 2 && !STORE, "the spread DMA: raw 16-word stages, double buffered");
+        // piece pc of stage ks: operand A's slots 0 .. KM - 1, then B's
+        // (into the buffer of stage ks, the bytes of stage kd: the last stage
+        // re-reads its own bytes into the free buffer, so that the pieces
+        // need no branch between the MFMAs)
+        auto piece = [&](int64_t ks, int64_t kd, int pc) {
+            unsigned char* An = mlds_buf + (int)((ks - ks0) & 1) * (2 * MOPB);
+            if (pc < KM) mfma_piece<KM>(F, rowbytes, row0, r0, r1, kd * KM, An, tid, pc);
+            else mfma_piece<KM>(F, rowbytes, col0, c0, c1, kd * KM, An + MOPB, tid, pc - KM);
+        };
+        if (ks0 < ks1)
+            for (int pc = 0; pc < 2 * KM; pc++) piece(ks0, ks0, pc);
+        for (int64_t ks = ks0; ks < ks1; ks++) {
+            // stage ks landed everywhere, and stage ks - 1's buffer is free
+            asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+            const int64_t kd = ks + 1 < ks1 ? ks + 1 : ks;
+            const unsigned char* A = mlds_buf + (int)((ks - ks0) & 1) * (2 * MOPB);
+            const unsigned char* B = A + MOPB;
+#pragma unroll
+            for (int q = 0; q < KM; q++) {
+                v4i_t af[2], bf[4];
+#pragma unroll
+                for (int a = 0; a < 2; a++)
+                    af[a] = *reinterpret_cast<const v4i_t*>(A + mlds<KM>(wr * 64 + a * 32 + r, KM * h + q));
+#pragma unroll
+                for (int b = 0; b < 4; b++)
+                    bf[b] = *reinterpret_cast<const v4i_t*>(B + mlds<KM>(wc * 128 + b * 32 + r, KM * h + q));
+#pragma unroll
+                for (int m = 0; m < 4; m++) {
+                    v4i_t an[2], bn[4];
+#pragma unroll
+                    for (int a = 0; a < 2; a++) an[a] = raw_nibbles((uint32_t)af[a][m]);
+#pragma unroll
+                    for (int b = 0; b < 4; b++) bn[b] = raw_nibbles((uint32_t)bf[b][m]);
+#pragma unroll
+                    for (int a = 0; a < 2; a++)
+#pragma unroll
+                        for (int b = 0; b < 4; b++) {
+                            const v8i_t av = {an[a][0], an[a][1], an[a][2], an[a][3], 0, 0, 0, 0};
+                            const v8i_t bv = {bn[b][0], bn[b][1], bn[b][2], bn[b][3], 0, 0, 0, 0};
+                            acc[a][b] =
+                                __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(av, bv, acc[a][b], 4, 4, 0, 0, 0, 0);
+                        }
+                    if (q * 4 + m < 2 * KM) piece(ks + 1, kd, q * 4 + m);
+                }
+            }
+        }
+    } else {
     auto issue = [&](int64_t ks) {
         unsigned char* An = mlds_buf + (int)((ks - ks0) % NS) * (2 * MOPB);
         mfma_stage<KM>(F, rowbytes, row0, r0, r1, ks * KM, An, tid);
@@ -823,6 +899,7 @@ __global__ __launch_bounds__(MNT, 2) void bitset_mfma_kernel(
                 }
         }
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // stage free for the next DMA
+    }
     }
     // D of block (a, b): row (q & 3) + 8 (q >> 2) + 4 h of the block, column r
 #pragma unroll
@@ -2705,6 +2782,11 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     const int mkm = mraw ? (mkm2 ? 8 : 16) : mkm2 ? 2 : 4;     // words a stage (below)
     const bool mstore = p.nmt > 0 && !s->sparse && mraw && !mkm2 && ctx->option(OPT_BITSET_MFMA_STORE, 0) != 0 &&
                         mfma_min_splits(tWm / mkm, mkm) == 1;
+    // raw 16-word stages: the next stage's DMA spread between the MFMAs, one
+    // barrier a stage (bitset_mfma_kernel SPREAD; 0: the round-5 schedule.
+    // Waves 4-7 at priority 1 as well measured neutral: C4 slice span 14.25-
+    // 14.40 vs 14.08-14.63 ms, profiles/r06/s12)
+    const bool mspread = ctx->option(OPT_BITSET_MFMA_SCHED, 1) != 0;
     const bool dense_first = side && (mstore || (!serial && ctx->option(OPT_DENSE_FIRST, s->sparse ? 0 : 1) != 0));
     if (side && !mstore) GD_HIP(hipEventRecord(ctx->ev_fork, st));
     auto launch_side = [&]() {
@@ -2795,6 +2877,7 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
                                                                r1, c0, c1, upper ? 1 : 0, d_I, ldI);
             };
             if (raw && !km2 && mstore) mlaunch(&bitset_mfma_kernel<4, 2, true, true>, 2 * 2 * mopb<4>());
+            else if (raw && !km2 && mspread) mlaunch(&bitset_mfma_kernel<4, 2, true, false, true>, 2 * 2 * mopb<4>());
             else if (raw && !km2) mlaunch(&bitset_mfma_kernel<4, 2, true>, 2 * 2 * mopb<4>());
             else if (raw && ns == 4) mlaunch(&bitset_mfma_kernel<2, 4, true>, 4 * 2 * mopb<2>());
             else if (raw && ns == 3) mlaunch(&bitset_mfma_kernel<2, 3, true>, 3 * 2 * mopb<2>());

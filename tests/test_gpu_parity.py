@@ -927,7 +927,7 @@ def test_sparse_equals_dense_at_size(ctx, opts):
 
 
 @pytest.mark.parametrize("mfma", [None, "nibble", "km2_group", "km2_ns3", "km2_ns4", "raw_group", "raw_km2",
-                                  "raw_km2_ns3", "store", 0])
+                                  "raw_km2_ns3", "store", "sched0", "sched1_split3", 0])
 @pytest.mark.parametrize("T", [0, 3])
 def test_dense_tiles_mfma_exact(ctx, opts, mfma, T):
     """The dense tier's tiles on the matrix cores (FP4 MFMA, 256 x 256 pairs
@@ -941,9 +941,14 @@ def test_dense_tiles_mfma_exact(ctx, opts, mfma, T):
     of 3 and 4 stages (options bitset_mfma_km, bitset_mfma_group,
     bitset_mfma_ns); raw stages of 8 words (a 64 KiB ring, bitset_mfma_km 2)
     in rings of 2 and 3; one K split storing its counts, the rare tier after
-    it (option bitset_mfma_store)."""
+    it (option bitset_mfma_store); the raw stages' DMA spread between the
+    MFMAs with one barrier a stage (round 6, default; also over three K
+    splits) and round 5's schedule (option bitset_mfma_sched 0)."""
     import gdist
-    if mfma == "store":
+    if mfma and str(mfma).startswith("sched"):
+        opts(bitset_mfma=1, bitset_mfma_sched=int(mfma[5]), sparse=0,
+             bitset_mfma_splits=3 if mfma.endswith("split3") else None)
+    elif mfma == "store":
         opts(bitset_mfma=1, bitset_mfma_store=1, sparse=0)
     elif mfma == "raw_km2":
         opts(bitset_mfma=1, bitset_mfma_km=2, sparse=0)
