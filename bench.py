@@ -547,7 +547,10 @@ def main():
                     v = ctx.option(name)
                     return dflt if v is None else v
                 if _o("bitset_mfma_raw", 1) and _o("bitset_mfma_km", 4) != 2 and not _o("bitset_mfma_store", 0):
-                    mfma_kinst = f"bitset_mfma_kernel<4, 2, true, false, {'true' if _o('bitset_mfma_sched', 1) else 'false'}>"
+                    sp_ = bool(_o("bitset_mfma_sched", 1))
+                    pl_ = sp_ and bool(_o("bitset_mfma_plane", 1))
+                    mfma_kinst = (f"bitset_mfma_kernel<4, 2, true, false, {'true' if sp_ else 'false'}, "
+                                  f"{'true' if pl_ else 'false'}>")
                 else:
                     mfma_kinst = "bitset_mfma_kernel"
                 # the dense tiles on the matrix cores: pairs x W x 64 bit-products x 2 ops

@@ -757,7 +757,17 @@ __device__ __forceinline__ v4i_t raw_nibbles(uint32_t x) {
 // pieces at the top of the stage, where the CU's 64 KiB of requests held
 // the MFMA pipe (tiles alone: C4 slice 7.45 vs 7.98 ms, C3 0.72 vs 0.79;
 // profiles/r06/s12)
-template <int KM, int NS, bool RAW = false, bool STORE = false, bool SPREAD = false>
+// PLANE (round 6, with SPREAD; option bitset_mfma_plane): MFMA step m takes
+// bit m of every nibble of the chunk's four dwords (x & 0x11111111 << m;
+// plane 3, the sign bit, shifted into bit 2) instead of the four bits of
+// dword m moved to bit 1: 5 VALU a dword instead of 7. The planes' nibbles
+// are the e2m1 codes 0x1 / 0x2 / 0x4 = 0.5 / 1.0 / 2.0, each step under the
+// e8m0 scale (both operands) that makes them 1.0 (128 / 127 / 126), so every
+// product is still 0 or 1 (scripts/microbench/fp4_scale_probe.hip)
+__device__ __forceinline__ int bit_plane(uint32_t x, int m) {
+    return (int)(m < 3 ? (x & (0x11111111u << m)) : ((x >> 1) & 0x44444444u));
+}
+template <int KM, int NS, bool RAW = false, bool STORE = false, bool SPREAD = false, bool PLANE = false>
 __global__ __launch_bounds__(MNT, 2) void bitset_mfma_kernel(
     const unsigned char* __restrict__ F, int64_t W, const int2* __restrict__ tiles, int ntiles, int splits,
     int64_t nstages, int64_t r0, int64_t r1, int64_t c0, int64_t c1, int upper, int32_t* __restrict__ I,
@@ -817,10 +827,24 @@ __global__ __launch_bounds__(MNT, 2) void bitset_mfma_kernel(
 #pragma unroll
                 for (int m = 0; m < 4; m++) {
                     v4i_t an[2], bn[4];
+                    if constexpr (PLANE) {
 #pragma unroll
-                    for (int a = 0; a < 2; a++) an[a] = raw_nibbles((uint32_t)af[a][m]);
+                        for (int a = 0; a < 2; a++)
+                            an[a] = v4i_t{bit_plane((uint32_t)af[a][0], m), bit_plane((uint32_t)af[a][1], m),
+                                          bit_plane((uint32_t)af[a][2], m), bit_plane((uint32_t)af[a][3], m)};
 #pragma unroll
-                    for (int b = 0; b < 4; b++) bn[b] = raw_nibbles((uint32_t)bf[b][m]);
+                        for (int b = 0; b < 4; b++)
+                            bn[b] = v4i_t{bit_plane((uint32_t)bf[b][0], m), bit_plane((uint32_t)bf[b][1], m),
+                                          bit_plane((uint32_t)bf[b][2], m), bit_plane((uint32_t)bf[b][3], m)};
+                    } else {
+#pragma unroll
+                        for (int a = 0; a < 2; a++) an[a] = raw_nibbles((uint32_t)af[a][m]);
+#pragma unroll
+                        for (int b = 0; b < 4; b++) bn[b] = raw_nibbles((uint32_t)bf[b][m]);
+                    }
+                    // plane m's nibbles are 0.5 / 1.0 / 2.0 / 2.0: scales 2, 1, 1/2, 1/2 a side
+                    constexpr int kPlaneScale[4] = {128, 127, 126, 126};
+                    const int sc = PLANE ? kPlaneScale[m] : 0;
 #pragma unroll
                     for (int a = 0; a < 2; a++)
 #pragma unroll
@@ -828,7 +852,7 @@ __global__ __launch_bounds__(MNT, 2) void bitset_mfma_kernel(
                             const v8i_t av = {an[a][0], an[a][1], an[a][2], an[a][3], 0, 0, 0, 0};
                             const v8i_t bv = {bn[b][0], bn[b][1], bn[b][2], bn[b][3], 0, 0, 0, 0};
                             acc[a][b] =
-                                __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(av, bv, acc[a][b], 4, 4, 0, 0, 0, 0);
+                                __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(av, bv, acc[a][b], 4, 4, 0, sc, 0, sc);
                         }
                     if (q * 4 + m < 2 * KM) piece(ks + 1, kd, q * 4 + m);
                 }
@@ -2787,6 +2811,9 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
     // Waves 4-7 at priority 1 as well measured neutral: C4 slice span 14.25-
     // 14.40 vs 14.08-14.63 ms, profiles/r06/s12)
     const bool mspread = ctx->option(OPT_BITSET_MFMA_SCHED, 1) != 0;
+    // bit-plane operands (PLANE; tiles alone C3 0.709-0.714 vs 0.715-0.736 ms,
+    // C4 slice 7.38-7.50 vs 7.51-7.54, spans unchanged: profiles/r06/s17)
+    const bool mplane = ctx->option(OPT_BITSET_MFMA_PLANE, 1) != 0;
     const bool dense_first = side && (mstore || (!serial && ctx->option(OPT_DENSE_FIRST, s->sparse ? 0 : 1) != 0));
     if (side && !mstore) GD_HIP(hipEventRecord(ctx->ev_fork, st));
     auto launch_side = [&]() {
@@ -2877,6 +2904,8 @@ void bitset_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1, 
                                                                r1, c0, c1, upper ? 1 : 0, d_I, ldI);
             };
             if (raw && !km2 && mstore) mlaunch(&bitset_mfma_kernel<4, 2, true, true>, 2 * 2 * mopb<4>());
+            else if (raw && !km2 && mspread && mplane)
+                mlaunch(&bitset_mfma_kernel<4, 2, true, false, true, true>, 2 * 2 * mopb<4>());
             else if (raw && !km2 && mspread) mlaunch(&bitset_mfma_kernel<4, 2, true, false, true>, 2 * 2 * mopb<4>());
             else if (raw && !km2) mlaunch(&bitset_mfma_kernel<4, 2, true>, 2 * 2 * mopb<4>());
             else if (raw && ns == 4) mlaunch(&bitset_mfma_kernel<2, 4, true>, 4 * 2 * mopb<2>());

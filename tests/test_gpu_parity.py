@@ -927,7 +927,7 @@ def test_sparse_equals_dense_at_size(ctx, opts):
 
 
 @pytest.mark.parametrize("mfma", [None, "nibble", "km2_group", "km2_ns3", "km2_ns4", "raw_group", "raw_km2",
-                                  "raw_km2_ns3", "store", "sched0", "sched1_split3", 0])
+                                  "raw_km2_ns3", "store", "sched0", "sched1_split3", "plane0", 0])
 @pytest.mark.parametrize("T", [0, 3])
 def test_dense_tiles_mfma_exact(ctx, opts, mfma, T):
     """The dense tier's tiles on the matrix cores (FP4 MFMA, 256 x 256 pairs
@@ -943,9 +943,13 @@ def test_dense_tiles_mfma_exact(ctx, opts, mfma, T):
     in rings of 2 and 3; one K split storing its counts, the rare tier after
     it (option bitset_mfma_store); the raw stages' DMA spread between the
     MFMAs with one barrier a stage (round 6, default; also over three K
-    splits) and round 5's schedule (option bitset_mfma_sched 0)."""
+    splits) and round 5's schedule (option bitset_mfma_sched 0); bit-plane
+    operands under per-step e8m0 scales (round 6, default) and the nibbles
+    of one dword a step (plane0: option bitset_mfma_plane 0)."""
     import gdist
-    if mfma and str(mfma).startswith("sched"):
+    if mfma == "plane0":
+        opts(bitset_mfma=1, bitset_mfma_plane=0, sparse=0)
+    elif mfma and str(mfma).startswith("sched"):
         opts(bitset_mfma=1, bitset_mfma_sched=int(mfma[5]), sparse=0,
              bitset_mfma_splits=3 if mfma.endswith("split3") else None)
     elif mfma == "store":
@@ -1005,8 +1009,9 @@ def test_dense_tiles_mfma_past_f32_bound(ctx, opts, splits):
     eI, eD = oracle.matrix(off, codes, 0, n, 0, n, flags=0, nthreads=4)
     iu = np.triu_indices(n, 1)
     assert eI[iu].min() > (1 << 24), eI[iu]       # the premise: counts past 2^24
-    for mfma, raw, km in ((1, None, None), (1, None, 2), (1, 0, None), (0, None, None)):
-        opts(bitset_mfma=mfma, bitset_mfma_raw=raw, bitset_mfma_km=km)
+    for mfma, raw, km, plane in ((1, None, None, None), (1, None, None, 0), (1, None, 2, None), (1, 0, None, None),
+                                 (0, None, None, None)):
+        opts(bitset_mfma=mfma, bitset_mfma_raw=raw, bitset_mfma_km=km, bitset_mfma_plane=plane)
         for up in (True, False):
             I, D = sets.matrix(upper=up, method=gdist.METHOD_BITSET)
             if up:
