@@ -239,6 +239,7 @@ struct Timing {
     X(BITSET_MFMA_GROUP, "bitset_mfma_group") /* MFMA tiles: G x 2G tile blocks in launch order (0: row-major) */ \
     X(BITSET_MFMA_STORE, "bitset_mfma_store") /* MFMA tiles: 1 one K split storing its counts, the side families after it; 0 atomics */ \
     X(BITSET_MFMA_SCHED, "bitset_mfma_sched") /* raw MFMA tiles: 1 (default) next stage's DMA between the MFMAs, 0 round 5 */ \
+    X(SKETCH_PERM, "sketch_perm")             /* ring kernel, 256 slots: 1 (default) slot addresses by one v_perm_b32, 0 AND + shift-add */ \
     X(BITSET_MFMA_PLANE, "bitset_mfma_plane") /* raw MFMA tiles: 1 (default) bit-plane operands under per-step scales, 0 nibbles of one dword */ \
     X(SORT_RADIX, "sort_radix")               /* 10: onesweep radix sorts of u64 keys in 10-bit passes (A/B) */\
     X(VARIANT, "variant")                     /* variant tier: 1 force, 0 off (default: by the dictionary) */ \

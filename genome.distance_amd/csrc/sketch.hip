@@ -324,15 +324,26 @@ typedef int32_t i32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 // C5: 430 vs 336 ms with a 448-slot ring, the waiting pairs add phases). Positions, steps and the
 // closed form are the merge's: results are identical
 // (test_sketch_merge_edges_vs_oracle runs rings of 16..448 slots).
+typedef __attribute__((address_space(3))) const int32_t lds_i32;   // an LDS dword
 __global__ __launch_bounds__(kSkTile * kSkTile) void sketch_ring_kernel(
     const int32_t* __restrict__ sig, const int64_t* __restrict__ off, int width, int RS, int kmax, int64_t r0,
     int64_t r1, int64_t c0, int64_t c1, int64_t tile0, int tiles_c, int upper, int jaccard, int empty_nan,
-    int32_t* __restrict__ common_out, double* __restrict__ D, int64_t ld, int fallback, int tri) {
+    int32_t* __restrict__ common_out, double* __restrict__ D, int64_t ld, int fallback, int tri, int sperm) {
 #pragma clang fp contract(off)
     constexpr int R = kSkTile, C = kSkTile, NT = R * C, NW = NT / 64, NS = kSkLanes;
-    extern __shared__ int32_t sm[];   // [RS + 1][64]: ring slot q of sketch s at 64 q + s, row RS = row 0
-    __shared__ int64_t s_base[NS];
-    __shared__ int32_t s_n[NS], s_top[NS], s_min[NS], s_imax[NS];
+    // [RS + 1][64]: ring slot q of sketch s at 64 q + s, row RS = row 0; then
+    // the sketches' metadata and three flag words (round 6: no static LDS, so
+    // the ring starts at LDS address 0 and a slot's byte offset is its LDS
+    // address: the 256-slot walk's one-v_perm addresses need no add)
+    extern __shared__ __attribute__((aligned(16))) int32_t sm[];
+    int64_t* s_base = reinterpret_cast<int64_t*>(sm + (RS + 1) * NS);     // 8-byte aligned: 256 B a ring row
+    int32_t* s_n = reinterpret_cast<int32_t*>(s_base + NS);
+    int32_t* s_top = s_n + NS;
+    int32_t* s_min = s_top + NS;
+    int32_t* s_imax = s_min + NS;
+    int32_t* s_or = s_imax + NS;                                           // block_or's three flag words
+    // the ring's LDS byte address (0: the kernel declares no static LDS)
+    const uint32_t ring0 = (uint32_t)(size_t)(const lds_i32*)sm;
     const int64_t bt = tile0 + blockIdx.x;
     int tr, tcb;
     if (tri) {
@@ -362,8 +373,23 @@ __global__ __launch_bounds__(kSkTile * kSkTile) void sketch_ring_kernel(
         s_n[s] = n;
         s_top[s] = 0;
         s_imax[s] = n > 0 && sig[b + n - 1] == 0x7FFFFFFF;
+        if (s < 3) s_or[s] = 0;
     }
     __syncthreads();
+    // __syncthreads_or without its own LDS: use k ORs into flag k mod 3 (zeroed
+    // by use k - 2, whose readers all passed use k - 1's barrier) and zeroes
+    // flag (k + 1) mod 3, whose last readers (use k - 2) passed this use's
+    // writes' barrier; one barrier a use
+    int orc = 0;
+    auto block_or = [&](bool v) -> bool {
+        const int k = orc % 3;
+        if (v) s_or[k] = 1;
+        if (threadIdx.x == 0) s_or[k == 2 ? 0 : k + 1] = 0;
+        __syncthreads();
+        const bool r = s_or[k] != 0;
+        orc++;
+        return r;
+    };
     const int64_t i = row0 + ty, j = col0 + tx;
     const bool valid = i < r1 && j < c1 && !(upper && j <= i);
     const int ina = s_n[ty], inb = s_n[R + tx];
@@ -438,16 +464,36 @@ __global__ __launch_bounds__(kSkTile * kSkTile) void sketch_ring_kernel(
                     const int ns = min(K - done, max(ina - pa, inb - pb));
                     if (ns < 2) break;
                     const int nr = ns >> 1;
-                    for (int r = 0; r < nr; r++) {
-                        const int32_t* pA = Arow + (pa & mask) * NS;      // slot RS - 1: pA[NS] is the mirror row
-                        const int32_t* pB = Brow + (pb & mask) * NS;
-                        const int32_t a0 = pA[0], a1 = pA[NS], b0 = pB[0], b1 = pB[NS];
-                        const bool le = a0 <= b0, ge = b0 <= a0;
-                        const int32_t x = le ? a1 : a0, y = ge ? b1 : b0;
-                        pa += le;
-                        pb += ge;
-                        pa += x <= y;
-                        pb += y <= x;
+                    if (RS == 256 && sperm && ring0 == 0) {
+                        // 256-slot rings (the default): a slot's byte offset in
+                        // the ring is (p & 255) << 8 | the sketch's 4 s < 256,
+                        // one v_perm_b32 (byte 1 = p's low byte, byte 0 = 4 s)
+                        // instead of an AND and a shift-add, used as the LDS
+                        // address itself (the ring starts at 0; round 6)
+                        const uint32_t ra = 4u * (uint32_t)ty, rb = 4u * (uint32_t)(R + tx);
+                        for (int r = 0; r < nr; r++) {
+                            const lds_i32* pA = (const lds_i32*)(size_t)__builtin_amdgcn_perm((uint32_t)pa, ra, 0x0C0C0400u);
+                            const lds_i32* pB = (const lds_i32*)(size_t)__builtin_amdgcn_perm((uint32_t)pb, rb, 0x0C0C0400u);
+                            const int32_t a0 = pA[0], a1 = pA[NS], b0 = pB[0], b1 = pB[NS];
+                            const bool le = a0 <= b0, ge = b0 <= a0;
+                            const int32_t x = le ? a1 : a0, y = ge ? b1 : b0;
+                            pa += le;
+                            pb += ge;
+                            pa += x <= y;
+                            pb += y <= x;
+                        }
+                    } else {
+                        for (int r = 0; r < nr; r++) {
+                            const int32_t* pA = Arow + (pa & mask) * NS;      // slot RS - 1: pA[NS] is the mirror row
+                            const int32_t* pB = Brow + (pb & mask) * NS;
+                            const int32_t a0 = pA[0], a1 = pA[NS], b0 = pB[0], b1 = pB[NS];
+                            const bool le = a0 <= b0, ge = b0 <= a0;
+                            const int32_t x = le ? a1 : a0, y = ge ? b1 : b0;
+                            pa += le;
+                            pb += ge;
+                            pa += x <= y;
+                            pb += y <= x;
+                        }
                     }
                     done += 2 * nr;
                 }
@@ -477,8 +523,8 @@ __global__ __launch_bounds__(kSkTile * kSkTile) void sketch_ring_kernel(
                 open = false;
             }
         }
-        stalled = !__syncthreads_or(done > 0 ? 1 : 0);
-        if (!__syncthreads_or(open ? 1 : 0)) break;
+        stalled = !block_or(done > 0);
+        if (!block_or(open)) break;
     }
     if (!valid) return;
     const int common = ia + ib - steps;
@@ -500,16 +546,17 @@ __global__ __launch_bounds__(kSkTile * kSkTile) void sketch_ring_kernel(
 template <int R, int C>
 constexpr size_t sketch_meta_bytes() { return (size_t)(R + C) * (sizeof(int64_t) + sizeof(int32_t)); }
 
-// ring kernel LDS: RS ring rows + the mirror row, 64 dwords each
-inline size_t sketch_ring_lds(int rs) { return (size_t)(rs + 1) * kSkLanes * 4; }
+// ring kernel LDS: RS ring rows + the mirror row, 64 dwords each, then the
+// metadata (int64 base + four int32 per sketch) and three flag words
+inline size_t sketch_ring_lds(int rs) { return (size_t)(rs + 1) * kSkLanes * 4 + (size_t)kSkLanes * 24 + 16; }
 
 int launch_sketch_ring(hipStream_t st, const gdist_sets* sk, int width, int rs, int kmax, int64_t r0, int64_t r1,
                         int64_t c0, int64_t c1, bool upper, int jac, int en, int32_t* d_common, double* d_D,
-                        int64_t ld, bool fallback) {
+                        int64_t ld, bool fallback, bool sperm) {
     const size_t lds = sketch_ring_lds(rs);
     GD_REQUIRE(rs >= 16 && (rs & (rs - 1)) == 0 && kmax >= 2 && kmax < rs,
                "sketch ring: a power of two >= 16 slots, 2 <= steps per phase < slots");
-    GD_REQUIRE(lds + (size_t)kSkLanes * 24 + 64 <= (size_t)LDS_SK_MAX, "sketch ring exceeds LDS");
+    GD_REQUIRE(lds + 64 <= (size_t)LDS_SK_MAX, "sketch ring exceeds LDS");
     const int tr = (int)ceil_div(r1 - r0, kSkTile), tc = (int)ceil_div(c1 - c0, kSkTile);
     // a square upper triangle (the all-pairs call) launches only tiles on or
     // above the diagonal instead of exiting the lower half's workgroups
@@ -524,7 +571,7 @@ int launch_sketch_ring(hipStream_t st, const gdist_sets* sk, int width, int rs, 
     for (int64_t t0 = 0; t0 < grid; t0 += per, launches++)
         kern<<<(unsigned)std::min(per, grid - t0), threads, lds, st>>>(
             sk->codes.as<int32_t>(), sk->off.as<int64_t>(), width, rs, kmax, r0, r1, c0, c1, t0, tc, upper, jac, en,
-            d_common, d_D, ld, fallback ? 1 : 0, tri ? 1 : 0);
+            d_common, d_D, ld, fallback ? 1 : 0, tri ? 1 : 0, sperm ? 1 : 0);
     GD_HIP(hipGetLastError());
     return launches;
 }
@@ -697,7 +744,8 @@ void sketch_matrix(gdist_ctx* ctx, const gdist_sets* sk, int64_t r0, int64_t r1,
         const int kmax = (int)std::max<int64_t>(2, std::min<int64_t>(ctx->option(OPT_SKETCH_CAP, 160), 1 << 20));
         const int rs = (int)std::max<int64_t>(16, std::min<int64_t>(ctx->option(OPT_SKETCH_RING, 256), 1 << 20));
         launches = launch_sketch_ring(st, sk, width, rs, std::min(kmax, rs - 1), r0, r1, c0, c1, upper, jac, en,
-                                      d_common, d_D, ld, ctx->option(OPT_SKETCH_WAIT, 0) == 0);
+                                      d_common, d_D, ld, ctx->option(OPT_SKETCH_WAIT, 0) == 0,
+                                      ctx->option(OPT_SKETCH_PERM, 1) != 0);
     } else {
         if (!only16)
             launches = launch_sketch_tiles<16, 24>(st, sk, width, r0, r1, c0, c1, upper, jac, en, d_common, d_D, ld,

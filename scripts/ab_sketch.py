@@ -17,7 +17,7 @@ rounds = int(os.environ.get("AB_ROUNDS", "3"))
 check_rows = min(n, 2048)
 
 
-KNOBS = ("sketch_tile", "sketch_k", "sketch_phase", "sketch_cap", "sketch_v2", "sketch_ring", "sketch_wait")
+KNOBS = ("sketch_tile", "sketch_k", "sketch_phase", "sketch_cap", "sketch_v2", "sketch_ring", "sketch_wait", "sketch_perm")
 
 
 def apply(v):

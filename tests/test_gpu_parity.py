@@ -462,7 +462,7 @@ def test_sketch_matrix_vs_oracle(ctx):
 @pytest.mark.parametrize("phase,cap,ring,v2,k", [
     (1, None, None, 1, 2), (1, 2, 512, 1, 2), (1, 7, 512, 1, 2), (1, 64, 256, 1, 2), (1, 255, 256, 1, 2),
     (1, 5000, 128, 1, 2), (1, 15, 16, 1, 2), (1, 8, 32, 1, 2), (1, 120, 512, 1, 2), ("w", 15, 16, 1, 2),
-    ("w", 8, 32, 1, 2), ("w", 64, 256, 1, 2),
+    ("w", 8, 32, 1, 2), ("w", 64, 256, 1, 2), ("p0", None, None, 1, 2), ("p0", 64, 256, 1, 2),
     (0, 300, None, 1, 2), (0, 300, None, 0, 2), (0, 300, None, 0, 4), (0, 300, None, 0, 1)])
 def test_sketch_merge_edges_vs_oracle(ctx, opts, phase, cap, ring, v2, k):
     """Uploaded sketches with the merge's edge cases, every pair against the
@@ -471,13 +471,15 @@ def test_sketch_merge_edges_vs_oracle(ctx, opts, phase, cap, ring, v2, k):
     phase; pairs without room in a small ring take global-memory steps, or
     with sketch_wait wait for the slower pairs until a phase makes no
     progress; sketch_phase = 0 with sketch_v2 / sketch_k: whole sketches in
-    LDS): empty and short sketches,
+    LDS; p0: 256-slot rings addressed by AND + shift-add instead of one
+    v_perm_b32, option sketch_perm 0): empty and short sketches,
     identical ones, disjoint ones, INT_MIN / INT_MAX hashes (INT_MAX is the
     LDS sentinel: such pairs take the checked loop)."""
     import gdist
     wait = phase == "w"                       # ring pairs without room wait (option sketch_wait)
-    opts(sketch_phase=1 if wait else phase, sketch_wait=1 if wait else None, sketch_cap=cap, sketch_ring=ring,
-         sketch_v2=v2, sketch_k=k)
+    perm0 = phase == "p0"
+    opts(sketch_phase=1 if (wait or perm0) else phase, sketch_wait=1 if wait else None, sketch_cap=cap,
+         sketch_ring=ring, sketch_v2=v2, sketch_k=k, sketch_perm=0 if perm0 else None)
     rng = np.random.default_rng(1234)
     for w in (64, 1000):
         sk = []
