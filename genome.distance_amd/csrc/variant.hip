@@ -1597,11 +1597,12 @@ void variant_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1,
         // slices a row: ~8 workgroups a CU over few rows, else ~1,536 of a
         // row's entries a slice (C3: 2,266 a row; walk alone 0.81 ms with 2
         // slices, 0.85 with 3, 0.88 with 1: profiles/r05/s21)
-        const int64_t per_row = ceil_div(s->vw_entries, std::max<int64_t>(1, s->nsets));
+        // (round 6: one slice a row past ~8 workgroups a CU — beside the
+        // round-6 MFMA tiles C3's step is 1.376 vs 1.406 ms with 1 slice
+        // against 2, C3-realistic 1.494 vs 1.541; profiles/r06/s24)
         const int nsplit = ctx->has_option(OPT_VARIANT_SPLIT)
                                ? (int)std::max<int64_t>(1, std::min<int64_t>(64, ctx->option(OPT_VARIANT_SPLIT, 1)))
-                               : (int)std::max<int64_t>(1, std::min<int64_t>(16, std::max(ceil_div((int64_t)ctx->cus * 8, su),
-                                                                                         ceil_div(per_row, 1536))));
+                               : (int)std::max<int64_t>(1, std::min<int64_t>(16, ceil_div((int64_t)ctx->cus * 8, su)));
         const int64_t grid = su * nsplit;
         GD_REQUIRE(grid < (int64_t(1) << 31), "variant-tier grid too large");
         const bool c16 = s->vw_row_wmax < 65536 && ctx->option(OPT_VARIANT_C16, 1) != 0;
@@ -1625,6 +1626,10 @@ void variant_matrix(gdist_ctx* ctx, const gdist_sets* s, int64_t r0, int64_t r1,
     // (option variant_split: a given number of slices a row)
     // (~16 workgroups a CU over few rows: the C4 slice's 1,024 rows in 4
     // slices, walk alone 7.35 vs 7.5 ms with 2, 8.2 with 1; profiles/r05/s35)
+    // (round 6: 16 slices a row measured 13.52 vs 13.96 ms on the C4 slice
+    // beside the round-6 MFMA tiles, 8: 13.66 (profiles/r06/s24), but the
+    // C4-realistic slice took 23.0 vs 19.3-19.5 ms with 16 (profiles/r06/
+    // final6): kept at ~16 workgroups a CU)
     const int nsplit = ctx->has_option(OPT_VARIANT_SPLIT)
                            ? (int)std::max<int64_t>(1, std::min<int64_t>(64, ctx->option(OPT_VARIANT_SPLIT, 1)))
                            : (int)std::max<int64_t>(1, std::min<int64_t>(64, ceil_div((int64_t)ctx->cus * 16, units)));
